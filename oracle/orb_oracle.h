@@ -1,0 +1,162 @@
+/*
+ * oracle/orb_oracle.h -- CPU restatement of the reference hot path (TEST INFRASTRUCTURE ONLY).
+ *
+ * This library is the parity checker for the HIP path in slam_framework_amd/. Only tests/,
+ * __graft_entry__.smoke() and bench.py's cpu_baseline leg may load it. The product library
+ * (libslamgpu.so) never links or calls anything in here.
+ *
+ * What it restates (every function cites the reference file:line it follows, paths relative
+ * to the reference repository root):
+ *   - ORBextractor (src/orb_features/orb_extractor.cpp): ctor tables, ComputePyramid,
+ *     ComputeKeyPointsOctTree (cell FAST + threshold fallback), DistributeOctTree,
+ *     IC_Angle / computeOrientation, GaussianBlur + computeOrbDescriptor, Compute.
+ *   - Frame::ComputeStereoMatches, AssignFeaturesToGrid, GetFeaturesInArea (src/data/frame.cpp).
+ *   - OrbMatcher::DescriptorDistance and both per-frame SearchByProjection overloads
+ *     (src/orb_features/orb_matcher.cpp).
+ *   - The OpenCV 3.3.1 primitives those call (resize INTER_LINEAR 8U, GaussianBlur 7x7 8U,
+ *     FAST_t<16> + cornerScore<16>, fastAtan2, cvRound) and glibc 2.35's x86-64 FMA sinf/cosf
+ *     (the reference's `cos(float)`/`sin(float)` resolve to them, orb_extractor.cpp:54).
+ *
+ * PARITY STATUS: "parity unpinned" against the reference binary. The reference cannot be built
+ * in this image (it needs OpenCV 3.x and Eigen3, neither present) and it ships no tests, golden
+ * vectors or fixtures for this path. What IS pinned:
+ *   - oc_sinf/oc_cosf are checked bit-exactly against this host's glibc 2.35 libm (FMA ifunc
+ *     variant) -- tests/test_oracle_math.py and oracle/check_sincosf.c;
+ *   - the ctor tables (level sizes, per-level budgets, umax) against SURVEY.md section 8;
+ *   - FAST against a brute-force definition of the 9-of-16 segment test;
+ *   - the Release-build (-O3 -march=native, GCC fp-contract=fast) FMA association of the
+ *     reference's own float expressions, read from g++ 11 disassembly.
+ * OpenCV-primitive semantics are the declared OpenCV 3.3.1 non-IPP paths.
+ */
+#ifndef SLAMGPU_ORB_ORACLE_H_
+#define SLAMGPU_ORB_ORACLE_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define OC_MAX_LEVELS 32
+
+/* Byte-identical to cv::KeyPoint (28 bytes). */
+typedef struct {
+  float x, y, size, angle, response;
+  int32_t octave, class_id;
+} oc_keypoint;
+
+/* ORBextractor constructor arguments (orb_extractor.h:35-39). */
+typedef struct {
+  int nfeatures;
+  float scale_factor;
+  int nlevels;
+  int ini_th_fast;
+  int min_th_fast;
+} oc_orb_params;
+
+/* Everything the ORBextractor ctor precomputes (orb_extractor.cpp:351-411). */
+typedef struct {
+  int nfeatures, nlevels, ini_th_fast, min_th_fast;
+  double scale_factor; /* the member is a double (orb_extractor.h:80) */
+  float scale[OC_MAX_LEVELS], inv_scale[OC_MAX_LEVELS];
+  float sigma2[OC_MAX_LEVELS], inv_sigma2[OC_MAX_LEVELS];
+  int features_per_level[OC_MAX_LEVELS];
+  int umax[16];
+} oc_orb_tables;
+
+/* Image pyramid: level l is a w[l] x h[l] u8 image with row pitch step[l] (no border). */
+typedef struct {
+  int nlevels;
+  int w[OC_MAX_LEVELS], h[OC_MAX_LEVELS];
+  size_t step[OC_MAX_LEVELS];
+  uint8_t* data[OC_MAX_LEVELS];
+} oc_pyramid;
+
+/* ---- OpenCV / glibc primitive semantics ------------------------------------------------- */
+int oc_cv_round(float v);                              /* cvRound(float): half-to-even      */
+float oc_fast_atan2(float y, float x);                 /* cv::fastAtan2, degrees [0,360)    */
+float oc_sinf(float x);                                /* glibc 2.35 __sinf_fma             */
+float oc_cosf(float x);                                /* glibc 2.35 __cosf_fma             */
+void oc_resize_linear_u8(const uint8_t* src, int sw, int sh, size_t sstep, uint8_t* dst, int dw,
+                         int dh, size_t dstep);
+void oc_gaussian_blur7_u8(const uint8_t* src, int w, int h, size_t sstep, uint8_t* dst,
+                          size_t dstep);
+/* cv::FAST(img, kps, threshold, nonmax) on a w x h view; returns #kps (<= cap written). */
+int oc_fast16(const uint8_t* img, int w, int h, size_t step, int threshold, int nonmax,
+              oc_keypoint* out, int cap);
+
+/* ---- ORBextractor ----------------------------------------------------------------------- */
+void oc_orb_init(oc_orb_tables* t, const oc_orb_params* p);
+void oc_level_size(const oc_orb_tables* t, int cols, int rows, int level, int* w, int* h);
+int oc_pyramid_alloc(oc_pyramid* p, const oc_orb_tables* t, int cols, int rows);
+void oc_pyramid_free(oc_pyramid* p);
+void oc_compute_pyramid(const oc_orb_tables* t, const uint8_t* img, size_t step, oc_pyramid* p);
+/* Cell FAST for one level: candidates in octree coordinates (level coords - minBorder). */
+int oc_level_candidates(const oc_orb_tables* t, const oc_pyramid* p, int level,
+                        oc_keypoint* out, int cap);
+/* DistributeOctTree; returns #kept (<= cap written), list order. */
+int oc_distribute_octree(const oc_keypoint* keys, int n, int minX, int maxX, int minY, int maxY,
+                         int N, oc_keypoint* out, int cap);
+float oc_ic_angle(const uint8_t* img, size_t step, float x, float y, const int* umax);
+void oc_orb_descriptor(const oc_keypoint* kp, const uint8_t* blurred, size_t step,
+                       uint8_t desc[32]);
+/* Full ORBextractor::Compute. Returns #keypoints (or -needed if cap too small). If pyr is
+ * non-NULL it must be allocated with oc_pyramid_alloc and receives the level images. */
+int oc_orb_extract(const oc_orb_tables* t, const uint8_t* img, int rows, int cols, size_t step,
+                   oc_keypoint* kps, uint8_t* desc, int cap, oc_pyramid* pyr);
+
+/* ---- Matching ---------------------------------------------------------------------------- */
+int oc_descriptor_distance(const uint8_t* a, const uint8_t* b);
+
+/* Frame::ComputeStereoMatches. Outputs u_right[nl], depth[nl] (-1 = none) and, if non-NULL,
+ * sad_best[nl] (the SAD score used by the median filter, -1 if no match). */
+void oc_stereo_match(const oc_orb_tables* t, const oc_keypoint* kl, const uint8_t* dl, int nl,
+                     const oc_keypoint* kr, const uint8_t* dr, int nr, const oc_pyramid* pl,
+                     const oc_pyramid* pr, float fx, float bf, float* u_right, float* depth,
+                     int* sad_best);
+
+/* Frame image bounds and 64x48 grid (frame.cpp:211-248, 339-346, 678-703). */
+typedef struct {
+  float min_x, max_x, min_y, max_y;
+  float cell_w, cell_h; /* grid_element_width_/height_ */
+} oc_grid_geom;
+void oc_grid_geom_init(oc_grid_geom* g, int cols, int rows);
+/* Frame::GetFeaturesInArea; returns count (<= cap written), reference order. */
+int oc_features_in_area(const oc_grid_geom* g, const oc_keypoint* kps, int n, float x, float y,
+                        float r, int min_level, int max_level, int* out, int cap);
+
+/* Map-point state shared by the two SearchByProjection restatements. mp ids index mp_nobs. */
+typedef struct {
+  const oc_keypoint* kps;  /* undistorted keypoints (== keypoints, k1 = 0) */
+  const uint8_t* desc;     /* n x 32 */
+  const float* u_right;    /* StereoCoordRight */
+  int n;
+  int* map_point;          /* in/out: mp id per keypoint or -1 (Frame::map_points_) */
+} oc_frame_view;
+
+/* OrbMatcher::SearchByProjection(Frame&, const Frame&, th, bMono) (orb_matcher.cpp:1312-1453).
+ * Last frame: its keypoints, map point ids and outlier flags. Map points: world xyz (3 floats
+ * each), descriptors (32 B each), NumObservations. Pose: current Rcw (row-major 3x3), tcw,
+ * tlc_z (z of the current camera centre in the last camera frame), baseline. */
+int oc_search_by_projection_frame(const oc_grid_geom* g, const oc_orb_tables* t,
+                                  oc_frame_view* cur, const oc_keypoint* last_kps,
+                                  const int* last_mp, const uint8_t* last_outlier, int n_last,
+                                  const float* mp_xyz, const uint8_t* mp_desc,
+                                  const int* mp_nobs, const float* Rcw, const float* tcw,
+                                  float tlc_z, float baseline, float fx, float fy, float cx,
+                                  float cy, float bf, float th, int mono, int check_ori);
+
+/* OrbMatcher::SearchByProjection(Frame&, vector<MapPoint*>, th) (orb_matcher.cpp:13-103).
+ * Query q is map point id q. in_view/is_bad/level/view_cos/proj_{x,y,xr} are its track_* data. */
+int oc_search_by_projection_mps(const oc_grid_geom* g, const oc_orb_tables* t,
+                                oc_frame_view* cur, int n_mp, const uint8_t* in_view,
+                                const uint8_t* is_bad, const int* level, const float* view_cos,
+                                const float* proj_x, const float* proj_y, const float* proj_xr,
+                                const uint8_t* mp_desc, const int* mp_nobs, float nnratio,
+                                int th);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SLAMGPU_ORB_ORACLE_H_ */

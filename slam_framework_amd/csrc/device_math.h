@@ -1,0 +1,151 @@
+// device_math.h -- bit-exact device versions of the float semantics the hot path depends on.
+//
+// Built with -ffp-contract=off: every fused multiply-add below is an explicit fma()/fmaf(),
+// placed where the reference's Release build (or the library it calls) fuses.
+//   - glibc 2.35 sinf/cosf, x86-64 FMA variant (reference: std::cos(float)/std::sin(float) at
+//     src/orb_features/orb_extractor.cpp:54). Double-precision polynomial on the VALU.
+//   - OpenCV 3.3.1 fastAtan2 (reference: orb_extractor.cpp:44), no FMA.
+//   - cvRound(float) = round half to even (v_rndne_f32).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace slamgpu {
+
+struct SinCosTable {
+  double sign[4];
+  double hpi_inv, hpi;
+  double c0, c1, s1, c2, s2, c3, s3, c4;
+};
+
+__device__ __forceinline__ const SinCosTable& sincos_table(int k) {
+  // Same constants as libm's __sincosf_table (second record negates the cosine terms).
+  static __device__ __constant__ SinCosTable t[2] = {
+      {{1.0, -1.0, -1.0, 1.0}, 0x1.45f306dc9c883p+23, 0x1.921fb54442d18p+0, 0x1p+0,
+       -0x1.ffffffd0c621cp-2, -0x1.555545995a603p-3, 0x1.55553e1068f19p-5,
+       0x1.1107605230bc4p-7, -0x1.6c087e89a359dp-10, -0x1.994eb3774cf24p-13,
+       0x1.99343027bf8c3p-16},
+      {{1.0, -1.0, -1.0, 1.0}, 0x1.45f306dc9c883p+23, 0x1.921fb54442d18p+0, -0x1p+0,
+       0x1.ffffffd0c621cp-2, -0x1.555545995a603p-3, -0x1.55553e1068f19p-5,
+       0x1.1107605230bc4p-7, 0x1.6c087e89a359dp-10, -0x1.994eb3774cf24p-13,
+       -0x1.99343027bf8c3p-16}};
+  return t[k];
+}
+
+__device__ __forceinline__ float sc_sin_poly(double x, double x2, const SinCosTable& p) {
+  double s1 = fma(x2, p.s3, p.s2);
+  double x3 = x2 * x;
+  double x7 = x2 * x3;
+  double s = fma(x3, p.s1, x);
+  return (float)fma(s1, x7, s);
+}
+
+__device__ __forceinline__ float sc_cos_poly(double x2, const SinCosTable& p) {
+  double x4 = x2 * x2;
+  double c1 = fma(x2, p.c1, p.c0);
+  double c2 = fma(x2, p.c4, p.c3);
+  double x6 = x2 * x4;
+  double c = fma(x4, p.c2, c1);
+  return (float)fma(c2, x6, c);
+}
+
+// sin and cos of one float, as glibc's separate sinf() and cosf() calls return them.
+// Valid for |y| < 120 (keypoint angles are in [0, 2pi)); larger inputs fall back to libm.
+__device__ __forceinline__ void glibc_sincosf(float y, float* sout, float* cout) {
+  const uint32_t top = (__float_as_uint(y) >> 20) & 0x7ff;
+  const double x = (double)y;
+  if (top < 0x3f4) {
+    if (top < 0x398) {
+      *sout = y;
+      *cout = 1.0f;
+      return;
+    }
+    const double x2 = x * x;
+    *sout = sc_sin_poly(x, x2, sincos_table(0));
+    *cout = sc_cos_poly(x2, sincos_table(0));
+    return;
+  }
+  if (top < 0x42f) {
+    const SinCosTable& t0 = sincos_table(0);
+    const double r = x * t0.hpi_inv;
+    const int n = ((int32_t)r + 0x800000) >> 24;
+    const double xr = fma(-(double)n, t0.hpi, x);
+    const SinCosTable& p = sincos_table((n & 2) ? 1 : 0);
+    const double x2 = xr * xr;
+    const double xs = xr * t0.sign[n & 3];
+    if ((n & 1) == 0) {
+      *sout = sc_sin_poly(xs, x2, p);
+      *cout = sc_cos_poly(x2, p);
+    } else {
+      *sout = sc_cos_poly(x2, p);
+      *cout = sc_sin_poly(xs, x2, p);
+    }
+    return;
+  }
+  *sout = sinf(y);
+  *cout = cosf(y);
+}
+
+// cv::fastAtan2 (OpenCV 3.3.1, degrees in [0, 360)).
+__device__ __forceinline__ float cv_fast_atan2(float y, float x) {
+  const float k180pi = (float)(180.0 / 3.14159265358979323846);
+  const float p1 = 0.9997878412794807f * k180pi;
+  const float p3 = -0.3258083974640975f * k180pi;
+  const float p5 = 0.1555786518463281f * k180pi;
+  const float p7 = -0.04432655554792128f * k180pi;
+  const float eps = (float)2.2204460492503131e-16;
+  const float ax = fabsf(x), ay = fabsf(y);
+  float a, c, c2;
+  if (ax >= ay) {
+    c = ay / (ax + eps);
+    c2 = c * c;
+    a = (((p7 * c2 + p5) * c2 + p3) * c2 + p1) * c;
+  } else {
+    c = ax / (ay + eps);
+    c2 = c * c;
+    a = 90.f - (((p7 * c2 + p5) * c2 + p3) * c2 + p1) * c;
+  }
+  if (x < 0) a = 180.f - a;
+  if (y < 0) a = 360.f - a;
+  return a;
+}
+
+__device__ __forceinline__ int cv_round(float v) { return (int)rintf(v); }
+
+// ---- wavefront (64-lane) helpers --------------------------------------------------------
+__device__ __forceinline__ int lane_id() { return __lane_id(); }
+
+template <typename T>
+__device__ __forceinline__ T wave_min(T v) {
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) {
+    T o = __shfl_xor(v, off, 64);
+    v = o < v ? o : v;
+  }
+  return v;
+}
+
+template <typename T>
+__device__ __forceinline__ T wave_max(T v) {
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) {
+    T o = __shfl_xor(v, off, 64);
+    v = o > v ? o : v;
+  }
+  return v;
+}
+
+template <typename T>
+__device__ __forceinline__ T wave_sum(T v) {
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off, 64);
+  return v;
+}
+
+// Number of set bits of `mask` strictly below this lane.
+__device__ __forceinline__ int lanes_below(uint64_t mask) {
+  return __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32),
+                                   __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0));
+}
+
+}  // namespace slamgpu

@@ -1,0 +1,682 @@
+// match_kernels.hip -- stereo and projection matching on gfx950, batched over frames.
+//
+//   stereo_rows     right-keypoint row table          Frame::ComputeStereoMatches :412-433
+//   stereo_match    row-band Hamming + 11x11 SAD      :446-562   (one wave per left keypoint)
+//   stereo_median   2.1 x median SAD rejection        :564-576   (one workgroup per frame)
+//   grid_build      64x48 keypoint grid (CSR)         Frame::AssignFeaturesToGrid :234-248
+//   search_cand     projection + window + Hamming     OrbMatcher::SearchByProjection (both
+//   search_resolve  greedy in-order claims            overloads, orb_matcher.cpp:13-103 and
+//                                                     :1312-1453) + rotation histogram
+// Every Hamming distance is popcount(a ^ b) over 4 x u64 (== DescriptorDistance, :1630-1646).
+// The projection matchers are greedy in query order (a keypoint taken by an earlier query whose
+// map point has observations is skipped, :59-63 / :1389-1393), so candidate search is parallel
+// over queries and only a short claim-resolution pass per frame is sequential.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "device_math.h"
+#include "match_kernels.h"
+
+namespace slamgpu {
+
+constexpr int TH_HIGH = 100, TH_LOW = 50, HISTO_LENGTH = 30;
+constexpr uint64_t kNoKey = ~0ull;
+
+__device__ __forceinline__ int hamming32(const uint8_t* a, const uint8_t* b) {
+  const uint64_t* pa = reinterpret_cast<const uint64_t*>(a);
+  const uint64_t* pb = reinterpret_cast<const uint64_t*>(b);
+  return __popcll(pa[0] ^ pb[0]) + __popcll(pa[1] ^ pb[1]) + __popcll(pa[2] ^ pb[2]) +
+         __popcll(pa[3] ^ pb[3]);
+}
+
+__device__ __forceinline__ const uint8_t* level_img(const ImageBatch& b, const OrbGeom* g,
+                                                    int img, int level, int* pitch) {
+  if (level == 0) {
+    *pitch = b.in_pitch;
+    return batch_image(b, img);
+  }
+  *pitch = g->lv[level].pitch;
+  return b.pyr + (int64_t)img * g->pyr_bytes + g->lv[level].offset;
+}
+
+// 256-thread exclusive scan of arr[0..n) in place; returns the total.
+template <int CAP>
+__device__ int scan256(int* arr, int n, int* wsum) {
+  constexpr int per = (CAP + 255) / 256;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int base = threadIdx.x * per;
+  int loc[per];
+  int s = 0;
+#pragma unroll
+  for (int i = 0; i < per; i++) {
+    loc[i] = (base + i < n) ? arr[base + i] : 0;
+    s += loc[i];
+  }
+  int x = s;
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const int y = __shfl_up(x, off, 64);
+    if (lane >= off) x += y;
+  }
+  if (lane == 63) wsum[wid] = x;
+  __syncthreads();
+  int pre = 0, tot = 0;
+#pragma unroll
+  for (int w = 0; w < 4; w++) {
+    pre += (w < wid) ? wsum[w] : 0;
+    tot += wsum[w];
+  }
+  pre += x - s;
+#pragma unroll
+  for (int i = 0; i < per; i++) {
+    if (base + i < n) arr[base + i] = pre;
+    pre += loc[i];
+  }
+  __syncthreads();
+  return tot;
+}
+
+// ---------------------------------------------------------------------------------------
+// Stereo (frame.cpp:406-577). Frame f: left = image 2f, right = image 2f+1.
+constexpr int kMaxRows = 2048;
+
+__global__ __launch_bounds__(256) void stereo_rows_kernel(const OrbGeom* __restrict__ g,
+                                                          FrameKps ext, int nrows,
+                                                          StereoWorkspace ws,
+                                                          uint32_t* __restrict__ err) {
+  __shared__ int cnt[kMaxRows + 1];
+  __shared__ int wsum[4];
+  const int f = blockIdx.x, tid = threadIdx.x;
+  const int ir = 2 * f + 1;
+  const KeyPoint* kr = ext.kps + ir * ext.stride;
+  const int nr = ext.n[ir * ext.n_stride];
+  int* rs = ws.row_start + (int64_t)f * (nrows + 1);
+  int* items = ws.row_items + (int64_t)f * ws.row_cap;
+  for (int i = tid; i <= nrows; i += 256) cnt[i] = 0;
+  __syncthreads();
+  for (int i = tid; i < nr; i += 256) {
+    const KeyPoint kp = kr[i];
+    const float r = 2.0f * g->lv[kp.octave].scale;
+    const int maxr = (int)ceilf(kp.y + r), minr = (int)floorf(kp.y - r);
+    for (int yi = max(minr, 0); yi <= min(maxr, nrows - 1); ++yi) atomicAdd(&cnt[yi], 1);
+  }
+  __syncthreads();
+  const int total = scan256<kMaxRows + 1>(cnt, nrows, wsum);
+  for (int i = tid; i < nrows; i += 256) rs[i] = cnt[i];
+  if (tid == 0) {
+    rs[nrows] = total;
+    if (total > ws.row_cap) atomicOr(err, kErrRowOverflow);
+  }
+  __syncthreads();
+  for (int i = tid; i < nr; i += 256) {
+    const KeyPoint kp = kr[i];
+    const float r = 2.0f * g->lv[kp.octave].scale;
+    const int maxr = (int)ceilf(kp.y + r), minr = (int)floorf(kp.y - r);
+    for (int yi = max(minr, 0); yi <= min(maxr, nrows - 1); ++yi) {
+      const int pos = atomicAdd(&cnt[yi], 1);
+      if (pos < ws.row_cap) items[pos] = i;
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void stereo_match_kernel(ImageBatch b,
+                                                           const OrbGeom* __restrict__ g,
+                                                           FrameKps ext, Camera cam, int nrows,
+                                                           StereoWorkspace ws, StereoOut out) {
+  const int f = blockIdx.y;
+  const int lane = threadIdx.x & 63;
+  const int iL = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int il = 2 * f, ir = 2 * f + 1;
+  const int nl = ext.n[il * ext.n_stride];
+  if (iL >= nl) return;
+  const int64_t o = (int64_t)f * g->kp_cap + iL;
+  if (lane == 0) {
+    out.u_right[o] = -1.0f;
+    out.depth[o] = -1.0f;
+    ws.sad[o] = -1;
+  }
+  const KeyPoint kpL = ext.kps[il * ext.stride + iL];
+  const KeyPoint* kr = ext.kps + ir * ext.stride;
+  const int levelL = kpL.octave;
+  const float vL = kpL.y, uL = kpL.x;
+  const int row = (int)vL;
+  if (row < 0 || row >= nrows) return;
+  const int* rs = ws.row_start + (int64_t)f * (nrows + 1);
+  const int* items = ws.row_items + (int64_t)f * ws.row_cap;
+  const int c0 = rs[row], c1 = min(rs[row + 1], ws.row_cap);
+  if (c0 >= c1) return;
+  const float baseline = cam.bf / cam.fx;  // see DESIGN.md: maxD is UB in the reference (:436)
+  const float minZ = baseline, minD = 0, maxD = cam.bf / minZ;
+  const float minU = uL - maxD, maxU = uL - minD;
+  if (maxU < 0) return;
+  const uint8_t* dL = ext.desc + (il * ext.stride + iL) * 32;
+  const uint8_t* dRb = ext.desc + ir * ext.stride * 32;
+  uint32_t best = ((uint32_t)TH_HIGH << 16) | 0xffffu;
+  for (int c = c0 + lane; c < c1; c += 64) {
+    const int iR = items[c];
+    const KeyPoint kpR = kr[iR];
+    if (kpR.octave < levelL - 1 || kpR.octave > levelL + 1) continue;
+    const float uR = kpR.x;
+    if (uR >= minU && uR <= maxU) {
+      const int dist = hamming32(dL, dRb + iR * 32);
+      const uint32_t key = ((uint32_t)dist << 16) | (uint32_t)iR;
+      if (dist < TH_HIGH && key < best) best = key;
+    }
+  }
+  best = wave_min(best);
+  const int bestDist = (int)(best >> 16);
+  const int thOrbDist = (TH_HIGH + TH_LOW) / 2;
+  if (bestDist >= thOrbDist) return;
+  const int bestIdxR = (int)(best & 0xffff);
+  // sliding-window SAD at the left keypoint's level (:481-531)
+  const float uR0 = kr[bestIdxR].x;
+  const float scaleFactor = g->lv[levelL].inv_scale;
+  const float scaleduL = roundf(kpL.x * scaleFactor);
+  const float scaledvL = roundf(kpL.y * scaleFactor);
+  const float scaleduR0 = roundf(uR0 * scaleFactor);
+  const int w = 5, L = 5;
+  const LevelGeom& LG = g->lv[levelL];
+  const float iniu = scaleduR0 + L - w;
+  const float endu = scaleduR0 + L + w + 1;
+  if (iniu < 0 || endu >= (float)LG.w) return;
+  const int yc = (int)scaledvL, xcl = (int)scaleduL, xcr = (int)scaleduR0;
+  // windows the reference would reject with a cv::Mat ROI assertion are treated as no match
+  if (yc - w < 0 || yc + w >= LG.h || xcl - w < 0 || xcl + w >= LG.w || xcr - L - w < 0) return;
+  int pl, pr;
+  const uint8_t* IL = level_img(b, g, il, levelL, &pl);
+  const uint8_t* IR = level_img(b, g, ir, levelL, &pr);
+  int sad = 0x7fffffff;
+  if (lane < 2 * L + 1) {
+    const int incR = lane - L;
+    const int cl = IL[(int64_t)yc * pl + xcl];
+    const int cr = IR[(int64_t)yc * pr + xcr + incR];
+    int acc = 0;
+    for (int yy = -w; yy <= w; yy++) {
+      const uint8_t* rl = IL + (int64_t)(yc + yy) * pl + xcl - w;
+      const uint8_t* rr = IR + (int64_t)(yc + yy) * pr + xcr + incR - w;
+#pragma unroll
+      for (int xx = 0; xx < 2 * w + 1; xx++) acc += abs((rl[xx] - cl) - (rr[xx] - cr));
+    }
+    sad = acc;
+  }
+  float vDists[11];
+#pragma unroll
+  for (int k = 0; k < 11; k++) vDists[k] = (float)__shfl(sad, k, 64);
+  if (lane != 0) return;
+  int bestSad = 0x7fffffff, bestincR = 0;
+#pragma unroll
+  for (int k = 0; k < 11; k++) {
+    if (vDists[k] < (float)bestSad) {
+      bestSad = (int)vDists[k];
+      bestincR = k - L;
+    }
+  }
+  if (bestincR == -L || bestincR == L) return;
+  const float dist1 = vDists[L + bestincR - 1];
+  const float dist2 = vDists[L + bestincR];
+  const float dist3 = vDists[L + bestincR + 1];
+  const float deltaR = (dist1 - dist3) / (2.0f * (dist1 + dist3 - 2.0f * dist2));
+  if (deltaR < -1 || deltaR > 1) return;
+  float bestuR = LG.scale * ((float)scaleduR0 + (float)bestincR + deltaR);
+  float disparity = (uL - bestuR);
+  if (disparity >= minD && disparity < maxD) {
+    if (disparity <= 0) {
+      disparity = 0.01f;
+      bestuR = uL - 0.01f;
+    }
+    out.depth[o] = cam.bf / disparity;
+    out.u_right[o] = bestuR;
+    ws.sad[o] = bestSad;
+  }
+}
+
+// Median SAD filter (:564-576): drop matches whose SAD >= 2.1 * median.
+__global__ __launch_bounds__(256) void stereo_median_kernel(const OrbGeom* __restrict__ g,
+                                                            FrameKps ext, StereoWorkspace ws,
+                                                            StereoOut out) {
+  constexpr int kCap = 4096;
+  __shared__ int vals[kCap];
+  __shared__ int n_valid;
+  const int f = blockIdx.x, tid = threadIdx.x;
+  const int nl = min(ext.n[2 * f * ext.n_stride], kCap);
+  const int64_t base = (int64_t)f * g->kp_cap;
+  if (tid == 0) n_valid = 0;
+  __syncthreads();
+  for (int i = tid; i < nl; i += 256) {
+    const int s = ws.sad[base + i];
+    if (s >= 0) vals[atomicAdd(&n_valid, 1)] = s;
+  }
+  __syncthreads();
+  const int n = n_valid;
+  if (n == 0) return;  // the reference indexes an empty vector here (UB); we skip the filter
+  int P2 = 1;
+  while (P2 < n) P2 <<= 1;
+  for (int i = n + tid; i < P2; i += 256) vals[i] = 0x7fffffff;
+  __syncthreads();
+  for (int k = 2; k <= P2; k <<= 1)
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      for (int i = tid; i < P2; i += 256) {
+        const int ixj = i ^ j;
+        if (ixj > i) {
+          const int x = vals[i], y = vals[ixj];
+          if (((i & k) == 0) ? (x > y) : (x < y)) {
+            vals[i] = y;
+            vals[ixj] = x;
+          }
+        }
+      }
+      __syncthreads();
+    }
+  const float median = (float)vals[n / 2];
+  const float thDist = (1.5f * 1.4f) * median;
+  for (int i = tid; i < nl; i += 256) {
+    const int s = ws.sad[base + i];
+    if (s >= 0 && !((float)s < thDist)) {
+      out.u_right[base + i] = -1.0f;
+      out.depth[base + i] = -1.0f;
+      ws.sad[base + i] = -1;
+    }
+  }
+}
+
+void launch_stereo(const ImageBatch& b, const OrbGeomDev& gd, const Camera& cam, int n_frames,
+                   const StereoWorkspace& ws, const StereoOut& out, hipStream_t st) {
+  const OrbGeom& g = *gd.host;
+  FrameKps ext{gd.out.kps, gd.out.desc, gd.out.nkps, g.kp_cap, 1};
+  const int nrows = g.lv[0].h;
+  hipLaunchKernelGGL(stereo_rows_kernel, dim3(n_frames), dim3(256), 0, st, gd.dev, ext, nrows,
+                     ws, gd.ws.err);
+  hipLaunchKernelGGL(stereo_match_kernel, dim3((g.kp_cap + 3) / 4, n_frames), dim3(256), 0, st,
+                     b, gd.dev, ext, cam, nrows, ws, out);
+  hipLaunchKernelGGL(stereo_median_kernel, dim3(n_frames), dim3(256), 0, st, gd.dev, ext, ws,
+                     out);
+}
+
+// ---------------------------------------------------------------------------------------
+// Grid (AssignFeaturesToGrid + PosInGrid, frame.cpp:234-248, 339-346).
+__device__ __forceinline__ int grid_cell(const Camera& cam, float x, float y) {
+  const int px = (int)roundf((x - cam.min_x) / cam.cell_w);
+  const int py = (int)roundf((y - cam.min_y) / cam.cell_h);
+  if (px < 0 || px >= kGridCols || py < 0 || py >= kGridRows) return -1;
+  return px * kGridRows + py;
+}
+
+__global__ __launch_bounds__(256) void grid_build_kernel(FrameKps cur, Camera cam, int kp_cap,
+                                                         GridWorkspace gw) {
+  __shared__ int cnt[kGridCells + 1];
+  __shared__ int wsum[4];
+  const int f = blockIdx.x, tid = threadIdx.x;
+  const KeyPoint* k = cur.kps + f * cur.stride;
+  const int n = cur.n[f * cur.n_stride];
+  int* cs = gw.cell_start + (int64_t)f * (kGridCells + 1);
+  int* items = gw.cell_items + (int64_t)f * kp_cap;
+  for (int i = tid; i <= kGridCells; i += 256) cnt[i] = 0;
+  __syncthreads();
+  for (int i = tid; i < n; i += 256) {
+    const int c = grid_cell(cam, k[i].x, k[i].y);
+    if (c >= 0) atomicAdd(&cnt[c], 1);
+  }
+  __syncthreads();
+  const int total = scan256<kGridCells + 1>(cnt, kGridCells, wsum);
+  for (int i = tid; i < kGridCells; i += 256) cs[i] = cnt[i];
+  if (tid == 0) cs[kGridCells] = total;
+  __syncthreads();
+  for (int i = tid; i < n; i += 256) {
+    const int c = grid_cell(cam, k[i].x, k[i].y);
+    if (c >= 0) items[atomicAdd(&cnt[c], 1)] = i;
+  }
+}
+
+void launch_grid(const FrameKps& cur, const Camera& cam, int n_frames, int kp_cap,
+                 const GridWorkspace& gw, hipStream_t st) {
+  hipLaunchKernelGGL(grid_build_kernel, dim3(n_frames), dim3(256), 0, st, cur, cam, kp_cap, gw);
+}
+
+// ---------------------------------------------------------------------------------------
+// Candidate scan of one query by one wave: Frame::GetFeaturesInArea (frame.cpp:348-403) plus the
+// matcher's per-candidate filters, keeping the kTopK best candidates by (distance, position in
+// GetFeaturesInArea order). That order visits cells x-major then y, each cell by keypoint index,
+// so the position key is (ix * 48 + iy, index) -- which makes the lexicographic minimum equal
+// to the first strict-'<' winner of the reference's sequential loop.
+struct ScanCtx {
+  float x, y, r;         // GetFeaturesInArea(x, y, r, min_level, max_level)
+  int min_level, max_level;
+  float ur, gate;        // skip if u_right > 0 && fabsf(ur - u_right) > gate
+  int max_dist;          // keep candidates with distance <= max_dist
+  const uint8_t* desc;   // query descriptor
+};
+
+struct FrameView {
+  const KeyPoint* kps;
+  const uint8_t* desc;
+  const float* u_right;
+  const int* cell_start;
+  const int* cell_items;
+  const uint8_t* blocked;
+};
+
+__device__ int scan_query(const ScanCtx& c, const Camera& cam, const FrameView& F,
+                          const uint32_t* claimed, uint64_t* top, int lane) {
+  const int nMinCellX = max(0, (int)floorf((c.x - cam.min_x - c.r) / cam.cell_w));
+  const int nMaxCellX = min(kGridCols - 1, (int)ceilf((c.x - cam.min_x + c.r) / cam.cell_w));
+  const int nMinCellY = max(0, (int)floorf((c.y - cam.min_y - c.r) / cam.cell_h));
+  const int nMaxCellY = min(kGridRows - 1, (int)ceilf((c.y - cam.min_y + c.r) / cam.cell_h));
+  uint64_t t[kTopK];
+#pragma unroll
+  for (int k = 0; k < kTopK; k++) t[k] = kNoKey;
+  int cnt = 0;
+  if (!(nMaxCellX < 0 || nMinCellX >= kGridCols || nMaxCellY < 0 || nMinCellY >= kGridRows)) {
+    const bool bCheckLevels = (c.min_level > 0) || (c.max_level >= 0);
+    const int ny = nMaxCellY - nMinCellY + 1;
+    const int total = (nMaxCellX - nMinCellX + 1) * ny;
+    for (int ci = lane; ci < total; ci += 64) {
+      const int ix = nMinCellX + ci / ny, iy = nMinCellY + ci % ny;
+      const int cell = ix * kGridRows + iy;
+      const int p1 = F.cell_start[cell + 1];
+      for (int p = F.cell_start[cell]; p < p1; p++) {
+        const int i = F.cell_items[p];
+        const KeyPoint kp = F.kps[i];
+        if (bCheckLevels) {
+          if (kp.octave < c.min_level) continue;
+          if (c.max_level >= 0 && kp.octave > c.max_level) continue;
+        }
+        const float distx = kp.x - c.x, disty = kp.y - c.y;
+        if (!(fabsf(distx) < c.r && fabsf(disty) < c.r)) continue;
+        if (F.blocked[i]) continue;
+        if (claimed && (claimed[i >> 5] >> (i & 31)) & 1u) continue;
+        const float ur = F.u_right[i];
+        if (ur > 0 && fabsf(c.ur - ur) > c.gate) continue;
+        const int dist = hamming32(c.desc, F.desc + i * 32);
+        if (dist > c.max_dist) continue;
+        const uint64_t key = ((uint64_t)dist << 32) | ((uint64_t)cell << 12) | (uint64_t)i;
+        cnt++;
+        if (key < t[kTopK - 1]) {
+          t[kTopK - 1] = key;
+#pragma unroll
+          for (int k = kTopK - 1; k > 0; k--)
+            if (t[k] < t[k - 1]) {
+              const uint64_t s = t[k];
+              t[k] = t[k - 1];
+              t[k - 1] = s;
+            }
+        }
+      }
+    }
+  }
+  // merge the per-lane sorted lists: kTopK rounds of wave minimum
+#pragma unroll
+  for (int k = 0; k < kTopK; k++) {
+    const uint64_t m = wave_min(t[0]);
+    if (t[0] == m && m != kNoKey) {
+#pragma unroll
+      for (int j = 0; j < kTopK - 1; j++) t[j] = t[j + 1];
+      t[kTopK - 1] = kNoKey;
+    }
+    top[k] = m;
+  }
+  return wave_sum(cnt);
+}
+
+__device__ __forceinline__ int key_idx(uint64_t k) { return (int)(k & 0xfff); }
+__device__ __forceinline__ int key_dist(uint64_t k) { return (int)(k >> 32); }
+
+// OpenCV small float gemm d = A*b + c (matmul.cpp, len 3): float dot, then (float)((double)+).
+__device__ __forceinline__ float mat3_row(const float* R, int r, const float* x, float c) {
+  const float dot = R[3 * r] * x[0] + R[3 * r + 1] * x[1] + R[3 * r + 2] * x[2];
+  return (float)((double)dot + (double)c);
+}
+
+// SearchByProjection(CurrentFrame, LastFrame) per-query setup (orb_matcher.cpp:1336-1376).
+__device__ bool f2f_ctx(const F2FQuery& q, const F2FPose& P, const Camera& cam,
+                        const OrbGeom* g, ScanCtx* c) {
+  const float xc = mat3_row(P.Rcw, 0, q.xyz, P.tcw[0]);
+  const float yc = mat3_row(P.Rcw, 1, q.xyz, P.tcw[1]);
+  const float zc = mat3_row(P.Rcw, 2, q.xyz, P.tcw[2]);
+  const float invzc = (float)(1.0 / (double)zc);
+  if (invzc < 0) return false;
+  const float u = fmaf(cam.fx * xc, invzc, cam.cx);
+  const float v = fmaf(cam.fy * yc, invzc, cam.cy);
+  if (u < cam.min_x || u > cam.max_x) return false;
+  if (v < cam.min_y || v > cam.max_y) return false;
+  const int nLastOctave = q.last_octave;
+  const float radius = P.th * g->lv[nLastOctave].scale;
+  const bool bForward = P.tlc_z > P.baseline && !P.mono;
+  const bool bBackward = -P.tlc_z > P.baseline && !P.mono;
+  c->x = u;
+  c->y = v;
+  c->r = radius;
+  if (bForward) {
+    c->min_level = nLastOctave;
+    c->max_level = -1;
+  } else if (bBackward) {
+    c->min_level = 0;
+    c->max_level = nLastOctave;
+  } else {
+    c->min_level = nLastOctave - 1;
+    c->max_level = nLastOctave + 1;
+  }
+  c->ur = fmaf(-cam.bf, invzc, u);
+  c->gate = radius;
+  c->max_dist = TH_HIGH;  // a candidate above TH_HIGH can never become the accepted match
+  c->desc = q.desc;
+  return true;
+}
+
+// SearchByProjection(F, vpMapPoints, th) per-query setup (orb_matcher.cpp:21-41, 105-111).
+__device__ bool mps_ctx(const MpsQuery& q, int th, const OrbGeom* g, ScanCtx* c) {
+  if (!q.in_view || q.is_bad) return false;
+  float r = ((double)q.view_cos > 0.998) ? 2.5f : 4.0f;
+  if (th != 1) r *= (float)th;
+  const float rs = r * g->lv[q.level].scale;
+  c->x = q.proj_x;
+  c->y = q.proj_y;
+  c->r = rs;
+  c->min_level = q.level - 1;
+  c->max_level = q.level;
+  c->ur = q.proj_xr;
+  c->gate = rs;
+  c->max_dist = 256;
+  c->desc = q.desc;
+  return true;
+}
+
+template <typename Q>
+__global__ __launch_bounds__(256) void search_cand_kernel(
+    FrameKps cur, const float* __restrict__ u_right, int64_t ur_stride, Camera cam,
+    const OrbGeom* __restrict__ g, const Q* __restrict__ queries, const F2FPose* __restrict__ poses,
+    int th, GridWorkspace gw, MatchWorkspace mw, MatchIO io) {
+  const int f = blockIdx.y;
+  const int lane = threadIdx.x & 63;
+  const int qi = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (qi >= io.q_count[f]) return;
+  const int q = io.q_start[f] + qi;
+  FrameView F;
+  F.kps = cur.kps + f * cur.stride;
+  F.desc = cur.desc + f * cur.stride * 32;
+  F.u_right = u_right + f * ur_stride;
+  F.cell_start = gw.cell_start + (int64_t)f * (kGridCells + 1);
+  F.cell_items = gw.cell_items + (int64_t)f * g->kp_cap;
+  F.blocked = io.blocked + f * io.mp_stride;
+  ScanCtx c;
+  bool ok;
+  if constexpr (sizeof(Q) == sizeof(F2FQuery)) {
+    ok = f2f_ctx(queries[q], poses[f], cam, g, &c);
+  } else {
+    ok = mps_ctx(queries[q], th, g, &c);
+  }
+  uint64_t top[kTopK];
+  int n = 0;
+  if (ok) {
+    n = scan_query(c, cam, F, nullptr, top, lane);
+  } else {
+#pragma unroll
+    for (int k = 0; k < kTopK; k++) top[k] = kNoKey;
+  }
+  if (lane < kTopK) {
+    uint64_t v = top[0];
+#pragma unroll
+    for (int k = 1; k < kTopK; k++)
+      if (lane == k) v = top[k];
+    mw.topk[(int64_t)q * kTopK + lane] = v;
+  }
+  if (lane == 0) mw.ncand[q] = ok ? n : 0;
+}
+
+// Sequential, in-query-order claim resolution: one wave per frame.
+template <typename Q>
+__global__ __launch_bounds__(64) void search_resolve_kernel(
+    FrameKps cur, const float* __restrict__ u_right, int64_t ur_stride, Camera cam,
+    const OrbGeom* __restrict__ g, const Q* __restrict__ queries, const F2FPose* __restrict__ poses,
+    int th, float nnratio, GridWorkspace gw, MatchWorkspace mw, MatchIO io) {
+  constexpr bool kF2F = sizeof(Q) == sizeof(F2FQuery);
+  __shared__ uint32_t claimed[128];  // kp_cap <= 4096
+  __shared__ int hist[HISTO_LENGTH];
+  const int f = blockIdx.x;
+  const int lane = threadIdx.x;
+  const int n = cur.n[f * cur.n_stride];
+  for (int i = lane; i < 128; i += 64) claimed[i] = 0;
+  if (lane < HISTO_LENGTH) hist[lane] = 0;
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  FrameView F;
+  F.kps = cur.kps + f * cur.stride;
+  F.desc = cur.desc + f * cur.stride * 32;
+  F.u_right = u_right + f * ur_stride;
+  F.cell_start = gw.cell_start + (int64_t)f * (kGridCells + 1);
+  F.cell_items = gw.cell_items + (int64_t)f * g->kp_cap;
+  F.blocked = io.blocked + f * io.mp_stride;
+  int* mp = io.map_point + f * io.mp_stride;
+  uint8_t* blk = io.blocked + f * io.mp_stride;
+  const int q0 = io.q_start[f], qn = io.q_count[f];
+  int nm = 0;
+  for (int qi = 0; qi < qn; qi++) {
+    const int q = q0 + qi;
+    const int nc = mw.ncand[q];
+    if (lane == 0) mw.rot_bin[q] = -1;
+    if (nc == 0) continue;
+    uint64_t key = (lane < kTopK) ? mw.topk[(int64_t)q * kTopK + lane] : kNoKey;
+    bool ok = key != kNoKey && !((claimed[key_idx(key) >> 5] >> (key_idx(key) & 31)) & 1u);
+    uint64_t msk = __ballot(ok);
+    uint64_t b1 = kNoKey, b2 = kNoKey;
+    const int need = kF2F ? 1 : 2;
+    if (__popcll(msk) < need && nc > kTopK) {
+      // every kept candidate is already claimed: rescan with the live claims
+      ScanCtx c;
+      bool okc;
+      if constexpr (kF2F) okc = f2f_ctx(queries[q], poses[f], cam, g, &c);
+      else okc = mps_ctx(queries[q], th, g, &c);
+      uint64_t top[kTopK];
+      if (okc) scan_query(c, cam, F, claimed, top, lane);
+      b1 = okc ? top[0] : kNoKey;
+      b2 = okc ? top[1] : kNoKey;
+    } else {
+      const int l1 = msk ? __ffsll((long long)msk) - 1 : -1;
+      const uint64_t msk2 = l1 >= 0 ? (msk & ~(1ull << l1)) : 0;
+      const int l2 = msk2 ? __ffsll((long long)msk2) - 1 : -1;
+      const uint64_t k1 = __shfl(key, l1 < 0 ? 0 : l1, 64);
+      const uint64_t k2 = __shfl(key, l2 < 0 ? 0 : l2, 64);
+      b1 = l1 >= 0 ? k1 : kNoKey;
+      b2 = l2 >= 0 ? k2 : kNoKey;
+    }
+    if (b1 == kNoKey) continue;
+    const int bestDist = key_dist(b1);
+    if (bestDist > TH_HIGH) continue;
+    const int idx = key_idx(b1);
+    if constexpr (!kF2F) {
+      const int bestLevel = F.kps[idx].octave;
+      const int bestDist2 = b2 == kNoKey ? 256 : key_dist(b2);
+      const int bestLevel2 = b2 == kNoKey ? -1 : F.kps[key_idx(b2)].octave;
+      if (bestLevel == bestLevel2 && (float)bestDist > nnratio * (float)bestDist2) continue;
+    }
+    const Q& qq = queries[q];
+    if (lane == 0) {
+      mp[idx] = qq.mp_id;
+      blk[idx] = qq.blocks ? 1 : 0;
+      if (qq.blocks) claimed[idx >> 5] |= 1u << (idx & 31);
+    }
+    nm++;
+    if constexpr (kF2F) {
+      if (poses[f].check_ori) {
+        float rot = qq.last_angle - F.kps[idx].angle;
+        if (rot < 0.0f) rot += 360.0f;
+        const float factor = 1.0f / HISTO_LENGTH;
+        int bin = (int)roundf(rot * factor);
+        if (bin == HISTO_LENGTH) bin = 0;
+        if (lane == 0) {
+          mw.rot_bin[q] = bin;
+          mw.best_idx[q] = idx;
+          hist[bin]++;
+        }
+      }
+    }
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  }
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  if constexpr (kF2F) {
+    if (poses[f].check_ori) {
+      // ComputeThreeMaxima (orb_matcher.cpp:1584-1625)
+      int max1 = 0, max2 = 0, max3 = 0, ind1 = -1, ind2 = -1, ind3 = -1;
+      for (int i = 0; i < HISTO_LENGTH; i++) {
+        const int s = hist[i];
+        if (s > max1) {
+          max3 = max2; max2 = max1; max1 = s;
+          ind3 = ind2; ind2 = ind1; ind1 = i;
+        } else if (s > max2) {
+          max3 = max2; max2 = s;
+          ind3 = ind2; ind2 = i;
+        } else if (s > max3) {
+          max3 = s;
+          ind3 = i;
+        }
+      }
+      if (max2 < 0.1f * (float)max1) {
+        ind2 = -1;
+        ind3 = -1;
+      } else if (max3 < 0.1f * (float)max1) {
+        ind3 = -1;
+      }
+      // SetMapPoint(rotHist[i][j], nullptr) for every entry of a rejected bin (:1441-1450)
+      int removed = 0;
+      for (int qi = lane; qi < qn; qi += 64) {
+        const int bin = mw.rot_bin[q0 + qi];
+        if (bin >= 0 && bin != ind1 && bin != ind2 && bin != ind3) {
+          const int idx = mw.best_idx[q0 + qi];
+          mp[idx] = -1;
+          blk[idx] = 0;
+          removed++;
+        }
+      }
+      nm -= wave_sum(removed);
+    }
+  }
+  (void)n;
+  if (lane == 0) io.nmatches[f] = nm;
+}
+
+void launch_search_frame(const FrameKps& cur, const float* u_right, int64_t ur_stride,
+                         const Camera& cam, const OrbGeomDev& g, const F2FQuery* queries,
+                         const F2FPose* poses, int n_frames, int max_q, const GridWorkspace& gw,
+                         const MatchWorkspace& mw, const MatchIO& io, hipStream_t st) {
+  if (max_q > 0)
+    hipLaunchKernelGGL(search_cand_kernel<F2FQuery>, dim3((max_q + 3) / 4, n_frames), dim3(256),
+                       0, st, cur, u_right, ur_stride, cam, g.dev, queries, poses, 0, gw, mw, io);
+  hipLaunchKernelGGL(search_resolve_kernel<F2FQuery>, dim3(n_frames), dim3(64), 0, st, cur,
+                     u_right, ur_stride, cam, g.dev, queries, poses, 0, 0.0f, gw, mw, io);
+}
+
+void launch_search_mps(const FrameKps& cur, const float* u_right, int64_t ur_stride,
+                       const Camera& cam, const OrbGeomDev& g, const MpsQuery* queries,
+                       float nnratio, int th, int n_frames, int max_q, const GridWorkspace& gw,
+                       const MatchWorkspace& mw, const MatchIO& io, hipStream_t st) {
+  if (max_q > 0)
+    hipLaunchKernelGGL(search_cand_kernel<MpsQuery>, dim3((max_q + 3) / 4, n_frames), dim3(256),
+                       0, st, cur, u_right, ur_stride, cam, g.dev, queries,
+                       (const F2FPose*)nullptr, th, gw, mw, io);
+  hipLaunchKernelGGL(search_resolve_kernel<MpsQuery>, dim3(n_frames), dim3(64), 0, st, cur,
+                     u_right, ur_stride, cam, g.dev, queries, (const F2FPose*)nullptr, th,
+                     nnratio, gw, mw, io);
+}
+
+}  // namespace slamgpu

@@ -1,0 +1,208 @@
+// orb_geometry.cpp -- ORBextractor ctor tables and per-level launch geometry (host side).
+//
+// Mirrors src/orb_features/orb_extractor.cpp:351-411 (scale tables, per-level budget, umax),
+// :706-733 (cell grid), :480-488 (octree initial split) and :1051-1057 (level sizes), plus
+// OpenCV 3.3.1 resize's coefficient tables (imgproc resize.cpp, INTER_LINEAR, CV_8U).
+// Compiled with -ffp-contract=off so float arithmetic matches the reference expression by
+// expression.
+#include "orb_geometry.h"
+#include "orb_tables.h"
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+
+namespace slamgpu {
+
+static inline int cv_round_h(float v) { return (int)std::lrintf(v); }
+static inline int16_t sat_short(float v) {
+  int i = (int)std::lrintf(v);
+  return (int16_t)std::min(32767, std::max(-32768, i));
+}
+
+void compute_tables(const OrbParams& p, OrbTables* t) {
+  std::memset(t, 0, sizeof(*t));
+  t->nlevels = p.nlevels;
+  const double sf = (double)p.scale_factor;  // ORBextractor::scaleFactor is a double
+  t->scale[0] = 1.0f;
+  t->sigma2[0] = 1.0f;
+  for (int i = 1; i < p.nlevels; i++) {
+    t->scale[i] = (float)((double)t->scale[i - 1] * sf);
+    t->sigma2[i] = t->scale[i] * t->scale[i];
+  }
+  for (int i = 0; i < p.nlevels; i++) {
+    t->inv_scale[i] = 1.0f / t->scale[i];
+    t->inv_sigma2[i] = 1.0f / t->sigma2[i];
+  }
+  const float factor = (float)(1.0f / sf);
+  float nDesired = (float)p.nfeatures * (1 - factor) /
+                   (1 - (float)std::pow((double)factor, (double)p.nlevels));
+  int sum = 0;
+  for (int l = 0; l < p.nlevels - 1; l++) {
+    t->features_per_level[l] = cv_round_h(nDesired);
+    sum += t->features_per_level[l];
+    nDesired *= factor;
+  }
+  t->features_per_level[p.nlevels - 1] = std::max(p.nfeatures - sum, 0);
+  int v, v0;
+  const int vmax = (int)std::floor(kHalfPatch * std::sqrt(2.f) / 2 + 1);
+  const int vmin = (int)std::ceil(kHalfPatch * std::sqrt(2.f) / 2);
+  const double hp2 = kHalfPatch * kHalfPatch;
+  for (v = 0; v <= vmax; ++v) t->umax[v] = (int)std::lrint(std::sqrt(hp2 - v * v));
+  for (v = kHalfPatch, v0 = 0; v >= vmin; --v) {
+    while (t->umax[v0] == t->umax[v0 + 1]) ++v0;
+    t->umax[v] = v0;
+    ++v0;
+  }
+}
+
+// getGaussianKernel(7, 2, CV_32F) then convertTo(CV_32S, 256) (OpenCV 3.3.1 smooth.cpp /
+// filter.cpp createSeparableLinearFilter for 8U): {18, 34, 49, 55, 49, 34, 18}, sum 257.
+static void gauss_kernel_int(int k[7]) {
+  float cf[7];
+  double sum = 0;
+  const double sigma = 2.0, scale2X = -0.5 / (sigma * sigma);
+  for (int i = 0; i < 7; i++) {
+    double x = i - 3.0;
+    cf[i] = (float)std::exp(scale2X * x * x);
+    sum += cf[i];
+  }
+  sum = 1. / sum;
+  for (int i = 0; i < 7; i++) {
+    cf[i] = (float)(cf[i] * sum);
+    k[i] = (int)std::lrint((double)cf[i] * 256.0);
+  }
+}
+
+static inline int round_up(int v, int a) { return (v + a - 1) / a * a; }
+
+int compute_geometry(const OrbParams& p, int cols, int rows, OrbGeom* g,
+                     std::vector<ResizeX>* rx, std::vector<ResizeY>* ry) {
+  if (p.nlevels < 1 || p.nlevels > kMaxLevels || cols < 64 || rows < 64 || cols > 4095 ||
+      rows > 2047 || p.nfeatures < 1)
+    return -1;
+  OrbTables t;
+  compute_tables(p, &t);
+  std::memset(g, 0, sizeof(*g));
+  g->nlevels = p.nlevels;
+  g->cols = cols;
+  g->rows = rows;
+  g->nfeatures = p.nfeatures;
+  g->ini_th = p.ini_th_fast;
+  g->min_th = p.min_th_fast;
+  std::memcpy(g->umax, t.umax, sizeof(g->umax));
+  rx->clear();
+  ry->clear();
+  int64_t pyr_off = 0;
+  int cell_base = 0, max_wcell = 0, max_hcell = 0;
+  for (int l = 0; l < p.nlevels; l++) {
+    LevelGeom& L = g->lv[l];
+    L.scale = t.scale[l];
+    L.inv_scale = t.inv_scale[l];
+    L.w = cv_round_h((float)cols * t.inv_scale[l]);
+    L.h = cv_round_h((float)rows * t.inv_scale[l]);
+    if (L.w < 2 * kEdgeThreshold + 8 || L.h < 2 * kEdgeThreshold + 8) return -2;
+    L.pitch = round_up(L.w, 64);
+    if (l == 0) {
+      L.offset = 0;  // level 0 lives in the caller's image buffer
+    } else {
+      L.offset = pyr_off;
+      pyr_off += (int64_t)L.pitch * L.h;
+      pyr_off = (pyr_off + 255) & ~(int64_t)255;
+    }
+    // FAST cell grid (:712-733); float arithmetic as in the reference.
+    const float W = 30;
+    L.max_bx = L.w - kEdgeThreshold + 3;
+    L.max_by = L.h - kEdgeThreshold + 3;
+    const float width = (float)(L.max_bx - kMinBorder);
+    const float height = (float)(L.max_by - kMinBorder);
+    L.ncols = (int)(width / W);
+    L.nrows = (int)(height / W);
+    L.wcell = (int)std::ceil(width / L.ncols);
+    L.hcell = (int)std::ceil(height / L.nrows);
+    L.cell_base = cell_base;
+    cell_base += L.ncols * L.nrows;
+    max_wcell = std::max(max_wcell, L.wcell);
+    max_hcell = std::max(max_hcell, L.hcell);
+    // octree (:484-486)
+    L.budget = t.features_per_level[l];
+    L.n_ini = (int)std::round((float)(L.max_bx - kMinBorder) / (L.max_by - kMinBorder));
+    if (L.n_ini < 1) return -3;
+    L.hx = (float)(L.max_bx - kMinBorder) / L.n_ini;
+    L.node_cap = std::max(4 * L.n_ini, L.budget + 3);
+    L.out_cap = L.node_cap;
+    L.patch_size = (float)(int)(kPatchSize * t.scale[l]);
+    // resize tables for level l from level l-1 (OpenCV resize.cpp resize/resizeGeneric_)
+    if (l > 0) {
+      const LevelGeom& S = g->lv[l - 1];
+      const double inv_scale_x = (double)L.w / S.w, inv_scale_y = (double)L.h / S.h;
+      const double scale_x = 1. / inv_scale_x, scale_y = 1. / inv_scale_y;
+      L.rx_base = (int)rx->size();
+      L.xmax = L.w;
+      for (int dx = 0; dx < L.w; dx++) {
+        float fx = (float)((dx + 0.5) * scale_x - 0.5);
+        int sx = (int)std::floor(fx);
+        fx -= sx;
+        if (sx < 0) { fx = 0; sx = 0; }
+        if (sx + 1 >= S.w) {
+          L.xmax = std::min(L.xmax, dx);
+          if (sx >= S.w - 1) { fx = 0; sx = S.w - 1; }
+        }
+        ResizeX e;
+        e.sx = sx;
+        e.a0 = sat_short((1.f - fx) * 2048);
+        e.a1 = sat_short(fx * 2048);
+        rx->push_back(e);
+      }
+      L.ry_base = (int)ry->size();
+      for (int dy = 0; dy < L.h; dy++) {
+        float fy = (float)((dy + 0.5) * scale_y - 0.5);
+        int sy = (int)std::floor(fy);
+        fy -= sy;
+        ResizeY e;
+        e.y0 = std::min(std::max(sy, 0), S.h - 1);
+        e.y1 = std::min(std::max(sy + 1, 0), S.h - 1);
+        e.b0 = sat_short((1.f - fy) * 2048);
+        e.b1 = sat_short(fy * 2048);
+        ry->push_back(e);
+      }
+    }
+  }
+  g->cells_per_image = cell_base;
+  int64_t boff = 0;
+  int btiles = 0;
+  for (int l = 0; l < p.nlevels; l++) {
+    LevelGeom& L = g->lv[l];
+    L.blur_offset = boff;
+    boff += (int64_t)L.pitch * L.h;
+    boff = (boff + 255) & ~(int64_t)255;
+    L.blur_tile_base = btiles;
+    btiles += ((L.w + 63) / 64) * ((L.h + 15) / 16);
+  }
+  g->blur_bytes = boff;
+  g->blur_tiles = btiles;
+  gauss_kernel_int(g->gauss);
+  // strict 8-neighbour NMS keeps at most one pixel per 2x2 block of the detect area
+  g->cell_cap = ((max_wcell + 1) / 2) * ((max_hcell + 1) / 2);
+  g->pyr_bytes = pyr_off;
+  int64_t key_off = 0, node_off = 0;
+  int out_off = 0;
+  for (int l = 0; l < p.nlevels; l++) {
+    LevelGeom& L = g->lv[l];
+    const int64_t ncell = (int64_t)L.ncols * L.nrows;
+    L.key_cap = (int)std::min<int64_t>(ncell * g->cell_cap, 65536);
+    L.key_base = key_off;
+    key_off += 2 * (int64_t)L.key_cap;           // ping-pong
+    L.node_base = node_off;
+    node_off += 3 * (int64_t)L.node_cap * 4 + 64;  // two lists + speculative children
+    L.out_base = out_off;
+    out_off += L.out_cap;
+  }
+  g->keys_per_image = key_off;
+  g->nodes_per_image = node_off;
+  g->out_per_image = out_off;
+  g->kp_cap = out_off;
+  return 0;
+}
+
+}  // namespace slamgpu

@@ -1,0 +1,98 @@
+// orb_geometry.h -- host-computed, device-consumed description of one ORB configuration.
+//
+// Everything here is a pure function of the ORBextractor ctor arguments and the image size
+// (src/orb_features/orb_extractor.cpp:351-411 for the tables, :706-733 for the FAST cell grid,
+// :480-488 for the octree's initial split, :1051-1057 for the level sizes). It is computed once
+// on the host (orb_geometry.cpp) and passed by value to the kernels.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace slamgpu {
+
+constexpr int kMaxLevels = 12;
+constexpr int kEdgeThreshold = 19;
+constexpr int kMinBorder = kEdgeThreshold - 3;  // minBorderX/Y (:712)
+constexpr int kPatchSize = 31;
+constexpr int kHalfPatch = 15;
+constexpr int kDiscPixels = 749;               // |{(u,v): |v|<=15, |u|<=umax[|v|]}|
+
+struct LevelGeom {
+  int w, h;             // level image size
+  int pitch;            // row pitch of this level in the pyramid buffers (level >= 1)
+  int64_t offset;       // byte offset of this level inside one image's pyramid buffer
+  int64_t blur_offset;  // byte offset of this level inside one image's blurred buffer
+  // FAST cell grid (ComputeKeyPointsOctTree :712-733)
+  int max_bx, max_by;   // maxBorderX/Y
+  int ncols, nrows;     // cells
+  int wcell, hcell;
+  int cell_base;        // first cell of this level in the per-image cell list
+  // DistributeOctTree (:480-488)
+  int budget;           // mnFeaturesPerLevel[level]
+  int n_ini;
+  float hx;
+  int node_cap;         // max list length: max(4*n_ini, budget + 3)
+  int key_cap;          // max FAST candidates per (image, level) kept in scratch
+  int64_t key_base;     // offset (in keys) of this level in the per-image key scratch
+  int64_t node_base;    // offset (in nodes) of this level in the per-image node scratch
+  int out_base;         // offset (in keypoints) of this level in the per-image octree output
+  int out_cap;          // max keypoints this level can emit
+  // resize tables (level >= 1) in the shared table buffer
+  int rx_base, ry_base; // offsets into the x (per dst column) / y (per dst row) tables
+  int blur_tile_base;   // first 64x16 blur tile of this level
+  int xmax;             // first dst column that copies S[sx] * 2048 (resize HResizeLinear)
+  float scale, inv_scale;
+  float patch_size;     // (float)(int)(PATCH_SIZE * scale) (:778)
+};
+
+struct OrbGeom {
+  int nlevels, cols, rows;
+  int nfeatures, ini_th, min_th;
+  int cells_per_image;
+  int cell_cap;          // max FAST survivors stored per cell
+  int64_t pyr_bytes;     // bytes of one image's pyramid (levels >= 1) buffer
+  int64_t blur_bytes;    // bytes of one image's blurred pyramid (levels >= 0) buffer
+  int blur_tiles;        // 64x16 blur tiles over all levels of one image
+  int gauss[7];          // GaussianBlur 7x7 sigma 2 integer kernel (x256)
+  int64_t keys_per_image;
+  int64_t nodes_per_image;
+  int out_per_image;     // sum of out_cap
+  int kp_cap;            // max keypoints per image after Compute (== out_per_image)
+  int umax[16];
+  LevelGeom lv[kMaxLevels];
+};
+
+// Resize tables (HResizeLinear / VResizeLinear coefficients, 11-bit fixed point).
+struct ResizeX { int32_t sx; int16_t a0, a1; };
+struct ResizeY { int32_t y0, y1; int16_t b0, b1; };
+
+// One FAST survivor / octree key: x_rel (12 b) | y_rel (11 b) << 12 | score (8 b) << 23,
+// coordinates relative to (minBorderX, minBorderY).
+__host__ __device__ inline uint32_t pack_key(int x, int y, int score) {
+  return (uint32_t)x | ((uint32_t)y << 12) | ((uint32_t)score << 23);
+}
+__host__ __device__ inline int key_x(uint32_t k) { return (int)(k & 0xfff); }
+__host__ __device__ inline int key_y(uint32_t k) { return (int)((k >> 12) & 0x7ff); }
+__host__ __device__ inline int key_score(uint32_t k) { return (int)(k >> 23); }
+
+// Octree list node: rectangle [x0,x1] x [y0,y1] (UL/UR/BL/BR of ExtractorNode), keys
+// [kbeg, kbeg+n) in key buffer `buf`, creation sequence number (the pointer-order proxy).
+struct OctNode {
+  int16_t x0, x1, y0, y1;
+  int32_t kbeg;
+  int32_t n;
+  int32_t seq;
+  int32_t buf;
+};
+
+// Error bits raised on the device (slamgpu_last_error reports them).
+enum : uint32_t {
+  kErrKeyOverflow = 1u << 0,   // more FAST candidates than key_cap for some level
+  kErrNodeOverflow = 1u << 1,  // octree list exceeded node_cap
+  kErrCellOverflow = 1u << 2,  // FAST survivors exceeded cell_cap
+  kErrSortOverflow = 1u << 3,  // octree inner-loop set exceeded the LDS sort capacity
+  kErrRowOverflow = 1u << 4,   // stereo row table overflow
+  kErrCandOverflow = 1u << 5,  // matcher candidate list overflow
+};
+
+}  // namespace slamgpu

@@ -1,0 +1,866 @@
+// orb_kernels.hip -- the ORBextractor::Compute hot path as gfx950 kernels, batched over images.
+//
+// Pipeline for a batch of n images (all levels of all images in flight together):
+//   pyr_down      level l from level l-1 (resize INTER_LINEAR 8U)        one launch per level
+//   blur7         7x7 Gaussian of every level (descriptor input)         one launch
+//   fast_cells    per-cell FAST-9 score, threshold fallback, cell NMS    one wave per cell
+//   octree        DistributeOctTree, exact list / pointer-order semantics one workgroup per level
+//   orient_desc   IC_Angle + rBRIEF, output in ORBextractor::Compute order one wave per keypoint
+// Reference: src/orb_features/orb_extractor.cpp (citations per kernel). Built with
+// -ffp-contract=off; fused multiply-adds are explicit where the reference's Release build fuses.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "device_math.h"
+#include "orb_geometry.h"
+#include "orb_kernels.h"
+
+namespace slamgpu {
+
+__constant__ int8_t c_pattern[1024] = {
+#include "orb_pattern.inc"
+};
+
+// ---------------------------------------------------------------------------------------
+// Level addressing. Level 0 is the caller's image; levels >= 1 live in the pyramid buffer.
+__device__ __forceinline__ const uint8_t* level_ptr(const ImageBatch& b, const OrbGeom* g,
+                                                    int img, int level, int* pitch) {
+  if (level == 0) {
+    *pitch = b.in_pitch;
+    return batch_image(b, img);
+  }
+  *pitch = g->lv[level].pitch;
+  return b.pyr + (int64_t)img * g->pyr_bytes + g->lv[level].offset;
+}
+
+// ---------------------------------------------------------------------------------------
+// pyr_down: ComputePyramid (:1051-1075) -> cv::resize(level l-1, level l, INTER_LINEAR).
+// HResizeLinear (int = S[sx]*a0 + S[sx+1]*a1, or S[sx]*2048 from xmax on) then VResizeLinear
+// ((b0*(r0>>4))>>16) + ((b1*(r1>>4))>>16) + 2) >> 2. Each thread produces 4 adjacent pixels.
+__global__ __launch_bounds__(256) void pyr_down_kernel(ImageBatch b, const OrbGeom* __restrict__ g,
+                                                       int level,
+                                                       const ResizeX* __restrict__ rxt,
+                                                       const ResizeY* __restrict__ ryt) {
+  const int img = blockIdx.z;
+  const int dy = blockIdx.y;
+  const LevelGeom& D = g->lv[level];
+  int spitch;
+  const uint8_t* src = level_ptr(b, g, img, level - 1, &spitch);
+  uint8_t* dst = b.pyr + (int64_t)img * g->pyr_bytes + D.offset + (int64_t)dy * D.pitch;
+  const ResizeY ey = ryt[D.ry_base + dy];
+  const uint8_t* S0 = src + (int64_t)ey.y0 * spitch;
+  const uint8_t* S1 = src + (int64_t)ey.y1 * spitch;
+  const int x0 = (blockIdx.x * blockDim.x + threadIdx.x) * 4;
+  if (x0 >= D.w) return;
+  uint32_t packed = 0;
+#pragma unroll
+  for (int k = 0; k < 4; k++) {
+    const int dx = x0 + k;
+    int v = 0;
+    if (dx < D.w) {
+      const ResizeX ex = rxt[D.rx_base + dx];
+      int r0, r1;
+      if (dx < D.xmax) {
+        r0 = S0[ex.sx] * ex.a0 + S0[ex.sx + 1] * ex.a1;
+        r1 = S1[ex.sx] * ex.a0 + S1[ex.sx + 1] * ex.a1;
+      } else {
+        r0 = S0[ex.sx] * 2048;
+        r1 = S1[ex.sx] * 2048;
+      }
+      v = (((ey.b0 * (r0 >> 4)) >> 16) + ((ey.b1 * (r1 >> 4)) >> 16) + 2) >> 2;
+    }
+    packed |= (uint32_t)(v & 0xff) << (8 * k);
+  }
+  if (x0 + 4 <= D.w) {
+    *reinterpret_cast<uint32_t*>(dst + x0) = packed;  // pitch is a multiple of 64
+  } else {
+    for (int k = 0; x0 + k < D.w; k++) dst[x0 + k] = (uint8_t)(packed >> (8 * k));
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// blur7: Compute (:1029-1030) clone + GaussianBlur(7x7, 2, 2, BORDER_REFLECT_101) per level.
+// Row pass: exact int sums over the reflect-101 extended row. Column pass: OpenCV 3.3.1's
+// SymmColumnVec_32s8u covers x < w - w%4 and rounds V/65536 half-to-even; the scalar tail rounds
+// (V + 32768) >> 16. A 256-thread block produces a 64x16 tile.
+__device__ __forceinline__ int reflect101(int i, int n) {
+  if (i < 0) i = -i;
+  if (i >= n) i = 2 * n - 2 - i;
+  return i;
+}
+
+__global__ __launch_bounds__(256) void blur7_kernel(ImageBatch b, const OrbGeom* __restrict__ g) {
+  __shared__ uint8_t tin[22][72];
+  __shared__ int th[22][64];
+  const int img = blockIdx.y;
+  int tile = blockIdx.x;
+  int level = 0;
+  while (level + 1 < g->nlevels && tile >= g->lv[level + 1].blur_tile_base) level++;
+  const LevelGeom& L = g->lv[level];
+  tile -= L.blur_tile_base;
+  const int tiles_x = (L.w + 63) / 64;
+  const int tx0 = (tile % tiles_x) * 64, ty0 = (tile / tiles_x) * 16;
+  int spitch;
+  const uint8_t* src = level_ptr(b, g, img, level, &spitch);
+  uint8_t* dst = b.blur + (int64_t)img * g->blur_bytes + L.blur_offset;
+  const int t = threadIdx.x;
+  for (int i = t; i < 22 * 70; i += 256) {
+    const int r = i / 70, c = i % 70;
+    const int sy = reflect101(ty0 - 3 + r, L.h), sx = reflect101(tx0 - 3 + c, L.w);
+    tin[r][c] = src[(int64_t)sy * spitch + sx];
+  }
+  __syncthreads();
+  const int k0 = g->gauss[0], k1 = g->gauss[1], k2 = g->gauss[2], k3 = g->gauss[3];
+  for (int i = t; i < 22 * 64; i += 256) {
+    const int r = i >> 6, c = i & 63;
+    const uint8_t* p = &tin[r][c];
+    th[r][c] = k3 * p[3] + k2 * (p[2] + p[4]) + k1 * (p[1] + p[5]) + k0 * (p[0] + p[6]);
+  }
+  __syncthreads();
+  const int xvec = L.w - (L.w % 4);
+  const int c = t & 63;
+  const int x = tx0 + c;
+  for (int r = t >> 6; r < 16; r += 4) {
+    const int y = ty0 + r;
+    if (y >= L.h || x >= L.w) continue;
+    const int v = k3 * th[r + 3][c] + k2 * (th[r + 2][c] + th[r + 4][c]) +
+                  k1 * (th[r + 1][c] + th[r + 5][c]) + k0 * (th[r][c] + th[r + 6][c]);
+    int o = (x < xvec) ? (int)rintf((float)v * (1.0f / 65536.0f)) : ((v + 32768) >> 16);
+    o = o < 0 ? 0 : (o > 255 ? 255 : o);
+    dst[(int64_t)y * L.pitch + x] = (uint8_t)o;
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// fast_cells: ComputeKeyPointsOctTree cell loop (:730-770) with cv::FAST(th, nonmax=true).
+// For a FAST corner the cornerScore<16> value does not depend on the threshold it was found
+// at: score = s - 1 with s = max over the 16 contiguous 9-arcs of min |I_ring - I_center|
+// (same sign along the arc), and p is a corner at threshold t iff s > t. So one s-map per cell
+// serves both passes: NMS at iniTh, and again at minTh if nothing survived (:753-757).
+// NMS is strict '>' against the 8 neighbours' scores at that t, zero outside the detect area
+// (cell-local, as cv::FAST sees only the cell view). Survivors are written in row-major order.
+constexpr int kCellWaves = 4;
+constexpr int kTileStride = 68;   // >= max view width (wCell + 6 <= 66)
+constexpr int kTileRows = 66;
+constexpr int kScoreStride = 64;  // >= max detect width
+constexpr int kScoreRows = 60;
+
+__device__ __forceinline__ int fast_s(const uint8_t* t, int o) {
+  // ring offsets (dx, dy) of makeOffsets(16) in tile coordinates
+  const int v = t[o];
+  int d[16];
+  d[0] = v - t[o + 3 * kTileStride];
+  d[1] = v - t[o + 1 + 3 * kTileStride];
+  d[2] = v - t[o + 2 + 2 * kTileStride];
+  d[3] = v - t[o + 3 + 1 * kTileStride];
+  d[4] = v - t[o + 3];
+  d[5] = v - t[o + 3 - 1 * kTileStride];
+  d[6] = v - t[o + 2 - 2 * kTileStride];
+  d[7] = v - t[o + 1 - 3 * kTileStride];
+  d[8] = v - t[o - 3 * kTileStride];
+  d[9] = v - t[o - 1 - 3 * kTileStride];
+  d[10] = v - t[o - 2 - 2 * kTileStride];
+  d[11] = v - t[o - 3 - 1 * kTileStride];
+  d[12] = v - t[o - 3];
+  d[13] = v - t[o - 3 + 1 * kTileStride];
+  d[14] = v - t[o - 2 + 2 * kTileStride];
+  d[15] = v - t[o - 1 + 3 * kTileStride];
+  int mn2[16], mx2[16];
+#pragma unroll
+  for (int k = 0; k < 16; k++) {
+    mn2[k] = min(d[k], d[(k + 1) & 15]);
+    mx2[k] = max(d[k], d[(k + 1) & 15]);
+  }
+  int mn4[16], mx4[16];
+#pragma unroll
+  for (int k = 0; k < 16; k++) {
+    mn4[k] = min(mn2[k], mn2[(k + 2) & 15]);
+    mx4[k] = max(mx2[k], mx2[(k + 2) & 15]);
+  }
+  int sd = -1024, sb = 1024;
+#pragma unroll
+  for (int k = 0; k < 16; k++) {
+    const int mn9 = min(min(mn4[k], mn4[(k + 4) & 15]), d[(k + 8) & 15]);
+    const int mx9 = max(max(mx4[k], mx4[(k + 4) & 15]), d[(k + 8) & 15]);
+    sd = max(sd, mn9);   // darker ring: v - p > t along the arc
+    sb = min(sb, mx9);   // brighter ring: p - v > t  <=>  max(v - p) < -t
+  }
+  return max(sd, -sb);
+}
+
+__global__ __launch_bounds__(256) void fast_cells_kernel(ImageBatch b,
+                                                         const OrbGeom* __restrict__ g,
+                                                         uint32_t* __restrict__ cell_keys,
+                                                         int* __restrict__ cell_count,
+                                                         uint32_t* __restrict__ err) {
+  __shared__ uint8_t s_tile[kCellWaves][kTileRows * kTileStride];
+  __shared__ uint8_t s_score[kCellWaves][kScoreRows * kScoreStride];
+  const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int img = blockIdx.y;
+  const int cell = blockIdx.x * kCellWaves + wid;
+  if (cell >= g->cells_per_image) return;
+  int level = 0;
+  while (level + 1 < g->nlevels && cell >= g->lv[level + 1].cell_base) level++;
+  const LevelGeom& L = g->lv[level];
+  const int c = cell - L.cell_base;
+  const int ci = c / L.ncols, cj = c % L.ncols;
+  const int64_t slot = (int64_t)img * g->cells_per_image + cell;
+  // cell view bounds (:735-749), all integer valued
+  const int iniY = kMinBorder + ci * L.hcell;
+  const int iniX = kMinBorder + cj * L.wcell;
+  int maxY = iniY + L.hcell + 6, maxX = iniX + L.wcell + 6;
+  if (iniY >= L.max_by - 3 || iniX >= L.max_bx - 6) {
+    if (lane == 0) cell_count[slot] = 0;
+    return;
+  }
+  if (maxY > L.max_by) maxY = L.max_by;
+  if (maxX > L.max_bx) maxX = L.max_bx;
+  const int vh = maxY - iniY, vw = maxX - iniX;
+  const int dh = vh - 6, dw = vw - 6;  // detect area [3, vh-3) x [3, vw-3)
+  int pitch;
+  const uint8_t* src = level_ptr(b, g, img, level, &pitch) + (int64_t)iniY * pitch + iniX;
+  uint8_t* tile = s_tile[wid];
+  uint8_t* sc = s_score[wid];
+  for (int r = 0; r < vh; r++)
+    for (int x = lane; x < vw; x += 64) tile[r * kTileStride + x] = src[(int64_t)r * pitch + x];
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  // score map; rows are processed 64/w_pad at a time so lanes map to (row, col) without division
+  const int wpad = dw <= 32 ? 32 : 64;
+  const int rows_per = 64 / wpad;
+  const int lr = lane / wpad, lc = lane % wpad;
+  int smax = 0;
+  for (int r0 = 0; r0 < dh; r0 += rows_per) {
+    const int r = r0 + lr;
+    if (r < dh && lc < dw) {
+      const int s = fast_s(tile, (r + 3) * kTileStride + lc + 3);
+      const int sv = s < 0 ? 0 : s;
+      sc[r * kScoreStride + lc] = (uint8_t)sv;
+      smax = max(smax, sv);
+    }
+  }
+  smax = wave_max(smax);
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  uint32_t* out = cell_keys + slot * g->cell_cap;
+  // FAST at iniTh; the reference re-runs at minTh when the iniTh *output* (after NMS) is empty
+  // (:753-757) -- corners can exist at iniTh and still all be suppressed by equal neighbours.
+  int count = 0;
+  for (int pass = (smax > g->ini_th) ? 0 : 1; pass < 2 && count == 0; pass++) {
+    const int th = pass == 0 ? g->ini_th : g->min_th;
+    for (int r0 = 0; r0 < dh; r0 += rows_per) {
+      const int r = r0 + lr;
+      bool keep = false;
+      int s = 0;
+      if (r < dh && lc < dw) {
+        s = sc[r * kScoreStride + lc];
+        if (s > th) {
+          const int score = s - 1;
+          keep = true;
+#pragma unroll
+          for (int dy = -1; dy <= 1; dy++)
+#pragma unroll
+            for (int dx = -1; dx <= 1; dx++) {
+              if (dx == 0 && dy == 0) continue;
+              const int rr = r + dy, cc = lc + dx;
+              int ns = 0;
+              if (rr >= 0 && rr < dh && cc >= 0 && cc < dw) {
+                const int q = sc[rr * kScoreStride + cc];
+                ns = q > th ? q - 1 : 0;
+              }
+              keep = keep && (score > ns);
+            }
+        }
+      }
+      const uint64_t m = __ballot(keep);
+      if (keep) {
+        const int pos = count + lanes_below(m);
+        if (pos < g->cell_cap) {
+          const int x_rel = iniX + 3 + lc - kMinBorder, y_rel = iniY + 3 + r - kMinBorder;
+          out[pos] = pack_key(x_rel, y_rel, s - 1);
+        }
+      }
+      count += __popcll(m);
+    }
+  }
+  if (lane == 0) {
+    if (count > g->cell_cap) {
+      atomicOr(err, kErrCellOverflow);
+      count = g->cell_cap;
+    }
+    cell_count[slot] = count;
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// octree: DistributeOctTree (:480-704), one 256-thread workgroup per (image, level).
+// The std::list is kept as an array in list order and rebuilt every pass; node keys are
+// contiguous index ranges that DivideNode splits by a stable 4-way partition (ballot ranks)
+// into the other half of a ping-pong key buffer. Creation sequence numbers stand in for the
+// heap addresses the reference sorts by (:625); see SURVEY.md Appendix B.1.
+//   outer pass (:528-613): every node with > 1 key is divided, children are pushed to the front
+//     in list order (n1..n4), so the new list is [children in reverse push order] + [nodes
+//     with one key, in order];
+//   inner loop (:615-676): the vPrev nodes are divided in descending (size, seq) order and the
+//     loop stops once the list reaches N -- done speculatively in parallel, then cut with a
+//     prefix sum; processed nodes leave the list and their children go to the front.
+constexpr int kOctThreads = 256;
+constexpr int kOctWaves = kOctThreads / 64;
+constexpr int kOctCap = 2048;  // max list length / inner-loop set size held in LDS
+
+struct OctShared {
+  uint64_t sortk[kOctCap];
+  int a[kOctCap];
+  int b[kOctCap];
+  int c[kOctCap];
+  int wsum[kOctWaves];
+  int bucket[64 + 1];
+  int m, seq_next, mode, nexp, finish, ktotal, total;
+};
+
+// Block-wide exclusive scan of v (one value per thread); returns prefix, *total gets the sum.
+__device__ __forceinline__ int block_scan(int v, int* wsum, int* total) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  int x = v;
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const int y = __shfl_up(x, off, 64);
+    if (lane >= off) x += y;
+  }
+  if (lane == 63) wsum[wid] = x;
+  __syncthreads();
+  int pre = 0, tot = 0;
+#pragma unroll
+  for (int w = 0; w < kOctWaves; w++) {
+    const int s = wsum[w];
+    pre += (w < wid) ? s : 0;
+    tot += s;
+  }
+  __syncthreads();
+  *total = tot;
+  return pre + x - v;
+}
+
+// Exclusive scan of arr[0..n) in place (n <= kOctCap); returns the total.
+__device__ int block_scan_array(int* arr, int n, int* wsum) {
+  constexpr int per = kOctCap / kOctThreads;
+  const int base = threadIdx.x * per;
+  int loc[per];
+  int s = 0;
+#pragma unroll
+  for (int i = 0; i < per; i++) {
+    loc[i] = (base + i < n) ? arr[base + i] : 0;
+    s += loc[i];
+  }
+  int total;
+  int pre = block_scan(s, wsum, &total);
+#pragma unroll
+  for (int i = 0; i < per; i++) {
+    if (base + i < n) arr[base + i] = pre;
+    pre += loc[i];
+  }
+  __syncthreads();
+  return total;
+}
+
+// DivideNode (:422-478) of `nd` by one wave: stable partition of its keys into n1..n4.
+__device__ void divide_wave(const OctNode& nd, uint32_t* const keys[2], OctNode ch[4],
+                            int lane) {
+  const int hx = (nd.x1 - nd.x0 + 1) >> 1;  // ceil((float)(UR.x-UL.x)/2)
+  const int hy = (nd.y1 - nd.y0 + 1) >> 1;  // ceil((float)(BR.y-UL.y)/2)
+  const int xm = nd.x0 + hx, ym = nd.y0 + hy;
+  const uint32_t* src = keys[nd.buf] + nd.kbeg;
+  uint32_t* dst = keys[nd.buf ^ 1] + nd.kbeg;
+  int cnt[4] = {0, 0, 0, 0};
+  for (int s = 0; s < nd.n; s += 64) {
+    const int i = s + lane;
+    int q = -1;
+    if (i < nd.n) {
+      const uint32_t k = src[i];
+      q = (key_x(k) >= xm ? 1 : 0) + (key_y(k) >= ym ? 2 : 0);
+    }
+#pragma unroll
+    for (int qq = 0; qq < 4; qq++) cnt[qq] += __popcll(__ballot(q == qq));
+  }
+  int start[4];
+  start[0] = 0;
+  start[1] = cnt[0];
+  start[2] = cnt[0] + cnt[1];
+  start[3] = start[2] + cnt[2];
+  int run[4] = {start[0], start[1], start[2], start[3]};
+  for (int s = 0; s < nd.n; s += 64) {
+    const int i = s + lane;
+    int q = -1;
+    uint32_t k = 0;
+    if (i < nd.n) {
+      k = src[i];
+      q = (key_x(k) >= xm ? 1 : 0) + (key_y(k) >= ym ? 2 : 0);
+    }
+#pragma unroll
+    for (int qq = 0; qq < 4; qq++) {
+      const uint64_t m = __ballot(q == qq);
+      if (q == qq) dst[run[qq] + lanes_below(m)] = k;
+      run[qq] += __popcll(m);
+    }
+  }
+  const int16_t xs[3] = {(int16_t)nd.x0, (int16_t)xm, (int16_t)nd.x1};
+  const int16_t ys[3] = {(int16_t)nd.y0, (int16_t)ym, (int16_t)nd.y1};
+#pragma unroll
+  for (int qq = 0; qq < 4; qq++) {
+    const int qx = qq & 1, qy = qq >> 1;
+    ch[qq].x0 = xs[qx];
+    ch[qq].x1 = xs[qx + 1];
+    ch[qq].y0 = ys[qy];
+    ch[qq].y1 = ys[qy + 1];
+    ch[qq].kbeg = nd.kbeg + start[qq];
+    ch[qq].n = cnt[qq];
+    ch[qq].seq = 0;
+    ch[qq].buf = nd.buf ^ 1;
+  }
+}
+
+__global__ __launch_bounds__(kOctThreads) void octree_kernel(
+    const OrbGeom* __restrict__ g, const uint32_t* __restrict__ cell_keys,
+    const int* __restrict__ cell_count, uint32_t* __restrict__ key_scratch,
+    OctNode* __restrict__ node_scratch, uint32_t* __restrict__ oct_keys,
+    int* __restrict__ oct_count, uint32_t* __restrict__ err) {
+  __shared__ OctShared S;
+  const int level = blockIdx.x, img = blockIdx.y;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const LevelGeom& L = g->lv[level];
+  const int N = L.budget;
+  const int ncell = L.ncols * L.nrows;
+  const int64_t cbase = (int64_t)img * g->cells_per_image + L.cell_base;
+  uint32_t* const keys[2] = {key_scratch + img * g->keys_per_image + L.key_base,
+                             key_scratch + img * g->keys_per_image + L.key_base + L.key_cap};
+  OctNode* const lists[2] = {node_scratch + img * g->nodes_per_image + L.node_base,
+                             node_scratch + img * g->nodes_per_image + L.node_base +
+                                 2 * L.node_cap};
+  OctNode* const child = node_scratch + img * g->nodes_per_image + L.node_base + 4 * L.node_cap;
+  int* const outc = oct_count + img * g->nlevels + level;
+  uint32_t* const outk = oct_keys + (int64_t)img * g->out_per_image + L.out_base;
+
+  // ---- 1. gather FAST candidates in cell row-major order into keys[0]
+  for (int c0 = 0; c0 < ncell; c0 += kOctCap) {
+    const int n = min(kOctCap, ncell - c0);
+    for (int i = tid; i < n; i += kOctThreads) S.a[i] = cell_count[cbase + c0 + i];
+    __syncthreads();
+    if (tid == 0) S.total = 0;
+    const int tot = block_scan_array(S.a, n, S.wsum);
+    const int base = (c0 == 0) ? 0 : S.ktotal;
+    for (int i = wid; i < n; i += kOctWaves) {
+      const int cnt = cell_count[cbase + c0 + i];
+      const int off = base + S.a[i];
+      const uint32_t* src = cell_keys + (cbase + c0 + i) * g->cell_cap;
+      for (int k = lane; k < cnt; k += 64)
+        if (off + k < L.key_cap) keys[0][off + k] = src[k];
+    }
+    __syncthreads();
+    if (tid == 0) S.ktotal = base + tot;
+    __syncthreads();
+  }
+  int K = S.ktotal;
+  if (K > L.key_cap) {
+    if (tid == 0) atomicOr(err, kErrKeyOverflow);
+    K = L.key_cap;
+  }
+  if (K == 0) {
+    if (tid == 0) *outc = 0;
+    return;
+  }
+  // ---- 2. initial nodes (:484-526): bucket (int)(x / hX), stable, by wave 0
+  const int nIni = L.n_ini;
+  const float hX = L.hx;
+  if (wid == 0) {
+    for (int q0 = 0; q0 < nIni; q0 += 64) {
+      const int qn = min(64, nIni - q0);
+      int cnt = 0;
+      for (int s = 0; s < K; s += 64) {
+        const int i = s + lane;
+        int q = -1;
+        if (i < K) q = (int)((float)key_x(keys[0][i]) / hX) - q0;
+        for (int qq = 0; qq < qn; qq++) {
+          const int pc = __popcll(__ballot(q == qq));
+          if (lane == qq) cnt += pc;
+        }
+      }
+      if (lane < qn) S.a[q0 + lane] = cnt;
+    }
+  }
+  __syncthreads();
+  if (tid == 0) {
+    int run = 0;
+    for (int q = 0; q < nIni; q++) {
+      const int c = S.a[q];
+      S.b[q] = run;
+      run += c;
+    }
+  }
+  __syncthreads();
+  if (wid == 0) {
+    for (int q0 = 0; q0 < nIni; q0 += 64) {
+      const int qn = min(64, nIni - q0);
+      int run = (lane < qn) ? S.b[q0 + lane] : 0;
+      for (int s = 0; s < K; s += 64) {
+        const int i = s + lane;
+        int q = -1;
+        uint32_t k = 0;
+        if (i < K) {
+          k = keys[0][i];
+          q = (int)((float)key_x(k) / hX) - q0;
+        }
+        for (int qq = 0; qq < qn; qq++) {
+          const uint64_t m = __ballot(q == qq);
+          const int r = __shfl(run, qq, 64);
+          if (q == qq) keys[1][r + lanes_below(m)] = k;
+          if (lane == qq) run += __popcll(m);
+        }
+      }
+    }
+  }
+  __syncthreads();
+  if (tid == 0) {
+    int m = 0;
+    for (int i = 0; i < nIni; i++) {
+      const int c = S.a[i];
+      if (c == 0) continue;  // empty initial nodes are erased (:513-526)
+      OctNode nd;
+      nd.x0 = (int16_t)(int)(hX * (float)i);
+      nd.x1 = (int16_t)(int)(hX * (float)(i + 1));
+      nd.y0 = 0;
+      nd.y1 = (int16_t)(L.max_by - kMinBorder);
+      nd.kbeg = S.b[i];
+      nd.n = c;
+      nd.seq = i;
+      nd.buf = 1;
+      lists[0][m++] = nd;
+    }
+    S.m = m;
+    S.seq_next = nIni;
+    S.mode = 0;
+    S.finish = 0;
+    S.nexp = 0;
+  }
+  __syncthreads();
+  int cur = 0;
+  // ---- 3. passes
+  while (true) {
+    const int m = S.m;
+    OctNode* const Lc = lists[cur];
+    OctNode* const Ln = lists[cur ^ 1];
+    if (S.mode == 0) {
+      // outer pass: divide every node with > 1 key, in list order
+      for (int j = wid; j < m; j += kOctWaves) {
+        const OctNode nd = Lc[j];
+        int t = 0, e = 0;
+        if (nd.n > 1) {
+          OctNode ch[4];
+          divide_wave(nd, keys, ch, lane);
+          if (lane == 0)
+            for (int q = 0; q < 4; q++) {
+              child[4 * j + q] = ch[q];
+              t += ch[q].n > 0;
+              e += ch[q].n > 1;
+            }
+        }
+        if (lane == 0) {
+          S.a[j] = t;               // children pushed
+          S.b[j] = (nd.n == 1);     // survives in place
+          S.c[j] = e;               // expandable children
+        }
+      }
+      __syncthreads();
+      const int T = block_scan_array(S.a, m, S.wsum);
+      const int U = block_scan_array(S.b, m, S.wsum);
+      const int E = block_scan_array(S.c, m, S.wsum);
+      const int newm = T + U;
+      const int seq0 = S.seq_next;
+      const bool ovf = newm > min(2 * L.node_cap, kOctCap) || E > kOctCap;
+      if (!ovf) {
+        for (int j = tid; j < m; j += kOctThreads) {
+          const OctNode nd = Lc[j];
+          if (nd.n > 1) {
+            int gpos = S.a[j], epos = S.c[j];
+            for (int q = 0; q < 4; q++) {
+              OctNode ch = child[4 * j + q];
+              if (ch.n == 0) continue;
+              ch.seq = seq0 + gpos;
+              const int pos = T - 1 - gpos;
+              Ln[pos] = ch;
+              if (ch.n > 1) S.sortk[epos++] = (uint64_t)pos;  // vSize in push order
+              gpos++;
+            }
+          } else {
+            Ln[T + S.b[j]] = nd;
+          }
+        }
+      }
+      __syncthreads();
+      if (tid == 0) {
+        if (ovf) {
+          atomicOr(err, kErrNodeOverflow);
+          S.finish = 1;
+        } else {
+          S.m = newm;
+          S.seq_next = seq0 + T;
+          S.nexp = E;
+          if (newm >= N || newm == m) S.finish = 1;
+          else if (newm + E * 3 > N) S.mode = 1;
+        }
+      }
+      if (!ovf) cur ^= 1;
+      __syncthreads();
+      if (S.finish) break;
+    } else {
+      // inner loop iteration: vPrev = S.sortk[0..V) (list positions, push order)
+      const int V = S.nexp;
+      int P2 = 1;
+      while (P2 < V) P2 <<= 1;
+      for (int i = tid; i < P2; i += kOctThreads) {
+        uint64_t key = 0;  // pads sort to the end (descending)
+        if (i < V) {
+          const int pos = (int)S.sortk[i];
+          const OctNode& nd = Lc[pos];
+          key = ((uint64_t)nd.n << 44) | ((uint64_t)(uint32_t)nd.seq << 12) | (uint64_t)pos;
+        }
+        S.sortk[i] = key;
+      }
+      __syncthreads();
+      // bitonic sort, descending by (n, seq): reference processes sort() ascending from the end
+      for (int k = 2; k <= P2; k <<= 1) {
+        for (int jj = k >> 1; jj > 0; jj >>= 1) {
+          for (int i = tid; i < P2; i += kOctThreads) {
+            const int ixj = i ^ jj;
+            if (ixj > i) {
+              const uint64_t x = S.sortk[i], y = S.sortk[ixj];
+              const bool desc = (i & k) == 0;
+              if (desc ? (x < y) : (x > y)) {
+                S.sortk[i] = y;
+                S.sortk[ixj] = x;
+              }
+            }
+          }
+          __syncthreads();
+        }
+      }
+      // speculative division of every vPrev node in processing order
+      for (int j = wid; j < V; j += kOctWaves) {
+        const int pos = (int)(S.sortk[j] & 0xfff);
+        const OctNode nd = Lc[pos];
+        OctNode ch[4];
+        divide_wave(nd, keys, ch, lane);
+        if (lane == 0) {
+          int t = 0, e = 0;
+          for (int q = 0; q < 4; q++) {
+            child[4 * j + q] = ch[q];
+            t += ch[q].n > 0;
+            e += ch[q].n > 1;
+          }
+          S.a[j] = t;
+          S.c[j] = e;
+          S.b[j] = t - 1;
+        }
+      }
+      __syncthreads();
+      // cut: first j with m + sum_{i<=j}(t_i - 1) >= N
+      for (int i = tid; i < V; i += kOctThreads) S.b[i] = S.a[i] - 1;
+      __syncthreads();
+      block_scan_array(S.b, V, S.wsum);  // exclusive prefix of (t - 1)
+      if (tid == 0) S.total = V - 1;
+      __syncthreads();
+      for (int j = tid; j < V; j += kOctThreads)
+        if (m + S.b[j] + (S.a[j] - 1) >= N) atomicMin(&S.total, j);
+      __syncthreads();
+      const int J = S.total;  // last processed index
+      const int nproc = J + 1;
+      for (int i = tid; i < V; i += kOctThreads)
+        if (i >= nproc) {
+          S.a[i] = 0;
+          S.c[i] = 0;
+        }
+      __syncthreads();
+      const int T = block_scan_array(S.a, V, S.wsum);  // push-order child positions
+      const int E = block_scan_array(S.c, V, S.wsum);
+      // survivors: old list minus processed nodes
+      for (int i = tid; i < m; i += kOctThreads) S.b[i] = 1;
+      __syncthreads();
+      for (int j = tid; j < nproc; j += kOctThreads) S.b[(int)(S.sortk[j] & 0xfff)] = 0;
+      __syncthreads();
+      const int U = block_scan_array(S.b, m, S.wsum);
+      // block_scan_array overwrote the flags with prefixes; recover flags from processed set
+      const int newm = T + U;
+      const int seq0 = S.seq_next;
+      const bool ovf = newm > min(2 * L.node_cap, kOctCap) || E > kOctCap;
+      __shared__ uint8_t processed[kOctCap];
+      for (int i = tid; i < m; i += kOctThreads) processed[i] = 0;
+      __syncthreads();
+      for (int j = tid; j < nproc; j += kOctThreads) processed[(int)(S.sortk[j] & 0xfff)] = 1;
+      __syncthreads();
+      // new vSize goes to a temporary (S.c keeps E prefixes): reuse child area tail? keep in LDS
+      __shared__ int vnext[kOctCap];
+      if (!ovf) {
+        for (int j = tid; j < nproc; j += kOctThreads) {
+          int gpos = S.a[j], epos = S.c[j];
+          for (int q = 0; q < 4; q++) {
+            OctNode ch = child[4 * j + q];
+            if (ch.n == 0) continue;
+            ch.seq = seq0 + gpos;
+            const int pos = T - 1 - gpos;
+            Ln[pos] = ch;
+            if (ch.n > 1) vnext[epos++] = pos;
+            gpos++;
+          }
+        }
+        for (int i = tid; i < m; i += kOctThreads)
+          if (!processed[i]) Ln[T + S.b[i]] = Lc[i];
+      }
+      __syncthreads();
+      for (int i = tid; i < E; i += kOctThreads) S.sortk[i] = (uint64_t)vnext[i];
+      __syncthreads();
+      if (tid == 0) {
+        if (ovf) {
+          atomicOr(err, kErrNodeOverflow);
+          S.finish = 1;
+        } else {
+          S.m = newm;
+          S.seq_next = seq0 + T;
+          S.nexp = E;
+          if (newm >= N || newm == m) S.finish = 1;
+        }
+      }
+      if (!ovf) cur ^= 1;
+      __syncthreads();
+      if (S.finish) break;
+    }
+  }
+  // ---- 4. retain the best key of each node (:682-701): strict '>' keeps the first maximum
+  const int m = S.m;
+  const OctNode* Lf = lists[cur];
+  const int mout = min(m, L.out_cap);
+  for (int j = tid; j < mout; j += kOctThreads) {
+    const OctNode nd = Lf[j];
+    const uint32_t* ks = keys[nd.buf] + nd.kbeg;
+    uint32_t best = ks[0];
+    for (int k = 1; k < nd.n; k++) {
+      const uint32_t kk = ks[k];
+      if (key_score(kk) > key_score(best)) best = kk;
+    }
+    outk[j] = best;
+  }
+  if (tid == 0) {
+    if (m > L.out_cap) atomicOr(err, kErrNodeOverflow);
+    *outc = mout;
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// orient_desc: computeOrientation/IC_Angle (:413-420, :18-45) on the unblurred level, then
+// computeOrbDescriptor (:49-88) on the blurred level, one wave per keypoint. Output order is
+// ORBextractor::Compute's: levels 0..L-1 concatenated, each in octree list order (:1020-1048).
+// Descriptor sample offsets use the Release-build FMA association (g++ -O3 -march=native):
+// row = cvRound(fma(px, b, py*a)), col = cvRound(fma(px, a, -(py*b))).
+__global__ __launch_bounds__(256) void orient_desc_kernel(
+    ImageBatch b, const OrbGeom* __restrict__ g, const int2* __restrict__ disc,
+    const uint32_t* __restrict__ oct_keys, const int* __restrict__ oct_count,
+    KeyPoint* __restrict__ kps, uint8_t* __restrict__ desc, int* __restrict__ nkps) {
+  const int img = blockIdx.y;
+  const int lane = threadIdx.x & 63;
+  const int w = blockIdx.x * 4 + (threadIdx.x >> 6);
+  int level = -1, idx = 0, off = 0, total = 0;
+  for (int l = 0; l < g->nlevels; l++) {
+    const int c = oct_count[img * g->nlevels + l];
+    if (level < 0 && w < total + c) {
+      level = l;
+      idx = w - total;
+      off = total;
+    }
+    total += c;
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0) nkps[img] = total;
+  if (level < 0) return;
+  (void)off;
+  const LevelGeom& L = g->lv[level];
+  const uint32_t key = oct_keys[(int64_t)img * g->out_per_image + L.out_base + idx];
+  const int x = key_x(key) + kMinBorder, y = key_y(key) + kMinBorder;
+  int pitch;
+  const uint8_t* im = level_ptr(b, g, img, level, &pitch);
+  const uint8_t* center = im + (int64_t)y * pitch + x;
+  int m10 = 0, m01 = 0;
+  for (int i = lane; i < kDiscPixels; i += 64) {
+    const int2 uv = disc[i];
+    const int v = center[uv.y * pitch + uv.x];
+    m10 += uv.x * v;
+    m01 += uv.y * v;
+  }
+  m10 = wave_sum(m10);
+  m01 = wave_sum(m01);
+  const float angle = cv_fast_atan2((float)m01, (float)m10);
+  const float factorPI = (float)(3.14159265358979323846 / 180.0);
+  float sa, ca;
+  glibc_sincosf(angle * factorPI, &sa, &ca);
+  const float a = ca, bb = sa;
+  const uint8_t* bl = b.blur + (int64_t)img * g->blur_bytes + L.blur_offset;
+  const int bp = L.pitch;
+  const uint8_t* bc = bl + (int64_t)y * bp + x;
+  uint64_t words[4];
+#pragma unroll
+  for (int r = 0; r < 4; r++) {
+    const int t = r * 64 + lane;
+    const float px0 = (float)c_pattern[4 * t], py0 = (float)c_pattern[4 * t + 1];
+    const float px1 = (float)c_pattern[4 * t + 2], py1 = (float)c_pattern[4 * t + 3];
+    const int ry0 = cv_round(fmaf(px0, bb, py0 * a));
+    const int rx0 = cv_round(fmaf(px0, a, -(py0 * bb)));
+    const int ry1 = cv_round(fmaf(px1, bb, py1 * a));
+    const int rx1 = cv_round(fmaf(px1, a, -(py1 * bb)));
+    const int v0 = bc[ry0 * bp + rx0];
+    const int v1 = bc[ry1 * bp + rx1];
+    words[r] = __ballot(v0 < v1);
+  }
+  const int64_t o = (int64_t)img * g->kp_cap + off + idx;
+  if (lane < 4) {
+    uint64_t wv = words[0];
+    if (lane == 1) wv = words[1];
+    if (lane == 2) wv = words[2];
+    if (lane == 3) wv = words[3];
+    reinterpret_cast<uint64_t*>(desc + o * 32)[lane] = wv;
+  }
+  if (lane == 0) {
+    KeyPoint kp;
+    kp.x = (float)x;
+    kp.y = (float)y;
+    if (level != 0) {
+      kp.x *= L.scale;
+      kp.y *= L.scale;
+    }
+    kp.size = L.patch_size;
+    kp.angle = angle;
+    kp.response = (float)key_score(key);
+    kp.octave = level;
+    kp.class_id = -1;
+    kps[o] = kp;
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// Host-side launchers.
+void launch_extract(const ImageBatch& b, const OrbGeomDev& gd, int n_images, hipStream_t st) {
+  const OrbGeom& g = *gd.host;
+  for (int l = 1; l < g.nlevels; l++) {
+    const int w = g.lv[l].w, h = g.lv[l].h;
+    dim3 grid((w + 1023) / 1024, h, n_images);
+    hipLaunchKernelGGL(pyr_down_kernel, grid, dim3(256), 0, st, b, gd.dev, l, gd.rx, gd.ry);
+  }
+  hipLaunchKernelGGL(blur7_kernel, dim3(g.blur_tiles, n_images), dim3(256), 0, st, b, gd.dev);
+  hipLaunchKernelGGL(fast_cells_kernel,
+                     dim3((g.cells_per_image + kCellWaves - 1) / kCellWaves, n_images),
+                     dim3(64 * kCellWaves), 0, st, b, gd.dev, gd.ws.cell_keys,
+                     gd.ws.cell_count, gd.ws.err);
+  hipLaunchKernelGGL(octree_kernel, dim3(g.nlevels, n_images), dim3(kOctThreads), 0, st, gd.dev,
+                     gd.ws.cell_keys, gd.ws.cell_count, gd.ws.key_scratch, gd.ws.node_scratch,
+                     gd.ws.oct_keys, gd.ws.oct_count, gd.ws.err);
+  hipLaunchKernelGGL(orient_desc_kernel, dim3((g.kp_cap + 3) / 4, n_images), dim3(256), 0, st,
+                     b, gd.dev, gd.disc, gd.ws.oct_keys, gd.ws.oct_count, gd.out.kps,
+                     gd.out.desc, gd.out.nkps);
+}
+
+}  // namespace slamgpu

@@ -1,0 +1,567 @@
+// runtime.cpp -- host runtime behind the C ABI (include/slamgpu.h).
+//
+// One slamgpu_ctx = one device + stream + every workspace the batched kernels need, sized at
+// creation for max_frames stereo pairs so that the *_device calls never allocate (they can be
+// captured into a HIP graph). The host-buffer calls are thin wrappers that stage through the
+// context's own device buffers and synchronise, mirroring the reference call sites:
+// ORBextractor::Compute (orb_extractor.cpp:985), the stereo Frame ctor (frame.cpp:61-111) and
+// OrbMatcher::SearchByProjection (orb_matcher.cpp:13, :1312).
+#include <hip/hip_runtime.h>
+
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/slamgpu.h"
+#include "match_kernels.h"
+#include "orb_kernels.h"
+#include "orb_tables.h"
+
+using namespace slamgpu;
+
+struct slamgpu_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  OrbParams params{};
+  OrbTables tables{};
+  OrbGeom geom{};
+  int max_frames = 0, max_images = 0;
+  std::string err;
+  // device geometry
+  OrbGeom* d_geom = nullptr;
+  ResizeX* d_rx = nullptr;
+  ResizeY* d_ry = nullptr;
+  int2* d_disc = nullptr;
+  // images staged by the host-buffer calls (left at d_in, right at d_in + in_stride)
+  uint8_t* d_in = nullptr;
+  int in_pitch = 0;
+  int64_t in_stride = 0;
+  // batch state
+  ImageBatch batch{};
+  int n_frames_last = 0, n_images_last = 0;
+  Camera cam{};
+  bool have_cam = false;
+  // extractor buffers
+  uint8_t* d_pyr = nullptr;
+  uint8_t* d_blur = nullptr;
+  ExtractWorkspace ws{};
+  ExtractOutput out{};
+  // stereo
+  StereoWorkspace sws{};
+  StereoOut sout{};
+  // grid + matchers
+  GridWorkspace gws{};
+  MatchWorkspace mws{};
+  int mw_cap = 0;
+  int* d_qmeta = nullptr;  // [2][max_frames] q_start / q_count for host calls
+  int* d_nm = nullptr;
+  void* d_qbuf = nullptr;
+  size_t qbuf_bytes = 0;
+  int32_t* d_mp = nullptr;
+  uint8_t* d_blk = nullptr;
+  std::vector<void*> allocs;
+  OrbGeomDev gd() const {
+    OrbGeomDev g;
+    g.host = &geom;
+    g.dev = d_geom;
+    g.rx = d_rx;
+    g.ry = d_ry;
+    g.disc = d_disc;
+    g.ws = ws;
+    g.out = out;
+    return g;
+  }
+};
+
+static int fail(slamgpu_ctx* c, int code, const char* fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof(buf), fmt, ap);
+  va_end(ap);
+  if (c) c->err = buf;
+  return code;
+}
+
+#define HIPCHECK(c, x)                                                                 \
+  do {                                                                                 \
+    hipError_t e_ = (x);                                                               \
+    if (e_ != hipSuccess)                                                              \
+      return fail(c, SLAMGPU_EHIP, "%s failed: %s", #x, hipGetErrorString(e_));        \
+  } while (0)
+
+template <typename T>
+static int dalloc(slamgpu_ctx* c, T** p, size_t count) {
+  void* q = nullptr;
+  const size_t bytes = count * sizeof(T) + 256;
+  hipError_t e = hipMalloc(&q, bytes);
+  if (e != hipSuccess)
+    return fail(c, SLAMGPU_EHIP, "hipMalloc(%zu) failed: %s", bytes, hipGetErrorString(e));
+  c->allocs.push_back(q);
+  *p = static_cast<T*>(q);
+  return 0;
+}
+
+static int hcheck(slamgpu_ctx* c, hipError_t e) {
+  return e == hipSuccess ? 0 : fail(c, SLAMGPU_EHIP, "HIP error: %s", hipGetErrorString(e));
+}
+
+static hipStream_t pick_stream(slamgpu_ctx* c, void* s) {
+  return s ? static_cast<hipStream_t>(s) : c->stream;
+}
+
+static void set_camera(slamgpu_ctx* c, const slamgpu_camera* cam) {
+  Camera k;
+  k.fx = cam->fx;
+  k.fy = cam->fy;
+  k.cx = cam->cx;
+  k.cy = cam->cy;
+  k.bf = cam->bf;
+  // Frame::ComputeImageBounds (k1 == 0) and MakeInitialComputations (frame.cpp:197-209)
+  k.min_x = 0.0f;
+  k.max_x = (float)c->geom.cols;
+  k.min_y = 0.0f;
+  k.max_y = (float)c->geom.rows;
+  k.cell_w = (float)(k.max_x - k.min_x) / (kGridCols);
+  k.cell_h = (float)(k.max_y - k.min_y) / (kGridRows);
+  c->cam = k;
+  c->have_cam = true;
+}
+
+static int check_device_err(slamgpu_ctx* c) {
+  uint32_t e = 0;
+  HIPCHECK(c, hipMemcpy(&e, c->ws.err, sizeof(e), hipMemcpyDeviceToHost));
+  if (e) {
+    (void)hipMemset(c->ws.err, 0, sizeof(uint32_t));
+    return fail(c, SLAMGPU_EDEVICE, "device capacity overflow (bits 0x%x)", e);
+  }
+  return 0;
+}
+
+extern "C" {
+
+int slamgpu_create(int device, const slamgpu_orb_params* p, int cols, int rows, int max_frames,
+                   slamgpu_ctx** out) {
+  if (!p || !out || max_frames < 1) return SLAMGPU_EINVAL;
+  *out = nullptr;
+  slamgpu_ctx* c = new slamgpu_ctx();
+  c->params = OrbParams{p->nfeatures, p->scale_factor, p->nlevels,
+                        std::min(std::max(p->ini_th_fast, 0), 255),
+                        std::min(std::max(p->min_th_fast, 0), 255)};
+  std::vector<ResizeX> rx;
+  std::vector<ResizeY> ry;
+  if (compute_geometry(c->params, cols, rows, &c->geom, &rx, &ry) != 0) {
+    delete c;
+    return SLAMGPU_EINVAL;
+  }
+  compute_tables(c->params, &c->tables);
+  for (int l = 0; l < c->geom.nlevels; l++)
+    if (c->geom.lv[l].node_cap > 1024) {
+      delete c;
+      return SLAMGPU_EINVAL;  // octree LDS arrays hold <= 2048 list nodes
+    }
+  c->device = device;
+  c->max_frames = max_frames;
+  c->max_images = 2 * max_frames;
+  int rc = 0;
+#define TRY(x)             \
+  do {                     \
+    if ((rc = (x)) != 0) { \
+      *out = c;            \
+      return rc;           \
+    }                      \
+  } while (0)
+  TRY(hipSetDevice(device) == hipSuccess ? 0 : fail(c, SLAMGPU_EHIP, "hipSetDevice"));
+  TRY(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) == hipSuccess
+          ? 0
+          : fail(c, SLAMGPU_EHIP, "hipStreamCreate"));
+  const OrbGeom& g = c->geom;
+  const int n = c->max_images;
+  TRY(dalloc(c, &c->d_geom, 1));
+  TRY(dalloc(c, &c->d_rx, rx.size() + 1));
+  TRY(dalloc(c, &c->d_ry, ry.size() + 1));
+  TRY(dalloc(c, &c->d_disc, kDiscPixels));
+  TRY(hcheck(c, hipMemcpy(c->d_geom, &g, sizeof(OrbGeom), hipMemcpyHostToDevice)));
+  TRY(hcheck(c, hipMemcpy(c->d_rx, rx.data(), rx.size() * sizeof(ResizeX), hipMemcpyHostToDevice)));
+  TRY(hcheck(c, hipMemcpy(c->d_ry, ry.data(), ry.size() * sizeof(ResizeY), hipMemcpyHostToDevice)));
+  // IC_Angle circular patch (orb_extractor.cpp:18-45): rows |v| <= 15, |u| <= umax[|v|]
+  std::vector<int2> disc;
+  for (int v = -kHalfPatch; v <= kHalfPatch; v++) {
+    const int d = g.umax[v < 0 ? -v : v];
+    for (int u = -d; u <= d; u++) disc.push_back(make_int2(u, v));
+  }
+  if ((int)disc.size() != kDiscPixels) {
+    *out = c;
+    return fail(c, SLAMGPU_EINVAL, "IC_Angle patch has %zu pixels", disc.size());
+  }
+  TRY(hcheck(c, hipMemcpy(c->d_disc, disc.data(), disc.size() * sizeof(int2), hipMemcpyHostToDevice)));
+  c->in_pitch = (cols + 63) / 64 * 64;
+  c->in_stride = (int64_t)c->in_pitch * rows;
+  TRY(dalloc(c, &c->d_in, 2 * (size_t)c->in_stride));
+  TRY(dalloc(c, &c->d_pyr, (size_t)n * g.pyr_bytes));
+  TRY(dalloc(c, &c->d_blur, (size_t)n * g.blur_bytes));
+  TRY(dalloc(c, &c->ws.cell_keys, (size_t)n * g.cells_per_image * g.cell_cap));
+  TRY(dalloc(c, &c->ws.cell_count, (size_t)n * g.cells_per_image));
+  TRY(dalloc(c, &c->ws.key_scratch, (size_t)n * g.keys_per_image));
+  TRY(dalloc(c, &c->ws.node_scratch, (size_t)n * g.nodes_per_image));
+  TRY(dalloc(c, &c->ws.oct_keys, (size_t)n * g.out_per_image));
+  TRY(dalloc(c, &c->ws.oct_count, (size_t)n * g.nlevels));
+  TRY(dalloc(c, &c->ws.err, 4));
+  TRY(hcheck(c, hipMemset(c->ws.err, 0, sizeof(uint32_t))));
+  TRY(dalloc(c, &c->out.kps, (size_t)n * g.kp_cap));
+  TRY(dalloc(c, &c->out.desc, (size_t)n * g.kp_cap * 32));
+  TRY(dalloc(c, &c->out.nkps, (size_t)n));
+  TRY(hcheck(c, hipMemset(c->out.nkps, 0, sizeof(int) * n)));
+  const int rows0 = g.lv[0].h;
+  c->sws.row_cap = g.kp_cap * 24;
+  TRY(dalloc(c, &c->sws.row_start, (size_t)max_frames * (rows0 + 1)));
+  TRY(dalloc(c, &c->sws.row_items, (size_t)max_frames * c->sws.row_cap));
+  TRY(dalloc(c, &c->sws.sad, (size_t)max_frames * g.kp_cap));
+  TRY(dalloc(c, &c->sout.u_right, (size_t)max_frames * g.kp_cap));
+  TRY(dalloc(c, &c->sout.depth, (size_t)max_frames * g.kp_cap));
+  TRY(dalloc(c, &c->gws.cell_start, (size_t)max_frames * (kGridCells + 1)));
+  TRY(dalloc(c, &c->gws.cell_items, (size_t)max_frames * g.kp_cap));
+  TRY(dalloc(c, &c->gws.cell_fill, (size_t)max_frames * kGridCells));
+  TRY(dalloc(c, &c->d_qmeta, 2 * (size_t)max_frames));
+  TRY(dalloc(c, &c->d_nm, (size_t)max_frames));
+  TRY(dalloc(c, &c->d_mp, (size_t)g.kp_cap));
+  TRY(dalloc(c, &c->d_blk, (size_t)g.kp_cap));
+#undef TRY
+  *out = c;
+  return 0;
+}
+
+void slamgpu_destroy(slamgpu_ctx* c) {
+  if (!c) return;
+  (void)hipSetDevice(c->device);
+  if (c->stream) (void)hipStreamSynchronize(c->stream);
+  for (void* p : c->allocs) (void)hipFree(p);
+  if (c->stream) (void)hipStreamDestroy(c->stream);
+  delete c;
+}
+
+const char* slamgpu_last_error(const slamgpu_ctx* c) { return c ? c->err.c_str() : "null ctx"; }
+
+int slamgpu_kp_capacity(const slamgpu_ctx* c) { return c ? c->geom.kp_cap : 0; }
+
+int slamgpu_scale_tables(const slamgpu_ctx* c, float* scale, float* inv_scale, float* sigma2,
+                         float* inv_sigma2, int* fpl) {
+  if (!c) return SLAMGPU_EINVAL;
+  for (int l = 0; l < c->tables.nlevels; l++) {
+    if (scale) scale[l] = c->tables.scale[l];
+    if (inv_scale) inv_scale[l] = c->tables.inv_scale[l];
+    if (sigma2) sigma2[l] = c->tables.sigma2[l];
+    if (inv_sigma2) inv_sigma2[l] = c->tables.inv_sigma2[l];
+    if (fpl) fpl[l] = c->tables.features_per_level[l];
+  }
+  return 0;
+}
+
+static int run_frontend(slamgpu_ctx* c, const ImageBatch& b, int n_frames, int n_images,
+                        bool stereo, hipStream_t st) {
+  c->batch = b;
+  c->n_frames_last = n_frames;
+  c->n_images_last = n_images;
+  OrbGeomDev g = c->gd();
+  launch_extract(b, g, n_images, st);
+  if (stereo) {
+    launch_stereo(b, g, c->cam, n_frames, c->sws, c->sout, st);
+    FrameKps cur{c->out.kps, c->out.desc, c->out.nkps, 2 * (int64_t)c->geom.kp_cap, 2};
+    launch_grid(cur, c->cam, n_frames, c->geom.kp_cap, c->gws, st);
+  }
+  HIPCHECK(c, hipGetLastError());
+  return 0;
+}
+
+int slamgpu_extract(slamgpu_ctx* c, const uint8_t* img, size_t step, slamgpu_keypoint* kps,
+                    uint8_t* desc, int cap, int* n_out) {
+  if (!c || !img) return SLAMGPU_EINVAL;
+  HIPCHECK(c, hipSetDevice(c->device));
+  HIPCHECK(c, hipMemcpy2DAsync(c->d_in, c->in_pitch, img, step, c->geom.cols, c->geom.rows,
+                               hipMemcpyHostToDevice, c->stream));
+  ImageBatch b{c->d_in, c->d_in + c->in_stride, 2 * c->in_stride, c->in_pitch, c->d_pyr,
+               c->d_blur};
+  int rc = run_frontend(c, b, 1, 1, false, c->stream);
+  if (rc) return rc;
+  HIPCHECK(c, hipStreamSynchronize(c->stream));
+  if ((rc = check_device_err(c))) return rc;
+  return slamgpu_download_keypoints(c, 0, kps, desc, cap, n_out);
+}
+
+int slamgpu_get_pyramid_level(slamgpu_ctx* c, int img, int level, uint8_t* dst, size_t dst_step,
+                              int* w_out, int* h_out) {
+  if (!c || img < 0 || img >= c->n_images_last || level < 0 || level >= c->geom.nlevels)
+    return SLAMGPU_EINVAL;
+  const LevelGeom& L = c->geom.lv[level];
+  if (w_out) *w_out = L.w;
+  if (h_out) *h_out = L.h;
+  if (!dst) return 0;
+  const uint8_t* src;
+  size_t pitch;
+  if (level == 0) {
+    src = ((img & 1) ? c->batch.in_r : c->batch.in_l) + (int64_t)(img >> 1) * c->batch.in_stride;
+    pitch = c->batch.in_pitch;
+  } else {
+    src = c->d_pyr + (int64_t)img * c->geom.pyr_bytes + L.offset;
+    pitch = L.pitch;
+  }
+  HIPCHECK(c, hipStreamSynchronize(c->stream));
+  HIPCHECK(c, hipMemcpy2D(dst, dst_step, src, pitch, L.w, L.h, hipMemcpyDeviceToHost));
+  return 0;
+}
+
+int slamgpu_debug_level_keys(slamgpu_ctx* c, int img, int level, int stage, uint32_t* keys,
+                             int cap, int* n_out) {
+  if (!c || img < 0 || img >= c->n_images_last || level < 0 || level >= c->geom.nlevels)
+    return SLAMGPU_EINVAL;
+  HIPCHECK(c, hipStreamSynchronize(c->stream));
+  const OrbGeom& g = c->geom;
+  const LevelGeom& L = g.lv[level];
+  std::vector<uint32_t> out;
+  if (stage == 0) {
+    const int ncell = L.ncols * L.nrows;
+    std::vector<int> cnt(ncell);
+    const int64_t cb = (int64_t)img * g.cells_per_image + L.cell_base;
+    HIPCHECK(c, hipMemcpy(cnt.data(), c->ws.cell_count + cb, sizeof(int) * ncell,
+                          hipMemcpyDeviceToHost));
+    std::vector<uint32_t> cell(g.cell_cap);
+    for (int i = 0; i < ncell; i++) {
+      if (!cnt[i]) continue;
+      HIPCHECK(c, hipMemcpy(cell.data(), c->ws.cell_keys + (cb + i) * g.cell_cap,
+                            sizeof(uint32_t) * cnt[i], hipMemcpyDeviceToHost));
+      out.insert(out.end(), cell.begin(), cell.begin() + cnt[i]);
+    }
+  } else {
+    int n = 0;
+    HIPCHECK(c, hipMemcpy(&n, c->ws.oct_count + img * g.nlevels + level, sizeof(int),
+                          hipMemcpyDeviceToHost));
+    out.resize(n);
+    if (n)
+      HIPCHECK(c, hipMemcpy(out.data(), c->ws.oct_keys + (int64_t)img * g.out_per_image + L.out_base,
+                            sizeof(uint32_t) * n, hipMemcpyDeviceToHost));
+  }
+  if (n_out) *n_out = (int)out.size();
+  if ((int)out.size() > cap) return fail(c, SLAMGPU_ECAP, "need %zu keys", out.size());
+  if (keys && !out.empty()) std::memcpy(keys, out.data(), out.size() * sizeof(uint32_t));
+  return 0;
+}
+
+int slamgpu_frame_stereo(slamgpu_ctx* c, const uint8_t* left, const uint8_t* right, size_t step,
+                         const slamgpu_camera* cam) {
+  if (!c || !left || !right || !cam) return SLAMGPU_EINVAL;
+  HIPCHECK(c, hipSetDevice(c->device));
+  set_camera(c, cam);
+  HIPCHECK(c, hipMemcpy2DAsync(c->d_in, c->in_pitch, left, step, c->geom.cols, c->geom.rows,
+                               hipMemcpyHostToDevice, c->stream));
+  HIPCHECK(c, hipMemcpy2DAsync(c->d_in + c->in_stride, c->in_pitch, right, step, c->geom.cols,
+                               c->geom.rows, hipMemcpyHostToDevice, c->stream));
+  ImageBatch b{c->d_in, c->d_in + c->in_stride, 2 * c->in_stride, c->in_pitch, c->d_pyr,
+               c->d_blur};
+  int rc = run_frontend(c, b, 1, 2, true, c->stream);
+  if (rc) return rc;
+  return slamgpu_sync(c, nullptr);
+}
+
+int slamgpu_frontend_device(slamgpu_ctx* c, const uint8_t* d_left, const uint8_t* d_right,
+                            size_t frame_stride, size_t pitch, int n_frames,
+                            const slamgpu_camera* cam, void* stream) {
+  if (!c || !d_left || !d_right || !cam || n_frames < 1 || n_frames > c->max_frames ||
+      pitch < (size_t)c->geom.cols)
+    return fail(c, SLAMGPU_EINVAL, "slamgpu_frontend_device: bad arguments");
+  set_camera(c, cam);
+  ImageBatch b{d_left, d_right, (int64_t)frame_stride, (int)pitch, c->d_pyr, c->d_blur};
+  return run_frontend(c, b, n_frames, 2 * n_frames, true, pick_stream(c, stream));
+}
+
+int slamgpu_sync(slamgpu_ctx* c, void* stream) {
+  if (!c) return SLAMGPU_EINVAL;
+  HIPCHECK(c, hipStreamSynchronize(pick_stream(c, stream)));
+  return check_device_err(c);
+}
+
+int slamgpu_download_keypoints(slamgpu_ctx* c, int img, slamgpu_keypoint* kps, uint8_t* desc,
+                               int cap, int* n_out) {
+  if (!c || img < 0 || img >= c->n_images_last) return SLAMGPU_EINVAL;
+  int n = 0;
+  HIPCHECK(c, hipStreamSynchronize(c->stream));
+  HIPCHECK(c, hipMemcpy(&n, c->out.nkps + img, sizeof(int), hipMemcpyDeviceToHost));
+  if (n_out) *n_out = n;
+  if (n > cap) return fail(c, SLAMGPU_ECAP, "need %d keypoints, cap %d", n, cap);
+  const int64_t o = (int64_t)img * c->geom.kp_cap;
+  if (kps && n)
+    HIPCHECK(c, hipMemcpy(kps, c->out.kps + o, sizeof(KeyPoint) * n, hipMemcpyDeviceToHost));
+  if (desc && n)
+    HIPCHECK(c, hipMemcpy(desc, c->out.desc + o * 32, 32 * (size_t)n, hipMemcpyDeviceToHost));
+  return 0;
+}
+
+int slamgpu_download_stereo(slamgpu_ctx* c, int frame, float* u_right, float* depth, int cap,
+                            int* n_out) {
+  if (!c || frame < 0 || frame >= c->n_frames_last) return SLAMGPU_EINVAL;
+  int n = 0;
+  HIPCHECK(c, hipStreamSynchronize(c->stream));
+  HIPCHECK(c, hipMemcpy(&n, c->out.nkps + 2 * frame, sizeof(int), hipMemcpyDeviceToHost));
+  if (n_out) *n_out = n;
+  if (n > cap) return fail(c, SLAMGPU_ECAP, "need %d entries, cap %d", n, cap);
+  const int64_t o = (int64_t)frame * c->geom.kp_cap;
+  if (u_right && n)
+    HIPCHECK(c, hipMemcpy(u_right, c->sout.u_right + o, 4 * (size_t)n, hipMemcpyDeviceToHost));
+  if (depth && n)
+    HIPCHECK(c, hipMemcpy(depth, c->sout.depth + o, 4 * (size_t)n, hipMemcpyDeviceToHost));
+  return 0;
+}
+
+int slamgpu_device_results(const slamgpu_ctx* c, slamgpu_device_view* v) {
+  if (!c || !v) return SLAMGPU_EINVAL;
+  v->kps = reinterpret_cast<const slamgpu_keypoint*>(c->out.kps);
+  v->desc = c->out.desc;
+  v->nkps = c->out.nkps;
+  v->u_right = c->sout.u_right;
+  v->depth = c->sout.depth;
+  v->kp_cap = c->geom.kp_cap;
+  return 0;
+}
+
+int slamgpu_descriptor_distance(const uint8_t* a, const uint8_t* b) {
+  int dist = 0;
+  for (int i = 0; i < 32; i++) dist += __builtin_popcount((unsigned)(a[i] ^ b[i]));
+  return dist;
+}
+
+// ---- matchers ------------------------------------------------------------------------------
+static int ensure_match_ws(slamgpu_ctx* c, int total_queries) {
+  if (total_queries <= c->mw_cap) return 0;
+  int cap = std::max(total_queries, 4096);
+  int rc;
+  if ((rc = dalloc(c, &c->mws.topk, (size_t)cap * kTopK))) return rc;
+  if ((rc = dalloc(c, &c->mws.ncand, (size_t)cap))) return rc;
+  if ((rc = dalloc(c, &c->mws.rot_bin, (size_t)cap))) return rc;
+  if ((rc = dalloc(c, &c->mws.best_idx, (size_t)cap))) return rc;
+  c->mw_cap = cap;
+  return 0;
+}
+
+static FrameKps left_views(const slamgpu_ctx* c) {
+  return FrameKps{c->out.kps, c->out.desc, c->out.nkps, 2 * (int64_t)c->geom.kp_cap, 2};
+}
+
+int slamgpu_search_by_projection_frame_device(slamgpu_ctx* c, const slamgpu_f2f_query* d_q,
+                                              int total_queries, const int* d_q_start,
+                                              const int* d_q_count, int max_queries,
+                                              const slamgpu_f2f_pose* d_poses,
+                                              int32_t* d_map_point, uint8_t* d_blocked,
+                                              int64_t mp_stride, int* d_nmatches, int n_frames,
+                                              void* stream) {
+  if (!c || !c->have_cam || n_frames < 1 || n_frames > c->n_frames_last ||
+      mp_stride < c->geom.kp_cap)
+    return fail(c, SLAMGPU_EINVAL, "search_by_projection_frame_device: bad arguments");
+  int rc = ensure_match_ws(c, total_queries);
+  if (rc) return rc;
+  MatchIO io{d_q_start, d_q_count, d_map_point, d_blocked, d_nmatches, mp_stride};
+  launch_search_frame(left_views(c), c->sout.u_right, c->geom.kp_cap, c->cam, c->gd(),
+                      reinterpret_cast<const F2FQuery*>(d_q),
+                      reinterpret_cast<const F2FPose*>(d_poses), n_frames, max_queries, c->gws,
+                      c->mws, io, pick_stream(c, stream));
+  HIPCHECK(c, hipGetLastError());
+  return 0;
+}
+
+int slamgpu_search_by_projection_mps_device(slamgpu_ctx* c, const slamgpu_mps_query* d_q,
+                                            int total_queries, const int* d_q_start,
+                                            const int* d_q_count, int max_queries, float nnratio,
+                                            int th, int32_t* d_map_point, uint8_t* d_blocked,
+                                            int64_t mp_stride, int* d_nmatches, int n_frames,
+                                            void* stream) {
+  if (!c || !c->have_cam || n_frames < 1 || n_frames > c->n_frames_last ||
+      mp_stride < c->geom.kp_cap)
+    return fail(c, SLAMGPU_EINVAL, "search_by_projection_mps_device: bad arguments");
+  int rc = ensure_match_ws(c, total_queries);
+  if (rc) return rc;
+  MatchIO io{d_q_start, d_q_count, d_map_point, d_blocked, d_nmatches, mp_stride};
+  launch_search_mps(left_views(c), c->sout.u_right, c->geom.kp_cap, c->cam, c->gd(),
+                    reinterpret_cast<const MpsQuery*>(d_q), nnratio, th, n_frames, max_queries,
+                    c->gws, c->mws, io, pick_stream(c, stream));
+  HIPCHECK(c, hipGetLastError());
+  return 0;
+}
+
+}  // extern "C"
+
+// Host-buffer matcher calls on one frame of the last frontend/frame call.
+template <typename QT>
+static int host_search(slamgpu_ctx* c, int frame, const QT* queries, int nq, int32_t* map_point,
+                       uint8_t* blocked, int n, int* nmatches, size_t extra_bytes,
+                       const void* extra, bool f2f, float nnratio, int th) {
+  if (!c || frame < 0 || frame >= c->n_frames_last || nq < 0 || !map_point || !blocked)
+    return SLAMGPU_EINVAL;
+  if (n > c->geom.kp_cap) return fail(c, SLAMGPU_EINVAL, "n > kp capacity");
+  const size_t need = sizeof(QT) * (size_t)std::max(nq, 1) + extra_bytes + 256;
+  if (need > c->qbuf_bytes) {
+    int rc = dalloc(c, reinterpret_cast<uint8_t**>(&c->d_qbuf), need);
+    if (rc) return rc;
+    c->qbuf_bytes = need;
+  }
+  int rc = ensure_match_ws(c, nq);
+  if (rc) return rc;
+  hipStream_t st = c->stream;
+  uint8_t* qb = static_cast<uint8_t*>(c->d_qbuf);
+  if (nq) HIPCHECK(c, hipMemcpyAsync(qb, queries, sizeof(QT) * nq, hipMemcpyHostToDevice, st));
+  uint8_t* eb = qb + (sizeof(QT) * (size_t)std::max(nq, 1) + 255) / 256 * 256;
+  if (extra_bytes)
+    HIPCHECK(c, hipMemcpyAsync(eb, extra, extra_bytes, hipMemcpyHostToDevice, st));
+  // frame `frame` only: use a one-frame view shifted to that frame
+  int meta[2] = {0, nq};
+  HIPCHECK(c, hipMemcpyAsync(c->d_qmeta, meta, sizeof(meta), hipMemcpyHostToDevice, st));
+  HIPCHECK(c, hipMemsetAsync(c->d_mp, 0xff, sizeof(int32_t) * c->geom.kp_cap, st));
+  HIPCHECK(c, hipMemsetAsync(c->d_blk, 0, c->geom.kp_cap, st));
+  if (n) {
+    HIPCHECK(c, hipMemcpyAsync(c->d_mp, map_point, sizeof(int32_t) * n, hipMemcpyHostToDevice, st));
+    HIPCHECK(c, hipMemcpyAsync(c->d_blk, blocked, n, hipMemcpyHostToDevice, st));
+  }
+  const int64_t kc = c->geom.kp_cap;
+  FrameKps cur{c->out.kps + 2 * frame * kc, c->out.desc + 2 * frame * kc * 32,
+               c->out.nkps + 2 * frame, 2 * kc, 2};
+  GridWorkspace gw = c->gws;
+  gw.cell_start += (int64_t)frame * (kGridCells + 1);
+  gw.cell_items += (int64_t)frame * kc;
+  MatchIO io{c->d_qmeta, c->d_qmeta + 1, c->d_mp, c->d_blk, c->d_nm, kc};
+  if (f2f)
+    launch_search_frame(cur, c->sout.u_right + frame * kc, kc, c->cam, c->gd(),
+                        reinterpret_cast<const F2FQuery*>(qb),
+                        reinterpret_cast<const F2FPose*>(eb), 1, nq, gw, c->mws, io, st);
+  else
+    launch_search_mps(cur, c->sout.u_right + frame * kc, kc, c->cam, c->gd(),
+                      reinterpret_cast<const MpsQuery*>(qb), nnratio, th, 1, nq, gw, c->mws, io,
+                      st);
+  HIPCHECK(c, hipGetLastError());
+  if (n) {
+    HIPCHECK(c, hipMemcpyAsync(map_point, c->d_mp, sizeof(int32_t) * n, hipMemcpyDeviceToHost, st));
+    HIPCHECK(c, hipMemcpyAsync(blocked, c->d_blk, n, hipMemcpyDeviceToHost, st));
+  }
+  int nm = 0;
+  HIPCHECK(c, hipMemcpyAsync(&nm, c->d_nm, sizeof(int), hipMemcpyDeviceToHost, st));
+  HIPCHECK(c, hipStreamSynchronize(st));
+  if (nmatches) *nmatches = nm;
+  return check_device_err(c);
+}
+
+extern "C" {
+
+int slamgpu_search_by_projection_frame(slamgpu_ctx* c, int frame, const slamgpu_f2f_query* q,
+                                       int nq, const slamgpu_f2f_pose* pose, int32_t* map_point,
+                                       uint8_t* blocked, int n, int* nmatches) {
+  if (!pose) return SLAMGPU_EINVAL;
+  return host_search(c, frame, q, nq, map_point, blocked, n, nmatches, sizeof(slamgpu_f2f_pose),
+                     pose, true, 0.f, 0);
+}
+
+int slamgpu_search_by_projection_mps(slamgpu_ctx* c, int frame, const slamgpu_mps_query* q,
+                                     int nq, float nnratio, int th, int32_t* map_point,
+                                     uint8_t* blocked, int n, int* nmatches) {
+  return host_search(c, frame, q, nq, map_point, blocked, n, nmatches, 0, nullptr, false,
+                     nnratio, th);
+}
+
+}  // extern "C"

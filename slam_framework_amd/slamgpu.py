@@ -1,0 +1,307 @@
+"""ctypes binding of libslamgpu.so (include/slamgpu.h) and the reference-shaped Python surface.
+
+Classes mirror the reference's C++ classes for this path:
+  ORBextractor   src/orb_features/orb_extractor.h:25-93  (Compute, Get* tables, GetImagePyramid)
+  OrbMatcher     src/orb_features/orb_matcher.h:14-119   (DescriptorDistance, SearchByProjection)
+  StereoFrontend the stereo Frame ctor's hot part (frame.cpp:61-111) batched over frames.
+The library is the only compute path: there is no CPU fallback, and every entry point raises if
+libslamgpu.so is missing or a HIP call fails.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import numpy as np
+
+_PKG = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_PKG, "libslamgpu.so")
+
+KP_DTYPE = np.dtype([("x", "<f4"), ("y", "<f4"), ("size", "<f4"), ("angle", "<f4"),
+                     ("response", "<f4"), ("octave", "<i4"), ("class_id", "<i4")])
+
+F2F_QUERY_DTYPE = np.dtype([("xyz", "<f4", (3,)), ("last_angle", "<f4"), ("last_octave", "<i4"),
+                            ("mp_id", "<i4"), ("blocks", "<i4"), ("pad", "<i4"),
+                            ("desc", "u1", (32,))])
+F2F_POSE_DTYPE = np.dtype([("Rcw", "<f4", (9,)), ("tcw", "<f4", (3,)), ("tlc_z", "<f4"),
+                           ("baseline", "<f4"), ("th", "<f4"), ("mono", "<i4"),
+                           ("check_ori", "<i4"), ("pad", "<i4")])
+MPS_QUERY_DTYPE = np.dtype([("proj_x", "<f4"), ("proj_y", "<f4"), ("proj_xr", "<f4"),
+                            ("view_cos", "<f4"), ("level", "<i4"), ("in_view", "<i4"),
+                            ("is_bad", "<i4"), ("mp_id", "<i4"), ("blocks", "<i4"),
+                            ("pad", "<i4", (3,)), ("desc", "u1", (32,))])
+assert KP_DTYPE.itemsize == 28 and F2F_QUERY_DTYPE.itemsize == 64
+assert F2F_POSE_DTYPE.itemsize == 72 and MPS_QUERY_DTYPE.itemsize == 80
+
+EXPORTS = [
+    "slamgpu_create", "slamgpu_destroy", "slamgpu_last_error", "slamgpu_kp_capacity",
+    "slamgpu_scale_tables", "slamgpu_extract", "slamgpu_get_pyramid_level",
+    "slamgpu_frame_stereo", "slamgpu_frontend_device", "slamgpu_sync",
+    "slamgpu_download_keypoints", "slamgpu_download_stereo", "slamgpu_device_results",
+    "slamgpu_descriptor_distance", "slamgpu_search_by_projection_frame",
+    "slamgpu_search_by_projection_mps", "slamgpu_search_by_projection_frame_device",
+    "slamgpu_search_by_projection_mps_device", "slamgpu_debug_level_keys",
+]
+
+
+class OrbParams(C.Structure):
+    _fields_ = [("nfeatures", C.c_int), ("scale_factor", C.c_float), ("nlevels", C.c_int),
+                ("ini_th_fast", C.c_int), ("min_th_fast", C.c_int)]
+
+
+class Camera(C.Structure):
+    _fields_ = [("fx", C.c_float), ("fy", C.c_float), ("cx", C.c_float), ("cy", C.c_float),
+                ("bf", C.c_float)]
+
+
+class DeviceView(C.Structure):
+    _fields_ = [("kps", C.c_void_p), ("desc", C.c_void_p), ("nkps", C.c_void_p),
+                ("u_right", C.c_void_p), ("depth", C.c_void_p), ("kp_cap", C.c_int)]
+
+
+class SlamGpuError(RuntimeError):
+    pass
+
+
+_lib = None
+
+
+def lib():
+    """Load libslamgpu.so (fails loudly if it has not been built)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise ImportError(f"{LIB_PATH} missing: run `python -m slam_framework_amd.build`")
+        L = C.CDLL(LIB_PATH)
+        vp, ip, fp, sz = C.c_void_p, C.c_int, C.c_float, C.c_size_t
+        L.slamgpu_create.argtypes = [ip, C.POINTER(OrbParams), ip, ip, ip, C.POINTER(vp)]
+        L.slamgpu_destroy.argtypes = [vp]
+        L.slamgpu_destroy.restype = None
+        L.slamgpu_last_error.argtypes = [vp]
+        L.slamgpu_last_error.restype = C.c_char_p
+        L.slamgpu_kp_capacity.argtypes = [vp]
+        L.slamgpu_scale_tables.argtypes = [vp, vp, vp, vp, vp, vp]
+        L.slamgpu_extract.argtypes = [vp, vp, sz, vp, vp, ip, C.POINTER(ip)]
+        L.slamgpu_get_pyramid_level.argtypes = [vp, ip, ip, vp, sz, C.POINTER(ip), C.POINTER(ip)]
+        L.slamgpu_frame_stereo.argtypes = [vp, vp, vp, sz, C.POINTER(Camera)]
+        L.slamgpu_frontend_device.argtypes = [vp, vp, vp, sz, sz, ip, C.POINTER(Camera), vp]
+        L.slamgpu_sync.argtypes = [vp, vp]
+        L.slamgpu_download_keypoints.argtypes = [vp, ip, vp, vp, ip, C.POINTER(ip)]
+        L.slamgpu_download_stereo.argtypes = [vp, ip, vp, vp, ip, C.POINTER(ip)]
+        L.slamgpu_device_results.argtypes = [vp, C.POINTER(DeviceView)]
+        L.slamgpu_descriptor_distance.argtypes = [vp, vp]
+        L.slamgpu_search_by_projection_frame.argtypes = [vp, ip, vp, ip, vp, vp, vp, ip,
+                                                         C.POINTER(ip)]
+        L.slamgpu_search_by_projection_mps.argtypes = [vp, ip, vp, ip, fp, ip, vp, vp, ip,
+                                                       C.POINTER(ip)]
+        L.slamgpu_search_by_projection_frame_device.argtypes = [
+            vp, vp, ip, vp, vp, ip, vp, vp, vp, C.c_int64, vp, ip, vp]
+        L.slamgpu_search_by_projection_mps_device.argtypes = [
+            vp, vp, ip, vp, vp, ip, fp, ip, vp, vp, C.c_int64, vp, ip, vp]
+        L.slamgpu_debug_level_keys.argtypes = [vp, ip, ip, ip, vp, ip, C.POINTER(ip)]
+        _lib = L
+    return _lib
+
+
+def _ptr(a):
+    if a is None:
+        return None
+    if isinstance(a, np.ndarray):
+        return a.ctypes.data_as(C.c_void_p)
+    return C.c_void_p(int(a.data_ptr()))  # torch tensor
+
+
+class Context:
+    """Owns one slamgpu_ctx (one device, one stream, workspaces for max_frames stereo pairs)."""
+
+    def __init__(self, cols, rows, nfeatures=2000, scale_factor=1.2, nlevels=8, ini_th_fast=20,
+                 min_th_fast=7, max_frames=1, device=0):
+        self.params = OrbParams(nfeatures, scale_factor, nlevels, ini_th_fast, min_th_fast)
+        self.cols, self.rows, self.nlevels = cols, rows, nlevels
+        self.max_frames = max_frames
+        h = C.c_void_p()
+        rc = lib().slamgpu_create(device, C.byref(self.params), cols, rows, max_frames,
+                                  C.byref(h))
+        self.h = h
+        if rc != 0:
+            msg = lib().slamgpu_last_error(h).decode() if h else ""
+            if h:
+                lib().slamgpu_destroy(h)
+                self.h = None
+            raise SlamGpuError(f"slamgpu_create failed ({rc}): {msg}")
+        self.kp_cap = lib().slamgpu_kp_capacity(self.h)
+
+    def check(self, rc):
+        if rc != 0:
+            raise SlamGpuError(f"slamgpu error {rc}: {lib().slamgpu_last_error(self.h).decode()}")
+
+    def close(self):
+        if getattr(self, "h", None):
+            lib().slamgpu_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def scale_tables(self):
+        n = self.nlevels
+        arrs = [np.zeros(n, np.float32) for _ in range(4)] + [np.zeros(n, np.int32)]
+        self.check(lib().slamgpu_scale_tables(self.h, *[_ptr(a) for a in arrs]))
+        return arrs
+
+    def extract(self, img):
+        img = np.ascontiguousarray(img, dtype=np.uint8)
+        assert img.shape == (self.rows, self.cols)
+        kps = np.zeros(self.kp_cap, KP_DTYPE)
+        desc = np.zeros((self.kp_cap, 32), np.uint8)
+        n = C.c_int()
+        self.check(lib().slamgpu_extract(self.h, _ptr(img), img.strides[0], _ptr(kps), _ptr(desc),
+                                         self.kp_cap, C.byref(n)))
+        return kps[:n.value].copy(), desc[:n.value].copy()
+
+    def pyramid_level(self, img, level):
+        w, h = C.c_int(), C.c_int()
+        self.check(lib().slamgpu_get_pyramid_level(self.h, img, level, None, 0, C.byref(w),
+                                                   C.byref(h)))
+        out = np.zeros((h.value, w.value), np.uint8)
+        self.check(lib().slamgpu_get_pyramid_level(self.h, img, level, _ptr(out), w.value,
+                                                   C.byref(w), C.byref(h)))
+        return out
+
+    def debug_level_keys(self, img, level, stage):
+        """Packed (x_rel, y_rel, score) keys of one level: stage 0 FAST, 1 octree output."""
+        n = C.c_int()
+        cap = 1 << 17
+        out = np.zeros(cap, np.uint32)
+        self.check(lib().slamgpu_debug_level_keys(self.h, img, level, stage, _ptr(out), cap,
+                                                  C.byref(n)))
+        return out[:n.value].copy()
+
+    def frame_stereo(self, left, right, cam):
+        left = np.ascontiguousarray(left, dtype=np.uint8)
+        right = np.ascontiguousarray(right, dtype=np.uint8)
+        self.cam = Camera(*cam)
+        self.check(lib().slamgpu_frame_stereo(self.h, _ptr(left), _ptr(right), left.strides[0],
+                                              C.byref(self.cam)))
+
+    def frontend_device(self, d_left, d_right, frame_stride, pitch, n_frames, cam, stream=None):
+        """d_left/d_right: device pointers (int) or torch uint8 CUDA tensors."""
+        self.cam = Camera(*cam)
+        pl = d_left if isinstance(d_left, int) else int(d_left.data_ptr())
+        pr = d_right if isinstance(d_right, int) else int(d_right.data_ptr())
+        self.check(lib().slamgpu_frontend_device(self.h, C.c_void_p(pl), C.c_void_p(pr),
+                                                 frame_stride, pitch, n_frames,
+                                                 C.byref(self.cam), C.c_void_p(stream or 0)))
+
+    def sync(self, stream=None):
+        self.check(lib().slamgpu_sync(self.h, C.c_void_p(stream or 0)))
+
+    def keypoints(self, img):
+        kps = np.zeros(self.kp_cap, KP_DTYPE)
+        desc = np.zeros((self.kp_cap, 32), np.uint8)
+        n = C.c_int()
+        self.check(lib().slamgpu_download_keypoints(self.h, img, _ptr(kps), _ptr(desc),
+                                                    self.kp_cap, C.byref(n)))
+        return kps[:n.value].copy(), desc[:n.value].copy()
+
+    def stereo(self, frame):
+        ur = np.zeros(self.kp_cap, np.float32)
+        depth = np.zeros(self.kp_cap, np.float32)
+        n = C.c_int()
+        self.check(lib().slamgpu_download_stereo(self.h, frame, _ptr(ur), _ptr(depth),
+                                                 self.kp_cap, C.byref(n)))
+        return ur[:n.value].copy(), depth[:n.value].copy()
+
+    def device_results(self):
+        v = DeviceView()
+        self.check(lib().slamgpu_device_results(self.h, C.byref(v)))
+        return v
+
+    def search_by_projection_frame(self, frame, queries, pose, map_point, blocked):
+        queries = np.ascontiguousarray(queries, dtype=F2F_QUERY_DTYPE)
+        pose = np.ascontiguousarray(np.atleast_1d(pose), dtype=F2F_POSE_DTYPE)
+        assert map_point.dtype == np.int32 and blocked.dtype == np.uint8
+        nm = C.c_int()
+        self.check(lib().slamgpu_search_by_projection_frame(
+            self.h, frame, _ptr(queries), len(queries), _ptr(pose), _ptr(map_point),
+            _ptr(blocked), len(map_point), C.byref(nm)))
+        return nm.value
+
+    def search_by_projection_mps(self, frame, queries, nnratio, th, map_point, blocked):
+        queries = np.ascontiguousarray(queries, dtype=MPS_QUERY_DTYPE)
+        assert map_point.dtype == np.int32 and blocked.dtype == np.uint8
+        nm = C.c_int()
+        self.check(lib().slamgpu_search_by_projection_mps(
+            self.h, frame, _ptr(queries), len(queries), nnratio, th, _ptr(map_point),
+            _ptr(blocked), len(map_point), C.byref(nm)))
+        return nm.value
+
+
+class ORBextractor:
+    """Reference-shaped ORBextractor (orb_extractor.h:25-93) on the MI355X path.
+
+    The device context is sized per image size, so it is created on the first Compute() and
+    re-created if the image size changes."""
+
+    def __init__(self, nfeatures, scaleFactor, nlevels, iniThFAST, minThFAST, device=0):
+        self.args = (nfeatures, scaleFactor, nlevels, iniThFAST, minThFAST)
+        self.nlevels = nlevels
+        self.scaleFactor = scaleFactor
+        self.device = device
+        self.ctx = None
+
+    def _ctx(self, cols, rows):
+        if self.ctx is None or (self.ctx.cols, self.ctx.rows) != (cols, rows):
+            n, s, l, ini, mn = self.args
+            self.ctx = Context(cols, rows, n, s, l, ini, mn, max_frames=1, device=self.device)
+        return self.ctx
+
+    def Compute(self, image, mask=None):
+        """Returns (keypoints[N] as KP_DTYPE, descriptors N x 32 u8); empty image -> None."""
+        image = np.asarray(image)
+        if image.size == 0:
+            return None
+        assert image.dtype == np.uint8 and image.ndim == 2
+        return self._ctx(image.shape[1], image.shape[0]).extract(image)
+
+    def GetLevels(self):
+        return self.nlevels
+
+    def GetScaleFactor(self):
+        return self.scaleFactor
+
+    def _tables(self):
+        return (self.ctx or Context(256, 256, *self.args, max_frames=1)).scale_tables()
+
+    def GetScaleFactors(self):
+        return self._tables()[0]
+
+    def GetInverseScaleFactors(self):
+        return self._tables()[1]
+
+    def GetScaleSigmaSquares(self):
+        return self._tables()[2]
+
+    def GetInverseScaleSigmaSquares(self):
+        return self._tables()[3]
+
+    def GetImagePyramid(self):
+        return [self.ctx.pyramid_level(0, l) for l in range(self.nlevels)]
+
+
+class OrbMatcher:
+    """Reference-shaped OrbMatcher (orb_matcher.h:14-119) for the per-frame searches."""
+    TH_LOW, TH_HIGH, HISTO_LENGTH = 50, 100, 30
+
+    def __init__(self, nnratio=0.6, checkOri=True):
+        self.mfNNratio = float(nnratio)
+        self.mbCheckOrientation = bool(checkOri)
+
+    @staticmethod
+    def DescriptorDistance(a, b):
+        a = np.ascontiguousarray(a, dtype=np.uint8)
+        b = np.ascontiguousarray(b, dtype=np.uint8)
+        return lib().slamgpu_descriptor_distance(_ptr(a), _ptr(b))

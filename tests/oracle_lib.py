@@ -1,0 +1,197 @@
+"""ctypes binding of oracle/liborb_oracle.so -- the CPU restatement used as the parity checker.
+
+Test infrastructure only: imported by tests/, __graft_entry__.smoke() and bench.py's
+cpu_baseline leg, never by the product package.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ORACLE_DIR = os.path.join(ROOT, "oracle")
+LIB_PATH = os.path.join(ORACLE_DIR, "liborb_oracle.so")
+
+KP_DTYPE = np.dtype([("x", "<f4"), ("y", "<f4"), ("size", "<f4"), ("angle", "<f4"),
+                     ("response", "<f4"), ("octave", "<i4"), ("class_id", "<i4")])
+assert KP_DTYPE.itemsize == 28
+
+MAX_LEVELS = 32
+
+
+class OrbParams(C.Structure):
+    _fields_ = [("nfeatures", C.c_int), ("scale_factor", C.c_float), ("nlevels", C.c_int),
+                ("ini_th_fast", C.c_int), ("min_th_fast", C.c_int)]
+
+
+class OrbTables(C.Structure):
+    _fields_ = [("nfeatures", C.c_int), ("nlevels", C.c_int), ("ini_th_fast", C.c_int),
+                ("min_th_fast", C.c_int), ("scale_factor", C.c_double),
+                ("scale", C.c_float * MAX_LEVELS), ("inv_scale", C.c_float * MAX_LEVELS),
+                ("sigma2", C.c_float * MAX_LEVELS), ("inv_sigma2", C.c_float * MAX_LEVELS),
+                ("features_per_level", C.c_int * MAX_LEVELS), ("umax", C.c_int * 16)]
+
+
+class Pyramid(C.Structure):
+    _fields_ = [("nlevels", C.c_int), ("w", C.c_int * MAX_LEVELS), ("h", C.c_int * MAX_LEVELS),
+                ("step", C.c_size_t * MAX_LEVELS), ("data", C.POINTER(C.c_uint8) * MAX_LEVELS)]
+
+
+class GridGeom(C.Structure):
+    _fields_ = [("min_x", C.c_float), ("max_x", C.c_float), ("min_y", C.c_float),
+                ("max_y", C.c_float), ("cell_w", C.c_float), ("cell_h", C.c_float)]
+
+
+class FrameView(C.Structure):
+    _fields_ = [("kps", C.c_void_p), ("desc", C.c_void_p), ("u_right", C.c_void_p),
+                ("n", C.c_int), ("map_point", C.c_void_p)]
+
+
+def build() -> None:
+    subprocess.run(["make", "-s", "-C", ORACLE_DIR, "liborb_oracle.so"], check=True)
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            build()
+        L = C.CDLL(LIB_PATH)
+        vp, ip, fp = C.c_void_p, C.c_int, C.c_float
+        L.oc_orb_init.argtypes = [C.POINTER(OrbTables), C.POINTER(OrbParams)]
+        L.oc_cv_round.argtypes = [fp]
+        L.oc_fast_atan2.argtypes = [fp, fp]
+        L.oc_fast_atan2.restype = fp
+        L.oc_sinf.argtypes = [fp]
+        L.oc_sinf.restype = fp
+        L.oc_cosf.argtypes = [fp]
+        L.oc_cosf.restype = fp
+        L.oc_resize_linear_u8.argtypes = [vp, ip, ip, C.c_size_t, vp, ip, ip, C.c_size_t]
+        L.oc_gaussian_blur7_u8.argtypes = [vp, ip, ip, C.c_size_t, vp, C.c_size_t]
+        L.oc_fast16.argtypes = [vp, ip, ip, C.c_size_t, ip, ip, vp, ip]
+        L.oc_pyramid_alloc.argtypes = [C.POINTER(Pyramid), C.POINTER(OrbTables), ip, ip]
+        L.oc_pyramid_free.argtypes = [C.POINTER(Pyramid)]
+        L.oc_compute_pyramid.argtypes = [C.POINTER(OrbTables), vp, C.c_size_t, C.POINTER(Pyramid)]
+        L.oc_level_candidates.argtypes = [C.POINTER(OrbTables), C.POINTER(Pyramid), ip, vp, ip]
+        L.oc_distribute_octree.argtypes = [vp, ip, ip, ip, ip, ip, ip, vp, ip]
+        L.oc_ic_angle.argtypes = [vp, C.c_size_t, fp, fp, vp]
+        L.oc_ic_angle.restype = fp
+        L.oc_orb_descriptor.argtypes = [vp, vp, C.c_size_t, vp]
+        L.oc_orb_extract.argtypes = [C.POINTER(OrbTables), vp, ip, ip, C.c_size_t, vp, vp, ip,
+                                     C.POINTER(Pyramid)]
+        L.oc_descriptor_distance.argtypes = [vp, vp]
+        L.oc_stereo_match.argtypes = [C.POINTER(OrbTables), vp, vp, ip, vp, vp, ip,
+                                      C.POINTER(Pyramid), C.POINTER(Pyramid), fp, fp, vp, vp, vp]
+        L.oc_grid_geom_init.argtypes = [C.POINTER(GridGeom), ip, ip]
+        L.oc_features_in_area.argtypes = [C.POINTER(GridGeom), vp, ip, fp, fp, fp, ip, ip, vp, ip]
+        L.oc_search_by_projection_frame.argtypes = [
+            C.POINTER(GridGeom), C.POINTER(OrbTables), C.POINTER(FrameView), vp, vp, vp, ip,
+            vp, vp, vp, vp, vp, fp, fp, fp, fp, fp, fp, fp, fp, ip, ip]
+        L.oc_search_by_projection_mps.argtypes = [
+            C.POINTER(GridGeom), C.POINTER(OrbTables), C.POINTER(FrameView), ip, vp, vp, vp, vp,
+            vp, vp, vp, vp, vp, fp, ip]
+        _lib = L
+    return _lib
+
+
+def ptr(a: np.ndarray):
+    return a.ctypes.data_as(C.c_void_p)
+
+
+def tables(nfeatures=2000, scale_factor=1.2, nlevels=8, ini_th=20, min_th=7) -> OrbTables:
+    p = OrbParams(nfeatures, scale_factor, nlevels, ini_th, min_th)
+    t = OrbTables()
+    lib().oc_orb_init(C.byref(t), C.byref(p))
+    return t
+
+
+class OraclePyramid:
+    """Owns an oc_pyramid; .level(l) returns a numpy view copy."""
+
+    def __init__(self, t: OrbTables, cols: int, rows: int):
+        self.p = Pyramid()
+        if lib().oc_pyramid_alloc(C.byref(self.p), C.byref(t), cols, rows) != 0:
+            raise MemoryError("oc_pyramid_alloc")
+
+    def level(self, l: int) -> np.ndarray:
+        w, h, s = self.p.w[l], self.p.h[l], self.p.step[l]
+        buf = np.ctypeslib.as_array(self.p.data[l], shape=(h * s,))
+        return buf.reshape(h, s)[:, :w].copy()
+
+    def __del__(self):
+        try:
+            lib().oc_pyramid_free(C.byref(self.p))
+        except Exception:
+            pass
+
+
+def extract(t: OrbTables, img: np.ndarray, with_pyramid=False):
+    """ORBextractor::Compute on a 2-D u8 image -> (kps[N] KP_DTYPE, desc[N,32] u8[, pyramid])."""
+    img = np.ascontiguousarray(img, dtype=np.uint8)
+    rows, cols = img.shape
+    cap = t.nfeatures + 64 * t.nlevels
+    kps = np.zeros(cap, KP_DTYPE)
+    desc = np.zeros((cap, 32), np.uint8)
+    pyr = OraclePyramid(t, cols, rows)
+    n = lib().oc_orb_extract(C.byref(t), ptr(img), rows, cols, cols, ptr(kps), ptr(desc), cap,
+                             C.byref(pyr.p))
+    if n < 0:
+        cap = -n
+        kps = np.zeros(cap, KP_DTYPE)
+        desc = np.zeros((cap, 32), np.uint8)
+        n = lib().oc_orb_extract(C.byref(t), ptr(img), rows, cols, cols, ptr(kps), ptr(desc),
+                                 cap, C.byref(pyr.p))
+    if with_pyramid:
+        return kps[:n].copy(), desc[:n].copy(), pyr
+    return kps[:n].copy(), desc[:n].copy()
+
+
+def stereo(t, kl, dl, kr, dr, pyr_l, pyr_r, fx, bf):
+    nl = len(kl)
+    ur = np.zeros(nl, np.float32)
+    depth = np.zeros(nl, np.float32)
+    sad = np.zeros(nl, np.int32)
+    kl = np.ascontiguousarray(kl)
+    kr = np.ascontiguousarray(kr)
+    dl = np.ascontiguousarray(dl)
+    dr = np.ascontiguousarray(dr)
+    lib().oc_stereo_match(C.byref(t), ptr(kl), ptr(dl), nl, ptr(kr), ptr(dr), len(kr),
+                          C.byref(pyr_l.p), C.byref(pyr_r.p), fx, bf, ptr(ur), ptr(depth),
+                          ptr(sad))
+    return ur, depth, sad
+
+
+def grid_geom(cols, rows) -> GridGeom:
+    g = GridGeom()
+    lib().oc_grid_geom_init(C.byref(g), cols, rows)
+    return g
+
+
+def pack_keys(kps) -> np.ndarray:
+    """oc_keypoint candidates (octree coords) -> packed keys as the HIP path stores them."""
+    x = kps["x"].astype(np.int64)
+    y = kps["y"].astype(np.int64)
+    s = kps["response"].astype(np.int64)
+    return (x | (y << 12) | (s << 23)).astype(np.uint32)
+
+
+def level_candidates(t, pyr, level):
+    cap = 1 << 17
+    out = np.zeros(cap, KP_DTYPE)
+    n = lib().oc_level_candidates(C.byref(t), C.byref(pyr.p), level, ptr(out), cap)
+    return out[:n].copy()
+
+
+def distribute_octree(t, pyr, level, cands):
+    w, h = pyr.p.w[level], pyr.p.h[level]
+    cands = np.ascontiguousarray(cands)
+    out = np.zeros(len(cands) + 1, KP_DTYPE)
+    n = lib().oc_distribute_octree(ptr(cands), len(cands), 16, w - 16, 16, h - 16,
+                                   t.features_per_level[level], ptr(out), len(out))
+    return out[:n].copy()
