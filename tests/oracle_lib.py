@@ -195,3 +195,47 @@ def distribute_octree(t, pyr, level, cands):
     n = lib().oc_distribute_octree(ptr(cands), len(cands), 16, w - 16, 16, h - 16,
                                    t.features_per_level[level], ptr(out), len(out))
     return out[:n].copy()
+
+
+def _frame_view(kps, desc, ur, mp):
+    fv = FrameView()
+    fv.kps = kps.ctypes.data
+    fv.desc = desc.ctypes.data
+    fv.u_right = ur.ctypes.data
+    fv.n = len(kps)
+    fv.map_point = mp.ctypes.data
+    return fv
+
+
+def search_frame(t, g, cur_kps, cur_desc, cur_ur, cur_mp, last_kps, last_mp, last_outlier,
+                 mp_xyz, mp_desc, mp_nobs, Rcw, tcw, tlc_z, baseline, cam, th, mono, check_ori):
+    """OrbMatcher::SearchByProjection(CurrentFrame, LastFrame, th, bMono); cur_mp is in/out."""
+    arrs = [np.ascontiguousarray(a) for a in (cur_kps, cur_desc, cur_ur)]
+    fv = _frame_view(arrs[0], arrs[1], arrs[2], cur_mp)
+    last_kps = np.ascontiguousarray(last_kps)
+    mp_xyz = np.ascontiguousarray(mp_xyz, np.float32)
+    mp_desc = np.ascontiguousarray(mp_desc, np.uint8)
+    mp_nobs = np.ascontiguousarray(mp_nobs, np.int32)
+    R = np.ascontiguousarray(Rcw, np.float32).reshape(-1)
+    tt = np.ascontiguousarray(tcw, np.float32).reshape(-1)
+    fx, fy, cx, cy, bf = cam
+    return lib().oc_search_by_projection_frame(
+        C.byref(g), C.byref(t), C.byref(fv), ptr(last_kps), ptr(last_mp), ptr(last_outlier),
+        len(last_kps), ptr(mp_xyz), ptr(mp_desc), ptr(mp_nobs), ptr(R), ptr(tt), tlc_z, baseline,
+        fx, fy, cx, cy, bf, th, mono, check_ori)
+
+
+def search_mps(t, g, cur_kps, cur_desc, cur_ur, cur_mp, q, mp_nobs, nnratio, th):
+    """OrbMatcher::SearchByProjection(F, vpMapPoints, th) with map point id == query index."""
+    arrs = [np.ascontiguousarray(a) for a in (cur_kps, cur_desc, cur_ur)]
+    fv = _frame_view(arrs[0], arrs[1], arrs[2], cur_mp)
+    cols = {k: np.ascontiguousarray(q[k]) for k in q.dtype.names}
+    in_view = cols["in_view"].astype(np.uint8)
+    is_bad = cols["is_bad"].astype(np.uint8)
+    level = cols["level"].astype(np.int32)
+    desc = np.ascontiguousarray(q["desc"], np.uint8)
+    mp_nobs = np.ascontiguousarray(mp_nobs, np.int32)
+    return lib().oc_search_by_projection_mps(
+        C.byref(g), C.byref(t), C.byref(fv), len(q), ptr(in_view), ptr(is_bad), ptr(level),
+        ptr(cols["view_cos"]), ptr(cols["proj_x"]), ptr(cols["proj_y"]), ptr(cols["proj_xr"]),
+        ptr(desc), ptr(mp_nobs), nnratio, th)
