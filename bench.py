@@ -1,0 +1,263 @@
+#!/usr/bin/env python3
+"""bench.py -- stereo frames/s of the ORB extract + match hot path on MI355X.
+
+One step = one pass of the hot path over one batch of B synthetic 1241x376 stereo frames that are
+already resident in HBM (BASELINE.json configs[1]): ORBextractor::Compute on both views
+(2000 features, 8 levels), Frame::ComputeStereoMatches, the 64x48 keypoint grid, the previous
+frame's stereo points as visual-odometry map points, and OrbMatcher::SearchByProjection(
+CurrentFrame, LastFrame, th=7) -- the tracker's per-frame motion-model search. Frame 0 of a batch
+is the halo frame of frame 1's search, so a step completes B-1 frames.
+
+Multi-GPU (python -m torch.distributed.run --nproc-per-node N bench.py --gpus N): every rank
+processes its own batch of frames (frames are independent units: weak scaling, no data-path
+collective); the barrier and the max-over-ranks timing use the RCCL process group.
+
+Prints ONE JSON line on rank 0 (driver contract), with `roofline` for the dominant kernel
+(HIP-event timed inside the timed region) and `cpu_baseline` (the oracle/ restatement on host
+cores, rank 0 only). Per-kernel breakdowns go to stderr.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+
+# Algorithmic HBM bytes per launch unit of each kernel (DESIGN.md "Roofline model"); unit = one
+# image, except stereo/grid/search kernels whose unit is one stereo frame.
+LEVEL_PX = None  # filled from the context geometry
+
+
+def kernel_bytes(name, n_images, n_frames, kp_per_image, level_px, n_queries):
+    """Algorithmic bytes one step moves through the named kernel (all its launches)."""
+    px = sum(level_px)
+    if name == "pyr_down":       # read level l-1, write level l
+        return n_images * sum(level_px[l - 1] + level_px[l] for l in range(1, len(level_px)))
+    if name == "blur7":          # read + write every level
+        return n_images * 2 * px
+    if name == "fast_cells":     # read every level once (+ small candidate writes)
+        return n_images * px
+    if name == "orient_desc":    # 749-px disc + 37x37 blurred window + 60 B out per keypoint
+        return n_images * kp_per_image * (749 + 37 * 37 + 60)
+    if name == "stereo_match":   # left+right kps/desc (60 B each) + SAD windows (11x11 + 11x21)
+        return n_frames * kp_per_image * (2 * 60 + 121 + 231)
+    if name == "search_cand":    # query (64 B) + window candidates' kps/desc (~60 B each, ~8)
+        return n_queries * (64 + 8 * 60)
+    if name == "octree":         # FAST candidates read + kept keys written (4 B each)
+        return n_images * 4 * 2 * kp_per_image
+    return None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--batch", type=int, default=128, help="stereo frames per GPU per step")
+    ap.add_argument("--distinct", type=int, default=16, help="distinct synthetic frames per rank")
+    ap.add_argument("--cpu-frames", type=int, default=0, help="oracle sample size (0 = auto)")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    from slam_framework_amd import slamgpu as G
+    from slam_framework_amd import synthetic as S
+
+    cols, rows, B, D = S.KITTI_COLS, S.KITTI_ROWS, args.batch, args.distinct
+    cam = S.KITTI_CAM
+    # ---- synthetic input, uploaded once (resident in HBM before the timed region)
+    Ls, Rs = S.sequence(1000 + rank, D)
+    pitch = 1280
+    host_l = np.zeros((B, rows, pitch), np.uint8)
+    host_r = np.zeros((B, rows, pitch), np.uint8)
+    for f in range(B):
+        host_l[f, :, :cols] = Ls[f % D]
+        host_r[f, :, :cols] = Rs[f % D]
+    d_l = torch.from_numpy(host_l).to(dev)
+    d_r = torch.from_numpy(host_r).to(dev)
+    stride = rows * pitch
+    poses = np.zeros(B, G.F2F_POSE_DTYPE)
+    for f in range(B):
+        poses["Rcw"][f] = S.rotation(f % D).astype(np.float32).reshape(-1)
+    poses["baseline"] = np.float32(cam[4]) / np.float32(cam[0])
+    poses["th"] = 7.0
+    poses["check_ori"] = 1
+    d_poses = torch.from_numpy(poses.view(np.uint8).copy()).to(dev)
+
+    ctx = G.Context(cols, rows, 2000, 1.2, 8, 20, 7, max_frames=B, device=local)
+    kc = ctx.kp_cap
+    d_q = torch.empty(B * kc * G.F2F_QUERY_DTYPE.itemsize, dtype=torch.uint8, device=dev)
+    d_qs = torch.empty(B, dtype=torch.int32, device=dev)
+    d_qc = torch.empty(B, dtype=torch.int32, device=dev)
+    d_mp = torch.empty(B * kc, dtype=torch.int32, device=dev)
+    d_blk = torch.empty(B * kc, dtype=torch.uint8, device=dev)
+    d_nm = torch.empty(B, dtype=torch.int32, device=dev)
+
+    def step():
+        st = torch.cuda.current_stream().cuda_stream
+        ctx.frontend_device(int(d_l.data_ptr()), int(d_r.data_ptr()), stride, pitch, B, cam, st)
+        ctx.make_vo_queries_device(d_poses, 1, d_q, d_qs, d_qc, B, st)
+        d_mp.fill_(-1)
+        d_blk.zero_()
+        ctx.search_by_projection_frame_device(d_q, B * kc, d_qs, d_qc, kc, d_poses, d_mp, d_blk,
+                                              kc, d_nm, B, st)
+
+    for _ in range(max(1, args.warmup)):
+        step()
+    torch.cuda.synchronize()
+    ctx.sync()
+    # sanity of what the timed steps compute (not timed)
+    nk = np.array([ctx.keypoints(i)[0].shape[0] for i in range(min(4, 2 * B))])
+    nm = d_nm.cpu().numpy()
+    nq = d_qc.cpu().numpy()
+    print(f"[rank {rank}] keypoints/image {nk.tolist()} queries/frame {nq[1:5].tolist()} "
+          f"matches/frame {nm[1:5].tolist()}", file=sys.stderr)
+
+    # ---- per-kernel breakdown pass (untimed) to pick the dominant kernel
+    names = ["pyr_down", "blur7", "fast_cells", "octree", "orient_desc", "stereo_rows",
+             "stereo_match", "stereo_median", "grid_build", "vo_queries", "search_cand",
+             "search_resolve"]
+    ctx.timing_start("*", 4096)
+    step()
+    ctx.timing_stop()
+    brk = {n: ctx.timing_read(n) for n in names}
+    tot = sum(v[0] for v in brk.values())
+    print("[rank %d] kernel ms/step: " % rank + ", ".join(
+        f"{n} {brk[n][0]:.3f} ({100 * brk[n][0] / tot:.0f}%)" for n in names), file=sys.stderr)
+    dominant = max(names, key=lambda n: brk[n][0])
+
+    # ---- timed region
+    launches_per_step = max(1, brk[dominant][1])
+    ctx.timing_start(dominant, launches_per_step * args.steps + 16)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t1 = time.perf_counter()
+    ctx.timing_stop()
+    ctx.sync()
+    elapsed = t1 - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    dom_ms, dom_n = ctx.timing_read(dominant)
+
+    frames = world * (B - 1) * args.steps
+    value = frames / elapsed
+    ms_per_step = 1000.0 * elapsed / args.steps
+
+    if rank == 0:
+        level_px = [ctx.pyramid_level(0, l).size for l in range(8)]
+        kp_img = float(nk.mean())
+        nqueries = int(nq.sum())
+        dom_bytes = kernel_bytes(dominant, 2 * B, B, kp_img, level_px, nqueries)
+        avg_launch_s = dom_ms / 1000.0 / max(1, dom_n)
+        per_launch_bytes = dom_bytes / max(1, launches_per_step) if dom_bytes else None
+        achieved = (per_launch_bytes / avg_launch_s / 1e9) if per_launch_bytes else None
+        roofline = {
+            "kernel": dominant, "bound": "hbm",
+            "achieved": round(achieved, 2) if achieved else None,
+            "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 5) if achieved else None,
+            "traffic": None,
+            "avg_launch_us": round(avg_launch_s * 1e6, 2), "launches": dom_n,
+            "algorithmic_bytes_per_launch": per_launch_bytes,
+        }
+        cpu = None
+        if not args.no_cpu_baseline:
+            cpu = cpu_baseline(Ls, Rs, args.cpu_frames)
+        line = {
+            "metric": "stereo frames/sec ORB extract+match @1241x376, 2000 kp/frame",
+            "value": round(value, 2), "unit": "stereo frames/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 3),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u8",
+            "data": "synthetic (seeded rectangles scene, pure-rotation sequence)",
+            "config": {"workload": "configs[1]: synthetic 1241x376 stereo stream, 2000 kp/frame, "
+                                   "extract L+R + stereo match + frame-to-frame match",
+                       "frames_per_gpu_per_step": B - 1, "batch": B, "nfeatures": 2000,
+                       "nlevels": 8, "scale_factor": 1.2, "fast_th": [20, 7],
+                       "parallelism": f"frame-sharded x{world}"},
+            "roofline": roofline,
+            "cpu_baseline": cpu,
+            "kernel_ms_per_step": {n: round(brk[n][0], 4) for n in names},
+        }
+        print(json.dumps(line))
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+def cpu_baseline(Ls, Rs, n_frames):
+    """The oracle/ restatement (scalar C) on host threads: extract L+R, stereo, frame-to-frame
+    search against the previous frame's stereo points. Each thread runs its own consecutive
+    frames; wall time over all threads."""
+    import concurrent.futures as cf
+
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import oracle_lib as O
+    import scenario
+    from slam_framework_amd import synthetic as S
+
+    O.build()
+    t = O.tables()
+    g = O.grid_geom(S.KITTI_COLS, S.KITTI_ROWS)
+    cam = S.KITTI_CAM
+    threads = min(16, os.cpu_count() or 1)
+    per_thread = max(2, (n_frames or 8 * threads) // threads)
+    D = len(Ls)
+
+    def run(tid):
+        prev = None
+        for k in range(per_thread):
+            f = (tid * per_thread + k) % D
+            kl, dl, pl = O.extract(t, Ls[f], True)
+            kr, dr, pr = O.extract(t, Rs[f], True)
+            ur, depth, _ = O.stereo(t, kl, dl, kr, dr, pl, pr, cam[0], cam[4])
+            if prev is not None:
+                q, lmp, lout, xyz, md, nobs = scenario.vo_queries(prev[0], prev[1], prev[2],
+                                                                  prev[3])
+                p = scenario.pose(f)
+                mp = np.full(len(kl), -1, np.int32)
+                O.search_frame(t, g, kl, dl, ur, mp, prev[0], lmp, lout, xyz, md, nobs,
+                               p["Rcw"][0].reshape(3, 3), p["tcw"][0], 0.0,
+                               float(p["baseline"][0]), cam, 7.0, 0, 1)
+            prev = (kl, dl, depth, f)
+        return per_thread
+
+    t0 = time.perf_counter()
+    with cf.ThreadPoolExecutor(threads) as ex:
+        done = sum(ex.map(run, range(threads)))
+    wall = time.perf_counter() - t0
+    return {"value": round(done / wall, 2), "unit": "stereo frames/s", "cores": threads,
+            "kind": "port",
+            "sample": f"{done} synthetic stereo frames ({threads} threads x {per_thread}); "
+                      f"oracle/ scalar C restatement: extract L+R + stereo + frame-to-frame",
+            "wall_s": round(wall, 2)}
+
+
+if __name__ == "__main__":
+    main()

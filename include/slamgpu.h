@@ -196,6 +196,26 @@ int slamgpu_search_by_projection_mps_device(slamgpu_ctx* ctx, const slamgpu_mps_
                                             int64_t mp_stride, int* d_nmatches, int n_frames,
                                             void* stream);
 
+/* Builds frame-to-frame queries on the device from the last frontend call: for frame f >= 1,
+ * every left keypoint of frame f-1 with stereo depth becomes a map point at
+ * Frame::UnprojectStereo(i) (frame.cpp:594-607) under d_poses[f-1] -- the visual-odometry points
+ * of Tracker::UpdateLastFrame (tracker.cpp:695-753) with all stereo points kept. `blocks` sets
+ * their NumObservations() > 0 flag. Frame f's queries go to d_queries[f * kp_cap ...]
+ * (d_queries holds n_frames * kp_cap entries); frame 0 gets none. Feed the outputs to
+ * slamgpu_search_by_projection_frame_device with total_queries = n_frames * kp_cap. */
+int slamgpu_make_vo_queries_device(slamgpu_ctx* ctx, const slamgpu_f2f_pose* d_poses, int blocks,
+                                   slamgpu_f2f_query* d_queries, int* d_q_start, int* d_q_count,
+                                   int n_frames, void* stream);
+
+/* ---- measurement ---------------------------------------------------------------------------- */
+/* Brackets every launch of `kernel` ("*" = all kernels) with HIP events on its stream until
+ * slamgpu_timing_stop; slamgpu_timing_read sums the recorded durations. Kernel names: pyr_down,
+ * blur7, fast_cells, octree, orient_desc, stereo_rows, stereo_match, stereo_median, grid_build,
+ * vo_queries, search_cand, search_resolve. */
+int slamgpu_timing_start(slamgpu_ctx* ctx, const char* kernel, int max_launches);
+int slamgpu_timing_stop(slamgpu_ctx* ctx, void* stream);
+int slamgpu_timing_read(slamgpu_ctx* ctx, const char* kernel, double* total_ms, int* launches);
+
 #ifdef __cplusplus
 }
 #endif

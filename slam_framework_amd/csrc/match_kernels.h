@@ -118,4 +118,11 @@ void launch_search_mps(const FrameKps& cur, const float* u_right, int64_t ur_str
                        const GridWorkspace& gw, const MatchWorkspace& mw, const MatchIO& io,
                        hipStream_t st);
 
+// Queries for frame f from frame f-1's stereo keypoints (frame 0 gets none); queries of frame f
+// occupy queries[f * kp_cap ...].
+void launch_vo_queries(const FrameKps& src, const float* depth, int64_t depth_stride,
+                       const Camera& cam, const F2FPose* poses, int blocks, int kp_cap,
+                       F2FQuery* queries, int* q_start, int* q_count, int n_frames,
+                       hipStream_t st);
+
 }  // namespace slamgpu

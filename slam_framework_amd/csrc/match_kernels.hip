@@ -15,6 +15,7 @@
 #include <stdint.h>
 
 #include "device_math.h"
+#include "timing.h"
 #include "match_kernels.h"
 
 namespace slamgpu {
@@ -284,11 +285,11 @@ void launch_stereo(const ImageBatch& b, const OrbGeomDev& gd, const Camera& cam,
   const OrbGeom& g = *gd.host;
   FrameKps ext{gd.out.kps, gd.out.desc, gd.out.nkps, g.kp_cap, 1};
   const int nrows = g.lv[0].h;
-  hipLaunchKernelGGL(stereo_rows_kernel, dim3(n_frames), dim3(256), 0, st, gd.dev, ext, nrows,
+  SLAMGPU_LAUNCH("stereo_rows", st, stereo_rows_kernel, dim3(n_frames), dim3(256), 0, st, gd.dev, ext, nrows,
                      ws, gd.ws.err);
-  hipLaunchKernelGGL(stereo_match_kernel, dim3((g.kp_cap + 3) / 4, n_frames), dim3(256), 0, st,
+  SLAMGPU_LAUNCH("stereo_match", st, stereo_match_kernel, dim3((g.kp_cap + 3) / 4, n_frames), dim3(256), 0, st,
                      b, gd.dev, ext, cam, nrows, ws, out);
-  hipLaunchKernelGGL(stereo_median_kernel, dim3(n_frames), dim3(256), 0, st, gd.dev, ext, ws,
+  SLAMGPU_LAUNCH("stereo_median", st, stereo_median_kernel, dim3(n_frames), dim3(256), 0, st, gd.dev, ext, ws,
                      out);
 }
 
@@ -329,7 +330,7 @@ __global__ __launch_bounds__(256) void grid_build_kernel(FrameKps cur, Camera ca
 
 void launch_grid(const FrameKps& cur, const Camera& cam, int n_frames, int kp_cap,
                  const GridWorkspace& gw, hipStream_t st) {
-  hipLaunchKernelGGL(grid_build_kernel, dim3(n_frames), dim3(256), 0, st, cur, cam, kp_cap, gw);
+  SLAMGPU_LAUNCH("grid_build", st, grid_build_kernel, dim3(n_frames), dim3(256), 0, st, cur, cam, kp_cap, gw);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -660,9 +661,9 @@ void launch_search_frame(const FrameKps& cur, const float* u_right, int64_t ur_s
                          const F2FPose* poses, int n_frames, int max_q, const GridWorkspace& gw,
                          const MatchWorkspace& mw, const MatchIO& io, hipStream_t st) {
   if (max_q > 0)
-    hipLaunchKernelGGL(search_cand_kernel<F2FQuery>, dim3((max_q + 3) / 4, n_frames), dim3(256),
+    SLAMGPU_LAUNCH("search_cand", st, search_cand_kernel<F2FQuery>, dim3((max_q + 3) / 4, n_frames), dim3(256),
                        0, st, cur, u_right, ur_stride, cam, g.dev, queries, poses, 0, gw, mw, io);
-  hipLaunchKernelGGL(search_resolve_kernel<F2FQuery>, dim3(n_frames), dim3(64), 0, st, cur,
+  SLAMGPU_LAUNCH("search_resolve", st, search_resolve_kernel<F2FQuery>, dim3(n_frames), dim3(64), 0, st, cur,
                      u_right, ur_stride, cam, g.dev, queries, poses, 0, 0.0f, gw, mw, io);
 }
 
@@ -671,12 +672,90 @@ void launch_search_mps(const FrameKps& cur, const float* u_right, int64_t ur_str
                        float nnratio, int th, int n_frames, int max_q, const GridWorkspace& gw,
                        const MatchWorkspace& mw, const MatchIO& io, hipStream_t st) {
   if (max_q > 0)
-    hipLaunchKernelGGL(search_cand_kernel<MpsQuery>, dim3((max_q + 3) / 4, n_frames), dim3(256),
+    SLAMGPU_LAUNCH("search_cand", st, search_cand_kernel<MpsQuery>, dim3((max_q + 3) / 4, n_frames), dim3(256),
                        0, st, cur, u_right, ur_stride, cam, g.dev, queries,
                        (const F2FPose*)nullptr, th, gw, mw, io);
-  hipLaunchKernelGGL(search_resolve_kernel<MpsQuery>, dim3(n_frames), dim3(64), 0, st, cur,
+  SLAMGPU_LAUNCH("search_resolve", st, search_resolve_kernel<MpsQuery>, dim3(n_frames), dim3(64), 0, st, cur,
                      u_right, ur_stride, cam, g.dev, queries, (const F2FPose*)nullptr, th,
                      nnratio, gw, mw, io);
+}
+
+// ---------------------------------------------------------------------------------------
+// VO map points of the previous frame as queries for frame f (Tracker::UpdateLastFrame's
+// visual-odometry points, tracker.cpp:695-753, with every stereo keypoint kept): keypoint i of
+// frame f-1 with depth > 0 becomes a point at Frame::UnprojectStereo(i) (frame.cpp:594-607).
+// Queries keep last-frame keypoint order (block-wide ordered compaction).
+__global__ __launch_bounds__(256) void vo_queries_kernel(FrameKps src, const float* __restrict__ depth,
+                                                         int64_t depth_stride, Camera cam,
+                                                         const F2FPose* __restrict__ poses,
+                                                         int blocks, int kp_cap,
+                                                         F2FQuery* __restrict__ queries,
+                                                         int* __restrict__ q_start,
+                                                         int* __restrict__ q_count) {
+  __shared__ int wsum[4];
+  __shared__ int base;
+  const int f = blockIdx.x, tid = threadIdx.x;
+  if (tid == 0) {
+    q_start[f] = f * kp_cap;
+    base = 0;
+  }
+  if (f == 0) {
+    if (tid == 0) q_count[0] = 0;
+    return;
+  }
+  const int s = f - 1;
+  const KeyPoint* k = src.kps + s * src.stride;
+  const uint8_t* d = src.desc + s * src.stride * 32;
+  const int n = src.n[s * src.n_stride];
+  const float* z = depth + s * depth_stride;
+  const F2FPose& P = poses[s];
+  // Twc: Rwc = Rcw^T, Ow = -Rcw^T tcw
+  float Rwc[9], Ow[3];
+  for (int r = 0; r < 3; r++)
+    for (int c = 0; c < 3; c++) Rwc[3 * r + c] = P.Rcw[3 * c + r];
+  for (int r = 0; r < 3; r++)
+    Ow[r] = -(Rwc[3 * r] * P.tcw[0] + Rwc[3 * r + 1] * P.tcw[1] + Rwc[3 * r + 2] * P.tcw[2]);
+  const float invfx = 1.0f / cam.fx, invfy = 1.0f / cam.fy;
+  __syncthreads();
+  for (int c0 = 0; c0 < n; c0 += 256) {
+    const int i = c0 + tid;
+    const bool ok = i < n && z[i] > 0;
+    const int lane = tid & 63, wid = tid >> 6;
+    const uint64_t m = __ballot(ok);
+    if (lane == 0) wsum[wid] = __popcll(m);
+    __syncthreads();
+    int pre = base;
+    for (int w = 0; w < wid; w++) pre += wsum[w];
+    pre += lanes_below(m);
+    if (ok) {
+      const KeyPoint kp = k[i];
+      const float zz = z[i];
+      const float x = (kp.x - cam.cx) * zz * invfx;
+      const float y = (kp.y - cam.cy) * zz * invfy;
+      F2FQuery q;
+      const float xc[3] = {x, y, zz};
+      for (int r = 0; r < 3; r++) q.xyz[r] = mat3_row(Rwc, r, xc, Ow[r]);
+      q.last_angle = kp.angle;
+      q.last_octave = kp.octave;
+      q.mp_id = i;
+      q.blocks = blocks;
+      q.pad = 0;
+      for (int b = 0; b < 32; b++) q.desc[b] = d[i * 32 + b];
+      queries[(int64_t)f * kp_cap + pre] = q;
+    }
+    __syncthreads();
+    if (tid == 0) base += wsum[0] + wsum[1] + wsum[2] + wsum[3];
+    __syncthreads();
+  }
+  if (tid == 0) q_count[f] = base;
+}
+
+void launch_vo_queries(const FrameKps& src, const float* depth, int64_t depth_stride,
+                       const Camera& cam, const F2FPose* poses, int blocks, int kp_cap,
+                       F2FQuery* queries, int* q_start, int* q_count, int n_frames,
+                       hipStream_t st) {
+  SLAMGPU_LAUNCH("vo_queries", st, vo_queries_kernel, dim3(n_frames), dim3(256), 0, st, src, depth,
+                 depth_stride, cam, poses, blocks, kp_cap, queries, q_start, q_count);
 }
 
 }  // namespace slamgpu

@@ -12,6 +12,7 @@
 #include <stdint.h>
 
 #include "device_math.h"
+#include "timing.h"
 #include "orb_geometry.h"
 #include "orb_kernels.h"
 
@@ -848,17 +849,17 @@ void launch_extract(const ImageBatch& b, const OrbGeomDev& gd, int n_images, hip
   for (int l = 1; l < g.nlevels; l++) {
     const int w = g.lv[l].w, h = g.lv[l].h;
     dim3 grid((w + 1023) / 1024, h, n_images);
-    hipLaunchKernelGGL(pyr_down_kernel, grid, dim3(256), 0, st, b, gd.dev, l, gd.rx, gd.ry);
+    SLAMGPU_LAUNCH("pyr_down", st, pyr_down_kernel, grid, dim3(256), 0, st, b, gd.dev, l, gd.rx, gd.ry);
   }
-  hipLaunchKernelGGL(blur7_kernel, dim3(g.blur_tiles, n_images), dim3(256), 0, st, b, gd.dev);
-  hipLaunchKernelGGL(fast_cells_kernel,
+  SLAMGPU_LAUNCH("blur7", st, blur7_kernel, dim3(g.blur_tiles, n_images), dim3(256), 0, st, b, gd.dev);
+  SLAMGPU_LAUNCH("fast_cells", st, fast_cells_kernel,
                      dim3((g.cells_per_image + kCellWaves - 1) / kCellWaves, n_images),
                      dim3(64 * kCellWaves), 0, st, b, gd.dev, gd.ws.cell_keys,
                      gd.ws.cell_count, gd.ws.err);
-  hipLaunchKernelGGL(octree_kernel, dim3(g.nlevels, n_images), dim3(kOctThreads), 0, st, gd.dev,
+  SLAMGPU_LAUNCH("octree", st, octree_kernel, dim3(g.nlevels, n_images), dim3(kOctThreads), 0, st, gd.dev,
                      gd.ws.cell_keys, gd.ws.cell_count, gd.ws.key_scratch, gd.ws.node_scratch,
                      gd.ws.oct_keys, gd.ws.oct_count, gd.ws.err);
-  hipLaunchKernelGGL(orient_desc_kernel, dim3((g.kp_cap + 3) / 4, n_images), dim3(256), 0, st,
+  SLAMGPU_LAUNCH("orient_desc", st, orient_desc_kernel, dim3((g.kp_cap + 3) / 4, n_images), dim3(256), 0, st,
                      b, gd.dev, gd.disc, gd.ws.oct_keys, gd.ws.oct_count, gd.out.kps,
                      gd.out.desc, gd.out.nkps);
 }

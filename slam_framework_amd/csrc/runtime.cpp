@@ -18,8 +18,13 @@
 #include "match_kernels.h"
 #include "orb_kernels.h"
 #include "orb_tables.h"
+#include "timing.h"
 
 using namespace slamgpu;
+
+namespace slamgpu {
+thread_local KernelTimer* g_timer = nullptr;
+}
 
 struct slamgpu_ctx {
   int device = 0;
@@ -62,6 +67,7 @@ struct slamgpu_ctx {
   int32_t* d_mp = nullptr;
   uint8_t* d_blk = nullptr;
   std::vector<void*> allocs;
+  KernelTimer timer;
   OrbGeomDev gd() const {
     OrbGeomDev g;
     g.host = &geom;
@@ -73,6 +79,13 @@ struct slamgpu_ctx {
     g.out = out;
     return g;
   }
+};
+
+// Makes the context's timer visible to the SLAMGPU_LAUNCH sites for the duration of a call.
+struct TimerScope {
+  KernelTimer* prev;
+  explicit TimerScope(slamgpu_ctx* c) : prev(g_timer) { g_timer = c && c->timer.on ? &c->timer : nullptr; }
+  ~TimerScope() { g_timer = prev; }
 };
 
 static int fail(slamgpu_ctx* c, int code, const char* fmt, ...) {
@@ -128,6 +141,10 @@ static void set_camera(slamgpu_ctx* c, const slamgpu_camera* cam) {
   k.cell_h = (float)(k.max_y - k.min_y) / (kGridRows);
   c->cam = k;
   c->have_cam = true;
+}
+
+static FrameKps left_views(const slamgpu_ctx* c) {
+  return FrameKps{c->out.kps, c->out.desc, c->out.nkps, 2 * (int64_t)c->geom.kp_cap, 2};
 }
 
 static int check_device_err(slamgpu_ctx* c) {
@@ -237,6 +254,7 @@ void slamgpu_destroy(slamgpu_ctx* c) {
   if (!c) return;
   (void)hipSetDevice(c->device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
+  for (hipEvent_t e : c->timer.pool) (void)hipEventDestroy(e);
   for (void* p : c->allocs) (void)hipFree(p);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
@@ -261,6 +279,7 @@ int slamgpu_scale_tables(const slamgpu_ctx* c, float* scale, float* inv_scale, f
 
 static int run_frontend(slamgpu_ctx* c, const ImageBatch& b, int n_frames, int n_images,
                         bool stereo, hipStream_t st) {
+  TimerScope ts(c);
   c->batch = b;
   c->n_frames_last = n_frames;
   c->n_images_last = n_images;
@@ -424,6 +443,62 @@ int slamgpu_device_results(const slamgpu_ctx* c, slamgpu_device_view* v) {
   return 0;
 }
 
+int slamgpu_make_vo_queries_device(slamgpu_ctx* c, const slamgpu_f2f_pose* d_poses, int blocks,
+                                   slamgpu_f2f_query* d_queries, int* d_q_start, int* d_q_count,
+                                   int n_frames, void* stream) {
+  if (!c || !c->have_cam || n_frames < 1 || n_frames > c->n_frames_last)
+    return fail(c, SLAMGPU_EINVAL, "make_vo_queries_device: bad arguments");
+  TimerScope ts(c);
+  launch_vo_queries(left_views(c), c->sout.depth, c->geom.kp_cap, c->cam,
+                    reinterpret_cast<const F2FPose*>(d_poses), blocks, c->geom.kp_cap,
+                    reinterpret_cast<F2FQuery*>(d_queries), d_q_start, d_q_count, n_frames,
+                    pick_stream(c, stream));
+  HIPCHECK(c, hipGetLastError());
+  return 0;
+}
+
+int slamgpu_timing_start(slamgpu_ctx* c, const char* kernel, int max_launches) {
+  if (!c || !kernel || max_launches < 1) return SLAMGPU_EINVAL;
+  HIPCHECK(c, hipSetDevice(c->device));
+  KernelTimer& t = c->timer;
+  while ((int)t.pool.size() < 2 * max_launches) {
+    hipEvent_t e;
+    HIPCHECK(c, hipEventCreate(&e));
+    t.pool.push_back(e);
+  }
+  t.target = kernel;
+  t.used = 0;
+  t.names.clear();
+  t.overflow = false;
+  t.on = true;
+  return 0;
+}
+
+int slamgpu_timing_stop(slamgpu_ctx* c, void* stream) {
+  if (!c) return SLAMGPU_EINVAL;
+  c->timer.on = false;
+  HIPCHECK(c, hipStreamSynchronize(pick_stream(c, stream)));
+  HIPCHECK(c, hipDeviceSynchronize());
+  if (c->timer.overflow) return fail(c, SLAMGPU_ECAP, "timing event pool exhausted");
+  return 0;
+}
+
+int slamgpu_timing_read(slamgpu_ctx* c, const char* kernel, double* total_ms, int* launches) {
+  if (!c || !kernel) return SLAMGPU_EINVAL;
+  double tot = 0;
+  int n = 0;
+  for (size_t i = 0; i < c->timer.used; i++) {
+    if (std::strcmp(kernel, "*") != 0 && std::strcmp(kernel, c->timer.names[i]) != 0) continue;
+    float ms = 0;
+    HIPCHECK(c, hipEventElapsedTime(&ms, c->timer.pool[2 * i], c->timer.pool[2 * i + 1]));
+    tot += ms;
+    n++;
+  }
+  if (total_ms) *total_ms = tot;
+  if (launches) *launches = n;
+  return 0;
+}
+
 int slamgpu_descriptor_distance(const uint8_t* a, const uint8_t* b) {
   int dist = 0;
   for (int i = 0; i < 32; i++) dist += __builtin_popcount((unsigned)(a[i] ^ b[i]));
@@ -443,9 +518,6 @@ static int ensure_match_ws(slamgpu_ctx* c, int total_queries) {
   return 0;
 }
 
-static FrameKps left_views(const slamgpu_ctx* c) {
-  return FrameKps{c->out.kps, c->out.desc, c->out.nkps, 2 * (int64_t)c->geom.kp_cap, 2};
-}
 
 int slamgpu_search_by_projection_frame_device(slamgpu_ctx* c, const slamgpu_f2f_query* d_q,
                                               int total_queries, const int* d_q_start,
@@ -460,6 +532,7 @@ int slamgpu_search_by_projection_frame_device(slamgpu_ctx* c, const slamgpu_f2f_
   int rc = ensure_match_ws(c, total_queries);
   if (rc) return rc;
   MatchIO io{d_q_start, d_q_count, d_map_point, d_blocked, d_nmatches, mp_stride};
+  TimerScope ts(c);
   launch_search_frame(left_views(c), c->sout.u_right, c->geom.kp_cap, c->cam, c->gd(),
                       reinterpret_cast<const F2FQuery*>(d_q),
                       reinterpret_cast<const F2FPose*>(d_poses), n_frames, max_queries, c->gws,
@@ -480,6 +553,7 @@ int slamgpu_search_by_projection_mps_device(slamgpu_ctx* c, const slamgpu_mps_qu
   int rc = ensure_match_ws(c, total_queries);
   if (rc) return rc;
   MatchIO io{d_q_start, d_q_count, d_map_point, d_blocked, d_nmatches, mp_stride};
+  TimerScope ts(c);
   launch_search_mps(left_views(c), c->sout.u_right, c->geom.kp_cap, c->cam, c->gd(),
                     reinterpret_cast<const MpsQuery*>(d_q), nnratio, th, n_frames, max_queries,
                     c->gws, c->mws, io, pick_stream(c, stream));
@@ -527,6 +601,7 @@ static int host_search(slamgpu_ctx* c, int frame, const QT* queries, int nq, int
   gw.cell_start += (int64_t)frame * (kGridCells + 1);
   gw.cell_items += (int64_t)frame * kc;
   MatchIO io{c->d_qmeta, c->d_qmeta + 1, c->d_mp, c->d_blk, c->d_nm, kc};
+  TimerScope ts(c);
   if (f2f)
     launch_search_frame(cur, c->sout.u_right + frame * kc, kc, c->cam, c->gd(),
                         reinterpret_cast<const F2FQuery*>(qb),

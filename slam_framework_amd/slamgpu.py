@@ -41,6 +41,8 @@ EXPORTS = [
     "slamgpu_descriptor_distance", "slamgpu_search_by_projection_frame",
     "slamgpu_search_by_projection_mps", "slamgpu_search_by_projection_frame_device",
     "slamgpu_search_by_projection_mps_device", "slamgpu_debug_level_keys",
+    "slamgpu_make_vo_queries_device", "slamgpu_timing_start", "slamgpu_timing_stop",
+    "slamgpu_timing_read",
 ]
 
 
@@ -99,6 +101,10 @@ def lib():
         L.slamgpu_search_by_projection_mps_device.argtypes = [
             vp, vp, ip, vp, vp, ip, fp, ip, vp, vp, C.c_int64, vp, ip, vp]
         L.slamgpu_debug_level_keys.argtypes = [vp, ip, ip, ip, vp, ip, C.POINTER(ip)]
+        L.slamgpu_make_vo_queries_device.argtypes = [vp, vp, ip, vp, vp, vp, ip, vp]
+        L.slamgpu_timing_start.argtypes = [vp, C.c_char_p, ip]
+        L.slamgpu_timing_stop.argtypes = [vp, vp]
+        L.slamgpu_timing_read.argtypes = [vp, C.c_char_p, C.POINTER(C.c_double), C.POINTER(ip)]
         _lib = L
     return _lib
 
@@ -219,6 +225,32 @@ class Context:
         v = DeviceView()
         self.check(lib().slamgpu_device_results(self.h, C.byref(v)))
         return v
+
+    # ---- batched device path (torch CUDA tensors or raw device pointers) ----
+    def make_vo_queries_device(self, d_poses, blocks, d_queries, d_q_start, d_q_count, n_frames,
+                               stream=None):
+        self.check(lib().slamgpu_make_vo_queries_device(
+            self.h, _ptr(d_poses), blocks, _ptr(d_queries), _ptr(d_q_start), _ptr(d_q_count),
+            n_frames, C.c_void_p(stream or 0)))
+
+    def search_by_projection_frame_device(self, d_queries, total_queries, d_q_start, d_q_count,
+                                          max_queries, d_poses, d_map_point, d_blocked, mp_stride,
+                                          d_nmatches, n_frames, stream=None):
+        self.check(lib().slamgpu_search_by_projection_frame_device(
+            self.h, _ptr(d_queries), total_queries, _ptr(d_q_start), _ptr(d_q_count), max_queries,
+            _ptr(d_poses), _ptr(d_map_point), _ptr(d_blocked), mp_stride, _ptr(d_nmatches),
+            n_frames, C.c_void_p(stream or 0)))
+
+    def timing_start(self, kernel="*", max_launches=8192):
+        self.check(lib().slamgpu_timing_start(self.h, kernel.encode(), max_launches))
+
+    def timing_stop(self, stream=None):
+        self.check(lib().slamgpu_timing_stop(self.h, C.c_void_p(stream or 0)))
+
+    def timing_read(self, kernel):
+        ms, n = C.c_double(), C.c_int()
+        self.check(lib().slamgpu_timing_read(self.h, kernel.encode(), C.byref(ms), C.byref(n)))
+        return ms.value, n.value
 
     def search_by_projection_frame(self, frame, queries, pose, map_point, blocked):
         queries = np.ascontiguousarray(queries, dtype=F2F_QUERY_DTYPE)
