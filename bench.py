@@ -159,12 +159,11 @@ def main():
     t1 = time.perf_counter()
     ctx.timing_stop()
     ctx.sync()
-    elapsed = t1 - t0
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    from slam_framework_amd import dist as SD
+    elapsed = SD.max_over_ranks(t1 - t0, dev)
     dom_ms, dom_n = ctx.timing_read(dominant)
+    # per-rank result summary gathered to every rank (validation, outside the timed region)
+    summ = SD.gather_summary([int(nk.sum()), int(d_nm.sum().item()), int(d_qc.sum().item())], dev)
 
     frames = world * (B - 1) * args.steps
     value = frames / elapsed
@@ -204,6 +203,7 @@ def main():
             "roofline": roofline,
             "cpu_baseline": cpu,
             "kernel_ms_per_step": {n: round(brk[n][0], 4) for n in names},
+            "per_rank_matches_per_step": summ[:, 1].tolist(),
         }
         print(json.dumps(line))
     if world > 1:
