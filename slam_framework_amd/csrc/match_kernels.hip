@@ -550,12 +550,24 @@ __global__ __launch_bounds__(64) void search_resolve_kernel(
   uint8_t* blk = io.blocked + f * io.mp_stride;
   const int q0 = io.q_start[f], qn = io.q_count[f];
   int nm = 0;
-  for (int qi = 0; qi < qn; qi++) {
+  // queries are resolved in order; their kept candidates are staged through LDS in chunks
+  __shared__ uint64_t s_top[256 * kTopK];
+  __shared__ int s_nc[256];
+  for (int c0 = 0; c0 < qn; c0 += 256) {
+  const int cn = min(256, qn - c0);
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  for (int i = lane; i < cn * kTopK; i += 64) s_top[i] = mw.topk[(int64_t)(q0 + c0) * kTopK + i];
+  for (int i = lane; i < cn; i += 64) s_nc[i] = mw.ncand[q0 + c0 + i];
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  for (int qc = 0; qc < cn; qc++) {
+    const int qi = c0 + qc;
     const int q = q0 + qi;
-    const int nc = mw.ncand[q];
+    const int nc = s_nc[qc];
     if (lane == 0) mw.rot_bin[q] = -1;
     if (nc == 0) continue;
-    uint64_t key = (lane < kTopK) ? mw.topk[(int64_t)q * kTopK + lane] : kNoKey;
+    uint64_t key = (lane < kTopK) ? s_top[qc * kTopK + lane] : kNoKey;
     bool ok = key != kNoKey && !((claimed[key_idx(key) >> 5] >> (key_idx(key) & 31)) & 1u);
     uint64_t msk = __ballot(ok);
     uint64_t b1 = kNoKey, b2 = kNoKey;
@@ -612,6 +624,7 @@ __global__ __launch_bounds__(64) void search_resolve_kernel(
     }
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  }
   }
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
   __builtin_amdgcn_wave_barrier();

@@ -177,7 +177,7 @@ int compute_geometry(const OrbParams& p, int cols, int rows, OrbGeom* g,
     boff += (int64_t)L.pitch * L.h;
     boff = (boff + 255) & ~(int64_t)255;
     L.blur_tile_base = btiles;
-    btiles += ((L.w + 63) / 64) * ((L.h + 15) / 16);
+    btiles += ((L.w + 255) / 256) * ((L.h + 127) / 128);  // blur7 tiles: 256 x 128
   }
   g->blur_bytes = boff;
   g->blur_tiles = btiles;

@@ -39,7 +39,7 @@ struct LevelGeom {
   int out_cap;          // max keypoints this level can emit
   // resize tables (level >= 1) in the shared table buffer
   int rx_base, ry_base; // offsets into the x (per dst column) / y (per dst row) tables
-  int blur_tile_base;   // first 64x16 blur tile of this level
+  int blur_tile_base;   // first 256x128 blur tile of this level
   int xmax;             // first dst column that copies S[sx] * 2048 (resize HResizeLinear)
   float scale, inv_scale;
   float patch_size;     // (float)(int)(PATCH_SIZE * scale) (:778)
@@ -52,7 +52,7 @@ struct OrbGeom {
   int cell_cap;          // max FAST survivors stored per cell
   int64_t pyr_bytes;     // bytes of one image's pyramid (levels >= 1) buffer
   int64_t blur_bytes;    // bytes of one image's blurred pyramid (levels >= 0) buffer
-  int blur_tiles;        // 64x16 blur tiles over all levels of one image
+  int blur_tiles;        // 256x128 blur tiles over all levels of one image
   int gauss[7];          // GaussianBlur 7x7 sigma 2 integer kernel (x256)
   int64_t keys_per_image;
   int64_t nodes_per_image;

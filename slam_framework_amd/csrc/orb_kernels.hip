@@ -42,17 +42,19 @@ __global__ __launch_bounds__(256) void pyr_down_kernel(ImageBatch b, const OrbGe
                                                        int level,
                                                        const ResizeX* __restrict__ rxt,
                                                        const ResizeY* __restrict__ ryt) {
-  const int img = blockIdx.z;
-  const int dy = blockIdx.y;
+  const int img = blockIdx.y;
   const LevelGeom& D = g->lv[level];
+  const int groups = (D.w + 3) >> 2;  // 4-pixel groups per row; flattened over (row, group)
+  const int item = blockIdx.x * blockDim.x + threadIdx.x;
+  const int dy = item / groups;
+  if (dy >= D.h) return;
+  const int x0 = (item - dy * groups) * 4;
   int spitch;
   const uint8_t* src = level_ptr(b, g, img, level - 1, &spitch);
   uint8_t* dst = b.pyr + (int64_t)img * g->pyr_bytes + D.offset + (int64_t)dy * D.pitch;
   const ResizeY ey = ryt[D.ry_base + dy];
   const uint8_t* S0 = src + (int64_t)ey.y0 * spitch;
   const uint8_t* S1 = src + (int64_t)ey.y1 * spitch;
-  const int x0 = (blockIdx.x * blockDim.x + threadIdx.x) * 4;
-  if (x0 >= D.w) return;
   uint32_t packed = 0;
 #pragma unroll
   for (int k = 0; k < 4; k++) {
@@ -83,52 +85,90 @@ __global__ __launch_bounds__(256) void pyr_down_kernel(ImageBatch b, const OrbGe
 // blur7: Compute (:1029-1030) clone + GaussianBlur(7x7, 2, 2, BORDER_REFLECT_101) per level.
 // Row pass: exact int sums over the reflect-101 extended row. Column pass: OpenCV 3.3.1's
 // SymmColumnVec_32s8u covers x < w - w%4 and rounds V/65536 half-to-even; the scalar tail rounds
-// (V + 32768) >> 16. A 256-thread block produces a 64x16 tile.
+// (V + 32768) >> 16. Each thread owns 4 adjacent columns of a 32-row strip and slides a 7-row
+// window of row sums down it in registers (one aligned 12-byte read per input row, no LDS);
+// a 256-thread block covers 256 columns x 128 rows.
 __device__ __forceinline__ int reflect101(int i, int n) {
   if (i < 0) i = -i;
   if (i >= n) i = 2 * n - 2 - i;
   return i;
 }
 
+constexpr int kBlurTileW = 256, kBlurTileH = 128, kBlurStrip = 32;
+
 __global__ __launch_bounds__(256) void blur7_kernel(ImageBatch b, const OrbGeom* __restrict__ g) {
-  __shared__ uint8_t tin[22][72];
-  __shared__ int th[22][64];
   const int img = blockIdx.y;
   int tile = blockIdx.x;
   int level = 0;
   while (level + 1 < g->nlevels && tile >= g->lv[level + 1].blur_tile_base) level++;
   const LevelGeom& L = g->lv[level];
   tile -= L.blur_tile_base;
-  const int tiles_x = (L.w + 63) / 64;
-  const int tx0 = (tile % tiles_x) * 64, ty0 = (tile / tiles_x) * 16;
+  const int tiles_x = (L.w + kBlurTileW - 1) / kBlurTileW;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int x = (tile % tiles_x) * kBlurTileW + 4 * lane;
+  const int y0 = (tile / tiles_x) * kBlurTileH + wid * kBlurStrip;
+  if (x >= L.w || y0 >= L.h) return;
   int spitch;
   const uint8_t* src = level_ptr(b, g, img, level, &spitch);
   uint8_t* dst = b.blur + (int64_t)img * g->blur_bytes + L.blur_offset;
-  const int t = threadIdx.x;
-  for (int i = t; i < 22 * 70; i += 256) {
-    const int r = i / 70, c = i % 70;
-    const int sy = reflect101(ty0 - 3 + r, L.h), sx = reflect101(tx0 - 3 + c, L.w);
-    tin[r][c] = src[(int64_t)sy * spitch + sx];
-  }
-  __syncthreads();
+  const int w = L.w, h = L.h;
+  const bool fast = x >= 4 && x + 8 <= w && (((uintptr_t)src | (uintptr_t)spitch) & 3) == 0;
   const int k0 = g->gauss[0], k1 = g->gauss[1], k2 = g->gauss[2], k3 = g->gauss[3];
-  for (int i = t; i < 22 * 64; i += 256) {
-    const int r = i >> 6, c = i & 63;
-    const uint8_t* p = &tin[r][c];
-    th[r][c] = k3 * p[3] + k2 * (p[2] + p[4]) + k1 * (p[1] + p[5]) + k0 * (p[0] + p[6]);
-  }
-  __syncthreads();
-  const int xvec = L.w - (L.w % 4);
-  const int c = t & 63;
-  const int x = tx0 + c;
-  for (int r = t >> 6; r < 16; r += 4) {
-    const int y = ty0 + r;
-    if (y >= L.h || x >= L.w) continue;
-    const int v = k3 * th[r + 3][c] + k2 * (th[r + 2][c] + th[r + 4][c]) +
-                  k1 * (th[r + 1][c] + th[r + 5][c]) + k0 * (th[r][c] + th[r + 6][c]);
-    int o = (x < xvec) ? (int)rintf((float)v * (1.0f / 65536.0f)) : ((v + 32768) >> 16);
-    o = o < 0 ? 0 : (o > 255 ? 255 : o);
-    dst[(int64_t)y * L.pitch + x] = (uint8_t)o;
+  const bool vec_round = x < w - (w % 4);  // whole 4-column group on one side of xvec
+  const int y1 = min(y0 + kBlurStrip, h);
+  int ring[7][4];
+  // input rows y0-3 .. y1+2; output row r-3 once 7 rows are in the ring
+  for (int r0 = y0 - 3; r0 < y1 + 3; r0 += 7) {
+#pragma unroll
+    for (int k = 0; k < 7; k++) {
+      const int r = r0 + k;
+      if (r < y1 + 3) {
+        const uint8_t* row = src + (int64_t)reflect101(r, h) * spitch;
+        int px[10];  // columns x-3 .. x+6
+        if (fast) {
+          const uint32_t w0 = *reinterpret_cast<const uint32_t*>(row + x - 4);
+          const uint32_t w1 = *reinterpret_cast<const uint32_t*>(row + x);
+          const uint32_t w2 = *reinterpret_cast<const uint32_t*>(row + x + 4);
+          px[0] = (w0 >> 8) & 0xff;
+          px[1] = (w0 >> 16) & 0xff;
+          px[2] = w0 >> 24;
+          px[3] = w1 & 0xff;
+          px[4] = (w1 >> 8) & 0xff;
+          px[5] = (w1 >> 16) & 0xff;
+          px[6] = w1 >> 24;
+          px[7] = w2 & 0xff;
+          px[8] = (w2 >> 8) & 0xff;
+          px[9] = (w2 >> 16) & 0xff;
+        } else {
+#pragma unroll
+          for (int i = 0; i < 10; i++) px[i] = row[reflect101(x - 3 + i, w)];
+        }
+#pragma unroll
+        for (int j = 0; j < 4; j++)
+          ring[k][j] = k3 * px[j + 3] + k2 * (px[j + 2] + px[j + 4]) +
+                       k1 * (px[j + 1] + px[j + 5]) + k0 * (px[j] + px[j + 6]);
+        const int yo = r - 3;  // output row whose window ends at input row r
+        if (yo >= y0) {
+          uint32_t packed = 0;
+#pragma unroll
+          for (int j = 0; j < 4; j++) {
+            const int v = k3 * ring[(k + 4) % 7][j] +
+                          k2 * (ring[(k + 3) % 7][j] + ring[(k + 5) % 7][j]) +
+                          k1 * (ring[(k + 2) % 7][j] + ring[(k + 6) % 7][j]) +
+                          k0 * (ring[(k + 1) % 7][j] + ring[k][j]);
+            int o = vec_round ? (int)rintf((float)v * (1.0f / 65536.0f)) : ((v + 32768) >> 16);
+            o = o < 0 ? 0 : (o > 255 ? 255 : o);
+            packed |= (uint32_t)o << (8 * j);
+          }
+          uint8_t* drow = dst + (int64_t)yo * L.pitch;
+          if (x + 4 <= w) {
+            *reinterpret_cast<uint32_t*>(drow + x) = packed;
+          } else {
+            for (int j = 0; x + j < w; j++) drow[x + j] = (uint8_t)(packed >> (8 * j));
+          }
+        }
+      }
+    }
   }
 }
 
@@ -141,13 +181,15 @@ __global__ __launch_bounds__(256) void blur7_kernel(ImageBatch b, const OrbGeom*
 // NMS is strict '>' against the 8 neighbours' scores at that t, zero outside the detect area
 // (cell-local, as cv::FAST sees only the cell view). Survivors are written in row-major order.
 constexpr int kCellWaves = 4;
-constexpr int kTileStride = 68;   // >= max view width (wCell + 6 <= 66)
+constexpr int kTileStride = 72;   // >= max view width + 3 alignment bytes (wCell + 6 + 3 <= 69)
 constexpr int kTileRows = 66;
 constexpr int kScoreStride = 64;  // >= max detect width
 constexpr int kScoreRows = 60;
+constexpr int kCandCap = kScoreStride * kScoreRows;
 
+// max over the 16 contiguous 9-arcs of min(v - ring) ("darker" strength) and of min(ring - v)
+// ("brighter"); p is a FAST-9 corner at threshold t iff the result is > t.
 __device__ __forceinline__ int fast_s(const uint8_t* t, int o) {
-  // ring offsets (dx, dy) of makeOffsets(16) in tile coordinates
   const int v = t[o];
   int d[16];
   d[0] = v - t[o + 3 * kTileStride];
@@ -181,12 +223,26 @@ __device__ __forceinline__ int fast_s(const uint8_t* t, int o) {
   int sd = -1024, sb = 1024;
 #pragma unroll
   for (int k = 0; k < 16; k++) {
-    const int mn9 = min(min(mn4[k], mn4[(k + 4) & 15]), d[(k + 8) & 15]);
-    const int mx9 = max(max(mx4[k], mx4[(k + 4) & 15]), d[(k + 8) & 15]);
-    sd = max(sd, mn9);   // darker ring: v - p > t along the arc
-    sb = min(sb, mx9);   // brighter ring: p - v > t  <=>  max(v - p) < -t
+    sd = max(sd, min(min(mn4[k], mn4[(k + 4) & 15]), d[(k + 8) & 15]));
+    sb = min(sb, max(max(mx4[k], mx4[(k + 4) & 15]), d[(k + 8) & 15]));
   }
   return max(sd, -sb);
+}
+
+// Exact necessary condition for a corner at threshold t: every 9-arc of the 16-ring contains
+// one pixel of each opposite pair (0,8), (4,12), (2,10), (6,14) -- FAST_t's own pre-test.
+__device__ __forceinline__ bool fast_maybe(const uint8_t* t, int o, int th) {
+  const int v = t[o];
+  const int lo = v - th, hi = v + th;
+  const int p0 = t[o + 3 * kTileStride], p8 = t[o - 3 * kTileStride];
+  const int p4 = t[o + 3], p12 = t[o - 3];
+  const int p2 = t[o + 2 + 2 * kTileStride], p10 = t[o - 2 - 2 * kTileStride];
+  const int p6 = t[o + 2 - 2 * kTileStride], p14 = t[o - 2 + 2 * kTileStride];
+  const bool dark = (p0 < lo || p8 < lo) && (p4 < lo || p12 < lo) && (p2 < lo || p10 < lo) &&
+                    (p6 < lo || p14 < lo);
+  const bool bright = (p0 > hi || p8 > hi) && (p4 > hi || p12 > hi) && (p2 > hi || p10 > hi) &&
+                      (p6 > hi || p14 > hi);
+  return dark || bright;
 }
 
 __global__ __launch_bounds__(256) void fast_cells_kernel(ImageBatch b,
@@ -194,8 +250,9 @@ __global__ __launch_bounds__(256) void fast_cells_kernel(ImageBatch b,
                                                          uint32_t* __restrict__ cell_keys,
                                                          int* __restrict__ cell_count,
                                                          uint32_t* __restrict__ err) {
-  __shared__ uint8_t s_tile[kCellWaves][kTileRows * kTileStride];
-  __shared__ uint8_t s_score[kCellWaves][kScoreRows * kScoreStride];
+  __shared__ __attribute__((aligned(16))) uint8_t s_tile[kCellWaves][kTileRows * kTileStride];
+  __shared__ __attribute__((aligned(16))) uint8_t s_score[kCellWaves][kScoreRows * kScoreStride];
+  __shared__ uint16_t s_cand[kCellWaves][kCandCap];
   const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int img = blockIdx.y;
   const int cell = blockIdx.x * kCellWaves + wid;
@@ -219,26 +276,69 @@ __global__ __launch_bounds__(256) void fast_cells_kernel(ImageBatch b,
   const int vh = maxY - iniY, vw = maxX - iniX;
   const int dh = vh - 6, dw = vw - 6;  // detect area [3, vh-3) x [3, vw-3)
   int pitch;
-  const uint8_t* src = level_ptr(b, g, img, level, &pitch) + (int64_t)iniY * pitch + iniX;
+  const uint8_t* base = level_ptr(b, g, img, level, &pitch);
   uint8_t* tile = s_tile[wid];
   uint8_t* sc = s_score[wid];
-  for (int r = 0; r < vh; r++)
-    for (int x = lane; x < vw; x += 64) tile[r * kTileStride + x] = src[(int64_t)r * pitch + x];
+  uint16_t* cand = s_cand[wid];
+  // ---- tile load: aligned dwords covering [iniX & ~3, maxX), all issued before any LDS store
+  const int ax = iniX & ~3, off = iniX - ax;
+  const int nd = (vw + off + 3) >> 2;  // dwords per row (<= 18)
+  const int total = nd * vh;
+  const bool aligned = (((uintptr_t)base | (uintptr_t)pitch) & 3) == 0;
+  if (aligned) {
+    constexpr int kMaxPer = (18 * kTileRows + 63) / 64;
+    uint32_t v[kMaxPer];
+#pragma unroll
+    for (int k = 0; k < kMaxPer; k++) {
+      const int i = lane + 64 * k;
+      if (i < total) {
+        const int r = i / nd, q = i - r * nd;
+        v[k] = *reinterpret_cast<const uint32_t*>(base + (int64_t)(iniY + r) * pitch + ax + 4 * q);
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < kMaxPer; k++) {
+      const int i = lane + 64 * k;
+      if (i < total) {
+        const int r = i / nd, q = i - r * nd;
+        *reinterpret_cast<uint32_t*>(tile + r * kTileStride + 4 * q) = v[k];
+      }
+    }
+  } else {
+    for (int r = 0; r < vh; r++)
+      for (int x = lane; x < vw + off; x += 64)
+        tile[r * kTileStride + x] = base[(int64_t)(iniY + r) * pitch + ax + x];
+  }
+  // zero the score map (dwords)
+  for (int i = lane; i < kScoreRows * kScoreStride / 4; i += 64)
+    reinterpret_cast<uint32_t*>(sc)[i] = 0;
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-  // score map; rows are processed 64/w_pad at a time so lanes map to (row, col) without division
+  // ---- prefilter every detect pixel at the lower threshold; compact survivors (row-major)
+  const int tmin = min(g->ini_th, g->min_th);
   const int wpad = dw <= 32 ? 32 : 64;
   const int rows_per = 64 / wpad;
   const int lr = lane / wpad, lc = lane % wpad;
-  int smax = 0;
+  int ncand = 0;
   for (int r0 = 0; r0 < dh; r0 += rows_per) {
     const int r = r0 + lr;
-    if (r < dh && lc < dw) {
-      const int s = fast_s(tile, (r + 3) * kTileStride + lc + 3);
-      const int sv = s < 0 ? 0 : s;
-      sc[r * kScoreStride + lc] = (uint8_t)sv;
-      smax = max(smax, sv);
-    }
+    const bool in = r < dh && lc < dw;
+    const bool maybe = in && fast_maybe(tile, (r + 3) * kTileStride + lc + 3 + off, tmin);
+    const uint64_t m = __ballot(maybe);
+    if (maybe) cand[ncand + lanes_below(m)] = (uint16_t)(r * kScoreStride + lc);
+    ncand += __popcll(m);
+  }
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  // ---- exact FAST score of the survivors
+  int smax = 0;
+  for (int i = lane; i < ncand; i += 64) {
+    const int pix = cand[i];
+    const int r = pix / kScoreStride, cc = pix % kScoreStride;
+    const int s = fast_s(tile, (r + 3) * kTileStride + cc + 3 + off);
+    const int sv = s < 0 ? 0 : s;
+    sc[pix] = (uint8_t)sv;
+    smax = max(smax, sv);
   }
   smax = wave_max(smax);
   __builtin_amdgcn_wave_barrier();
@@ -246,15 +346,19 @@ __global__ __launch_bounds__(256) void fast_cells_kernel(ImageBatch b,
   uint32_t* out = cell_keys + slot * g->cell_cap;
   // FAST at iniTh; the reference re-runs at minTh when the iniTh *output* (after NMS) is empty
   // (:753-757) -- corners can exist at iniTh and still all be suppressed by equal neighbours.
+  // Non-survivors of the prefilter have s <= tmin: never corners, score 0 for NMS.
   int count = 0;
   for (int pass = (smax > g->ini_th) ? 0 : 1; pass < 2 && count == 0; pass++) {
     const int th = pass == 0 ? g->ini_th : g->min_th;
-    for (int r0 = 0; r0 < dh; r0 += rows_per) {
-      const int r = r0 + lr;
+    for (int i0 = 0; i0 < ncand; i0 += 64) {
+      const int i = i0 + lane;
       bool keep = false;
-      int s = 0;
-      if (r < dh && lc < dw) {
-        s = sc[r * kScoreStride + lc];
+      int s = 0, r = 0, cc = 0;
+      if (i < ncand) {
+        const int pix = cand[i];
+        r = pix / kScoreStride;
+        cc = pix % kScoreStride;
+        s = sc[pix];
         if (s > th) {
           const int score = s - 1;
           keep = true;
@@ -263,10 +367,10 @@ __global__ __launch_bounds__(256) void fast_cells_kernel(ImageBatch b,
 #pragma unroll
             for (int dx = -1; dx <= 1; dx++) {
               if (dx == 0 && dy == 0) continue;
-              const int rr = r + dy, cc = lc + dx;
+              const int rr = r + dy, c2 = cc + dx;
               int ns = 0;
-              if (rr >= 0 && rr < dh && cc >= 0 && cc < dw) {
-                const int q = sc[rr * kScoreStride + cc];
+              if (rr >= 0 && rr < dh && c2 >= 0 && c2 < dw) {
+                const int q = sc[rr * kScoreStride + c2];
                 ns = q > th ? q - 1 : 0;
               }
               keep = keep && (score > ns);
@@ -277,7 +381,7 @@ __global__ __launch_bounds__(256) void fast_cells_kernel(ImageBatch b,
       if (keep) {
         const int pos = count + lanes_below(m);
         if (pos < g->cell_cap) {
-          const int x_rel = iniX + 3 + lc - kMinBorder, y_rel = iniY + 3 + r - kMinBorder;
+          const int x_rel = iniX + 3 + cc - kMinBorder, y_rel = iniY + 3 + r - kMinBorder;
           out[pos] = pack_key(x_rel, y_rel, s - 1);
         }
       }
@@ -785,11 +889,66 @@ __global__ __launch_bounds__(256) void orient_desc_kernel(
   const int x = key_x(key) + kMinBorder, y = key_y(key) + kMinBorder;
   int pitch;
   const uint8_t* im = level_ptr(b, g, img, level, &pitch);
-  const uint8_t* center = im + (int64_t)y * pitch + x;
+  const uint8_t* bl = b.blur + (int64_t)img * g->blur_bytes + L.blur_offset;
+  const int bp = L.pitch;
+  // stage the 31x31 patch (IC_Angle) and the 37x37 blurred window (rBRIEF samples reach
+  // |offset| <= 18) into LDS with aligned dword loads
+  __shared__ __attribute__((aligned(16))) uint8_t s_raw[4][31 * 36];
+  __shared__ __attribute__((aligned(16))) uint8_t s_blur[4][37 * 40];
+  uint8_t* raw = s_raw[threadIdx.x >> 6];
+  uint8_t* blr = s_blur[threadIdx.x >> 6];
+  const int rx0 = (x - 15) & ~3, roff = x - 15 - rx0;  // raw patch column origin
+  const int bx0 = (x - 18) & ~3, boff = x - 18 - bx0;  // blurred window column origin
+  if ((((uintptr_t)im | (uintptr_t)pitch) & 3) == 0) {
+    uint32_t v[5];
+#pragma unroll
+    for (int k = 0; k < 5; k++) {
+      const int i = lane + 64 * k;
+      if (i < 31 * 9) {
+        const int r = i / 9, q = i - r * 9;
+        v[k] = *reinterpret_cast<const uint32_t*>(im + (int64_t)(y - 15 + r) * pitch + rx0 + 4 * q);
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < 5; k++) {
+      const int i = lane + 64 * k;
+      if (i < 31 * 9) {
+        const int r = i / 9, q = i - r * 9;
+        *reinterpret_cast<uint32_t*>(raw + r * 36 + 4 * q) = v[k];
+      }
+    }
+  } else {
+    for (int i = lane; i < 31 * 36; i += 64) {
+      const int r = i / 36, q = i - r * 36;
+      raw[i] = im[(int64_t)(y - 15 + r) * pitch + rx0 + q];
+    }
+  }
+  {
+    uint32_t v[6];
+#pragma unroll
+    for (int k = 0; k < 6; k++) {
+      const int i = lane + 64 * k;
+      if (i < 37 * 10) {
+        const int r = i / 10, q = i - r * 10;
+        v[k] = *reinterpret_cast<const uint32_t*>(bl + (int64_t)(y - 18 + r) * bp + bx0 + 4 * q);
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < 6; k++) {
+      const int i = lane + 64 * k;
+      if (i < 37 * 10) {
+        const int r = i / 10, q = i - r * 10;
+        *reinterpret_cast<uint32_t*>(blr + r * 40 + 4 * q) = v[k];
+      }
+    }
+  }
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  const uint8_t* center = raw + 15 * 36 + 15 + roff;
   int m10 = 0, m01 = 0;
   for (int i = lane; i < kDiscPixels; i += 64) {
     const int2 uv = disc[i];
-    const int v = center[uv.y * pitch + uv.x];
+    const int v = center[uv.y * 36 + uv.x];
     m10 += uv.x * v;
     m01 += uv.y * v;
   }
@@ -800,9 +959,8 @@ __global__ __launch_bounds__(256) void orient_desc_kernel(
   float sa, ca;
   glibc_sincosf(angle * factorPI, &sa, &ca);
   const float a = ca, bb = sa;
-  const uint8_t* bl = b.blur + (int64_t)img * g->blur_bytes + L.blur_offset;
-  const int bp = L.pitch;
-  const uint8_t* bc = bl + (int64_t)y * bp + x;
+  const uint8_t* bc = blr + 18 * 40 + 18 + boff;
+  constexpr int bpl = 40;
   uint64_t words[4];
 #pragma unroll
   for (int r = 0; r < 4; r++) {
@@ -813,8 +971,8 @@ __global__ __launch_bounds__(256) void orient_desc_kernel(
     const int rx0 = cv_round(fmaf(px0, a, -(py0 * bb)));
     const int ry1 = cv_round(fmaf(px1, bb, py1 * a));
     const int rx1 = cv_round(fmaf(px1, a, -(py1 * bb)));
-    const int v0 = bc[ry0 * bp + rx0];
-    const int v1 = bc[ry1 * bp + rx1];
+    const int v0 = bc[ry0 * bpl + rx0];
+    const int v1 = bc[ry1 * bpl + rx1];
     words[r] = __ballot(v0 < v1);
   }
   const int64_t o = (int64_t)img * g->kp_cap + off + idx;
@@ -847,8 +1005,8 @@ __global__ __launch_bounds__(256) void orient_desc_kernel(
 void launch_extract(const ImageBatch& b, const OrbGeomDev& gd, int n_images, hipStream_t st) {
   const OrbGeom& g = *gd.host;
   for (int l = 1; l < g.nlevels; l++) {
-    const int w = g.lv[l].w, h = g.lv[l].h;
-    dim3 grid((w + 1023) / 1024, h, n_images);
+    const int items = ((g.lv[l].w + 3) / 4) * g.lv[l].h;
+    dim3 grid((items + 255) / 256, n_images);
     SLAMGPU_LAUNCH("pyr_down", st, pyr_down_kernel, grid, dim3(256), 0, st, b, gd.dev, l, gd.rx, gd.ry);
   }
   SLAMGPU_LAUNCH("blur7", st, blur7_kernel, dim3(g.blur_tiles, n_images), dim3(256), 0, st, b, gd.dev);
