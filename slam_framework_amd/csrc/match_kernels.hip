@@ -548,17 +548,36 @@ __global__ __launch_bounds__(64) void search_resolve_kernel(
   F.blocked = io.blocked + f * io.mp_stride;
   int* mp = io.map_point + f * io.mp_stride;
   uint8_t* blk = io.blocked + f * io.mp_stride;
+  bool check_ori = false;
+  if constexpr (kF2F) check_ori = poses[f].check_ori != 0;
   const int q0 = io.q_start[f], qn = io.q_count[f];
   int nm = 0;
-  // queries are resolved in order; their kept candidates are staged through LDS in chunks
+  // queries are resolved in order; everything the sequential loop reads (kept candidates,
+  // query identity, keypoint angle/octave) is staged through LDS so the loop has no global loads
   __shared__ uint64_t s_top[256 * kTopK];
   __shared__ int s_nc[256];
+  __shared__ int s_mpid[256];
+  __shared__ float s_qang[256];
+  __shared__ float s_kang[4096];
+  __shared__ int8_t s_koct[4096];
+  for (int i = lane; i < n; i += 64) {
+    const KeyPoint kp = F.kps[i];
+    s_kang[i] = kp.angle;
+    s_koct[i] = (int8_t)kp.octave;
+  }
   for (int c0 = 0; c0 < qn; c0 += 256) {
   const int cn = min(256, qn - c0);
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
   __builtin_amdgcn_wave_barrier();
   for (int i = lane; i < cn * kTopK; i += 64) s_top[i] = mw.topk[(int64_t)(q0 + c0) * kTopK + i];
-  for (int i = lane; i < cn; i += 64) s_nc[i] = mw.ncand[q0 + c0 + i];
+  for (int i = lane; i < cn; i += 64) {
+    s_nc[i] = mw.ncand[q0 + c0 + i];
+    const Q& qq = queries[q0 + c0 + i];
+    s_mpid[i] = (qq.mp_id & 0x7fffffff) | (qq.blocks ? (int)0x80000000u : 0);
+    float ang = 0.f;
+    if constexpr (kF2F) ang = qq.last_angle;
+    s_qang[i] = ang;
+  }
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
   __builtin_amdgcn_wave_barrier();
   for (int qc = 0; qc < cn; qc++) {
@@ -596,21 +615,22 @@ __global__ __launch_bounds__(64) void search_resolve_kernel(
     if (bestDist > TH_HIGH) continue;
     const int idx = key_idx(b1);
     if constexpr (!kF2F) {
-      const int bestLevel = F.kps[idx].octave;
+      const int bestLevel = s_koct[idx];
       const int bestDist2 = b2 == kNoKey ? 256 : key_dist(b2);
-      const int bestLevel2 = b2 == kNoKey ? -1 : F.kps[key_idx(b2)].octave;
+      const int bestLevel2 = b2 == kNoKey ? -1 : s_koct[key_idx(b2)];
       if (bestLevel == bestLevel2 && (float)bestDist > nnratio * (float)bestDist2) continue;
     }
-    const Q& qq = queries[q];
+    const int mpw = s_mpid[qc];
+    const bool qblocks = mpw < 0;
     if (lane == 0) {
-      mp[idx] = qq.mp_id;
-      blk[idx] = qq.blocks ? 1 : 0;
-      if (qq.blocks) claimed[idx >> 5] |= 1u << (idx & 31);
+      mp[idx] = mpw & 0x7fffffff;
+      blk[idx] = qblocks ? 1 : 0;
+      if (qblocks) claimed[idx >> 5] |= 1u << (idx & 31);
     }
     nm++;
     if constexpr (kF2F) {
-      if (poses[f].check_ori) {
-        float rot = qq.last_angle - F.kps[idx].angle;
+      if (check_ori) {
+        float rot = s_qang[qc] - s_kang[idx];
         if (rot < 0.0f) rot += 360.0f;
         const float factor = 1.0f / HISTO_LENGTH;
         int bin = (int)roundf(rot * factor);
@@ -629,7 +649,7 @@ __global__ __launch_bounds__(64) void search_resolve_kernel(
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
   __builtin_amdgcn_wave_barrier();
   if constexpr (kF2F) {
-    if (poses[f].check_ori) {
+    if (check_ori) {
       // ComputeThreeMaxima (orb_matcher.cpp:1584-1625)
       int max1 = 0, max2 = 0, max3 = 0, ind1 = -1, ind2 = -1, ind3 = -1;
       for (int i = 0; i < HISTO_LENGTH; i++) {

@@ -184,6 +184,22 @@ int compute_geometry(const OrbParams& p, int cols, int rows, OrbGeom* g,
   gauss_kernel_int(g->gauss);
   // strict 8-neighbour NMS keeps at most one pixel per 2x2 block of the detect area
   g->cell_cap = ((max_wcell + 1) / 2) * ((max_hcell + 1) / 2);
+  g->fast_tile_stride = round_up(max_wcell + 6 + 3, 4);
+  g->fast_tile_rows = max_hcell + 6;
+  g->fast_score_stride = max_wcell;
+  g->fast_score_rows = max_hcell;
+  g->fast_lds_per_wave = round_up(g->fast_tile_stride * g->fast_tile_rows, 16) +
+                         round_up(g->fast_score_stride * g->fast_score_rows, 16) +
+                         round_up(2 * g->fast_score_stride * g->fast_score_rows, 16);
+  if (max_wcell > 64) return -4;
+  // pyr_down stages the source rows of 4 output rows (kPyrBand) in <= 16 LDS rows
+  for (int l = 1; l < p.nlevels; l++) {
+    const LevelGeom& L = g->lv[l];
+    for (int dy0 = 0; dy0 < L.h; dy0 += 4) {
+      const int dy1 = std::min(dy0 + 4, L.h);
+      if ((*ry)[L.ry_base + dy1 - 1].y1 - (*ry)[L.ry_base + dy0].y0 + 1 > 16) return -5;
+    }
+  }
   g->pyr_bytes = pyr_off;
   int64_t key_off = 0, node_off = 0;
   int out_off = 0;

@@ -50,6 +50,10 @@ struct OrbGeom {
   int nfeatures, ini_th, min_th;
   int cells_per_image;
   int cell_cap;          // max FAST survivors stored per cell
+  // fast_cells LDS layout per wave (sized from the largest cell of this configuration)
+  int fast_tile_stride, fast_tile_rows;    // cell view + 3 alignment bytes
+  int fast_score_stride, fast_score_rows;  // detect area
+  int fast_lds_per_wave;                   // bytes (tile + score + u16 candidate list)
   int64_t pyr_bytes;     // bytes of one image's pyramid (levels >= 1) buffer
   int64_t blur_bytes;    // bytes of one image's blurred pyramid (levels >= 0) buffer
   int blur_tiles;        // 256x128 blur tiles over all levels of one image

@@ -37,47 +37,91 @@ __device__ __forceinline__ const uint8_t* level_ptr(const ImageBatch& b, const O
 // ---------------------------------------------------------------------------------------
 // pyr_down: ComputePyramid (:1051-1075) -> cv::resize(level l-1, level l, INTER_LINEAR).
 // HResizeLinear (int = S[sx]*a0 + S[sx+1]*a1, or S[sx]*2048 from xmax on) then VResizeLinear
-// ((b0*(r0>>4))>>16) + ((b1*(r1>>4))>>16) + 2) >> 2. Each thread produces 4 adjacent pixels.
+// ((b0*(r0>>4))>>16) + ((b1*(r1>>4))>>16) + 2) >> 2. A block produces a band of kPyrBand output
+// rows: the source rows it needs are staged into LDS with coalesced dword loads, then every
+// thread produces 4 adjacent output pixels per row from LDS.
+constexpr int kPyrBand = 4;
+constexpr int kPyrSrcRows = 16;  // source rows staged per band (host checks the scale fits)
+
 __global__ __launch_bounds__(256) void pyr_down_kernel(ImageBatch b, const OrbGeom* __restrict__ g,
                                                        int level,
                                                        const ResizeX* __restrict__ rxt,
                                                        const ResizeY* __restrict__ ryt) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t s_src[];
   const int img = blockIdx.y;
   const LevelGeom& D = g->lv[level];
-  const int groups = (D.w + 3) >> 2;  // 4-pixel groups per row; flattened over (row, group)
-  const int item = blockIdx.x * blockDim.x + threadIdx.x;
-  const int dy = item / groups;
-  if (dy >= D.h) return;
-  const int x0 = (item - dy * groups) * 4;
+  const LevelGeom& S = g->lv[level - 1];
+  const int dy0 = blockIdx.x * kPyrBand;
+  const int dy1 = min(dy0 + kPyrBand, D.h);
+  const int sy_lo = ryt[D.ry_base + dy0].y0;
+  const int sy_hi = ryt[D.ry_base + dy1 - 1].y1;
+  const int nsr = sy_hi - sy_lo + 1;
+  const int sstride = (S.w + 3) & ~3;
   int spitch;
   const uint8_t* src = level_ptr(b, g, img, level - 1, &spitch);
-  uint8_t* dst = b.pyr + (int64_t)img * g->pyr_bytes + D.offset + (int64_t)dy * D.pitch;
-  const ResizeY ey = ryt[D.ry_base + dy];
-  const uint8_t* S0 = src + (int64_t)ey.y0 * spitch;
-  const uint8_t* S1 = src + (int64_t)ey.y1 * spitch;
-  uint32_t packed = 0;
+  const int tid = threadIdx.x;
+  const int nd = sstride >> 2;
+  if ((((uintptr_t)src | (uintptr_t)spitch) & 3) == 0) {
+    // issue 8 dword loads per thread before the first LDS store (memory-level parallelism)
+    for (int i0 = tid; i0 < nsr * nd; i0 += 8 * 256) {
+      uint32_t v[8];
 #pragma unroll
-  for (int k = 0; k < 4; k++) {
-    const int dx = x0 + k;
-    int v = 0;
-    if (dx < D.w) {
-      const ResizeX ex = rxt[D.rx_base + dx];
-      int r0, r1;
-      if (dx < D.xmax) {
-        r0 = S0[ex.sx] * ex.a0 + S0[ex.sx + 1] * ex.a1;
-        r1 = S1[ex.sx] * ex.a0 + S1[ex.sx + 1] * ex.a1;
-      } else {
-        r0 = S0[ex.sx] * 2048;
-        r1 = S1[ex.sx] * 2048;
+      for (int k = 0; k < 8; k++) {
+        const int i = i0 + 256 * k;
+        if (i < nsr * nd) {
+          const int r = i / nd, q = i - r * nd;
+          v[k] = *reinterpret_cast<const uint32_t*>(src + (int64_t)(sy_lo + r) * spitch + 4 * q);
+        }
       }
-      v = (((ey.b0 * (r0 >> 4)) >> 16) + ((ey.b1 * (r1 >> 4)) >> 16) + 2) >> 2;
+#pragma unroll
+      for (int k = 0; k < 8; k++) {
+        const int i = i0 + 256 * k;
+        if (i < nsr * nd) {
+          const int r = i / nd, q = i - r * nd;
+          *reinterpret_cast<uint32_t*>(s_src + r * sstride + 4 * q) = v[k];
+        }
+      }
     }
-    packed |= (uint32_t)(v & 0xff) << (8 * k);
-  }
-  if (x0 + 4 <= D.w) {
-    *reinterpret_cast<uint32_t*>(dst + x0) = packed;  // pitch is a multiple of 64
   } else {
-    for (int k = 0; x0 + k < D.w; k++) dst[x0 + k] = (uint8_t)(packed >> (8 * k));
+    for (int i = tid; i < nsr * sstride; i += 256) {
+      const int r = i / sstride, q = i - r * sstride;
+      s_src[i] = q < S.w ? src[(int64_t)(sy_lo + r) * spitch + q] : 0;
+    }
+  }
+  __syncthreads();
+  const int groups = (D.w + 3) >> 2;
+  for (int item = tid; item < (dy1 - dy0) * groups; item += 256) {
+    const int rr = item / groups;
+    const int x0 = (item - rr * groups) * 4;
+    const int dy = dy0 + rr;
+    const ResizeY ey = ryt[D.ry_base + dy];
+    const uint8_t* S0 = s_src + (ey.y0 - sy_lo) * sstride;
+    const uint8_t* S1 = s_src + (ey.y1 - sy_lo) * sstride;
+    uint8_t* dst = b.pyr + (int64_t)img * g->pyr_bytes + D.offset + (int64_t)dy * D.pitch;
+    uint32_t packed = 0;
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      const int dx = x0 + k;
+      int v = 0;
+      if (dx < D.w) {
+        const ResizeX ex = rxt[D.rx_base + dx];
+        int r0, r1;
+        if (dx < D.xmax) {
+          r0 = S0[ex.sx] * ex.a0 + S0[ex.sx + 1] * ex.a1;
+          r1 = S1[ex.sx] * ex.a0 + S1[ex.sx + 1] * ex.a1;
+        } else {
+          r0 = S0[ex.sx] * 2048;
+          r1 = S1[ex.sx] * 2048;
+        }
+        v = (((ey.b0 * (r0 >> 4)) >> 16) + ((ey.b1 * (r1 >> 4)) >> 16) + 2) >> 2;
+      }
+      packed |= (uint32_t)(v & 0xff) << (8 * k);
+    }
+    if (x0 + 4 <= D.w) {
+      *reinterpret_cast<uint32_t*>(dst + x0) = packed;  // pitch is a multiple of 64
+    } else {
+      for (int k = 0; x0 + k < D.w; k++) dst[x0 + k] = (uint8_t)(packed >> (8 * k));
+    }
   }
 }
 
@@ -181,15 +225,10 @@ __global__ __launch_bounds__(256) void blur7_kernel(ImageBatch b, const OrbGeom*
 // NMS is strict '>' against the 8 neighbours' scores at that t, zero outside the detect area
 // (cell-local, as cv::FAST sees only the cell view). Survivors are written in row-major order.
 constexpr int kCellWaves = 4;
-constexpr int kTileStride = 72;   // >= max view width + 3 alignment bytes (wCell + 6 + 3 <= 69)
-constexpr int kTileRows = 66;
-constexpr int kScoreStride = 64;  // >= max detect width
-constexpr int kScoreRows = 60;
-constexpr int kCandCap = kScoreStride * kScoreRows;
 
 // max over the 16 contiguous 9-arcs of min(v - ring) ("darker" strength) and of min(ring - v)
 // ("brighter"); p is a FAST-9 corner at threshold t iff the result is > t.
-__device__ __forceinline__ int fast_s(const uint8_t* t, int o) {
+__device__ __forceinline__ int fast_s(const uint8_t* t, int o, const int kTileStride) {
   const int v = t[o];
   int d[16];
   d[0] = v - t[o + 3 * kTileStride];
@@ -231,7 +270,8 @@ __device__ __forceinline__ int fast_s(const uint8_t* t, int o) {
 
 // Exact necessary condition for a corner at threshold t: every 9-arc of the 16-ring contains
 // one pixel of each opposite pair (0,8), (4,12), (2,10), (6,14) -- FAST_t's own pre-test.
-__device__ __forceinline__ bool fast_maybe(const uint8_t* t, int o, int th) {
+__device__ __forceinline__ bool fast_maybe(const uint8_t* t, int o, int th,
+                                           const int kTileStride) {
   const int v = t[o];
   const int lo = v - th, hi = v + th;
   const int p0 = t[o + 3 * kTileStride], p8 = t[o - 3 * kTileStride];
@@ -250,10 +290,10 @@ __global__ __launch_bounds__(256) void fast_cells_kernel(ImageBatch b,
                                                          uint32_t* __restrict__ cell_keys,
                                                          int* __restrict__ cell_count,
                                                          uint32_t* __restrict__ err) {
-  __shared__ __attribute__((aligned(16))) uint8_t s_tile[kCellWaves][kTileRows * kTileStride];
-  __shared__ __attribute__((aligned(16))) uint8_t s_score[kCellWaves][kScoreRows * kScoreStride];
-  __shared__ uint16_t s_cand[kCellWaves][kCandCap];
+  extern __shared__ __attribute__((aligned(16))) uint8_t s_fast[];
   const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int kTileStride = g->fast_tile_stride, kScoreStride = g->fast_score_stride;
+  const int kScoreRows = g->fast_score_rows;
   const int img = blockIdx.y;
   const int cell = blockIdx.x * kCellWaves + wid;
   if (cell >= g->cells_per_image) return;
@@ -277,16 +317,16 @@ __global__ __launch_bounds__(256) void fast_cells_kernel(ImageBatch b,
   const int dh = vh - 6, dw = vw - 6;  // detect area [3, vh-3) x [3, vw-3)
   int pitch;
   const uint8_t* base = level_ptr(b, g, img, level, &pitch);
-  uint8_t* tile = s_tile[wid];
-  uint8_t* sc = s_score[wid];
-  uint16_t* cand = s_cand[wid];
+  uint8_t* tile = s_fast + wid * g->fast_lds_per_wave;
+  uint8_t* sc = tile + ((kTileStride * g->fast_tile_rows + 15) & ~15);
+  uint16_t* cand = reinterpret_cast<uint16_t*>(sc + ((kScoreStride * kScoreRows + 15) & ~15));
   // ---- tile load: aligned dwords covering [iniX & ~3, maxX), all issued before any LDS store
   const int ax = iniX & ~3, off = iniX - ax;
   const int nd = (vw + off + 3) >> 2;  // dwords per row (<= 18)
   const int total = nd * vh;
   const bool aligned = (((uintptr_t)base | (uintptr_t)pitch) & 3) == 0;
   if (aligned) {
-    constexpr int kMaxPer = (18 * kTileRows + 63) / 64;
+    constexpr int kMaxPer = (18 * 66 + 63) / 64;  // wCell, hCell < 60
     uint32_t v[kMaxPer];
 #pragma unroll
     for (int k = 0; k < kMaxPer; k++) {
@@ -310,7 +350,7 @@ __global__ __launch_bounds__(256) void fast_cells_kernel(ImageBatch b,
         tile[r * kTileStride + x] = base[(int64_t)(iniY + r) * pitch + ax + x];
   }
   // zero the score map (dwords)
-  for (int i = lane; i < kScoreRows * kScoreStride / 4; i += 64)
+  for (int i = lane; i < (kScoreRows * kScoreStride + 3) / 4; i += 64)
     reinterpret_cast<uint32_t*>(sc)[i] = 0;
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
@@ -323,7 +363,8 @@ __global__ __launch_bounds__(256) void fast_cells_kernel(ImageBatch b,
   for (int r0 = 0; r0 < dh; r0 += rows_per) {
     const int r = r0 + lr;
     const bool in = r < dh && lc < dw;
-    const bool maybe = in && fast_maybe(tile, (r + 3) * kTileStride + lc + 3 + off, tmin);
+    const bool maybe =
+        in && fast_maybe(tile, (r + 3) * kTileStride + lc + 3 + off, tmin, kTileStride);
     const uint64_t m = __ballot(maybe);
     if (maybe) cand[ncand + lanes_below(m)] = (uint16_t)(r * kScoreStride + lc);
     ncand += __popcll(m);
@@ -335,7 +376,7 @@ __global__ __launch_bounds__(256) void fast_cells_kernel(ImageBatch b,
   for (int i = lane; i < ncand; i += 64) {
     const int pix = cand[i];
     const int r = pix / kScoreStride, cc = pix % kScoreStride;
-    const int s = fast_s(tile, (r + 3) * kTileStride + cc + 3 + off);
+    const int s = fast_s(tile, (r + 3) * kTileStride + cc + 3 + off, kTileStride);
     const int sv = s < 0 ? 0 : s;
     sc[pix] = (uint8_t)sv;
     smax = max(smax, sv);
@@ -868,9 +909,19 @@ __global__ __launch_bounds__(256) void orient_desc_kernel(
     ImageBatch b, const OrbGeom* __restrict__ g, const int2* __restrict__ disc,
     const uint32_t* __restrict__ oct_keys, const int* __restrict__ oct_count,
     KeyPoint* __restrict__ kps, uint8_t* __restrict__ desc, int* __restrict__ nkps) {
-  const int img = blockIdx.y;
+  // XCD-aware mapping: blocks are dealt round-robin over the 8 XCDs, so give every block of one
+  // image the same (linear id % 8) -- an image's pyramid then stays in one XCD's L2.
+  // (bijective when the image count is a multiple of 8; otherwise the natural order is used)
+  const int bpi = gridDim.x;  // blocks per image
+  int img = blockIdx.y, bx = blockIdx.x;
+  if ((gridDim.y & 7) == 0) {
+    const int lin = blockIdx.x + blockIdx.y * bpi;
+    const int xcd = lin & 7, j = lin >> 3;  // j-th block dealt to this XCD group
+    img = xcd + 8 * (j / bpi);
+    bx = j % bpi;
+  }
   const int lane = threadIdx.x & 63;
-  const int w = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int w = bx * 4 + (threadIdx.x >> 6);
   int level = -1, idx = 0, off = 0, total = 0;
   for (int l = 0; l < g->nlevels; l++) {
     const int c = oct_count[img * g->nlevels + l];
@@ -881,7 +932,7 @@ __global__ __launch_bounds__(256) void orient_desc_kernel(
     }
     total += c;
   }
-  if (blockIdx.x == 0 && threadIdx.x == 0) nkps[img] = total;
+  if (bx == 0 && threadIdx.x == 0) nkps[img] = total;
   if (level < 0) return;
   (void)off;
   const LevelGeom& L = g->lv[level];
@@ -1005,14 +1056,16 @@ __global__ __launch_bounds__(256) void orient_desc_kernel(
 void launch_extract(const ImageBatch& b, const OrbGeomDev& gd, int n_images, hipStream_t st) {
   const OrbGeom& g = *gd.host;
   for (int l = 1; l < g.nlevels; l++) {
-    const int items = ((g.lv[l].w + 3) / 4) * g.lv[l].h;
-    dim3 grid((items + 255) / 256, n_images);
-    SLAMGPU_LAUNCH("pyr_down", st, pyr_down_kernel, grid, dim3(256), 0, st, b, gd.dev, l, gd.rx, gd.ry);
+    dim3 grid((g.lv[l].h + kPyrBand - 1) / kPyrBand, n_images);
+    const size_t lds = (size_t)kPyrSrcRows * ((g.lv[l - 1].w + 3) & ~3);
+    SLAMGPU_LAUNCH("pyr_down", st, pyr_down_kernel, grid, dim3(256), lds, st, b, gd.dev, l, gd.rx,
+                   gd.ry);
   }
   SLAMGPU_LAUNCH("blur7", st, blur7_kernel, dim3(g.blur_tiles, n_images), dim3(256), 0, st, b, gd.dev);
   SLAMGPU_LAUNCH("fast_cells", st, fast_cells_kernel,
                      dim3((g.cells_per_image + kCellWaves - 1) / kCellWaves, n_images),
-                     dim3(64 * kCellWaves), 0, st, b, gd.dev, gd.ws.cell_keys,
+                     dim3(64 * kCellWaves), (size_t)kCellWaves * g.fast_lds_per_wave, st, b,
+                     gd.dev, gd.ws.cell_keys,
                      gd.ws.cell_count, gd.ws.err);
   SLAMGPU_LAUNCH("octree", st, octree_kernel, dim3(g.nlevels, n_images), dim3(kOctThreads), 0, st, gd.dev,
                      gd.ws.cell_keys, gd.ws.cell_count, gd.ws.key_scratch, gd.ws.node_scratch,

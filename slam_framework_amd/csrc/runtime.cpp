@@ -174,6 +174,10 @@ int slamgpu_create(int device, const slamgpu_orb_params* p, int cols, int rows, 
     return SLAMGPU_EINVAL;
   }
   compute_tables(c->params, &c->tables);
+  if (c->geom.kp_cap > 4096) {  // matcher keys carry a 12-bit keypoint index
+    delete c;
+    return SLAMGPU_EINVAL;
+  }
   for (int l = 0; l < c->geom.nlevels; l++)
     if (c->geom.lv[l].node_cap > 1024) {
       delete c;
