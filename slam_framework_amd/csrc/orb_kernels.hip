@@ -90,37 +90,56 @@ __global__ __launch_bounds__(256) void pyr_down_kernel(ImageBatch b, const OrbGe
   }
   __syncthreads();
   const int groups = (D.w + 3) >> 2;
-  for (int item = tid; item < (dy1 - dy0) * groups; item += 256) {
-    const int rr = item / groups;
-    const int x0 = (item - rr * groups) * 4;
-    const int dy = dy0 + rr;
-    const ResizeY ey = ryt[D.ry_base + dy];
-    const uint8_t* S0 = s_src + (ey.y0 - sy_lo) * sstride;
-    const uint8_t* S1 = s_src + (ey.y1 - sy_lo) * sstride;
-    uint8_t* dst = b.pyr + (int64_t)img * g->pyr_bytes + D.offset + (int64_t)dy * D.pitch;
-    uint32_t packed = 0;
+  const int nitems = (dy1 - dy0) * groups;
+  // items (row, 4-pixel group) are processed 4 per thread at a time with all table loads issued
+  // before the first dependent LDS read
+  for (int base = tid; base < nitems; base += 4 * 256) {
+    ResizeX ex[4][4];
+    ResizeY ey[4];
+    int dyv[4], x0v[4];
 #pragma unroll
-    for (int k = 0; k < 4; k++) {
-      const int dx = x0 + k;
-      int v = 0;
-      if (dx < D.w) {
-        const ResizeX ex = rxt[D.rx_base + dx];
+    for (int u = 0; u < 4; u++) {
+      const int item = base + 256 * u;
+      const int it = item < nitems ? item : 0;
+      const int rr = it / groups;
+      dyv[u] = dy0 + rr;
+      x0v[u] = (it - rr * groups) * 4;
+      ey[u] = ryt[D.ry_base + dyv[u]];
+#pragma unroll
+      for (int k = 0; k < 4; k++) {
+        const int dx = min(x0v[u] + k, D.w - 1);
+        ex[u][k] = rxt[D.rx_base + dx];
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < 4; u++) {
+      const int item = base + 256 * u;
+      if (item >= nitems) break;
+      const int x0 = x0v[u], dy = dyv[u];
+      const uint8_t* S0 = s_src + (ey[u].y0 - sy_lo) * sstride;
+      const uint8_t* S1 = s_src + (ey[u].y1 - sy_lo) * sstride;
+      uint8_t* dst = b.pyr + (int64_t)img * g->pyr_bytes + D.offset + (int64_t)dy * D.pitch;
+      uint32_t packed = 0;
+#pragma unroll
+      for (int k = 0; k < 4; k++) {
+        const int dx = x0 + k;
+        const ResizeX e = ex[u][k];
         int r0, r1;
         if (dx < D.xmax) {
-          r0 = S0[ex.sx] * ex.a0 + S0[ex.sx + 1] * ex.a1;
-          r1 = S1[ex.sx] * ex.a0 + S1[ex.sx + 1] * ex.a1;
+          r0 = S0[e.sx] * e.a0 + S0[e.sx + 1] * e.a1;
+          r1 = S1[e.sx] * e.a0 + S1[e.sx + 1] * e.a1;
         } else {
-          r0 = S0[ex.sx] * 2048;
-          r1 = S1[ex.sx] * 2048;
+          r0 = S0[e.sx] * 2048;
+          r1 = S1[e.sx] * 2048;
         }
-        v = (((ey.b0 * (r0 >> 4)) >> 16) + ((ey.b1 * (r1 >> 4)) >> 16) + 2) >> 2;
+        const int v = (((ey[u].b0 * (r0 >> 4)) >> 16) + ((ey[u].b1 * (r1 >> 4)) >> 16) + 2) >> 2;
+        packed |= (uint32_t)(v & 0xff) << (8 * k);
       }
-      packed |= (uint32_t)(v & 0xff) << (8 * k);
-    }
-    if (x0 + 4 <= D.w) {
-      *reinterpret_cast<uint32_t*>(dst + x0) = packed;  // pitch is a multiple of 64
-    } else {
-      for (int k = 0; x0 + k < D.w; k++) dst[x0 + k] = (uint8_t)(packed >> (8 * k));
+      if (x0 + 4 <= D.w) {
+        *reinterpret_cast<uint32_t*>(dst + x0) = packed;  // pitch is a multiple of 64
+      } else {
+        for (int k = 0; x0 + k < D.w; k++) dst[x0 + k] = (uint8_t)(packed >> (8 * k));
+      }
     }
   }
 }
@@ -328,22 +347,26 @@ __global__ __launch_bounds__(256) void fast_cells_kernel(ImageBatch b,
   if (aligned) {
     constexpr int kMaxPer = (18 * 66 + 63) / 64;  // wCell, hCell < 60
     uint32_t v[kMaxPer];
+    int ro[kMaxPer];
+    // (row, dword) of element lane + 64k, stepped without divisions
+    const int dr = 64 / nd, dq = 64 - dr * nd;
+    int r = lane / nd, q = lane - (lane / nd) * nd;
 #pragma unroll
     for (int k = 0; k < kMaxPer; k++) {
-      const int i = lane + 64 * k;
-      if (i < total) {
-        const int r = i / nd, q = i - r * nd;
+      ro[k] = (r << 8) | q;
+      if (lane + 64 * k < total)
         v[k] = *reinterpret_cast<const uint32_t*>(base + (int64_t)(iniY + r) * pitch + ax + 4 * q);
+      r += dr;
+      q += dq;
+      if (q >= nd) {
+        q -= nd;
+        r++;
       }
     }
 #pragma unroll
-    for (int k = 0; k < kMaxPer; k++) {
-      const int i = lane + 64 * k;
-      if (i < total) {
-        const int r = i / nd, q = i - r * nd;
-        *reinterpret_cast<uint32_t*>(tile + r * kTileStride + 4 * q) = v[k];
-      }
-    }
+    for (int k = 0; k < kMaxPer; k++)
+      if (lane + 64 * k < total)
+        *reinterpret_cast<uint32_t*>(tile + (ro[k] >> 8) * kTileStride + 4 * (ro[k] & 255)) = v[k];
   } else {
     for (int r = 0; r < vh; r++)
       for (int x = lane; x < vw + off; x += 64)
@@ -901,153 +924,196 @@ __global__ __launch_bounds__(kOctThreads) void octree_kernel(
 
 // ---------------------------------------------------------------------------------------
 // orient_desc: computeOrientation/IC_Angle (:413-420, :18-45) on the unblurred level, then
-// computeOrbDescriptor (:49-88) on the blurred level, one wave per keypoint. Output order is
-// ORBextractor::Compute's: levels 0..L-1 concatenated, each in octree list order (:1020-1048).
-// Descriptor sample offsets use the Release-build FMA association (g++ -O3 -march=native):
+// computeOrbDescriptor (:49-88) on the blurred level. Output order is ORBextractor::Compute's:
+// levels 0..L-1 concatenated, each in octree list order (:1020-1048). Descriptor sample offsets
+// use the Release-build FMA association (g++ -O3 -march=native):
 // row = cvRound(fma(px, b, py*a)), col = cvRound(fma(px, a, -(py*b))).
-__global__ __launch_bounds__(256) void orient_desc_kernel(
-    ImageBatch b, const OrbGeom* __restrict__ g, const int2* __restrict__ disc,
-    const uint32_t* __restrict__ oct_keys, const int* __restrict__ oct_count,
-    KeyPoint* __restrict__ kps, uint8_t* __restrict__ desc, int* __restrict__ nkps) {
-  // XCD-aware mapping: blocks are dealt round-robin over the 8 XCDs, so give every block of one
-  // image the same (linear id % 8) -- an image's pyramid then stays in one XCD's L2.
-  // (bijective when the image count is a multiple of 8; otherwise the natural order is used)
-  const int bpi = gridDim.x;  // blocks per image
-  int img = blockIdx.y, bx = blockIdx.x;
-  if ((gridDim.y & 7) == 0) {
-    const int lin = blockIdx.x + blockIdx.y * bpi;
-    const int xcd = lin & 7, j = lin >> 3;  // j-th block dealt to this XCD group
-    img = xcd + 8 * (j / bpi);
-    bx = j % bpi;
-  }
-  const int lane = threadIdx.x & 63;
-  const int w = bx * 4 + (threadIdx.x >> 6);
-  int level = -1, idx = 0, off = 0, total = 0;
-  for (int l = 0; l < g->nlevels; l++) {
-    const int c = oct_count[img * g->nlevels + l];
-    if (level < 0 && w < total + c) {
-      level = l;
-      idx = w - total;
-      off = total;
-    }
-    total += c;
-  }
-  if (bx == 0 && threadIdx.x == 0) nkps[img] = total;
-  if (level < 0) return;
-  (void)off;
-  const LevelGeom& L = g->lv[level];
-  const uint32_t key = oct_keys[(int64_t)img * g->out_per_image + L.out_base + idx];
-  const int x = key_x(key) + kMinBorder, y = key_y(key) + kMinBorder;
-  int pitch;
-  const uint8_t* im = level_ptr(b, g, img, level, &pitch);
-  const uint8_t* bl = b.blur + (int64_t)img * g->blur_bytes + L.blur_offset;
-  const int bp = L.pitch;
-  // stage the 31x31 patch (IC_Angle) and the 37x37 blurred window (rBRIEF samples reach
-  // |offset| <= 18) into LDS with aligned dword loads
-  __shared__ __attribute__((aligned(16))) uint8_t s_raw[4][31 * 36];
-  __shared__ __attribute__((aligned(16))) uint8_t s_blur[4][37 * 40];
-  uint8_t* raw = s_raw[threadIdx.x >> 6];
-  uint8_t* blr = s_blur[threadIdx.x >> 6];
-  const int rx0 = (x - 15) & ~3, roff = x - 15 - rx0;  // raw patch column origin
-  const int bx0 = (x - 18) & ~3, boff = x - 18 - bx0;  // blurred window column origin
-  if ((((uintptr_t)im | (uintptr_t)pitch) & 3) == 0) {
-    uint32_t v[5];
+// Each wave handles kKpPerWave consecutive keypoints: their keys are loaded up front, and the
+// next keypoint's 31x31 raw patch and 37x37 blurred window (samples reach |offset| <= 18, SURVEY
+// App. B.13) are loaded into registers while the current one is computed from LDS.
+constexpr int kKpPerWave = 8;
+constexpr int kRawStride = 36, kBlurStride = 40;
+
+struct PatchRegs {
+  uint32_t raw[5];   // 31 rows x 9 dwords
+  uint32_t blr[6];   // 37 rows x 10 dwords
+};
+
+__device__ __forceinline__ void patch_load(PatchRegs& p, const uint8_t* im, int pitch,
+                                           bool im_aligned, const uint8_t* bl, int bp, int x,
+                                           int y, int lane) {
+  const int rx0 = (x - 15) & ~3, bx0 = (x - 18) & ~3;
+  if (im_aligned) {
 #pragma unroll
     for (int k = 0; k < 5; k++) {
       const int i = lane + 64 * k;
-      if (i < 31 * 9) {
-        const int r = i / 9, q = i - r * 9;
-        v[k] = *reinterpret_cast<const uint32_t*>(im + (int64_t)(y - 15 + r) * pitch + rx0 + 4 * q);
-      }
+      const int r = i / 9, q = i - r * 9;  // constant divisor
+      if (i < 31 * 9)
+        p.raw[k] = *reinterpret_cast<const uint32_t*>(im + (int64_t)(y - 15 + r) * pitch + rx0 + 4 * q);
     }
+  }
+#pragma unroll
+  for (int k = 0; k < 6; k++) {
+    const int i = lane + 64 * k;
+    const int r = i / 10, q = i - r * 10;
+    if (i < 37 * 10)
+      p.blr[k] = *reinterpret_cast<const uint32_t*>(bl + (int64_t)(y - 18 + r) * bp + bx0 + 4 * q);
+  }
+}
+
+__device__ __forceinline__ void patch_store(const PatchRegs& p, uint8_t* raw, uint8_t* blr,
+                                            const uint8_t* im, int pitch, bool im_aligned, int x,
+                                            int y, int lane) {
+  if (im_aligned) {
 #pragma unroll
     for (int k = 0; k < 5; k++) {
       const int i = lane + 64 * k;
-      if (i < 31 * 9) {
-        const int r = i / 9, q = i - r * 9;
-        *reinterpret_cast<uint32_t*>(raw + r * 36 + 4 * q) = v[k];
-      }
+      const int r = i / 9, q = i - r * 9;
+      if (i < 31 * 9) *reinterpret_cast<uint32_t*>(raw + r * kRawStride + 4 * q) = p.raw[k];
     }
-  } else {
-    for (int i = lane; i < 31 * 36; i += 64) {
-      const int r = i / 36, q = i - r * 36;
+  } else {  // caller image with an odd pitch/base: byte loads straight into LDS
+    const int rx0 = (x - 15) & ~3;
+    for (int i = lane; i < 31 * kRawStride; i += 64) {
+      const int r = i / kRawStride, q = i - r * kRawStride;
       raw[i] = im[(int64_t)(y - 15 + r) * pitch + rx0 + q];
     }
   }
-  {
-    uint32_t v[6];
 #pragma unroll
-    for (int k = 0; k < 6; k++) {
-      const int i = lane + 64 * k;
-      if (i < 37 * 10) {
-        const int r = i / 10, q = i - r * 10;
-        v[k] = *reinterpret_cast<const uint32_t*>(bl + (int64_t)(y - 18 + r) * bp + bx0 + 4 * q);
+  for (int k = 0; k < 6; k++) {
+    const int i = lane + 64 * k;
+    const int r = i / 10, q = i - r * 10;
+    if (i < 37 * 10) *reinterpret_cast<uint32_t*>(blr + r * kBlurStride + 4 * q) = p.blr[k];
+  }
+}
+
+__global__ __launch_bounds__(256) void orient_desc_kernel(
+    ImageBatch b, const OrbGeom* __restrict__ g, const uint32_t* __restrict__ oct_keys,
+    const int* __restrict__ oct_count, KeyPoint* __restrict__ kps, uint8_t* __restrict__ desc,
+    int* __restrict__ nkps) {
+  __shared__ __attribute__((aligned(16))) uint8_t s_raw[4][31 * kRawStride];
+  __shared__ __attribute__((aligned(16))) uint8_t s_blur[4][37 * kBlurStride];
+  __shared__ int s_umax[16];
+  // XCD-aware mapping: blocks are dealt round-robin over the 8 XCDs, so give every block of one
+  // image the same (linear id % 8) -- an image's pyramid then stays in one XCD's L2
+  // (bijective when the image count is a multiple of 8; otherwise the natural order is used).
+  const int bpi = gridDim.x;
+  int img = blockIdx.y, bx = blockIdx.x;
+  if ((gridDim.y & 7) == 0) {
+    const int lin = blockIdx.x + blockIdx.y * bpi;
+    const int xcd = lin & 7, j = lin >> 3;
+    img = xcd + 8 * (j / bpi);
+    bx = j % bpi;
+  }
+  if (threadIdx.x < 16) s_umax[threadIdx.x] = g->umax[threadIdx.x];
+  __syncthreads();
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  int lcount[kMaxLevels];
+  int total = 0;
+  for (int l = 0; l < g->nlevels; l++) {
+    lcount[l] = oct_count[img * g->nlevels + l];
+    total += lcount[l];
+  }
+  if (bx == 0 && threadIdx.x == 0) nkps[img] = total;
+  const int k0 = (bx * 4 + wid) * kKpPerWave;
+  if (k0 >= total) return;
+  const int nk = min(kKpPerWave, total - k0);
+  // lane j < nk: level / key of keypoint k0 + j
+  int my_level = 0, my_key = 0;
+  if (lane < nk) {
+    int t = k0 + lane, l = 0;
+    while (t >= lcount[l]) {
+      t -= lcount[l];
+      l++;
+    }
+    my_level = l;
+    my_key = (int)oct_keys[(int64_t)img * g->out_per_image + g->lv[l].out_base + t];
+  }
+  uint8_t* raw = s_raw[wid];
+  uint8_t* blr = s_blur[wid];
+  // IC_Angle work split: lane l < 62 sums half a patch row (row v, u < 0 or u >= 0)
+  const int hv = (lane >> 1) - 15, hhalf = lane & 1;
+  const int hd = lane < 62 ? s_umax[hv < 0 ? -hv : hv] : -1;
+  const int u_lo = hhalf ? 0 : -hd, u_hi = hhalf ? hd : -1;
+  PatchRegs pr;
+  auto geo = [&](int j, int& level, int& x, int& y, const uint8_t*& im, int& pitch,
+                 const uint8_t*& bl) {
+    level = __shfl(my_level, j, 64);
+    const uint32_t key = (uint32_t)__shfl(my_key, j, 64);
+    x = key_x(key) + kMinBorder;
+    y = key_y(key) + kMinBorder;
+    im = level_ptr(b, g, img, level, &pitch);
+    bl = b.blur + (int64_t)img * g->blur_bytes + g->lv[level].blur_offset;
+  };
+  int level, x, y, pitch;
+  const uint8_t *im, *bl;
+  geo(0, level, x, y, im, pitch, bl);
+  bool al = (((uintptr_t)im | (uintptr_t)pitch) & 3) == 0;
+  patch_load(pr, im, pitch, al, bl, g->lv[level].pitch, x, y, lane);
+  for (int j = 0; j < nk; j++) {
+    patch_store(pr, raw, blr, im, pitch, al, x, y, lane);
+    const int cl = level, cx = x, cy = y;
+    if (j + 1 < nk) {  // prefetch the next keypoint while this one is computed
+      geo(j + 1, level, x, y, im, pitch, bl);
+      al = (((uintptr_t)im | (uintptr_t)pitch) & 3) == 0;
+      patch_load(pr, im, pitch, al, bl, g->lv[level].pitch, x, y, lane);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    const LevelGeom& L = g->lv[cl];
+    const uint8_t* center = raw + 15 * kRawStride + 15 + ((cx - 15) & 3);
+    int m10 = 0, m01 = 0;
+    for (int u = u_lo; u <= u_hi; u++) {
+      const int v = center[hv * kRawStride + u];
+      m10 += u * v;
+      m01 += hv * v;
+    }
+    m10 = wave_sum(m10);
+    m01 = wave_sum(m01);
+    const float angle = cv_fast_atan2((float)m01, (float)m10);
+    const float factorPI = (float)(3.14159265358979323846 / 180.0);
+    float sa, ca;
+    glibc_sincosf(angle * factorPI, &sa, &ca);
+    const float a = ca, bb = sa;
+    const uint8_t* bc = blr + 18 * kBlurStride + 18 + ((cx - 18) & 3);
+    uint64_t words[4];
+#pragma unroll
+    for (int r = 0; r < 4; r++) {
+      const int t = r * 64 + lane;
+      const float px0 = (float)c_pattern[4 * t], py0 = (float)c_pattern[4 * t + 1];
+      const float px1 = (float)c_pattern[4 * t + 2], py1 = (float)c_pattern[4 * t + 3];
+      const int ry0 = cv_round(fmaf(px0, bb, py0 * a));
+      const int rx0 = cv_round(fmaf(px0, a, -(py0 * bb)));
+      const int ry1 = cv_round(fmaf(px1, bb, py1 * a));
+      const int rx1 = cv_round(fmaf(px1, a, -(py1 * bb)));
+      const int v0 = bc[ry0 * kBlurStride + rx0];
+      const int v1 = bc[ry1 * kBlurStride + rx1];
+      words[r] = __ballot(v0 < v1);
+    }
+    const int64_t o = (int64_t)img * g->kp_cap + k0 + j;
+    if (lane < 4) {
+      uint64_t wv = words[0];
+      if (lane == 1) wv = words[1];
+      if (lane == 2) wv = words[2];
+      if (lane == 3) wv = words[3];
+      reinterpret_cast<uint64_t*>(desc + o * 32)[lane] = wv;
+    }
+    if (lane == 0) {
+      KeyPoint kp;
+      kp.x = (float)cx;
+      kp.y = (float)cy;
+      if (cl != 0) {
+        kp.x *= L.scale;
+        kp.y *= L.scale;
       }
+      kp.size = L.patch_size;
+      kp.angle = angle;
+      kp.response = (float)key_score((uint32_t)__builtin_amdgcn_readlane(my_key, j));
+      kp.octave = cl;
+      kp.class_id = -1;
+      kps[o] = kp;
     }
-#pragma unroll
-    for (int k = 0; k < 6; k++) {
-      const int i = lane + 64 * k;
-      if (i < 37 * 10) {
-        const int r = i / 10, q = i - r * 10;
-        *reinterpret_cast<uint32_t*>(blr + r * 40 + 4 * q) = v[k];
-      }
-    }
-  }
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-  const uint8_t* center = raw + 15 * 36 + 15 + roff;
-  int m10 = 0, m01 = 0;
-  for (int i = lane; i < kDiscPixels; i += 64) {
-    const int2 uv = disc[i];
-    const int v = center[uv.y * 36 + uv.x];
-    m10 += uv.x * v;
-    m01 += uv.y * v;
-  }
-  m10 = wave_sum(m10);
-  m01 = wave_sum(m01);
-  const float angle = cv_fast_atan2((float)m01, (float)m10);
-  const float factorPI = (float)(3.14159265358979323846 / 180.0);
-  float sa, ca;
-  glibc_sincosf(angle * factorPI, &sa, &ca);
-  const float a = ca, bb = sa;
-  const uint8_t* bc = blr + 18 * 40 + 18 + boff;
-  constexpr int bpl = 40;
-  uint64_t words[4];
-#pragma unroll
-  for (int r = 0; r < 4; r++) {
-    const int t = r * 64 + lane;
-    const float px0 = (float)c_pattern[4 * t], py0 = (float)c_pattern[4 * t + 1];
-    const float px1 = (float)c_pattern[4 * t + 2], py1 = (float)c_pattern[4 * t + 3];
-    const int ry0 = cv_round(fmaf(px0, bb, py0 * a));
-    const int rx0 = cv_round(fmaf(px0, a, -(py0 * bb)));
-    const int ry1 = cv_round(fmaf(px1, bb, py1 * a));
-    const int rx1 = cv_round(fmaf(px1, a, -(py1 * bb)));
-    const int v0 = bc[ry0 * bpl + rx0];
-    const int v1 = bc[ry1 * bpl + rx1];
-    words[r] = __ballot(v0 < v1);
-  }
-  const int64_t o = (int64_t)img * g->kp_cap + off + idx;
-  if (lane < 4) {
-    uint64_t wv = words[0];
-    if (lane == 1) wv = words[1];
-    if (lane == 2) wv = words[2];
-    if (lane == 3) wv = words[3];
-    reinterpret_cast<uint64_t*>(desc + o * 32)[lane] = wv;
-  }
-  if (lane == 0) {
-    KeyPoint kp;
-    kp.x = (float)x;
-    kp.y = (float)y;
-    if (level != 0) {
-      kp.x *= L.scale;
-      kp.y *= L.scale;
-    }
-    kp.size = L.patch_size;
-    kp.angle = angle;
-    kp.response = (float)key_score(key);
-    kp.octave = level;
-    kp.class_id = -1;
-    kps[o] = kp;
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
   }
 }
 
@@ -1070,9 +1136,10 @@ void launch_extract(const ImageBatch& b, const OrbGeomDev& gd, int n_images, hip
   SLAMGPU_LAUNCH("octree", st, octree_kernel, dim3(g.nlevels, n_images), dim3(kOctThreads), 0, st, gd.dev,
                      gd.ws.cell_keys, gd.ws.cell_count, gd.ws.key_scratch, gd.ws.node_scratch,
                      gd.ws.oct_keys, gd.ws.oct_count, gd.ws.err);
-  SLAMGPU_LAUNCH("orient_desc", st, orient_desc_kernel, dim3((g.kp_cap + 3) / 4, n_images), dim3(256), 0, st,
-                     b, gd.dev, gd.disc, gd.ws.oct_keys, gd.ws.oct_count, gd.out.kps,
-                     gd.out.desc, gd.out.nkps);
+  SLAMGPU_LAUNCH("orient_desc", st, orient_desc_kernel,
+                 dim3((g.kp_cap + 4 * kKpPerWave - 1) / (4 * kKpPerWave), n_images), dim3(256), 0,
+                 st, b, gd.dev, gd.ws.oct_keys, gd.ws.oct_count, gd.out.kps, gd.out.desc,
+                 gd.out.nkps);
 }
 
 }  // namespace slamgpu
