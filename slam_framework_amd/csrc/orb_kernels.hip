@@ -928,71 +928,51 @@ __global__ __launch_bounds__(kOctThreads) void octree_kernel(
 // levels 0..L-1 concatenated, each in octree list order (:1020-1048). Descriptor sample offsets
 // use the Release-build FMA association (g++ -O3 -march=native):
 // row = cvRound(fma(px, b, py*a)), col = cvRound(fma(px, a, -(py*b))).
-// Each wave handles kKpPerWave consecutive keypoints: their keys are loaded up front, and the
-// next keypoint's 31x31 raw patch and 37x37 blurred window (samples reach |offset| <= 18, SURVEY
-// App. B.13) are loaded into registers while the current one is computed from LDS.
+// Each wave handles kKpPerWave consecutive keypoints in three phases, so the per-keypoint scalar
+// work (atan2, sincos) runs once for all of them and every load is in flight at once:
+//  1. issue all loads: each keypoint's 31x31 raw patch into registers (lane = half a patch row,
+//     5 dwords), its 37x37 blurred window (samples reach |offset| <= 18)
+//     straight into LDS with global_load_lds;
+//  2. IC_Angle moments with v_dot4_u32_u8 against per-lane disc weights (u+20 / 1 inside
+//     umax, 0 outside; sum(u*I) = sum((u+20)*I) - 20*sum(I), exact), a 16-value reduce-scatter
+//     across the wave, and one fastAtan2 + sincosf pass for the 8 keypoints;
+//  3. rBRIEF: 4 tests per lane per keypoint with packed-fp32 offsets; cvRound(v) == bits of
+//     (v + 1.5*2^23) for |v| < 2^22 (round-half-even in the add), which feeds the LDS address.
 constexpr int kKpPerWave = 8;
-constexpr int kRawStride = 36, kBlurStride = 40;
+constexpr int kBlurStride = 40, kBlurWin = 37 * kBlurStride;
+typedef float f32x2 __attribute__((ext_vector_type(2)));
 
-struct PatchRegs {
-  uint32_t raw[5];   // 31 rows x 9 dwords
-  uint32_t blr[6];   // 37 rows x 10 dwords
-};
-
-__device__ __forceinline__ void patch_load(PatchRegs& p, const uint8_t* im, int pitch,
-                                           bool im_aligned, const uint8_t* bl, int bp, int x,
-                                           int y, int lane) {
-  const int rx0 = (x - 15) & ~3, bx0 = (x - 18) & ~3;
-  if (im_aligned) {
+// Sum of the 16 per-lane values v[] over the wave; value i ends up in lanes 4i..4i+3.
+__device__ __forceinline__ int reduce_scatter16(int (&v)[16], int lane) {
+  int w[8], x[4], y[2];
 #pragma unroll
-    for (int k = 0; k < 5; k++) {
-      const int i = lane + 64 * k;
-      const int r = i / 9, q = i - r * 9;  // constant divisor
-      if (i < 31 * 9)
-        p.raw[k] = *reinterpret_cast<const uint32_t*>(im + (int64_t)(y - 15 + r) * pitch + rx0 + 4 * q);
-    }
+  for (int k = 0; k < 8; k++) {  // lanes 32-63 keep index k+8
+    auto p = __builtin_amdgcn_permlane32_swap(v[k], v[k + 8], false, false);
+    w[k] = (int)p[0] + (int)p[1];
   }
 #pragma unroll
-  for (int k = 0; k < 6; k++) {
-    const int i = lane + 64 * k;
-    const int r = i / 10, q = i - r * 10;
-    if (i < 37 * 10)
-      p.blr[k] = *reinterpret_cast<const uint32_t*>(bl + (int64_t)(y - 18 + r) * bp + bx0 + 4 * q);
+  for (int k = 0; k < 4; k++) {  // odd rows keep index +4
+    auto p = __builtin_amdgcn_permlane16_swap(w[k], w[k + 4], false, false);
+    x[k] = (int)p[0] + (int)p[1];
   }
-}
-
-__device__ __forceinline__ void patch_store(const PatchRegs& p, uint8_t* raw, uint8_t* blr,
-                                            const uint8_t* im, int pitch, bool im_aligned, int x,
-                                            int y, int lane) {
-  if (im_aligned) {
+  const bool up8 = lane & 8, up4 = lane & 4;
 #pragma unroll
-    for (int k = 0; k < 5; k++) {
-      const int i = lane + 64 * k;
-      const int r = i / 9, q = i - r * 9;
-      if (i < 31 * 9) *reinterpret_cast<uint32_t*>(raw + r * kRawStride + 4 * q) = p.raw[k];
-    }
-  } else {  // caller image with an odd pitch/base: byte loads straight into LDS
-    const int rx0 = (x - 15) & ~3;
-    for (int i = lane; i < 31 * kRawStride; i += 64) {
-      const int r = i / kRawStride, q = i - r * kRawStride;
-      raw[i] = im[(int64_t)(y - 15 + r) * pitch + rx0 + q];
-    }
+  for (int k = 0; k < 2; k++) {  // row_mirror: partner lane ^ 15
+    const int send = up8 ? x[k] : x[k + 2];
+    y[k] = (up8 ? x[k + 2] : x[k]) + __builtin_amdgcn_mov_dpp(send, 0x140, 0xf, 0xf, false);
   }
-#pragma unroll
-  for (int k = 0; k < 6; k++) {
-    const int i = lane + 64 * k;
-    const int r = i / 10, q = i - r * 10;
-    if (i < 37 * 10) *reinterpret_cast<uint32_t*>(blr + r * kBlurStride + 4 * q) = p.blr[k];
-  }
+  const int send = up4 ? y[0] : y[1];  // row_half_mirror: partner lane ^ 7
+  int z = (up4 ? y[1] : y[0]) + __builtin_amdgcn_mov_dpp(send, 0x141, 0xf, 0xf, false);
+  z += __builtin_amdgcn_mov_dpp(z, 0x4e, 0xf, 0xf, false);  // quad_perm [2,3,0,1]
+  z += __builtin_amdgcn_mov_dpp(z, 0xb1, 0xf, 0xf, false);  // quad_perm [1,0,3,2]
+  return z;
 }
 
 __global__ __launch_bounds__(256) void orient_desc_kernel(
     ImageBatch b, const OrbGeom* __restrict__ g, const uint32_t* __restrict__ oct_keys,
     const int* __restrict__ oct_count, KeyPoint* __restrict__ kps, uint8_t* __restrict__ desc,
     int* __restrict__ nkps) {
-  __shared__ __attribute__((aligned(16))) uint8_t s_raw[4][31 * kRawStride];
-  __shared__ __attribute__((aligned(16))) uint8_t s_blur[4][37 * kBlurStride];
-  __shared__ int s_umax[16];
+  __shared__ __attribute__((aligned(16))) uint8_t s_blur[4][kKpPerWave][kBlurWin];
   // XCD-aware mapping: blocks are dealt round-robin over the 8 XCDs, so give every block of one
   // image the same (linear id % 8) -- an image's pyramid then stays in one XCD's L2
   // (bijective when the image count is a multiple of 8; otherwise the natural order is used).
@@ -1004,8 +984,6 @@ __global__ __launch_bounds__(256) void orient_desc_kernel(
     img = xcd + 8 * (j / bpi);
     bx = j % bpi;
   }
-  if (threadIdx.x < 16) s_umax[threadIdx.x] = g->umax[threadIdx.x];
-  __syncthreads();
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   int lcount[kMaxLevels];
   int total = 0;
@@ -1028,92 +1006,157 @@ __global__ __launch_bounds__(256) void orient_desc_kernel(
     my_level = l;
     my_key = (int)oct_keys[(int64_t)img * g->out_per_image + g->lv[l].out_base + t];
   }
-  uint8_t* raw = s_raw[wid];
-  uint8_t* blr = s_blur[wid];
-  // IC_Angle work split: lane l < 62 sums half a patch row (row v, u < 0 or u >= 0)
-  const int hv = (lane >> 1) - 15, hhalf = lane & 1;
-  const int hd = lane < 62 ? s_umax[hv < 0 ? -hv : hv] : -1;
-  const int u_lo = hhalf ? 0 : -hd, u_hi = hhalf ? hd : -1;
-  PatchRegs pr;
-  auto geo = [&](int j, int& level, int& x, int& y, const uint8_t*& im, int& pitch,
-                 const uint8_t*& bl) {
-    level = __shfl(my_level, j, 64);
-    const uint32_t key = (uint32_t)__shfl(my_key, j, 64);
-    x = key_x(key) + kMinBorder;
-    y = key_y(key) + kMinBorder;
-    im = level_ptr(b, g, img, level, &pitch);
-    bl = b.blur + (int64_t)img * g->blur_bytes + g->lv[level].blur_offset;
-  };
-  int level, x, y, pitch;
-  const uint8_t *im, *bl;
-  geo(0, level, x, y, im, pitch, bl);
-  bool al = (((uintptr_t)im | (uintptr_t)pitch) & 3) == 0;
-  patch_load(pr, im, pitch, al, bl, g->lv[level].pitch, x, y, lane);
-  for (int j = 0; j < nk; j++) {
-    patch_store(pr, raw, blr, im, pitch, al, x, y, lane);
-    const int cl = level, cx = x, cy = y;
-    if (j + 1 < nk) {  // prefetch the next keypoint while this one is computed
-      geo(j + 1, level, x, y, im, pitch, bl);
-      al = (((uintptr_t)im | (uintptr_t)pitch) & 3) == 0;
-      patch_load(pr, im, pitch, al, bl, g->lv[level].pitch, x, y, lane);
-    }
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    const LevelGeom& L = g->lv[cl];
-    const uint8_t* center = raw + 15 * kRawStride + 15 + ((cx - 15) & 3);
-    int m10 = 0, m01 = 0;
-    for (int u = u_lo; u <= u_hi; u++) {
-      const int v = center[hv * kRawStride + u];
-      m10 += u * v;
-      m01 += hv * v;
-    }
-    m10 = wave_sum(m10);
-    m01 = wave_sum(m01);
-    const float angle = cv_fast_atan2((float)m01, (float)m10);
-    const float factorPI = (float)(3.14159265358979323846 / 180.0);
-    float sa, ca;
-    glibc_sincosf(angle * factorPI, &sa, &ca);
-    const float a = ca, bb = sa;
-    const uint8_t* bc = blr + 18 * kBlurStride + 18 + ((cx - 18) & 3);
-    uint64_t words[4];
+  // Per-lane IC_Angle geometry: lane = (patch row hr, half hh); dword k covers
+  // u = 16*hh + 4k + (0..3) - 15 of row v = hr - 15.
+  const int hr = lane >> 1, hh = lane & 1, hv = hr - 15;
+  const int hd = hr < 31 ? g->umax[hv < 0 ? -hv : hv] : -1;
+  uint32_t wt[4], one[4];
 #pragma unroll
-    for (int r = 0; r < 4; r++) {
-      const int t = r * 64 + lane;
-      const float px0 = (float)c_pattern[4 * t], py0 = (float)c_pattern[4 * t + 1];
-      const float px1 = (float)c_pattern[4 * t + 2], py1 = (float)c_pattern[4 * t + 3];
-      const int ry0 = cv_round(fmaf(px0, bb, py0 * a));
-      const int rx0 = cv_round(fmaf(px0, a, -(py0 * bb)));
-      const int ry1 = cv_round(fmaf(px1, bb, py1 * a));
-      const int rx1 = cv_round(fmaf(px1, a, -(py1 * bb)));
-      const int v0 = bc[ry0 * kBlurStride + rx0];
-      const int v1 = bc[ry1 * kBlurStride + rx1];
-      words[r] = __ballot(v0 < v1);
-    }
-    const int64_t o = (int64_t)img * g->kp_cap + k0 + j;
-    if (lane < 4) {
-      uint64_t wv = words[0];
-      if (lane == 1) wv = words[1];
-      if (lane == 2) wv = words[2];
-      if (lane == 3) wv = words[3];
-      reinterpret_cast<uint64_t*>(desc + o * 32)[lane] = wv;
-    }
-    if (lane == 0) {
-      KeyPoint kp;
-      kp.x = (float)cx;
-      kp.y = (float)cy;
-      if (cl != 0) {
-        kp.x *= L.scale;
-        kp.y *= L.scale;
+  for (int k = 0; k < 4; k++) {
+    wt[k] = 0;
+    one[k] = 0;
+#pragma unroll
+    for (int bb = 0; bb < 4; bb++) {
+      const int u = 16 * hh + 4 * k + bb - 15;
+      if (u >= -hd && u <= hd) {
+        wt[k] |= (uint32_t)(u + 20) << (8 * bb);
+        one[k] |= 1u << (8 * bb);
       }
-      kp.size = L.patch_size;
-      kp.angle = angle;
-      kp.response = (float)key_score((uint32_t)__builtin_amdgcn_readlane(my_key, j));
-      kp.octave = cl;
-      kp.class_id = -1;
-      kps[o] = kp;
     }
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-    __builtin_amdgcn_wave_barrier();
+  }
+  // Keys of the wave's keypoints as scalars; slots j >= nk repeat the last keypoint so that
+  // every phase is branch-free (their results are never stored).
+  uint32_t kkey[kKpPerWave];
+  int klev[kKpPerWave];
+#pragma unroll
+  for (int j = 0; j < kKpPerWave; j++) {
+    const int jj = min(j, nk - 1);
+    kkey[j] = (uint32_t)__builtin_amdgcn_readlane(my_key, jj);
+    klev[j] = __builtin_amdgcn_readlane(my_level, jj);
+  }
+  // Phase 1: all loads. Keypoint bases are wave-uniform (scalar); lane offsets are 24-bit.
+  int br[6], bq[6];
+#pragma unroll
+  for (int k = 0; k < 6; k++) {
+    const int i = lane + 64 * k;
+    br[k] = i / 10;
+    bq[k] = 4 * (i - br[k] * 10);
+  }
+  const int in_pitch = __builtin_amdgcn_readfirstlane(b.in_pitch);
+  const uint8_t* blur_img = b.blur + (int64_t)img * g->blur_bytes;
+  uint32_t raw[kKpPerWave][5];
+#pragma unroll
+  for (int j = 0; j < kKpPerWave; j++) {
+#pragma unroll
+    for (int k = 0; k < 5; k++) raw[j][k] = 0;
+    const int level = klev[j];
+    const int x = key_x(kkey[j]) + kMinBorder, y = key_y(kkey[j]) + kMinBorder;
+    const LevelGeom& L = g->lv[level];
+    const int pitch = level == 0 ? in_pitch : L.pitch;
+    const uint8_t* im = level == 0 ? batch_image(b, img)
+                                   : b.pyr + (int64_t)img * g->pyr_bytes + L.offset;
+    const uint8_t* rbase = im + (int64_t)(y - 15) * pitch + ((x - 15) & ~3);
+    const uint8_t* rp = rbase + (__umul24(hr, pitch) + 16 * hh);
+    if (hr < 31) {
+      if ((((uintptr_t)im | (uintptr_t)pitch) & 3) == 0) {
+#pragma unroll
+        for (int k = 0; k < 5; k++) raw[j][k] = reinterpret_cast<const uint32_t*>(rp)[k];
+      } else {  // caller image with an odd pitch/base
+#pragma unroll
+        for (int k = 0; k < 20; k++) raw[j][k >> 2] |= (uint32_t)rp[k] << (8 * (k & 3));
+      }
+    }
+    const int bp = L.pitch;
+    const uint8_t* bl = blur_img + L.blur_offset + (int64_t)(y - 18) * bp + ((x - 18) & ~3);
+#pragma unroll
+    for (int k = 0; k < 6; k++)
+      if (lane + 64 * k < 37 * 10)
+        __builtin_amdgcn_global_load_lds(
+            (const __attribute__((address_space(1))) void*)(bl + (__umul24(br[k], bp) + bq[k])),
+            (__attribute__((address_space(3))) void*)(&s_blur[wid][j][256 * k]), 4, 0, 0);
+  }
+  // Phase 2: moments -> angle, sin, cos (lane 8j holds keypoint j's).
+  int mv[16];
+#pragma unroll
+  for (int j = 0; j < kKpPerWave; j++) {
+    const int a = (key_x(kkey[j]) + kMinBorder - 15) & 3;
+    uint32_t s = 0, t = 0;
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      const uint32_t e = __builtin_amdgcn_alignbyte(raw[j][k + 1], raw[j][k], a);
+      s = __builtin_amdgcn_udot4(e, one[k], s, false);
+      t = __builtin_amdgcn_udot4(e, wt[k], t, false);
+    }
+    mv[2 * j] = (int)t - 20 * (int)s;  // m10 part
+    mv[2 * j + 1] = hv * (int)s;       // m01 part
+  }
+  int mom = reduce_scatter16(mv, lane);
+  const int m01 = __builtin_amdgcn_mov_dpp(mom, 0x104, 0xf, 0xf, false);  // row_shl:4
+  const float angle = cv_fast_atan2((float)m01, (float)mom);
+  const float factorPI = (float)(3.14159265358979323846 / 180.0);
+  float sa, ca;
+  glibc_sincosf(angle * factorPI, &sa, &ca);
+  // Phase 3: descriptors. Pattern test t = r*64 + lane.
+  f32x2 ppx[4][2], ppy[4][2];
+#pragma unroll
+  for (int r = 0; r < 4; r++) {
+    const int t = r * 64 + lane;
+#pragma unroll
+    for (int e = 0; e < 2; e++) {
+      const float px = (float)c_pattern[4 * t + 2 * e], py = (float)c_pattern[4 * t + 2 * e + 1];
+      ppx[r][e] = (f32x2){px, px};
+      ppy[r][e] = (f32x2){py, py};
+    }
+  }
+  __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): the global_load_lds windows have landed
+  const f32x2 magic = {12582912.0f, 12582912.0f};
+  uint32_t dlo = 0, dhi = 0;
+#pragma unroll
+  for (int j = 0; j < kKpPerWave; j++) {
+    {
+      const int x = key_x(kkey[j]) + kMinBorder;
+      const float cj = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(ca), 8 * j));
+      const float sj = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(sa), 8 * j));
+      const f32x2 ab = {sj, cj}, nab = {cj, -sj};
+      // LDS byte address of window(ry, rx) = base + (0x400000+ry)*40 + 0x4B400000+rx - C
+      const uint8_t* bc = &s_blur[wid][j][0] + 18 * kBlurStride + 18 + ((x - 18) & 3) -
+                          (int32_t)0x55400000u;
+#pragma unroll
+      for (int r = 0; r < 4; r++) {
+        int v[2];
+#pragma unroll
+        for (int e = 0; e < 2; e++) {
+          const f32x2 q = __builtin_elementwise_fma(ppx[r][e], ab, ppy[r][e] * nab) + magic;
+          const uint32_t yb = __float_as_uint(q.x), xb = __float_as_uint(q.y);
+          v[e] = bc[(int32_t)((yb & 0xFFFFFFu) * (uint32_t)kBlurStride + xb)];
+        }
+        const uint64_t word = __ballot(v[0] < v[1]);
+        if (lane == 4 * j + r) {
+          dlo = (uint32_t)word;
+          dhi = (uint32_t)(word >> 32);
+        }
+      }
+    }
+  }
+  const int64_t o = (int64_t)img * g->kp_cap + k0;
+  if (lane < 4 * nk)
+    reinterpret_cast<uint64_t*>(desc + o * 32)[lane] = ((uint64_t)dhi << 32) | dlo;
+  const float my_angle = __shfl(angle, 8 * lane, 64);
+  if (lane < nk) {
+    const LevelGeom& L = g->lv[my_level];
+    KeyPoint kp;
+    kp.x = (float)(key_x((uint32_t)my_key) + kMinBorder);
+    kp.y = (float)(key_y((uint32_t)my_key) + kMinBorder);
+    if (my_level != 0) {
+      kp.x *= L.scale;
+      kp.y *= L.scale;
+    }
+    kp.size = L.patch_size;
+    kp.angle = my_angle;
+    kp.response = (float)key_score((uint32_t)my_key);
+    kp.octave = my_level;
+    kp.class_id = -1;
+    kps[o + lane] = kp;
   }
 }
 
