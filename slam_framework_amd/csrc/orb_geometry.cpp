@@ -184,9 +184,11 @@ int compute_geometry(const OrbParams& p, int cols, int rows, OrbGeom* g,
   gauss_kernel_int(g->gauss);
   // strict 8-neighbour NMS keeps at most one pixel per 2x2 block of the detect area
   g->cell_cap = ((max_wcell + 1) / 2) * ((max_hcell + 1) / 2);
-  g->fast_tile_stride = round_up(max_wcell + 6 + 3, 4);
+  // tile: dwords covering the cell view from iniX & ~3, plus one spare dword per row for the
+  // prefilter's right-neighbour reads
+  g->fast_tile_stride = round_up(max_wcell + 6 + 3, 4) + 4;
   g->fast_tile_rows = max_hcell + 6;
-  g->fast_score_stride = max_wcell;
+  g->fast_score_stride = round_up(max_wcell + 6 + 3, 4);  // indexed by tile column
   g->fast_score_rows = max_hcell;
   g->fast_lds_per_wave = round_up(g->fast_tile_stride * g->fast_tile_rows, 16) +
                          round_up(g->fast_score_stride * g->fast_score_rows, 16) +
@@ -219,6 +221,26 @@ int compute_geometry(const OrbParams& p, int cols, int rows, OrbGeom* g,
   g->out_per_image = out_off;
   g->kp_cap = out_off;
   return 0;
+}
+
+void build_cells(const OrbGeom& g, std::vector<CellDesc>* cells) {
+  cells->assign(g.cells_per_image, CellDesc{});
+  for (int l = 0; l < g.nlevels; l++) {
+    const LevelGeom& L = g.lv[l];
+    for (int c = 0; c < L.ncols * L.nrows; c++) {
+      CellDesc& d = (*cells)[L.cell_base + c];
+      const int ci = c / L.ncols, cj = c % L.ncols;
+      const int iniY = kMinBorder + ci * L.hcell, iniX = kMinBorder + cj * L.wcell;
+      d.level = (int16_t)l;
+      d.ini_x = (int16_t)iniX;
+      d.ini_y = (int16_t)iniY;
+      if (iniY >= L.max_by - 3 || iniX >= L.max_bx - 6) continue;  // :737, :745
+      const int maxY = std::min(iniY + L.hcell + 6, L.max_by);
+      const int maxX = std::min(iniX + L.wcell + 6, L.max_bx);
+      d.vh = (int16_t)(maxY - iniY);
+      d.vw = (int16_t)(maxX - iniX);
+    }
+  }
 }
 
 }  // namespace slamgpu

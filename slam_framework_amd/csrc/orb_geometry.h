@@ -15,7 +15,13 @@ constexpr int kEdgeThreshold = 19;
 constexpr int kMinBorder = kEdgeThreshold - 3;  // minBorderX/Y (:712)
 constexpr int kPatchSize = 31;
 constexpr int kHalfPatch = 15;
-constexpr int kDiscPixels = 749;               // |{(u,v): |v|<=15, |u|<=umax[|v|]}|
+
+// One FAST cell's view (ComputeKeyPointsOctTree :735-749), precomputed per configuration so a
+// cell costs one 16-byte load instead of a chain of level lookups. vw = vh = 0: empty cell.
+struct CellDesc {
+  int16_t level, ini_x, ini_y, vw, vh, pad0, pad1, pad2;
+};
+static_assert(sizeof(CellDesc) == 16, "CellDesc is one dwordx4");
 
 struct LevelGeom {
   int w, h;             // level image size

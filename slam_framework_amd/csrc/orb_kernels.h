@@ -52,7 +52,7 @@ struct OrbGeomDev {
   const OrbGeom* dev;
   const ResizeX* rx;
   const ResizeY* ry;
-  const int2* disc;        // IC_Angle circular patch offsets (u, v), kDiscPixels entries
+  const CellDesc* cells;   // FAST cell views, cells_per_image entries (build_cells)
   ExtractWorkspace ws;
   ExtractOutput out;
 };

@@ -304,160 +304,256 @@ __device__ __forceinline__ bool fast_maybe(const uint8_t* t, int o, int th,
   return dark || bright;
 }
 
+// SWAR byte compares on 4 pixels per lane: bit 7 of each byte of the result is that byte's
+// answer, other bits are garbage (callers mask with kH). (Hacker's Delight 2-18 style.)
+constexpr uint32_t kH = 0x80808080u;
+__device__ __forceinline__ uint32_t swar_lt(uint32_t a, uint32_t b) {  // a < b
+  const uint32_t d = (a | kH) - (b & ~kH);  // bit 7: (a & 0x7f) >= (b & 0x7f), no borrows
+  return (~a & b) | (~(a ^ b) & ~d);
+}
+__device__ __forceinline__ uint32_t swar_sat_sub(uint32_t v, uint32_t t) {  // max(v - t, 0)
+  const uint32_t diff = ((v | kH) - (t & ~kH)) ^ ((v ^ ~t) & kH);
+  const uint32_t neg = ((swar_lt(v, t) & kH) >> 7) * 0xffu;
+  return diff & ~neg;
+}
+
+// A wave runs kCellsPerWave consecutive cells of one image: the next cell's tile is loaded
+// into registers while the current one is processed from LDS.
+constexpr int kCellsPerWave = 4;
+constexpr int kTileRegs = (18 * 66 + 63) / 64;  // dwords per lane for the largest cell view
+
+struct CellView {
+  int level, ini_x, ini_y, vw, vh, pitch, ax, off, nd;
+  const uint8_t* base;
+  bool aligned;
+};
+
+__device__ __forceinline__ CellView cell_view(const ImageBatch& b, const OrbGeom* g, int img,
+                                              int in_pitch, const uint4& d) {
+  CellView v;
+  v.level = (int)(int16_t)(d.x & 0xffff);
+  v.ini_x = (int)(int16_t)(d.x >> 16);
+  v.ini_y = (int)(int16_t)(d.y & 0xffff);
+  v.vw = (int)(int16_t)(d.y >> 16);
+  v.vh = (int)(int16_t)(d.z & 0xffff);
+  const LevelGeom& L = g->lv[v.level];
+  v.pitch = v.level == 0 ? in_pitch : L.pitch;
+  v.base = v.level == 0 ? batch_image(b, img) : b.pyr + (int64_t)img * g->pyr_bytes + L.offset;
+  v.ax = v.ini_x & ~3;
+  v.off = v.ini_x - v.ax;
+  v.nd = (v.vw + v.off + 3) >> 2;  // dwords per tile row (<= 18)
+  v.aligned = (((uintptr_t)v.base | (uintptr_t)v.pitch) & 3) == 0;
+  return v;
+}
+
+__device__ __forceinline__ uint4 readlane4(const uint4& x, int j) {
+  return make_uint4(__builtin_amdgcn_readlane(x.x, j), __builtin_amdgcn_readlane(x.y, j),
+                    __builtin_amdgcn_readlane(x.z, j), __builtin_amdgcn_readlane(x.w, j));
+}
+
 __global__ __launch_bounds__(256) void fast_cells_kernel(ImageBatch b,
                                                          const OrbGeom* __restrict__ g,
+                                                         const CellDesc* __restrict__ cells,
                                                          uint32_t* __restrict__ cell_keys,
                                                          int* __restrict__ cell_count,
                                                          uint32_t* __restrict__ err) {
   extern __shared__ __attribute__((aligned(16))) uint8_t s_fast[];
   const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int kTileStride = g->fast_tile_stride, kScoreStride = g->fast_score_stride;
-  const int kScoreRows = g->fast_score_rows;
   const int img = blockIdx.y;
-  const int cell = blockIdx.x * kCellWaves + wid;
-  if (cell >= g->cells_per_image) return;
-  int level = 0;
-  while (level + 1 < g->nlevels && cell >= g->lv[level + 1].cell_base) level++;
-  const LevelGeom& L = g->lv[level];
-  const int c = cell - L.cell_base;
-  const int ci = c / L.ncols, cj = c % L.ncols;
-  const int64_t slot = (int64_t)img * g->cells_per_image + cell;
-  // cell view bounds (:735-749), all integer valued
-  const int iniY = kMinBorder + ci * L.hcell;
-  const int iniX = kMinBorder + cj * L.wcell;
-  int maxY = iniY + L.hcell + 6, maxX = iniX + L.wcell + 6;
-  if (iniY >= L.max_by - 3 || iniX >= L.max_bx - 6) {
-    if (lane == 0) cell_count[slot] = 0;
-    return;
-  }
-  if (maxY > L.max_by) maxY = L.max_by;
-  if (maxX > L.max_bx) maxX = L.max_bx;
-  const int vh = maxY - iniY, vw = maxX - iniX;
-  const int dh = vh - 6, dw = vw - 6;  // detect area [3, vh-3) x [3, vw-3)
-  int pitch;
-  const uint8_t* base = level_ptr(b, g, img, level, &pitch);
+  const int ncells = g->cells_per_image;
+  const int c0 = (blockIdx.x * kCellWaves + wid) * kCellsPerWave;
+  if (c0 >= ncells) return;
+  const int nc = min(kCellsPerWave, ncells - c0);
+  const uint4 my_desc = lane < nc ? reinterpret_cast<const uint4*>(cells)[c0 + lane]
+                                  : make_uint4(0, 0, 0, 0);
+  const int in_pitch = __builtin_amdgcn_readfirstlane(b.in_pitch);
   uint8_t* tile = s_fast + wid * g->fast_lds_per_wave;
   uint8_t* sc = tile + ((kTileStride * g->fast_tile_rows + 15) & ~15);
-  uint16_t* cand = reinterpret_cast<uint16_t*>(sc + ((kScoreStride * kScoreRows + 15) & ~15));
-  // ---- tile load: aligned dwords covering [iniX & ~3, maxX), all issued before any LDS store
-  const int ax = iniX & ~3, off = iniX - ax;
-  const int nd = (vw + off + 3) >> 2;  // dwords per row (<= 18)
-  const int total = nd * vh;
-  const bool aligned = (((uintptr_t)base | (uintptr_t)pitch) & 3) == 0;
-  if (aligned) {
-    constexpr int kMaxPer = (18 * 66 + 63) / 64;  // wCell, hCell < 60
-    uint32_t v[kMaxPer];
-    int ro[kMaxPer];
-    // (row, dword) of element lane + 64k, stepped without divisions
-    const int dr = 64 / nd, dq = 64 - dr * nd;
-    int r = lane / nd, q = lane - (lane / nd) * nd;
+  uint16_t* cand =
+      reinterpret_cast<uint16_t*>(sc + ((kScoreStride * g->fast_score_rows + 15) & ~15));
+  const int tmin = min(g->ini_th, g->min_th);
+  const uint32_t tt = (uint32_t)tmin * 0x01010101u;
+
+  // ---- tile prefetch: aligned dwords covering [ini_x & ~3, ini_x + vw) x [ini_y, ini_y + vh)
+  // into registers (tile column c = image column ax + c). Elements past the end re-copy a
+  // last-row dword (same value, same place).
+  uint32_t tv[kTileRegs];
+  int tlo[kTileRegs];
+  int tn = 0;
+  auto prefetch = [&](const CellView& v) {
+    tn = __builtin_amdgcn_readfirstlane(v.aligned ? (v.nd * v.vh + 63) >> 6 : 0);  // uniform
+    const uint8_t* src = v.base + (int64_t)v.ini_y * v.pitch + v.ax;
+    const int dr = 64 / v.nd, dq = 64 - dr * v.nd;
+    int r = lane / v.nd, q = lane - (lane / v.nd) * v.nd;
 #pragma unroll
-    for (int k = 0; k < kMaxPer; k++) {
-      ro[k] = (r << 8) | q;
-      if (lane + 64 * k < total)
-        v[k] = *reinterpret_cast<const uint32_t*>(base + (int64_t)(iniY + r) * pitch + ax + 4 * q);
+    for (int k = 0; k < kTileRegs; k++) {
+      if (k < tn) {
+        const int rc = min(r, v.vh - 1);
+        tlo[k] = rc * kTileStride + 4 * q;
+        tv[k] = *reinterpret_cast<const uint32_t*>(src + (__umul24(rc, v.pitch) + 4 * q));
+      }
       r += dr;
       q += dq;
-      if (q >= nd) {
-        q -= nd;
+      if (q >= v.nd) {
+        q -= v.nd;
         r++;
       }
     }
+  };
+  CellView nxt = cell_view(b, g, img, in_pitch, readlane4(my_desc, 0));
+  if (nxt.vh > 0) prefetch(nxt);
+
+  for (int ci = 0; ci < nc; ci++) {
+    const CellView v = nxt;
+    const int64_t slot = (int64_t)img * ncells + c0 + ci;
+    if (v.vh == 0) {  // empty cell (:737, :745)
+      if (lane == 0) cell_count[slot] = 0;
+      if (ci + 1 < nc) {
+        nxt = cell_view(b, g, img, in_pitch, readlane4(my_desc, ci + 1));
+        if (nxt.vh > 0) prefetch(nxt);
+      }
+      continue;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();  // previous cell's LDS reads are done
+    if (v.aligned) {
 #pragma unroll
-    for (int k = 0; k < kMaxPer; k++)
-      if (lane + 64 * k < total)
-        *reinterpret_cast<uint32_t*>(tile + (ro[k] >> 8) * kTileStride + 4 * (ro[k] & 255)) = v[k];
-  } else {
-    for (int r = 0; r < vh; r++)
-      for (int x = lane; x < vw + off; x += 64)
-        tile[r * kTileStride + x] = base[(int64_t)(iniY + r) * pitch + ax + x];
-  }
-  // zero the score map (dwords)
-  for (int i = lane; i < (kScoreRows * kScoreStride + 3) / 4; i += 64)
-    reinterpret_cast<uint32_t*>(sc)[i] = 0;
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-  // ---- prefilter every detect pixel at the lower threshold; compact survivors (row-major)
-  const int tmin = min(g->ini_th, g->min_th);
-  const int wpad = dw <= 32 ? 32 : 64;
-  const int rows_per = 64 / wpad;
-  const int lr = lane / wpad, lc = lane % wpad;
-  int ncand = 0;
-  for (int r0 = 0; r0 < dh; r0 += rows_per) {
-    const int r = r0 + lr;
-    const bool in = r < dh && lc < dw;
-    const bool maybe =
-        in && fast_maybe(tile, (r + 3) * kTileStride + lc + 3 + off, tmin, kTileStride);
-    const uint64_t m = __ballot(maybe);
-    if (maybe) cand[ncand + lanes_below(m)] = (uint16_t)(r * kScoreStride + lc);
-    ncand += __popcll(m);
-  }
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-  // ---- exact FAST score of the survivors
-  int smax = 0;
-  for (int i = lane; i < ncand; i += 64) {
-    const int pix = cand[i];
-    const int r = pix / kScoreStride, cc = pix % kScoreStride;
-    const int s = fast_s(tile, (r + 3) * kTileStride + cc + 3 + off, kTileStride);
-    const int sv = s < 0 ? 0 : s;
-    sc[pix] = (uint8_t)sv;
-    smax = max(smax, sv);
-  }
-  smax = wave_max(smax);
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-  uint32_t* out = cell_keys + slot * g->cell_cap;
-  // FAST at iniTh; the reference re-runs at minTh when the iniTh *output* (after NMS) is empty
-  // (:753-757) -- corners can exist at iniTh and still all be suppressed by equal neighbours.
-  // Non-survivors of the prefilter have s <= tmin: never corners, score 0 for NMS.
-  int count = 0;
-  for (int pass = (smax > g->ini_th) ? 0 : 1; pass < 2 && count == 0; pass++) {
-    const int th = pass == 0 ? g->ini_th : g->min_th;
-    for (int i0 = 0; i0 < ncand; i0 += 64) {
-      const int i = i0 + lane;
-      bool keep = false;
-      int s = 0, r = 0, cc = 0;
-      if (i < ncand) {
-        const int pix = cand[i];
-        r = pix / kScoreStride;
-        cc = pix % kScoreStride;
-        s = sc[pix];
-        if (s > th) {
-          const int score = s - 1;
-          keep = true;
+      for (int k = 0; k < kTileRegs; k++)
+        if (k < tn) *reinterpret_cast<uint32_t*>(tile + tlo[k]) = tv[k];
+    } else {  // caller image with an odd pitch/base: byte copy
+      for (int r = 0; r < v.vh; r++)
+        for (int x = lane; x < v.vw + v.off; x += 64)
+          tile[r * kTileStride + x] = v.base[(int64_t)(v.ini_y + r) * v.pitch + v.ax + x];
+    }
+    if (ci + 1 < nc) {  // next cell's loads fly while this one is processed
+      nxt = cell_view(b, g, img, in_pitch, readlane4(my_desc, ci + 1));
+      if (nxt.vh > 0) prefetch(nxt);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    const int off = v.off;
+    const int dh = v.vh - 6, dw = v.vw - 6;  // detect area [3, vh-3) x [3, vw-3)
+    // ---- prefilter every detect pixel at the lower threshold, 4 pixels (one tile dword) per
+    // lane; writes the score map's zeros and compacts survivors in row-major order.
+    // Detect pixel (rr, col): tile row rr + 3, tile column col in [off + 3, off + 3 + dw).
+    const int q_lo = (off + 3) >> 2, q_hi = (off + 2 + dw) >> 2;
+    const int nq = q_hi - q_lo + 1;
+    const int rows_per = 64 / nq;
+    const int lr = lane / nq, Q = q_lo + (lane - lr * nq);
+    const int blo = max(0, off + 3 - 4 * Q), bhi = min(4, off + 3 + dw - 4 * Q);
+    const uint32_t vmask =
+        (uint32_t)(((1ull << (8 * bhi)) - 1) & ~((1ull << (8 * blo)) - 1)) & kH;
+    const int qm = max(Q - 1, 0) - Q;  // dword step left (clamped at the tile edge)
+    int ncand = 0;
+    for (int r0 = 0; r0 < dh; r0 += rows_per) {
+      const int rr = r0 + lr;
+      uint32_t m = 0;
+      if (lr < rows_per && rr < dh) {
+        const uint8_t* row = tile + (rr + 3) * kTileStride + 4 * Q;
+        auto rd = [&](int dy, int dq) {
+          return *reinterpret_cast<const uint32_t*>(row + dy * kTileStride + 4 * dq);
+        };
+        const uint32_t c = rd(0, 0), cm = rd(0, qm), cp = rd(0, 1);
+        const uint32_t u2 = rd(2, 0), u2m = rd(2, qm), u2p = rd(2, 1);
+        const uint32_t d2 = rd(-2, 0), d2m = rd(-2, qm), d2p = rd(-2, 1);
+        const uint32_t p0 = rd(3, 0), p8 = rd(-3, 0);
+        const uint32_t p4 = __builtin_amdgcn_alignbyte(cp, c, 3);     // (+3, 0)
+        const uint32_t p12 = __builtin_amdgcn_alignbyte(c, cm, 1);    // (-3, 0)
+        const uint32_t p2 = __builtin_amdgcn_alignbyte(u2p, u2, 2);   // (+2, +2)
+        const uint32_t p14 = __builtin_amdgcn_alignbyte(u2, u2m, 2);  // (-2, +2)
+        const uint32_t p6 = __builtin_amdgcn_alignbyte(d2p, d2, 2);   // (+2, -2)
+        const uint32_t p10 = __builtin_amdgcn_alignbyte(d2, d2m, 2);  // (-2, -2)
+        const uint32_t vlo = swar_sat_sub(c, tt);    // p darker  iff p < vlo
+        const uint32_t vhi = ~swar_sat_sub(~c, tt);  // p brighter iff p > vhi
+        const uint32_t dark = (swar_lt(p0, vlo) | swar_lt(p8, vlo)) &
+                              (swar_lt(p4, vlo) | swar_lt(p12, vlo)) &
+                              (swar_lt(p2, vlo) | swar_lt(p10, vlo)) &
+                              (swar_lt(p6, vlo) | swar_lt(p14, vlo));
+        const uint32_t bright = (swar_lt(vhi, p0) | swar_lt(vhi, p8)) &
+                                (swar_lt(vhi, p4) | swar_lt(vhi, p12)) &
+                                (swar_lt(vhi, p2) | swar_lt(vhi, p10)) &
+                                (swar_lt(vhi, p6) | swar_lt(vhi, p14));
+        m = (dark | bright) & vmask;
+        *reinterpret_cast<uint32_t*>(sc + rr * kScoreStride + 4 * Q) = 0;
+      }
+      // row-major compaction: exclusive prefix of per-lane counts (0..4) via 3 ballots
+      const int cnt = __popc(m);
+      const uint64_t b0 = __ballot(cnt & 1), b1 = __ballot(cnt & 2), b2 = __ballot(cnt & 4);
+      int pos = ncand + lanes_below(b0) + 2 * lanes_below(b1) + 4 * lanes_below(b2);
+      const int pix0 = rr * kScoreStride + 4 * Q;
 #pragma unroll
-          for (int dy = -1; dy <= 1; dy++)
+      for (int bb = 0; bb < 4; bb++)
+        if (m & (0x80u << (8 * bb))) cand[pos++] = (uint16_t)(pix0 + bb);
+      ncand += __popcll(b0) + 2 * __popcll(b1) + 4 * __popcll(b2);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    // ---- exact FAST score of the survivors
+    int smax = 0;
+    for (int i = lane; i < ncand; i += 64) {
+      const int pix = cand[i];
+      const int r = pix / kScoreStride, cc = pix - r * kScoreStride;
+      const int s = fast_s(tile, (r + 3) * kTileStride + cc, kTileStride);
+      const int sv = s < 0 ? 0 : s;
+      sc[pix] = (uint8_t)sv;
+      smax = max(smax, sv);
+    }
+    smax = wave_max(smax);
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    uint32_t* out = cell_keys + slot * g->cell_cap;
+    // FAST at iniTh; the reference re-runs at minTh when the iniTh *output* (after NMS) is
+    // empty (:753-757) -- corners can exist at iniTh and still all be suppressed by equal
+    // neighbours. Non-survivors of the prefilter have s <= tmin: never corners, score 0 for NMS.
+    int count = 0;
+    for (int pass = (smax > g->ini_th) ? 0 : 1; pass < 2 && count == 0; pass++) {
+      const int th = pass == 0 ? g->ini_th : g->min_th;
+      for (int i0 = 0; i0 < ncand; i0 += 64) {
+        const int i = i0 + lane;
+        bool keep = false;
+        int s = 0, r = 0, cc = 0;
+        if (i < ncand) {
+          const int pix = cand[i];
+          r = pix / kScoreStride;
+          cc = pix - r * kScoreStride;
+          s = sc[pix];
+          if (s > th) {
+            const int score = s - 1;
+            keep = true;
 #pragma unroll
-            for (int dx = -1; dx <= 1; dx++) {
-              if (dx == 0 && dy == 0) continue;
-              const int rr = r + dy, c2 = cc + dx;
-              int ns = 0;
-              if (rr >= 0 && rr < dh && c2 >= 0 && c2 < dw) {
-                const int q = sc[rr * kScoreStride + c2];
-                ns = q > th ? q - 1 : 0;
+            for (int dy = -1; dy <= 1; dy++)
+#pragma unroll
+              for (int dx = -1; dx <= 1; dx++) {
+                if (dx == 0 && dy == 0) continue;
+                const int rr = r + dy, c2 = cc + dx;
+                int ns = 0;
+                if (rr >= 0 && rr < dh && c2 >= off + 3 && c2 < off + 3 + dw) {
+                  const int q = sc[rr * kScoreStride + c2];
+                  ns = q > th ? q - 1 : 0;
+                }
+                keep = keep && (score > ns);
               }
-              keep = keep && (score > ns);
-            }
+          }
         }
-      }
-      const uint64_t m = __ballot(keep);
-      if (keep) {
-        const int pos = count + lanes_below(m);
-        if (pos < g->cell_cap) {
-          const int x_rel = iniX + 3 + cc - kMinBorder, y_rel = iniY + 3 + r - kMinBorder;
-          out[pos] = pack_key(x_rel, y_rel, s - 1);
+        const uint64_t m = __ballot(keep);
+        if (keep) {
+          const int pos = count + lanes_below(m);
+          if (pos < g->cell_cap) {
+            const int x_rel = v.ax + cc - kMinBorder, y_rel = v.ini_y + 3 + r - kMinBorder;
+            out[pos] = pack_key(x_rel, y_rel, s - 1);
+          }
         }
+        count += __popcll(m);
       }
-      count += __popcll(m);
     }
-  }
-  if (lane == 0) {
-    if (count > g->cell_cap) {
-      atomicOr(err, kErrCellOverflow);
-      count = g->cell_cap;
+    if (lane == 0) {
+      if (count > g->cell_cap) {
+        atomicOr(err, kErrCellOverflow);
+        count = g->cell_cap;
+      }
+      cell_count[slot] = count;
     }
-    cell_count[slot] = count;
   }
 }
 
@@ -1172,9 +1268,10 @@ void launch_extract(const ImageBatch& b, const OrbGeomDev& gd, int n_images, hip
   }
   SLAMGPU_LAUNCH("blur7", st, blur7_kernel, dim3(g.blur_tiles, n_images), dim3(256), 0, st, b, gd.dev);
   SLAMGPU_LAUNCH("fast_cells", st, fast_cells_kernel,
-                     dim3((g.cells_per_image + kCellWaves - 1) / kCellWaves, n_images),
-                     dim3(64 * kCellWaves), (size_t)kCellWaves * g.fast_lds_per_wave, st, b,
-                     gd.dev, gd.ws.cell_keys,
+                 dim3((g.cells_per_image + kCellWaves * kCellsPerWave - 1) /
+                          (kCellWaves * kCellsPerWave), n_images),
+                 dim3(64 * kCellWaves), (size_t)kCellWaves * g.fast_lds_per_wave, st, b,
+                 gd.dev, gd.cells, gd.ws.cell_keys,
                      gd.ws.cell_count, gd.ws.err);
   SLAMGPU_LAUNCH("octree", st, octree_kernel, dim3(g.nlevels, n_images), dim3(kOctThreads), 0, st, gd.dev,
                      gd.ws.cell_keys, gd.ws.cell_count, gd.ws.key_scratch, gd.ws.node_scratch,

@@ -28,5 +28,7 @@ void compute_tables(const OrbParams& p, OrbTables* t);
 // Returns 0 on success, <0 if the configuration is outside what the kernels support.
 int compute_geometry(const OrbParams& p, int cols, int rows, OrbGeom* g,
                      std::vector<ResizeX>* rx, std::vector<ResizeY>* ry);
+// FAST cell views of all levels, in the kernels' per-image cell order (cells_per_image entries).
+void build_cells(const OrbGeom& g, std::vector<CellDesc>* cells);
 
 }  // namespace slamgpu

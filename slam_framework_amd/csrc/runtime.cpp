@@ -38,7 +38,7 @@ struct slamgpu_ctx {
   OrbGeom* d_geom = nullptr;
   ResizeX* d_rx = nullptr;
   ResizeY* d_ry = nullptr;
-  int2* d_disc = nullptr;
+  CellDesc* d_cells = nullptr;
   // images staged by the host-buffer calls (left at d_in, right at d_in + in_stride)
   uint8_t* d_in = nullptr;
   int in_pitch = 0;
@@ -74,7 +74,7 @@ struct slamgpu_ctx {
     g.dev = d_geom;
     g.rx = d_rx;
     g.ry = d_ry;
-    g.disc = d_disc;
+    g.cells = d_cells;
     g.ws = ws;
     g.out = out;
     return g;
@@ -203,21 +203,14 @@ int slamgpu_create(int device, const slamgpu_orb_params* p, int cols, int rows, 
   TRY(dalloc(c, &c->d_geom, 1));
   TRY(dalloc(c, &c->d_rx, rx.size() + 1));
   TRY(dalloc(c, &c->d_ry, ry.size() + 1));
-  TRY(dalloc(c, &c->d_disc, kDiscPixels));
+  std::vector<CellDesc> cells;
+  build_cells(g, &cells);
+  TRY(dalloc(c, &c->d_cells, cells.size()));
   TRY(hcheck(c, hipMemcpy(c->d_geom, &g, sizeof(OrbGeom), hipMemcpyHostToDevice)));
   TRY(hcheck(c, hipMemcpy(c->d_rx, rx.data(), rx.size() * sizeof(ResizeX), hipMemcpyHostToDevice)));
   TRY(hcheck(c, hipMemcpy(c->d_ry, ry.data(), ry.size() * sizeof(ResizeY), hipMemcpyHostToDevice)));
-  // IC_Angle circular patch (orb_extractor.cpp:18-45): rows |v| <= 15, |u| <= umax[|v|]
-  std::vector<int2> disc;
-  for (int v = -kHalfPatch; v <= kHalfPatch; v++) {
-    const int d = g.umax[v < 0 ? -v : v];
-    for (int u = -d; u <= d; u++) disc.push_back(make_int2(u, v));
-  }
-  if ((int)disc.size() != kDiscPixels) {
-    *out = c;
-    return fail(c, SLAMGPU_EINVAL, "IC_Angle patch has %zu pixels", disc.size());
-  }
-  TRY(hcheck(c, hipMemcpy(c->d_disc, disc.data(), disc.size() * sizeof(int2), hipMemcpyHostToDevice)));
+  TRY(hcheck(c, hipMemcpy(c->d_cells, cells.data(), cells.size() * sizeof(CellDesc),
+                          hipMemcpyHostToDevice)));
   c->in_pitch = (cols + 63) / 64 * 64;
   c->in_stride = (int64_t)c->in_pitch * rows;
   TRY(dalloc(c, &c->d_in, 2 * (size_t)c->in_stride));

@@ -15,7 +15,8 @@ import os
 import numpy as np
 
 _PKG = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_PKG, "libslamgpu.so")
+# SLAMGPU_LIB: load another build of the same library (A/B kernel experiments under tools/).
+LIB_PATH = os.environ.get("SLAMGPU_LIB") or os.path.join(_PKG, "libslamgpu.so")
 
 KP_DTYPE = np.dtype([("x", "<f4"), ("y", "<f4"), ("size", "<f4"), ("angle", "<f4"),
                      ("response", "<f4"), ("octave", "<i4"), ("class_id", "<i4")])
