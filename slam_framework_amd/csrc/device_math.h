@@ -114,6 +114,11 @@ __device__ __forceinline__ int cv_round(float v) { return (int)rintf(v); }
 
 // ---- wavefront (64-lane) helpers --------------------------------------------------------
 __device__ __forceinline__ int lane_id() { return __lane_id(); }
+// Wave index inside the workgroup, as a scalar (the compiler cannot prove threadIdx.x >> 6 is
+// wave-uniform; without this every address derived from it is computed per lane).
+__device__ __forceinline__ int wave_id() {
+  return __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+}
 
 template <typename T>
 __device__ __forceinline__ T wave_min(T v) {

@@ -44,7 +44,7 @@ __device__ __forceinline__ const uint8_t* level_img(const ImageBatch& b, const O
 template <int CAP>
 __device__ int scan256(int* arr, int n, int* wsum) {
   constexpr int per = (CAP + 255) / 256;
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63, wid = wave_id();
   const int base = threadIdx.x * per;
   int loc[per];
   int s = 0;
@@ -126,7 +126,7 @@ __global__ __launch_bounds__(256) void stereo_match_kernel(ImageBatch b,
                                                            StereoWorkspace ws, StereoOut out) {
   const int f = blockIdx.y;
   const int lane = threadIdx.x & 63;
-  const int iL = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int iL = blockIdx.x * 4 + wave_id();
   const int il = 2 * f, ir = 2 * f + 1;
   const int nl = ext.n[il * ext.n_stride];
   if (iL >= nl) return;
@@ -488,7 +488,7 @@ __global__ __launch_bounds__(256) void search_cand_kernel(
     int th, GridWorkspace gw, MatchWorkspace mw, MatchIO io) {
   const int f = blockIdx.y;
   const int lane = threadIdx.x & 63;
-  const int qi = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int qi = blockIdx.x * 4 + wave_id();
   if (qi >= io.q_count[f]) return;
   const int q = io.q_start[f] + qi;
   FrameView F;

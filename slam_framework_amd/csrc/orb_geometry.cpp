@@ -182,6 +182,14 @@ int compute_geometry(const OrbParams& p, int cols, int rows, OrbGeom* g,
   g->blur_bytes = boff;
   g->blur_tiles = btiles;
   gauss_kernel_int(g->gauss);
+  {  // blur7_kernel packs taps into bytes and row sums into u16 (sum of taps <= 257)
+    int sum = 0;
+    for (int i = 0; i < 7; i++) {
+      if (g->gauss[i] < 0 || g->gauss[i] > 255 || g->gauss[i] != g->gauss[6 - i]) return -6;
+      sum += g->gauss[i];
+    }
+    if (sum > 257) return -6;
+  }
   // strict 8-neighbour NMS keeps at most one pixel per 2x2 block of the detect area
   g->cell_cap = ((max_wcell + 1) / 2) * ((max_hcell + 1) / 2);
   // tile: dwords covering the cell view from iniX & ~3, plus one spare dword per row for the

@@ -151,10 +151,20 @@ __global__ __launch_bounds__(256) void pyr_down_kernel(ImageBatch b, const OrbGe
 // (V + 32768) >> 16. Each thread owns 4 adjacent columns of a 32-row strip and slides a 7-row
 // window of row sums down it in registers (one aligned 12-byte read per input row, no LDS);
 // a 256-thread block covers 256 columns x 128 rows.
+// All sums are exact integers, so they map onto the dot-product ALU: a row sum is two
+// v_dot4_u32_u8 (taps 0-3 and 4-6 of the byte window), and since the taps {18,34,49,55,49,34,18}
+// sum to 257 a row sum is <= 65535, so the column sum is three v_dot2_u32_u16 over packed pairs
+// of consecutive row sums plus one multiply-add. The host checks those bounds (orb_geometry.cpp).
 __device__ __forceinline__ int reflect101(int i, int n) {
   if (i < 0) i = -i;
   if (i >= n) i = 2 * n - 2 - i;
   return i;
+}
+
+typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ uint32_t dot2u(uint32_t a, uint32_t b, uint32_t c) {
+  return __builtin_amdgcn_udot2(__builtin_bit_cast(u16x2, a), __builtin_bit_cast(u16x2, b), c,
+                                false);
 }
 
 constexpr int kBlurTileW = 256, kBlurTileH = 128, kBlurStrip = 32;
@@ -167,7 +177,7 @@ __global__ __launch_bounds__(256) void blur7_kernel(ImageBatch b, const OrbGeom*
   const LevelGeom& L = g->lv[level];
   tile -= L.blur_tile_base;
   const int tiles_x = (L.w + kBlurTileW - 1) / kBlurTileW;
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63, wid = wave_id();
   const int x = (tile % tiles_x) * kBlurTileW + 4 * lane;
   const int y0 = (tile / tiles_x) * kBlurTileH + wid * kBlurStrip;
   if (x >= L.w || y0 >= L.h) return;
@@ -175,62 +185,161 @@ __global__ __launch_bounds__(256) void blur7_kernel(ImageBatch b, const OrbGeom*
   const uint8_t* src = level_ptr(b, g, img, level, &spitch);
   uint8_t* dst = b.blur + (int64_t)img * g->blur_bytes + L.blur_offset;
   const int w = L.w, h = L.h;
-  const bool fast = x >= 4 && x + 8 <= w && (((uintptr_t)src | (uintptr_t)spitch) & 3) == 0;
-  const int k0 = g->gauss[0], k1 = g->gauss[1], k2 = g->gauss[2], k3 = g->gauss[3];
+  // Dword path for every lane of a 4-aligned image; lanes whose taps cross the left/right image
+  // border (x < 4 or x + 8 > w) load clamped in-bounds dwords and leave their columns to
+  // blur7_edges_kernel. Caller images with an odd base/pitch take the byte path everywhere
+  // (wave-uniform).
+  const bool fast = (((uintptr_t)src | (uintptr_t)spitch) & 3) == 0;
+  const bool edge = fast && (x < 4 || x + 8 > w);
+  const int xl = edge ? min(max(x, 4), (w - 8) & ~3) : x;
+  const uint32_t k0 = g->gauss[0], k1 = g->gauss[1], k2 = g->gauss[2], k3 = g->gauss[3];
+  const uint32_t KA = k0 | k1 << 8 | k2 << 16 | k3 << 24;  // taps 0..3
+  const uint32_t KB = k2 | k1 << 8 | k0 << 16;             // taps 4..6
+  const uint32_t K01 = k0 | k1 << 16, K23 = k2 | k3 << 16, K21 = k2 | k1 << 16;
+  // rounding: half-to-even inside the vector span, half-up in the scalar tail
   const bool vec_round = x < w - (w % 4);  // whole 4-column group on one side of xvec
+  const uint32_t rbias = vec_round ? 0x7fffu : 0x8000u, rodd = vec_round ? 1u : 0u;
   const int y1 = min(y0 + kBlurStrip, h);
-  int ring[7][4];
+  // pr[s][j]: (row sum of ring slot s, row sum of slot s+1) packed as u16 pairs
+  uint32_t pr[7][4], prev[4] = {0, 0, 0, 0};
+  // Rows are fetched a 7-row group at a time, branch-free (rows past the strip reflect back
+  // into the image and are never output), and the next group is in flight while the current
+  // one is filtered.
+  uint32_t cur[7][3], nxt[7][3];
+  auto fetch = [&](int r0, uint32_t (&buf)[7][3]) {
+#pragma unroll
+    for (int k = 0; k < 7; k++) {
+      const uint8_t* row = src + (int64_t)reflect101(r0 + k, h) * spitch;
+      if (fast) {
+        buf[k][0] = *reinterpret_cast<const uint32_t*>(row + xl - 4);
+        buf[k][1] = *reinterpret_cast<const uint32_t*>(row + xl);
+        buf[k][2] = *reinterpret_cast<const uint32_t*>(row + xl + 4);
+      } else {  // bytes x-3 .. x+6 with reflect-101 columns
+        uint32_t wv[3] = {0, 0, 0};
+#pragma unroll
+        for (int i = 1; i <= 10; i++)
+          wv[i >> 2] |= (uint32_t)row[reflect101(x - 4 + i, w)] << (8 * (i & 3));
+        buf[k][0] = wv[0];
+        buf[k][1] = wv[1];
+        buf[k][2] = wv[2];
+      }
+    }
+  };
+  fetch(y0 - 3, cur);
   // input rows y0-3 .. y1+2; output row r-3 once 7 rows are in the ring
   for (int r0 = y0 - 3; r0 < y1 + 3; r0 += 7) {
+    if (r0 + 7 < y1 + 3) fetch(r0 + 7, nxt);
 #pragma unroll
     for (int k = 0; k < 7; k++) {
       const int r = r0 + k;
       if (r < y1 + 3) {
-        const uint8_t* row = src + (int64_t)reflect101(r, h) * spitch;
-        int px[10];  // columns x-3 .. x+6
-        if (fast) {
-          const uint32_t w0 = *reinterpret_cast<const uint32_t*>(row + x - 4);
-          const uint32_t w1 = *reinterpret_cast<const uint32_t*>(row + x);
-          const uint32_t w2 = *reinterpret_cast<const uint32_t*>(row + x + 4);
-          px[0] = (w0 >> 8) & 0xff;
-          px[1] = (w0 >> 16) & 0xff;
-          px[2] = w0 >> 24;
-          px[3] = w1 & 0xff;
-          px[4] = (w1 >> 8) & 0xff;
-          px[5] = (w1 >> 16) & 0xff;
-          px[6] = w1 >> 24;
-          px[7] = w2 & 0xff;
-          px[8] = (w2 >> 8) & 0xff;
-          px[9] = (w2 >> 16) & 0xff;
-        } else {
+        const uint32_t w0 = cur[k][0], w1 = cur[k][1], w2 = cur[k][2];  // bytes x-4 .. x+7
+        uint32_t n[4];
 #pragma unroll
-          for (int i = 0; i < 10; i++) px[i] = row[reflect101(x - 3 + i, w)];
+        for (int j = 0; j < 4; j++) {  // 7-tap window starts at byte x - 3 + j
+          const uint32_t lo = j == 3 ? w1 : __builtin_amdgcn_alignbyte(w1, w0, j + 1);
+          const uint32_t hi = j == 3 ? w2 : __builtin_amdgcn_alignbyte(w2, w1, j + 1);
+          n[j] = __builtin_amdgcn_udot4(lo, KA, __builtin_amdgcn_udot4(hi, KB, 0u, false), false);
+          pr[(k + 6) % 7][j] = prev[j] | n[j] << 16;
+          prev[j] = n[j];
         }
-#pragma unroll
-        for (int j = 0; j < 4; j++)
-          ring[k][j] = k3 * px[j + 3] + k2 * (px[j + 2] + px[j + 4]) +
-                       k1 * (px[j + 1] + px[j + 5]) + k0 * (px[j] + px[j + 6]);
         const int yo = r - 3;  // output row whose window ends at input row r
         if (yo >= y0) {
           uint32_t packed = 0;
 #pragma unroll
           for (int j = 0; j < 4; j++) {
-            const int v = k3 * ring[(k + 4) % 7][j] +
-                          k2 * (ring[(k + 3) % 7][j] + ring[(k + 5) % 7][j]) +
-                          k1 * (ring[(k + 2) % 7][j] + ring[(k + 6) % 7][j]) +
-                          k0 * (ring[(k + 1) % 7][j] + ring[k][j]);
-            int o = vec_round ? (int)rintf((float)v * (1.0f / 65536.0f)) : ((v + 32768) >> 16);
-            o = o < 0 ? 0 : (o > 255 ? 255 : o);
-            packed |= (uint32_t)o << (8 * j);
+            // window rows w0..w6 = slots k+1 .. k: (w0,w1), (w2,w3), (w4,w5) pairs, then w6
+            uint32_t v = dot2u(pr[(k + 1) % 7][j], K01, 0u);
+            v = dot2u(pr[(k + 3) % 7][j], K23, v);
+            v = dot2u(pr[(k + 5) % 7][j], K21, v);
+            v += k0 * n[j];
+            uint32_t o = (v + rbias + __builtin_amdgcn_ubfe(v, 16, rodd)) >> 16;
+            o = o > 255u ? 255u : o;
+            packed |= o << (8 * j);
           }
           uint8_t* drow = dst + (int64_t)yo * L.pitch;
-          if (x + 4 <= w) {
-            *reinterpret_cast<uint32_t*>(drow + x) = packed;
-          } else {
-            for (int j = 0; x + j < w; j++) drow[x + j] = (uint8_t)(packed >> (8 * j));
+          if (!edge) {
+            if (x + 4 <= w) {
+              *reinterpret_cast<uint32_t*>(drow + x) = packed;
+            } else {
+              for (int j = 0; x + j < w; j++) drow[x + j] = (uint8_t)(packed >> (8 * j));
+            }
           }
         }
       }
+    }
+#pragma unroll
+    for (int k = 0; k < 7; k++)
+#pragma unroll
+      for (int e = 0; e < 3; e++) cur[k][e] = nxt[k][e];
+  }
+}
+
+// blur7_edges: the columns blur7_kernel's dword path leaves out (the 4-column groups with
+// x < 4 or x + 8 > w), reflect-101 in both directions. One wave per (image, level, 32-row
+// strip): the 38 input rows' reflected edge bytes (13 per row and side) are staged in LDS with
+// coalesced loads, then lane (row, side) filters its <= 7 columns from registers.
+constexpr int kEdgeStrip = 32;
+
+__global__ __launch_bounds__(64) void blur7_edges_kernel(ImageBatch b, const OrbGeom* __restrict__ g) {
+  __shared__ __attribute__((aligned(16))) uint8_t s_e[kEdgeStrip + 6][2][16];
+  const int img = blockIdx.y, lane = threadIdx.x;
+  int strip = blockIdx.x, level = 0;
+  while (level < g->nlevels && strip >= (g->lv[level].h + kEdgeStrip - 1) / kEdgeStrip) {
+    strip -= (g->lv[level].h + kEdgeStrip - 1) / kEdgeStrip;
+    level++;
+  }
+  if (level >= g->nlevels) return;
+  const LevelGeom& L = g->lv[level];
+  const int w = L.w, h = L.h;
+  int spitch;
+  const uint8_t* src = level_ptr(b, g, img, level, &spitch);
+  if ((((uintptr_t)src | (uintptr_t)spitch) & 3) != 0) return;  // byte path covered it
+  const int y0 = strip * kEdgeStrip;
+  const int xr = ((w - 8) & ~3) + 4;  // first 4-aligned group with x + 8 > w
+  // stage: element j -> (row j / 26, side (j / 13) & 1, byte j % 13) = column c0 - 3 + byte
+  for (int j = lane; j < (kEdgeStrip + 6) * 26; j += 64) {
+    const int r = j / 26, rem = j - r * 26, side = rem >= 13, bt = rem - 13 * side;
+    const int c0 = side ? xr : 0;
+    const uint8_t* row = src + (int64_t)reflect101(y0 - 3 + r, h) * spitch;
+    s_e[r][side][bt] = row[reflect101(c0 - 3 + bt, w)];
+  }
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+  __syncthreads();
+  const int r = lane >> 1, side = lane & 1, y = y0 + r;
+  if (y >= h) return;
+  const int c0 = side ? xr : 0, nc = side ? w - xr : 4;  // nc <= 7
+  uint32_t pk[7][4];
+#pragma unroll
+  for (int dy = 0; dy < 7; dy++) {
+    const uint4 q = *reinterpret_cast<const uint4*>(&s_e[r + dy][side][0]);
+    pk[dy][0] = q.x;
+    pk[dy][1] = q.y;
+    pk[dy][2] = q.z;
+    pk[dy][3] = q.w & 0xffu;  // byte 12 only
+  }
+  const uint32_t k0 = g->gauss[0], k1 = g->gauss[1], k2 = g->gauss[2], k3 = g->gauss[3];
+  const uint32_t KA = k0 | k1 << 8 | k2 << 16 | k3 << 24, KB = k2 | k1 << 8 | k0 << 16;
+  const uint32_t kv[7] = {k0, k1, k2, k3, k2, k1, k0};
+  uint8_t* drow = b.blur + (int64_t)img * g->blur_bytes + L.blur_offset + (int64_t)y * L.pitch;
+#pragma unroll
+  for (int m = 0; m < 7; m++) {  // output column c0 + m: taps at local bytes m .. m+6
+    if (m < nc) {
+      uint32_t v = 0;
+#pragma unroll
+      for (int dy = 0; dy < 7; dy++) {
+        const uint32_t lo = (m & 3) == 0 ? pk[dy][m >> 2]
+                                         : __builtin_amdgcn_alignbyte(pk[dy][(m >> 2) + 1],
+                                                                      pk[dy][m >> 2], m & 3);
+        const uint32_t hi = (m & 3) == 0 ? pk[dy][(m >> 2) + 1]
+                                         : __builtin_amdgcn_alignbyte(pk[dy][(m >> 2) + 2],
+                                                                      pk[dy][(m >> 2) + 1], m & 3);
+        v += kv[dy] * __builtin_amdgcn_udot4(lo, KA, __builtin_amdgcn_udot4(hi, KB, 0u, false), false);
+      }
+      const int c = c0 + m;
+      const uint32_t o = (c & ~3) < w - (w % 4) ? (v + 0x7fffu + ((v >> 16) & 1u)) >> 16
+                                                : (v + 0x8000u) >> 16;
+      drow[c] = (uint8_t)(o > 255u ? 255u : o);
     }
   }
 }
@@ -358,7 +467,7 @@ __global__ __launch_bounds__(256) void fast_cells_kernel(ImageBatch b,
                                                          int* __restrict__ cell_count,
                                                          uint32_t* __restrict__ err) {
   extern __shared__ __attribute__((aligned(16))) uint8_t s_fast[];
-  const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int wid = wave_id(), lane = threadIdx.x & 63;
   const int kTileStride = g->fast_tile_stride, kScoreStride = g->fast_score_stride;
   const int img = blockIdx.y;
   const int ncells = g->cells_per_image;
@@ -585,7 +694,7 @@ struct OctShared {
 
 // Block-wide exclusive scan of v (one value per thread); returns prefix, *total gets the sum.
 __device__ __forceinline__ int block_scan(int v, int* wsum, int* total) {
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63, wid = wave_id();
   int x = v;
 #pragma unroll
   for (int off = 1; off < 64; off <<= 1) {
@@ -1080,7 +1189,7 @@ __global__ __launch_bounds__(256) void orient_desc_kernel(
     img = xcd + 8 * (j / bpi);
     bx = j % bpi;
   }
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63, wid = wave_id();
   int lcount[kMaxLevels];
   int total = 0;
   for (int l = 0; l < g->nlevels; l++) {
@@ -1267,6 +1376,12 @@ void launch_extract(const ImageBatch& b, const OrbGeomDev& gd, int n_images, hip
                    gd.ry);
   }
   SLAMGPU_LAUNCH("blur7", st, blur7_kernel, dim3(g.blur_tiles, n_images), dim3(256), 0, st, b, gd.dev);
+  {
+    int strips = 0;
+    for (int l = 0; l < g.nlevels; l++) strips += (g.lv[l].h + kEdgeStrip - 1) / kEdgeStrip;
+    SLAMGPU_LAUNCH("blur7_edges", st, blur7_edges_kernel, dim3(strips, n_images), dim3(64), 0, st,
+                   b, gd.dev);
+  }
   SLAMGPU_LAUNCH("fast_cells", st, fast_cells_kernel,
                  dim3((g.cells_per_image + kCellWaves * kCellsPerWave - 1) /
                           (kCellWaves * kCellsPerWave), n_images),
