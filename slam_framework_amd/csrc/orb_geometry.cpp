@@ -202,12 +202,13 @@ int compute_geometry(const OrbParams& p, int cols, int rows, OrbGeom* g,
                          round_up(g->fast_score_stride * g->fast_score_rows, 16) +
                          round_up(2 * g->fast_score_stride * g->fast_score_rows, 16);
   if (max_wcell > 64) return -4;
-  // pyr_down stages the source rows of 4 output rows (kPyrBand) in <= 16 LDS rows
+  // pyr_down reads the source bytes of 4 adjacent output columns as one 8-byte window
+  // starting at sx(x0): sx(x0 + 3) + 1 - sx(x0) <= 7 (any scale factor up to ~2).
   for (int l = 1; l < p.nlevels; l++) {
     const LevelGeom& L = g->lv[l];
-    for (int dy0 = 0; dy0 < L.h; dy0 += 4) {
-      const int dy1 = std::min(dy0 + 4, L.h);
-      if ((*ry)[L.ry_base + dy1 - 1].y1 - (*ry)[L.ry_base + dy0].y0 + 1 > 16) return -5;
+    for (int x0 = 0; x0 < L.w; x0 += 4) {
+      const int x3 = std::min(x0 + 3, L.w - 1);
+      if ((*rx)[L.rx_base + x3].sx - (*rx)[L.rx_base + x0].sx > 6) return -5;
     }
   }
   g->pyr_bytes = pyr_off;

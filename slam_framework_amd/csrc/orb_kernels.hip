@@ -37,110 +37,126 @@ __device__ __forceinline__ const uint8_t* level_ptr(const ImageBatch& b, const O
 // ---------------------------------------------------------------------------------------
 // pyr_down: ComputePyramid (:1051-1075) -> cv::resize(level l-1, level l, INTER_LINEAR).
 // HResizeLinear (int = S[sx]*a0 + S[sx+1]*a1, or S[sx]*2048 from xmax on) then VResizeLinear
-// ((b0*(r0>>4))>>16) + ((b1*(r1>>4))>>16) + 2) >> 2. A block produces a band of kPyrBand output
-// rows: the source rows it needs are staged into LDS with coalesced dword loads, then every
-// thread produces 4 adjacent output pixels per row from LDS.
-constexpr int kPyrBand = 4;
-constexpr int kPyrSrcRows = 16;  // source rows staged per band (host checks the scale fits)
+// ((b0*(r0>>4))>>16) + ((b1*(r1>>4))>>16) + 2) >> 2.
+// A lane owns 4 adjacent output columns and walks a 16-row strip. Each source row is fetched
+// once (3 dwords, in prefetched chunks of 4 rows) and its horizontal pass is computed once: the
+// 8-byte window starting at sx(x0) (host-checked to hold all 4 columns' pixel pairs) is cut with
+// two alignbytes, v_perm turns each column's pixel pair into a u16 pair and v_dot2_u32_u16
+// applies (a0, a1). An output row combines the current and previous source rows' results.
+typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ uint32_t dot2u(uint32_t a, uint32_t b, uint32_t c) {
+  return __builtin_amdgcn_udot2(__builtin_bit_cast(u16x2, a), __builtin_bit_cast(u16x2, b), c,
+                                false);
+}
+
+constexpr int kPyrStrip = 16;  // output rows per wave
+constexpr int kPyrChunk = 4;   // source rows fetched per batch
 
 __global__ __launch_bounds__(256) void pyr_down_kernel(ImageBatch b, const OrbGeom* __restrict__ g,
                                                        int level,
                                                        const ResizeX* __restrict__ rxt,
                                                        const ResizeY* __restrict__ ryt) {
-  extern __shared__ __attribute__((aligned(16))) uint8_t s_src[];
   const int img = blockIdx.y;
+  const int lane = threadIdx.x & 63, wid = wave_id();
   const LevelGeom& D = g->lv[level];
   const LevelGeom& S = g->lv[level - 1];
-  const int dy0 = blockIdx.x * kPyrBand;
-  const int dy1 = min(dy0 + kPyrBand, D.h);
-  const int sy_lo = ryt[D.ry_base + dy0].y0;
-  const int sy_hi = ryt[D.ry_base + dy1 - 1].y1;
-  const int nsr = sy_hi - sy_lo + 1;
-  const int sstride = (S.w + 3) & ~3;
+  const int tiles_x = (D.w + 255) >> 8;
+  const int tx = blockIdx.x % tiles_x, ty = blockIdx.x / tiles_x;
+  const int dy0 = (ty * 4 + wid) * kPyrStrip;
+  if (dy0 >= D.h) return;
+  const int nrows = min(kPyrStrip, D.h - dy0);
+  // the strip's row table, one entry per lane (read back with readlane)
+  int ry_y0 = 0, ry_y1 = 0, ry_b = 0;
+  if (lane < nrows) {
+    const ResizeY e = ryt[D.ry_base + dy0 + lane];
+    ry_y0 = e.y0;
+    ry_y1 = e.y1;
+    ry_b = (int)(uint16_t)e.b0 | (int)e.b1 << 16;
+  }
+  const int sy_lo = __builtin_amdgcn_readlane(ry_y0, 0);
+  const int sy_hi = __builtin_amdgcn_readlane(ry_y1, nrows - 1);
+  // per-lane column constants
+  const int x0 = (tx << 8) + 4 * lane;
+  int s0 = 0;
+  uint32_t sel[4], A[4];
+#pragma unroll
+  for (int k = 0; k < 4; k++) {
+    const int dx = min(x0 + k, D.w - 1);
+    const ResizeX e = rxt[D.rx_base + dx];
+    if (k == 0) s0 = e.sx;
+    const uint32_t bk = (uint32_t)min(e.sx - s0, 6);
+    sel[k] = bk | 0x0c00u | (bk + 1) << 16 | 0x0c000000u;  // bytes bk, bk+1 -> u16 lanes
+    A[k] = dx < D.xmax ? ((uint32_t)(uint16_t)e.a0 | (uint32_t)(uint16_t)e.a1 << 16) : 2048u;
+  }
+  const int q0 = s0 >> 2, sh = s0 & 3, qmax = (S.w - 1) >> 2;
   int spitch;
   const uint8_t* src = level_ptr(b, g, img, level - 1, &spitch);
-  const int tid = threadIdx.x;
-  const int nd = sstride >> 2;
-  if ((((uintptr_t)src | (uintptr_t)spitch) & 3) == 0) {
-    // issue 8 dword loads per thread before the first LDS store (memory-level parallelism)
-    for (int i0 = tid; i0 < nsr * nd; i0 += 8 * 256) {
-      uint32_t v[8];
+  const bool aligned = (((uintptr_t)src | (uintptr_t)spitch) & 3) == 0;
+  const int qa = min(q0, qmax), qb = min(q0 + 1, qmax), qc = min(q0 + 2, qmax);
+  auto fetch = [&](int sy, uint32_t (&wv)[3]) {
+    const uint8_t* row = src + (int64_t)min(sy, sy_hi) * spitch;
+    if (aligned) {  // clamped dwords stay inside the row; bytes past sx+1 carry zero weight
+      wv[0] = *reinterpret_cast<const uint32_t*>(row + 4 * qa);
+      wv[1] = *reinterpret_cast<const uint32_t*>(row + 4 * qb);
+      wv[2] = *reinterpret_cast<const uint32_t*>(row + 4 * qc);
+    } else {
 #pragma unroll
-      for (int k = 0; k < 8; k++) {
-        const int i = i0 + 256 * k;
-        if (i < nsr * nd) {
-          const int r = i / nd, q = i - r * nd;
-          v[k] = *reinterpret_cast<const uint32_t*>(src + (int64_t)(sy_lo + r) * spitch + 4 * q);
+      for (int i = 0; i < 3; i++) {
+        uint32_t v = 0;
+#pragma unroll
+        for (int j = 0; j < 4; j++) v |= (uint32_t)row[min(4 * (q0 + i) + j, S.w - 1)] << (8 * j);
+        wv[i] = v;
+      }
+    }
+  };
+  uint8_t* dst = b.pyr + (int64_t)img * g->pyr_bytes + D.offset;
+  uint32_t cur[kPyrChunk][3], nxt[kPyrChunk][3];
+#pragma unroll
+  for (int j = 0; j < kPyrChunk; j++) fetch(sy_lo + j, cur[j]);
+  uint32_t hp[4] = {0, 0, 0, 0}, hc[4] = {0, 0, 0, 0};
+  int nd = 0;  // next strip row to emit
+  for (int c0 = sy_lo; c0 <= sy_hi; c0 += kPyrChunk) {
+    if (c0 + kPyrChunk <= sy_hi) {
+#pragma unroll
+      for (int j = 0; j < kPyrChunk; j++) fetch(c0 + kPyrChunk + j, nxt[j]);
+    }
+#pragma unroll
+    for (int j = 0; j < kPyrChunk; j++) {
+      const int sy = c0 + j;
+      if (sy <= sy_hi) {
+        const uint32_t W0 = __builtin_amdgcn_alignbyte(cur[j][1], cur[j][0], sh);
+        const uint32_t W1 = __builtin_amdgcn_alignbyte(cur[j][2], cur[j][1], sh);
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+          hp[k] = hc[k];
+          hc[k] = dot2u(__builtin_amdgcn_perm(W1, W0, sel[k]), A[k], 0u);
+        }
+        // emit the strip rows whose lower source row is sy (rows are in y1 order)
+        while (nd < nrows && __builtin_amdgcn_readlane(ry_y1, nd) == sy) {
+          const bool same = __builtin_amdgcn_readlane(ry_y0, nd) == sy;
+          const uint32_t bb = (uint32_t)__builtin_amdgcn_readlane(ry_b, nd);
+          const uint32_t b0 = bb & 0xffffu, b1 = bb >> 16;
+          uint32_t packed = 0;
+#pragma unroll
+          for (int k = 0; k < 4; k++) {
+            const uint32_t r0 = (same ? hc[k] : hp[k]) >> 4, r1 = hc[k] >> 4;
+            const uint32_t v = (((b0 * r0) >> 16) + ((b1 * r1) >> 16) + 2) >> 2;
+            packed |= (v & 0xffu) << (8 * k);
+          }
+          uint8_t* drow = dst + (int64_t)(dy0 + nd) * D.pitch;
+          if (x0 + 4 <= D.w) {
+            *reinterpret_cast<uint32_t*>(drow + x0) = packed;  // pitch is a multiple of 64
+          } else {
+            for (int k = 0; x0 + k < D.w; k++) drow[x0 + k] = (uint8_t)(packed >> (8 * k));
+          }
+          nd++;
         }
       }
-#pragma unroll
-      for (int k = 0; k < 8; k++) {
-        const int i = i0 + 256 * k;
-        if (i < nsr * nd) {
-          const int r = i / nd, q = i - r * nd;
-          *reinterpret_cast<uint32_t*>(s_src + r * sstride + 4 * q) = v[k];
-        }
-      }
-    }
-  } else {
-    for (int i = tid; i < nsr * sstride; i += 256) {
-      const int r = i / sstride, q = i - r * sstride;
-      s_src[i] = q < S.w ? src[(int64_t)(sy_lo + r) * spitch + q] : 0;
-    }
-  }
-  __syncthreads();
-  const int groups = (D.w + 3) >> 2;
-  const int nitems = (dy1 - dy0) * groups;
-  // items (row, 4-pixel group) are processed 4 per thread at a time with all table loads issued
-  // before the first dependent LDS read
-  for (int base = tid; base < nitems; base += 4 * 256) {
-    ResizeX ex[4][4];
-    ResizeY ey[4];
-    int dyv[4], x0v[4];
-#pragma unroll
-    for (int u = 0; u < 4; u++) {
-      const int item = base + 256 * u;
-      const int it = item < nitems ? item : 0;
-      const int rr = it / groups;
-      dyv[u] = dy0 + rr;
-      x0v[u] = (it - rr * groups) * 4;
-      ey[u] = ryt[D.ry_base + dyv[u]];
-#pragma unroll
-      for (int k = 0; k < 4; k++) {
-        const int dx = min(x0v[u] + k, D.w - 1);
-        ex[u][k] = rxt[D.rx_base + dx];
-      }
     }
 #pragma unroll
-    for (int u = 0; u < 4; u++) {
-      const int item = base + 256 * u;
-      if (item >= nitems) break;
-      const int x0 = x0v[u], dy = dyv[u];
-      const uint8_t* S0 = s_src + (ey[u].y0 - sy_lo) * sstride;
-      const uint8_t* S1 = s_src + (ey[u].y1 - sy_lo) * sstride;
-      uint8_t* dst = b.pyr + (int64_t)img * g->pyr_bytes + D.offset + (int64_t)dy * D.pitch;
-      uint32_t packed = 0;
+    for (int j = 0; j < kPyrChunk; j++)
 #pragma unroll
-      for (int k = 0; k < 4; k++) {
-        const int dx = x0 + k;
-        const ResizeX e = ex[u][k];
-        int r0, r1;
-        if (dx < D.xmax) {
-          r0 = S0[e.sx] * e.a0 + S0[e.sx + 1] * e.a1;
-          r1 = S1[e.sx] * e.a0 + S1[e.sx + 1] * e.a1;
-        } else {
-          r0 = S0[e.sx] * 2048;
-          r1 = S1[e.sx] * 2048;
-        }
-        const int v = (((ey[u].b0 * (r0 >> 4)) >> 16) + ((ey[u].b1 * (r1 >> 4)) >> 16) + 2) >> 2;
-        packed |= (uint32_t)(v & 0xff) << (8 * k);
-      }
-      if (x0 + 4 <= D.w) {
-        *reinterpret_cast<uint32_t*>(dst + x0) = packed;  // pitch is a multiple of 64
-      } else {
-        for (int k = 0; x0 + k < D.w; k++) dst[x0 + k] = (uint8_t)(packed >> (8 * k));
-      }
-    }
+      for (int e = 0; e < 3; e++) cur[j][e] = nxt[j][e];
   }
 }
 
@@ -159,12 +175,6 @@ __device__ __forceinline__ int reflect101(int i, int n) {
   if (i < 0) i = -i;
   if (i >= n) i = 2 * n - 2 - i;
   return i;
-}
-
-typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
-__device__ __forceinline__ uint32_t dot2u(uint32_t a, uint32_t b, uint32_t c) {
-  return __builtin_amdgcn_udot2(__builtin_bit_cast(u16x2, a), __builtin_bit_cast(u16x2, b), c,
-                                false);
 }
 
 constexpr int kBlurTileW = 256, kBlurTileH = 128, kBlurStrip = 32;
@@ -1370,10 +1380,9 @@ __global__ __launch_bounds__(256) void orient_desc_kernel(
 void launch_extract(const ImageBatch& b, const OrbGeomDev& gd, int n_images, hipStream_t st) {
   const OrbGeom& g = *gd.host;
   for (int l = 1; l < g.nlevels; l++) {
-    dim3 grid((g.lv[l].h + kPyrBand - 1) / kPyrBand, n_images);
-    const size_t lds = (size_t)kPyrSrcRows * ((g.lv[l - 1].w + 3) & ~3);
-    SLAMGPU_LAUNCH("pyr_down", st, pyr_down_kernel, grid, dim3(256), lds, st, b, gd.dev, l, gd.rx,
-                   gd.ry);
+    const int tiles = ((g.lv[l].w + 255) >> 8) * ((g.lv[l].h + 4 * kPyrStrip - 1) / (4 * kPyrStrip));
+    SLAMGPU_LAUNCH("pyr_down", st, pyr_down_kernel, dim3(tiles, n_images), dim3(256), 0, st, b,
+                   gd.dev, l, gd.rx, gd.ry);
   }
   SLAMGPU_LAUNCH("blur7", st, blur7_kernel, dim3(g.blur_tiles, n_images), dim3(256), 0, st, b, gd.dev);
   {
