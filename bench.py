@@ -132,7 +132,7 @@ def main():
           f"matches/frame {nm[1:5].tolist()}", file=sys.stderr)
 
     # ---- per-kernel breakdown pass (untimed) to pick the dominant kernel
-    names = ["pyr_down", "blur7", "blur7_edges", "fast_cells", "octree", "orient_desc", "stereo_rows",
+    names = ["pyr_down", "blur7", "blur7_edges", "fast_cells", "octree", "octree_global", "orient_desc", "stereo_rows",
              "stereo_match", "stereo_median", "grid_build", "vo_queries", "search_cand",
              "search_resolve"]
     ctx.timing_start("*", 4096)

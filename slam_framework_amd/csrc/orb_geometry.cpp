@@ -227,6 +227,11 @@ int compute_geometry(const OrbParams& p, int cols, int rows, OrbGeom* g,
   }
   g->keys_per_image = key_off;
   g->nodes_per_image = node_off;
+  {
+    int nc = 0;
+    for (int l = 0; l < p.nlevels; l++) nc = std::max(nc, g->lv[l].node_cap);
+    g->oct_nc = round_up(nc, 64);
+  }
   g->out_per_image = out_off;
   g->kp_cap = out_off;
   return 0;

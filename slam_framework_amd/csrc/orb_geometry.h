@@ -66,6 +66,7 @@ struct OrbGeom {
   int gauss[7];          // GaussianBlur 7x7 sigma 2 integer kernel (x256)
   int64_t keys_per_image;
   int64_t nodes_per_image;
+  int oct_nc;            // LDS node-list capacity of octree_lds_kernel (max node_cap, rounded)
   int out_per_image;     // sum of out_cap
   int kp_cap;            // max keypoints per image after Compute (== out_per_image)
   int umax[16];

@@ -823,6 +823,7 @@ __global__ __launch_bounds__(kOctThreads) void octree_kernel(
   OctNode* const child = node_scratch + img * g->nodes_per_image + L.node_base + 4 * L.node_cap;
   int* const outc = oct_count + img * g->nlevels + level;
   uint32_t* const outk = oct_keys + (int64_t)img * g->out_per_image + L.out_base;
+  if (*outc != -1) return;  // done by octree_lds_kernel
 
   // ---- 1. gather FAST candidates in cell row-major order into keys[0]
   for (int c0 = 0; c0 < ncell; c0 += kOctCap) {
@@ -1138,6 +1139,457 @@ __global__ __launch_bounds__(kOctThreads) void octree_kernel(
 }
 
 // ---------------------------------------------------------------------------------------
+// octree_lds: the same DistributeOctTree with every pass in LDS. Keys live in one LDS buffer and
+// a division partitions its node's key range in place through registers (a lane per node for
+// n <= 8, a wave per node for n <= 2048); node lists are compact 16-byte nodes in LDS. A pass is
+//   count (children per node) -> block scans -> divide + place children at their final list
+//   positions,
+// so no child array exists. Work-groups whose candidates exceed kOctLdsKeys, or whose initial
+// nodes exceed kOctWaveKeys, mark oct_count = -1 and octree_kernel (global memory) redoes them.
+constexpr int kOctLdsKeys = 4096;
+constexpr int kOctWaveRegs = 32;
+constexpr int kOctWaveKeys = 64 * kOctWaveRegs;
+constexpr int kOctLaneKeys = 8;
+
+struct OctNodeC {
+  int16_t x0, x1, y0, y1;
+  uint16_t kbeg, n;
+  int32_t seq;
+};
+static_assert(sizeof(OctNodeC) == 16, "compact node");
+
+struct OctLdsShared {
+  int wsum[kOctWaves];
+  int m, seq_next, mode, nexp, finish, ktotal, cut, nbig, fallback;
+  int ini_cnt[16], ini_base[16];
+};
+
+__device__ __forceinline__ int quadrant(uint32_t k, int xm, int ym) {
+  return (key_x(k) >= xm ? 1 : 0) + (key_y(k) >= ym ? 2 : 0);
+}
+
+// children of nd given its 4 quadrant counts, in push order (UL, UR, BL, BR)
+__device__ __forceinline__ void node_children(const OctNodeC& nd, const int cnt[4], OctNodeC ch[4]) {
+  const int hx = (nd.x1 - nd.x0 + 1) >> 1, hy = (nd.y1 - nd.y0 + 1) >> 1;
+  const int16_t xs[3] = {nd.x0, (int16_t)(nd.x0 + hx), nd.x1};
+  const int16_t ys[3] = {nd.y0, (int16_t)(nd.y0 + hy), nd.y1};
+  int start = nd.kbeg;
+#pragma unroll
+  for (int q = 0; q < 4; q++) {
+    ch[q].x0 = xs[q & 1];
+    ch[q].x1 = xs[(q & 1) + 1];
+    ch[q].y0 = ys[q >> 1];
+    ch[q].y1 = ys[(q >> 1) + 1];
+    ch[q].kbeg = (uint16_t)start;
+    ch[q].n = (uint16_t)cnt[q];
+    ch[q].seq = 0;
+    start += cnt[q];
+  }
+}
+
+// one lane, n <= kOctLaneKeys: counts (and, if part, the in-place stable partition)
+__device__ __forceinline__ void lane_divide(const OctNodeC& nd, uint32_t* keys, int cnt[4], bool part) {
+  const int xm = nd.x0 + ((nd.x1 - nd.x0 + 1) >> 1), ym = nd.y0 + ((nd.y1 - nd.y0 + 1) >> 1);
+  uint32_t kr[kOctLaneKeys];
+  uint32_t c = 0;  // 4 packed 8-bit counters
+#pragma unroll
+  for (int r = 0; r < kOctLaneKeys; r++) {
+    if (r < nd.n) {
+      kr[r] = keys[nd.kbeg + r];
+      c += 1u << (8 * quadrant(kr[r], xm, ym));
+    }
+  }
+#pragma unroll
+  for (int q = 0; q < 4; q++) cnt[q] = (c >> (8 * q)) & 255;
+  if (part) {
+    uint32_t run = (c << 8) + (c << 16) + (c << 24);  // byte q: sum of counts below q
+#pragma unroll
+    for (int r = 0; r < kOctLaneKeys; r++) {
+      if (r < nd.n) {
+        const int q = quadrant(kr[r], xm, ym);
+        keys[nd.kbeg + ((run >> (8 * q)) & 255)] = kr[r];
+        run += 1u << (8 * q);
+      }
+    }
+  }
+}
+
+// one wave, n <= kOctWaveKeys: counts (wave-uniform) and, if part, the in-place partition
+__device__ __forceinline__ void wave_divide(const OctNodeC& nd, uint32_t* keys, int cnt[4], bool part,
+                                            int lane) {
+  const int xm = nd.x0 + ((nd.x1 - nd.x0 + 1) >> 1), ym = nd.y0 + ((nd.y1 - nd.y0 + 1) >> 1);
+  const int R = (nd.n + 63) >> 6;
+  uint32_t kr[kOctWaveRegs];
+  int qr[kOctWaveRegs];
+#pragma unroll
+  for (int q = 0; q < 4; q++) cnt[q] = 0;
+#pragma unroll
+  for (int r = 0; r < kOctWaveRegs; r++) {
+    if (r < R) {
+      const int i = 64 * r + lane;
+      kr[r] = i < nd.n ? keys[nd.kbeg + i] : 0u;
+      qr[r] = i < nd.n ? quadrant(kr[r], xm, ym) : -1;
+#pragma unroll
+      for (int q = 0; q < 4; q++) cnt[q] += __popcll(__ballot(qr[r] == q));
+    }
+  }
+  if (!part) return;
+  int run[4] = {0, cnt[0], cnt[0] + cnt[1], cnt[0] + cnt[1] + cnt[2]};
+#pragma unroll
+  for (int r = 0; r < kOctWaveRegs; r++) {
+    if (r < R) {
+#pragma unroll
+      for (int q = 0; q < 4; q++) {
+        const uint64_t m = __ballot(qr[r] == q);
+        if (qr[r] == q) keys[nd.kbeg + run[q] + lanes_below(m)] = kr[r];
+        run[q] += __popcll(m);
+      }
+    }
+  }
+}
+
+__global__ __launch_bounds__(kOctThreads) void octree_lds_kernel(
+    const OrbGeom* __restrict__ g, const uint32_t* __restrict__ cell_keys,
+    const int* __restrict__ cell_count, uint32_t* __restrict__ oct_keys,
+    int* __restrict__ oct_count, uint32_t* __restrict__ err) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t s_oct[];
+  __shared__ OctLdsShared S;
+  const int NC = g->oct_nc;
+  uint32_t* keys = reinterpret_cast<uint32_t*>(s_oct);
+  OctNodeC* lists[2] = {reinterpret_cast<OctNodeC*>(s_oct + 4 * kOctLdsKeys),
+                        reinterpret_cast<OctNodeC*>(s_oct + 4 * kOctLdsKeys) + NC};
+  uint64_t* sortk = reinterpret_cast<uint64_t*>(lists[1] + NC);
+  int* sa = reinterpret_cast<int*>(sortk + NC);
+  int* sb = sa + NC;
+  int* sc = sb + NC;
+  int* vnext = sc + NC;
+  int* bigs = vnext + NC;
+  uint8_t* processed = reinterpret_cast<uint8_t*>(bigs + NC);
+
+  const int level = blockIdx.x, img = blockIdx.y;
+  const int tid = threadIdx.x, lane = tid & 63, wid = wave_id();
+  const LevelGeom& L = g->lv[level];
+  const int N = L.budget;
+  const int ncell = L.ncols * L.nrows;
+  const int64_t cbase = (int64_t)img * g->cells_per_image + L.cell_base;
+  int* const outc = oct_count + img * g->nlevels + level;
+  uint32_t* const outk = oct_keys + (int64_t)img * g->out_per_image + L.out_base;
+
+  // ---- 1. gather FAST candidates in cell row-major order into keys[]: cell counts -> prefix
+  // (in the sortk area, 2*NC ints per chunk), then every key slot finds its cell by binary
+  // search, so all global loads of a chunk are independent.
+  int* cpre = reinterpret_cast<int*>(sortk);
+  const int CC = 2 * NC;
+  if (tid == 0) S.ktotal = 0;
+  for (int c0 = 0; c0 < ncell; c0 += CC) {
+    const int n = min(CC, ncell - c0);
+    for (int i = tid; i < n; i += kOctThreads) cpre[i] = cell_count[cbase + c0 + i];
+    __syncthreads();
+    const int base = S.ktotal;
+    int tot = 0;
+    for (int s0 = 0; s0 < n; s0 += kOctCap) {  // block_scan_array covers kOctCap entries
+      const int t = block_scan_array(cpre + s0, min(kOctCap, n - s0), S.wsum);
+      if (s0 > 0)
+        for (int i = tid; i < min(kOctCap, n - s0); i += kOctThreads) cpre[s0 + i] += tot;
+      tot += t;
+      __syncthreads();
+    }
+    const int kend = min(base + tot, kOctLdsKeys);
+    for (int k = base + tid; k < kend; k += kOctThreads) {
+      const int r = k - base;
+      int lo = 0, hi = n - 1;  // last cell with prefix <= r
+      while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (cpre[mid] <= r) lo = mid;
+        else hi = mid - 1;
+      }
+      keys[k] = cell_keys[(cbase + c0 + lo) * g->cell_cap + (r - cpre[lo])];
+    }
+    __syncthreads();
+    if (tid == 0) S.ktotal = base + tot;
+    __syncthreads();
+  }
+  const int K = S.ktotal;
+  const int nIni = L.n_ini;
+  if (K > kOctLdsKeys || nIni > 16) {
+    if (tid == 0) *outc = -1;  // octree_kernel handles it
+    return;
+  }
+  if (K == 0) {
+    if (tid == 0) *outc = 0;
+    return;
+  }
+  // ---- 2. initial nodes (:484-526): stable bucketing by (int)(x / hX), in place via registers
+  const float hX = L.hx;
+  constexpr int kPer = kOctLdsKeys / kOctThreads;  // keys per thread (blocked)
+  uint32_t kr[kPer];
+  int qb[kPer];
+  int cnt16[16];
+#pragma unroll
+  for (int b = 0; b < 16; b++) cnt16[b] = 0;
+#pragma unroll
+  for (int r = 0; r < kPer; r++) {
+    const int i = tid * kPer + r;
+    qb[r] = -1;
+    if (i < K) {
+      kr[r] = keys[i];
+      qb[r] = (int)((float)key_x(kr[r]) / hX);
+#pragma unroll
+      for (int b = 0; b < 16; b++) cnt16[b] += (qb[r] == b);
+    }
+  }
+  int pre16[16];
+#pragma unroll
+  for (int b = 0; b < 16; b++) {
+    pre16[b] = 0;
+    if (b < nIni) {  // nIni is uniform: every thread runs the same scans
+      int tot;
+      pre16[b] = block_scan(cnt16[b], S.wsum, &tot);
+      if (tid == 0) S.ini_cnt[b] = tot;
+    }
+  }
+  __syncthreads();
+  if (tid == 0) {
+    int run = 0, big = 0;
+    for (int b = 0; b < nIni; b++) {
+      S.ini_base[b] = run;
+      run += S.ini_cnt[b];
+      big |= S.ini_cnt[b] > kOctWaveKeys;
+    }
+    S.fallback = big;
+  }
+  __syncthreads();
+  if (S.fallback) {
+    if (tid == 0) *outc = -1;
+    return;
+  }
+  {
+    int run16[16];
+#pragma unroll
+    for (int b = 0; b < 16; b++) run16[b] = b < nIni ? S.ini_base[b] + pre16[b] : 0;
+#pragma unroll
+    for (int r = 0; r < kPer; r++) {
+      if (qb[r] >= 0 && qb[r] < nIni) {
+        int pos = 0;
+#pragma unroll
+        for (int b = 0; b < 16; b++)
+          if (qb[r] == b) pos = run16[b]++;
+        keys[pos] = kr[r];
+      }
+    }
+  }
+  __syncthreads();
+  if (tid == 0) {
+    int m = 0;
+    for (int i = 0; i < nIni; i++) {
+      const int c = S.ini_cnt[i];
+      if (c == 0) continue;  // empty initial nodes are erased (:513-526)
+      OctNodeC nd;
+      nd.x0 = (int16_t)(int)(hX * (float)i);
+      nd.x1 = (int16_t)(int)(hX * (float)(i + 1));
+      nd.y0 = 0;
+      nd.y1 = (int16_t)(L.max_by - kMinBorder);
+      nd.kbeg = (uint16_t)S.ini_base[i];
+      nd.n = (uint16_t)c;
+      nd.seq = i;
+      lists[0][m++] = nd;
+    }
+    S.m = m;
+    S.seq_next = nIni;
+    S.mode = 0;
+    S.finish = 0;
+    S.nexp = 0;
+  }
+  __syncthreads();
+  int cur = 0;
+  // ---- 3. passes. node(j) gives the j-th node to divide: list order (outer pass) or the
+  // sorted vPrev order (inner iteration).
+  while (true) {
+    const int m = S.m;
+    const OctNodeC* Lc = lists[cur];
+    OctNodeC* Ln = lists[cur ^ 1];
+    const bool outer = S.mode == 0;
+    const int V = outer ? m : S.nexp;
+    if (!outer) {
+      // vPrev = sortk[0..V) (list positions, push order) -> descending (n, seq)
+      int P2 = 1;
+      while (P2 < V) P2 <<= 1;
+      for (int i = tid; i < P2; i += kOctThreads) {
+        uint64_t key = 0;  // pads sort to the end (descending)
+        if (i < V) {
+          const int pos = (int)sortk[i];
+          const OctNodeC& nd = Lc[pos];
+          key = ((uint64_t)nd.n << 44) | ((uint64_t)(uint32_t)nd.seq << 12) | (uint64_t)pos;
+        }
+        sortk[i] = key;
+      }
+      __syncthreads();
+      for (int k = 2; k <= P2; k <<= 1) {
+        for (int jj = k >> 1; jj > 0; jj >>= 1) {
+          for (int i = tid; i < P2; i += kOctThreads) {
+            const int ixj = i ^ jj;
+            if (ixj > i) {
+              const uint64_t x = sortk[i], y = sortk[ixj];
+              const bool desc = (i & k) == 0;
+              if (desc ? (x < y) : (x > y)) {
+                sortk[i] = y;
+                sortk[ixj] = x;
+              }
+            }
+          }
+          __syncthreads();
+        }
+      }
+    }
+    auto node_index = [&](int j) { return outer ? j : (int)(sortk[j] & 0xfff); };
+    // -- count: t (non-empty children), e (children with > 1 key); outer pass: u (n == 1)
+    if (tid == 0) S.nbig = 0;
+    __syncthreads();
+    for (int j = tid; j < V; j += kOctThreads) {
+      const OctNodeC nd = Lc[node_index(j)];
+      int t = 0, e = 0;
+      if (nd.n > kOctLaneKeys) {
+        bigs[atomicAdd(&S.nbig, 1)] = j;
+      } else if (nd.n > 1) {
+        int cnt[4];
+        lane_divide(nd, keys, cnt, false);
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+          t += cnt[q] > 0;
+          e += cnt[q] > 1;
+        }
+      }
+      sa[j] = t;
+      sc[j] = e;
+      sb[j] = outer ? (nd.n == 1) : t - 1;
+    }
+    __syncthreads();
+    const int nbig = S.nbig;
+    for (int bi = wid; bi < nbig; bi += kOctWaves) {
+      const int j = bigs[bi];
+      const OctNodeC nd = Lc[node_index(j)];
+      int cnt[4];
+      wave_divide(nd, keys, cnt, false, lane);
+      if (lane == 0) {
+        int t = 0, e = 0;
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+          t += cnt[q] > 0;
+          e += cnt[q] > 1;
+        }
+        sa[j] = t;
+        sc[j] = e;
+        sb[j] = outer ? 0 : t - 1;
+      }
+    }
+    __syncthreads();
+    int nproc = V;
+    if (!outer) {
+      // cut: first j with m + sum_{i<=j}(t_i - 1) >= N (processing stops once the list is full)
+      block_scan_array(sb, V, S.wsum);  // exclusive prefix of (t - 1)
+      if (tid == 0) S.cut = V - 1;
+      __syncthreads();
+      for (int j = tid; j < V; j += kOctThreads)
+        if (m + sb[j] + (sa[j] - 1) >= N) atomicMin(&S.cut, j);
+      __syncthreads();
+      nproc = S.cut + 1;
+      for (int i = tid; i < V; i += kOctThreads)
+        if (i >= nproc) {
+          sa[i] = 0;
+          sc[i] = 0;
+        }
+      for (int i = tid; i < m; i += kOctThreads) processed[i] = 0;
+      __syncthreads();
+      for (int j = tid; j < nproc; j += kOctThreads) processed[node_index(j)] = 1;
+      __syncthreads();
+      for (int i = tid; i < m; i += kOctThreads) sb[i] = processed[i] ? 0 : 1;  // survivors
+      __syncthreads();
+    }
+    const int T = block_scan_array(sa, V, S.wsum);  // push-order child positions
+    const int E = block_scan_array(sc, V, S.wsum);
+    const int U = block_scan_array(sb, m, S.wsum);  // survivors keep their order
+    const int newm = T + U;
+    const int seq0 = S.seq_next;
+    const bool ovf = newm > NC || E > NC;
+    if (!ovf) {
+      // -- divide (in place) and place children: push order gpos -> list position T-1-gpos
+      auto place = [&](int j, const OctNodeC& nd, const int cnt[4]) {
+        OctNodeC ch[4];
+        node_children(nd, cnt, ch);
+        int gpos = sa[j], epos = sc[j];
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+          if (ch[q].n == 0) continue;
+          ch[q].seq = seq0 + gpos;
+          const int pos = T - 1 - gpos;
+          Ln[pos] = ch[q];
+          if (ch[q].n > 1) vnext[epos++] = pos;
+          gpos++;
+        }
+      };
+      for (int j = tid; j < nproc; j += kOctThreads) {
+        const OctNodeC nd = Lc[node_index(j)];
+        if (nd.n > 1 && nd.n <= kOctLaneKeys) {
+          int cnt[4];
+          lane_divide(nd, keys, cnt, true);
+          place(j, nd, cnt);
+        }
+      }
+      for (int bi = wid; bi < nbig; bi += kOctWaves) {
+        const int j = bigs[bi];
+        if (j >= nproc) continue;
+        const OctNodeC nd = Lc[node_index(j)];
+        int cnt[4];
+        wave_divide(nd, keys, cnt, true, lane);
+        if (lane == 0) place(j, nd, cnt);
+      }
+      // survivors
+      if (outer) {
+        for (int i = tid; i < m; i += kOctThreads)
+          if (Lc[i].n == 1) Ln[T + sb[i]] = Lc[i];
+      } else {
+        for (int i = tid; i < m; i += kOctThreads)
+          if (!processed[i]) Ln[T + sb[i]] = Lc[i];
+      }
+    }
+    __syncthreads();
+    for (int i = tid; i < E; i += kOctThreads) sortk[i] = (uint64_t)vnext[i];
+    if (tid == 0) {
+      if (ovf) {
+        atomicOr(err, kErrNodeOverflow);
+        S.finish = 1;
+      } else {
+        S.m = newm;
+        S.seq_next = seq0 + T;
+        S.nexp = E;
+        if (newm >= N || newm == m) S.finish = 1;
+        else if (outer && newm + E * 3 > N) S.mode = 1;
+      }
+    }
+    if (!ovf) cur ^= 1;
+    __syncthreads();
+    if (S.finish) break;
+  }
+  // ---- 4. retain the best key of each node (:682-701): strict '>' keeps the first maximum
+  const int m = S.m;
+  const OctNodeC* Lf = lists[cur];
+  const int mout = min(m, L.out_cap);
+  for (int j = tid; j < mout; j += kOctThreads) {
+    const OctNodeC nd = Lf[j];
+    uint32_t best = keys[nd.kbeg];
+    for (int k = 1; k < nd.n; k++) {
+      const uint32_t kk = keys[nd.kbeg + k];
+      if (key_score(kk) > key_score(best)) best = kk;
+    }
+    outk[j] = best;
+  }
+  if (tid == 0) {
+    if (m > L.out_cap) atomicOr(err, kErrNodeOverflow);
+    *outc = mout;
+  }
+}
+
+// ---------------------------------------------------------------------------------------
 // orient_desc: computeOrientation/IC_Angle (:413-420, :18-45) on the unblurred level, then
 // computeOrbDescriptor (:49-88) on the blurred level. Output order is ORBextractor::Compute's:
 // levels 0..L-1 concatenated, each in octree list order (:1020-1048). Descriptor sample offsets
@@ -1397,7 +1849,13 @@ void launch_extract(const ImageBatch& b, const OrbGeomDev& gd, int n_images, hip
                  dim3(64 * kCellWaves), (size_t)kCellWaves * g.fast_lds_per_wave, st, b,
                  gd.dev, gd.cells, gd.ws.cell_keys,
                      gd.ws.cell_count, gd.ws.err);
-  SLAMGPU_LAUNCH("octree", st, octree_kernel, dim3(g.nlevels, n_images), dim3(kOctThreads), 0, st, gd.dev,
+  {
+    const size_t lds = (size_t)4 * kOctLdsKeys + (size_t)g.oct_nc * (2 * sizeof(OctNodeC) + 8 + 5 * 4 + 1);
+    SLAMGPU_LAUNCH("octree", st, octree_lds_kernel, dim3(g.nlevels, n_images), dim3(kOctThreads),
+                   lds, st, gd.dev, gd.ws.cell_keys, gd.ws.cell_count, gd.ws.oct_keys,
+                   gd.ws.oct_count, gd.ws.err);
+  }
+  SLAMGPU_LAUNCH("octree_global", st, octree_kernel, dim3(g.nlevels, n_images), dim3(kOctThreads), 0, st, gd.dev,
                      gd.ws.cell_keys, gd.ws.cell_count, gd.ws.key_scratch, gd.ws.node_scratch,
                      gd.ws.oct_keys, gd.ws.oct_count, gd.ws.err);
   SLAMGPU_LAUNCH("orient_desc", st, orient_desc_kernel,
