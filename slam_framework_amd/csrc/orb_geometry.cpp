@@ -227,10 +227,28 @@ int compute_geometry(const OrbParams& p, int cols, int rows, OrbGeom* g,
   }
   g->keys_per_image = key_off;
   g->nodes_per_image = node_off;
-  {
-    int nc = 0;
-    for (int l = 0; l < p.nlevels; l++) nc = std::max(nc, g->lv[l].node_cap);
-    g->oct_nc = round_up(nc, 64);
+  {  // octree_img_kernel LDS: [keys u32 x kcap][per level: 2 node lists][per level: arrays]
+    constexpr int kLdsBudget = 156 * 1024, kNodeBytes = 12, kWorkBytesPerNode = 4 + 4 * 2 + 1;
+    int off = 0;
+    for (int l = 0; l < p.nlevels; l++) {
+      LevelGeom& L = g->lv[l];
+      L.oct_nc = round_up(L.node_cap, 64);
+      L.oct_list_off = off;
+      off += 2 * L.oct_nc * kNodeBytes;
+    }
+    for (int l = 0; l < p.nlevels; l++) {
+      LevelGeom& L = g->lv[l];
+      L.oct_work_off = off;
+      off += round_up(L.oct_nc * kWorkBytesPerNode, 16);
+    }
+    const int kcap = std::min((kLdsBudget - off) / 4, 65535);
+    if (kcap < 1024) return -6;
+    g->oct_kcap = kcap;
+    for (int l = 0; l < p.nlevels; l++) {  // keys go first
+      g->lv[l].oct_list_off += 4 * kcap;
+      g->lv[l].oct_work_off += 4 * kcap;
+    }
+    g->oct_lds_bytes = off + 4 * kcap;
   }
   g->out_per_image = out_off;
   g->kp_cap = out_off;

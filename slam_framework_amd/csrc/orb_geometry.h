@@ -43,6 +43,9 @@ struct LevelGeom {
   int64_t node_base;    // offset (in nodes) of this level in the per-image node scratch
   int out_base;         // offset (in keypoints) of this level in the per-image octree output
   int out_cap;          // max keypoints this level can emit
+  int oct_nc;           // octree_img_kernel: LDS node capacity (node_cap rounded to 64)
+  int oct_list_off;     //   byte offset of the two node lists in the work-group's LDS
+  int oct_work_off;     //   byte offset of sort keys / prefix arrays / flags
   // resize tables (level >= 1) in the shared table buffer
   int rx_base, ry_base; // offsets into the x (per dst column) / y (per dst row) tables
   int blur_tile_base;   // first 256x128 blur tile of this level
@@ -66,7 +69,8 @@ struct OrbGeom {
   int gauss[7];          // GaussianBlur 7x7 sigma 2 integer kernel (x256)
   int64_t keys_per_image;
   int64_t nodes_per_image;
-  int oct_nc;            // LDS node-list capacity of octree_lds_kernel (max node_cap, rounded)
+  int oct_lds_bytes;     // octree_img_kernel dynamic LDS (keys + per-level lists and arrays)
+  int oct_kcap;          // keys of all levels of one image that fit in that LDS
   int out_per_image;     // sum of out_cap
   int kp_cap;            // max keypoints per image after Compute (== out_per_image)
   int umax[16];

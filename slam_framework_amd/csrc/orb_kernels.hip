@@ -823,7 +823,7 @@ __global__ __launch_bounds__(kOctThreads) void octree_kernel(
   OctNode* const child = node_scratch + img * g->nodes_per_image + L.node_base + 4 * L.node_cap;
   int* const outc = oct_count + img * g->nlevels + level;
   uint32_t* const outk = oct_keys + (int64_t)img * g->out_per_image + L.out_base;
-  if (*outc != -1) return;  // done by octree_lds_kernel
+  if (*outc != -1) return;  // done by octree_img_kernel
 
   // ---- 1. gather FAST candidates in cell row-major order into keys[0]
   for (int c0 = 0; c0 < ncell; c0 += kOctCap) {
@@ -1139,297 +1139,355 @@ __global__ __launch_bounds__(kOctThreads) void octree_kernel(
 }
 
 // ---------------------------------------------------------------------------------------
-// octree_lds: the same DistributeOctTree with every pass in LDS. Keys live in one LDS buffer and
-// a division partitions its node's key range in place through registers (a lane per node for
-// n <= 8, a wave per node for n <= 2048); node lists are compact 16-byte nodes in LDS. A pass is
-//   count (children per node) -> block scans -> divide + place children at their final list
-//   positions,
-// so no child array exists. Work-groups whose candidates exceed kOctLdsKeys, or whose initial
-// nodes exceed kOctWaveKeys, mark oct_count = -1 and octree_kernel (global memory) redoes them.
-constexpr int kOctLdsKeys = 4096;
-constexpr int kOctWaveRegs = 32;
-constexpr int kOctWaveKeys = 64 * kOctWaveRegs;
-constexpr int kOctLaneKeys = 8;
+// octree_img: the same DistributeOctTree for all levels of one image in one work-group, one wave
+// per level, entirely in LDS and wave-synchronous (one work-group barrier, to allocate the key
+// ranges). Per level: keys (one range, partitioned in place), two node lists and the
+// count / prefix arrays of a pass (orb_geometry.cpp lays them out). A pass is
+//   count children per node -> wave scans -> divide in place + put children at their final
+//   list positions,
+// so no child array exists. Dividing a node: a lane per node for n <= 32, the wave through
+// registers for n <= 1024, the wave through global scratch above that.
+// Creation order (the stand-in for the reference's pointer order, :625) only breaks ties inside
+// vPrev, whose nodes were all created in the same pass -- in push order, i.e. ascending list
+// position -- so nodes carry no sequence number. Levels whose keys do not fit set
+// oct_count = -1 and octree_kernel (global memory) redoes them.
+constexpr int kOctLaneKeys = 32;  // <= 255 (8-bit packed quadrant counts)
+constexpr int kOctDivRegs = 16;
 
-struct OctNodeC {
+struct OctNodeS {
   int16_t x0, x1, y0, y1;
-  uint16_t kbeg, n;
-  int32_t seq;
+  uint32_t kn;  // kbeg | n << 16 (level-relative key range)
 };
-static_assert(sizeof(OctNodeC) == 16, "compact node");
-
-struct OctLdsShared {
-  int wsum[kOctWaves];
-  int m, seq_next, mode, nexp, finish, ktotal, cut, nbig, fallback;
-  int ini_cnt[16], ini_base[16];
-};
+static_assert(sizeof(OctNodeS) == 12, "compact node");
+__device__ __forceinline__ int node_kbeg(const OctNodeS& d) { return (int)(d.kn & 0xffffu); }
+__device__ __forceinline__ int node_n(const OctNodeS& d) { return (int)(d.kn >> 16); }
 
 __device__ __forceinline__ int quadrant(uint32_t k, int xm, int ym) {
   return (key_x(k) >= xm ? 1 : 0) + (key_y(k) >= ym ? 2 : 0);
 }
+__device__ __forceinline__ int node_xm(const OctNodeS& d) { return d.x0 + ((d.x1 - d.x0 + 1) >> 1); }
+__device__ __forceinline__ int node_ym(const OctNodeS& d) { return d.y0 + ((d.y1 - d.y0 + 1) >> 1); }
 
-// children of nd given its 4 quadrant counts, in push order (UL, UR, BL, BR)
-__device__ __forceinline__ void node_children(const OctNodeC& nd, const int cnt[4], OctNodeC ch[4]) {
-  const int hx = (nd.x1 - nd.x0 + 1) >> 1, hy = (nd.y1 - nd.y0 + 1) >> 1;
-  const int16_t xs[3] = {nd.x0, (int16_t)(nd.x0 + hx), nd.x1};
-  const int16_t ys[3] = {nd.y0, (int16_t)(nd.y0 + hy), nd.y1};
-  int start = nd.kbeg;
-#pragma unroll
-  for (int q = 0; q < 4; q++) {
-    ch[q].x0 = xs[q & 1];
-    ch[q].x1 = xs[(q & 1) + 1];
-    ch[q].y0 = ys[q >> 1];
-    ch[q].y1 = ys[(q >> 1) + 1];
-    ch[q].kbeg = (uint16_t)start;
-    ch[q].n = (uint16_t)cnt[q];
-    ch[q].seq = 0;
-    start += cnt[q];
-  }
+// exclusive prefix sum over the wave (DPP: row shifts, then row broadcasts); *total = sum
+__device__ __forceinline__ int wave_excl_scan(int v, int lane, int* total) {
+  int x = v;
+  x += __builtin_amdgcn_update_dpp(0, x, 0x111, 0xf, 0xf, false);  // row_shr:1
+  x += __builtin_amdgcn_update_dpp(0, x, 0x112, 0xf, 0xf, false);  // row_shr:2
+  x += __builtin_amdgcn_update_dpp(0, x, 0x114, 0xf, 0xf, false);  // row_shr:4
+  x += __builtin_amdgcn_update_dpp(0, x, 0x118, 0xf, 0xf, false);  // row_shr:8
+  x += __builtin_amdgcn_update_dpp(0, x, 0x142, 0xa, 0xf, false);  // row_bcast:15 -> rows 1, 3
+  x += __builtin_amdgcn_update_dpp(0, x, 0x143, 0xc, 0xf, false);  // row_bcast:31 -> rows 2, 3
+  *total = __builtin_amdgcn_readlane(x, 63);
+  (void)lane;
+  return x - v;
 }
 
-// one lane, n <= kOctLaneKeys: counts (and, if part, the in-place stable partition)
-__device__ __forceinline__ void lane_divide(const OctNodeC& nd, uint32_t* keys, int cnt[4], bool part) {
-  const int xm = nd.x0 + ((nd.x1 - nd.x0 + 1) >> 1), ym = nd.y0 + ((nd.y1 - nd.y0 + 1) >> 1);
+// in-place exclusive scan of a[0..n) (int16) by one wave; returns the total
+__device__ __forceinline__ int wave_scan_array(int16_t* a, int n, int lane) {
+  int carry = 0;
+  for (int c = 0; c < n; c += 64) {
+    const int i = c + lane;
+    const int v = i < n ? a[i] : 0;
+    int tot;
+    const int ex = wave_excl_scan(v, lane, &tot);
+    if (i < n) a[i] = (int16_t)(carry + ex);
+    carry += tot;
+  }
+  return carry;
+}
+
+// n <= kOctLaneKeys, one lane: 4 packed 8-bit quadrant counts; partitions in place if part
+__device__ __forceinline__ uint32_t lane_divide(const OctNodeS& nd, uint32_t* keys, bool part) {
+  const int xm = node_xm(nd), ym = node_ym(nd), kb = node_kbeg(nd), n = node_n(nd);
   uint32_t kr[kOctLaneKeys];
-  uint32_t c = 0;  // 4 packed 8-bit counters
+  uint32_t c = 0;
 #pragma unroll
-  for (int r = 0; r < kOctLaneKeys; r++) {
-    if (r < nd.n) {
-      kr[r] = keys[nd.kbeg + r];
+  for (int r = 0; r < kOctLaneKeys; r++)
+    if (r < n) {
+      kr[r] = keys[kb + r];
       c += 1u << (8 * quadrant(kr[r], xm, ym));
     }
-  }
-#pragma unroll
-  for (int q = 0; q < 4; q++) cnt[q] = (c >> (8 * q)) & 255;
   if (part) {
-    uint32_t run = (c << 8) + (c << 16) + (c << 24);  // byte q: sum of counts below q
+    uint32_t run = (c << 8) + (c << 16) + (c << 24);  // byte q: keys in quadrants below q
 #pragma unroll
-    for (int r = 0; r < kOctLaneKeys; r++) {
-      if (r < nd.n) {
+    for (int r = 0; r < kOctLaneKeys; r++)
+      if (r < n) {
         const int q = quadrant(kr[r], xm, ym);
-        keys[nd.kbeg + ((run >> (8 * q)) & 255)] = kr[r];
+        keys[kb + ((run >> (8 * q)) & 255)] = kr[r];
         run += 1u << (8 * q);
       }
-    }
   }
+  return c;
 }
 
-// one wave, n <= kOctWaveKeys: counts (wave-uniform) and, if part, the in-place partition
-__device__ __forceinline__ void wave_divide(const OctNodeC& nd, uint32_t* keys, int cnt[4], bool part,
-                                            int lane) {
-  const int xm = nd.x0 + ((nd.x1 - nd.x0 + 1) >> 1), ym = nd.y0 + ((nd.y1 - nd.y0 + 1) >> 1);
-  const int R = (nd.n + 63) >> 6;
-  uint32_t kr[kOctWaveRegs];
-  int qr[kOctWaveRegs];
+// one wave: quadrant counts of a node (uniform)
+__device__ __forceinline__ void wave_count(const OctNodeS& nd, const uint32_t* keys, int lane,
+                                           int cnt[4]) {
+  const int xm = node_xm(nd), ym = node_ym(nd), kb = node_kbeg(nd), n = node_n(nd);
 #pragma unroll
   for (int q = 0; q < 4; q++) cnt[q] = 0;
+  for (int s0 = 0; s0 < n; s0 += 64) {
+    const int q = s0 + lane < n ? quadrant(keys[kb + s0 + lane], xm, ym) : -1;
 #pragma unroll
-  for (int r = 0; r < kOctWaveRegs; r++) {
-    if (r < R) {
-      const int i = 64 * r + lane;
-      kr[r] = i < nd.n ? keys[nd.kbeg + i] : 0u;
-      qr[r] = i < nd.n ? quadrant(kr[r], xm, ym) : -1;
-#pragma unroll
-      for (int q = 0; q < 4; q++) cnt[q] += __popcll(__ballot(qr[r] == q));
-    }
+    for (int qq = 0; qq < 4; qq++) cnt[qq] += __popcll(__ballot(q == qq));
   }
-  if (!part) return;
+}
+
+// one wave: stable in-place partition of a node's keys; returns the counts (uniform)
+__device__ void wave_partition(const OctNodeS& nd, uint32_t* keys, uint32_t* gscratch, int lane,
+                               int cnt[4]) {
+  const int xm = node_xm(nd), ym = node_ym(nd), kb = node_kbeg(nd), n = node_n(nd);
+  wave_count(nd, keys, lane, cnt);
   int run[4] = {0, cnt[0], cnt[0] + cnt[1], cnt[0] + cnt[1] + cnt[2]};
+  if (n <= 64 * kOctDivRegs) {  // through registers
+    const int R = (n + 63) >> 6;
+    uint32_t kr[kOctDivRegs];
+    int qr[kOctDivRegs];
 #pragma unroll
-  for (int r = 0; r < kOctWaveRegs; r++) {
-    if (r < R) {
+    for (int r = 0; r < kOctDivRegs; r++) {
+      qr[r] = -1;
+      if (r < R && 64 * r + lane < n) {
+        kr[r] = keys[kb + 64 * r + lane];
+        qr[r] = quadrant(kr[r], xm, ym);
+      }
+    }
 #pragma unroll
-      for (int q = 0; q < 4; q++) {
-        const uint64_t m = __ballot(qr[r] == q);
-        if (qr[r] == q) keys[nd.kbeg + run[q] + lanes_below(m)] = kr[r];
-        run[q] += __popcll(m);
+    for (int r = 0; r < kOctDivRegs; r++)
+      if (r < R) {
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+          const uint64_t m = __ballot(qr[r] == q);
+          if (qr[r] == q) keys[kb + run[q] + lanes_below(m)] = kr[r];
+          run[q] += __popcll(m);
+        }
+      }
+  } else {  // through this level's global scratch (first passes of very dense levels only)
+    for (int i = lane; i < n; i += 64) gscratch[kb + i] = keys[kb + i];
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "agent");
+    for (int s0 = 0; s0 < n; s0 += 64) {
+      const int i = s0 + lane;
+      uint32_t k = 0;
+      int q = -1;
+      if (i < n) {
+        k = gscratch[kb + i];
+        q = quadrant(k, xm, ym);
+      }
+#pragma unroll
+      for (int qq = 0; qq < 4; qq++) {
+        const uint64_t m = __ballot(q == qq);
+        if (q == qq) keys[kb + run[qq] + lanes_below(m)] = k;
+        run[qq] += __popcll(m);
       }
     }
   }
 }
 
-__global__ __launch_bounds__(kOctThreads) void octree_lds_kernel(
+__global__ __launch_bounds__(64 * kMaxLevels) void octree_img_kernel(
     const OrbGeom* __restrict__ g, const uint32_t* __restrict__ cell_keys,
-    const int* __restrict__ cell_count, uint32_t* __restrict__ oct_keys,
-    int* __restrict__ oct_count, uint32_t* __restrict__ err) {
+    const int* __restrict__ cell_count, uint32_t* __restrict__ key_scratch,
+    uint32_t* __restrict__ oct_keys, int* __restrict__ oct_count, uint32_t* __restrict__ err) {
   extern __shared__ __attribute__((aligned(16))) uint8_t s_oct[];
-  __shared__ OctLdsShared S;
-  const int NC = g->oct_nc;
-  uint32_t* keys = reinterpret_cast<uint32_t*>(s_oct);
-  OctNodeC* lists[2] = {reinterpret_cast<OctNodeC*>(s_oct + 4 * kOctLdsKeys),
-                        reinterpret_cast<OctNodeC*>(s_oct + 4 * kOctLdsKeys) + NC};
-  uint64_t* sortk = reinterpret_cast<uint64_t*>(lists[1] + NC);
-  int* sa = reinterpret_cast<int*>(sortk + NC);
-  int* sb = sa + NC;
-  int* sc = sb + NC;
-  int* vnext = sc + NC;
-  int* bigs = vnext + NC;
-  uint8_t* processed = reinterpret_cast<uint8_t*>(bigs + NC);
-
-  const int level = blockIdx.x, img = blockIdx.y;
-  const int tid = threadIdx.x, lane = tid & 63, wid = wave_id();
-  const LevelGeom& L = g->lv[level];
-  const int N = L.budget;
+  __shared__ int s_K[kMaxLevels];
+  const int img = blockIdx.x, lane = threadIdx.x & 63, level = wave_id();
+  const int nlev = g->nlevels;
+  const bool active = level < nlev;
+  const LevelGeom& L = g->lv[active ? level : 0];
   const int ncell = L.ncols * L.nrows;
   const int64_t cbase = (int64_t)img * g->cells_per_image + L.cell_base;
-  int* const outc = oct_count + img * g->nlevels + level;
-  uint32_t* const outk = oct_keys + (int64_t)img * g->out_per_image + L.out_base;
-
-  // ---- 1. gather FAST candidates in cell row-major order into keys[]: cell counts -> prefix
-  // (in the sortk area, 2*NC ints per chunk), then every key slot finds its cell by binary
-  // search, so all global loads of a chunk are independent.
-  int* cpre = reinterpret_cast<int*>(sortk);
-  const int CC = 2 * NC;
-  if (tid == 0) S.ktotal = 0;
-  for (int c0 = 0; c0 < ncell; c0 += CC) {
-    const int n = min(CC, ncell - c0);
-    for (int i = tid; i < n; i += kOctThreads) cpre[i] = cell_count[cbase + c0 + i];
-    __syncthreads();
-    const int base = S.ktotal;
-    int tot = 0;
-    for (int s0 = 0; s0 < n; s0 += kOctCap) {  // block_scan_array covers kOctCap entries
-      const int t = block_scan_array(cpre + s0, min(kOctCap, n - s0), S.wsum);
-      if (s0 > 0)
-        for (int i = tid; i < min(kOctCap, n - s0); i += kOctThreads) cpre[s0 + i] += tot;
-      tot += t;
-      __syncthreads();
-    }
-    const int kend = min(base + tot, kOctLdsKeys);
-    for (int k = base + tid; k < kend; k += kOctThreads) {
-      const int r = k - base;
-      int lo = 0, hi = n - 1;  // last cell with prefix <= r
-      while (lo < hi) {
-        const int mid = (lo + hi + 1) >> 1;
-        if (cpre[mid] <= r) lo = mid;
-        else hi = mid - 1;
-      }
-      keys[k] = cell_keys[(cbase + c0 + lo) * g->cell_cap + (r - cpre[lo])];
-    }
-    __syncthreads();
-    if (tid == 0) S.ktotal = base + tot;
-    __syncthreads();
+  // ---- 1. candidate counts -> this level's key range (levels that do not fit fall back)
+  int K = 0;
+  if (active) {
+    for (int c = lane; c < ncell; c += 64) K += cell_count[cbase + c];
+    K = wave_sum(K);
+    if (lane == 0) s_K[level] = K;
   }
-  const int K = S.ktotal;
+  __syncthreads();
+  if (!active) return;
+  int* const outc = oct_count + img * nlev + level;
+  uint32_t* const outk = oct_keys + (int64_t)img * g->out_per_image + L.out_base;
   const int nIni = L.n_ini;
-  if (K > kOctLdsKeys || nIni > 16) {
-    if (tid == 0) *outc = -1;  // octree_kernel handles it
+  int koff = 0;
+  bool fits = true;
+  for (int l = 0; l <= level; l++) {
+    const bool f = koff + s_K[l] <= g->oct_kcap;
+    if (l == level) fits = f;
+    else if (f) koff += s_K[l];
+  }
+  if (!fits || nIni > 16) {
+    if (lane == 0) *outc = -1;  // octree_kernel redoes this level
     return;
   }
   if (K == 0) {
-    if (tid == 0) *outc = 0;
+    if (lane == 0) *outc = 0;
     return;
   }
-  // ---- 2. initial nodes (:484-526): stable bucketing by (int)(x / hX), in place via registers
+  uint32_t* const keys = reinterpret_cast<uint32_t*>(s_oct) + koff;
+  uint32_t* const gscratch = key_scratch + img * g->keys_per_image + L.key_base;
+  const int NC = L.oct_nc;
+  OctNodeS* const lists = reinterpret_cast<OctNodeS*>(s_oct + L.oct_list_off);
+  uint32_t* const sortk = reinterpret_cast<uint32_t*>(s_oct + L.oct_work_off);
+  int16_t* const pt = reinterpret_cast<int16_t*>(sortk + NC);
+  int16_t* const pe = pt + NC;
+  int16_t* const pu = pe + NC;
+  int16_t* const vnext = pu + NC;
+  uint8_t* const processed = reinterpret_cast<uint8_t*>(vnext + NC);
+
+  // ---- 2. gather in cell row-major order, stably bucketed into the initial nodes
+  // (:484-526, bucket (int)(x / hX)). Fast path (<= 512 cells, K <= 3072): all cell counts
+  // up front, keys stored in cell order with independent loads (a key slot finds its cell by a
+  // binary search over the lanes' prefixes), then one in-place stable partition through
+  // registers. Otherwise two sweeps over global memory (count, then place).
   const float hX = L.hx;
-  constexpr int kPer = kOctLdsKeys / kOctThreads;  // keys per thread (blocked)
-  uint32_t kr[kPer];
-  int qb[kPer];
-  int cnt16[16];
+  constexpr int kGatherChunks = 8, kGatherRegs = 48;
+  int bcnt = 0;  // lane b < nIni: keys in bucket b
+  if (ncell <= 64 * kGatherChunks && K <= 64 * kGatherRegs) {
+    int ccnt[kGatherChunks];
 #pragma unroll
-  for (int b = 0; b < 16; b++) cnt16[b] = 0;
-#pragma unroll
-  for (int r = 0; r < kPer; r++) {
-    const int i = tid * kPer + r;
-    qb[r] = -1;
-    if (i < K) {
-      kr[r] = keys[i];
-      qb[r] = (int)((float)key_x(kr[r]) / hX);
-#pragma unroll
-      for (int b = 0; b < 16; b++) cnt16[b] += (qb[r] == b);
+    for (int ch = 0; ch < kGatherChunks; ch++) {
+      const int c = 64 * ch + lane;
+      ccnt[ch] = c < ncell ? cell_count[cbase + c] : 0;
     }
-  }
-  int pre16[16];
+    int kb = 0;
 #pragma unroll
-  for (int b = 0; b < 16; b++) {
-    pre16[b] = 0;
-    if (b < nIni) {  // nIni is uniform: every thread runs the same scans
-      int tot;
-      pre16[b] = block_scan(cnt16[b], S.wsum, &tot);
-      if (tid == 0) S.ini_cnt[b] = tot;
+    for (int ch = 0; ch < kGatherChunks; ch++) {
+      if (64 * ch < ncell) {
+        int ctot;
+        const int cex = wave_excl_scan(ccnt[ch], lane, &ctot);
+        for (int r0 = 0; r0 < ctot; r0 += 64) {
+          const int r = r0 + lane;
+          int lo = 0;
+#pragma unroll
+          for (int step = 32; step >= 1; step >>= 1) {
+            const int cand = lo + step;
+            const int pv = __shfl(cex, cand & 63, 64);
+            if (cand < 64 && pv <= r) lo = cand;
+          }
+          const int base = __shfl(cex, lo, 64);
+          if (r < ctot) keys[kb + r] = cell_keys[(cbase + 64 * ch + lo) * g->cell_cap + (r - base)];
+        }
+        kb += ctot;
+      }
     }
-  }
-  __syncthreads();
-  if (tid == 0) {
-    int run = 0, big = 0;
-    for (int b = 0; b < nIni; b++) {
-      S.ini_base[b] = run;
-      run += S.ini_cnt[b];
-      big |= S.ini_cnt[b] > kOctWaveKeys;
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    const int R = (K + 63) >> 6;
+    uint32_t kr[kGatherRegs];
+    int br[kGatherRegs];
+#pragma unroll
+    for (int r = 0; r < kGatherRegs; r++) {
+      br[r] = -1;
+      if (r < R && 64 * r + lane < K) {
+        kr[r] = keys[64 * r + lane];
+        br[r] = (int)((float)key_x(kr[r]) / hX);
+        if (br[r] >= nIni) br[r] = -1;
+      }
     }
-    S.fallback = big;
-  }
-  __syncthreads();
-  if (S.fallback) {
-    if (tid == 0) *outc = -1;
-    return;
-  }
-  {
-    int run16[16];
 #pragma unroll
-    for (int b = 0; b < 16; b++) run16[b] = b < nIni ? S.ini_base[b] + pre16[b] : 0;
+    for (int r = 0; r < kGatherRegs; r++)
+      if (r < R)
+        for (int bb = 0; bb < nIni; bb++) {
+          const int pc = __popcll(__ballot(br[r] == bb));
+          if (lane == bb) bcnt += pc;
+        }
+    int tot;
+    int brun = wave_excl_scan(lane < nIni ? bcnt : 0, lane, &tot);
 #pragma unroll
-    for (int r = 0; r < kPer; r++) {
-      if (qb[r] >= 0 && qb[r] < nIni) {
-        int pos = 0;
+    for (int r = 0; r < kGatherRegs; r++)
+      if (r < R)
+        for (int bb = 0; bb < nIni; bb++) {
+          const uint64_t mm = __ballot(br[r] == bb);
+          const int at = __shfl(brun, bb, 64);
+          if (br[r] == bb) keys[at + lanes_below(mm)] = kr[r];
+          if (lane == bb) brun += __popcll(mm);
+        }
+  } else {
+    for (int sweep = 0; sweep < 2; sweep++) {
+      int brun = 0;  // lane b: next free slot of bucket b (sweep 2)
+      if (sweep == 1) {
+        int tot;
+        brun = wave_excl_scan(lane < nIni ? bcnt : 0, lane, &tot);
+      }
+      for (int c0 = 0; c0 < ncell; c0 += 64) {
+        const int cnt = c0 + lane < ncell ? cell_count[cbase + c0 + lane] : 0;
+        int ctot;
+        const int cex = wave_excl_scan(cnt, lane, &ctot);
+        for (int r0 = 0; r0 < ctot; r0 += 64) {
+          const int r = r0 + lane;
+          // binary search on all lanes (shuffles read every lane's prefix)
+          int lo = 0;
 #pragma unroll
-        for (int b = 0; b < 16; b++)
-          if (qb[r] == b) pos = run16[b]++;
-        keys[pos] = kr[r];
+          for (int step = 32; step >= 1; step >>= 1) {
+            const int cand = lo + step;
+            const int pv = __shfl(cex, cand & 63, 64);
+            if (cand < 64 && pv <= r) lo = cand;
+          }
+          const int base = __shfl(cex, lo, 64);
+          int b = -1;
+          uint32_t k = 0;
+          if (r < ctot) {
+            k = cell_keys[(cbase + c0 + lo) * g->cell_cap + (r - base)];
+            b = (int)((float)key_x(k) / hX);
+            if (b >= nIni) b = -1;
+          }
+          for (int bb = 0; bb < nIni; bb++) {
+            const uint64_t m = __ballot(b == bb);
+            if (sweep == 1) {
+              const int at = __shfl(brun, bb, 64);
+              if (b == bb) keys[at + lanes_below(m)] = k;
+              if (lane == bb) brun += __popcll(m);
+            } else if (lane == bb) {
+              bcnt += __popcll(m);
+            }
+          }
+        }
       }
     }
   }
-  __syncthreads();
-  if (tid == 0) {
-    int m = 0;
-    for (int i = 0; i < nIni; i++) {
-      const int c = S.ini_cnt[i];
-      if (c == 0) continue;  // empty initial nodes are erased (:513-526)
-      OctNodeC nd;
-      nd.x0 = (int16_t)(int)(hX * (float)i);
-      nd.x1 = (int16_t)(int)(hX * (float)(i + 1));
+  // initial nodes: non-empty buckets in order (empty ones are erased, :513-526)
+  int m = 0;
+  {
+    int tot;
+    const int bbase = wave_excl_scan(lane < nIni ? bcnt : 0, lane, &tot);
+    const bool has = lane < nIni && bcnt > 0;
+    const uint64_t hm = __ballot(has);
+    if (has) {
+      OctNodeS nd;
+      nd.x0 = (int16_t)(int)(hX * (float)lane);
+      nd.x1 = (int16_t)(int)(hX * (float)(lane + 1));
       nd.y0 = 0;
       nd.y1 = (int16_t)(L.max_by - kMinBorder);
-      nd.kbeg = (uint16_t)S.ini_base[i];
-      nd.n = (uint16_t)c;
-      nd.seq = i;
-      lists[0][m++] = nd;
+      nd.kn = (uint32_t)bbase | (uint32_t)bcnt << 16;
+      lists[lanes_below(hm)] = nd;
     }
-    S.m = m;
-    S.seq_next = nIni;
-    S.mode = 0;
-    S.finish = 0;
-    S.nexp = 0;
+    m = __popcll(hm);
   }
-  __syncthreads();
-  int cur = 0;
-  // ---- 3. passes. node(j) gives the j-th node to divide: list order (outer pass) or the
-  // sorted vPrev order (inner iteration).
+  // ---- 3. passes
+  const int N = L.budget;
+  int cur = 0, nexp = 0;
+  bool outer = true;
   while (true) {
-    const int m = S.m;
-    const OctNodeC* Lc = lists[cur];
-    OctNodeC* Ln = lists[cur ^ 1];
-    const bool outer = S.mode == 0;
-    const int V = outer ? m : S.nexp;
-    if (!outer) {
-      // vPrev = sortk[0..V) (list positions, push order) -> descending (n, seq)
-      int P2 = 1;
+    const OctNodeS* Lc = lists + cur * NC;
+    OctNodeS* Ln = lists + (cur ^ 1) * NC;
+    const int V = outer ? m : nexp;
+    if (!outer) {  // vPrev: positions in push order -> descending (n, creation order)
+      int P2 = 64;
       while (P2 < V) P2 <<= 1;
-      for (int i = tid; i < P2; i += kOctThreads) {
-        uint64_t key = 0;  // pads sort to the end (descending)
+      for (int i = lane; i < P2; i += 64) {
+        uint32_t key = 0;  // pads sort to the end
         if (i < V) {
           const int pos = (int)sortk[i];
-          const OctNodeC& nd = Lc[pos];
-          key = ((uint64_t)nd.n << 44) | ((uint64_t)(uint32_t)nd.seq << 12) | (uint64_t)pos;
+          key = (uint32_t)node_n(Lc[pos]) << 12 | (uint32_t)(4095 - pos);
         }
         sortk[i] = key;
       }
-      __syncthreads();
-      for (int k = 2; k <= P2; k <<= 1) {
+      for (int k = 2; k <= P2; k <<= 1)
         for (int jj = k >> 1; jj > 0; jj >>= 1) {
-          for (int i = tid; i < P2; i += kOctThreads) {
+          __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+          __builtin_amdgcn_wave_barrier();
+          for (int i = lane; i < P2; i += 64) {
             const int ixj = i ^ jj;
             if (ixj > i) {
-              const uint64_t x = sortk[i], y = sortk[ixj];
+              const uint32_t x = sortk[i], y = sortk[ixj];
               const bool desc = (i & k) == 0;
               if (desc ? (x < y) : (x > y)) {
                 sortk[i] = y;
@@ -1437,153 +1495,180 @@ __global__ __launch_bounds__(kOctThreads) void octree_lds_kernel(
               }
             }
           }
-          __syncthreads();
         }
-      }
+      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+      __builtin_amdgcn_wave_barrier();
     }
-    auto node_index = [&](int j) { return outer ? j : (int)(sortk[j] & 0xfff); };
-    // -- count: t (non-empty children), e (children with > 1 key); outer pass: u (n == 1)
-    if (tid == 0) S.nbig = 0;
-    __syncthreads();
-    for (int j = tid; j < V; j += kOctThreads) {
-      const OctNodeC nd = Lc[node_index(j)];
+    auto nidx = [&](int j) { return outer ? j : 4095 - (int)(sortk[j] & 0xfffu); };
+    // -- count children: t (non-empty), e (> 1 key); pu = survivor flag (outer) or t - 1
+    for (int j0 = 0; j0 < V; j0 += 64) {
+      const int j = j0 + lane;
+      const bool valid = j < V;
+      OctNodeS nd{};
+      if (valid) nd = Lc[nidx(j)];
+      const int n = node_n(nd);
       int t = 0, e = 0;
-      if (nd.n > kOctLaneKeys) {
-        bigs[atomicAdd(&S.nbig, 1)] = j;
-      } else if (nd.n > 1) {
+      if (valid && n > 1 && n <= kOctLaneKeys) {
+        const uint32_t c = lane_divide(nd, keys, false);
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+          const int cq = (c >> (8 * q)) & 255;
+          t += cq > 0;
+          e += cq > 1;
+        }
+      }
+      uint64_t bigm = __ballot(valid && n > kOctLaneKeys);
+      while (bigm) {
+        const int bl = __builtin_ctzll(bigm);
+        bigm &= bigm - 1;
+        const OctNodeS nb = Lc[nidx(j0 + bl)];
         int cnt[4];
-        lane_divide(nd, keys, cnt, false);
+        wave_count(nb, keys, lane, cnt);
+        if (lane == bl) {
 #pragma unroll
-        for (int q = 0; q < 4; q++) {
-          t += cnt[q] > 0;
-          e += cnt[q] > 1;
+          for (int q = 0; q < 4; q++) {
+            t += cnt[q] > 0;
+            e += cnt[q] > 1;
+          }
         }
       }
-      sa[j] = t;
-      sc[j] = e;
-      sb[j] = outer ? (nd.n == 1) : t - 1;
-    }
-    __syncthreads();
-    const int nbig = S.nbig;
-    for (int bi = wid; bi < nbig; bi += kOctWaves) {
-      const int j = bigs[bi];
-      const OctNodeC nd = Lc[node_index(j)];
-      int cnt[4];
-      wave_divide(nd, keys, cnt, false, lane);
-      if (lane == 0) {
-        int t = 0, e = 0;
-#pragma unroll
-        for (int q = 0; q < 4; q++) {
-          t += cnt[q] > 0;
-          e += cnt[q] > 1;
-        }
-        sa[j] = t;
-        sc[j] = e;
-        sb[j] = outer ? 0 : t - 1;
+      if (valid) {
+        pt[j] = (int16_t)t;
+        pe[j] = (int16_t)e;
+        pu[j] = (int16_t)(outer ? (n == 1) : t - 1);
       }
     }
-    __syncthreads();
     int nproc = V;
     if (!outer) {
-      // cut: first j with m + sum_{i<=j}(t_i - 1) >= N (processing stops once the list is full)
-      block_scan_array(sb, V, S.wsum);  // exclusive prefix of (t - 1)
-      if (tid == 0) S.cut = V - 1;
-      __syncthreads();
-      for (int j = tid; j < V; j += kOctThreads)
-        if (m + sb[j] + (sa[j] - 1) >= N) atomicMin(&S.cut, j);
-      __syncthreads();
-      nproc = S.cut + 1;
-      for (int i = tid; i < V; i += kOctThreads)
-        if (i >= nproc) {
-          sa[i] = 0;
-          sc[i] = 0;
+      // processing stops once the list reaches N: first j with m + sum_{i<=j}(t_i - 1) >= N
+      int carry = 0;
+      nproc = V;
+      for (int j0 = 0; j0 < V; j0 += 64) {
+        const int j = j0 + lane;
+        const int v = j < V ? pu[j] : 0;
+        int tot;
+        const int incl = carry + wave_excl_scan(v, lane, &tot) + v;
+        const uint64_t hit = __ballot(j < V && m + incl >= N);
+        if (hit) {
+          nproc = j0 + __builtin_ctzll(hit) + 1;
+          break;
         }
-      for (int i = tid; i < m; i += kOctThreads) processed[i] = 0;
-      __syncthreads();
-      for (int j = tid; j < nproc; j += kOctThreads) processed[node_index(j)] = 1;
-      __syncthreads();
-      for (int i = tid; i < m; i += kOctThreads) sb[i] = processed[i] ? 0 : 1;  // survivors
-      __syncthreads();
+        carry += tot;
+      }
+      for (int i = lane; i < m; i += 64) processed[i] = 0;
+      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      for (int j = lane; j < nproc; j += 64) processed[nidx(j)] = 1;
+      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      for (int i = lane; i < m; i += 64) pu[i] = (int16_t)(processed[i] ? 0 : 1);
     }
-    const int T = block_scan_array(sa, V, S.wsum);  // push-order child positions
-    const int E = block_scan_array(sc, V, S.wsum);
-    const int U = block_scan_array(sb, m, S.wsum);  // survivors keep their order
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    const int T = wave_scan_array(pt, nproc, lane);  // push-order child positions
+    const int E = wave_scan_array(pe, nproc, lane);
+    const int U = wave_scan_array(pu, m, lane);      // survivors keep their order
     const int newm = T + U;
-    const int seq0 = S.seq_next;
-    const bool ovf = newm > NC || E > NC;
-    if (!ovf) {
-      // -- divide (in place) and place children: push order gpos -> list position T-1-gpos
-      auto place = [&](int j, const OctNodeC& nd, const int cnt[4]) {
-        OctNodeC ch[4];
-        node_children(nd, cnt, ch);
-        int gpos = sa[j], epos = sc[j];
+    if (newm > NC || E > NC) {
+      if (lane == 0) atomicOr(err, kErrNodeOverflow);
+      break;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    // -- divide in place and place children: push order gpos -> list position T-1-gpos
+    auto place = [&](int j, const OctNodeS& nd, uint32_t c4) {
+      int gpos = pt[j], epos = pe[j];
+      const int xm = node_xm(nd), ym = node_ym(nd);
+      const int16_t xs[3] = {nd.x0, (int16_t)xm, nd.x1};
+      const int16_t ys[3] = {nd.y0, (int16_t)ym, nd.y1};
+      int start = node_kbeg(nd);
 #pragma unroll
-        for (int q = 0; q < 4; q++) {
-          if (ch[q].n == 0) continue;
-          ch[q].seq = seq0 + gpos;
+      for (int q = 0; q < 4; q++) {
+        const int cq = (int)((c4 >> (8 * q)) & 255u);
+        if (cq > 0) {
+          OctNodeS ch;
+          ch.x0 = xs[q & 1];
+          ch.x1 = xs[(q & 1) + 1];
+          ch.y0 = ys[q >> 1];
+          ch.y1 = ys[(q >> 1) + 1];
+          ch.kn = (uint32_t)start | (uint32_t)cq << 16;
           const int pos = T - 1 - gpos;
-          Ln[pos] = ch[q];
-          if (ch[q].n > 1) vnext[epos++] = pos;
+          Ln[pos] = ch;
+          if (cq > 1) vnext[epos++] = (int16_t)pos;
           gpos++;
         }
-      };
-      for (int j = tid; j < nproc; j += kOctThreads) {
-        const OctNodeC nd = Lc[node_index(j)];
-        if (nd.n > 1 && nd.n <= kOctLaneKeys) {
-          int cnt[4];
-          lane_divide(nd, keys, cnt, true);
-          place(j, nd, cnt);
+        start += cq;
+      }
+    };
+    for (int j0 = 0; j0 < nproc; j0 += 64) {
+      const int j = j0 + lane;
+      const bool valid = j < nproc;
+      OctNodeS nd{};
+      if (valid) nd = Lc[nidx(j)];
+      const int n = node_n(nd);
+      if (valid && n > 1 && n <= kOctLaneKeys) place(j, nd, lane_divide(nd, keys, true));
+      uint64_t bigm = __ballot(valid && n > kOctLaneKeys);
+      while (bigm) {
+        const int bl = __builtin_ctzll(bigm);
+        bigm &= bigm - 1;
+        const OctNodeS nb = Lc[nidx(j0 + bl)];
+        int cnt[4];
+        wave_partition(nb, keys, gscratch, lane, cnt);
+        if (lane == 0) {
+          // counts can exceed 255 here: place() takes 8-bit counts, so place big ones inline
+          int gpos = pt[j0 + bl], epos = pe[j0 + bl];
+          const int xm = node_xm(nb), ym = node_ym(nb);
+          const int16_t xs[3] = {nb.x0, (int16_t)xm, nb.x1};
+          const int16_t ys[3] = {nb.y0, (int16_t)ym, nb.y1};
+          int start = node_kbeg(nb);
+          for (int q = 0; q < 4; q++) {
+            if (cnt[q] > 0) {
+              OctNodeS ch;
+              ch.x0 = xs[q & 1];
+              ch.x1 = xs[(q & 1) + 1];
+              ch.y0 = ys[q >> 1];
+              ch.y1 = ys[(q >> 1) + 1];
+              ch.kn = (uint32_t)start | (uint32_t)cnt[q] << 16;
+              const int pos = T - 1 - gpos;
+              Ln[pos] = ch;
+              if (cnt[q] > 1) vnext[epos++] = (int16_t)pos;
+              gpos++;
+            }
+            start += cnt[q];
+          }
         }
       }
-      for (int bi = wid; bi < nbig; bi += kOctWaves) {
-        const int j = bigs[bi];
-        if (j >= nproc) continue;
-        const OctNodeC nd = Lc[node_index(j)];
-        int cnt[4];
-        wave_divide(nd, keys, cnt, true, lane);
-        if (lane == 0) place(j, nd, cnt);
-      }
-      // survivors
-      if (outer) {
-        for (int i = tid; i < m; i += kOctThreads)
-          if (Lc[i].n == 1) Ln[T + sb[i]] = Lc[i];
-      } else {
-        for (int i = tid; i < m; i += kOctThreads)
-          if (!processed[i]) Ln[T + sb[i]] = Lc[i];
-      }
     }
-    __syncthreads();
-    for (int i = tid; i < E; i += kOctThreads) sortk[i] = (uint64_t)vnext[i];
-    if (tid == 0) {
-      if (ovf) {
-        atomicOr(err, kErrNodeOverflow);
-        S.finish = 1;
-      } else {
-        S.m = newm;
-        S.seq_next = seq0 + T;
-        S.nexp = E;
-        if (newm >= N || newm == m) S.finish = 1;
-        else if (outer && newm + E * 3 > N) S.mode = 1;
-      }
+    for (int i = lane; i < m; i += 64) {
+      const OctNodeS nd = Lc[i];
+      if (outer ? node_n(nd) == 1 : !processed[i]) Ln[T + pu[i]] = nd;
     }
-    if (!ovf) cur ^= 1;
-    __syncthreads();
-    if (S.finish) break;
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    for (int i = lane; i < E; i += 64) sortk[i] = (uint32_t)vnext[i];
+    const int mprev = m;
+    m = newm;
+    nexp = E;
+    cur ^= 1;
+    if (newm >= N || newm == mprev) break;
+    if (outer && newm + E * 3 > N) outer = false;
   }
   // ---- 4. retain the best key of each node (:682-701): strict '>' keeps the first maximum
-  const int m = S.m;
-  const OctNodeC* Lf = lists[cur];
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  const OctNodeS* Lf = lists + cur * NC;
   const int mout = min(m, L.out_cap);
-  for (int j = tid; j < mout; j += kOctThreads) {
-    const OctNodeC nd = Lf[j];
-    uint32_t best = keys[nd.kbeg];
-    for (int k = 1; k < nd.n; k++) {
-      const uint32_t kk = keys[nd.kbeg + k];
+  for (int j = lane; j < mout; j += 64) {
+    const OctNodeS nd = Lf[j];
+    const int kb = node_kbeg(nd), n = node_n(nd);
+    uint32_t best = keys[kb];
+    for (int k = 1; k < n; k++) {
+      const uint32_t kk = keys[kb + k];
       if (key_score(kk) > key_score(best)) best = kk;
     }
     outk[j] = best;
   }
-  if (tid == 0) {
+  if (lane == 0) {
     if (m > L.out_cap) atomicOr(err, kErrNodeOverflow);
     *outc = mout;
   }
@@ -1849,12 +1934,9 @@ void launch_extract(const ImageBatch& b, const OrbGeomDev& gd, int n_images, hip
                  dim3(64 * kCellWaves), (size_t)kCellWaves * g.fast_lds_per_wave, st, b,
                  gd.dev, gd.cells, gd.ws.cell_keys,
                      gd.ws.cell_count, gd.ws.err);
-  {
-    const size_t lds = (size_t)4 * kOctLdsKeys + (size_t)g.oct_nc * (2 * sizeof(OctNodeC) + 8 + 5 * 4 + 1);
-    SLAMGPU_LAUNCH("octree", st, octree_lds_kernel, dim3(g.nlevels, n_images), dim3(kOctThreads),
-                   lds, st, gd.dev, gd.ws.cell_keys, gd.ws.cell_count, gd.ws.oct_keys,
-                   gd.ws.oct_count, gd.ws.err);
-  }
+  SLAMGPU_LAUNCH("octree", st, octree_img_kernel, dim3(n_images), dim3(64 * g.nlevels),
+                 (size_t)g.oct_lds_bytes, st, gd.dev, gd.ws.cell_keys, gd.ws.cell_count,
+                 gd.ws.key_scratch, gd.ws.oct_keys, gd.ws.oct_count, gd.ws.err);
   SLAMGPU_LAUNCH("octree_global", st, octree_kernel, dim3(g.nlevels, n_images), dim3(kOctThreads), 0, st, gd.dev,
                      gd.ws.cell_keys, gd.ws.cell_count, gd.ws.key_scratch, gd.ws.node_scratch,
                      gd.ws.oct_keys, gd.ws.oct_count, gd.ws.err);
