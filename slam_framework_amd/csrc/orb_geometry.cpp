@@ -194,13 +194,16 @@ int compute_geometry(const OrbParams& p, int cols, int rows, OrbGeom* g,
   g->cell_cap = ((max_wcell + 1) / 2) * ((max_hcell + 1) / 2);
   // tile: dwords covering the cell view from iniX & ~3, plus one spare dword per row for the
   // prefilter's right-neighbour reads
-  g->fast_tile_stride = round_up(max_wcell + 6 + 3, 4) + 4;
+  // fast_cells_kernel is compiled for row strides 64 and 128 (tile and score map share it; the
+  // score map is indexed by tile column). A row holds the cell view from iniX & ~3 plus the
+  // prefilter's spare right-neighbour dword.
+  g->fast_tile_stride = round_up(max_wcell + 6 + 3, 4) + 4 <= 64 ? 64 : 128;
   g->fast_tile_rows = max_hcell + 6;
-  g->fast_score_stride = round_up(max_wcell + 6 + 3, 4);  // indexed by tile column
+  g->fast_score_stride = g->fast_tile_stride;
   g->fast_score_rows = max_hcell;
   g->fast_lds_per_wave = round_up(g->fast_tile_stride * g->fast_tile_rows, 16) +
                          round_up(g->fast_score_stride * g->fast_score_rows, 16) +
-                         round_up(2 * g->fast_score_stride * g->fast_score_rows, 16);
+                         round_up(2 * max_wcell * max_hcell, 16);  // u16 candidate list
   if (max_wcell > 64) return -4;
   // pyr_down reads the source bytes of 4 adjacent output columns as one 8-byte window
   // starting at sx(x0): sx(x0 + 3) + 1 - sx(x0) <= 7 (any scale factor up to ~2).

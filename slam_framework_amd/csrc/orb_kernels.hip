@@ -406,6 +406,39 @@ __device__ __forceinline__ int fast_s(const uint8_t* t, int o, const int kTileSt
   return max(sd, -sb);
 }
 
+// fast_s on int16 pairs: x_k = (v - p_k, p_k - v), so one min/max network yields both the dark
+// arc minimum (low half) and minus the bright arc maximum (high half): s = max(lo, hi).
+typedef short i16x2 __attribute__((ext_vector_type(2)));
+template <int ts>
+__device__ __forceinline__ int fast_s_pk(const uint8_t* t, int o) {
+  const int v = t[o];
+  const i16x2 v2 = {(short)v, (short)-v}, np = {-1, 1};
+  // ring offsets relative to the top-left of the 7x7 window (immediates, all >= 0)
+  constexpr int offs[16] = {3 + 6 * ts, 4 + 6 * ts, 5 + 5 * ts, 6 + 4 * ts, 6 + 3 * ts, 6 + 2 * ts,
+                            5 + ts,     4,          3,          2,          1 + ts,     2 * ts,
+                            3 * ts,     4 * ts,     1 + 5 * ts, 2 + 6 * ts};
+  const uint8_t* w = t + o - 3 - 3 * ts;
+  i16x2 x[16];
+#pragma unroll
+  for (int k = 0; k < 16; k++) {
+    const uint32_t p = w[offs[k]];
+    x[k] = __builtin_bit_cast(i16x2, p * 0x10001u) * np + v2;
+  }
+  i16x2 m2[16], m4[16];
+#pragma unroll
+  for (int k = 0; k < 16; k++) m2[k] = __builtin_elementwise_min(x[k], x[(k + 1) & 15]);
+#pragma unroll
+  for (int k = 0; k < 16; k++) m4[k] = __builtin_elementwise_min(m2[k], m2[(k + 2) & 15]);
+  i16x2 best = {-32768, -32768};
+#pragma unroll
+  for (int k = 0; k < 16; k++) {
+    const i16x2 arc = __builtin_elementwise_min(__builtin_elementwise_min(m4[k], m4[(k + 4) & 15]),
+                                                x[(k + 8) & 15]);
+    best = __builtin_elementwise_max(best, arc);
+  }
+  return max((int)best.x, (int)best.y);
+}
+
 // Exact necessary condition for a corner at threshold t: every 9-arc of the 16-ring contains
 // one pixel of each opposite pair (0,8), (4,12), (2,10), (6,14) -- FAST_t's own pre-test.
 __device__ __forceinline__ bool fast_maybe(const uint8_t* t, int o, int th,
@@ -423,23 +456,12 @@ __device__ __forceinline__ bool fast_maybe(const uint8_t* t, int o, int th,
   return dark || bright;
 }
 
-// SWAR byte compares on 4 pixels per lane: bit 7 of each byte of the result is that byte's
-// answer, other bits are garbage (callers mask with kH). (Hacker's Delight 2-18 style.)
+// bit 7 of every byte: the per-pixel flag format of the prefilter masks
 constexpr uint32_t kH = 0x80808080u;
-__device__ __forceinline__ uint32_t swar_lt(uint32_t a, uint32_t b) {  // a < b
-  const uint32_t d = (a | kH) - (b & ~kH);  // bit 7: (a & 0x7f) >= (b & 0x7f), no borrows
-  return (~a & b) | (~(a ^ b) & ~d);
-}
-__device__ __forceinline__ uint32_t swar_sat_sub(uint32_t v, uint32_t t) {  // max(v - t, 0)
-  const uint32_t diff = ((v | kH) - (t & ~kH)) ^ ((v ^ ~t) & kH);
-  const uint32_t neg = ((swar_lt(v, t) & kH) >> 7) * 0xffu;
-  return diff & ~neg;
-}
 
 // A wave runs kCellsPerWave consecutive cells of one image: the next cell's tile is loaded
 // into registers while the current one is processed from LDS.
 constexpr int kCellsPerWave = 4;
-constexpr int kTileRegs = (18 * 66 + 63) / 64;  // dwords per lane for the largest cell view
 
 struct CellView {
   int level, ini_x, ini_y, vw, vh, pitch, ax, off, nd;
@@ -470,6 +492,7 @@ __device__ __forceinline__ uint4 readlane4(const uint4& x, int j) {
                     __builtin_amdgcn_readlane(x.z, j), __builtin_amdgcn_readlane(x.w, j));
 }
 
+template <int TS>
 __global__ __launch_bounds__(256) void fast_cells_kernel(ImageBatch b,
                                                          const OrbGeom* __restrict__ g,
                                                          const CellDesc* __restrict__ cells,
@@ -478,7 +501,9 @@ __global__ __launch_bounds__(256) void fast_cells_kernel(ImageBatch b,
                                                          uint32_t* __restrict__ err) {
   extern __shared__ __attribute__((aligned(16))) uint8_t s_fast[];
   const int wid = wave_id(), lane = threadIdx.x & 63;
-  const int kTileStride = g->fast_tile_stride, kScoreStride = g->fast_score_stride;
+  constexpr int kTileStride = TS, kScoreStride = TS;  // == g->fast_tile_stride
+  constexpr int kLpr = TS / 4, kRps = 64 / kLpr;        // tile copy: lanes per row, rows per step
+  constexpr int kTileSteps = (70 + kRps - 1) / kRps;    // cell views are <= 70 rows
   const int img = blockIdx.y;
   const int ncells = g->cells_per_image;
   const int c0 = (blockIdx.x * kCellWaves + wid) * kCellsPerWave;
@@ -492,33 +517,22 @@ __global__ __launch_bounds__(256) void fast_cells_kernel(ImageBatch b,
   uint16_t* cand =
       reinterpret_cast<uint16_t*>(sc + ((kScoreStride * g->fast_score_rows + 15) & ~15));
   const int tmin = min(g->ini_th, g->min_th);
-  const uint32_t tt = (uint32_t)tmin * 0x01010101u;
 
   // ---- tile prefetch: aligned dwords covering [ini_x & ~3, ini_x + vw) x [ini_y, ini_y + vh)
-  // into registers (tile column c = image column ax + c). Elements past the end re-copy a
-  // last-row dword (same value, same place).
-  uint32_t tv[kTileRegs];
-  int tlo[kTileRegs];
+  // into registers, lane = (row within a step, dword): each element is a scalar row base plus a
+  // per-lane offset. Tile column c = image column ax + c.
+  const int plr = lane / kLpr, pld = lane % kLpr;
+  uint32_t tv[kTileSteps];
   int tn = 0;
   auto prefetch = [&](const CellView& v) {
-    tn = __builtin_amdgcn_readfirstlane(v.aligned ? (v.nd * v.vh + 63) >> 6 : 0);  // uniform
+    tn = v.aligned ? (v.vh + kRps - 1) / kRps : 0;  // wave-uniform
     const uint8_t* src = v.base + (int64_t)v.ini_y * v.pitch + v.ax;
-    const int dr = 64 / v.nd, dq = 64 - dr * v.nd;
-    int r = lane / v.nd, q = lane - (lane / v.nd) * v.nd;
+    const int goff = __umul24(plr, v.pitch) + 4 * pld;
+    const bool dok = pld < v.nd;
 #pragma unroll
-    for (int k = 0; k < kTileRegs; k++) {
-      if (k < tn) {
-        const int rc = min(r, v.vh - 1);
-        tlo[k] = rc * kTileStride + 4 * q;
-        tv[k] = *reinterpret_cast<const uint32_t*>(src + (__umul24(rc, v.pitch) + 4 * q));
-      }
-      r += dr;
-      q += dq;
-      if (q >= v.nd) {
-        q -= v.nd;
-        r++;
-      }
-    }
+    for (int k = 0; k < kTileSteps; k++)
+      if (k < tn && dok && k * kRps + plr < v.vh)
+        tv[k] = *reinterpret_cast<const uint32_t*>(src + (int64_t)(k * kRps) * v.pitch + goff);
   };
   CellView nxt = cell_view(b, g, img, in_pitch, readlane4(my_desc, 0));
   if (nxt.vh > 0) prefetch(nxt);
@@ -537,9 +551,11 @@ __global__ __launch_bounds__(256) void fast_cells_kernel(ImageBatch b,
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     __builtin_amdgcn_wave_barrier();  // previous cell's LDS reads are done
     if (v.aligned) {
+      const bool dok = pld < v.nd;
 #pragma unroll
-      for (int k = 0; k < kTileRegs; k++)
-        if (k < tn) *reinterpret_cast<uint32_t*>(tile + tlo[k]) = tv[k];
+      for (int k = 0; k < kTileSteps; k++)
+        if (k < tn && dok && k * kRps + plr < v.vh)
+          *reinterpret_cast<uint32_t*>(tile + (k * kRps + plr) * TS + 4 * pld) = tv[k];
     } else {  // caller image with an odd pitch/base: byte copy
       for (int r = 0; r < v.vh; r++)
         for (int x = lane; x < v.vw + v.off; x += 64)
@@ -577,23 +593,41 @@ __global__ __launch_bounds__(256) void fast_cells_kernel(ImageBatch b,
         const uint32_t u2 = rd(2, 0), u2m = rd(2, qm), u2p = rd(2, 1);
         const uint32_t d2 = rd(-2, 0), d2m = rd(-2, qm), d2p = rd(-2, 1);
         const uint32_t p0 = rd(3, 0), p8 = rd(-3, 0);
-        const uint32_t p4 = __builtin_amdgcn_alignbyte(cp, c, 3);     // (+3, 0)
-        const uint32_t p12 = __builtin_amdgcn_alignbyte(c, cm, 1);    // (-3, 0)
-        const uint32_t p2 = __builtin_amdgcn_alignbyte(u2p, u2, 2);   // (+2, +2)
-        const uint32_t p14 = __builtin_amdgcn_alignbyte(u2, u2m, 2);  // (-2, +2)
-        const uint32_t p6 = __builtin_amdgcn_alignbyte(d2p, d2, 2);   // (+2, -2)
-        const uint32_t p10 = __builtin_amdgcn_alignbyte(d2, d2m, 2);  // (-2, -2)
-        const uint32_t vlo = swar_sat_sub(c, tt);    // p darker  iff p < vlo
-        const uint32_t vhi = ~swar_sat_sub(~c, tt);  // p brighter iff p > vhi
-        const uint32_t dark = (swar_lt(p0, vlo) | swar_lt(p8, vlo)) &
-                              (swar_lt(p4, vlo) | swar_lt(p12, vlo)) &
-                              (swar_lt(p2, vlo) | swar_lt(p10, vlo)) &
-                              (swar_lt(p6, vlo) | swar_lt(p14, vlo));
-        const uint32_t bright = (swar_lt(vhi, p0) | swar_lt(vhi, p8)) &
-                                (swar_lt(vhi, p4) | swar_lt(vhi, p12)) &
-                                (swar_lt(vhi, p2) | swar_lt(vhi, p10)) &
-                                (swar_lt(vhi, p6) | swar_lt(vhi, p14));
-        m = (dark | bright) & vmask;
+        // even pixels (bytes 0, 2) and odd pixels (bytes 1, 3) of each ring position as u16
+        // pairs; v_perm picks the shifted bytes straight out of two adjacent dwords
+        typedef unsigned short u16x2_t __attribute__((ext_vector_type(2)));
+        auto U = [](uint32_t x) { return __builtin_bit_cast(u16x2_t, x); };
+        const u16x2_t tt2 = U((uint32_t)tmin * 0x10001u);
+        uint32_t any[2];
+#pragma unroll
+        for (int h = 0; h < 2; h++) {
+          const uint32_t sh = h ? 0x00010001u : 0u;  // odd pixels: data selectors + 1
+          const uint32_t s0 = 0x0c020c00u + sh, s1 = 0x0c030c01u + sh, s2 = 0x0c040c02u + sh,
+                         s3 = 0x0c050c03u + sh;
+          const u16x2_t v = U(__builtin_amdgcn_perm(c, c, s0));
+          const u16x2_t a0 = U(__builtin_amdgcn_perm(p0, p0, s0));      // (0, +3)
+          const u16x2_t a8 = U(__builtin_amdgcn_perm(p8, p8, s0));      // (0, -3)
+          const u16x2_t a4 = U(__builtin_amdgcn_perm(cp, c, s3));       // (+3, 0)
+          const u16x2_t a12 = U(__builtin_amdgcn_perm(c, cm, s1));      // (-3, 0)
+          const u16x2_t a2 = U(__builtin_amdgcn_perm(u2p, u2, s2));     // (+2, +2)
+          const u16x2_t a14 = U(__builtin_amdgcn_perm(u2, u2m, s2));    // (-2, +2)
+          const u16x2_t a6 = U(__builtin_amdgcn_perm(d2p, d2, s2));     // (+2, -2)
+          const u16x2_t a10 = U(__builtin_amdgcn_perm(d2, d2m, s2));    // (-2, -2)
+          // FAST_t pre-test on the 4 opposite pairs: darker needs min(pair) < v - t for all
+          // pairs, brighter needs max(pair) > v + t for all pairs
+          const u16x2_t D = __builtin_elementwise_max(
+              __builtin_elementwise_max(__builtin_elementwise_min(a0, a8), __builtin_elementwise_min(a4, a12)),
+              __builtin_elementwise_max(__builtin_elementwise_min(a2, a10), __builtin_elementwise_min(a6, a14)));
+          const u16x2_t B = __builtin_elementwise_min(
+              __builtin_elementwise_min(__builtin_elementwise_max(a0, a8), __builtin_elementwise_max(a4, a12)),
+              __builtin_elementwise_min(__builtin_elementwise_max(a2, a10), __builtin_elementwise_max(a6, a14)));
+          const u16x2_t lo = __builtin_elementwise_sub_sat(v, tt2), hi = v + tt2;
+          any[h] = __builtin_bit_cast(uint32_t, __builtin_elementwise_sub_sat(lo, D)) |
+                   __builtin_bit_cast(uint32_t, __builtin_elementwise_sub_sat(B, hi));
+        }
+        // non-zero u16 lane -> bit 7 of that pixel's byte
+        m = ((((any[0] + 0x7fff7fffu) & 0x80008000u) >> 8) | ((any[1] + 0x7fff7fffu) & 0x80008000u)) &
+            vmask;
         *reinterpret_cast<uint32_t*>(sc + rr * kScoreStride + 4 * Q) = 0;
       }
       // row-major compaction: exclusive prefix of per-lane counts (0..4) via 3 ballots
@@ -609,62 +643,67 @@ __global__ __launch_bounds__(256) void fast_cells_kernel(ImageBatch b,
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     __builtin_amdgcn_wave_barrier();
     // ---- exact FAST score of the survivors
-    int smax = 0;
     for (int i = lane; i < ncand; i += 64) {
       const int pix = cand[i];
       const int r = pix / kScoreStride, cc = pix - r * kScoreStride;
-      const int s = fast_s(tile, (r + 3) * kTileStride + cc, kTileStride);
-      const int sv = s < 0 ? 0 : s;
-      sc[pix] = (uint8_t)sv;
-      smax = max(smax, sv);
+      const int s = fast_s_pk<TS>(tile, (r + 3) * kTileStride + cc);
+      sc[pix] = (uint8_t)(s < 0 ? 0 : s);
     }
-    smax = wave_max(smax);
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     __builtin_amdgcn_wave_barrier();
     uint32_t* out = cell_keys + slot * g->cell_cap;
-    // FAST at iniTh; the reference re-runs at minTh when the iniTh *output* (after NMS) is
-    // empty (:753-757) -- corners can exist at iniTh and still all be suppressed by equal
-    // neighbours. Non-survivors of the prefilter have s <= tmin: never corners, score 0 for NMS.
-    int count = 0;
-    for (int pass = (smax > g->ini_th) ? 0 : 1; pass < 2 && count == 0; pass++) {
-      const int th = pass == 0 ? g->ini_th : g->min_th;
-      for (int i0 = 0; i0 < ncand; i0 += 64) {
-        const int i = i0 + lane;
-        bool keep = false;
-        int s = 0, r = 0, cc = 0;
-        if (i < ncand) {
-          const int pix = cand[i];
-          r = pix / kScoreStride;
-          cc = pix - r * kScoreStride;
-          s = sc[pix];
-          if (s > th) {
-            const int score = s - 1;
-            keep = true;
+    // NMS at iniTh and at minTh in one sweep: the reference re-runs FAST at minTh when the iniTh
+    // *output* (after NMS) is empty (:753-757). Strict '>' against the 8 neighbours' scores at
+    // that threshold, zero outside the detect area; non-candidates have s <= tmin (score 0).
+    // iniTh survivors go straight out, minTh survivors are compacted in place in cand[].
+    const int t0 = g->ini_th, t1 = g->min_th;
+    int count0 = 0, count1 = 0;
+    for (int i0 = 0; i0 < ncand; i0 += 64) {
+      const int i = i0 + lane;
+      bool k0 = false, k1 = false;
+      int s = 0, r = 0, cc = 0, pix = 0;
+      if (i < ncand) {
+        pix = cand[i];
+        r = pix / kScoreStride;
+        cc = pix - r * kScoreStride;
+        s = sc[pix];
+        const int score = s - 1;
+        k0 = s > t0;
+        k1 = s > t1;
+        if (k0 || k1) {
 #pragma unroll
-            for (int dy = -1; dy <= 1; dy++)
+          for (int dy = -1; dy <= 1; dy++)
 #pragma unroll
-              for (int dx = -1; dx <= 1; dx++) {
-                if (dx == 0 && dy == 0) continue;
-                const int rr = r + dy, c2 = cc + dx;
-                int ns = 0;
-                if (rr >= 0 && rr < dh && c2 >= off + 3 && c2 < off + 3 + dw) {
-                  const int q = sc[rr * kScoreStride + c2];
-                  ns = q > th ? q - 1 : 0;
-                }
-                keep = keep && (score > ns);
-              }
-          }
+            for (int dx = -1; dx <= 1; dx++) {
+              if (dx == 0 && dy == 0) continue;
+              const int rr = r + dy, c2 = cc + dx;
+              int q = 0;
+              if (rr >= 0 && rr < dh && c2 >= off + 3 && c2 < off + 3 + dw)
+                q = sc[rr * kScoreStride + c2];
+              k0 = k0 && score > (q > t0 ? q - 1 : 0);
+              k1 = k1 && score > (q > t1 ? q - 1 : 0);
+            }
         }
-        const uint64_t m = __ballot(keep);
-        if (keep) {
-          const int pos = count + lanes_below(m);
-          if (pos < g->cell_cap) {
-            const int x_rel = v.ax + cc - kMinBorder, y_rel = v.ini_y + 3 + r - kMinBorder;
-            out[pos] = pack_key(x_rel, y_rel, s - 1);
-          }
-        }
-        count += __popcll(m);
       }
+      const uint64_t m0 = __ballot(k0), m1 = __ballot(k1);
+      if (k0) {
+        const int pos = count0 + lanes_below(m0);
+        if (pos < g->cell_cap) out[pos] = pack_key(v.ax + cc - kMinBorder, v.ini_y + 3 + r - kMinBorder, s - 1);
+      }
+      if (k1) cand[count1 + lanes_below(m1)] = (uint16_t)pix;  // never passes the read index
+      count0 += __popcll(m0);
+      count1 += __popcll(m1);
+    }
+    int count = count0;
+    if (count0 == 0) {
+      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      for (int i = lane; i < min(count1, g->cell_cap); i += 64) {
+        const int pix = cand[i];
+        const int r = pix / kScoreStride, cc = pix - r * kScoreStride;
+        out[i] = pack_key(v.ax + cc - kMinBorder, v.ini_y + 3 + r - kMinBorder, sc[pix] - 1);
+      }
+      count = count1;
     }
     if (lane == 0) {
       if (count > g->cell_cap) {
@@ -1928,7 +1967,15 @@ void launch_extract(const ImageBatch& b, const OrbGeomDev& gd, int n_images, hip
     SLAMGPU_LAUNCH("blur7_edges", st, blur7_edges_kernel, dim3(strips, n_images), dim3(64), 0, st,
                    b, gd.dev);
   }
-  SLAMGPU_LAUNCH("fast_cells", st, fast_cells_kernel,
+  if (g.fast_tile_stride == 64)
+    SLAMGPU_LAUNCH("fast_cells", st, fast_cells_kernel<64>,
+                 dim3((g.cells_per_image + kCellWaves * kCellsPerWave - 1) /
+                          (kCellWaves * kCellsPerWave), n_images),
+                 dim3(64 * kCellWaves), (size_t)kCellWaves * g.fast_lds_per_wave, st, b,
+                 gd.dev, gd.cells, gd.ws.cell_keys,
+                     gd.ws.cell_count, gd.ws.err);
+  else
+    SLAMGPU_LAUNCH("fast_cells", st, fast_cells_kernel<128>,
                  dim3((g.cells_per_image + kCellWaves * kCellsPerWave - 1) /
                           (kCellWaves * kCellsPerWave), n_images),
                  dim3(64 * kCellWaves), (size_t)kCellWaves * g.fast_lds_per_wave, st, b,
