@@ -36,6 +36,26 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 LEVEL_PX = None  # filled from the context geometry
 
 
+TRAFFIC_FILE = os.path.join(ROOT, "profiles", "traffic.json")
+
+
+def measured_traffic(kernel, batch):
+    """HBM bytes per dispatch of `kernel` measured by tools/pmc_traffic.sh + tools/traffic.py on
+    this bench configuration (rocprofv3 FETCH_SIZE/WRITE_SIZE passes, gfx950 read calibration),
+    committed as profiles/traffic.json; None when absent or measured on another batch size."""
+    try:
+        with open(TRAFFIC_FILE) as f:
+            d = json.load(f)
+    except (OSError, ValueError):
+        return None, None
+    if d.get("batch") != batch:
+        return None, None
+    for k, v in d.get("kernels", {}).items():
+        if k.split("<")[0].replace("_kernel", "") == kernel:
+            return v.get("hbm_bytes_per_dispatch"), d.get("source")
+    return None, None
+
+
 def kernel_bytes(name, n_images, n_frames, kp_per_image, level_px, n_queries):
     """Algorithmic bytes one step moves through the named kernel (all its launches)."""
     px = sum(level_px)
@@ -75,6 +95,9 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
+    # One explicit stream for torch ops and library launches alike: a null stream handle would
+    # put the library's kernels on the context's own (non-blocking) stream, unordered with torch.
+    torch.cuda.set_stream(torch.cuda.Stream(device=dev))
     if world > 1:
         dist.init_process_group("nccl", device_id=dev)
 
@@ -186,6 +209,10 @@ def main():
             "avg_launch_us": round(avg_launch_s * 1e6, 2), "launches": dom_n,
             "algorithmic_bytes_per_launch": per_launch_bytes,
         }
+        traffic, tsrc = measured_traffic(dominant, B)
+        if traffic is not None:
+            roofline["traffic"] = round(traffic)
+            roofline["traffic_source"] = tsrc
         cpu = None
         if not args.no_cpu_baseline:
             cpu = cpu_baseline(Ls, Rs, args.cpu_frames)
@@ -227,7 +254,7 @@ def cpu_baseline(Ls, Rs, n_frames):
     g = O.grid_geom(S.KITTI_COLS, S.KITTI_ROWS)
     cam = S.KITTI_CAM
     threads = min(16, os.cpu_count() or 1)
-    per_thread = max(2, (n_frames or 8 * threads) // threads)
+    per_thread = max(2, (n_frames or 16 * threads) // threads)
     D = len(Ls)
 
     def run(tid):
