@@ -552,99 +552,155 @@ __global__ __launch_bounds__(64) void search_resolve_kernel(
   if constexpr (kF2F) check_ori = poses[f].check_ori != 0;
   const int q0 = io.q_start[f], qn = io.q_count[f];
   int nm = 0;
-  // queries are resolved in order; everything the sequential loop reads (kept candidates,
-  // query identity, keypoint angle/octave) is staged through LDS so the loop has no global loads
-  __shared__ uint64_t s_top[256 * kTopK];
-  __shared__ int s_nc[256];
-  __shared__ int s_mpid[256];
-  __shared__ float s_qang[256];
+  // The reference resolves queries strictly in order: a query takes its first candidate (in
+  // (distance, GetFeaturesInArea) order) not claimed by an earlier *blocking* query
+  // (orb_matcher.cpp:59-63, :1389-1393). Here 64 queries (one per lane) are resolved together
+  // to the same result: each lane's choice is iterated to a fixed point against the claims
+  // committed so far and the choices of the earlier lanes (owner[] holds the lowest blocking
+  // lane per keypoint) -- lane i is final once lanes < i are, and conflicts are rare, so a few
+  // rounds suffice. A lane whose kept top-K is exhausted while more candidates exist is rescanned
+  // alone, at its place in the order. For non-blocking duplicates the last writer of mp[idx]
+  // wins, as in the sequential loop.
   __shared__ float s_kang[4096];
   __shared__ int8_t s_koct[4096];
+  __shared__ int owner[4096];
   for (int i = lane; i < n; i += 64) {
     const KeyPoint kp = F.kps[i];
     s_kang[i] = kp.angle;
     s_koct[i] = (int8_t)kp.octave;
-  }
-  for (int c0 = 0; c0 < qn; c0 += 256) {
-  const int cn = min(256, qn - c0);
-  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  for (int i = lane; i < cn * kTopK; i += 64) s_top[i] = mw.topk[(int64_t)(q0 + c0) * kTopK + i];
-  for (int i = lane; i < cn; i += 64) {
-    s_nc[i] = mw.ncand[q0 + c0 + i];
-    const Q& qq = queries[q0 + c0 + i];
-    s_mpid[i] = (qq.mp_id & 0x7fffffff) | (qq.blocks ? (int)0x80000000u : 0);
-    float ang = 0.f;
-    if constexpr (kF2F) ang = qq.last_angle;
-    s_qang[i] = ang;
+    owner[i] = INT_MAX;
   }
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
   __builtin_amdgcn_wave_barrier();
-  for (int qc = 0; qc < cn; qc++) {
-    const int qi = c0 + qc;
+  const int need = kF2F ? 1 : 2;
+  auto is_claimed = [&](int idx) { return (claimed[idx >> 5] >> (idx & 31)) & 1u; };
+  for (int c0 = 0; c0 < qn; c0 += 64) {
+    const int qi = c0 + lane;
+    const bool valid = qi < qn;
     const int q = q0 + qi;
-    const int nc = s_nc[qc];
-    if (lane == 0) mw.rot_bin[q] = -1;
-    if (nc == 0) continue;
-    uint64_t key = (lane < kTopK) ? s_top[qc * kTopK + lane] : kNoKey;
-    bool ok = key != kNoKey && !((claimed[key_idx(key) >> 5] >> (key_idx(key) & 31)) & 1u);
-    uint64_t msk = __ballot(ok);
-    uint64_t b1 = kNoKey, b2 = kNoKey;
-    const int need = kF2F ? 1 : 2;
-    if (__popcll(msk) < need && nc > kTopK) {
-      // every kept candidate is already claimed: rescan with the live claims
-      ScanCtx c;
-      bool okc;
-      if constexpr (kF2F) okc = f2f_ctx(queries[q], poses[f], cam, g, &c);
-      else okc = mps_ctx(queries[q], th, g, &c);
-      uint64_t top[kTopK];
-      if (okc) scan_query(c, cam, F, claimed, top, lane);
-      b1 = okc ? top[0] : kNoKey;
-      b2 = okc ? top[1] : kNoKey;
+    uint64_t key[kTopK];
+    int nc = 0, mpw = 0;
+    float qang = 0.f;
+    if (valid) {
+#pragma unroll
+      for (int k = 0; k < kTopK; k++) key[k] = mw.topk[(int64_t)q * kTopK + k];
+      nc = mw.ncand[q];
+      const Q& qq = queries[q];
+      mpw = (qq.mp_id & 0x7fffffff) | (qq.blocks ? (int)0x80000000u : 0);
+      if constexpr (kF2F) qang = qq.last_angle;
+      mw.rot_bin[q] = -1;
     } else {
-      const int l1 = msk ? __ffsll((long long)msk) - 1 : -1;
-      const uint64_t msk2 = l1 >= 0 ? (msk & ~(1ull << l1)) : 0;
-      const int l2 = msk2 ? __ffsll((long long)msk2) - 1 : -1;
-      const uint64_t k1 = __shfl(key, l1 < 0 ? 0 : l1, 64);
-      const uint64_t k2 = __shfl(key, l2 < 0 ? 0 : l2, 64);
-      b1 = l1 >= 0 ? k1 : kNoKey;
-      b2 = l2 >= 0 ? k2 : kNoKey;
+#pragma unroll
+      for (int k = 0; k < kTopK; k++) key[k] = kNoKey;
     }
-    if (b1 == kNoKey) continue;
-    const int bestDist = key_dist(b1);
-    if (bestDist > TH_HIGH) continue;
-    const int idx = key_idx(b1);
-    if constexpr (!kF2F) {
-      const int bestLevel = s_koct[idx];
-      const int bestDist2 = b2 == kNoKey ? 256 : key_dist(b2);
-      const int bestLevel2 = b2 == kNoKey ? -1 : s_koct[key_idx(b2)];
-      if (bestLevel == bestLevel2 && (float)bestDist > nnratio * (float)bestDist2) continue;
-    }
-    const int mpw = s_mpid[qc];
     const bool qblocks = mpw < 0;
-    if (lane == 0) {
-      mp[idx] = mpw & 0x7fffffff;
-      blk[idx] = qblocks ? 1 : 0;
-      if (qblocks) claimed[idx >> 5] |= 1u << (idx & 31);
-    }
-    nm++;
-    if constexpr (kF2F) {
-      if (check_ori) {
-        float rot = s_qang[qc] - s_kang[idx];
-        if (rot < 0.0f) rot += 360.0f;
-        const float factor = 1.0f / HISTO_LENGTH;
-        int bin = (int)roundf(rot * factor);
-        if (bin == HISTO_LENGTH) bin = 0;
-        if (lane == 0) {
-          mw.rot_bin[q] = bin;
-          mw.best_idx[q] = idx;
-          hist[bin]++;
+    int start = 0;
+    while (start < 64 && c0 + start < qn) {
+      const bool act = valid && lane >= start && nc > 0;
+      // -- fixed point of the choices of lanes >= start
+      uint64_t b1 = kNoKey, b2 = kNoKey;
+      int navail = 0, mine = -1, prev = -2;
+      for (int it = 0; it < 64; it++) {
+        b1 = kNoKey;
+        b2 = kNoKey;
+        navail = 0;
+        if (act) {
+#pragma unroll
+          for (int k = 0; k < kTopK; k++) {
+            if (key[k] == kNoKey) continue;
+            const int idx = key_idx(key[k]);
+            if (is_claimed(idx) || owner[idx] < lane) continue;
+            if (navail == 0) b1 = key[k];
+            else if (navail == 1) b2 = key[k];
+            navail++;
+          }
         }
+        // accepted blocking choice -> owner (the lowest such lane wins the keypoint)
+        bool acc = b1 != kNoKey && key_dist(b1) <= TH_HIGH;
+        if constexpr (!kF2F) {
+          if (acc) {
+            const int lv1 = s_koct[key_idx(b1)];
+            const int d2 = b2 == kNoKey ? 256 : key_dist(b2);
+            const int lv2 = b2 == kNoKey ? -1 : s_koct[key_idx(b2)];
+            if (lv1 == lv2 && (float)key_dist(b1) > nnratio * (float)d2) acc = false;
+          }
+        }
+        mine = (act && acc && qblocks) ? key_idx(b1) : -1;
+        if (!__ballot(mine != prev)) break;
+        if (prev >= 0) owner[prev] = INT_MAX;
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        if (mine >= 0) atomicMin(&owner[mine], lane);
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        prev = mine;
       }
+      // -- the first lane that needs a rescan ends this round's committed range
+      const uint64_t rs = __ballot(act && navail < need && nc > kTopK);
+      const int r = rs ? __ffsll((long long)rs) - 1 : 64;
+      if (prev >= 0) owner[prev] = INT_MAX;  // committed claims move to claimed[]
+      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      auto commit = [&](bool doit, uint64_t c1, uint64_t c2) {
+        // acceptance (F2F: distance gate; local map: + ratio test, :76-99)
+        const bool touched = doit && c1 != kNoKey;
+        bool acc = touched && key_dist(c1) <= TH_HIGH;
+        if constexpr (!kF2F) {
+          if (acc) {
+            const int lv1 = s_koct[key_idx(c1)];
+            const int d2 = c2 == kNoKey ? 256 : key_dist(c2);
+            const int lv2 = c2 == kNoKey ? -1 : s_koct[key_idx(c2)];
+            if (lv1 == lv2 && (float)key_dist(c1) > nnratio * (float)d2) acc = false;
+          }
+        }
+        const int idx = touched ? key_idx(c1) : 0;
+        nm += __popcll(__ballot(acc));
+        // last writer (highest lane) of each keypoint sets mp / blocked
+        if (touched) owner[idx] = 0;
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        if (acc) atomicMax(&owner[idx], lane + 1);
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        if (acc && owner[idx] == lane + 1) {
+          mp[idx] = mpw & 0x7fffffff;
+          blk[idx] = qblocks ? 1 : 0;
+        }
+        if (acc && qblocks) atomicOr(&claimed[idx >> 5], 1u << (idx & 31));
+        if constexpr (kF2F) {
+          if (acc && check_ori) {
+            float rot = qang - s_kang[idx];
+            if (rot < 0.0f) rot += 360.0f;
+            const float factor = 1.0f / HISTO_LENGTH;
+            int bin = (int)roundf(rot * factor);
+            if (bin == HISTO_LENGTH) bin = 0;
+            mw.rot_bin[q] = bin;
+            mw.best_idx[q] = idx;
+            atomicAdd(&hist[bin], 1);
+          }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        if (touched) owner[idx] = INT_MAX;
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+      };
+      commit(act && lane < r, b1, b2);
+      if (r < 64 && c0 + r < qn) {
+        // lane r: every kept candidate is taken -> rescan its window with the live claims
+        ScanCtx c;
+        bool okc;
+        const int qr = q0 + c0 + r;
+        if constexpr (kF2F) okc = f2f_ctx(queries[qr], poses[f], cam, g, &c);
+        else okc = mps_ctx(queries[qr], th, g, &c);
+        uint64_t top[kTopK];
+        if (okc) scan_query(c, cam, F, claimed, top, lane);
+        const uint64_t t1 = __shfl(okc ? top[0] : kNoKey, 0, 64);
+        const uint64_t t2 = __shfl(okc ? top[1] : kNoKey, 0, 64);
+        commit(lane == r, t1, t2);
+      }
+      start = r + 1;
     }
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-  }
   }
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
   __builtin_amdgcn_wave_barrier();
