@@ -186,18 +186,33 @@ __global__ __launch_bounds__(256) void stereo_match_kernel(ImageBatch b,
   int pl, pr;
   const uint8_t* IL = level_img(b, g, il, levelL, &pl);
   const uint8_t* IR = level_img(b, g, ir, levelL, &pr);
-  int sad = 0x7fffffff;
-  if (lane < 2 * L + 1) {
-    const int incR = lane - L;
-    const int cl = IL[(int64_t)yc * pl + xcl];
-    const int cr = IR[(int64_t)yc * pr + xcr + incR];
-    int acc = 0;
-    for (int yy = -w; yy <= w; yy++) {
+  // SAD of the 11 window offsets: the 121 (offset, row) pairs are spread over the wave (two
+  // rounds), each lane summing one 11-pixel row; rows are then summed per offset through LDS.
+  __shared__ int s_part[4][128];
+  int* part = s_part[wave_id()];
+#pragma unroll
+  for (int rnd = 0; rnd < 2; rnd++) {
+    const int p = lane + 64 * rnd;
+    if (p < 121) {
+      const int k = p / 11, yy = p - 11 * k - w;
+      const int incR = k - L;
+      const int cl = IL[(int64_t)yc * pl + xcl];
+      const int cr = IR[(int64_t)yc * pr + xcr + incR];
       const uint8_t* rl = IL + (int64_t)(yc + yy) * pl + xcl - w;
       const uint8_t* rr = IR + (int64_t)(yc + yy) * pr + xcr + incR - w;
+      int acc = 0;
 #pragma unroll
       for (int xx = 0; xx < 2 * w + 1; xx++) acc += abs((rl[xx] - cl) - (rr[xx] - cr));
+      part[p] = acc;
     }
+  }
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  int sad = 0x7fffffff;
+  if (lane < 2 * L + 1) {
+    int acc = 0;
+#pragma unroll
+    for (int yy = 0; yy < 2 * w + 1; yy++) acc += part[11 * lane + yy];
     sad = acc;
   }
   float vDists[11];
