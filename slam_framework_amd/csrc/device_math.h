@@ -111,6 +111,7 @@ __device__ __forceinline__ float cv_fast_atan2(float y, float x) {
 }
 
 __device__ __forceinline__ int cv_round(float v) { return (int)rintf(v); }
+__device__ __forceinline__ int max3(int a, int b, int c) { return max(max(a, b), c); }
 
 // ---- wavefront (64-lane) helpers --------------------------------------------------------
 __device__ __forceinline__ int lane_id() { return __lane_id(); }

@@ -200,7 +200,7 @@ int compute_geometry(const OrbParams& p, int cols, int rows, OrbGeom* g,
   g->fast_tile_stride = round_up(max_wcell + 6 + 3, 4) + 4 <= 64 ? 64 : 128;
   g->fast_tile_rows = max_hcell + 6;
   g->fast_score_stride = g->fast_tile_stride;
-  g->fast_score_rows = max_hcell;
+  g->fast_score_rows = max_hcell + 2;  // detect rows + a zero row above and below
   g->fast_lds_per_wave = round_up(g->fast_tile_stride * g->fast_tile_rows, 16) +
                          round_up(g->fast_score_stride * g->fast_score_rows, 16) +
                          round_up(2 * max_wcell * max_hcell, 16);  // u16 candidate list

@@ -569,8 +569,14 @@ __global__ __launch_bounds__(256) void fast_cells_kernel(ImageBatch b,
     __builtin_amdgcn_wave_barrier();
     const int off = v.off;
     const int dh = v.vh - 6, dw = v.vw - 6;  // detect area [3, vh-3) x [3, vw-3)
+    // ---- score map: rows -1 .. dh of the detect area, all zero (a zero frame around the detect
+    // area lets the NMS read 3x3 neighbourhoods without bounds checks); sc1 = row 0.
+    uint8_t* sc1 = sc + kScoreStride;
+#pragma unroll 4
+    for (int rz = plr - 1; rz <= dh; rz += kRps)
+      *reinterpret_cast<uint32_t*>(sc1 + rz * kScoreStride + 4 * pld) = 0;
     // ---- prefilter every detect pixel at the lower threshold, 4 pixels (one tile dword) per
-    // lane; writes the score map's zeros and compacts survivors in row-major order.
+    // lane; compacts survivors in row-major order.
     // Detect pixel (rr, col): tile row rr + 3, tile column col in [off + 3, off + 3 + dw).
     const int q_lo = (off + 3) >> 2, q_hi = (off + 2 + dw) >> 2;
     const int nq = q_hi - q_lo + 1;
@@ -628,7 +634,6 @@ __global__ __launch_bounds__(256) void fast_cells_kernel(ImageBatch b,
         // non-zero u16 lane -> bit 7 of that pixel's byte
         m = ((((any[0] + 0x7fff7fffu) & 0x80008000u) >> 8) | ((any[1] + 0x7fff7fffu) & 0x80008000u)) &
             vmask;
-        *reinterpret_cast<uint32_t*>(sc + rr * kScoreStride + 4 * Q) = 0;
       }
       // row-major compaction: exclusive prefix of per-lane counts (0..4) via 3 ballots
       const int cnt = __popc(m);
@@ -647,14 +652,17 @@ __global__ __launch_bounds__(256) void fast_cells_kernel(ImageBatch b,
       const int pix = cand[i];
       const int r = pix / kScoreStride, cc = pix - r * kScoreStride;
       const int s = fast_s_pk<TS>(tile, (r + 3) * kTileStride + cc);
-      sc[pix] = (uint8_t)(s < 0 ? 0 : s);
+      sc1[pix] = (uint8_t)(s < 0 ? 0 : s);
     }
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     __builtin_amdgcn_wave_barrier();
     uint32_t* out = cell_keys + slot * g->cell_cap;
     // NMS at iniTh and at minTh in one sweep: the reference re-runs FAST at minTh when the iniTh
-    // *output* (after NMS) is empty (:753-757). Strict '>' against the 8 neighbours' scores at
-    // that threshold, zero outside the detect area; non-candidates have s <= tmin (score 0).
+    // *output* (after NMS) is empty (:753-757). cv::FAST keeps p at threshold t iff
+    // s - 1 > ns for all 8 neighbours, ns = (q > t ? q - 1 : 0), zero outside the detect area;
+    // non-candidates have s <= tmin (score 0). With Q = max of the 8 neighbours' s that is
+    //   s > t  &&  s >= 2  &&  Q < max(s, t + 1),
+    // so one 3x3 byte maximum (zero-framed map, no bounds checks) serves both thresholds.
     // iniTh survivors go straight out, minTh survivors are compacted in place in cand[].
     const int t0 = g->ini_th, t1 = g->min_th;
     int count0 = 0, count1 = 0;
@@ -666,24 +674,19 @@ __global__ __launch_bounds__(256) void fast_cells_kernel(ImageBatch b,
         pix = cand[i];
         r = pix / kScoreStride;
         cc = pix - r * kScoreStride;
-        s = sc[pix];
-        const int score = s - 1;
-        k0 = s > t0;
-        k1 = s > t1;
-        if (k0 || k1) {
-#pragma unroll
-          for (int dy = -1; dy <= 1; dy++)
-#pragma unroll
-            for (int dx = -1; dx <= 1; dx++) {
-              if (dx == 0 && dy == 0) continue;
-              const int rr = r + dy, c2 = cc + dx;
-              int q = 0;
-              if (rr >= 0 && rr < dh && c2 >= off + 3 && c2 < off + 3 + dw)
-                q = sc[rr * kScoreStride + c2];
-              k0 = k0 && score > (q > t0 ? q - 1 : 0);
-              k1 = k1 && score > (q > t1 ? q - 1 : 0);
-            }
-        }
+        const uint8_t* nb = sc1 + pix - kScoreStride - 1;  // (r - 1, cc - 1)
+        const int al = (int)((uintptr_t)nb & 3);
+        const uint32_t* nw = reinterpret_cast<const uint32_t*>(nb - al);
+        constexpr int kW = kScoreStride / 4;
+        const uint32_t rA = __builtin_amdgcn_alignbyte(nw[1], nw[0], al);
+        const uint32_t rB = __builtin_amdgcn_alignbyte(nw[kW + 1], nw[kW], al);
+        const uint32_t rC = __builtin_amdgcn_alignbyte(nw[2 * kW + 1], nw[2 * kW], al);
+        s = (rB >> 8) & 255;
+        const int q = max(max(max3((int)(rA & 255), (int)((rA >> 8) & 255), (int)((rA >> 16) & 255)),
+                              max((int)(rB & 255), (int)((rB >> 16) & 255))),
+                          max3((int)(rC & 255), (int)((rC >> 8) & 255), (int)((rC >> 16) & 255)));
+        k0 = s > t0 && s >= 2 && q < max(s, t0 + 1);
+        k1 = s > t1 && s >= 2 && q < max(s, t1 + 1);
       }
       const uint64_t m0 = __ballot(k0), m1 = __ballot(k1);
       if (k0) {
@@ -701,7 +704,7 @@ __global__ __launch_bounds__(256) void fast_cells_kernel(ImageBatch b,
       for (int i = lane; i < min(count1, g->cell_cap); i += 64) {
         const int pix = cand[i];
         const int r = pix / kScoreStride, cc = pix - r * kScoreStride;
-        out[i] = pack_key(v.ax + cc - kMinBorder, v.ini_y + 3 + r - kMinBorder, sc[pix] - 1);
+        out[i] = pack_key(v.ax + cc - kMinBorder, v.ini_y + 3 + r - kMinBorder, sc1[pix] - 1);
       }
       count = count1;
     }
