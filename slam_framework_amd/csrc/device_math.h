@@ -112,6 +112,10 @@ __device__ __forceinline__ float cv_fast_atan2(float y, float x) {
 
 __device__ __forceinline__ int cv_round(float v) { return (int)rintf(v); }
 __device__ __forceinline__ int max3(int a, int b, int c) { return max(max(a, b), c); }
+// high 32 bits of a 24 x 24-bit product (v_mul_hi_u32_u24); a, b < 2^24
+__device__ __forceinline__ uint32_t mulhi24(uint32_t a, uint32_t b) {
+  return (uint32_t)(((uint64_t)(a & 0xffffffu) * (uint64_t)(b & 0xffffffu)) >> 32);
+}
 
 // ---- wavefront (64-lane) helpers --------------------------------------------------------
 __device__ __forceinline__ int lane_id() { return __lane_id(); }

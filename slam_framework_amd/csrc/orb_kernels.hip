@@ -86,7 +86,8 @@ __global__ __launch_bounds__(256) void pyr_down_kernel(ImageBatch b, const OrbGe
     if (k == 0) s0 = e.sx;
     const uint32_t bk = (uint32_t)min(e.sx - s0, 6);
     sel[k] = bk | 0x0c00u | (bk + 1) << 16 | 0x0c000000u;  // bytes bk, bk+1 -> u16 lanes
-    A[k] = dx < D.xmax ? ((uint32_t)(uint16_t)e.a0 | (uint32_t)(uint16_t)e.a1 << 16) : 2048u;
+    // coefficients x16 (<= 32768): the dot product yields 16 * r, see the vertical pass
+    A[k] = dx < D.xmax ? ((uint32_t)(16 * e.a0) | (uint32_t)(16 * e.a1) << 16) : 32768u;
   }
   const int q0 = s0 >> 2, sh = s0 & 3, qmax = (S.w - 1) >> 2;
   int spitch;
@@ -94,11 +95,12 @@ __global__ __launch_bounds__(256) void pyr_down_kernel(ImageBatch b, const OrbGe
   const bool aligned = (((uintptr_t)src | (uintptr_t)spitch) & 3) == 0;
   const int qa = min(q0, qmax), qb = min(q0 + 1, qmax), qc = min(q0 + 2, qmax);
   auto fetch = [&](int sy, uint32_t (&wv)[3]) {
-    const uint8_t* row = src + (int64_t)min(sy, sy_hi) * spitch;
+    const uint8_t* row = src + (int64_t)min(sy, sy_hi) * spitch;  // wave-uniform
     if (aligned) {  // clamped dwords stay inside the row; bytes past sx+1 carry zero weight
-      wv[0] = *reinterpret_cast<const uint32_t*>(row + 4 * qa);
-      wv[1] = *reinterpret_cast<const uint32_t*>(row + 4 * qb);
-      wv[2] = *reinterpret_cast<const uint32_t*>(row + 4 * qc);
+      const uint32_t* rw = reinterpret_cast<const uint32_t*>(row);
+      wv[0] = rw[(uint32_t)qa];
+      wv[1] = rw[(uint32_t)qb];
+      wv[2] = rw[(uint32_t)qc];
     } else {
 #pragma unroll
       for (int i = 0; i < 3; i++) {
@@ -135,12 +137,14 @@ __global__ __launch_bounds__(256) void pyr_down_kernel(ImageBatch b, const OrbGe
         while (nd < nrows && __builtin_amdgcn_readlane(ry_y1, nd) == sy) {
           const bool same = __builtin_amdgcn_readlane(ry_y0, nd) == sy;
           const uint32_t bb = (uint32_t)__builtin_amdgcn_readlane(ry_b, nd);
-          const uint32_t b0 = bb & 0xffffu, b1 = bb >> 16;
+          // (b * (r >> 4)) >> 16 == mulhi24(b << 8, (r >> 4) << 8), and (r >> 4) << 8 is
+          // (16 r) & ~0xff with 16 r from the scaled dot product (all operands < 2^24)
+          const uint32_t b0 = (bb & 0xffffu) << 8, b1 = (bb >> 16) << 8;
           uint32_t packed = 0;
 #pragma unroll
           for (int k = 0; k < 4; k++) {
-            const uint32_t r0 = (same ? hc[k] : hp[k]) >> 4, r1 = hc[k] >> 4;
-            const uint32_t v = (((b0 * r0) >> 16) + ((b1 * r1) >> 16) + 2) >> 2;
+            const uint32_t r0 = (same ? hc[k] : hp[k]) & ~0xffu, r1 = hc[k] & ~0xffu;
+            const uint32_t v = (mulhi24(b0, r0) + mulhi24(b1, r1) + 2) >> 2;
             packed |= (v & 0xffu) << (8 * k);
           }
           uint8_t* drow = dst + (int64_t)(dy0 + nd) * D.pitch;
