@@ -7,6 +7,7 @@
  *
  * What it restates (every function cites the reference file:line it follows, paths relative
  * to the reference repository root):
+ *   - Optimizer::PoseOptimization (src/optimizer/optimizer.cpp:209-411, on g2o): pose_oracle.c
  *   - ORBextractor (src/orb_features/orb_extractor.cpp): ctor tables, ComputePyramid,
  *     ComputeKeyPointsOctTree (cell FAST + threshold fallback), DistributeOctTree,
  *     IC_Angle / computeOrientation, GaussianBlur + computeOrbDescriptor, Compute.
@@ -156,7 +157,25 @@ int oc_search_by_projection_mps(const oc_grid_geom* g, const oc_orb_tables* t,
                                 const uint8_t* mp_desc, const int* mp_nobs, float nnratio,
                                 int th);
 
+/* ---- Optimizer::PoseOptimization (pose_oracle.c) --------------------------------------------- */
+typedef struct {
+  float xw[3];    /* map point world position (MapPoint::GetWorldPos, f32)            */
+  float u, v;     /* undistorted keypoint                                             */
+  float ur;       /* right coordinate (Frame::StereoCoordRight); < 0 -> monocular edge */
+  int32_t octave; /* keypoint octave -> information = InvLevelSigma2[octave] * I      */
+} oc_pose_edge;
+
+/* Optimizer::PoseOptimization (optimizer.cpp:209-411). cam = fx, fy, cx, cy, bf (Frame's f32);
+ * Tcw 4x4 row-major f32 in/out; outlier[n] out; returns #initial - #bad (0 if < 3 edges).
+ * *lm_iterations (optional) counts g2o LM iterations over the 4 rounds. */
+int oc_pose_optimization(const float cam[5], const float* inv_sigma2, const oc_pose_edge* edges,
+                         int n, float Tcw[16], uint8_t* outlier, int* lm_iterations);
+void oc_se3_exp(const double u[6], double R[9], double t[3]);
+double oc_pose_edge_eval(const float cam[5], const double R[9], const double t[3],
+                         const oc_pose_edge* e, float inv_sigma2, double err[3], double J[18]);
+
 #ifdef __cplusplus
 }
 #endif
+
 #endif /* SLAMGPU_ORB_ORACLE_H_ */

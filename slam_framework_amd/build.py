@@ -30,7 +30,7 @@ def _stale() -> bool:
         return True
     t = os.path.getmtime(LIB)
     deps = sources() + glob.glob(os.path.join(CSRC, "*.h")) + glob.glob(os.path.join(CSRC, "*.inc"))
-    deps.append(os.path.join(os.path.dirname(PKG), "include", "slamgpu.h"))
+    deps += glob.glob(os.path.join(os.path.dirname(PKG), "include", "*.h"))
     return any(os.path.getmtime(d) > t for d in deps)
 
 

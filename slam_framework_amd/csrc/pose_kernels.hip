@@ -1,0 +1,585 @@
+// pose_kernels.hip -- Optimizer::PoseOptimization (optimizer.cpp:209-411) on the device.
+//
+// One workgroup per frame runs the reference's whole schedule: 4 rounds of g2o's
+// Levenberg-Marquardt (10 iterations each), outlier classification between rounds, robust kernel
+// dropped after round 2. Nothing goes back to the host between iterations. Batches run one wave
+// per frame (many frames resident per CU, no barriers); a handful of frames -- the per-frame
+// tracking call -- runs 8 waves per frame to cut latency.
+//
+// Work split. Edge k of a frame is slot k / (64 W) of thread k % (64 W). Per slot the thread
+// keeps two bits in registers: outlier (level 1, inactive), and whether the edge's last computed
+// chi2 exceeds the f32 threshold. g2o keeps the last error per edge, stale after a rejected LM
+// step (sparse_optimizer.cpp:61-88), and its classification only compares that chi2 with the
+// threshold, so the bit is all the state it needs. Edge inputs (28 B) are re-read from L2 every
+// pass; a 2000-edge frame is 56 KB.
+//
+// Per LM iteration there are 1 + #trials passes over the edges:
+//   linearise pass : error, chi2, Huber weight, 2x6/3x6 Jacobian, and the 21 + 6 + 1 sums of
+//                    H (upper triangle), b and the robust chi2 in one sweep (computeActiveErrors,
+//                    activeRobustChi2 and buildSystem all evaluate at the same estimate);
+//   trial pass     : error, chi2 and robust chi2 at exp(dx) * T.
+// The sums are reductions (reduce-scatter across the wave, wave partials through LDS), after
+// which every lane of every wave holds bitwise-identical totals and runs the LM control (6x6
+// LDLT, exp, lambda update) itself with uniform branches: no broadcast, no single-lane section.
+//
+// FP64 throughout, with the reference's f32 quirks: f32 inputs and outputs (Converter), float
+// inverse depth in the stereo projection (types_six_dof_expmap.cpp:299-306), f32 Huber deltas and
+// chi2 thresholds (optimizer.cpp:253-254, :352-401).
+#include <hip/hip_runtime.h>
+
+#include <cfloat>
+#include <cmath>
+
+#include "device_math.h"
+#include "pose_kernels.h"
+
+namespace slamgpu {
+namespace {
+
+constexpr int kNH = 21;  // upper triangle of the 6x6 H
+// Batches smaller than this run 8 waves per frame (latency); larger ones one wave per frame.
+constexpr int kPoseLatencyFrames = 64;
+
+struct Quat {
+  double x, y, z, w;
+};
+struct SE3 {
+  Quat r;
+  double t[3];
+};
+
+// Eigen Quaternion(const Matrix3&): Shepperd's method on the largest diagonal term.
+__device__ Quat quat_from_R(const double R[9]) {
+  Quat q;
+  const double tr = R[0] + R[4] + R[8];
+  if (tr > 0.0) {
+    double t = sqrt(tr + 1.0);
+    q.w = 0.5 * t;
+    t = 0.5 / t;
+    q.x = (R[7] - R[5]) * t;
+    q.y = (R[2] - R[6]) * t;
+    q.z = (R[3] - R[1]) * t;
+  } else if (R[4] <= R[0] && R[8] <= R[0]) {  // i = 0
+    double t = sqrt(R[0] - R[4] - R[8] + 1.0);
+    q.x = 0.5 * t;
+    t = 0.5 / t;
+    q.w = (R[7] - R[5]) * t;
+    q.y = (R[3] + R[1]) * t;
+    q.z = (R[6] + R[2]) * t;
+  } else if (R[8] <= (R[4] > R[0] ? R[4] : R[0]) && R[4] > R[0]) {  // i = 1
+    double t = sqrt(R[4] - R[8] - R[0] + 1.0);
+    q.y = 0.5 * t;
+    t = 0.5 / t;
+    q.w = (R[2] - R[6]) * t;
+    q.z = (R[7] + R[5]) * t;
+    q.x = (R[1] + R[3]) * t;
+  } else {  // i = 2
+    double t = sqrt(R[8] - R[0] - R[4] + 1.0);
+    q.z = 0.5 * t;
+    t = 0.5 / t;
+    q.w = (R[3] - R[1]) * t;
+    q.x = (R[2] + R[6]) * t;
+    q.y = (R[5] + R[7]) * t;
+  }
+  return q;
+}
+
+// SE3Quat::normalizeRotation (se3quat.h:280-285): w >= 0, unit norm.
+__device__ void normalize_rotation(Quat& q) {
+  if (q.w < 0) {
+    q.x = -q.x;
+    q.y = -q.y;
+    q.z = -q.z;
+    q.w = -q.w;
+  }
+  const double n = sqrt(q.x * q.x + q.y * q.y + q.z * q.z + q.w * q.w);
+  q.x /= n;
+  q.y /= n;
+  q.z /= n;
+  q.w /= n;
+}
+
+// q * v as Eigen evaluates it: v + 2w(q_v x v) + q_v x (2 q_v x v).
+__device__ __forceinline__ void quat_rotate(const Quat& q, const double v[3], double o[3]) {
+  double a = q.y * v[2] - q.z * v[1], b = q.z * v[0] - q.x * v[2], c = q.x * v[1] - q.y * v[0];
+  a += a;
+  b += b;
+  c += c;
+  o[0] = v[0] + q.w * a + (q.y * c - q.z * b);
+  o[1] = v[1] + q.w * b + (q.z * a - q.x * c);
+  o[2] = v[2] + q.w * c + (q.x * b - q.y * a);
+}
+
+__device__ void quat_to_R(const Quat& q, double R[9]) {  // Eigen toRotationMatrix
+  const double tx = 2 * q.x, ty = 2 * q.y, tz = 2 * q.z;
+  const double twx = tx * q.w, twy = ty * q.w, twz = tz * q.w;
+  const double txx = tx * q.x, txy = ty * q.x, txz = tz * q.x;
+  const double tyy = ty * q.y, tyz = tz * q.y, tzz = tz * q.z;
+  R[0] = 1 - (tyy + tzz);
+  R[1] = txy - twz;
+  R[2] = txz + twy;
+  R[3] = txy + twz;
+  R[4] = 1 - (txx + tzz);
+  R[5] = tyz - twx;
+  R[6] = txz - twy;
+  R[7] = tyz + twx;
+  R[8] = 1 - (txx + tyy);
+}
+
+// exp(dx) * T, VertexSE3Expmap::oplusImpl (types_six_dof_expmap.h:73-76) with SE3Quat::exp
+// (se3quat.h:223-257) and operator* (:92-99). dx = [omega, upsilon].
+__device__ SE3 se3_left_update(const double u[6], const SE3& T) {
+  const double w0 = u[0], w1 = u[1], w2 = u[2];
+  const double th = sqrt(w0 * w0 + w1 * w1 + w2 * w2);
+  const double O[9] = {0, -w2, w1, w2, 0, -w0, -w1, w0, 0};
+  double O2[9];
+  for (int i = 0; i < 3; i++)
+    for (int j = 0; j < 3; j++)
+      O2[3 * i + j] = O[3 * i] * O[j] + O[3 * i + 1] * O[3 + j] + O[3 * i + 2] * O[6 + j];
+  double a = 1.0, b = 1.0, c = 1.0;  // small-angle branch: R = V = I + O + O^2
+  if (!(th < 0.00001)) {
+    double s, co;
+    sincos(th, &s, &co);
+    a = s / th;
+    b = (1 - co) / (th * th);
+    c = (th - s) / (th * th * th);
+  }
+  double R[9], V[9];
+  for (int i = 0; i < 9; i++) {
+    const double I = (i % 4 == 0) ? 1.0 : 0.0;
+    R[i] = I + a * O[i] + b * O2[i];
+    V[i] = I + b * O[i] + c * O2[i];
+  }
+  SE3 E;
+  for (int i = 0; i < 3; i++) E.t[i] = V[3 * i] * u[3] + V[3 * i + 1] * u[4] + V[3 * i + 2] * u[5];
+  E.r = quat_from_R(R);
+  normalize_rotation(E.r);
+  SE3 out;  // E * T
+  double rt[3];
+  quat_rotate(E.r, T.t, rt);
+  for (int i = 0; i < 3; i++) out.t[i] = E.t[i] + rt[i];
+  const Quat& p = E.r;
+  const Quat& q = T.r;
+  out.r.w = p.w * q.w - p.x * q.x - p.y * q.y - p.z * q.z;
+  out.r.x = p.w * q.x + p.x * q.w + p.y * q.z - p.z * q.y;
+  out.r.y = p.w * q.y + p.y * q.w + p.z * q.x - p.x * q.z;
+  out.r.z = p.w * q.z + p.z * q.w + p.x * q.y - p.y * q.x;
+  normalize_rotation(out.r);
+  return out;
+}
+
+// H x = b for the 6x6 H + lambda I, LDLT without pivoting; a zero pivot gives a zero component
+// (Eigen's rule), a negative one fails the solve (LinearSolverDense::solve returns false and
+// g2o applies the previous x).
+__device__ bool ldlt_solve6(const double H[kNH], double lambda, const double b[6], double x[6]) {
+  double L[6][6], d[6];
+#pragma unroll
+  for (int j = 0; j < 6; j++) {
+    double dj = H[j * 6 - (j * (j - 1)) / 2] + lambda;  // H(j, j) in the packed upper triangle
+#pragma unroll
+    for (int k = 0; k < j; k++) dj -= L[j][k] * L[j][k] * d[k];
+    d[j] = dj;
+    if (dj < 0) return false;
+#pragma unroll
+    for (int i = j + 1; i < 6; i++) {
+      double s = H[j * 6 - (j * (j - 1)) / 2 + (i - j)];  // H(j, i) = H(i, j)
+#pragma unroll
+      for (int k = 0; k < j; k++) s -= L[i][k] * L[j][k] * d[k];
+      L[i][j] = dj > DBL_MIN ? s / dj : 0.0;
+    }
+  }
+  double y[6];
+#pragma unroll
+  for (int i = 0; i < 6; i++) {
+    double s = b[i];
+#pragma unroll
+    for (int k = 0; k < i; k++) s -= L[i][k] * y[k];
+    y[i] = s;
+  }
+#pragma unroll
+  for (int i = 0; i < 6; i++) y[i] = fabs(d[i]) > DBL_MIN ? y[i] / d[i] : 0.0;
+#pragma unroll
+  for (int i = 5; i >= 0; i--) {
+    double s = y[i];
+#pragma unroll
+    for (int k = i + 1; k < 6; k++) s -= L[k][i] * x[k];
+    x[i] = s;
+  }
+  return true;
+}
+
+// RobustKernelHuber::robustify (robust_kernel_impl.cpp:78-91): rho(e) and rho'(e). The sqrt and
+// division run only for lanes past the kernel's corner (a skipped branch for inlier waves).
+__device__ __forceinline__ double huber_rho0(double e, double delta) {
+  double r = e;
+  const double d2 = delta * delta;
+  if (e > d2) r = 2 * sqrt(e) * delta - d2;
+  return r;
+}
+__device__ __forceinline__ void huber_rho01(double e, double delta, double& r0, double& r1) {
+  r0 = e;
+  r1 = 1.0;
+  const double d2 = delta * delta;
+  if (e > d2) {
+    const double s = sqrt(e);
+    r0 = 2 * s * delta - d2;
+    r1 = delta / s;
+  }
+}
+
+// The estimate as the passes use it: Eigen maps points with the quaternion (q * v + t); the
+// passes use the equal rotation matrix (one 3x3 product per edge instead of two cross products).
+struct PassPose {
+  double R[9], t[3];
+};
+__device__ __forceinline__ PassPose pass_pose(const SE3& T) {
+  PassPose p;
+  quat_to_R(T.r, p.R);
+  p.t[0] = T.t[0];
+  p.t[1] = T.t[1];
+  p.t[2] = T.t[2];
+  return p;
+}
+
+struct EdgeEval {
+  double e[3];
+  double x, y, iz;  // camera coordinates, 1 / z
+  bool stereo;
+  double info;
+};
+
+// error = obs - cam_project(T.map(Xw)); returns chi2 = e' (info I) e. FMA contraction is allowed
+// here: the pose path is compared with a tolerance, not bit for bit.
+__device__ __forceinline__ double eval_edge(const slamgpu_pose_edge& E, const PoseParams& P,
+                                            const float* isig, const PassPose& T, EdgeEval& v) {
+#pragma clang fp contract(fast)
+  const double X0 = E.xw[0], X1 = E.xw[1], X2 = E.xw[2];
+  v.x = T.R[0] * X0 + T.R[1] * X1 + T.R[2] * X2 + T.t[0];
+  v.y = T.R[3] * X0 + T.R[4] * X1 + T.R[5] * X2 + T.t[1];
+  const double z = T.R[6] * X0 + T.R[7] * X1 + T.R[8] * X2 + T.t[2];
+  v.iz = 1.0 / z;
+  v.stereo = E.ur >= 0;
+  int oct = E.octave;
+  oct = oct < 0 ? 0 : (oct >= P.nlevels ? P.nlevels - 1 : oct);
+  v.info = (double)isig[oct];
+  // mono (EdgeSE3ProjectXYZOnlyPose, project2d): x / z, as x * (1/z) plus one residual step
+  // (the correctly rounded quotient but for rare ties); stereo (EdgeStereoSE3ProjectXYZOnlyPose):
+  // x * invz with `const float invz = 1.0f / z`
+  const double izf = (double)(float)v.iz;
+  double px = v.x * v.iz, py = v.y * v.iz;
+  px = __builtin_fma(__builtin_fma(-px, z, v.x), v.iz, px);
+  py = __builtin_fma(__builtin_fma(-py, z, v.y), v.iz, py);
+  if (v.stereo) {
+    px = v.x * izf;
+    py = v.y * izf;
+  }
+  const double u = px * (double)P.fx + (double)P.cx;
+  const double vv = py * (double)P.fy + (double)P.cy;
+  v.e[0] = (double)E.u - u;
+  v.e[1] = (double)E.v - vv;
+  v.e[2] = v.stereo ? (double)E.ur - (u - (double)P.bf * izf) : 0.0;
+  return v.info * (v.e[0] * v.e[0] + v.e[1] * v.e[1] + v.e[2] * v.e[2]);
+}
+
+// ---- reductions -------------------------------------------------------------------------------
+// Sum 32 per-lane doubles over the wave: after 5 halving exchanges lane l holds the sum of value
+// l >> 1 over 32 lanes; the last exchange (xor 1) completes it over all 64.
+__device__ __forceinline__ double wave_reduce_scatter32(double v[32]) {
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int h = 16, m = 32; h >= 1; h >>= 1, m >>= 1) {
+    // The upper lane of each pair keeps the upper half. Both candidates are read first and the
+    // choice is made on the values (v_cndmask), never on their addresses (which would move v
+    // to scratch).
+    const uint64_t up = (lane & m) ? ~0ull : 0ull;
+#pragma unroll
+    for (int i = 0; i < h; i++) {
+      const uint64_t lo = __builtin_bit_cast(uint64_t, v[i]);
+      const uint64_t hi = __builtin_bit_cast(uint64_t, v[i + h]);
+      const double send = __builtin_bit_cast(double, (lo & up) | (hi & ~up));
+      const double keep = __builtin_bit_cast(double, (hi & up) | (lo & ~up));
+      v[i] = keep + __shfl_xor(send, m);
+    }
+  }
+  return v[0] + __shfl_xor(v[0], 1);
+}
+
+// xor butterfly: every lane ends with the same bits (each level adds a + b on one side and b + a
+// on the other, and IEEE addition commutes).
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) v += __shfl_xor(v, m);
+  return v;
+}
+
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// Sums over the W waves of one frame's workgroup. Every wave ends with the same totals (its own
+// copy, summed in the same order), so the LM control that reads them stays uniform.
+template <int W>
+struct FrameSum {
+  double red[2][W][32];  // wave partials, double-buffered: a buffer is rewritten two sums later,
+  double tot[W][32];     // after a barrier every reader has passed
+  int rb;
+
+  // 32 sums (H, b, chi2) -> tot[wave][0..31]
+  __device__ __forceinline__ const double* sum32(double v[32]) {
+    const int lane = threadIdx.x & 63, w = wave_id();
+    const double s = wave_reduce_scatter32(v);
+    if (W == 1) {
+      if ((lane & 1) == 0) tot[0][lane >> 1] = s;
+    } else {
+      if ((lane & 1) == 0) red[rb][w][lane >> 1] = s;
+      __syncthreads();
+      if (lane < 32) {
+        double t = 0.0;
+#pragma unroll
+        for (int k = 0; k < W; k++) t += red[rb][k][lane];
+        tot[w][lane] = t;
+      }
+      rb ^= 1;
+    }
+    wave_lds_sync();
+    return tot[w];
+  }
+
+  __device__ __forceinline__ double sum1(double v) {
+    v = wave_sum(v);
+    if (W == 1) return v;
+    const int lane = threadIdx.x & 63, w = wave_id();
+    if (lane == 0) red[rb][w][0] = v;
+    __syncthreads();
+    double t = 0.0;
+#pragma unroll
+    for (int k = 0; k < W; k++) t += red[rb][k][0];
+    rb ^= 1;
+    return t;
+  }
+};
+
+// Optimizer::PoseOptimization for frame blockIdx.x with W waves. Edge k is slot k / (64 W) of
+// thread k % (64 W); per slot a thread keeps two bits: the edge is an outlier (level 1,
+// inactive), and the f32 test chi2 > threshold of the edge's last computed chi2 -- the only use
+// g2o's classification makes of the stored (possibly stale) error.
+template <int W>
+__global__ __launch_bounds__(64 * W) void pose_opt_kernel(
+    const slamgpu_pose_edge* __restrict__ edges, const int32_t* __restrict__ edge_start,
+    PoseParams P, float* __restrict__ Tcw, uint8_t* __restrict__ outlier_out,
+    int32_t* __restrict__ n_inliers, int32_t* __restrict__ lm_iterations) {
+#pragma clang fp contract(fast)  // tolerance-compared FP64 path: let the edge sums fuse
+  constexpr int kThreads = 64 * W;
+  constexpr int kEpt = SLAMGPU_POSE_MAX_EDGES / kThreads;
+  static_assert(kEpt <= 64, "slot masks are 64-bit");
+  __shared__ FrameSum<W> fs;
+  __shared__ float isig[SLAMGPU_MAX_LEVELS];  // Frame::mvInvLevelSigma2
+  const int f = blockIdx.x, tid = threadIdx.x;
+  const int e0 = edge_start[f];
+  const int n = edge_start[f + 1] - e0;
+  const slamgpu_pose_edge* E = edges + e0;
+  uint8_t* outl_out = outlier_out + e0;
+  if (n > SLAMGPU_POSE_MAX_EDGES || n < 0) {
+    if (tid == 0) {
+      n_inliers[f] = -1;
+      if (lm_iterations) lm_iterations[f] = 0;
+    }
+    return;
+  }
+  if (n < 3) {  // optimizer.cpp:312-314 (edges exist, their outlier flags were cleared)
+    for (int k = tid; k < n; k += kThreads) outl_out[k] = 0;
+    if (tid == 0) {
+      n_inliers[f] = 0;
+      if (lm_iterations) lm_iterations[f] = 0;
+    }
+    return;
+  }
+  float* Tf = Tcw + 16 * f;
+  if (tid < SLAMGPU_MAX_LEVELS) isig[tid] = P.inv_sigma2[tid];
+  fs.rb = 0;
+  __syncthreads();
+  const double delta_mono = (double)(float)sqrt(5.991), delta_stereo = (double)(float)sqrt(7.815);
+  const int nslots = tid < n ? (n - tid + kThreads - 1) / kThreads : 0;
+
+  uint64_t outl = 0, lastbad = 0;
+  int lm_total = 0, is_bad = 0;
+  bool robust = true;
+  SE3 T;
+
+  for (int round = 0; round < 4; round++) {
+    // optimizer.cpp:344 -- every round restarts from the frame's pose (Converter::toSE3Quat).
+    // Re-derived from the f32 input each round rather than kept live.
+    {
+      double R[9];
+      for (int i = 0; i < 3; i++) {
+        for (int j = 0; j < 3; j++) R[3 * i + j] = Tf[4 * i + j];
+        T.t[i] = Tf[4 * i + 3];
+      }
+      T.r = quat_from_R(R);
+      normalize_rotation(T.r);
+    }
+    double lambda = 0.0;
+    int ni = 2, nbad = 0;
+    for (int it = 0; it < 10; it++) {
+      // ---- linearise: computeActiveErrors + activeRobustChi2 + buildSystem at T ----
+      double acc[32];
+#pragma unroll
+      for (int i = 0; i < 32; i++) acc[i] = 0.0;
+      const PassPose TP = pass_pose(T);
+      for (int j = 0; j < nslots; j++) {
+        if ((outl >> j) & 1) continue;
+        const int k = tid + j * kThreads;
+        EdgeEval ev;
+        const double c2 = eval_edge(E[k], P, isig, TP, ev);
+        const uint64_t bit = 1ull << j;
+        lastbad = ((float)c2 > (ev.stereo ? 7.815f : 5.991f)) ? (lastbad | bit) : (lastbad & ~bit);
+        const double delta = ev.stereo ? delta_stereo : delta_mono;
+        double wgt = 1.0, r0 = c2;
+        if (robust) huber_rho01(c2, delta, r0, wgt);
+        acc[27] += r0;
+        // Jacobian of the error wrt [omega, upsilon] (types_six_dof_expmap.cpp:266-288, 311-364)
+        const double iz = ev.iz, iz2 = iz * iz, x = ev.x, y = ev.y;
+        const double fx = P.fx, fy = P.fy, bf = P.bf;
+        double J[3][6];
+        J[0][0] = x * y * iz2 * fx;
+        J[0][1] = -(1 + (x * x * iz2)) * fx;
+        J[0][2] = y * iz * fx;
+        J[0][3] = -iz * fx;
+        J[0][4] = 0;
+        J[0][5] = x * iz2 * fx;
+        J[1][0] = (1 + y * y * iz2) * fy;
+        J[1][1] = -x * y * iz2 * fy;
+        J[1][2] = -x * iz * fy;
+        J[1][3] = 0;
+        J[1][4] = -iz * fy;
+        J[1][5] = y * iz2 * fy;
+        const double sm = ev.stereo ? 1.0 : 0.0;  // the third row only for stereo edges
+        J[2][0] = sm * (J[0][0] - bf * y * iz2);
+        J[2][1] = sm * (J[0][1] + bf * x * iz2);
+        J[2][2] = sm * J[0][2];
+        J[2][3] = sm * J[0][3];
+        J[2][4] = 0;
+        J[2][5] = sm * (J[0][5] - bf * iz2);
+        // b -= rho' J' Omega e ; H += J' (rho' Omega) J  (base_unary_edge.hpp:43-71)
+        const double wi = wgt * ev.info;
+        int h = 0;
+#pragma unroll
+        for (int a = 0; a < 6; a++) {
+          const double ja0 = J[0][a] * ev.info, ja1 = J[1][a] * ev.info, ja2 = J[2][a] * ev.info;
+          acc[kNH + a] -= wgt * (ja0 * ev.e[0] + ja1 * ev.e[1] + ja2 * ev.e[2]);
+          const double wa0 = J[0][a] * wi, wa1 = J[1][a] * wi, wa2 = J[2][a] * wi;
+#pragma unroll
+          for (int c = a; c < 6; c++, h++) acc[h] += wa0 * J[0][c] + wa1 * J[1][c] + wa2 * J[2][c];
+        }
+      }
+      const double* S = fs.sum32(acc);
+      const double* H = S;
+      const double* b = S + kNH;
+      double currentChi = S[27];
+      const double iniChi = currentChi;
+      if (it == 0) {  // computeLambdaInit: tau * max |H_jj|, tau = 1e-5
+        double maxd = 0.0;
+#pragma unroll
+        for (int j = 0; j < 6; j++) maxd = fmax(fabs(H[j * 6 - (j * (j - 1)) / 2]), maxd);
+        lambda = 1e-5 * maxd;
+        ni = 2;
+        nbad = 0;
+      }
+      double rho = 0.0, x[6] = {0, 0, 0, 0, 0, 0};
+      int qmax = 0;
+      do {
+        const SE3 backup = T;
+        const bool ok = ldlt_solve6(H, lambda, b, x);
+        T = se3_left_update(x, backup);
+        // ---- trial: computeActiveErrors + activeRobustChi2 at the new estimate ----
+        double part = 0.0;
+        const PassPose TP = pass_pose(T);
+        for (int j = 0; j < nslots; j++) {
+          if ((outl >> j) & 1) continue;
+          EdgeEval ev;
+          const double c2 = eval_edge(E[tid + j * kThreads], P, isig, TP, ev);
+          const uint64_t bit = 1ull << j;
+          lastbad = ((float)c2 > (ev.stereo ? 7.815f : 5.991f)) ? (lastbad | bit) : (lastbad & ~bit);
+          part += robust ? huber_rho0(c2, ev.stereo ? delta_stereo : delta_mono) : c2;
+        }
+        double tempChi = fs.sum1(part);
+        if (!ok) tempChi = DBL_MAX;
+        double scale = 0.0;
+#pragma unroll
+        for (int j = 0; j < 6; j++) scale += x[j] * (lambda * x[j] + b[j]);
+        scale += 1e-3;
+        rho = (currentChi - tempChi) / scale;
+        if (rho > 0 && isfinite(tempChi)) {
+          double alpha = 1. - pow(2 * rho - 1, 3.0);
+          alpha = fmin(alpha, 2. / 3.);
+          lambda *= fmax(1. / 3., alpha);
+          ni = 2;
+          currentChi = tempChi;
+        } else {
+          lambda *= ni;
+          ni *= 2;
+          T = backup;  // pop: the edges keep the errors of the rejected estimate
+        }
+        qmax++;
+      } while (rho < 0 && qmax < 10);
+      lm_total++;
+      if (qmax == 10 || rho == 0) break;
+      if ((iniChi - currentChi) * 1e3 < iniChi) nbad++;
+      else nbad = 0;
+      if (nbad >= 3) break;
+    }
+    // ---- classify (optimizer.cpp:352-401): inactive edges get their error at the final T ----
+    double bad = 0.0;
+    const PassPose TP = pass_pose(T);
+    for (int j = 0; j < nslots; j++) {
+      const uint64_t bit = 1ull << j;
+      if (outl & bit) {
+        EdgeEval ev;
+        const double c2 = eval_edge(E[tid + j * kThreads], P, isig, TP, ev);
+        lastbad = ((float)c2 > (ev.stereo ? 7.815f : 5.991f)) ? (lastbad | bit) : (lastbad & ~bit);
+      }
+      bad += (lastbad & bit) ? 1.0 : 0.0;
+    }
+    outl = lastbad;
+    is_bad = (int)fs.sum1(bad);
+    if (round == 2) robust = false;
+    if (n < 10) break;
+  }
+  // ---- write back: Frame::SetPose(Converter::toCvMat(SE3quat_recov)), mvbOutlier ----
+  for (int j = 0; j < nslots; j++) outl_out[tid + j * kThreads] = (outl >> j) & 1;
+  if (tid == 0) {
+    double R[9];
+    quat_to_R(T.r, R);
+    for (int i = 0; i < 3; i++) {
+      for (int j = 0; j < 3; j++) Tf[4 * i + j] = (float)R[3 * i + j];
+      Tf[4 * i + 3] = (float)T.t[i];
+    }
+    Tf[12] = Tf[13] = Tf[14] = 0.f;
+    Tf[15] = 1.f;
+    n_inliers[f] = n - is_bad;
+    if (lm_iterations) lm_iterations[f] = lm_total;
+  }
+}
+
+}  // namespace
+
+hipError_t launch_pose_optimization(const slamgpu_pose_edge* d_edges, const int32_t* d_edge_start,
+                                    int n_frames, const PoseParams& P, float* d_Tcw,
+                                    uint8_t* d_outlier, int32_t* d_n_inliers,
+                                    int32_t* d_lm_iterations, hipStream_t st) {
+  if (n_frames <= 0) return hipSuccess;
+  if (n_frames < kPoseLatencyFrames) {
+    // few frames: 8 waves per frame for latency (the per-frame tracking call)
+    SLAMGPU_LAUNCH("pose_opt", st, pose_opt_kernel<8>, dim3(n_frames), dim3(512), 0, st, d_edges,
+                   d_edge_start, P, d_Tcw, d_outlier, d_n_inliers, d_lm_iterations);
+  } else {
+    // batches: one wave per frame, many frames resident per CU
+    SLAMGPU_LAUNCH("pose_opt", st, pose_opt_kernel<1>, dim3(n_frames), dim3(64), 0, st, d_edges,
+                   d_edge_start, P, d_Tcw, d_outlier, d_n_inliers, d_lm_iterations);
+  }
+  return hipGetLastError();
+}
+
+}  // namespace slamgpu

@@ -3,6 +3,7 @@
 Classes mirror the reference's C++ classes for this path:
   ORBextractor   src/orb_features/orb_extractor.h:25-93  (Compute, Get* tables, GetImagePyramid)
   OrbMatcher     src/orb_features/orb_matcher.h:14-119   (DescriptorDistance, SearchByProjection)
+  Optimizer      src/optimizer/optimizer.h:13-50         (PoseOptimization; include/slamgpu_optimizer.h)
   StereoFrontend the stereo Frame ctor's hot part (frame.cpp:61-111) batched over frames.
 The library is the only compute path: there is no CPU fallback, and every entry point raises if
 libslamgpu.so is missing or a HIP call fails.
@@ -31,7 +32,11 @@ MPS_QUERY_DTYPE = np.dtype([("proj_x", "<f4"), ("proj_y", "<f4"), ("proj_xr", "<
                             ("view_cos", "<f4"), ("level", "<i4"), ("in_view", "<i4"),
                             ("is_bad", "<i4"), ("mp_id", "<i4"), ("blocks", "<i4"),
                             ("pad", "<i4", (3,)), ("desc", "u1", (32,))])
-assert KP_DTYPE.itemsize == 28 and F2F_QUERY_DTYPE.itemsize == 64
+# slamgpu_pose_edge (include/slamgpu_optimizer.h): one PoseOptimization correspondence.
+POSE_EDGE_DTYPE = np.dtype([("xw", "<f4", (3,)), ("u", "<f4"), ("v", "<f4"), ("ur", "<f4"),
+                            ("octave", "<i4")])
+POSE_MAX_EDGES = 4096
+assert KP_DTYPE.itemsize == 28 and F2F_QUERY_DTYPE.itemsize == 64 and POSE_EDGE_DTYPE.itemsize == 28
 assert F2F_POSE_DTYPE.itemsize == 72 and MPS_QUERY_DTYPE.itemsize == 80
 
 EXPORTS = [
@@ -43,7 +48,8 @@ EXPORTS = [
     "slamgpu_search_by_projection_mps", "slamgpu_search_by_projection_frame_device",
     "slamgpu_search_by_projection_mps_device", "slamgpu_debug_level_keys",
     "slamgpu_make_vo_queries_device", "slamgpu_timing_start", "slamgpu_timing_stop",
-    "slamgpu_timing_read",
+    "slamgpu_timing_read", "slamgpu_pose_optimization", "slamgpu_pose_optimization_device",
+    "slamgpu_optimizer_last_error",
 ]
 
 
@@ -75,6 +81,13 @@ def lib():
     if _lib is None:
         if not os.path.exists(LIB_PATH):
             raise ImportError(f"{LIB_PATH} missing: run `python -m slam_framework_amd.build`")
+        # One HIP runtime per process: torch bundles its own libamdhip64.so.7. Loaded first, it
+        # also satisfies our library's libamdhip64.so.7 dependency; loaded after us, it would
+        # map a second runtime next to /opt/rocm's and fail to initialise the device.
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
         L = C.CDLL(LIB_PATH)
         vp, ip, fp, sz = C.c_void_p, C.c_int, C.c_float, C.c_size_t
         L.slamgpu_create.argtypes = [ip, C.POINTER(OrbParams), ip, ip, ip, C.POINTER(vp)]
@@ -106,6 +119,12 @@ def lib():
         L.slamgpu_timing_start.argtypes = [vp, C.c_char_p, ip]
         L.slamgpu_timing_stop.argtypes = [vp, vp]
         L.slamgpu_timing_read.argtypes = [vp, C.c_char_p, C.POINTER(C.c_double), C.POINTER(ip)]
+        L.slamgpu_pose_optimization.argtypes = [C.POINTER(Camera), vp, ip, vp, ip, vp, vp,
+                                                C.POINTER(ip)]
+        L.slamgpu_pose_optimization_device.argtypes = [C.POINTER(Camera), vp, ip, vp, vp, ip, vp,
+                                                       vp, vp, vp, vp]
+        L.slamgpu_optimizer_last_error.argtypes = []
+        L.slamgpu_optimizer_last_error.restype = C.c_char_p
         _lib = L
     return _lib
 
@@ -338,3 +357,42 @@ class OrbMatcher:
         a = np.ascontiguousarray(a, dtype=np.uint8)
         b = np.ascontiguousarray(b, dtype=np.uint8)
         return lib().slamgpu_descriptor_distance(_ptr(a), _ptr(b))
+
+
+def _opt_check(rc):
+    if rc != 0:
+        raise SlamGpuError(f"slamgpu optimizer error {rc}: "
+                           f"{lib().slamgpu_optimizer_last_error().decode()}")
+
+
+class Optimizer:
+    """The reference's Optimizer (src/optimizer/optimizer.h:13-50) for the hot path.
+
+    PoseOptimization takes the frame's correspondences as POSE_EDGE_DTYPE records (map point
+    world position, undistorted keypoint, right coordinate or -1, octave) instead of a Frame&:
+    the caller's Frame -> edge gather is optimizer.cpp:239-309 without the g2o objects."""
+
+    @staticmethod
+    def PoseOptimization(edges, Tcw, cam, inv_sigma2):
+        """Optimizer::PoseOptimization (optimizer.cpp:209-411). Returns (n_inliers, Tcw', outlier):
+        the reference's return value, the optimised pose (f32 4x4; the input pose when fewer
+        than 3 edges) and Frame::mvbOutlier for the edges."""
+        edges = np.ascontiguousarray(edges, dtype=POSE_EDGE_DTYPE)
+        T = np.ascontiguousarray(np.asarray(Tcw, np.float32).reshape(4, 4)).copy()
+        isig = np.ascontiguousarray(inv_sigma2, np.float32)
+        outl = np.zeros(len(edges), np.uint8)
+        n_inl = C.c_int()
+        _opt_check(lib().slamgpu_pose_optimization(C.byref(Camera(*cam)), _ptr(isig), len(isig),
+                                                   _ptr(edges), len(edges), _ptr(T), _ptr(outl),
+                                                   C.byref(n_inl)))
+        return n_inl.value, T, outl.astype(bool)
+
+
+def pose_optimization_device(cam, inv_sigma2, d_edges, d_edge_start, n_frames, d_Tcw, d_outlier,
+                             d_n_inliers, d_lm_iterations=None, stream=None):
+    """slamgpu_pose_optimization_device: PoseOptimization for a batch of frames in HBM."""
+    isig = np.ascontiguousarray(inv_sigma2, np.float32)
+    _opt_check(lib().slamgpu_pose_optimization_device(
+        C.byref(Camera(*cam)), _ptr(isig), len(isig), _ptr(d_edges), _ptr(d_edge_start), n_frames,
+        _ptr(d_Tcw), _ptr(d_outlier), _ptr(d_n_inliers), _ptr(d_lm_iterations),
+        C.c_void_p(stream) if stream else None))

@@ -102,3 +102,83 @@ def sequence(seed: int, n: int, cols: int = KITTI_COLS, rows: int = KITTI_ROWS):
     for t in range(n):
         L[t], R[t] = stereo_pair(seed, cols, rows, t)
     return L, R
+
+
+def _rodrigues(w: np.ndarray) -> np.ndarray:
+    th = float(np.linalg.norm(w))
+    if th == 0.0:
+        return np.eye(3)
+    k = w / th
+    Kx = np.array([[0, -k[2], k[1]], [k[2], 0, -k[0]], [-k[1], k[0], 0]])
+    return np.eye(3) + np.sin(th) * Kx + (1 - np.cos(th)) * (Kx @ Kx)
+
+
+def level_inv_sigma2(scale_factor: float = 1.2, nlevels: int = 8) -> np.ndarray:
+    """Frame::mvInvLevelSigma2 as ORBextractor builds it (orb_extractor.cpp:357-369, f32)."""
+    s2 = np.ones(nlevels, np.float32)
+    sc = np.float32(1.0)
+    sf = float(np.float32(scale_factor))  # float ctor argument kept in a double member
+    for i in range(1, nlevels):
+        sc = np.float32(float(sc) * sf)
+        s2[i] = np.float32(sc * sc)
+    return (np.float32(1.0) / s2).astype(np.float32)
+
+
+def pose_problem(seed: int, n: int = 2000, stereo_frac: float = 0.6, outlier_frac: float = 0.1,
+                 noise_px: float = 0.7, rot_err: float = 0.02, trans_err: float = 0.1,
+                 cam=KITTI_CAM, cols: int = KITTI_COLS, rows: int = KITTI_ROWS, nlevels: int = 8,
+                 scale_factor: float = 1.2):
+    """One PoseOptimization input (configs[3]): n map point / keypoint correspondences of a
+    KITTI-like stereo frame.
+
+    True pose: a random rotation (about 10 degrees) and translation (about 5 m). Each point is a
+    pixel drawn uniformly over the image at depth U[2, 60] m, seen at octave ~ Geometric(0.45)
+    capped at nlevels-1 with N(0, noise_px * scale^octave) pixel noise; a stereo_frac fraction
+    has a right coordinate ur = u - bf / z (same noise), the rest ur = -1 (monocular).
+    outlier_frac of the observations are replaced by uniform pixels (gross mismatches). The
+    initial pose is the true one perturbed by rot_err rad and trans_err m, as a constant-velocity
+    prediction would be. Returns (edges[POSE_EDGE_DTYPE order], Tcw_init f32 4x4, Tcw_true f64
+    4x4, inv_sigma2 f32[nlevels], is_outlier bool[n])."""
+    rng = np.random.default_rng(seed)
+    fx, fy, cx, cy, bf = cam
+    Rt = _rodrigues(rng.normal(0, 0.1, 3))
+    tt = rng.normal(0, 3.0, 3)
+    u = rng.uniform(0, cols, n)
+    v = rng.uniform(0, rows, n)
+    z = rng.uniform(2.0, 60.0, n)
+    Xc = np.stack([(u - cx) / fx * z, (v - cy) / fy * z, z], 1)
+    Xw = (Xc - tt) @ Rt  # Rt^T (Xc - t)
+    octave = np.minimum(rng.geometric(0.45, n) - 1, nlevels - 1).astype(np.int32)
+    sig = noise_px * np.power(scale_factor, octave)
+    uo = u + rng.normal(0, 1, n) * sig
+    vo = v + rng.normal(0, 1, n) * sig
+    stereo = rng.uniform(0, 1, n) < stereo_frac
+    uro = np.where(stereo, u - bf / z + rng.normal(0, 1, n) * sig, -1.0)
+    bad = rng.uniform(0, 1, n) < outlier_frac
+    uo = np.where(bad, rng.uniform(0, cols, n), uo)
+    vo = np.where(bad, rng.uniform(0, rows, n), vo)
+    uro = np.where(bad & stereo, np.maximum(uo - rng.uniform(0, 90, n), 0.0), uro)
+    from .slamgpu import POSE_EDGE_DTYPE
+    edges = np.zeros(n, POSE_EDGE_DTYPE)
+    edges["xw"] = Xw.astype(np.float32)
+    edges["u"] = uo.astype(np.float32)
+    edges["v"] = vo.astype(np.float32)
+    edges["ur"] = uro.astype(np.float32)
+    edges["octave"] = octave
+    T_true = np.eye(4)
+    T_true[:3, :3], T_true[:3, 3] = Rt, tt
+    T0 = np.eye(4)
+    T0[:3, :3] = _rodrigues(rng.normal(0, rot_err / np.sqrt(3), 3)) @ Rt
+    T0[:3, 3] = tt + rng.normal(0, trans_err / np.sqrt(3), 3)
+    return edges, T0.astype(np.float32), T_true, level_inv_sigma2(scale_factor, nlevels), bad
+
+
+def pose_batch(seed: int, n_frames: int, n: int = 2000, **kw):
+    """n_frames independent pose problems packed as the device call takes them: edges of frame f
+    at [start[f], start[f+1]), poses (n_frames, 4, 4) f32."""
+    probs = [pose_problem(seed + f, n, **kw) for f in range(n_frames)]
+    edges = np.concatenate([p[0] for p in probs])
+    start = np.zeros(n_frames + 1, np.int32)
+    start[1:] = np.cumsum([len(p[0]) for p in probs])
+    poses = np.stack([p[1] for p in probs])
+    return edges, start, poses, probs[0][3], probs

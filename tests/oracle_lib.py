@@ -239,3 +239,53 @@ def search_mps(t, g, cur_kps, cur_desc, cur_ur, cur_mp, q, mp_nobs, nnratio, th)
         C.byref(g), C.byref(t), C.byref(fv), len(q), ptr(in_view), ptr(is_bad), ptr(level),
         ptr(cols["view_cos"]), ptr(cols["proj_x"]), ptr(cols["proj_y"]), ptr(cols["proj_xr"]),
         ptr(desc), ptr(mp_nobs), nnratio, th)
+
+
+# ---- PoseOptimization (oracle/pose_oracle.c) ------------------------------------------------
+POSE_EDGE_DTYPE = np.dtype([("xw", "<f4", (3,)), ("u", "<f4"), ("v", "<f4"), ("ur", "<f4"),
+                            ("octave", "<i4")])
+
+
+def _pose_lib():
+    L = lib()
+    if not getattr(L, "_pose_bound", False):
+        vp, ip = C.c_void_p, C.c_int
+        L.oc_pose_optimization.argtypes = [vp, vp, vp, ip, vp, vp, C.POINTER(ip)]
+        L.oc_se3_exp.argtypes = [vp, vp, vp]
+        L.oc_se3_exp.restype = None
+        L.oc_pose_edge_eval.argtypes = [vp, vp, vp, vp, C.c_float, vp, vp]
+        L.oc_pose_edge_eval.restype = C.c_double
+        L._pose_bound = True
+    return L
+
+
+def pose_optimization(cam, inv_sigma2, edges, Tcw):
+    """Optimizer::PoseOptimization restated: returns (n_inliers, Tcw', outlier, lm_iterations)."""
+    cam = np.asarray(cam, np.float32)
+    isig = np.ascontiguousarray(inv_sigma2, np.float32)
+    e = np.ascontiguousarray(edges).view(POSE_EDGE_DTYPE)
+    T = np.ascontiguousarray(np.asarray(Tcw, np.float32).reshape(4, 4)).copy()
+    outl = np.zeros(max(len(e), 1), np.uint8)
+    it = C.c_int()
+    r = _pose_lib().oc_pose_optimization(ptr(cam), ptr(isig), ptr(e), len(e), ptr(T), ptr(outl),
+                                         C.byref(it))
+    return r, T, outl[:len(e)].astype(bool), it.value
+
+
+def se3_exp(u):
+    u = np.ascontiguousarray(u, np.float64)
+    R, t = np.zeros(9), np.zeros(3)
+    _pose_lib().oc_se3_exp(ptr(u), ptr(R), ptr(t))
+    return R.reshape(3, 3), t
+
+
+def pose_edge_eval(cam, R, t, edge, inv_sigma2):
+    """(chi2, error[3], Jacobian[3, 6]) of one edge at pose (R, t)."""
+    cam = np.asarray(cam, np.float32)
+    R = np.ascontiguousarray(R, np.float64)
+    t = np.ascontiguousarray(t, np.float64)
+    e1 = np.ascontiguousarray(np.asarray(edge).reshape(1)).view(POSE_EDGE_DTYPE)
+    err, J = np.zeros(3), np.zeros(18)
+    c = _pose_lib().oc_pose_edge_eval(ptr(cam), ptr(R), ptr(t), ptr(e1), float(inv_sigma2),
+                                      ptr(err), ptr(J))
+    return c, err, J.reshape(3, 6)

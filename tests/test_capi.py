@@ -1,5 +1,5 @@
-"""The C-ABI library builds for gfx950, loads, and exports every function include/slamgpu.h
-declares (no compute calls: no GPU here)."""
+"""The C-ABI library builds for gfx950, loads, and exports every function include/*.h declares
+(no compute calls: no GPU here)."""
 import os
 import re
 
@@ -9,9 +9,13 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def declared_functions():
-    src = open(os.path.join(ROOT, "include", "slamgpu.h")).read()
-    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
-    return sorted(set(re.findall(r"\b(slamgpu_[a-z0-9_]+)\s*\(", src)))
+    names = set()
+    for h in sorted(os.listdir(os.path.join(ROOT, "include"))):
+        if h.endswith(".h"):
+            src = open(os.path.join(ROOT, "include", h)).read()
+            src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+            names |= set(re.findall(r"\b(slamgpu_[a-z0-9_]+)\s*\(", src))
+    return sorted(names)
 
 
 def test_library_exports_header():

@@ -2,18 +2,20 @@
 # Per-kernel PMC passes over a short bench run: one rocprofv3 invocation per counter group,
 # kernel-trace only (never combined with sys/runtime traces).
 #   KERNEL=fast_cells tools/pmc_kernel.sh            -> gpurun_out/pmck/<kernel>/p<i>/...
+#   CMD="python3 tools/pose_time.py 1024 2" KERNEL=pose_opt tools/pmc_kernel.sh
 set -e
 export TMPDIR=/tmp
 K=${KERNEL:-fast_cells}
 OUT=${OUT:-gpurun_out/pmck/$K}
 ARGS=${ARGS:-"--steps 2 --warmup 1 --no-cpu-baseline"}
+CMD=${CMD:-"python3 bench.py $ARGS"}
 mkdir -p $OUT
 i=0
 while read -r grp; do
   [ -z "$grp" ] && continue
   i=$((i+1))
   timeout -k 10 240 rocprofv3 --pmc $grp --kernel-include-regex "$K" --kernel-trace \
-    --output-format csv -d $OUT/p$i -o run -- python3 bench.py $ARGS > $OUT/p$i.log 2>&1
+    --output-format csv -d $OUT/p$i -o run -- $CMD > $OUT/p$i.log 2>&1
   echo "pass $i ok: $grp"
 done <<GROUPS
 MeanOccupancyPerCU
