@@ -2,10 +2,12 @@
  * slamgpu_optimizer.h -- C ABI of the MI355X motion-only / local bundle adjustment
  * (libslamgpu.so, same library as slamgpu.h).
  *
- * Drop-in boundary for the reference's Optimizer (src/optimizer/optimizer.h:14-40, a class of
+ * Drop-in boundary for the reference's Optimizer (src/optimizer/optimizer.h:13-50, a class of
  * static functions over g2o):
- *   slamgpu_pose_optimization         Optimizer::PoseOptimization(Frame*)  optimizer.cpp:209-411
+ *   slamgpu_pose_optimization         Optimizer::PoseOptimization(Frame&)  optimizer.cpp:209-411
  *   slamgpu_pose_optimization_device  the same, batched over frames, inputs resident in HBM
+ *   slamgpu_local_bundle_adjustment   Optimizer::LocalBundleAdjustment     optimizer.cpp:413-716
+ *   slamgpu_local_bundle_adjustment_device   the same, batched over independent problems
  * These calls hold no state, so they take no handle. Every function returns 0 or a negative
  * SLAMGPU_E* code (slamgpu.h) with a message in slamgpu_optimizer_last_error() (per thread).
  *
@@ -59,6 +61,65 @@ int slamgpu_pose_optimization_device(const slamgpu_camera* cam, const float* inv
                                      const int32_t* d_edge_start, int n_frames, float* d_Tcw,
                                      uint8_t* d_outlier, int32_t* d_n_inliers,
                                      int32_t* d_lm_iterations, void* stream);
+
+/* ---- LocalBundleAdjustment ----------------------------------------------------------------- */
+/* One observation of a local map point (an EdgeSE3ProjectXYZ / EdgeStereoSE3ProjectXYZ,
+ * optimizer.cpp:548-606): the observing keyframe (index into the problem's keyframes), the
+ * undistorted keypoint, its right coordinate (< 0 = monocular) and octave. 20 bytes.
+ * Observations are grouped by map point in the order the reference inserts the edges
+ * (point_obs_start is the CSR row pointer); a point has at most one observation per keyframe. */
+typedef struct {
+  int32_t keyframe;
+  float u, v, ur;
+  int32_t octave;
+} slamgpu_ba_obs;
+
+/* kf_mode: the role a keyframe vertex plays (optimizer.cpp:413-506). */
+#define SLAMGPU_KF_LOCAL 0        /* local keyframe: optimised, pose written back */
+#define SLAMGPU_KF_LOCAL_FIXED 1  /* local keyframe with id 0: fixed, pose written back */
+#define SLAMGPU_KF_FIXED 2        /* fixed camera (sees a local point): neither */
+/* Largest local (optimised) window and keyframe count per problem the device solver takes. */
+#define SLAMGPU_BA_MAX_LOCAL_KF 24
+#define SLAMGPU_BA_MAX_KF 256
+
+/* Replaces: void Optimizer::LocalBundleAdjustment(KeyFrame*, bool* stop_flag, const Map&)
+ * (optimizer.cpp:413-716) after its graph gathering: kf_Tcw[16 n_kf] (row-major f32, updated for
+ * modes 0 and 1), points[3 n_points] (MapPoint::GetWorldPos, all updated), the observations, and
+ * erase[n_obs]: 1 where the reference puts (keyframe, point) in vToErase (the caller then runs
+ * EraseMapPointMatch / EraseObservation and MapPoint::UpdateNormalAndDepth). stop_flag (may be
+ * NULL) is read once before the optimisation starts, as the reference checks it
+ * (optimizer.cpp:616-618). *lm_iterations (may be NULL): LM iterations run. Synchronous. */
+int slamgpu_local_bundle_adjustment(const slamgpu_camera* cam, const float* inv_sigma2,
+                                    int nlevels, float* kf_Tcw, const uint8_t* kf_mode, int n_kf,
+                                    float* points, int n_points, const int32_t* point_obs_start,
+                                    const slamgpu_ba_obs* obs, const int* stop_flag,
+                                    uint8_t* erase, int* lm_iterations);
+
+/* A problem of a batch: its keyframes d_kf_*[kf_begin, kf_begin + n_kf) and points
+ * d_points[point_begin, point_begin + n_points); observations are
+ * d_obs[d_point_obs_start[point_begin] .. d_point_obs_start[point_begin + n_points]) with
+ * keyframe indices relative to kf_begin. */
+typedef struct {
+  int32_t kf_begin, n_kf, point_begin, n_points;
+} slamgpu_ba_problem;
+
+/* Device workspace the batched call needs for these totals over all problems. */
+size_t slamgpu_local_ba_workspace_bytes(int total_kf, int total_points, int total_obs);
+
+/* Batched, asynchronous on `stream`, every pointer device memory. d_point_obs_start has
+ * total_points + 1 entries (global observation offsets). d_status[p]: LM iterations run (>= 0),
+ * or -1 more than SLAMGPU_BA_MAX_LOCAL_KF local keyframes, -2 a point observed twice by one
+ * keyframe, -3 a keyframe index outside the problem or more than SLAMGPU_BA_MAX_KF keyframes
+ * (the problem's outputs are then untouched). d_stop_flag (may be NULL; may be host-mapped
+ * memory): polled before every LM iteration -- a non-zero value ends the optimisation as
+ * g2o's force-stop flag does (SparseOptimizer::terminate). */
+int slamgpu_local_bundle_adjustment_device(
+    const slamgpu_camera* cam, const float* inv_sigma2, int nlevels,
+    const slamgpu_ba_problem* d_problems, int n_problems, float* d_kf_Tcw,
+    const uint8_t* d_kf_mode, float* d_points, const int32_t* d_point_obs_start,
+    const slamgpu_ba_obs* d_obs, uint8_t* d_erase, int32_t* d_status, void* d_workspace,
+    size_t workspace_bytes, int total_kf, int total_points, int total_obs,
+    const int32_t* d_stop_flag, void* stream);
 
 const char* slamgpu_optimizer_last_error(void);
 

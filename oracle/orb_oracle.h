@@ -8,6 +8,7 @@
  * What it restates (every function cites the reference file:line it follows, paths relative
  * to the reference repository root):
  *   - Optimizer::PoseOptimization (src/optimizer/optimizer.cpp:209-411, on g2o): pose_oracle.c
+ *   - Optimizer::LocalBundleAdjustment (optimizer.cpp:413-716, on g2o): ba_oracle.c
  *   - ORBextractor (src/orb_features/orb_extractor.cpp): ctor tables, ComputePyramid,
  *     ComputeKeyPointsOctTree (cell FAST + threshold fallback), DistributeOctTree,
  *     IC_Angle / computeOrientation, GaussianBlur + computeOrbDescriptor, Compute.
@@ -173,6 +174,24 @@ int oc_pose_optimization(const float cam[5], const float* inv_sigma2, const oc_p
 void oc_se3_exp(const double u[6], double R[9], double t[3]);
 double oc_pose_edge_eval(const float cam[5], const double R[9], const double t[3],
                          const oc_pose_edge* e, float inv_sigma2, double err[3], double J[18]);
+
+/* ---- Optimizer::LocalBundleAdjustment (ba_oracle.c) -------------------------------------- */
+/* One observation of a local map point: keyframe index, undistorted keypoint, right coordinate
+ * (< 0 monocular), octave. Observations are grouped by point (point_obs_start, CSR). */
+typedef struct {
+  int32_t keyframe;
+  float u, v, ur;
+  int32_t octave;
+} oc_ba_obs;
+/* kf_mode: 0 local (optimised, written back), 1 local but fixed (keyframe id 0; written back),
+ * 2 fixed camera (neither). erase[e]: the reference's vToErase membership of observation e. */
+int oc_local_bundle_adjustment(const float cam[5], const float* inv_sigma2, float* kf_Tcw,
+                               const uint8_t* kf_mode, int n_kf, float* points, int n_points,
+                               const int32_t* point_obs_start, const oc_ba_obs* obs,
+                               uint8_t* erase, int* lm_iterations);
+double oc_ba_edge_eval(const float cam[5], const double R[9], const double t[3], const double X[3],
+                       const oc_ba_obs* o, float inv_sigma2, double err[3], double Jl[9],
+                       double Jp[18]);
 
 #ifdef __cplusplus
 }

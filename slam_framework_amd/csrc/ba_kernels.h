@@ -1,0 +1,36 @@
+// ba_kernels.h -- launcher and workspace of the device LocalBundleAdjustment (ba_kernels.hip).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/slamgpu_optimizer.h"
+#include "pose_kernels.h"
+
+namespace slamgpu {
+
+static_assert(sizeof(slamgpu_ba_obs) == 20, "ba observation layout");
+
+// Device scratch of a batch, indexed by global keyframe / point / observation index.
+struct BaWorkspace {
+  double* chi2;      // [obs] last computed chi2 (g2o keeps the last error per edge)
+  double* hpl;       // [obs][6 x 3] Hpl block of a local-keyframe edge
+  double* bdinv;     // [obs][6 x 3] Hpl Dinv of the current trial
+  uint8_t* act;      // [obs] edge at level 0
+  int32_t* psorted;  // [obs] a point's active local-keyframe edges sorted by keyframe
+  int2* hits;        // [obs * ((MAX_LOCAL_KF + 2) / 2)] S-block point pairs
+  double* pt;        // [points][32] estimate, backup, Hll, bl, Dinv, db, xl
+  uint32_t* pmask;   // [points] local keyframes with an active edge to the point
+  double* kf;        // [keyframes][64] estimate (q, t, R), backup, Hpp, bp
+};
+
+// Lays the workspace out from `base` (nullptr: only computes *bytes).
+BaWorkspace ba_workspace_layout(void* base, int total_kf, int total_points, int total_obs,
+                                size_t* bytes);
+
+hipError_t launch_local_ba(const PoseParams& P, const slamgpu_ba_problem* d_problems,
+                           int n_problems, float* d_kf_Tcw, const uint8_t* d_kf_mode,
+                           float* d_points, const int32_t* d_pstart, const slamgpu_ba_obs* d_obs,
+                           uint8_t* d_erase, int32_t* d_status, const BaWorkspace& ws,
+                           const int32_t* d_stop, hipStream_t st);
+
+}  // namespace slamgpu

@@ -1,0 +1,1001 @@
+// ba_kernels.hip -- Optimizer::LocalBundleAdjustment (optimizer.cpp:413-716) on the device.
+//
+// One 1024-thread workgroup per problem runs the reference's whole schedule: 5 robust LM
+// iterations, the level-1 outlier test, 10 plain iterations, the erase test and the write-back.
+// Every LM trial solves the full system by the Schur complement on the points, as g2o's
+// BlockSolver does (block_solver.hpp:351-497):
+//
+//   point pass   (thread per point)   Dinv_p = (Hll_p + lambda I)^-1, db_p = Dinv_p bl_p and
+//                                     BDinv_e = Hpl_e Dinv_p for the point's free-keyframe edges
+//   S assembly   (wave per 6x6 block) S(kh, kl) = [kh == kl](Hpp + lambda I)
+//                                       - sum over the points seen by both BDinv_e(kh) Hpl_e(kl)^T
+//                                     lanes over the block's point pairs, deterministic wave sums
+//   reduced rhs  (wave per keyframe)  bs_k = bp_k - sum_e Hpl_e db_p
+//   LDLT         (whole workgroup)    S in LDS (lower triangle, 6K <= 144), 6x6-blocked
+//                                     right-looking factorisation with the forward solve fused
+//   back-subst.  (thread per point)   xl_p = Dinv_p (bl_p - sum_e Hpl_e^T xp_k)
+//
+// The pairs of every S block are listed once per phase (the active edge set only changes between
+// the phases) in point order with ballot prefix counts, so every sum runs in a fixed order: the
+// kernel is deterministic, with no floating-point atomics. Linearisation is a point pass (error,
+// chi2, Huber weight, point and pose Jacobians, Hll, bl, Hpl per edge) and a keyframe pass (a wave
+// per local keyframe sums Hpp and bp over its edges). FP64 throughout, with the reference's f32
+// quirks (types_six_dof_expmap.cpp:150-157: float inverse depth, bf * invz as a float product).
+// MFMA is not used: the Schur blocks are 6x3 by 3x6 products scattered over ~10^4 point pairs,
+// and FP64 MFMA has the FP64 vector rate on gfx950.
+#include <hip/hip_runtime.h>
+
+#include <cfloat>
+#include <cmath>
+
+#include "ba_kernels.h"
+#include "device_math.h"
+#include "se3_device.h"
+
+namespace slamgpu {
+namespace {
+
+using se3::Quat;
+using se3::SE3;
+
+constexpr int kThreads = 1024;
+constexpr int kWaves = kThreads / 64;
+constexpr int kMaxK = SLAMGPU_BA_MAX_LOCAL_KF;
+constexpr int kMaxN = 6 * kMaxK;
+constexpr int kMaxBlk = kMaxK * (kMaxK + 1) / 2;
+constexpr int kPairsPerObs = (kMaxK + 2) / 2;  // >= (m + 1) / 2 pairs per free edge, m <= kMaxK
+
+__device__ __forceinline__ int tri(int i) { return i * (i + 1) / 2; }
+__device__ __forceinline__ int sidx(int i, int j) { return tri(i) + j; }  // lower, j <= i
+__device__ __forceinline__ int hidx(int a, int c) {  // packed upper triangle of a 6x6, a <= c
+  return a * 6 - (a * (a - 1)) / 2 + (c - a);
+}
+
+// ---- per-KF / per-point workspace records (ba_kernels.h: BaWorkspace) -----------------------
+// kf record (64 doubles): q 0..3, t 4..6, R 8..16, backup q 17..20 t 21..23, Hpp 24..44,
+// bp 45..50, xp 51..56, Hpp-diag max 57
+constexpr int KQ = 0, KT = 4, KR = 8, KBQ = 17, KBT = 21, KH = 24, KB = 45;
+// point record (32 doubles): X 0..2, Xb 3..5, Hll 6..11 (00 01 02 11 12 22), bl 12..14,
+// Dinv 15..20 (same packing), db 21..23, xl 24..26
+constexpr int PX = 0, PXB = 3, PH = 6, PB = 12, PD = 15, PDB = 21, PXL = 24;
+__device__ __forceinline__ int s3(int i, int j) {  // packed symmetric 3x3
+  const int a = i < j ? i : j, b = i < j ? j : i;
+  return a == 0 ? b : (a == 1 ? 2 + b : 5);
+}
+
+__device__ __forceinline__ void load_T(const double* kr, SE3& T) {
+  T.r.x = kr[KQ];
+  T.r.y = kr[KQ + 1];
+  T.r.z = kr[KQ + 2];
+  T.r.w = kr[KQ + 3];
+  T.t[0] = kr[KT];
+  T.t[1] = kr[KT + 1];
+  T.t[2] = kr[KT + 2];
+}
+__device__ __forceinline__ void store_T(double* kr, const SE3& T) {
+  kr[KQ] = T.r.x;
+  kr[KQ + 1] = T.r.y;
+  kr[KQ + 2] = T.r.z;
+  kr[KQ + 3] = T.r.w;
+  kr[KT] = T.t[0];
+  kr[KT + 1] = T.t[1];
+  kr[KT + 2] = T.t[2];
+  double R[9];
+  se3::quat_to_R(T.r, R);
+  for (int i = 0; i < 9; i++) kr[KR + i] = R[i];
+}
+
+struct ObsEval {
+  double x, y, z, iz;  // camera coordinates, 1 / z
+  double e[3];
+  double info;
+  bool stereo;
+};
+
+// e = obs - cam_project(T.map(X)) for EdgeSE3ProjectXYZ / EdgeStereoSE3ProjectXYZ; returns chi2.
+__device__ __forceinline__ double eval_obs(const slamgpu_ba_obs& o, const PoseParams& P,
+                                           const float* isig, const double* kr, const double X[3],
+                                           ObsEval& v) {
+  Quat q;
+  q.x = kr[KQ];
+  q.y = kr[KQ + 1];
+  q.z = kr[KQ + 2];
+  q.w = kr[KQ + 3];
+  double p[3];
+  se3::quat_rotate(q, X, p);
+  v.x = p[0] + kr[KT];
+  v.y = p[1] + kr[KT + 1];
+  v.z = p[2] + kr[KT + 2];
+  v.iz = 1.0 / v.z;
+  v.stereo = o.ur >= 0;
+  int oct = o.octave;
+  oct = oct < 0 ? 0 : (oct >= P.nlevels ? P.nlevels - 1 : oct);
+  v.info = (double)isig[oct];
+  double px, py;
+  if (!v.stereo) {  // project2d: x / z
+    px = v.x / v.z;
+    py = v.y / v.z;
+  } else {          // const float invz = 1.0f / z
+    const float izf = (float)v.iz;
+    px = v.x * (double)izf;
+    py = v.y * (double)izf;
+  }
+  const double u = px * (double)P.fx + (double)P.cx;
+  const double vv = py * (double)P.fy + (double)P.cy;
+  v.e[0] = (double)o.u - u;
+  v.e[1] = (double)o.v - vv;
+  v.e[2] = 0.0;
+  if (v.stereo) {  // res[2] = res[0] - bf * invz with `const float& bf`: a float product
+    const float bfz = P.bf * (float)v.iz;
+    v.e[2] = (double)o.ur - (u - (double)bfz);
+  }
+  return v.info * (v.e[0] * v.e[0] + v.e[1] * v.e[1] + v.e[2] * v.e[2]);
+}
+
+// Jl (D x 3, wrt the point) and Jp (D x 6, wrt the pose); row 2 is zero for monocular edges
+// (types_six_dof_expmap.cpp:103-137, 188-234).
+__device__ __forceinline__ void obs_jacobians(const ObsEval& v, const PoseParams& P,
+                                              const double* kr, double Jl[3][3], double Jp[3][6]) {
+  const double fx = P.fx, fy = P.fy, bf = P.bf, x = v.x, y = v.y, iz = v.iz, iz2 = iz * iz;
+  const double sm = v.stereo ? 1.0 : 0.0;
+  for (int j = 0; j < 3; j++) {
+    const double r0 = kr[KR + j], r1 = kr[KR + 3 + j], r2 = kr[KR + 6 + j];
+    Jl[0][j] = -fx * r0 * iz + fx * x * r2 * iz2;
+    Jl[1][j] = -fy * r1 * iz + fy * y * r2 * iz2;
+    Jl[2][j] = sm * (Jl[0][j] - bf * r2 * iz2);
+  }
+  Jp[0][0] = x * y * iz2 * fx;
+  Jp[0][1] = -(1 + x * x * iz2) * fx;
+  Jp[0][2] = y * iz * fx;
+  Jp[0][3] = -iz * fx;
+  Jp[0][4] = 0;
+  Jp[0][5] = x * iz2 * fx;
+  Jp[1][0] = (1 + y * y * iz2) * fy;
+  Jp[1][1] = -x * y * iz2 * fy;
+  Jp[1][2] = -x * iz * fy;
+  Jp[1][3] = 0;
+  Jp[1][4] = -iz * fy;
+  Jp[1][5] = y * iz2 * fy;
+  Jp[2][0] = sm * (Jp[0][0] - bf * y * iz2);
+  Jp[2][1] = sm * (Jp[0][1] + bf * x * iz2);
+  Jp[2][2] = sm * Jp[0][2];
+  Jp[2][3] = sm * Jp[0][3];
+  Jp[2][4] = 0;
+  Jp[2][5] = sm * (Jp[0][5] - bf * iz2);
+}
+
+__device__ __forceinline__ double huber_delta(bool stereo) {
+  return stereo ? (double)(float)sqrt(7.815) : (double)(float)sqrt(5.991);
+}
+
+// ---- reductions -------------------------------------------------------------------------------
+__device__ __forceinline__ double wave_reduce_scatter32(double v[32]) {
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int h = 16, m = 32; h >= 1; h >>= 1, m >>= 1) {
+    const uint64_t up = (lane & m) ? ~0ull : 0ull;
+#pragma unroll
+    for (int i = 0; i < h; i++) {
+      const uint64_t lo = __builtin_bit_cast(uint64_t, v[i]);
+      const uint64_t hi = __builtin_bit_cast(uint64_t, v[i + h]);
+      const double send = __builtin_bit_cast(double, (lo & up) | (hi & ~up));
+      const double keep = __builtin_bit_cast(double, (hi & up) | (lo & ~up));
+      v[i] = keep + __shfl_xor(send, m);
+    }
+  }
+  return v[0] + __shfl_xor(v[0], 1);
+}
+
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) v += __shfl_xor(v, m);
+  return v;
+}
+__device__ __forceinline__ double wave_max(double v) {
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) v = fmax(v, __shfl_xor(v, m));
+  return v;
+}
+
+__device__ __forceinline__ uint32_t lanes_below(uint64_t bal) {
+  return __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32),
+                                   __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
+}
+
+struct BaShared {
+  double S[kMaxN * (kMaxN + 1) / 2];  // reduced camera system, packed lower triangle
+  double rhs[kMaxN];                  // bs, then y = L^-1 bs, then the solution
+  double xp[kMaxN];                   // the pose step of the last successful solve (g2o's _x)
+  double dg[kMaxN];                   // D of the LDLT
+  double V[kMaxN][6];                 // panel L_IJ D_J of the current block column
+  double red[2][kWaves][2];           // block-sum partials (double-buffered)
+  int blk_cnt[kMaxBlk];
+  int blk_off[kMaxBlk + 1];
+  int blk_run[kMaxBlk];
+  int wcnt[kWaves][kMaxBlk];
+  int blk_kk[kMaxBlk];  // kh << 8 | kl
+  int8_t free_of_kf[SLAMGPU_BA_MAX_KF];
+  int kf_of_free[kMaxK];
+  int K, err, ok;
+  int rb;
+};
+
+// Deterministic block sum of two values: wave butterflies (bitwise identical in every lane), wave
+// partials summed in wave order by every thread.
+__device__ __forceinline__ void block_sum2(BaShared& sh, double& a, double& b) {
+  a = wave_sum(a);
+  b = wave_sum(b);
+  const int lane = threadIdx.x & 63, w = wave_id();
+  if (lane == 0) {
+    sh.red[sh.rb][w][0] = a;
+    sh.red[sh.rb][w][1] = b;
+  }
+  __syncthreads();
+  double s0 = 0.0, s1 = 0.0;
+  for (int k = 0; k < kWaves; k++) {
+    s0 += sh.red[sh.rb][k][0];
+    s1 += sh.red[sh.rb][k][1];
+  }
+  a = s0;
+  b = s1;
+  __syncthreads();  // every reader done before the buffer flips back
+  if (threadIdx.x == 0) sh.rb ^= 1;
+  __syncthreads();
+}
+
+__device__ __forceinline__ double block_max(BaShared& sh, double a) {
+  a = wave_max(a);
+  const int lane = threadIdx.x & 63, w = wave_id();
+  if (lane == 0) sh.red[sh.rb][w][0] = a;
+  __syncthreads();
+  double m = 0.0;
+  for (int k = 0; k < kWaves; k++) m = fmax(m, sh.red[sh.rb][k][0]);
+  __syncthreads();
+  if (threadIdx.x == 0) sh.rb ^= 1;
+  __syncthreads();
+  return m;
+}
+
+// Eigen's 3x3 inverse of a symmetric matrix in packed form (cofactors over the determinant).
+__device__ __forceinline__ void inverse3_sym(const double m[6], double r[6]) {
+  const double a00 = m[0], a01 = m[1], a02 = m[2], a11 = m[3], a12 = m[4], a22 = m[5];
+  const double c00 = a11 * a22 - a12 * a12;
+  const double c10 = a02 * a12 - a01 * a22;
+  const double c20 = a01 * a12 - a02 * a11;
+  const double det = c00 * a00 + c10 * a01 + c20 * a02;
+  const double id = 1.0 / det;
+  r[0] = c00 * id;
+  r[1] = c10 * id;
+  r[2] = c20 * id;
+  r[3] = (a00 * a22 - a02 * a02) * id;
+  r[4] = (a02 * a01 - a00 * a12) * id;
+  r[5] = (a00 * a11 - a01 * a01) * id;
+}
+
+struct Problem {
+  const slamgpu_ba_obs* obs;
+  const int32_t* pstart;  // point's first observation (global)
+  int o0, n_obs, p0, n_pts, k0, n_kf;
+  BaWorkspace ws;
+};
+
+__device__ __forceinline__ double* kfrec(const Problem& pb, int kf) {
+  return pb.ws.kf + (size_t)(pb.k0 + kf) * 64;
+}
+__device__ __forceinline__ double* ptrec(const Problem& pb, int p) {
+  return pb.ws.pt + (size_t)(pb.p0 + p) * 32;
+}
+
+// ---- structure of the active edge set ------------------------------------------------------------
+// Per point: the mask of local keyframes it has active edges to and those edges sorted by local
+// keyframe (psorted). Per S block (kh >= kl): the list of its point pairs in point order, built
+// with wave ballots and prefix counts (no atomics on positions). A diagonal block (k, k) lists
+// (edge, point): it doubles as keyframe k's edge list.
+__device__ void build_structure(BaShared& sh, const Problem& pb) {
+  const int tid = threadIdx.x, lane = tid & 63, w = wave_id(), K = sh.K;
+  const int nblk = K * (K + 1) / 2;
+  for (int b = tid; b < nblk; b += kThreads) {
+    sh.blk_cnt[b] = 0;
+    sh.blk_run[b] = 0;
+  }
+  // per point mask + sorted active free edges
+  for (int p = tid; p < pb.n_pts; p += kThreads) {
+    const int s = pb.pstart[pb.p0 + p] - pb.o0, e1 = pb.pstart[pb.p0 + p + 1] - pb.o0;
+    uint32_t mask = 0;
+    int m = 0;
+    for (int e = s; e < e1; e++) {
+      if (!pb.ws.act[pb.o0 + e]) continue;
+      const int f = sh.free_of_kf[pb.obs[pb.o0 + e].keyframe];
+      if (f < 0) continue;
+      mask |= 1u << f;
+      // insertion by local keyframe index into psorted[s .. s + m)
+      int i = m;
+      while (i > 0) {
+        const int prev = pb.ws.psorted[pb.o0 + s + i - 1];
+        if (sh.free_of_kf[pb.obs[pb.o0 + prev].keyframe] < f) break;
+        pb.ws.psorted[pb.o0 + s + i] = prev;
+        i--;
+      }
+      pb.ws.psorted[pb.o0 + s + i] = e;
+      m++;
+    }
+    pb.ws.pmask[pb.p0 + p] = mask;
+  }
+  __syncthreads();
+  // pass 1: pair counts per block
+  for (int base = 0; base < pb.n_pts; base += kThreads) {
+    const int p = base + tid;
+    const uint32_t mask = p < pb.n_pts ? pb.ws.pmask[pb.p0 + p] : 0u;
+    uint32_t om = 0;
+    for (int k = 0; k < K; k++) om |= __ballot((mask >> k) & 1) ? (1u << k) : 0u;
+    for (uint32_t a = om; a; a &= a - 1) {
+      const int kh = __builtin_ctz(a);
+      for (uint32_t c = om & ((2u << kh) - 1); c; c &= c - 1) {
+        const int kl = __builtin_ctz(c);
+        const uint64_t bal = __ballot(((mask >> kh) & 1) && ((mask >> kl) & 1));
+        if (lane == 0 && bal) atomicAdd(&sh.blk_cnt[tri(kh) + kl], __popcll(bal));
+      }
+    }
+  }
+  __syncthreads();
+  if (tid == 0) {
+    int off = 0;
+    for (int b = 0; b < nblk; b++) {
+      sh.blk_off[b] = off;
+      off += sh.blk_cnt[b];
+    }
+    sh.blk_off[nblk] = off;
+    for (int kh = 0; kh < K; kh++)
+      for (int kl = 0; kl <= kh; kl++) sh.blk_kk[tri(kh) + kl] = kh << 8 | kl;
+  }
+  __syncthreads();
+  // pass 2: positions (block offset + earlier rounds + earlier waves + earlier lanes)
+  int2* hits = pb.ws.hits + (size_t)pb.o0 * kPairsPerObs;
+  for (int base = 0; base < pb.n_pts; base += kThreads) {
+    for (int i = tid; i < kWaves * nblk; i += kThreads) sh.wcnt[i / nblk][i % nblk] = 0;
+    __syncthreads();
+    const int p = base + tid;
+    const uint32_t mask = p < pb.n_pts ? pb.ws.pmask[pb.p0 + p] : 0u;
+    uint32_t om = 0;
+    for (int k = 0; k < K; k++) om |= __ballot((mask >> k) & 1) ? (1u << k) : 0u;
+    for (uint32_t a = om; a; a &= a - 1) {
+      const int kh = __builtin_ctz(a);
+      for (uint32_t c = om & ((2u << kh) - 1); c; c &= c - 1) {
+        const int kl = __builtin_ctz(c);
+        const uint64_t bal = __ballot(((mask >> kh) & 1) && ((mask >> kl) & 1));
+        if (lane == 0) sh.wcnt[w][tri(kh) + kl] = __popcll(bal);
+      }
+    }
+    __syncthreads();
+    for (int b = tid; b < nblk; b += kThreads) {
+      int run = sh.blk_run[b];
+      for (int k = 0; k < kWaves; k++) {
+        const int c = sh.wcnt[k][b];
+        sh.wcnt[k][b] = run;
+        run += c;
+      }
+      sh.blk_run[b] = run;
+    }
+    __syncthreads();
+    const int s = p < pb.n_pts ? pb.pstart[pb.p0 + p] - pb.o0 : 0;
+    for (uint32_t a = om; a; a &= a - 1) {
+      const int kh = __builtin_ctz(a);
+      for (uint32_t c = om & ((2u << kh) - 1); c; c &= c - 1) {
+        const int kl = __builtin_ctz(c);
+        const bool mine = ((mask >> kh) & 1) && ((mask >> kl) & 1);
+        const uint64_t bal = __ballot(mine);
+        if (mine) {
+          const int b = tri(kh) + kl;
+          const int pos = sh.blk_off[b] + sh.wcnt[w][b] + (int)lanes_below(bal);
+          const int eh = pb.ws.psorted[pb.o0 + s + __popc(mask & ((1u << kh) - 1))];
+          const int el = pb.ws.psorted[pb.o0 + s + __popc(mask & ((1u << kl) - 1))];
+          hits[pos] = kh == kl ? make_int2(eh, p) : make_int2(eh, el);
+        }
+      }
+    }
+    __syncthreads();
+  }
+}
+
+// ---- linearisation ------------------------------------------------------------------------------
+// Point pass: errors and chi2 of the active edges (stored: g2o keeps the last error per edge),
+// Hll, bl, Hpl; returns this thread's robust chi2 and max |Hll_jj| partials.
+__device__ void linearise_points(BaShared& sh, const Problem& pb, const PoseParams& P,
+                                 const float* isig, bool robust, double& chi, double& maxd) {
+  for (int p = threadIdx.x; p < pb.n_pts; p += kThreads) {
+    double* pr = ptrec(pb, p);
+    const double X[3] = {pr[PX], pr[PX + 1], pr[PX + 2]};
+    double H[6] = {0, 0, 0, 0, 0, 0}, bl[3] = {0, 0, 0};
+    int nact = 0;
+    const int s = pb.pstart[pb.p0 + p], e1 = pb.pstart[pb.p0 + p + 1];
+    for (int ge = s; ge < e1; ge++) {
+      if (!pb.ws.act[ge]) continue;
+      nact++;
+      const slamgpu_ba_obs o = pb.obs[ge];
+      const double* kr = kfrec(pb, o.keyframe);
+      ObsEval v;
+      const double c2 = eval_obs(o, P, isig, kr, X, v);
+      pb.ws.chi2[ge] = c2;
+      double wgt = 1.0;
+      if (robust) {
+        const double d = huber_delta(v.stereo), d2 = d * d;
+        if (c2 > d2) {
+          const double sq = sqrt(c2);
+          chi += 2 * sq * d - d2;
+          wgt = d / sq;
+        } else {
+          chi += c2;
+        }
+      } else {
+        chi += c2;
+      }
+      double Jl[3][3], Jp[3][6];
+      obs_jacobians(v, P, kr, Jl, Jp);
+      const double W = wgt * v.info;
+      // omega_r = -Omega e * rho' (base_binary_edge.hpp:72-110)
+      const double or0 = -(v.info * v.e[0]) * wgt, or1 = -(v.info * v.e[1]) * wgt,
+                   or2 = -(v.info * v.e[2]) * wgt;
+      for (int i = 0; i < 3; i++) {
+        bl[i] += Jl[0][i] * or0 + Jl[1][i] * or1 + Jl[2][i] * or2;
+        for (int j = i; j < 3; j++)
+          H[s3(i, j)] += (Jl[0][i] * W) * Jl[0][j] + (Jl[1][i] * W) * Jl[1][j] +
+                         (Jl[2][i] * W) * Jl[2][j];
+      }
+      if (sh.free_of_kf[o.keyframe] >= 0) {
+        double* hp = pb.ws.hpl + (size_t)ge * 18;
+        for (int i = 0; i < 6; i++)
+          for (int j = 0; j < 3; j++)
+            hp[3 * i + j] = (Jp[0][i] * W) * Jl[0][j] + (Jp[1][i] * W) * Jl[1][j] +
+                            (Jp[2][i] * W) * Jl[2][j];
+      }
+    }
+    for (int i = 0; i < 6; i++) pr[PH + i] = H[i];
+    for (int i = 0; i < 3; i++) pr[PB + i] = bl[i];
+    if (nact) maxd = fmax(maxd, fmax(fabs(H[0]), fmax(fabs(H[3]), fabs(H[5]))));
+  }
+}
+
+// Keyframe pass: a wave per local keyframe sums Hpp (upper triangle) and bp over its active
+// edges (the diagonal block's pair list, in point order); returns max |Hpp_jj| partials.
+__device__ void linearise_keyframes(BaShared& sh, const Problem& pb, const PoseParams& P,
+                                    const float* isig, bool robust, double& maxd) {
+  const int lane = threadIdx.x & 63, w = wave_id(), K = sh.K;
+  const int2* hits = pb.ws.hits + (size_t)pb.o0 * kPairsPerObs;
+  for (int f = w; f < K; f += kWaves) {
+    const int b = tri(f) + f, cnt = sh.blk_cnt[b], off = sh.blk_off[b];
+    double* kr = kfrec(pb, sh.kf_of_free[f]);
+    double acc[32];
+#pragma unroll
+    for (int i = 0; i < 32; i++) acc[i] = 0.0;
+    for (int h = lane; h < cnt; h += 64) {
+      const int2 ep = hits[off + h];
+      const int ge = pb.o0 + ep.x;
+      const double* pr = ptrec(pb, ep.y);
+      const double X[3] = {pr[PX], pr[PX + 1], pr[PX + 2]};
+      ObsEval v;
+      const double c2 = eval_obs(pb.obs[ge], P, isig, kr, X, v);
+      double wgt = 1.0;
+      if (robust) {
+        const double d = huber_delta(v.stereo);
+        if (c2 > d * d) wgt = d / sqrt(c2);
+      }
+      double Jl[3][3], Jp[3][6];
+      obs_jacobians(v, P, kr, Jl, Jp);
+      const double W = wgt * v.info;
+      const double or0 = -(v.info * v.e[0]) * wgt, or1 = -(v.info * v.e[1]) * wgt,
+                   or2 = -(v.info * v.e[2]) * wgt;
+      int hh = 0;
+#pragma unroll
+      for (int a = 0; a < 6; a++) {
+        acc[21 + a] += Jp[0][a] * or0 + Jp[1][a] * or1 + Jp[2][a] * or2;
+        const double wa0 = Jp[0][a] * W, wa1 = Jp[1][a] * W, wa2 = Jp[2][a] * W;
+#pragma unroll
+        for (int c = a; c < 6; c++, hh++) acc[hh] += wa0 * Jp[0][c] + wa1 * Jp[1][c] + wa2 * Jp[2][c];
+      }
+    }
+    const double s = wave_reduce_scatter32(acc);
+    if ((lane & 1) == 0 && (lane >> 1) < 27) kr[KH + (lane >> 1)] = s;
+    if (cnt > 0) {
+      const bool dg = (lane & 1) == 0 && (lane >> 1) < 21 &&
+                      ((lane >> 1) == 0 || (lane >> 1) == 6 || (lane >> 1) == 11 ||
+                       (lane >> 1) == 15 || (lane >> 1) == 18 || (lane >> 1) == 20);
+      maxd = fmax(maxd, dg ? fabs(s) : 0.0);
+    }
+  }
+}
+
+// ---- one LM trial: Schur solve ------------------------------------------------------------------
+__device__ void schur_points(BaShared& sh, const Problem& pb, double lambda) {
+  for (int p = threadIdx.x; p < pb.n_pts; p += kThreads) {
+    double* pr = ptrec(pb, p);
+    double D[6], Di[6];
+    for (int i = 0; i < 6; i++) D[i] = pr[PH + i];
+    D[0] += lambda;
+    D[3] += lambda;
+    D[5] += lambda;
+    inverse3_sym(D, Di);
+    const double b0 = pr[PB], b1 = pr[PB + 1], b2 = pr[PB + 2];
+    for (int i = 0; i < 6; i++) pr[PD + i] = Di[i];
+    pr[PDB] = Di[0] * b0 + Di[1] * b1 + Di[2] * b2;
+    pr[PDB + 1] = Di[1] * b0 + Di[3] * b1 + Di[4] * b2;
+    pr[PDB + 2] = Di[2] * b0 + Di[4] * b1 + Di[5] * b2;
+    const int s = pb.pstart[pb.p0 + p], e1 = pb.pstart[pb.p0 + p + 1];
+    for (int ge = s; ge < e1; ge++) {
+      if (!pb.ws.act[ge] || sh.free_of_kf[pb.obs[ge].keyframe] < 0) continue;
+      const double* hp = pb.ws.hpl + (size_t)ge * 18;
+      double* bd = pb.ws.bdinv + (size_t)ge * 18;
+      for (int i = 0; i < 6; i++) {
+        const double h0 = hp[3 * i], h1 = hp[3 * i + 1], h2 = hp[3 * i + 2];
+        bd[3 * i] = h0 * Di[0] + h1 * Di[1] + h2 * Di[2];
+        bd[3 * i + 1] = h0 * Di[1] + h1 * Di[3] + h2 * Di[4];
+        bd[3 * i + 2] = h0 * Di[2] + h1 * Di[4] + h2 * Di[5];
+      }
+    }
+  }
+}
+
+__device__ void assemble_S(BaShared& sh, const Problem& pb, double lambda) {
+  const int lane = threadIdx.x & 63, w = wave_id(), K = sh.K, nblk = K * (K + 1) / 2;
+  const int2* hits = pb.ws.hits + (size_t)pb.o0 * kPairsPerObs;
+  for (int b = w; b < nblk; b += kWaves) {
+    const int kh = sh.blk_kk[b] >> 8, kl = sh.blk_kk[b] & 255;
+    const int cnt = sh.blk_cnt[b], off = sh.blk_off[b];
+    const bool diag = kh == kl;
+    const double* kr = kfrec(pb, sh.kf_of_free[kh]);
+    for (int half = 0; half < 2; half++) {
+      double acc[32];
+#pragma unroll
+      for (int i = 0; i < 32; i++) acc[i] = 0.0;
+      for (int h = lane; h < cnt; h += 64) {
+        const int2 ep = hits[off + h];
+        const int eh = pb.o0 + ep.x, el = pb.o0 + (diag ? ep.x : ep.y);
+        const double* bd = pb.ws.bdinv + (size_t)eh * 18 + 9 * half;
+        const double* hp = pb.ws.hpl + (size_t)el * 18;
+        double B[9], Hl[18];
+#pragma unroll
+        for (int i = 0; i < 9; i++) B[i] = bd[i];
+#pragma unroll
+        for (int i = 0; i < 18; i++) Hl[i] = hp[i];
+#pragma unroll
+        for (int r = 0; r < 3; r++)
+#pragma unroll
+          for (int c = 0; c < 6; c++)
+            acc[6 * r + c] += B[3 * r] * Hl[3 * c] + B[3 * r + 1] * Hl[3 * c + 1] +
+                              B[3 * r + 2] * Hl[3 * c + 2];
+      }
+      const double s = wave_reduce_scatter32(acc);
+      const int idx = lane >> 1;
+      if ((lane & 1) == 0 && idx < 18) {
+        const int r = 3 * half + idx / 6, c = idx % 6;
+        const int i = 6 * kh + r, j = 6 * kl + c;
+        if (!diag || j <= i) {
+          double base = 0.0;
+          if (diag) base = kr[KH + hidx(c, r)] + (r == c ? lambda : 0.0);
+          sh.S[sidx(i, j)] = base - s;
+        }
+      }
+    }
+  }
+  // reduced right-hand side: bs_k = bp_k - sum_e Hpl_e db_p
+  for (int f = w; f < K; f += kWaves) {
+    const int b = tri(f) + f, cnt = sh.blk_cnt[b], off = sh.blk_off[b];
+    const double* kr = kfrec(pb, sh.kf_of_free[f]);
+    double acc[32];
+#pragma unroll
+    for (int i = 0; i < 32; i++) acc[i] = 0.0;
+    for (int h = lane; h < cnt; h += 64) {
+      const int2 ep = hits[off + h];
+      const double* hp = pb.ws.hpl + (size_t)(pb.o0 + ep.x) * 18;
+      const double* pr = ptrec(pb, ep.y);
+      const double d0 = pr[PDB], d1 = pr[PDB + 1], d2 = pr[PDB + 2];
+#pragma unroll
+      for (int i = 0; i < 6; i++) acc[i] += hp[3 * i] * d0 + hp[3 * i + 1] * d1 + hp[3 * i + 2] * d2;
+    }
+    const double s = wave_reduce_scatter32(acc);
+    if ((lane & 1) == 0 && (lane >> 1) < 6) sh.rhs[6 * f + (lane >> 1)] = kr[KB + (lane >> 1)] - s;
+  }
+}
+
+// LDLT of S (n = 6K, 6x6 block columns, right-looking) with the forward solve of the rhs fused;
+// then D^-1 and the backward solve by wave 0. Fails (sh.ok = 0) on an exact zero pivot, as
+// Eigen's SimplicialLDLT does. On success sh.xp receives the solution; on failure it keeps the
+// previous one, which g2o applies anyway (optimization_algorithm_levenberg.cpp:107-109).
+__device__ void factor_solve(BaShared& sh) {
+  const int tid = threadIdx.x, lane = tid & 63, K = sh.K, n = 6 * K;
+  if (tid == 0) sh.ok = 1;
+  __syncthreads();
+  for (int J = 0; J < K; J++) {
+    const int j0 = 6 * J;
+    // 1. diagonal block: unblocked LDLT of the 6x6, forward-solve its rhs (one lane)
+    if (tid == 0) {
+      for (int j = j0; j < j0 + 6; j++) {
+        double d = sh.S[sidx(j, j)];
+        for (int k = j0; k < j; k++) d -= sh.S[sidx(j, k)] * sh.S[sidx(j, k)] * sh.dg[k];
+        if (d == 0.0) sh.ok = 0;
+        sh.dg[j] = d;
+        for (int i = j + 1; i < j0 + 6; i++) {
+          double s = sh.S[sidx(i, j)];
+          for (int k = j0; k < j; k++) s -= sh.S[sidx(i, k)] * sh.S[sidx(j, k)] * sh.dg[k];
+          sh.S[sidx(i, j)] = d != 0.0 ? s / d : 0.0;
+        }
+      }
+      for (int i = j0; i < j0 + 6; i++) {
+        double s = sh.rhs[i];
+        for (int k = j0; k < i; k++) s -= sh.S[sidx(i, k)] * sh.rhs[k];
+        sh.rhs[i] = s;
+      }
+    }
+    __syncthreads();
+    if (!sh.ok) return;
+    // 2. panel rows below: V_i = A_iJ L_JJ^-T (so that L_iJ = V_i D_J^-1); rhs_i -= L_iJ y_J
+    for (int i = j0 + 6 + tid; i < n; i += kThreads) {
+      double v[6];
+      for (int c = 0; c < 6; c++) {
+        double s = sh.S[sidx(i, j0 + c)];
+        for (int k = 0; k < c; k++) s -= v[k] * sh.S[sidx(j0 + c, j0 + k)];
+        v[c] = s;
+      }
+      double r = sh.rhs[i];
+      for (int c = 0; c < 6; c++) {
+        sh.V[i][c] = v[c];
+        const double l = v[c] / sh.dg[j0 + c];
+        sh.S[sidx(i, j0 + c)] = l;
+        r -= l * sh.rhs[j0 + c];
+      }
+      sh.rhs[i] = r;
+    }
+    __syncthreads();
+    // 3. trailing update A_ik -= sum_c L_ic D_c L_kc = sum_c L_ic V_kc, j0 + 6 <= k <= i
+    const int m = n - j0 - 6;
+    for (int q = tid; q < m * m; q += kThreads) {
+      const int ii = q / m, kk = q - ii * m;
+      if (kk > ii) continue;
+      const int i = j0 + 6 + ii, k = j0 + 6 + kk;
+      double s = sh.S[sidx(i, k)];
+#pragma unroll
+      for (int c = 0; c < 6; c++) s -= sh.S[sidx(i, j0 + c)] * sh.V[k][c];
+      sh.S[sidx(i, k)] = s;
+    }
+    __syncthreads();
+  }
+  // D^-1, then L^T x = z (wave 0, column-oriented from the last row)
+  if (wave_id() == 0) {
+    for (int i = lane; i < n; i += 64) sh.rhs[i] /= sh.dg[i];
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    for (int k = n - 1; k > 0; k--) {
+      const double xk = sh.rhs[k];
+      for (int i = lane; i < k; i += 64) sh.rhs[i] -= sh.S[sidx(k, i)] * xk;
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    }
+    for (int i = lane; i < n; i += 64) sh.xp[i] = sh.rhs[i];
+  }
+  __syncthreads();
+}
+
+// ---- kernel -----------------------------------------------------------------------------------
+__global__ __launch_bounds__(kThreads) void local_ba_kernel(
+    PoseParams P, const slamgpu_ba_problem* __restrict__ problems, float* __restrict__ kf_Tcw,
+    const uint8_t* __restrict__ kf_mode, float* __restrict__ points,
+    const int32_t* __restrict__ pstart, const slamgpu_ba_obs* __restrict__ obs,
+    uint8_t* __restrict__ erase, int32_t* __restrict__ status, BaWorkspace ws,
+    const int32_t* stop_flag) {
+#pragma clang fp contract(fast)  // tolerance-compared FP64 path
+  __shared__ BaShared sh;
+  __shared__ float isig[SLAMGPU_MAX_LEVELS];
+  const int tid = threadIdx.x;
+  const slamgpu_ba_problem pr = problems[blockIdx.x];
+  Problem pb;
+  pb.obs = obs;
+  pb.pstart = pstart;
+  pb.p0 = pr.point_begin;
+  pb.n_pts = pr.n_points;
+  pb.k0 = pr.kf_begin;
+  pb.n_kf = pr.n_kf;
+  pb.o0 = pstart[pb.p0];
+  pb.n_obs = pstart[pb.p0 + pb.n_pts] - pb.o0;
+  pb.ws = ws;
+  if (tid < SLAMGPU_MAX_LEVELS) isig[tid] = P.inv_sigma2[tid];
+  if (tid == 0) {
+    sh.err = 0;
+    sh.rb = 0;
+    int K = 0;
+    if (pb.n_kf > SLAMGPU_BA_MAX_KF || pb.n_kf < 0) {
+      sh.err = -3;
+    } else {
+      for (int k = 0; k < pb.n_kf; k++) {
+        const bool fr = kf_mode[pb.k0 + k] == SLAMGPU_KF_LOCAL;
+        if (fr && K < kMaxK) sh.kf_of_free[K] = k;
+        sh.free_of_kf[k] = fr ? (int8_t)(K < kMaxK ? K : -1) : (int8_t)-1;
+        K += fr;
+      }
+      if (K > kMaxK) sh.err = -1;
+    }
+    sh.K = K;
+  }
+  __syncthreads();
+  // validation: keyframe indices and one observation per keyframe per point
+  if (sh.err == 0) {
+    for (int p = tid; p < pb.n_pts; p += kThreads) {
+      const int s = pstart[pb.p0 + p], e1 = pstart[pb.p0 + p + 1];
+      for (int e = s; e < e1; e++) {
+        const int k = obs[e].keyframe;
+        if (k < 0 || k >= pb.n_kf) {
+          atomicMin(&sh.err, -3);
+          break;
+        }
+        for (int e2 = s; e2 < e; e2++)
+          if (obs[e2].keyframe == k) atomicMin(&sh.err, -2);
+      }
+    }
+  }
+  __syncthreads();
+  if (sh.err != 0) {
+    if (tid == 0) status[blockIdx.x] = sh.err;
+    return;
+  }
+  if (stop_flag && __atomic_load_n(stop_flag, __ATOMIC_RELAXED)) {  // optimizer.cpp:616-618
+    for (int e = tid; e < pb.n_obs; e += kThreads) erase[pb.o0 + e] = 0;
+    if (tid == 0) status[blockIdx.x] = 0;
+    return;
+  }
+  // initial estimates (Converter::toSE3Quat / toVector3d)
+  for (int k = tid; k < pb.n_kf; k += kThreads) {
+    const float* T = kf_Tcw + (size_t)(pb.k0 + k) * 16;
+    double R[9];
+    SE3 E;
+    for (int i = 0; i < 3; i++) {
+      for (int j = 0; j < 3; j++) R[3 * i + j] = T[4 * i + j];
+      E.t[i] = T[4 * i + 3];
+    }
+    E.r = se3::quat_from_R(R);
+    se3::normalize_rotation(E.r);
+    store_T(kfrec(pb, k), E);
+  }
+  for (int p = tid; p < pb.n_pts; p += kThreads) {
+    double* r = ptrec(pb, p);
+    for (int i = 0; i < 3; i++) r[PX + i] = points[(size_t)(pb.p0 + p) * 3 + i];
+    for (int i = 0; i < 3; i++) r[PXL + i] = 0.0;
+  }
+  for (int e = tid; e < pb.n_obs; e += kThreads) {
+    ws.act[pb.o0 + e] = 1;
+    ws.chi2[pb.o0 + e] = 0.0;
+  }
+  if (tid < kMaxN) sh.xp[tid] = 0.0;
+  __syncthreads();
+
+  const int K = sh.K, n = 6 * K;
+  int lm_total = 0;
+  bool stopped = false;
+  for (int phase = 0; phase < 2 && !stopped; phase++) {
+    const bool robust = phase == 0;
+    const int iterations = phase == 0 ? 5 : 10;
+    build_structure(sh, pb);
+    double lambda = 0.0;
+    int ni = 2, nbad = 0;
+    for (int it = 0; it < iterations; it++) {
+      if (stop_flag && __atomic_load_n(stop_flag, __ATOMIC_RELAXED)) {
+        stopped = true;
+        break;
+      }
+      // ---- linearise: computeActiveErrors + activeRobustChi2 + buildSystem ----
+      double chi = 0.0, maxd = 0.0;
+      linearise_points(sh, pb, P, isig, robust, chi, maxd);
+      linearise_keyframes(sh, pb, P, isig, robust, maxd);
+      __syncthreads();
+      double zero = 0.0;
+      block_sum2(sh, chi, zero);
+      double currentChi = chi;
+      const double iniChi = currentChi;
+      if (it == 0) {  // computeLambdaInit over the active vertices
+        lambda = 1e-5 * block_max(sh, maxd);
+        ni = 2;
+        nbad = 0;
+      }
+      double rho = 0.0;
+      int qmax = 0;
+      do {
+        // ---- solve ----
+        schur_points(sh, pb, lambda);
+        __syncthreads();
+        assemble_S(sh, pb, lambda);
+        __syncthreads();
+        factor_solve(sh);  // ends with a barrier; sh.xp = the pose step when sh.ok
+        const bool ok = sh.ok;
+        // ---- update (backup first): points X += xl, keyframes exp(xp) * T ----
+        double scale = 0.0, temp = 0.0;
+        for (int p = tid; p < pb.n_pts; p += kThreads) {
+          double* r = ptrec(pb, p);
+          const int s = pstart[pb.p0 + p], e1 = pstart[pb.p0 + p + 1];
+          int nact = 0;
+          double c0 = r[PB], c1 = r[PB + 1], c2 = r[PB + 2];
+          for (int ge = s; ge < e1; ge++) {
+            if (!ws.act[ge]) continue;
+            nact++;
+            const int f = sh.free_of_kf[obs[ge].keyframe];
+            if (f < 0 || !ok) continue;
+            const double* hp = ws.hpl + (size_t)ge * 18;
+            for (int i = 0; i < 6; i++) {
+              const double x = sh.xp[6 * f + i];
+              c0 -= hp[3 * i] * x;
+              c1 -= hp[3 * i + 1] * x;
+              c2 -= hp[3 * i + 2] * x;
+            }
+          }
+          if (ok) {  // a failed solve leaves the previous x in place (g2o's _x)
+            r[PXL] = r[PD] * c0 + r[PD + 1] * c1 + r[PD + 2] * c2;
+            r[PXL + 1] = r[PD + 1] * c0 + r[PD + 3] * c1 + r[PD + 4] * c2;
+            r[PXL + 2] = r[PD + 2] * c0 + r[PD + 4] * c1 + r[PD + 5] * c2;
+          }
+          for (int i = 0; i < 3; i++) r[PXB + i] = r[PX + i];
+          if (nact) {  // oplus on the active vertices only
+            for (int i = 0; i < 3; i++) {
+              const double x = r[PXL + i];
+              r[PX + i] += x;
+              scale += x * (lambda * x + r[PB + i]);
+            }
+          }
+        }
+        if (tid < K) {
+          double* kr = kfrec(pb, sh.kf_of_free[tid]);
+          if (sh.blk_cnt[tri(tid) + tid] > 0) {
+            double x[6];
+            for (int i = 0; i < 6; i++) {
+              x[i] = sh.xp[6 * tid + i];
+              scale += x[i] * (lambda * x[i] + kr[KB + i]);
+            }
+            SE3 T;
+            load_T(kr, T);
+            for (int i = 0; i < 4; i++) kr[KBQ + i] = kr[KQ + i];
+            for (int i = 0; i < 3; i++) kr[KBT + i] = kr[KT + i];
+            store_T(kr, se3::se3_left_update(x, T));
+          }
+        }
+        __syncthreads();
+        // ---- errors at the new estimate ----
+        for (int p = tid; p < pb.n_pts; p += kThreads) {
+          const double* r = ptrec(pb, p);
+          const double X[3] = {r[PX], r[PX + 1], r[PX + 2]};
+          const int s = pstart[pb.p0 + p], e1 = pstart[pb.p0 + p + 1];
+          for (int ge = s; ge < e1; ge++) {
+            if (!ws.act[ge]) continue;
+            const slamgpu_ba_obs o = obs[ge];
+            ObsEval v;
+            const double c2 = eval_obs(o, P, isig, kfrec(pb, o.keyframe), X, v);
+            ws.chi2[ge] = c2;
+            if (robust) {
+              const double d = huber_delta(v.stereo), d2 = d * d;
+              temp += c2 > d2 ? 2 * sqrt(c2) * d - d2 : c2;
+            } else {
+              temp += c2;
+            }
+          }
+        }
+        block_sum2(sh, temp, scale);
+        double tempChi = ok ? temp : DBL_MAX;
+        scale += 1e-3;
+        rho = (currentChi - tempChi) / scale;
+        if (rho > 0 && isfinite(tempChi)) {
+          double alpha = 1. - pow(2 * rho - 1, 3.0);
+          alpha = fmin(alpha, 2. / 3.);
+          lambda *= fmax(1. / 3., alpha);
+          ni = 2;
+          currentChi = tempChi;
+        } else {
+          lambda *= ni;
+          ni *= 2;
+          // pop: restore the estimates; the edges keep the rejected errors
+          for (int p = tid; p < pb.n_pts; p += kThreads) {
+            double* r = ptrec(pb, p);
+            for (int i = 0; i < 3; i++) r[PX + i] = r[PXB + i];
+          }
+          if (tid < K) {
+            double* kr = kfrec(pb, sh.kf_of_free[tid]);
+            if (sh.blk_cnt[tri(tid) + tid] > 0) {
+              SE3 T;
+              T.r.x = kr[KBQ];
+              T.r.y = kr[KBQ + 1];
+              T.r.z = kr[KBQ + 2];
+              T.r.w = kr[KBQ + 3];
+              for (int i = 0; i < 3; i++) T.t[i] = kr[KBT + i];
+              store_T(kr, T);
+            }
+          }
+          __syncthreads();
+        }
+        qmax++;
+      } while (rho < 0 && qmax < 10);
+      lm_total++;
+      if (qmax == 10 || rho == 0) break;
+      if ((iniChi - currentChi) * 1e3 < iniChi) nbad++;
+      else nbad = 0;
+      if (nbad >= 3) break;
+    }
+    if (phase == 0) {
+      if (stop_flag && __atomic_load_n(stop_flag, __ATOMIC_RELAXED)) stopped = true;  // do_more
+      if (stopped) break;
+      // optimizer.cpp:632-665: chi2 > threshold or depth <= 0 -> level 1
+      for (int p = tid; p < pb.n_pts; p += kThreads) {
+        const double* r = ptrec(pb, p);
+        const double X[3] = {r[PX], r[PX + 1], r[PX + 2]};
+        const int s = pstart[pb.p0 + p], e1 = pstart[pb.p0 + p + 1];
+        for (int ge = s; ge < e1; ge++) {
+          const slamgpu_ba_obs o = obs[ge];
+          ObsEval v;
+          eval_obs(o, P, isig, kfrec(pb, o.keyframe), X, v);
+          if (ws.chi2[ge] > (o.ur >= 0 ? 7.815 : 5.991) || !(v.z > 0.0)) ws.act[ge] = 0;
+        }
+      }
+      __syncthreads();
+    }
+  }
+  // optimizer.cpp:672-700: erase list over every edge; :702-716 write-back
+  for (int p = tid; p < pb.n_pts; p += kThreads) {
+    const double* r = ptrec(pb, p);
+    const double X[3] = {r[PX], r[PX + 1], r[PX + 2]};
+    const int s = pstart[pb.p0 + p], e1 = pstart[pb.p0 + p + 1];
+    for (int ge = s; ge < e1; ge++) {
+      const slamgpu_ba_obs o = obs[ge];
+      ObsEval v;
+      eval_obs(o, P, isig, kfrec(pb, o.keyframe), X, v);
+      erase[ge] = (ws.chi2[ge] > (o.ur >= 0 ? 7.815 : 5.991) || !(v.z > 0.0)) ? 1 : 0;
+    }
+    for (int i = 0; i < 3; i++) points[(size_t)(pb.p0 + p) * 3 + i] = (float)r[PX + i];
+  }
+  for (int k = tid; k < pb.n_kf; k += kThreads) {
+    if (kf_mode[pb.k0 + k] == SLAMGPU_KF_FIXED) continue;
+    const double* kr = kfrec(pb, k);
+    float* T = kf_Tcw + (size_t)(pb.k0 + k) * 16;
+    for (int i = 0; i < 3; i++) {
+      for (int j = 0; j < 3; j++) T[4 * i + j] = (float)kr[KR + 3 * i + j];
+      T[4 * i + 3] = (float)kr[KT + i];
+    }
+    T[12] = T[13] = T[14] = 0.f;
+    T[15] = 1.f;
+  }
+  if (tid == 0) status[blockIdx.x] = lm_total;
+  (void)n;
+}
+
+}  // namespace
+
+BaWorkspace ba_workspace_layout(void* base, int total_kf, int total_points, int total_obs,
+                                size_t* bytes) {
+  auto al = [](size_t x) { return (x + 255) / 256 * 256; };
+  size_t off = 0;
+  BaWorkspace w{};
+  char* b = static_cast<char*>(base);
+  auto take = [&](size_t n) {
+    char* p = b ? b + off : nullptr;
+    off += al(n);
+    return p;
+  };
+  w.chi2 = reinterpret_cast<double*>(take(sizeof(double) * (size_t)total_obs));
+  w.hpl = reinterpret_cast<double*>(take(sizeof(double) * 18 * (size_t)total_obs));
+  w.bdinv = reinterpret_cast<double*>(take(sizeof(double) * 18 * (size_t)total_obs));
+  w.act = reinterpret_cast<uint8_t*>(take((size_t)total_obs));
+  w.psorted = reinterpret_cast<int32_t*>(take(sizeof(int32_t) * (size_t)total_obs));
+  w.hits = reinterpret_cast<int2*>(take(sizeof(int2) * kPairsPerObs * (size_t)total_obs));
+  w.pt = reinterpret_cast<double*>(take(sizeof(double) * 32 * (size_t)total_points));
+  w.pmask = reinterpret_cast<uint32_t*>(take(sizeof(uint32_t) * (size_t)total_points));
+  w.kf = reinterpret_cast<double*>(take(sizeof(double) * 64 * (size_t)total_kf));
+  if (bytes) *bytes = off + 256;
+  return w;
+}
+
+hipError_t launch_local_ba(const PoseParams& P, const slamgpu_ba_problem* d_problems,
+                           int n_problems, float* d_kf_Tcw, const uint8_t* d_kf_mode,
+                           float* d_points, const int32_t* d_pstart, const slamgpu_ba_obs* d_obs,
+                           uint8_t* d_erase, int32_t* d_status, const BaWorkspace& ws,
+                           const int32_t* d_stop, hipStream_t st) {
+  if (n_problems <= 0) return hipSuccess;
+  SLAMGPU_LAUNCH("local_ba", st, local_ba_kernel, dim3(n_problems), dim3(kThreads), 0, st, P,
+                 d_problems, d_kf_Tcw, d_kf_mode, d_points, d_pstart, d_obs, d_erase, d_status, ws,
+                 d_stop);
+  return hipGetLastError();
+}
+
+}  // namespace slamgpu

@@ -12,6 +12,7 @@
 #include <string>
 
 #include "../../include/slamgpu_optimizer.h"
+#include "ba_kernels.h"
 #include "pose_kernels.h"
 
 using namespace slamgpu;
@@ -51,7 +52,7 @@ int make_params(const slamgpu_camera* cam, const float* inv_sigma2, int nlevels,
   return 0;
 }
 
-// Per-thread staging for the synchronous call: [start offsets | edges | Tcw | outlier | result].
+// Per-thread staging buffer of the synchronous calls (grown on demand).
 struct HostStage {
   int device = -1;
   hipStream_t stream = nullptr;
@@ -63,6 +64,31 @@ struct HostStage {
   }
 };
 thread_local HostStage t_stage;
+
+int stage_reserve(HostStage& S, size_t need) {
+  int dev = 0;
+  OPT_HIPCHECK(hipGetDevice(&dev));
+  if (S.device != dev) {
+    if (S.buf) (void)hipFree(S.buf);
+    if (S.stream) (void)hipStreamDestroy(S.stream);
+    S.buf = nullptr;
+    S.stream = nullptr;
+    S.bytes = 0;
+    OPT_HIPCHECK(hipStreamCreateWithFlags(&S.stream, hipStreamNonBlocking));
+    S.device = dev;
+  }
+  if (need > S.bytes) {
+    if (S.buf) OPT_HIPCHECK(hipFree(S.buf));
+    S.buf = nullptr;
+    S.bytes = 0;
+    const size_t cap = need < (1u << 20) ? (1u << 20) : need;
+    OPT_HIPCHECK(hipMalloc(&S.buf, cap));
+    S.bytes = cap;
+  }
+  return 0;
+}
+
+size_t al256(size_t x) { return (x + 255) / 256 * 256; }
 
 }  // namespace
 
@@ -98,29 +124,10 @@ int slamgpu_pose_optimization(const slamgpu_camera* cam, const float* inv_sigma2
   for (int i = 0; i < n; i++)
     if (edges[i].octave < 0 || edges[i].octave >= nlevels)
       return fail(SLAMGPU_EINVAL, "edge %d: octave %d outside [0, %d)", i, edges[i].octave, nlevels);
-  int dev = 0;
-  OPT_HIPCHECK(hipGetDevice(&dev));
   HostStage& S = t_stage;
-  if (S.device != dev) {
-    if (S.buf) (void)hipFree(S.buf);
-    if (S.stream) (void)hipStreamDestroy(S.stream);
-    S.buf = nullptr;
-    S.stream = nullptr;
-    S.bytes = 0;
-    OPT_HIPCHECK(hipStreamCreateWithFlags(&S.stream, hipStreamNonBlocking));
-    S.device = dev;
-  }
-  const size_t off_e = 256, off_T = off_e + ((size_t)n * sizeof(slamgpu_pose_edge) + 255) / 256 * 256;
-  const size_t off_o = off_T + 256, off_r = off_o + ((size_t)n + 255) / 256 * 256;
-  const size_t need = off_r + 256;
-  if (need > S.bytes) {
-    if (S.buf) OPT_HIPCHECK(hipFree(S.buf));
-    S.buf = nullptr;
-    S.bytes = 0;
-    const size_t cap = need < (1u << 20) ? (1u << 20) : need;
-    OPT_HIPCHECK(hipMalloc(&S.buf, cap));
-    S.bytes = cap;
-  }
+  const size_t off_e = 256, off_T = off_e + al256((size_t)n * sizeof(slamgpu_pose_edge));
+  const size_t off_o = off_T + 256, off_r = off_o + al256((size_t)n);
+  if (int r = stage_reserve(S, off_r + 256)) return r;
   char* b = static_cast<char*>(S.buf);
   const int32_t start[2] = {0, n};
   OPT_HIPCHECK(hipMemcpyAsync(b, start, sizeof(start), hipMemcpyHostToDevice, S.stream));
@@ -139,6 +146,119 @@ int slamgpu_pose_optimization(const slamgpu_camera* cam, const float* inv_sigma2
     OPT_HIPCHECK(hipMemcpyAsync(outlier, b + off_o, n, hipMemcpyDeviceToHost, S.stream));
   OPT_HIPCHECK(hipStreamSynchronize(S.stream));
   *n_inliers = res;
+  return 0;
+}
+
+size_t slamgpu_local_ba_workspace_bytes(int total_kf, int total_points, int total_obs) {
+  size_t bytes = 0;
+  ba_workspace_layout(nullptr, total_kf < 0 ? 0 : total_kf, total_points < 0 ? 0 : total_points,
+                      total_obs < 0 ? 0 : total_obs, &bytes);
+  return bytes;
+}
+
+int slamgpu_local_bundle_adjustment_device(
+    const slamgpu_camera* cam, const float* inv_sigma2, int nlevels,
+    const slamgpu_ba_problem* d_problems, int n_problems, float* d_kf_Tcw,
+    const uint8_t* d_kf_mode, float* d_points, const int32_t* d_point_obs_start,
+    const slamgpu_ba_obs* d_obs, uint8_t* d_erase, int32_t* d_status, void* d_workspace,
+    size_t workspace_bytes, int total_kf, int total_points, int total_obs,
+    const int32_t* d_stop_flag, void* stream) {
+  PoseParams P;
+  if (int r = make_params(cam, inv_sigma2, nlevels, &P)) return r;
+  if (n_problems < 0 || total_kf < 0 || total_points < 0 || total_obs < 0)
+    return fail(SLAMGPU_EINVAL, "negative sizes");
+  if (n_problems == 0) return 0;
+  if (!d_problems || !d_kf_Tcw || !d_kf_mode || !d_point_obs_start || !d_status ||
+      (total_points > 0 && !d_points) || (total_obs > 0 && (!d_obs || !d_erase)))
+    return fail(SLAMGPU_EINVAL, "null device buffer");
+  size_t need = 0;
+  ba_workspace_layout(nullptr, total_kf, total_points, total_obs, &need);
+  if (!d_workspace || workspace_bytes < need)
+    return fail(SLAMGPU_ECAP, "workspace of %zu bytes < %zu needed", workspace_bytes, need);
+  const BaWorkspace ws = ba_workspace_layout(d_workspace, total_kf, total_points, total_obs, nullptr);
+  OPT_HIPCHECK(launch_local_ba(P, d_problems, n_problems, d_kf_Tcw, d_kf_mode, d_points,
+                               d_point_obs_start, d_obs, d_erase, d_status, ws, d_stop_flag,
+                               static_cast<hipStream_t>(stream)));
+  return 0;
+}
+
+int slamgpu_local_bundle_adjustment(const slamgpu_camera* cam, const float* inv_sigma2,
+                                    int nlevels, float* kf_Tcw, const uint8_t* kf_mode, int n_kf,
+                                    float* points, int n_points, const int32_t* point_obs_start,
+                                    const slamgpu_ba_obs* obs, const int* stop_flag,
+                                    uint8_t* erase, int* lm_iterations) {
+  PoseParams P;
+  if (int r = make_params(cam, inv_sigma2, nlevels, &P)) return r;
+  if (lm_iterations) *lm_iterations = 0;
+  if (n_kf < 0 || n_points < 0 || !kf_Tcw || !kf_mode || !point_obs_start || (n_points && !points))
+    return fail(SLAMGPU_EINVAL, "bad arguments");
+  if (point_obs_start[0] != 0) return fail(SLAMGPU_EINVAL, "point_obs_start[0] must be 0");
+  const int n_obs = point_obs_start[n_points];
+  if (n_obs < 0 || (n_obs > 0 && (!obs || !erase))) return fail(SLAMGPU_EINVAL, "bad observations");
+  if (n_kf > SLAMGPU_BA_MAX_KF)
+    return fail(SLAMGPU_ECAP, "%d keyframes > SLAMGPU_BA_MAX_KF (%d)", n_kf, SLAMGPU_BA_MAX_KF);
+  int n_local = 0;
+  for (int k = 0; k < n_kf; k++) {
+    if (kf_mode[k] > SLAMGPU_KF_FIXED) return fail(SLAMGPU_EINVAL, "kf_mode[%d] = %d", k, kf_mode[k]);
+    n_local += kf_mode[k] == SLAMGPU_KF_LOCAL;
+  }
+  if (n_local > SLAMGPU_BA_MAX_LOCAL_KF)
+    return fail(SLAMGPU_ECAP, "%d local keyframes > SLAMGPU_BA_MAX_LOCAL_KF (%d)", n_local,
+                SLAMGPU_BA_MAX_LOCAL_KF);
+  for (int p = 0; p < n_points; p++)
+    if (point_obs_start[p + 1] < point_obs_start[p])
+      return fail(SLAMGPU_EINVAL, "point_obs_start not monotone at %d", p);
+  for (int e = 0; e < n_obs; e++) {
+    if (obs[e].keyframe < 0 || obs[e].keyframe >= n_kf)
+      return fail(SLAMGPU_EINVAL, "observation %d: keyframe %d outside [0, %d)", e, obs[e].keyframe, n_kf);
+    if (obs[e].octave < 0 || obs[e].octave >= nlevels)
+      return fail(SLAMGPU_EINVAL, "observation %d: octave %d outside [0, %d)", e, obs[e].octave, nlevels);
+  }
+  if (stop_flag && *stop_flag) {  // optimizer.cpp:616-618: return before optimising
+    for (int e = 0; e < n_obs; e++) erase[e] = 0;
+    return 0;
+  }
+  size_t wsb = 0;
+  ba_workspace_layout(nullptr, n_kf, n_points, n_obs, &wsb);
+  const size_t o_prob = 0, o_T = 256, o_mode = o_T + al256(64 * (size_t)n_kf);
+  const size_t o_pts = o_mode + al256(n_kf), o_ps = o_pts + al256(12 * (size_t)n_points);
+  const size_t o_obs = o_ps + al256(4 * ((size_t)n_points + 1));
+  const size_t o_er = o_obs + al256(sizeof(slamgpu_ba_obs) * (size_t)n_obs);
+  const size_t o_st = o_er + al256((size_t)n_obs), o_ws = o_st + 256;
+  HostStage& S = t_stage;
+  if (int r = stage_reserve(S, o_ws + wsb)) return r;
+  char* b = static_cast<char*>(S.buf);
+  const slamgpu_ba_problem prob = {0, n_kf, 0, n_points};
+  OPT_HIPCHECK(hipMemcpyAsync(b + o_prob, &prob, sizeof(prob), hipMemcpyHostToDevice, S.stream));
+  OPT_HIPCHECK(hipMemcpyAsync(b + o_T, kf_Tcw, 64 * (size_t)n_kf, hipMemcpyHostToDevice, S.stream));
+  OPT_HIPCHECK(hipMemcpyAsync(b + o_mode, kf_mode, n_kf, hipMemcpyHostToDevice, S.stream));
+  if (n_points)
+    OPT_HIPCHECK(hipMemcpyAsync(b + o_pts, points, 12 * (size_t)n_points, hipMemcpyHostToDevice, S.stream));
+  OPT_HIPCHECK(hipMemcpyAsync(b + o_ps, point_obs_start, 4 * ((size_t)n_points + 1),
+                              hipMemcpyHostToDevice, S.stream));
+  if (n_obs)
+    OPT_HIPCHECK(hipMemcpyAsync(b + o_obs, obs, sizeof(slamgpu_ba_obs) * (size_t)n_obs,
+                                hipMemcpyHostToDevice, S.stream));
+  const BaWorkspace ws = ba_workspace_layout(b + o_ws, n_kf, n_points, n_obs, nullptr);
+  OPT_HIPCHECK(launch_local_ba(P, reinterpret_cast<slamgpu_ba_problem*>(b + o_prob), 1,
+                               reinterpret_cast<float*>(b + o_T), reinterpret_cast<uint8_t*>(b + o_mode),
+                               reinterpret_cast<float*>(b + o_pts), reinterpret_cast<int32_t*>(b + o_ps),
+                               reinterpret_cast<slamgpu_ba_obs*>(b + o_obs),
+                               reinterpret_cast<uint8_t*>(b + o_er), reinterpret_cast<int32_t*>(b + o_st),
+                               ws, nullptr, S.stream));
+  int32_t st = 0;
+  OPT_HIPCHECK(hipMemcpyAsync(&st, b + o_st, 4, hipMemcpyDeviceToHost, S.stream));
+  OPT_HIPCHECK(hipStreamSynchronize(S.stream));
+  if (st < 0) {
+    if (st == -2) return fail(SLAMGPU_EINVAL, "a map point is observed twice by one keyframe");
+    return fail(SLAMGPU_EDEVICE, "local BA kernel status %d", st);
+  }
+  OPT_HIPCHECK(hipMemcpyAsync(kf_Tcw, b + o_T, 64 * (size_t)n_kf, hipMemcpyDeviceToHost, S.stream));
+  if (n_points)
+    OPT_HIPCHECK(hipMemcpyAsync(points, b + o_pts, 12 * (size_t)n_points, hipMemcpyDeviceToHost, S.stream));
+  if (n_obs) OPT_HIPCHECK(hipMemcpyAsync(erase, b + o_er, n_obs, hipMemcpyDeviceToHost, S.stream));
+  OPT_HIPCHECK(hipStreamSynchronize(S.stream));
+  if (lm_iterations) *lm_iterations = st;
   return 0;
 }
 

@@ -36,6 +36,9 @@ MPS_QUERY_DTYPE = np.dtype([("proj_x", "<f4"), ("proj_y", "<f4"), ("proj_xr", "<
 POSE_EDGE_DTYPE = np.dtype([("xw", "<f4", (3,)), ("u", "<f4"), ("v", "<f4"), ("ur", "<f4"),
                             ("octave", "<i4")])
 POSE_MAX_EDGES = 4096
+# slamgpu_ba_obs (include/slamgpu_optimizer.h): one LocalBundleAdjustment observation.
+BA_OBS_DTYPE = np.dtype([("keyframe", "<i4"), ("u", "<f4"), ("v", "<f4"), ("ur", "<f4"),
+                         ("octave", "<i4")])
 assert KP_DTYPE.itemsize == 28 and F2F_QUERY_DTYPE.itemsize == 64 and POSE_EDGE_DTYPE.itemsize == 28
 assert F2F_POSE_DTYPE.itemsize == 72 and MPS_QUERY_DTYPE.itemsize == 80
 
@@ -49,7 +52,8 @@ EXPORTS = [
     "slamgpu_search_by_projection_mps_device", "slamgpu_debug_level_keys",
     "slamgpu_make_vo_queries_device", "slamgpu_timing_start", "slamgpu_timing_stop",
     "slamgpu_timing_read", "slamgpu_pose_optimization", "slamgpu_pose_optimization_device",
-    "slamgpu_optimizer_last_error",
+    "slamgpu_optimizer_last_error", "slamgpu_local_bundle_adjustment",
+    "slamgpu_local_bundle_adjustment_device", "slamgpu_local_ba_workspace_bytes",
 ]
 
 
@@ -123,6 +127,13 @@ def lib():
                                                 C.POINTER(ip)]
         L.slamgpu_pose_optimization_device.argtypes = [C.POINTER(Camera), vp, ip, vp, vp, ip, vp,
                                                        vp, vp, vp, vp]
+        L.slamgpu_local_bundle_adjustment.argtypes = [C.POINTER(Camera), vp, ip, vp, vp, ip, vp,
+                                                      ip, vp, vp, vp, vp, C.POINTER(ip)]
+        L.slamgpu_local_ba_workspace_bytes.argtypes = [ip, ip, ip]
+        L.slamgpu_local_ba_workspace_bytes.restype = sz
+        L.slamgpu_local_bundle_adjustment_device.argtypes = [
+            C.POINTER(Camera), vp, ip, vp, ip, vp, vp, vp, vp, vp, vp, vp, vp, sz, ip, ip, ip, vp,
+            vp]
         L.slamgpu_optimizer_last_error.argtypes = []
         L.slamgpu_optimizer_last_error.restype = C.c_char_p
         _lib = L
@@ -387,6 +398,28 @@ class Optimizer:
                                                    C.byref(n_inl)))
         return n_inl.value, T, outl.astype(bool)
 
+    @staticmethod
+    def LocalBundleAdjustment(kf_Tcw, kf_mode, points, point_obs_start, obs, cam, inv_sigma2,
+                              stop_flag=False):
+        """Optimizer::LocalBundleAdjustment (optimizer.cpp:413-716) on the gathered graph.
+        kf_mode per keyframe: 0 local, 1 local fixed (id 0), 2 fixed camera; observations
+        grouped by point (CSR point_obs_start). Returns (kf_Tcw', points', erase,
+        lm_iterations); erase marks the reference's vToErase observations."""
+        kf = np.ascontiguousarray(np.asarray(kf_Tcw, np.float32).reshape(-1, 4, 4)).copy()
+        mode = np.ascontiguousarray(kf_mode, np.uint8)
+        pts = np.ascontiguousarray(np.asarray(points, np.float32).reshape(-1, 3)).copy()
+        start = np.ascontiguousarray(point_obs_start, np.int32)
+        ob = np.ascontiguousarray(obs, dtype=BA_OBS_DTYPE)
+        isig = np.ascontiguousarray(inv_sigma2, np.float32)
+        erase = np.zeros(max(len(ob), 1), np.uint8)
+        its = C.c_int()
+        stop = C.c_int(1 if stop_flag else 0)
+        _opt_check(lib().slamgpu_local_bundle_adjustment(
+            C.byref(Camera(*cam)), _ptr(isig), len(isig), _ptr(kf), _ptr(mode), len(mode),
+            _ptr(pts), len(pts), _ptr(start), _ptr(ob), C.byref(stop), _ptr(erase),
+            C.byref(its)))
+        return kf, pts, erase[:len(ob)].astype(bool), its.value
+
 
 def pose_optimization_device(cam, inv_sigma2, d_edges, d_edge_start, n_frames, d_Tcw, d_outlier,
                              d_n_inliers, d_lm_iterations=None, stream=None):
@@ -396,3 +429,21 @@ def pose_optimization_device(cam, inv_sigma2, d_edges, d_edge_start, n_frames, d
         C.byref(Camera(*cam)), _ptr(isig), len(isig), _ptr(d_edges), _ptr(d_edge_start), n_frames,
         _ptr(d_Tcw), _ptr(d_outlier), _ptr(d_n_inliers), _ptr(d_lm_iterations),
         C.c_void_p(stream) if stream else None))
+
+
+def local_ba_workspace_bytes(total_kf, total_points, total_obs):
+    return int(lib().slamgpu_local_ba_workspace_bytes(total_kf, total_points, total_obs))
+
+
+def local_bundle_adjustment_device(cam, inv_sigma2, d_problems, n_problems, d_kf_Tcw, d_kf_mode,
+                                   d_points, d_point_obs_start, d_obs, d_erase, d_status,
+                                   d_workspace, total_kf, total_points, total_obs,
+                                   d_stop_flag=None, stream=None):
+    """slamgpu_local_bundle_adjustment_device: LocalBundleAdjustment for a batch of problems."""
+    isig = np.ascontiguousarray(inv_sigma2, np.float32)
+    _opt_check(lib().slamgpu_local_bundle_adjustment_device(
+        C.byref(Camera(*cam)), _ptr(isig), len(isig), _ptr(d_problems), n_problems,
+        _ptr(d_kf_Tcw), _ptr(d_kf_mode), _ptr(d_points), _ptr(d_point_obs_start), _ptr(d_obs),
+        _ptr(d_erase), _ptr(d_status), _ptr(d_workspace),
+        int(d_workspace.numel() * d_workspace.element_size()), total_kf, total_points, total_obs,
+        _ptr(d_stop_flag), C.c_void_p(stream) if stream else None))

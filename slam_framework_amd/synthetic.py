@@ -182,3 +182,96 @@ def pose_batch(seed: int, n_frames: int, n: int = 2000, **kw):
     start[1:] = np.cumsum([len(p[0]) for p in probs])
     poses = np.stack([p[1] for p in probs])
     return edges, start, poses, probs[0][3], probs
+
+
+def ba_problem(seed: int, n_local: int = 20, n_fixed: int = 6, n_points: int = 3000,
+               max_obs: int = 6, stereo_frac: float = 0.6, outlier_frac: float = 0.05,
+               noise_px: float = 0.7, rot_err: float = 0.003, trans_err: float = 0.03,
+               point_err: float = 0.05, first_local_fixed: bool = False, cam=KITTI_CAM,
+               cols: int = KITTI_COLS, rows: int = KITTI_ROWS, nlevels: int = 8,
+               scale_factor: float = 1.2):
+    """One LocalBundleAdjustment input (configs[4]: 20 keyframes x 3000 map points).
+
+    A KITTI-like drive: keyframe k sits 1.2 m further along z with a slow yaw. The n_fixed
+    oldest keyframes are fixed cameras (kf_mode 2), the n_local newest the local window
+    (kf_mode 0; the first one 1 = local but fixed, like keyframe id 0, if first_local_fixed).
+    Each map point lies ahead of the window and is observed by 2..max_obs keyframes that see it
+    inside the image at depth (1, 60) m, with at least one local keyframe among them, in random
+    order (the reference iterates a std::map keyed by KeyFrame*); observations carry
+    octave-scaled pixel noise, stereo_frac of them a right coordinate, outlier_frac are gross
+    mismatches. The local poses and the points start perturbed (rot_err rad, trans_err m,
+    point_err m). Returns a dict of the arrays the device call takes plus the ground truth."""
+    rng = np.random.default_rng(seed)
+    fx, fy, cx, cy, bf = cam
+    n_kf = n_fixed + n_local
+    Rs, cs = [], []
+    for k in range(n_kf):
+        yaw = 0.01 * k
+        R_wc = _rodrigues(np.array([0.0, yaw, 0.0]))
+        c = np.array([3.0 * np.sin(0.01 * k), 0.0, 1.2 * k])
+        Rs.append(R_wc.T)  # Rcw
+        cs.append(c)
+    T_true = np.zeros((n_kf, 4, 4))
+    for k in range(n_kf):
+        T_true[k, :3, :3] = Rs[k]
+        T_true[k, :3, 3] = -Rs[k] @ cs[k]
+        T_true[k, 3, 3] = 1.0
+    mode = np.full(n_kf, 2, np.uint8)
+    mode[n_fixed:] = 0
+    if first_local_fixed:
+        mode[n_fixed] = 1
+    local = np.nonzero(mode != 2)[0]
+    pts, obs_lists = [], []
+    z0, z1 = cs[n_fixed][2] + 2.0, cs[-1][2] + 45.0
+    while len(pts) < n_points:
+        X = np.array([rng.uniform(-25, 25), rng.uniform(-4, 3), rng.uniform(z0, z1)])
+        seen = []
+        for k in range(n_kf):
+            Xc = T_true[k, :3, :3] @ X + T_true[k, :3, 3]
+            if not (1.0 < Xc[2] < 60.0):
+                continue
+            u, v = fx * Xc[0] / Xc[2] + cx, fy * Xc[1] / Xc[2] + cy
+            if 0 <= u < cols and 0 <= v < rows:
+                seen.append(k)
+        if len(seen) < 2 or not any(mode[k] == 0 for k in seen):
+            continue
+        m = int(rng.integers(2, max_obs + 1))
+        if len(seen) > m:
+            loc = [k for k in seen if mode[k] == 0]
+            first = int(rng.choice(loc))
+            rest = [k for k in seen if k != first]
+            seen = [first] + list(rng.choice(rest, m - 1, replace=False))
+        rng.shuffle(seen)
+        pts.append(X)
+        obs_lists.append(seen)
+    from .slamgpu import BA_OBS_DTYPE
+    n_obs = sum(len(o) for o in obs_lists)
+    obs = np.zeros(n_obs, BA_OBS_DTYPE)
+    start = np.zeros(n_points + 1, np.int32)
+    i = 0
+    for p, (X, ks) in enumerate(zip(pts, obs_lists)):
+        start[p] = i
+        for k in ks:
+            Xc = T_true[k, :3, :3] @ X + T_true[k, :3, 3]
+            u, v = fx * Xc[0] / Xc[2] + cx, fy * Xc[1] / Xc[2] + cy
+            octv = min(int(rng.geometric(0.45)) - 1, nlevels - 1)
+            sig = noise_px * scale_factor ** octv
+            uo, vo = u + rng.normal(0, sig), v + rng.normal(0, sig)
+            stereo = rng.uniform() < stereo_frac
+            uro = u - bf / Xc[2] + rng.normal(0, sig) if stereo else -1.0
+            if rng.uniform() < outlier_frac:
+                uo, vo = rng.uniform(0, cols), rng.uniform(0, rows)
+                if stereo:
+                    uro = max(uo - rng.uniform(0, 90), 0.0)
+            obs[i] = (k, uo, vo, uro, octv)
+            i += 1
+    start[n_points] = i
+    kf = T_true.copy()
+    for k in np.nonzero(mode == 0)[0]:
+        kf[k, :3, :3] = _rodrigues(rng.normal(0, rot_err / np.sqrt(3), 3)) @ kf[k, :3, :3]
+        kf[k, :3, 3] += rng.normal(0, trans_err / np.sqrt(3), 3)
+    P = np.array(pts) + rng.normal(0, point_err / np.sqrt(3), (n_points, 3))
+    return {"kf_Tcw": kf.astype(np.float32), "kf_mode": mode, "points": P.astype(np.float32),
+            "point_obs_start": start, "obs": obs,
+            "inv_sigma2": level_inv_sigma2(scale_factor, nlevels),
+            "kf_true": T_true, "points_true": np.array(pts)}

@@ -289,3 +289,50 @@ def pose_edge_eval(cam, R, t, edge, inv_sigma2):
     c = _pose_lib().oc_pose_edge_eval(ptr(cam), ptr(R), ptr(t), ptr(e1), float(inv_sigma2),
                                       ptr(err), ptr(J))
     return c, err, J.reshape(3, 6)
+
+
+# ---- LocalBundleAdjustment (oracle/ba_oracle.c) -------------------------------------------
+BA_OBS_DTYPE = np.dtype([("keyframe", "<i4"), ("u", "<f4"), ("v", "<f4"), ("ur", "<f4"),
+                         ("octave", "<i4")])
+
+
+def _ba_lib():
+    L = lib()
+    if not getattr(L, "_ba_bound", False):
+        vp, ip = C.c_void_p, C.c_int
+        L.oc_local_bundle_adjustment.argtypes = [vp, vp, vp, vp, ip, vp, ip, vp, vp, vp,
+                                                 C.POINTER(ip)]
+        L.oc_ba_edge_eval.argtypes = [vp, vp, vp, vp, vp, C.c_float, vp, vp, vp]
+        L.oc_ba_edge_eval.restype = C.c_double
+        L._ba_bound = True
+    return L
+
+
+def local_ba(cam, prob):
+    """Optimizer::LocalBundleAdjustment restated on a synthetic.ba_problem dict. Returns
+    (kf_Tcw', points', erase, lm_iterations)."""
+    cam = np.asarray(cam, np.float32)
+    kf = np.ascontiguousarray(prob["kf_Tcw"], np.float32).copy()
+    pts = np.ascontiguousarray(prob["points"], np.float32).copy()
+    mode = np.ascontiguousarray(prob["kf_mode"], np.uint8)
+    start = np.ascontiguousarray(prob["point_obs_start"], np.int32)
+    obs = np.ascontiguousarray(prob["obs"]).view(BA_OBS_DTYPE)
+    isig = np.ascontiguousarray(prob["inv_sigma2"], np.float32)
+    erase = np.zeros(max(len(obs), 1), np.uint8)
+    it = C.c_int()
+    r = _ba_lib().oc_local_bundle_adjustment(ptr(cam), ptr(isig), ptr(kf), ptr(mode), len(mode),
+                                             ptr(pts), len(pts), ptr(start), ptr(obs),
+                                             ptr(erase), C.byref(it))
+    assert r == 0
+    return kf, pts, erase[:len(obs)].astype(bool), it.value
+
+
+def ba_edge_eval(cam, R, t, X, ob, inv_sigma2):
+    """(chi2, error[3], Jl[3, 3], Jp[3, 6]) of one binary edge."""
+    cam = np.asarray(cam, np.float32)
+    R, t, X = (np.ascontiguousarray(a, np.float64) for a in (R, t, X))
+    o1 = np.ascontiguousarray(np.asarray(ob).reshape(1)).view(BA_OBS_DTYPE)
+    err, Jl, Jp = np.zeros(3), np.zeros(9), np.zeros(18)
+    c = _ba_lib().oc_ba_edge_eval(ptr(cam), ptr(R), ptr(t), ptr(X), ptr(o1), float(inv_sigma2),
+                                  ptr(err), ptr(Jl), ptr(Jp))
+    return c, err, Jl.reshape(3, 3), Jp.reshape(3, 6)

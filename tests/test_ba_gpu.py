@@ -1,0 +1,121 @@
+"""Device LocalBundleAdjustment (slam_framework_amd/csrc/ba_kernels.hip) against the oracle.
+
+Tolerance (north star: "local-BA poses within 1e-5 of reference"): the device sums the normal
+equations in trees and solves the reduced camera system by a blocked LDLT, the oracle sums in
+edge order with an unblocked one, so they agree to rounding. An element of an optimised pose or
+point may differ from the oracle's by 1e-5 x |its largest delta over the problem| + 4 f32 ulps of
+the element. The erase flags must be identical.
+
+Through the C ABI: slamgpu_local_bundle_adjustment (the per-call drop-in) and
+slamgpu_local_bundle_adjustment_device (a batch of problems, inputs in HBM)."""
+import numpy as np
+import pytest
+
+from slam_framework_amd import synthetic as S
+
+pytestmark = pytest.mark.gpu
+CAM = S.KITTI_CAM
+EPS32 = np.finfo(np.float32).eps
+
+
+def assert_close(A, A_ref, A0, what):
+    A, A_ref, A0 = (np.asarray(a, np.float64) for a in (A, A_ref, A0))
+    delta = np.abs(A_ref - A0).max()
+    tol = 1e-5 * delta + 4 * EPS32 * np.maximum(np.abs(A_ref), 1.0)
+    err = np.abs(A - A_ref)
+    assert (err <= tol).all(), f"{what}: max err {err.max():.3g} (delta {delta:.3g})"
+
+
+def run_host(G, P, stop=False):
+    return G.Optimizer.LocalBundleAdjustment(P["kf_Tcw"], P["kf_mode"], P["points"],
+                                             P["point_obs_start"], P["obs"], CAM,
+                                             P["inv_sigma2"], stop_flag=stop)
+
+
+CASES = [  # (seed, n_local, n_fixed, n_points, stereo_frac, outlier_frac, first_local_fixed)
+    (1, 6, 2, 300, 0.6, 0.05, False),
+    (2, 10, 4, 1000, 0.0, 0.05, False),
+    (3, 10, 4, 1000, 1.0, 0.05, True),
+    (4, 20, 6, 3000, 0.6, 0.05, False),
+    (5, 24, 3, 1500, 0.5, 0.10, False),
+]
+
+
+@pytest.mark.parametrize("seed,nl,nf,npt,sf,of,lf", CASES)
+def test_local_ba_host_matches_oracle(oracle, gpu_lib, seed, nl, nf, npt, sf, of, lf):
+    P = S.ba_problem(seed, n_local=nl, n_fixed=nf, n_points=npt, stereo_frac=sf,
+                     outlier_frac=of, first_local_fixed=lf)
+    kf_o, pts_o, er_o, its_o = oracle.local_ba(CAM, P)
+    kf, pts, er, its = run_host(gpu_lib, P)
+    assert np.array_equal(er, er_o), f"{(er != er_o).sum()} erase flags differ"
+    assert_close(kf, kf_o, P["kf_Tcw"], "keyframe poses")
+    assert_close(pts, pts_o, P["points"], "points")
+    fixed = P["kf_mode"] == 2
+    assert np.array_equal(kf[fixed], P["kf_Tcw"][fixed])
+    assert its > 0
+
+
+def test_local_ba_stop_flag_leaves_inputs(gpu_lib):
+    P = S.ba_problem(7, n_local=4, n_fixed=1, n_points=100)
+    kf, pts, er, its = run_host(gpu_lib, P, stop=True)
+    assert its == 0 and not er.any()
+    assert np.array_equal(kf, P["kf_Tcw"]) and np.array_equal(pts, P["points"])
+
+
+def test_local_ba_rejects_bad_graphs(gpu_lib):
+    P = S.ba_problem(8, n_local=25, n_fixed=1, n_points=200)
+    with pytest.raises(gpu_lib.SlamGpuError):
+        run_host(gpu_lib, P)
+    P = S.ba_problem(9, n_local=4, n_fixed=1, n_points=50)
+    st = P["point_obs_start"]
+    P["obs"]["keyframe"][st[3] + 1] = P["obs"]["keyframe"][st[3]]  # point 3 seen twice by a KF
+    with pytest.raises(gpu_lib.SlamGpuError):
+        run_host(gpu_lib, P)
+
+
+def test_local_ba_device_batch_matches_oracle(oracle, gpu_lib):
+    import torch
+
+    G = gpu_lib
+    probs = [S.ba_problem(20 + i, n_local=nl, n_fixed=nf, n_points=npt, stereo_frac=sf)
+             for i, (nl, nf, npt, sf) in enumerate([(20, 6, 3000, 0.6), (5, 2, 200, 0.3),
+                                                    (12, 0, 800, 1.0), (1, 3, 50, 0.5),
+                                                    (24, 4, 2000, 0.6)])]
+    B = len(probs)
+    kf = np.concatenate([p["kf_Tcw"] for p in probs])
+    mode = np.concatenate([p["kf_mode"] for p in probs])
+    pts = np.concatenate([p["points"] for p in probs])
+    obs = np.concatenate([p["obs"] for p in probs])
+    desc = np.zeros((B, 4), np.int32)
+    starts, ko, po, oo = [], 0, 0, 0
+    for i, p in enumerate(probs):
+        desc[i] = (ko, len(p["kf_mode"]), po, len(p["points"]))
+        starts.append(p["point_obs_start"][:-1] + oo)
+        ko += len(p["kf_mode"])
+        po += len(p["points"])
+        oo += len(p["obs"])
+    start = np.concatenate(starts + [np.array([oo], np.int32)]).astype(np.int32)
+    dev = torch.device("cuda", 0)
+    st = torch.cuda.Stream(device=dev)
+    wsb = G.local_ba_workspace_bytes(ko, po, oo)
+    with torch.cuda.stream(st):
+        d = {k: torch.from_numpy(np.ascontiguousarray(v).view(np.uint8).copy()).to(dev)
+             for k, v in dict(desc=desc, kf=kf, mode=mode, pts=pts, start=start, obs=obs).items()}
+        d_er = torch.full((oo,), 7, dtype=torch.uint8, device=dev)
+        d_st = torch.full((B,), -9, dtype=torch.int32, device=dev)
+        d_ws = torch.empty(wsb, dtype=torch.uint8, device=dev)
+        G.local_bundle_adjustment_device(CAM, probs[0]["inv_sigma2"], d["desc"], B, d["kf"],
+                                         d["mode"], d["pts"], d["start"], d["obs"], d_er, d_st,
+                                         d_ws, ko, po, oo, stream=st.cuda_stream)
+    st.synchronize()
+    kf_g = d["kf"].cpu().numpy().view(np.float32).reshape(-1, 4, 4)
+    pts_g = d["pts"].cpu().numpy().view(np.float32).reshape(-1, 3)
+    er_g, st_g = d_er.cpu().numpy().astype(bool), d_st.cpu().numpy()
+    for i, p in enumerate(probs):
+        k0, nk, p0, npn = desc[i]
+        o0 = start[p0]
+        kf_o, pts_o, er_o, _ = oracle.local_ba(CAM, p)
+        assert st_g[i] > 0, f"problem {i}: status {st_g[i]}"
+        assert np.array_equal(er_g[o0:o0 + len(p["obs"])], er_o), f"problem {i}"
+        assert_close(kf_g[k0:k0 + nk], kf_o, p["kf_Tcw"], f"problem {i} poses")
+        assert_close(pts_g[p0:p0 + npn], pts_o, p["points"], f"problem {i} points")

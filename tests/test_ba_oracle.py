@@ -1,0 +1,113 @@
+"""Pins the LocalBundleAdjustment oracle (oracle/ba_oracle.c). As for PoseOptimization, g2o +
+Eigen cannot be built here, so there is no golden vector of the reference: "parity unpinned"
+against the reference binary. The restatement is pinned by:
+
+  - binary edge Jacobians (types_six_dof_expmap.cpp:103-137, 188-234) equal to central finite
+    differences of the edge error, wrt the point (X + dX) and the pose (exp(dx) * T), mono and
+    stereo;
+  - noise-free scenes: the local window converges to the generating poses from a perturbed
+    start, fixed cameras are left untouched, nothing is erased;
+  - every gross outlier is erased, no observation of an uncontaminated point is
+    (optimizer.cpp:672-700);
+  - a local keyframe with id 0 (kf_mode 1) keeps its pose, written back through the quaternion.
+CPU only."""
+import numpy as np
+import pytest
+
+import oracle_lib as O
+from slam_framework_amd import synthetic as S
+
+CAM = S.KITTI_CAM
+
+
+def _point_of(P, e):
+    return int(np.searchsorted(P["point_obs_start"], e, side="right") - 1)
+
+
+@pytest.mark.parametrize("stereo", [False, True])
+def test_binary_edge_jacobians_match_finite_differences(stereo):
+    P = S.ba_problem(2, n_local=5, n_fixed=2, n_points=60, outlier_frac=0.0,
+                     stereo_frac=1.0 if stereo else 0.0)
+    # the stereo error goes through a float inverse depth: wider step, looser tolerance
+    h, rtol = (1e-3, 2e-3) if stereo else (1e-6, 1e-6)
+    D = 3 if stereo else 2
+    for e in range(0, 60, 3):
+        ob = P["obs"][e]
+        T = P["kf_true"][ob["keyframe"]]
+        R, t, X = T[:3, :3], T[:3, 3], P["points_true"][_point_of(P, e)]
+        _, _, Jl, Jp = O.ba_edge_eval(CAM, R, t, X, ob, 1.0)
+        nl, npj = np.zeros((3, 3)), np.zeros((3, 6))
+        for i in range(3):
+            d = np.zeros(3)
+            d[i] = h
+            nl[:, i] = (O.ba_edge_eval(CAM, R, t, X + d, ob, 1.0)[1] -
+                        O.ba_edge_eval(CAM, R, t, X - d, ob, 1.0)[1]) / (2 * h)
+        for i in range(6):
+            d = np.zeros(6)
+            d[i] = h
+            Rp, tp = O.se3_exp(d)
+            Rm, tm = O.se3_exp(-d)
+            npj[:, i] = (O.ba_edge_eval(CAM, Rp @ R, Rp @ t + tp, X, ob, 1.0)[1] -
+                         O.ba_edge_eval(CAM, Rm @ R, Rm @ t + tm, X, ob, 1.0)[1]) / (2 * h)
+        np.testing.assert_allclose(Jl[:D], nl[:D], atol=rtol * np.abs(Jl[:D]).max())
+        np.testing.assert_allclose(Jp[:D], npj[:D], atol=rtol * np.abs(Jp[:D]).max())
+
+
+def test_stereo_right_coordinate_uses_float_bf_product():
+    P = S.ba_problem(4, n_local=3, n_fixed=1, n_points=5, stereo_frac=1.0, outlier_frac=0.0,
+                     noise_px=0.0)
+    ob = P["obs"][0]
+    T = P["kf_true"][ob["keyframe"]]
+    X = P["points_true"][0]
+    _, err, _, _ = O.ba_edge_eval(CAM, T[:3, :3], T[:3, 3], X, ob, 1.0)
+    Xc = T[:3, :3] @ X + T[:3, 3]
+    invz = np.float32(1.0 / Xc[2])
+    u = Xc[0] * np.float64(invz) * np.float64(np.float32(CAM[0])) + np.float64(np.float32(CAM[2]))
+    ur = u - np.float64(np.float32(np.float32(CAM[4]) * invz))
+    assert err[2] == pytest.approx(float(ob["ur"]) - ur, abs=1e-9)
+
+
+@pytest.mark.parametrize("stereo_frac", [0.0, 0.6])
+def test_noise_free_window_converges(stereo_frac):
+    P = S.ba_problem(3, n_local=10, n_fixed=4, n_points=800, noise_px=0.0, outlier_frac=0.0,
+                     stereo_frac=stereo_frac)
+    kf, pts, erase, its = O.local_ba(CAM, P)
+    loc = P["kf_mode"] == 0
+    fixed = P["kf_mode"] == 2
+    e0 = np.abs(P["kf_Tcw"][loc][:, :3, 3] - P["kf_true"][loc][:, :3, 3]).max()
+    e1 = np.abs(kf[loc][:, :3, 3] - P["kf_true"][loc][:, :3, 3]).max()
+    assert e1 < 0.02 * e0
+    assert np.array_equal(kf[fixed], P["kf_Tcw"][fixed])
+    assert not erase.any()
+    assert 2 <= its <= 15
+
+
+def test_gross_outliers_are_erased():
+    P = S.ba_problem(5, n_local=8, n_fixed=3, n_points=600, noise_px=0.0, outlier_frac=0.08)
+    kf, pts, erase, _ = O.local_ba(CAM, P)
+    obs = P["obs"]
+    # a gross outlier is an observation far from the true projection
+    fx, fy, cx, cy, _ = CAM
+    far = np.zeros(len(obs), bool)
+    for e, ob in enumerate(obs):
+        T = P["kf_true"][ob["keyframe"]]
+        Xc = T[:3, :3] @ P["points_true"][_point_of(P, e)] + T[:3, 3]
+        du = ob["u"] - (fx * Xc[0] / Xc[2] + cx)
+        dv = ob["v"] - (fy * Xc[1] / Xc[2] + cy)
+        far[e] = np.hypot(du, dv) > 10.0
+    st = P["point_obs_start"]
+    contaminated = np.zeros(len(obs), bool)  # observations of a point with a gross outlier
+    for p in range(len(st) - 1):
+        contaminated[st[p]:st[p + 1]] = far[st[p]:st[p + 1]].any()
+    assert far.sum() > 50
+    assert erase[far].all()  # every gross outlier is erased
+    # a gross outlier drags its point, so the point's good observations may go with it; the
+    # observations of clean points never do
+    assert not erase[~contaminated].any()
+
+
+def test_local_fixed_keyframe_written_back_unchanged():
+    P = S.ba_problem(6, n_local=6, n_fixed=2, n_points=300, first_local_fixed=True)
+    kf, _, _, _ = O.local_ba(CAM, P)
+    k = int(np.nonzero(P["kf_mode"] == 1)[0][0])
+    np.testing.assert_allclose(kf[k], P["kf_Tcw"][k], atol=2e-7)
