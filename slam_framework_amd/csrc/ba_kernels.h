@@ -18,7 +18,10 @@ struct BaWorkspace {
   uint8_t* act;      // [obs] edge at level 0
   int32_t* psorted;  // [obs] a point's active local-keyframe edges sorted by keyframe
   int2* hits;        // [obs * ((MAX_LOCAL_KF + 2) / 2)] S-block point pairs
-  double* pt;        // [points][32] estimate, backup, Hll, bl, Dinv, db, xl
+  double* pt;        // [27][points] (SoA) estimate, backup, Hll, bl, Dinv, db, xl
+  double* ehb;       // [obs][9] an edge's Hll and bl terms / Hpl^T xp
+  int32_t* opoint;   // [obs] the edge's point (index within its problem)
+  int n_pt;          // total points (the SoA stride)
   uint32_t* pmask;   // [points] local keyframes with an active edge to the point
   double* kf;        // [keyframes][64] estimate (q, t, R), backup, Hpp, bp
 };

@@ -38,6 +38,23 @@ namespace {
 using se3::Quat;
 using se3::SE3;
 
+// SLAMGPU_BA_PROFILE: thread 0 accumulates shader-clock cycles per phase into status[] slots
+// after the problem's own (tools/ba_profile.py, an instrumented build only). BA_TICK adds a
+// barrier only in that build: the kernel's own barriers are explicit.
+#ifdef SLAMGPU_BA_PROFILE
+#define BA_TICK(slot)                                       \
+  do {                                                      \
+    __syncthreads();                                        \
+    const long long t_ = clock64();                         \
+    if (threadIdx.x == 0) prof[slot] += (double)(t_ - t_last); \
+    t_last = t_;                                            \
+  } while (0)
+#else
+#define BA_TICK(slot) \
+  do {                \
+  } while (0)
+#endif
+
 constexpr int kThreads = 1024;
 constexpr int kWaves = kThreads / 64;
 constexpr int kMaxK = SLAMGPU_BA_MAX_LOCAL_KF;
@@ -55,9 +72,11 @@ __device__ __forceinline__ int hidx(int a, int c) {  // packed upper triangle of
 // kf record (64 doubles): q 0..3, t 4..6, R 8..16, backup q 17..20 t 21..23, Hpp 24..44,
 // bp 45..50, xp 51..56, Hpp-diag max 57
 constexpr int KQ = 0, KT = 4, KR = 8, KBQ = 17, KBT = 21, KH = 24, KB = 45;
-// point record (32 doubles): X 0..2, Xb 3..5, Hll 6..11 (00 01 02 11 12 22), bl 12..14,
-// Dinv 15..20 (same packing), db 21..23, xl 24..26
+// point fields (structure of arrays, ws.pt[field * ws.n_pt + point]): X 0..2, Xb 3..5,
+// Hll 6..11 (00 01 02 11 12 22), bl 12..14, Dinv 15..20 (same packing), db 21..23, xl 24..26
 constexpr int PX = 0, PXB = 3, PH = 6, PB = 12, PD = 15, PDB = 21, PXL = 24;
+// per-edge scratch record (ws.ehb, 9 doubles): the edge's Hll (6) and bl (3) terms; in the update
+// its first 3 hold Hpl^T xp
 __device__ __forceinline__ int s3(int i, int j) {  // packed symmetric 3x3
   const int a = i < j ? i : j, b = i < j ? j : i;
   return a == 0 ? b : (a == 1 ? 2 + b : 5);
@@ -282,8 +301,13 @@ struct Problem {
 __device__ __forceinline__ double* kfrec(const Problem& pb, int kf) {
   return pb.ws.kf + (size_t)(pb.k0 + kf) * 64;
 }
-__device__ __forceinline__ double* ptrec(const Problem& pb, int p) {
-  return pb.ws.pt + (size_t)(pb.p0 + p) * 32;
+struct PtRef {  // the SoA fields of one point
+  double* base;
+  size_t stride;
+  __device__ __forceinline__ double& operator[](int f) const { return base[(size_t)f * stride]; }
+};
+__device__ __forceinline__ PtRef ptrec(const Problem& pb, int p) {
+  return PtRef{pb.ws.pt + pb.p0 + p, (size_t)pb.ws.n_pt};
 }
 
 // ---- structure of the active edge set ------------------------------------------------------------
@@ -398,59 +422,72 @@ __device__ void build_structure(BaShared& sh, const Problem& pb) {
 }
 
 // ---- linearisation ------------------------------------------------------------------------------
-// Point pass: errors and chi2 of the active edges (stored: g2o keeps the last error per edge),
-// Hll, bl, Hpl; returns this thread's robust chi2 and max |Hll_jj| partials.
-__device__ void linearise_points(BaShared& sh, const Problem& pb, const PoseParams& P,
-                                 const float* isig, bool robust, double& chi, double& maxd) {
-  for (int p = threadIdx.x; p < pb.n_pts; p += kThreads) {
-    double* pr = ptrec(pb, p);
+// Edge pass: errors and chi2 of the active edges (stored: g2o keeps the last error per edge), the
+// edge's Hll and bl terms and its Hpl block; adds this thread's robust chi2 to `chi`.
+__device__ void linearise_edges(BaShared& sh, const Problem& pb, const PoseParams& P,
+                                const float* isig, bool robust, double& chi) {
+  for (int e = threadIdx.x; e < pb.n_obs; e += kThreads) {
+    const int ge = pb.o0 + e;
+    if (!pb.ws.act[ge]) continue;
+    const PtRef pr = ptrec(pb, pb.ws.opoint[ge]);
     const double X[3] = {pr[PX], pr[PX + 1], pr[PX + 2]};
-    double H[6] = {0, 0, 0, 0, 0, 0}, bl[3] = {0, 0, 0};
+    const slamgpu_ba_obs o = pb.obs[ge];
+    const double* kr = kfrec(pb, o.keyframe);
+    ObsEval v;
+    const double c2 = eval_obs(o, P, isig, kr, X, v);
+    pb.ws.chi2[ge] = c2;
+    double wgt = 1.0;
+    if (robust) {
+      const double d = huber_delta(v.stereo), d2 = d * d;
+      if (c2 > d2) {
+        const double sq = sqrt(c2);
+        chi += 2 * sq * d - d2;
+        wgt = d / sq;
+      } else {
+        chi += c2;
+      }
+    } else {
+      chi += c2;
+    }
+    double Jl[3][3], Jp[3][6];
+    obs_jacobians(v, P, kr, Jl, Jp);
+    const double W = wgt * v.info;
+    // omega_r = -Omega e * rho' (base_binary_edge.hpp:72-110)
+    const double or0 = -(v.info * v.e[0]) * wgt, or1 = -(v.info * v.e[1]) * wgt,
+                 or2 = -(v.info * v.e[2]) * wgt;
+    double* hb = pb.ws.ehb + (size_t)ge * 9;
+    for (int i = 0; i < 3; i++) {
+      hb[6 + i] = Jl[0][i] * or0 + Jl[1][i] * or1 + Jl[2][i] * or2;
+      for (int j = i; j < 3; j++)
+        hb[s3(i, j)] = (Jl[0][i] * W) * Jl[0][j] + (Jl[1][i] * W) * Jl[1][j] +
+                       (Jl[2][i] * W) * Jl[2][j];
+    }
+    if (sh.free_of_kf[o.keyframe] >= 0) {
+      double* hp = pb.ws.hpl + (size_t)ge * 18;
+      for (int i = 0; i < 6; i++)
+        for (int j = 0; j < 3; j++)
+          hp[3 * i + j] = (Jp[0][i] * W) * Jl[0][j] + (Jp[1][i] * W) * Jl[1][j] +
+                          (Jp[2][i] * W) * Jl[2][j];
+    }
+  }
+}
+
+// Point pass: Hll and bl as the sums of the point's edge terms in edge order; max |Hll_jj|.
+__device__ void sum_points(const Problem& pb, double& maxd) {
+  for (int p = threadIdx.x; p < pb.n_pts; p += kThreads) {
+    const PtRef pr = ptrec(pb, p);
+    double H[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
     int nact = 0;
     const int s = pb.pstart[pb.p0 + p], e1 = pb.pstart[pb.p0 + p + 1];
     for (int ge = s; ge < e1; ge++) {
       if (!pb.ws.act[ge]) continue;
       nact++;
-      const slamgpu_ba_obs o = pb.obs[ge];
-      const double* kr = kfrec(pb, o.keyframe);
-      ObsEval v;
-      const double c2 = eval_obs(o, P, isig, kr, X, v);
-      pb.ws.chi2[ge] = c2;
-      double wgt = 1.0;
-      if (robust) {
-        const double d = huber_delta(v.stereo), d2 = d * d;
-        if (c2 > d2) {
-          const double sq = sqrt(c2);
-          chi += 2 * sq * d - d2;
-          wgt = d / sq;
-        } else {
-          chi += c2;
-        }
-      } else {
-        chi += c2;
-      }
-      double Jl[3][3], Jp[3][6];
-      obs_jacobians(v, P, kr, Jl, Jp);
-      const double W = wgt * v.info;
-      // omega_r = -Omega e * rho' (base_binary_edge.hpp:72-110)
-      const double or0 = -(v.info * v.e[0]) * wgt, or1 = -(v.info * v.e[1]) * wgt,
-                   or2 = -(v.info * v.e[2]) * wgt;
-      for (int i = 0; i < 3; i++) {
-        bl[i] += Jl[0][i] * or0 + Jl[1][i] * or1 + Jl[2][i] * or2;
-        for (int j = i; j < 3; j++)
-          H[s3(i, j)] += (Jl[0][i] * W) * Jl[0][j] + (Jl[1][i] * W) * Jl[1][j] +
-                         (Jl[2][i] * W) * Jl[2][j];
-      }
-      if (sh.free_of_kf[o.keyframe] >= 0) {
-        double* hp = pb.ws.hpl + (size_t)ge * 18;
-        for (int i = 0; i < 6; i++)
-          for (int j = 0; j < 3; j++)
-            hp[3 * i + j] = (Jp[0][i] * W) * Jl[0][j] + (Jp[1][i] * W) * Jl[1][j] +
-                            (Jp[2][i] * W) * Jl[2][j];
-      }
+      const double* hb = pb.ws.ehb + (size_t)ge * 9;
+#pragma unroll
+      for (int i = 0; i < 9; i++) H[i] += hb[i];
     }
     for (int i = 0; i < 6; i++) pr[PH + i] = H[i];
-    for (int i = 0; i < 3; i++) pr[PB + i] = bl[i];
+    for (int i = 0; i < 3; i++) pr[PB + i] = H[6 + i];
     if (nact) maxd = fmax(maxd, fmax(fabs(H[0]), fmax(fabs(H[3]), fabs(H[5]))));
   }
 }
@@ -470,7 +507,7 @@ __device__ void linearise_keyframes(BaShared& sh, const Problem& pb, const PoseP
     for (int h = lane; h < cnt; h += 64) {
       const int2 ep = hits[off + h];
       const int ge = pb.o0 + ep.x;
-      const double* pr = ptrec(pb, ep.y);
+      const PtRef pr = ptrec(pb, ep.y);
       const double X[3] = {pr[PX], pr[PX + 1], pr[PX + 2]};
       ObsEval v;
       const double c2 = eval_obs(pb.obs[ge], P, isig, kr, X, v);
@@ -505,9 +542,9 @@ __device__ void linearise_keyframes(BaShared& sh, const Problem& pb, const PoseP
 }
 
 // ---- one LM trial: Schur solve ------------------------------------------------------------------
-__device__ void schur_points(BaShared& sh, const Problem& pb, double lambda) {
+__device__ void schur_points(const Problem& pb, double lambda) {
   for (int p = threadIdx.x; p < pb.n_pts; p += kThreads) {
-    double* pr = ptrec(pb, p);
+    const PtRef pr = ptrec(pb, p);
     double D[6], Di[6];
     for (int i = 0; i < 6; i++) D[i] = pr[PH + i];
     D[0] += lambda;
@@ -519,17 +556,24 @@ __device__ void schur_points(BaShared& sh, const Problem& pb, double lambda) {
     pr[PDB] = Di[0] * b0 + Di[1] * b1 + Di[2] * b2;
     pr[PDB + 1] = Di[1] * b0 + Di[3] * b1 + Di[4] * b2;
     pr[PDB + 2] = Di[2] * b0 + Di[4] * b1 + Di[5] * b2;
-    const int s = pb.pstart[pb.p0 + p], e1 = pb.pstart[pb.p0 + p + 1];
-    for (int ge = s; ge < e1; ge++) {
-      if (!pb.ws.act[ge] || sh.free_of_kf[pb.obs[ge].keyframe] < 0) continue;
-      const double* hp = pb.ws.hpl + (size_t)ge * 18;
-      double* bd = pb.ws.bdinv + (size_t)ge * 18;
-      for (int i = 0; i < 6; i++) {
-        const double h0 = hp[3 * i], h1 = hp[3 * i + 1], h2 = hp[3 * i + 2];
-        bd[3 * i] = h0 * Di[0] + h1 * Di[1] + h2 * Di[2];
-        bd[3 * i + 1] = h0 * Di[1] + h1 * Di[3] + h2 * Di[4];
-        bd[3 * i + 2] = h0 * Di[2] + h1 * Di[4] + h2 * Di[5];
-      }
+  }
+}
+
+// BDinv_e = Hpl_e Dinv_p for every active local-keyframe edge (edge-parallel).
+__device__ void schur_edges(BaShared& sh, const Problem& pb) {
+  for (int e = threadIdx.x; e < pb.n_obs; e += kThreads) {
+    const int ge = pb.o0 + e;
+    if (!pb.ws.act[ge] || sh.free_of_kf[pb.obs[ge].keyframe] < 0) continue;
+    const PtRef pr = ptrec(pb, pb.ws.opoint[ge]);
+    double Di[6];
+    for (int i = 0; i < 6; i++) Di[i] = pr[PD + i];
+    const double* hp = pb.ws.hpl + (size_t)ge * 18;
+    double* bd = pb.ws.bdinv + (size_t)ge * 18;
+    for (int i = 0; i < 6; i++) {
+      const double h0 = hp[3 * i], h1 = hp[3 * i + 1], h2 = hp[3 * i + 2];
+      bd[3 * i] = h0 * Di[0] + h1 * Di[1] + h2 * Di[2];
+      bd[3 * i + 1] = h0 * Di[1] + h1 * Di[3] + h2 * Di[4];
+      bd[3 * i + 2] = h0 * Di[2] + h1 * Di[4] + h2 * Di[5];
     }
   }
 }
@@ -586,7 +630,7 @@ __device__ void assemble_S(BaShared& sh, const Problem& pb, double lambda) {
     for (int h = lane; h < cnt; h += 64) {
       const int2 ep = hits[off + h];
       const double* hp = pb.ws.hpl + (size_t)(pb.o0 + ep.x) * 18;
-      const double* pr = ptrec(pb, ep.y);
+      const PtRef pr = ptrec(pb, ep.y);
       const double d0 = pr[PDB], d1 = pr[PDB + 1], d2 = pr[PDB + 2];
 #pragma unroll
       for (int i = 0; i < 6; i++) acc[i] += hp[3 * i] * d0 + hp[3 * i + 1] * d1 + hp[3 * i + 2] * d2;
@@ -606,24 +650,44 @@ __device__ void factor_solve(BaShared& sh) {
   __syncthreads();
   for (int J = 0; J < K; J++) {
     const int j0 = 6 * J;
-    // 1. diagonal block: unblocked LDLT of the 6x6, forward-solve its rhs (one lane)
+    // 1. diagonal block: unblocked LDLT of the 6x6 in one lane's registers, forward-solve its rhs
     if (tid == 0) {
-      for (int j = j0; j < j0 + 6; j++) {
-        double d = sh.S[sidx(j, j)];
-        for (int k = j0; k < j; k++) d -= sh.S[sidx(j, k)] * sh.S[sidx(j, k)] * sh.dg[k];
-        if (d == 0.0) sh.ok = 0;
-        sh.dg[j] = d;
-        for (int i = j + 1; i < j0 + 6; i++) {
-          double s = sh.S[sidx(i, j)];
-          for (int k = j0; k < j; k++) s -= sh.S[sidx(i, k)] * sh.S[sidx(j, k)] * sh.dg[k];
-          sh.S[sidx(i, j)] = d != 0.0 ? s / d : 0.0;
+      double A[6][6], d[6], y[6];
+#pragma unroll
+      for (int i = 0; i < 6; i++) {
+#pragma unroll
+        for (int j = 0; j <= i; j++) A[i][j] = sh.S[sidx(j0 + i, j0 + j)];
+        y[i] = sh.rhs[j0 + i];
+      }
+      bool good = true;
+#pragma unroll
+      for (int j = 0; j < 6; j++) {
+        double dj = A[j][j];
+#pragma unroll
+        for (int k = 0; k < j; k++) dj -= A[j][k] * A[j][k] * d[k];
+        good = good && dj != 0.0;
+        d[j] = dj;
+#pragma unroll
+        for (int i = j + 1; i < 6; i++) {
+          double s = A[i][j];
+#pragma unroll
+          for (int k = 0; k < j; k++) s -= A[i][k] * A[j][k] * d[k];
+          A[i][j] = dj != 0.0 ? s / dj : 0.0;
         }
       }
-      for (int i = j0; i < j0 + 6; i++) {
-        double s = sh.rhs[i];
-        for (int k = j0; k < i; k++) s -= sh.S[sidx(i, k)] * sh.rhs[k];
-        sh.rhs[i] = s;
+#pragma unroll
+      for (int i = 0; i < 6; i++) {
+#pragma unroll
+        for (int k = 0; k < i; k++) y[i] -= A[i][k] * y[k];
       }
+#pragma unroll
+      for (int i = 0; i < 6; i++) {
+        sh.dg[j0 + i] = d[i];
+        sh.rhs[j0 + i] = y[i];
+#pragma unroll
+        for (int j = 0; j < i; j++) sh.S[sidx(j0 + i, j0 + j)] = A[i][j];
+      }
+      if (!good) sh.ok = 0;
     }
     __syncthreads();
     if (!sh.ok) return;
@@ -756,9 +820,10 @@ __global__ __launch_bounds__(kThreads) void local_ba_kernel(
     store_T(kfrec(pb, k), E);
   }
   for (int p = tid; p < pb.n_pts; p += kThreads) {
-    double* r = ptrec(pb, p);
+    const PtRef r = ptrec(pb, p);
     for (int i = 0; i < 3; i++) r[PX + i] = points[(size_t)(pb.p0 + p) * 3 + i];
     for (int i = 0; i < 3; i++) r[PXL + i] = 0.0;
+    for (int ge = pstart[pb.p0 + p]; ge < pstart[pb.p0 + p + 1]; ge++) ws.opoint[ge] = p;
   }
   for (int e = tid; e < pb.n_obs; e += kThreads) {
     ws.act[pb.o0 + e] = 1;
@@ -769,11 +834,17 @@ __global__ __launch_bounds__(kThreads) void local_ba_kernel(
 
   const int K = sh.K, n = 6 * K;
   int lm_total = 0;
+#ifdef SLAMGPU_BA_PROFILE
+  double prof[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  long long t_last = clock64();
+#endif
   bool stopped = false;
   for (int phase = 0; phase < 2 && !stopped; phase++) {
     const bool robust = phase == 0;
     const int iterations = phase == 0 ? 5 : 10;
+    BA_TICK(7);
     build_structure(sh, pb);
+    BA_TICK(0);
     double lambda = 0.0;
     int ni = 2, nbad = 0;
     for (int it = 0; it < iterations; it++) {
@@ -783,8 +854,12 @@ __global__ __launch_bounds__(kThreads) void local_ba_kernel(
       }
       // ---- linearise: computeActiveErrors + activeRobustChi2 + buildSystem ----
       double chi = 0.0, maxd = 0.0;
-      linearise_points(sh, pb, P, isig, robust, chi, maxd);
+      BA_TICK(7);
+      linearise_edges(sh, pb, P, isig, robust, chi);
       linearise_keyframes(sh, pb, P, isig, robust, maxd);
+      __syncthreads();
+      sum_points(pb, maxd);
+      BA_TICK(1);
       __syncthreads();
       double zero = 0.0;
       block_sum2(sh, chi, zero);
@@ -799,33 +874,55 @@ __global__ __launch_bounds__(kThreads) void local_ba_kernel(
       int qmax = 0;
       do {
         // ---- solve ----
-        schur_points(sh, pb, lambda);
+        BA_TICK(7);
+        schur_points(pb, lambda);
         __syncthreads();
+        schur_edges(sh, pb);
+        __syncthreads();
+        BA_TICK(2);
         assemble_S(sh, pb, lambda);
         __syncthreads();
+        BA_TICK(3);
         factor_solve(sh);  // ends with a barrier; sh.xp = the pose step when sh.ok
+        BA_TICK(4);
         const bool ok = sh.ok;
         // ---- update (backup first): points X += xl, keyframes exp(xp) * T ----
         double scale = 0.0, temp = 0.0;
+        if (ok) {  // Hpl_e^T xp per local-keyframe edge (a failed solve keeps g2o's old _x)
+          for (int e = tid; e < pb.n_obs; e += kThreads) {
+            const int ge = pb.o0 + e;
+            const int f = sh.free_of_kf[obs[ge].keyframe];
+            if (!ws.act[ge] || f < 0) continue;
+            const double* hp = ws.hpl + (size_t)ge * 18;
+            double c0 = 0, c1 = 0, c2 = 0;
+            for (int i = 0; i < 6; i++) {
+              const double x = sh.xp[6 * f + i];
+              c0 += hp[3 * i] * x;
+              c1 += hp[3 * i + 1] * x;
+              c2 += hp[3 * i + 2] * x;
+            }
+            double* hb = ws.ehb + (size_t)ge * 9;
+            hb[0] = c0;
+            hb[1] = c1;
+            hb[2] = c2;
+          }
+          __syncthreads();
+        }
         for (int p = tid; p < pb.n_pts; p += kThreads) {
-          double* r = ptrec(pb, p);
+          const PtRef r = ptrec(pb, p);
           const int s = pstart[pb.p0 + p], e1 = pstart[pb.p0 + p + 1];
           int nact = 0;
           double c0 = r[PB], c1 = r[PB + 1], c2 = r[PB + 2];
           for (int ge = s; ge < e1; ge++) {
             if (!ws.act[ge]) continue;
             nact++;
-            const int f = sh.free_of_kf[obs[ge].keyframe];
-            if (f < 0 || !ok) continue;
-            const double* hp = ws.hpl + (size_t)ge * 18;
-            for (int i = 0; i < 6; i++) {
-              const double x = sh.xp[6 * f + i];
-              c0 -= hp[3 * i] * x;
-              c1 -= hp[3 * i + 1] * x;
-              c2 -= hp[3 * i + 2] * x;
-            }
+            if (!ok || sh.free_of_kf[obs[ge].keyframe] < 0) continue;
+            const double* hb = ws.ehb + (size_t)ge * 9;
+            c0 -= hb[0];
+            c1 -= hb[1];
+            c2 -= hb[2];
           }
-          if (ok) {  // a failed solve leaves the previous x in place (g2o's _x)
+          if (ok) {
             r[PXL] = r[PD] * c0 + r[PD + 1] * c1 + r[PD + 2] * c2;
             r[PXL + 1] = r[PD + 1] * c0 + r[PD + 3] * c1 + r[PD + 4] * c2;
             r[PXL + 2] = r[PD + 2] * c0 + r[PD + 4] * c1 + r[PD + 5] * c2;
@@ -855,26 +952,26 @@ __global__ __launch_bounds__(kThreads) void local_ba_kernel(
           }
         }
         __syncthreads();
-        // ---- errors at the new estimate ----
-        for (int p = tid; p < pb.n_pts; p += kThreads) {
-          const double* r = ptrec(pb, p);
+        // ---- errors at the new estimate (edge-parallel) ----
+        for (int e = tid; e < pb.n_obs; e += kThreads) {
+          const int ge = pb.o0 + e;
+          if (!ws.act[ge]) continue;
+          const PtRef r = ptrec(pb, ws.opoint[ge]);
           const double X[3] = {r[PX], r[PX + 1], r[PX + 2]};
-          const int s = pstart[pb.p0 + p], e1 = pstart[pb.p0 + p + 1];
-          for (int ge = s; ge < e1; ge++) {
-            if (!ws.act[ge]) continue;
-            const slamgpu_ba_obs o = obs[ge];
-            ObsEval v;
-            const double c2 = eval_obs(o, P, isig, kfrec(pb, o.keyframe), X, v);
-            ws.chi2[ge] = c2;
-            if (robust) {
-              const double d = huber_delta(v.stereo), d2 = d * d;
-              temp += c2 > d2 ? 2 * sqrt(c2) * d - d2 : c2;
-            } else {
-              temp += c2;
-            }
+          const slamgpu_ba_obs o = obs[ge];
+          ObsEval v;
+          const double c2 = eval_obs(o, P, isig, kfrec(pb, o.keyframe), X, v);
+          ws.chi2[ge] = c2;
+          if (robust) {
+            const double d = huber_delta(v.stereo), d2 = d * d;
+            temp += c2 > d2 ? 2 * sqrt(c2) * d - d2 : c2;
+          } else {
+            temp += c2;
           }
         }
+        BA_TICK(5);
         block_sum2(sh, temp, scale);
+        BA_TICK(6);
         double tempChi = ok ? temp : DBL_MAX;
         scale += 1e-3;
         rho = (currentChi - tempChi) / scale;
@@ -889,7 +986,7 @@ __global__ __launch_bounds__(kThreads) void local_ba_kernel(
           ni *= 2;
           // pop: restore the estimates; the edges keep the rejected errors
           for (int p = tid; p < pb.n_pts; p += kThreads) {
-            double* r = ptrec(pb, p);
+            const PtRef r = ptrec(pb, p);
             for (int i = 0; i < 3; i++) r[PX + i] = r[PXB + i];
           }
           if (tid < K) {
@@ -918,31 +1015,30 @@ __global__ __launch_bounds__(kThreads) void local_ba_kernel(
       if (stop_flag && __atomic_load_n(stop_flag, __ATOMIC_RELAXED)) stopped = true;  // do_more
       if (stopped) break;
       // optimizer.cpp:632-665: chi2 > threshold or depth <= 0 -> level 1
-      for (int p = tid; p < pb.n_pts; p += kThreads) {
-        const double* r = ptrec(pb, p);
+      for (int e = tid; e < pb.n_obs; e += kThreads) {
+        const int ge = pb.o0 + e;
+        const PtRef r = ptrec(pb, ws.opoint[ge]);
         const double X[3] = {r[PX], r[PX + 1], r[PX + 2]};
-        const int s = pstart[pb.p0 + p], e1 = pstart[pb.p0 + p + 1];
-        for (int ge = s; ge < e1; ge++) {
-          const slamgpu_ba_obs o = obs[ge];
-          ObsEval v;
-          eval_obs(o, P, isig, kfrec(pb, o.keyframe), X, v);
-          if (ws.chi2[ge] > (o.ur >= 0 ? 7.815 : 5.991) || !(v.z > 0.0)) ws.act[ge] = 0;
-        }
+        const slamgpu_ba_obs o = obs[ge];
+        ObsEval v;
+        eval_obs(o, P, isig, kfrec(pb, o.keyframe), X, v);
+        if (ws.chi2[ge] > (o.ur >= 0 ? 7.815 : 5.991) || !(v.z > 0.0)) ws.act[ge] = 0;
       }
       __syncthreads();
     }
   }
   // optimizer.cpp:672-700: erase list over every edge; :702-716 write-back
-  for (int p = tid; p < pb.n_pts; p += kThreads) {
-    const double* r = ptrec(pb, p);
+  for (int e = tid; e < pb.n_obs; e += kThreads) {
+    const int ge = pb.o0 + e;
+    const PtRef r = ptrec(pb, ws.opoint[ge]);
     const double X[3] = {r[PX], r[PX + 1], r[PX + 2]};
-    const int s = pstart[pb.p0 + p], e1 = pstart[pb.p0 + p + 1];
-    for (int ge = s; ge < e1; ge++) {
-      const slamgpu_ba_obs o = obs[ge];
-      ObsEval v;
-      eval_obs(o, P, isig, kfrec(pb, o.keyframe), X, v);
-      erase[ge] = (ws.chi2[ge] > (o.ur >= 0 ? 7.815 : 5.991) || !(v.z > 0.0)) ? 1 : 0;
-    }
+    const slamgpu_ba_obs o = obs[ge];
+    ObsEval v;
+    eval_obs(o, P, isig, kfrec(pb, o.keyframe), X, v);
+    erase[ge] = (ws.chi2[ge] > (o.ur >= 0 ? 7.815 : 5.991) || !(v.z > 0.0)) ? 1 : 0;
+  }
+  for (int p = tid; p < pb.n_pts; p += kThreads) {
+    const PtRef r = ptrec(pb, p);
     for (int i = 0; i < 3; i++) points[(size_t)(pb.p0 + p) * 3 + i] = (float)r[PX + i];
   }
   for (int k = tid; k < pb.n_kf; k += kThreads) {
@@ -957,6 +1053,10 @@ __global__ __launch_bounds__(kThreads) void local_ba_kernel(
     T[15] = 1.f;
   }
   if (tid == 0) status[blockIdx.x] = lm_total;
+#ifdef SLAMGPU_BA_PROFILE
+  if (tid == 0)
+    for (int i = 0; i < 8; i++) reinterpret_cast<double*>(status + gridDim.x + 1)[blockIdx.x * 8 + i] = prof[i];
+#endif
   (void)n;
 }
 
@@ -979,7 +1079,10 @@ BaWorkspace ba_workspace_layout(void* base, int total_kf, int total_points, int 
   w.act = reinterpret_cast<uint8_t*>(take((size_t)total_obs));
   w.psorted = reinterpret_cast<int32_t*>(take(sizeof(int32_t) * (size_t)total_obs));
   w.hits = reinterpret_cast<int2*>(take(sizeof(int2) * kPairsPerObs * (size_t)total_obs));
-  w.pt = reinterpret_cast<double*>(take(sizeof(double) * 32 * (size_t)total_points));
+  w.pt = reinterpret_cast<double*>(take(sizeof(double) * 27 * (size_t)total_points));
+  w.n_pt = total_points;
+  w.ehb = reinterpret_cast<double*>(take(sizeof(double) * 9 * (size_t)total_obs));
+  w.opoint = reinterpret_cast<int32_t*>(take(sizeof(int32_t) * (size_t)total_obs));
   w.pmask = reinterpret_cast<uint32_t*>(take(sizeof(uint32_t) * (size_t)total_points));
   w.kf = reinterpret_cast<double*>(take(sizeof(double) * 64 * (size_t)total_kf));
   if (bytes) *bytes = off + 256;
