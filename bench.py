@@ -85,6 +85,8 @@ def main():
     ap.add_argument("--distinct", type=int, default=16, help="distinct synthetic frames per rank")
     ap.add_argument("--cpu-frames", type=int, default=0, help="oracle sample size (0 = auto)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-optimizer", action="store_true",
+                    help="skip the PoseOptimization / LocalBundleAdjustment measurements")
     args = ap.parse_args()
 
     import torch
@@ -216,6 +218,10 @@ def main():
         cpu = None
         if not args.no_cpu_baseline:
             cpu = cpu_baseline(Ls, Rs, args.cpu_frames)
+        opt = None
+        if not args.no_optimizer:
+            opt = {"pose_optimization": bench_pose(dev, not args.no_cpu_baseline),
+                   "local_bundle_adjustment": bench_local_ba(dev, not args.no_cpu_baseline)}
         line = {
             "metric": "stereo frames/sec ORB extract+match @1241x376, 2000 kp/frame",
             "value": round(value, 2), "unit": "stereo frames/s", "n_gpus": world,
@@ -230,12 +236,171 @@ def main():
             "roofline": roofline,
             "cpu_baseline": cpu,
             "kernel_ms_per_step": {n: round(brk[n][0], 4) for n in names},
+            "optimizer": opt,
             "per_rank_matches_per_step": summ[:, 1].tolist(),
         }
         print(json.dumps(line))
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
+
+
+FP64_VALU_PEAK_TFLOPS = 78.6  # MI355X FP64 vector peak (MI355X_MICROARCH.md)
+# Algorithmic FP64 flops per pose edge: a linearise pass (error ~60, Jacobian ~40, H/b ~160)
+# and a trial pass (error + Huber ~60) per LM iteration (DESIGN.md "Optimizer rows").
+POSE_FLOPS_PER_EDGE_ITER = 320
+
+
+def _events_ms(fn, stream, reps):
+    """Median HIP-event time of fn() on `stream` (the stream the kernel is launched on)."""
+    import torch
+    ms = []
+    for _ in range(reps):
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record(stream)
+        fn()
+        b.record(stream)
+        b.synchronize()
+        ms.append(a.elapsed_time(b))
+    return float(np.median(ms))
+
+
+def bench_pose(dev, with_cpu):
+    """configs[3]: Optimizer::PoseOptimization on SURVEY.md section 8(d) C4 problems (2000 edges,
+    60% stereo, 10% gross outliers, start 2 deg / 0.3 m off; seeds 7, 8, ...), batched over 2048
+    frames and as a single-frame call; the oracle on host cores."""
+    import torch
+    from slam_framework_amd import slamgpu as G
+    from slam_framework_amd import synthetic as S
+
+    B, distinct = 2048, 64
+    probs = [S.c4_problem(7 + i) for i in range(distinct)]
+    edges = np.concatenate([p[0] for p in probs])
+    start = np.zeros(distinct + 1, np.int64)
+    start[1:] = np.cumsum([len(p[0]) for p in probs])
+    poses = np.stack([p[1] for p in probs])
+    isig = probs[0][3]
+    k = B // distinct
+    E = np.concatenate([edges] * k)
+    st = np.concatenate([start[:-1] + i * start[-1] for i in range(k)] + [[k * start[-1]]])
+    stream = torch.cuda.current_stream()
+    d_e = torch.from_numpy(E.view(np.uint8).copy()).to(dev)
+    d_s = torch.from_numpy(st.astype(np.int32)).to(dev)
+    d_T0 = torch.from_numpy(np.concatenate([poses] * k)).to(dev)
+    d_T = d_T0.clone()
+    d_o = torch.zeros(len(E), dtype=torch.uint8, device=dev)
+    d_r = torch.zeros(B, dtype=torch.int32, device=dev)
+    d_it = torch.zeros(B, dtype=torch.int32, device=dev)
+
+    def run(n):
+        d_T.copy_(d_T0)
+        G.pose_optimization_device(S.KITTI_CAM, isig, d_e, d_s, n, d_T, d_o, d_r, d_it,
+                                   stream.cuda_stream)
+    run(B)
+    torch.cuda.synchronize()
+    ms = _events_ms(lambda: run(B), stream, 5)
+    its = d_it.cpu().numpy()
+    flops = float((its.astype(np.float64) * np.diff(st)).sum()) * POSE_FLOPS_PER_EDGE_ITER
+    ms1 = _events_ms(lambda: run(1), stream, 10)
+    out = {"workload": "configs[3]: PoseOptimization on SURVEY 8(d) C4 (2000 edges/frame, 60% "
+                       "stereo, 10% gross outliers, 2 deg / 0.3 m start), 4 rounds x 10 LM "
+                       "iterations (FP64)",
+           "frames_per_s": round(B / ms * 1e3, 1), "batch_frames": B,
+           "ms_per_batch": round(ms, 3), "single_frame_ms": round(ms1, 4),
+           "lm_iterations_per_frame": round(float(its.mean()), 2),
+           "roofline": {"kernel": "pose_opt", "bound": "fp64 valu",
+                        "achieved": round(flops / (ms * 1e-3) / 1e12, 3),
+                        "peak": FP64_VALU_PEAK_TFLOPS, "unit": "TFLOP/s",
+                        "frac": round(flops / (ms * 1e-3) / 1e12 / FP64_VALU_PEAK_TFLOPS, 4),
+                        "flops_per_edge_iteration": POSE_FLOPS_PER_EDGE_ITER},
+           "cpu_baseline": None}
+    if with_cpu:
+        import concurrent.futures as cf
+        sys.path.insert(0, os.path.join(ROOT, "tests"))
+        import oracle_lib as O
+        O.build()
+        threads = min(16, os.cpu_count() or 1)
+        per = 16
+
+        def work(t):
+            for i in range(per):
+                p = probs[(t * per + i) % distinct]
+                O.pose_optimization(S.KITTI_CAM, isig, p[0], p[1])
+            return per
+        t0 = time.perf_counter()
+        with cf.ThreadPoolExecutor(threads) as ex:
+            done = sum(ex.map(work, range(threads)))
+        wall = time.perf_counter() - t0
+        out["cpu_baseline"] = {"value": round(done / wall, 1), "unit": "frames/s",
+                               "cores": threads, "kind": "port",
+                               "sample": f"{done} frames of 2000 edges ({threads} threads x "
+                                         f"{per}); oracle/pose_oracle.c FP64 restatement"}
+    return out
+
+
+def bench_local_ba(dev, with_cpu):
+    """configs[4]: Optimizer::LocalBundleAdjustment on SURVEY.md section 8(d) C5 (20 local + 5
+    fixed keyframes at 1 m spacing, 3000 map points seen by 2-6 keyframes, ~12k observations;
+    seed 11), one problem and a batch of 64; the oracle on host cores."""
+    import torch
+    from slam_framework_amd import slamgpu as G
+    from slam_framework_amd import synthetic as S
+
+    P = S.c5_problem(11)
+    nk, npn, no = len(P["kf_mode"]), len(P["points"]), len(P["obs"])
+    stream = torch.cuda.current_stream()
+    res = {}
+    for B in (1, 64):
+        desc = np.array([(i * nk, nk, i * npn, npn) for i in range(B)], np.int32)
+        start = np.concatenate([P["point_obs_start"][:-1] + i * no for i in range(B)] +
+                               [[B * no]]).astype(np.int32)
+        t = lambda a: torch.from_numpy(np.ascontiguousarray(a).view(np.uint8).copy()).to(dev)
+        d_desc, d_mode, d_start = t(desc), t(np.tile(P["kf_mode"], B)), t(start)
+        d_obs = t(np.tile(P["obs"], B))
+        kf0, pts0 = t(np.tile(P["kf_Tcw"], (B, 1, 1))), t(np.tile(P["points"], (B, 1)))
+        d_kf, d_pts = kf0.clone(), pts0.clone()
+        d_er = torch.zeros(B * no, dtype=torch.uint8, device=dev)
+        d_st = torch.zeros(B, dtype=torch.int32, device=dev)
+        d_ws = torch.empty(G.local_ba_workspace_bytes(B * nk, B * npn, B * no),
+                           dtype=torch.uint8, device=dev)
+
+        def run():
+            d_kf.copy_(kf0)
+            d_pts.copy_(pts0)
+            G.local_bundle_adjustment_device(S.KITTI_CAM, P["inv_sigma2"], d_desc, B, d_kf,
+                                             d_mode, d_pts, d_start, d_obs, d_er, d_st, d_ws,
+                                             B * nk, B * npn, B * no, stream=stream.cuda_stream)
+        run()
+        torch.cuda.synchronize()
+        res[B] = (_events_ms(run, stream, 3), int(d_st[0].item()))
+    out = {"workload": "configs[4]: LocalBundleAdjustment on SURVEY 8(d) C5, 20 local + 5 fixed "
+                       f"keyframes x 3000 map points ({no} observations), 5 robust + 10 LM "
+                       "iterations (FP64)",
+           "problems_per_s": round(64 / res[64][0] * 1e3, 1), "batch_problems": 64,
+           "single_problem_ms": round(res[1][0], 3), "lm_iterations": res[1][1],
+           "cpu_baseline": None}
+    if with_cpu:
+        import concurrent.futures as cf
+        sys.path.insert(0, os.path.join(ROOT, "tests"))
+        import oracle_lib as O
+        O.build()
+        threads = min(16, os.cpu_count() or 1)
+        per = 2
+        probs = [S.c5_problem(11 + i) for i in range(4)]
+
+        def work(tid):
+            for i in range(per):
+                O.local_ba(S.KITTI_CAM, probs[(tid + i) % len(probs)])
+            return per
+        t0 = time.perf_counter()
+        with cf.ThreadPoolExecutor(threads) as ex:
+            done = sum(ex.map(work, range(threads)))
+        wall = time.perf_counter() - t0
+        out["cpu_baseline"] = {"value": round(done / wall, 2), "unit": "problems/s",
+                               "cores": threads, "kind": "port",
+                               "sample": f"{done} problems ({threads} threads x {per}); "
+                                         "oracle/ba_oracle.c FP64 restatement"}
+    return out
 
 
 def cpu_baseline(Ls, Rs, n_frames):

@@ -173,6 +173,56 @@ def pose_problem(seed: int, n: int = 2000, stereo_frac: float = 0.6, outlier_fra
     return edges, T0.astype(np.float32), T_true, level_inv_sigma2(scale_factor, nlevels), bad
 
 
+def c4_problem(seed: int = 7, n: int = 2000, cam=KITTI_CAM, nlevels: int = 8,
+               scale_factor: float = 1.2):
+    """SURVEY.md section 8(d) C4, the PoseOptimization bench workload: n world points uniform in
+    x in [-15, 15], y in [-3, 3], z in [5, 40] m (camera frame of the true pose), KITTI
+    intrinsics, 60% stereo observations (ur = u - bf / z), octave U{0..7} with N(0, sigma_l^2)
+    pixel noise (sigma_l = 1.2^l), 10% gross outliers (+-30 px), initial pose perturbed by
+    2 degrees / 0.3 m. Same return tuple as pose_problem."""
+    rng = np.random.default_rng(seed)
+    fx, fy, cx, cy, bf = cam
+    Rt = _rodrigues(rng.normal(0, 0.1, 3))
+    tt = rng.normal(0, 3.0, 3)
+    Xc = np.stack([rng.uniform(-15, 15, n), rng.uniform(-3, 3, n), rng.uniform(5, 40, n)], 1)
+    Xw = (Xc - tt) @ Rt
+    u = fx * Xc[:, 0] / Xc[:, 2] + cx
+    v = fy * Xc[:, 1] / Xc[:, 2] + cy
+    octave = rng.integers(0, nlevels, n).astype(np.int32)
+    sig = np.power(scale_factor, octave)
+    uo, vo = u + rng.normal(0, 1, n) * sig, v + rng.normal(0, 1, n) * sig
+    stereo = rng.uniform(0, 1, n) < 0.6
+    uro = np.where(stereo, u - bf / Xc[:, 2] + rng.normal(0, 1, n) * sig, -1.0)
+    bad = rng.uniform(0, 1, n) < 0.1
+    uo = np.where(bad, uo + rng.choice([-30.0, 30.0], n), uo)
+    vo = np.where(bad, vo + rng.choice([-30.0, 30.0], n), vo)
+    uro = np.where(bad & stereo, uro + rng.choice([-30.0, 30.0], n), uro)
+    from .slamgpu import POSE_EDGE_DTYPE
+    edges = np.zeros(n, POSE_EDGE_DTYPE)
+    edges["xw"] = Xw.astype(np.float32)
+    edges["u"], edges["v"], edges["ur"] = uo, vo, uro
+    edges["octave"] = octave
+    T_true = np.eye(4)
+    T_true[:3, :3], T_true[:3, 3] = Rt, tt
+    axis = rng.normal(size=3)
+    axis /= np.linalg.norm(axis)
+    tdir = rng.normal(size=3)
+    tdir /= np.linalg.norm(tdir)
+    T0 = np.eye(4)
+    T0[:3, :3] = _rodrigues(np.deg2rad(2.0) * axis) @ Rt
+    T0[:3, 3] = tt + 0.3 * tdir
+    return edges, T0.astype(np.float32), T_true, level_inv_sigma2(scale_factor, nlevels), bad
+
+
+def c5_problem(seed: int = 11, **kw):
+    """SURVEY.md section 8(d) C5, the LocalBundleAdjustment bench workload: 20 free + 5 fixed
+    keyframes on a forward trajectory with 1 m spacing (the oldest, keyframe 0, among the fixed),
+    3000 points each seen by 2-6 keyframes (about 12k edges), the C4 noise model."""
+    args = dict(n_local=20, n_fixed=5, n_points=3000, max_obs=6, spacing=1.0)
+    args.update(kw)
+    return ba_problem(seed, **args)
+
+
 def pose_batch(seed: int, n_frames: int, n: int = 2000, **kw):
     """n_frames independent pose problems packed as the device call takes them: edges of frame f
     at [start[f], start[f+1]), poses (n_frames, 4, 4) f32."""
@@ -187,12 +237,13 @@ def pose_batch(seed: int, n_frames: int, n: int = 2000, **kw):
 def ba_problem(seed: int, n_local: int = 20, n_fixed: int = 6, n_points: int = 3000,
                max_obs: int = 6, stereo_frac: float = 0.6, outlier_frac: float = 0.05,
                noise_px: float = 0.7, rot_err: float = 0.003, trans_err: float = 0.03,
-               point_err: float = 0.05, first_local_fixed: bool = False, cam=KITTI_CAM,
+               point_err: float = 0.05, first_local_fixed: bool = False, spacing: float = 1.2,
+               cam=KITTI_CAM,
                cols: int = KITTI_COLS, rows: int = KITTI_ROWS, nlevels: int = 8,
                scale_factor: float = 1.2):
     """One LocalBundleAdjustment input (configs[4]: 20 keyframes x 3000 map points).
 
-    A KITTI-like drive: keyframe k sits 1.2 m further along z with a slow yaw. The n_fixed
+    A KITTI-like drive: keyframe k sits `spacing` m further along z with a slow yaw. The n_fixed
     oldest keyframes are fixed cameras (kf_mode 2), the n_local newest the local window
     (kf_mode 0; the first one 1 = local but fixed, like keyframe id 0, if first_local_fixed).
     Each map point lies ahead of the window and is observed by 2..max_obs keyframes that see it
@@ -208,7 +259,7 @@ def ba_problem(seed: int, n_local: int = 20, n_fixed: int = 6, n_points: int = 3
     for k in range(n_kf):
         yaw = 0.01 * k
         R_wc = _rodrigues(np.array([0.0, yaw, 0.0]))
-        c = np.array([3.0 * np.sin(0.01 * k), 0.0, 1.2 * k])
+        c = np.array([3.0 * np.sin(0.01 * k), 0.0, spacing * k])
         Rs.append(R_wc.T)  # Rcw
         cs.append(c)
     T_true = np.zeros((n_kf, 4, 4))

@@ -55,6 +55,16 @@ def test_local_ba_host_matches_oracle(oracle, gpu_lib, seed, nl, nf, npt, sf, of
     assert its > 0
 
 
+def test_local_ba_c5_matches_oracle(oracle, gpu_lib):
+    """20 free + 5 fixed keyframes, 3000 points, seed 11."""
+    P = S.c5_problem(11)
+    kf_o, pts_o, er_o, _ = oracle.local_ba(CAM, P)
+    kf, pts, er, its = run_host(gpu_lib, P)
+    assert np.array_equal(er, er_o)
+    assert_close(kf, kf_o, P["kf_Tcw"], "C5 poses")
+    assert_close(pts, pts_o, P["points"], "C5 points")
+
+
 def test_local_ba_stop_flag_leaves_inputs(gpu_lib):
     P = S.ba_problem(7, n_local=4, n_fixed=1, n_points=100)
     kf, pts, er, its = run_host(gpu_lib, P, stop=True)

@@ -48,6 +48,16 @@ def test_pose_optimization_host_matches_oracle(oracle, gpu_lib, seed, n, sf, of,
     assert_pose_close(T, T_o, T0, f"seed {seed}")
 
 
+@pytest.mark.parametrize("seed", [7, 8, 9])
+def test_pose_optimization_c4_matches_oracle(oracle, gpu_lib, seed):
+    """2 deg / 0.3 m start, +-30 px gross outliers."""
+    edges, T0, _, isig, _ = S.c4_problem(seed)
+    r_o, T_o, out_o, _ = oracle.pose_optimization(CAM, isig, edges, T0)
+    r, T, out = gpu_lib.Optimizer.PoseOptimization(edges, T0, CAM, isig)
+    assert r == r_o and np.array_equal(out, out_o)
+    assert_pose_close(T, T_o, T0, f"C4 seed {seed}")
+
+
 def test_pose_optimization_too_few_edges(gpu_lib):
     edges, T0, _, isig, _ = S.pose_problem(3, 2)
     r, T, out = gpu_lib.Optimizer.PoseOptimization(edges, T0, CAM, isig)

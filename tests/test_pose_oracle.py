@@ -142,3 +142,12 @@ def test_fewer_than_ten_edges_runs_one_round():
     r, T, outl, its = O.pose_optimization(CAM, isig, edges, T0)
     assert r == 9 and its <= 10  # one round of at most 10 LM iterations
     np.testing.assert_allclose(T[:3, 3], Tt[:3, 3], atol=1e-4)
+
+
+def test_c4_workload_converges():
+    """SURVEY 8(d) C4 (2 deg / 0.3 m start, 10% +-30 px outliers): the optimiser recovers the
+    pose to a few mm."""
+    edges, T0, Tt, isig, bad = S.c4_problem(7)
+    r, T, outl, _ = O.pose_optimization(CAM, isig, edges, T0)
+    assert np.abs(T[:3, 3] - Tt[:3, 3]).max() < 0.02
+    assert (outl == bad).mean() > 0.9
