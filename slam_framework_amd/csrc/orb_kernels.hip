@@ -520,7 +520,6 @@ __global__ __launch_bounds__(256) void fast_cells_kernel(ImageBatch b,
   uint8_t* sc = tile + ((kTileStride * g->fast_tile_rows + 15) & ~15);
   uint16_t* cand =
       reinterpret_cast<uint16_t*>(sc + ((kScoreStride * g->fast_score_rows + 15) & ~15));
-  const int tmin = min(g->ini_th, g->min_th);
 
   // ---- tile prefetch: aligned dwords covering [ini_x & ~3, ini_x + vw) x [ini_y, ini_y + vh)
   // into registers, lane = (row within a step, dword): each element is a scalar row base plus a
@@ -579,8 +578,10 @@ __global__ __launch_bounds__(256) void fast_cells_kernel(ImageBatch b,
 #pragma unroll 4
     for (int rz = plr - 1; rz <= dh; rz += kRps)
       *reinterpret_cast<uint32_t*>(sc1 + rz * kScoreStride + 4 * pld) = 0;
-    // ---- prefilter every detect pixel at the lower threshold, 4 pixels (one tile dword) per
-    // lane; compacts survivors in row-major order.
+    // ---- one FAST pass at threshold th: prefilter every detect pixel (4 pixels, one tile dword,
+    // per lane; survivors compacted in row-major order), exact score of the survivors into the
+    // score map, NMS at th, survivors out in row-major order. The score map keeps the scores of
+    // earlier passes (same values: s does not depend on the threshold).
     // Detect pixel (rr, col): tile row rr + 3, tile column col in [off + 3, off + 3 + dw).
     const int q_lo = (off + 3) >> 2, q_hi = (off + 2 + dw) >> 2;
     const int nq = q_hi - q_lo + 1;
@@ -590,127 +591,120 @@ __global__ __launch_bounds__(256) void fast_cells_kernel(ImageBatch b,
     const uint32_t vmask =
         (uint32_t)(((1ull << (8 * bhi)) - 1) & ~((1ull << (8 * blo)) - 1)) & kH;
     const int qm = max(Q - 1, 0) - Q;  // dword step left (clamped at the tile edge)
-    int ncand = 0;
-    for (int r0 = 0; r0 < dh; r0 += rows_per) {
-      const int rr = r0 + lr;
-      uint32_t m = 0;
-      if (lr < rows_per && rr < dh) {
-        const uint8_t* row = tile + (rr + 3) * kTileStride + 4 * Q;
-        auto rd = [&](int dy, int dq) {
-          return *reinterpret_cast<const uint32_t*>(row + dy * kTileStride + 4 * dq);
-        };
-        const uint32_t c = rd(0, 0), cm = rd(0, qm), cp = rd(0, 1);
-        const uint32_t u2 = rd(2, 0), u2m = rd(2, qm), u2p = rd(2, 1);
-        const uint32_t d2 = rd(-2, 0), d2m = rd(-2, qm), d2p = rd(-2, 1);
-        const uint32_t p0 = rd(3, 0), p8 = rd(-3, 0);
-        // even pixels (bytes 0, 2) and odd pixels (bytes 1, 3) of each ring position as u16
-        // pairs; v_perm picks the shifted bytes straight out of two adjacent dwords
-        typedef unsigned short u16x2_t __attribute__((ext_vector_type(2)));
-        auto U = [](uint32_t x) { return __builtin_bit_cast(u16x2_t, x); };
-        const u16x2_t tt2 = U((uint32_t)tmin * 0x10001u);
-        uint32_t any[2];
-#pragma unroll
-        for (int h = 0; h < 2; h++) {
-          const uint32_t sh = h ? 0x00010001u : 0u;  // odd pixels: data selectors + 1
-          const uint32_t s0 = 0x0c020c00u + sh, s1 = 0x0c030c01u + sh, s2 = 0x0c040c02u + sh,
-                         s3 = 0x0c050c03u + sh;
-          const u16x2_t v = U(__builtin_amdgcn_perm(c, c, s0));
-          const u16x2_t a0 = U(__builtin_amdgcn_perm(p0, p0, s0));      // (0, +3)
-          const u16x2_t a8 = U(__builtin_amdgcn_perm(p8, p8, s0));      // (0, -3)
-          const u16x2_t a4 = U(__builtin_amdgcn_perm(cp, c, s3));       // (+3, 0)
-          const u16x2_t a12 = U(__builtin_amdgcn_perm(c, cm, s1));      // (-3, 0)
-          const u16x2_t a2 = U(__builtin_amdgcn_perm(u2p, u2, s2));     // (+2, +2)
-          const u16x2_t a14 = U(__builtin_amdgcn_perm(u2, u2m, s2));    // (-2, +2)
-          const u16x2_t a6 = U(__builtin_amdgcn_perm(d2p, d2, s2));     // (+2, -2)
-          const u16x2_t a10 = U(__builtin_amdgcn_perm(d2, d2m, s2));    // (-2, -2)
-          // FAST_t pre-test on the 4 opposite pairs: darker needs min(pair) < v - t for all
-          // pairs, brighter needs max(pair) > v + t for all pairs
-          const u16x2_t D = __builtin_elementwise_max(
-              __builtin_elementwise_max(__builtin_elementwise_min(a0, a8), __builtin_elementwise_min(a4, a12)),
-              __builtin_elementwise_max(__builtin_elementwise_min(a2, a10), __builtin_elementwise_min(a6, a14)));
-          const u16x2_t B = __builtin_elementwise_min(
-              __builtin_elementwise_min(__builtin_elementwise_max(a0, a8), __builtin_elementwise_max(a4, a12)),
-              __builtin_elementwise_min(__builtin_elementwise_max(a2, a10), __builtin_elementwise_max(a6, a14)));
-          const u16x2_t lo = __builtin_elementwise_sub_sat(v, tt2), hi = v + tt2;
-          any[h] = __builtin_bit_cast(uint32_t, __builtin_elementwise_sub_sat(lo, D)) |
-                   __builtin_bit_cast(uint32_t, __builtin_elementwise_sub_sat(B, hi));
-        }
-        // non-zero u16 lane -> bit 7 of that pixel's byte
-        m = ((((any[0] + 0x7fff7fffu) & 0x80008000u) >> 8) | ((any[1] + 0x7fff7fffu) & 0x80008000u)) &
-            vmask;
-      }
-      // row-major compaction: exclusive prefix of per-lane counts (0..4) via 3 ballots
-      const int cnt = __popc(m);
-      const uint64_t b0 = __ballot(cnt & 1), b1 = __ballot(cnt & 2), b2 = __ballot(cnt & 4);
-      int pos = ncand + lanes_below(b0) + 2 * lanes_below(b1) + 4 * lanes_below(b2);
-      const int pix0 = rr * kScoreStride + 4 * Q;
-#pragma unroll
-      for (int bb = 0; bb < 4; bb++)
-        if (m & (0x80u << (8 * bb))) cand[pos++] = (uint16_t)(pix0 + bb);
-      ncand += __popcll(b0) + 2 * __popcll(b1) + 4 * __popcll(b2);
-    }
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    // ---- exact FAST score of the survivors
-    for (int i = lane; i < ncand; i += 64) {
-      const int pix = cand[i];
-      const int r = pix / kScoreStride, cc = pix - r * kScoreStride;
-      const int s = fast_s_pk<TS>(tile, (r + 3) * kTileStride + cc);
-      sc1[pix] = (uint8_t)(s < 0 ? 0 : s);
-    }
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-    __builtin_amdgcn_wave_barrier();
     uint32_t* out = cell_keys + slot * g->cell_cap;
-    // NMS at iniTh and at minTh in one sweep: the reference re-runs FAST at minTh when the iniTh
-    // *output* (after NMS) is empty (:753-757). cv::FAST keeps p at threshold t iff
-    // s - 1 > ns for all 8 neighbours, ns = (q > t ? q - 1 : 0), zero outside the detect area;
-    // non-candidates have s <= tmin (score 0). With Q = max of the 8 neighbours' s that is
-    //   s > t  &&  s >= 2  &&  Q < max(s, t + 1),
-    // so one 3x3 byte maximum (zero-framed map, no bounds checks) serves both thresholds.
-    // iniTh survivors go straight out, minTh survivors are compacted in place in cand[].
-    const int t0 = g->ini_th, t1 = g->min_th;
-    int count0 = 0, count1 = 0;
-    for (int i0 = 0; i0 < ncand; i0 += 64) {
-      const int i = i0 + lane;
-      bool k0 = false, k1 = false;
-      int s = 0, r = 0, cc = 0, pix = 0;
-      if (i < ncand) {
-        pix = cand[i];
-        r = pix / kScoreStride;
-        cc = pix - r * kScoreStride;
-        const uint8_t* nb = sc1 + pix - kScoreStride - 1;  // (r - 1, cc - 1)
-        const int al = (int)((uintptr_t)nb & 3);
-        const uint32_t* nw = reinterpret_cast<const uint32_t*>(nb - al);
-        constexpr int kW = kScoreStride / 4;
-        const uint32_t rA = __builtin_amdgcn_alignbyte(nw[1], nw[0], al);
-        const uint32_t rB = __builtin_amdgcn_alignbyte(nw[kW + 1], nw[kW], al);
-        const uint32_t rC = __builtin_amdgcn_alignbyte(nw[2 * kW + 1], nw[2 * kW], al);
-        s = (rB >> 8) & 255;
-        const int q = max(max(max3((int)(rA & 255), (int)((rA >> 8) & 255), (int)((rA >> 16) & 255)),
-                              max((int)(rB & 255), (int)((rB >> 16) & 255))),
-                          max3((int)(rC & 255), (int)((rC >> 8) & 255), (int)((rC >> 16) & 255)));
-        k0 = s > t0 && s >= 2 && q < max(s, t0 + 1);
-        k1 = s > t1 && s >= 2 && q < max(s, t1 + 1);
+    auto fast_pass = [&](int th) -> int {
+      int ncand = 0;
+      for (int r0 = 0; r0 < dh; r0 += rows_per) {
+        const int rr = r0 + lr;
+        uint32_t m = 0;
+        if (lr < rows_per && rr < dh) {
+          const uint8_t* row = tile + (rr + 3) * kTileStride + 4 * Q;
+          auto rd = [&](int dy, int dq) {
+            return *reinterpret_cast<const uint32_t*>(row + dy * kTileStride + 4 * dq);
+          };
+          const uint32_t c = rd(0, 0), cm = rd(0, qm), cp = rd(0, 1);
+          const uint32_t u2 = rd(2, 0), u2m = rd(2, qm), u2p = rd(2, 1);
+          const uint32_t d2 = rd(-2, 0), d2m = rd(-2, qm), d2p = rd(-2, 1);
+          const uint32_t p0 = rd(3, 0), p8 = rd(-3, 0);
+          // even pixels (bytes 0, 2) and odd pixels (bytes 1, 3) of each ring position as u16
+          // pairs; v_perm picks the shifted bytes straight out of two adjacent dwords
+          typedef unsigned short u16x2_t __attribute__((ext_vector_type(2)));
+          auto U = [](uint32_t x) { return __builtin_bit_cast(u16x2_t, x); };
+          const u16x2_t tt2 = U((uint32_t)th * 0x10001u);
+          uint32_t any[2];
+#pragma unroll
+          for (int h = 0; h < 2; h++) {
+            const uint32_t sh = h ? 0x00010001u : 0u;  // odd pixels: data selectors + 1
+            const uint32_t s0 = 0x0c020c00u + sh, s1 = 0x0c030c01u + sh, s2 = 0x0c040c02u + sh,
+                           s3 = 0x0c050c03u + sh;
+            const u16x2_t v = U(__builtin_amdgcn_perm(c, c, s0));
+            const u16x2_t a0 = U(__builtin_amdgcn_perm(p0, p0, s0));      // (0, +3)
+            const u16x2_t a8 = U(__builtin_amdgcn_perm(p8, p8, s0));      // (0, -3)
+            const u16x2_t a4 = U(__builtin_amdgcn_perm(cp, c, s3));       // (+3, 0)
+            const u16x2_t a12 = U(__builtin_amdgcn_perm(c, cm, s1));      // (-3, 0)
+            const u16x2_t a2 = U(__builtin_amdgcn_perm(u2p, u2, s2));     // (+2, +2)
+            const u16x2_t a14 = U(__builtin_amdgcn_perm(u2, u2m, s2));    // (-2, +2)
+            const u16x2_t a6 = U(__builtin_amdgcn_perm(d2p, d2, s2));     // (+2, -2)
+            const u16x2_t a10 = U(__builtin_amdgcn_perm(d2, d2m, s2));    // (-2, -2)
+            // FAST_t pre-test on the 4 opposite pairs: darker needs min(pair) < v - t for all
+            // pairs, brighter needs max(pair) > v + t for all pairs
+            const u16x2_t D = __builtin_elementwise_max(
+                __builtin_elementwise_max(__builtin_elementwise_min(a0, a8), __builtin_elementwise_min(a4, a12)),
+                __builtin_elementwise_max(__builtin_elementwise_min(a2, a10), __builtin_elementwise_min(a6, a14)));
+            const u16x2_t B = __builtin_elementwise_min(
+                __builtin_elementwise_min(__builtin_elementwise_max(a0, a8), __builtin_elementwise_max(a4, a12)),
+                __builtin_elementwise_min(__builtin_elementwise_max(a2, a10), __builtin_elementwise_max(a6, a14)));
+            const u16x2_t lo = __builtin_elementwise_sub_sat(v, tt2), hi = v + tt2;
+            any[h] = __builtin_bit_cast(uint32_t, __builtin_elementwise_sub_sat(lo, D)) |
+                     __builtin_bit_cast(uint32_t, __builtin_elementwise_sub_sat(B, hi));
+          }
+          // non-zero u16 lane -> bit 7 of that pixel's byte
+          m = ((((any[0] + 0x7fff7fffu) & 0x80008000u) >> 8) | ((any[1] + 0x7fff7fffu) & 0x80008000u)) &
+              vmask;
+        }
+        // row-major compaction: exclusive prefix of per-lane counts (0..4) via 3 ballots
+        const int cnt = __popc(m);
+        const uint64_t b0 = __ballot(cnt & 1), b1 = __ballot(cnt & 2), b2 = __ballot(cnt & 4);
+        int pos = ncand + lanes_below(b0) + 2 * lanes_below(b1) + 4 * lanes_below(b2);
+        const int pix0 = rr * kScoreStride + 4 * Q;
+#pragma unroll
+        for (int bb = 0; bb < 4; bb++)
+          if (m & (0x80u << (8 * bb))) cand[pos++] = (uint16_t)(pix0 + bb);
+        ncand += __popcll(b0) + 2 * __popcll(b1) + 4 * __popcll(b2);
       }
-      const uint64_t m0 = __ballot(k0), m1 = __ballot(k1);
-      if (k0) {
-        const int pos = count0 + lanes_below(m0);
-        if (pos < g->cell_cap) out[pos] = pack_key(v.ax + cc - kMinBorder, v.ini_y + 3 + r - kMinBorder, s - 1);
-      }
-      if (k1) cand[count1 + lanes_below(m1)] = (uint16_t)pix;  // never passes the read index
-      count0 += __popcll(m0);
-      count1 += __popcll(m1);
-    }
-    int count = count0;
-    if (count0 == 0) {
       __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
       __builtin_amdgcn_wave_barrier();
-      for (int i = lane; i < min(count1, g->cell_cap); i += 64) {
+      // exact FAST score of the survivors
+      for (int i = lane; i < ncand; i += 64) {
         const int pix = cand[i];
         const int r = pix / kScoreStride, cc = pix - r * kScoreStride;
-        out[i] = pack_key(v.ax + cc - kMinBorder, v.ini_y + 3 + r - kMinBorder, sc1[pix] - 1);
+        const int sv = fast_s_pk<TS>(tile, (r + 3) * kTileStride + cc);
+        sc1[pix] = (uint8_t)(sv < 0 ? 0 : sv);
       }
-      count = count1;
+      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      // NMS at th: cv::FAST keeps p iff s - 1 > ns for all 8 neighbours, ns = (q > th ? q - 1 :
+      // 0), zero outside the detect area. With Q = max of the 8 neighbours' s that is
+      //   s > th  &&  s >= 2  &&  Q < max(s, th + 1),
+      // and a neighbour this pass did not score has s <= th < s_p, so it cannot change the test.
+      int count = 0;
+      for (int i0 = 0; i0 < ncand; i0 += 64) {
+        const int i = i0 + lane;
+        bool keep = false;
+        int sv = 0, r = 0, cc = 0;
+        if (i < ncand) {
+          const int pix = cand[i];
+          r = pix / kScoreStride;
+          cc = pix - r * kScoreStride;
+          const uint8_t* nb = sc1 + pix - kScoreStride - 1;  // (r - 1, cc - 1)
+          const int al = (int)((uintptr_t)nb & 3);
+          const uint32_t* nw = reinterpret_cast<const uint32_t*>(nb - al);
+          constexpr int kW = kScoreStride / 4;
+          const uint32_t rA = __builtin_amdgcn_alignbyte(nw[1], nw[0], al);
+          const uint32_t rB = __builtin_amdgcn_alignbyte(nw[kW + 1], nw[kW], al);
+          const uint32_t rC = __builtin_amdgcn_alignbyte(nw[2 * kW + 1], nw[2 * kW], al);
+          sv = (rB >> 8) & 255;
+          const int q = max(max(max3((int)(rA & 255), (int)((rA >> 8) & 255), (int)((rA >> 16) & 255)),
+                                max((int)(rB & 255), (int)((rB >> 16) & 255))),
+                            max3((int)(rC & 255), (int)((rC >> 8) & 255), (int)((rC >> 16) & 255)));
+          keep = sv > th && sv >= 2 && q < max(sv, th + 1);
+        }
+        const uint64_t mk = __ballot(keep);
+        if (keep) {
+          const int pos = count + lanes_below(mk);
+          if (pos < g->cell_cap) out[pos] = pack_key(v.ax + cc - kMinBorder, v.ini_y + 3 + r - kMinBorder, sv - 1);
+        }
+        count += __popcll(mk);
+      }
+      return count;
+    };
+    // FAST at iniTh; the reference re-runs the whole cell at minTh when the iniTh output (after
+    // NMS) is empty (:753-757)
+    int count = fast_pass(g->ini_th);
+    if (count == 0) {
+      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      count = fast_pass(g->min_th);
     }
     if (lane == 0) {
       if (count > g->cell_cap) {
