@@ -37,6 +37,24 @@ LEVEL_PX = None  # filled from the context geometry
 
 
 TRAFFIC_FILE = os.path.join(ROOT, "profiles", "traffic.json")
+VALU_FILE = os.path.join(ROOT, "profiles", "valu.json")
+
+
+def measured_valu(kernel, batch):
+    """SQ_INSTS_VALU per dispatch of `kernel` (tools/pmc_valu.sh + tools/valu.py, committed as
+    profiles/valu.json) and the chip's VALU issue peak; (None, None) when absent or measured on
+    another batch size."""
+    try:
+        with open(VALU_FILE) as f:
+            d = json.load(f)
+    except (OSError, ValueError):
+        return None, None
+    if d.get("batch") != batch:
+        return None, None
+    for k, v in d.get("kernels", {}).items():
+        if k.split("<")[0].replace("_kernel", "") == kernel:
+            return v.get("sq_insts_valu_per_dispatch"), d.get("valu_issue_peak_per_s")
+    return None, None
 
 
 def measured_traffic(kernel, batch):
@@ -215,6 +233,15 @@ def main():
         if traffic is not None:
             roofline["traffic"] = round(traffic)
             roofline["traffic_source"] = tsrc
+        # the pipe that actually binds this integer kernel: VALU issue (PMC instruction count per
+        # dispatch over the live-measured dispatch time)
+        vi, vpeak = measured_valu(dominant, B)
+        if vi is not None:
+            rate = vi / avg_launch_s
+            roofline["valu_issue"] = {"wave_instr_per_launch": round(vi), "achieved": rate,
+                                      "peak": vpeak, "unit": "wave-instr/s",
+                                      "frac": round(rate / vpeak, 4),
+                                      "source": "profiles/valu.json"}
         cpu = None
         if not args.no_cpu_baseline:
             cpu = cpu_baseline(Ls, Rs, args.cpu_frames)
