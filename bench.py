@@ -400,7 +400,44 @@ def bench_local_ba(dev, with_cpu):
         run()
         torch.cuda.synchronize()
         res[B] = (_events_ms(run, stream, 3), int(d_st[0].item()))
-    out = {"workload": "configs[4]: LocalBundleAdjustment on SURVEY 8(d) C5, 20 local + 5 fixed "
+    # the batched reprojection residual / Jacobian / normal-equation build on its own (one
+    # computeActiveErrors + buildSystem of the first optimize() per problem), 256 problems
+    BL = 256
+    desc = np.array([(i * nk, nk, i * npn, npn) for i in range(BL)], np.int32)
+    start = np.concatenate([P["point_obs_start"][:-1] + i * no for i in range(BL)] +
+                           [[BL * no]]).astype(np.int32)
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a).view(np.uint8).copy()).to(dev)
+    d_desc, d_mode, d_start = t(desc), t(np.tile(P["kf_mode"], BL)), t(start)
+    d_obs, d_kf, d_pts = t(np.tile(P["obs"], BL)), t(np.tile(P["kf_Tcw"], (BL, 1, 1))), t(
+        np.tile(P["points"], (BL, 1)))
+    f64 = lambda *sh: torch.empty(sh, dtype=torch.float64, device=dev)
+    lin = {"chi2": f64(BL * no), "hpl": f64(BL * no, 18), "hll": f64(BL * npn, 6),
+           "bl": f64(BL * npn, 3), "hpp": f64(BL * nk, 21), "bp": f64(BL * nk, 6), "chi": f64(BL)}
+    d_st = torch.zeros(BL, dtype=torch.int32, device=dev)
+    d_ws = torch.empty(G.local_ba_workspace_bytes(BL * nk, BL * npn, BL * no), dtype=torch.uint8,
+                       device=dev)
+
+    def lin_run():
+        G.local_ba_linearize_device(S.KITTI_CAM, P["inv_sigma2"], d_desc, BL, d_kf, d_mode, d_pts,
+                                    d_start, d_obs, lin, d_st, d_ws, BL * nk, BL * npn, BL * no,
+                                    stream=stream.cuda_stream)
+    lin_run()
+    torch.cuda.synchronize()
+    lms = _events_ms(lin_run, stream, 5)
+    # algorithmic bytes: observation in (20 B) + chi2 and the 6x3 block out (8 + 144 B); point in
+    # (12 B) + its 3x3 block and b out (72 B); keyframe pose in (64 B) + 6x6 block and b out (216 B)
+    lin_bytes = BL * (no * (20 + 8 + 144) + npn * (12 + 72) + nk * (64 + 216))
+    lin_gbs = lin_bytes / (lms * 1e-3) / 1e9
+    out_lin = {"workload": "LocalBA residual/Jacobian/normal-equation build (computeActiveErrors + "
+                           f"buildSystem), {BL} C5 problems", "batch_problems": BL,
+               "ms_per_batch": round(lms, 3), "observations_per_s": round(BL * no / lms * 1e3),
+               "roofline": {"kernel": "local_ba_linearize", "bound": "hbm",
+                            "achieved": round(lin_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                            "frac": round(lin_gbs / HBM_PEAK_GBS, 4),
+                            "algorithmic_bytes_per_launch": lin_bytes}}
+    del d_ws, lin
+    out = {"linearize": out_lin,
+           "workload": "configs[4]: LocalBundleAdjustment on SURVEY 8(d) C5, 20 local + 5 fixed "
                        f"keyframes x 3000 map points ({no} observations), 5 robust + 10 LM "
                        "iterations (FP64)",
            "problems_per_s": round(64 / res[64][0] * 1e3, 1), "batch_problems": 64,

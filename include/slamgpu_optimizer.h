@@ -121,6 +121,35 @@ int slamgpu_local_bundle_adjustment_device(
     size_t workspace_bytes, int total_kf, int total_points, int total_obs,
     const int32_t* d_stop_flag, void* stream);
 
+/* The reprojection residual / Jacobian / normal-equation build of LocalBundleAdjustment's first
+ * optimize() (SparseOptimizer::computeActiveErrors + activeRobustChi2 + BlockSolver::buildSystem,
+ * sparse_optimizer.cpp:61-114, block_solver.hpp:499-556, base_binary_edge.hpp:55-122) at the
+ * input estimates, every edge at level 0 with its Huber kernel: the step every LM iteration of
+ * the solver repeats, batched over problems. All arrays are device memory, doubles:
+ *   chi2[obs], hpl[obs][18] (6x3 pose-point block, row-major; 0 for fixed keyframes),
+ *   hll[points][6] and bl[points][3] (point block, packed 00 01 02 11 12 22, and b),
+ *   hpp[keyframes][21] and bp[keyframes][6] (pose block, packed upper triangle row by row, and
+ *   b; 0 unless kf_mode is SLAMGPU_KF_LOCAL), chi[problems] (the robust chi2).
+ * g2o's sign convention: b = -J^T (rho' Omega) e. d_status[p]: 0 or the error codes of
+ * slamgpu_local_bundle_adjustment_device. */
+typedef struct {
+  double* chi2;
+  double* hpl;
+  double* hll;
+  double* bl;
+  double* hpp;
+  double* bp;
+  double* chi;
+} slamgpu_ba_linear;
+
+int slamgpu_local_ba_linearize_device(
+    const slamgpu_camera* cam, const float* inv_sigma2, int nlevels,
+    const slamgpu_ba_problem* d_problems, int n_problems, const float* d_kf_Tcw,
+    const uint8_t* d_kf_mode, const float* d_points, const int32_t* d_point_obs_start,
+    const slamgpu_ba_obs* d_obs, const slamgpu_ba_linear* out, int32_t* d_status,
+    void* d_workspace, size_t workspace_bytes, int total_kf, int total_points, int total_obs,
+    void* stream);
+
 const char* slamgpu_optimizer_last_error(void);
 
 #ifdef __cplusplus

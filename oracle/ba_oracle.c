@@ -420,6 +420,65 @@ static int depth_positive(const ba* B, int e) {  // isDepthPositive at the curre
   return Xc[2] > 0.0;
 }
 
+static void ba_init(ba* B, const float cam[5], const float* inv_sigma2, const float* kf_Tcw,
+                    const uint8_t* kf_mode, int n_kf, const float* points, int n_points,
+                    const int32_t* point_obs_start, const oc_ba_obs* obs) {
+  const int n_obs = point_obs_start[n_points];
+  memset(B, 0, sizeof(*B));
+  B->n_kf = n_kf;
+  B->n_pts = n_points;
+  B->n_obs = n_obs;
+  B->obs = obs;
+  B->pstart = point_obs_start;
+  for (int i = 0; i < 5; i++) B->cam[i] = cam[i];
+  B->bf_f = cam[4];
+  B->isig = inv_sigma2;
+  B->opoint = (int32_t*)malloc(sizeof(int32_t) * (n_obs + 1));
+  B->free_idx = (int*)malloc(sizeof(int) * (n_kf + 1));
+  B->T = (se3*)malloc(sizeof(se3) * (n_kf + 1));
+  B->X = (double*)malloc(sizeof(double) * (3 * n_points + 1));
+  B->active = (uint8_t*)malloc(n_obs + 1);
+  B->err = (double*)calloc(3 * n_obs + 1, sizeof(double));
+  B->chi2 = (double*)calloc(n_obs + 1, sizeof(double));
+  B->kf_nact = (int*)calloc(n_kf + 1, sizeof(int));
+  B->pt_nact = (int*)calloc(n_points + 1, sizeof(int));
+  for (int p = 0; p < n_points; p++)
+    for (int e = point_obs_start[p]; e < point_obs_start[p + 1]; e++) B->opoint[e] = p;
+  for (int k = 0; k < n_kf; k++) {
+    B->free_idx[k] = kf_mode[k] == 0 ? B->n_free++ : -1;
+    double R[9], t[3];
+    for (int i = 0; i < 3; i++) {
+      for (int j = 0; j < 3; j++) R[3 * i + j] = kf_Tcw[16 * k + 4 * i + j];
+      t[i] = kf_Tcw[16 * k + 4 * i + 3];
+    }
+    B->T[k] = se3_from_Rt(R, t);  // Converter::toSE3Quat(GetPose())
+  }
+  for (int i = 0; i < 3 * n_points; i++) B->X[i] = points[i];
+  B->Hpp = (double*)malloc(sizeof(double) * (36 * B->n_free + 1));
+  B->bp = (double*)malloc(sizeof(double) * (6 * B->n_free + 1));
+  B->Hll = (double*)malloc(sizeof(double) * (9 * n_points + 1));
+  B->bl = (double*)malloc(sizeof(double) * (3 * n_points + 1));
+  B->Hpl = (double*)calloc(18 * (size_t)n_obs + 1, sizeof(double));
+  memset(B->active, 1, n_obs + 1);
+}
+
+static void ba_free(ba* B) {
+  free(B->opoint);
+  free(B->free_idx);
+  free(B->T);
+  free(B->X);
+  free(B->active);
+  free(B->err);
+  free(B->chi2);
+  free(B->kf_nact);
+  free(B->pt_nact);
+  free(B->Hpp);
+  free(B->bp);
+  free(B->Hll);
+  free(B->bl);
+  free(B->Hpl);
+}
+
 int oc_local_bundle_adjustment(const float cam[5], const float* inv_sigma2, float* kf_Tcw,
                                const uint8_t* kf_mode, int n_kf, float* points, int n_points,
                                const int32_t* point_obs_start, const oc_ba_obs* obs,
@@ -428,42 +487,7 @@ int oc_local_bundle_adjustment(const float cam[5], const float* inv_sigma2, floa
   if (n_kf < 0 || n_points < 0 || point_obs_start[0] != 0) return -1;
   const int n_obs = point_obs_start[n_points];
   ba B;
-  memset(&B, 0, sizeof(B));
-  B.n_kf = n_kf;
-  B.n_pts = n_points;
-  B.n_obs = n_obs;
-  B.obs = obs;
-  B.pstart = point_obs_start;
-  for (int i = 0; i < 5; i++) B.cam[i] = cam[i];
-  B.bf_f = cam[4];
-  B.isig = inv_sigma2;
-  B.opoint = (int32_t*)malloc(sizeof(int32_t) * (n_obs + 1));
-  B.free_idx = (int*)malloc(sizeof(int) * (n_kf + 1));
-  B.T = (se3*)malloc(sizeof(se3) * (n_kf + 1));
-  B.X = (double*)malloc(sizeof(double) * (3 * n_points + 1));
-  B.active = (uint8_t*)malloc(n_obs + 1);
-  B.err = (double*)calloc(3 * n_obs + 1, sizeof(double));
-  B.chi2 = (double*)calloc(n_obs + 1, sizeof(double));
-  B.kf_nact = (int*)calloc(n_kf + 1, sizeof(int));
-  B.pt_nact = (int*)calloc(n_points + 1, sizeof(int));
-  for (int p = 0; p < n_points; p++)
-    for (int e = point_obs_start[p]; e < point_obs_start[p + 1]; e++) B.opoint[e] = p;
-  for (int k = 0; k < n_kf; k++) {
-    B.free_idx[k] = kf_mode[k] == 0 ? B.n_free++ : -1;
-    double R[9], t[3];
-    for (int i = 0; i < 3; i++) {
-      for (int j = 0; j < 3; j++) R[3 * i + j] = kf_Tcw[16 * k + 4 * i + j];
-      t[i] = kf_Tcw[16 * k + 4 * i + 3];
-    }
-    B.T[k] = se3_from_Rt(R, t);  // Converter::toSE3Quat(GetPose())
-  }
-  for (int i = 0; i < 3 * n_points; i++) B.X[i] = points[i];
-  B.Hpp = (double*)malloc(sizeof(double) * (36 * B.n_free + 1));
-  B.bp = (double*)malloc(sizeof(double) * (6 * B.n_free + 1));
-  B.Hll = (double*)malloc(sizeof(double) * (9 * n_points + 1));
-  B.bl = (double*)malloc(sizeof(double) * (3 * n_points + 1));
-  B.Hpl = (double*)calloc(18 * (size_t)n_obs + 1, sizeof(double));
-  memset(B.active, 1, n_obs + 1);
+  ba_init(&B, cam, inv_sigma2, kf_Tcw, kf_mode, n_kf, points, n_points, point_obs_start, obs);
 
   B.robust = 1;
   optimize(&B, 5, lm_iterations);  // optimizer.cpp:622-623
@@ -492,20 +516,7 @@ int oc_local_bundle_adjustment(const float cam[5], const float* inv_sigma2, floa
     kf_Tcw[16 * k + 15] = 1.f;
   }
   for (int i = 0; i < 3 * n_points; i++) points[i] = (float)B.X[i];
-  free(B.opoint);
-  free(B.free_idx);
-  free(B.T);
-  free(B.X);
-  free(B.active);
-  free(B.err);
-  free(B.chi2);
-  free(B.kf_nact);
-  free(B.pt_nact);
-  free(B.Hpp);
-  free(B.bp);
-  free(B.Hll);
-  free(B.bl);
-  free(B.Hpl);
+  ba_free(&B);
   return 0;
 }
 
@@ -538,4 +549,36 @@ double oc_ba_edge_eval(const float cam[5], const double R[9], const double t[3],
   const double c = ba_error(&B, 0, err, Xc);
   if (Jl && Jp) ba_jacobians(&B, 0, Jl, Jp);
   return c;
+}
+
+// computeActiveErrors + activeRobustChi2 + buildSystem of the first optimize() (every edge at level
+// 0, Huber kernels on) at the input estimates; the layout of slamgpu_ba_linear.
+double oc_ba_linearize(const float cam[5], const float* inv_sigma2, const float* kf_Tcw,
+                       const uint8_t* kf_mode, int n_kf, const float* points, int n_points,
+                       const int32_t* point_obs_start, const oc_ba_obs* obs, double* chi2,
+                       double* hpl, double* hll, double* bl, double* hpp, double* bp) {
+  ba B;
+  ba_init(&B, cam, inv_sigma2, kf_Tcw, kf_mode, n_kf, points, n_points, point_obs_start, obs);
+  B.robust = 1;
+  compute_active_errors(&B);
+  const double chi = active_robust_chi2(&B);
+  build_system(&B);
+  for (int e = 0; e < B.n_obs; e++) {
+    chi2[e] = B.chi2[e];
+    for (int i = 0; i < 18; i++) hpl[18 * e + i] = B.free_idx[obs[e].keyframe] >= 0 ? B.Hpl[18 * e + i] : 0.0;
+  }
+  static const int s3[6][2] = {{0, 0}, {0, 1}, {0, 2}, {1, 1}, {1, 2}, {2, 2}};
+  for (int p = 0; p < n_points; p++) {
+    for (int i = 0; i < 6; i++) hll[6 * p + i] = B.Hll[9 * p + 3 * s3[i][0] + s3[i][1]];
+    for (int i = 0; i < 3; i++) bl[3 * p + i] = B.bl[3 * p + i];
+  }
+  for (int k = 0; k < n_kf; k++) {
+    const int f = B.free_idx[k];
+    int h = 0;
+    for (int a = 0; a < 6; a++)
+      for (int c = a; c < 6; c++, h++) hpp[21 * k + h] = f >= 0 ? B.Hpp[36 * f + 6 * a + c] : 0.0;
+    for (int i = 0; i < 6; i++) bp[6 * k + i] = f >= 0 ? B.bp[6 * f + i] : 0.0;
+  }
+  ba_free(&B);
+  return chi;
 }

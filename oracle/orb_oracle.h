@@ -189,6 +189,10 @@ int oc_local_bundle_adjustment(const float cam[5], const float* inv_sigma2, floa
                                const uint8_t* kf_mode, int n_kf, float* points, int n_points,
                                const int32_t* point_obs_start, const oc_ba_obs* obs,
                                uint8_t* erase, int* lm_iterations);
+double oc_ba_linearize(const float cam[5], const float* inv_sigma2, const float* kf_Tcw,
+                       const uint8_t* kf_mode, int n_kf, const float* points, int n_points,
+                       const int32_t* point_obs_start, const oc_ba_obs* obs, double* chi2,
+                       double* hpl, double* hll, double* bl, double* hpp, double* bp);
 double oc_ba_edge_eval(const float cam[5], const double R[9], const double t[3], const double X[3],
                        const oc_ba_obs* o, float inv_sigma2, double err[3], double Jl[9],
                        double Jp[18]);

@@ -26,9 +26,27 @@ struct BaWorkspace {
   double* kf;        // [keyframes][64] estimate (q, t, R), backup, Hpp, bp
 };
 
+// Outputs of the linearisation entry point (slamgpu_ba_linear in slamgpu_optimizer.h).
+struct BaLinearOut {
+  double* chi2;  // [obs]
+  double* hpl;   // [obs][18]
+  double* hll;   // [points][6]
+  double* bl;    // [points][3]
+  double* hpp;   // [keyframes][21]
+  double* bp;    // [keyframes][6]
+  double* chi;   // [problems]
+};
+
 // Lays the workspace out from `base` (nullptr: only computes *bytes).
 BaWorkspace ba_workspace_layout(void* base, int total_kf, int total_points, int total_obs,
                                 size_t* bytes);
+
+hipError_t launch_local_ba_linearize(const PoseParams& P, const slamgpu_ba_problem* d_problems,
+                                     int n_problems, const float* d_kf_Tcw,
+                                     const uint8_t* d_kf_mode, const float* d_points,
+                                     const int32_t* d_pstart, const slamgpu_ba_obs* d_obs,
+                                     int32_t* d_status, const BaWorkspace& ws,
+                                     const BaLinearOut& out, hipStream_t st);
 
 hipError_t launch_local_ba(const PoseParams& P, const slamgpu_ba_problem* d_problems,
                            int n_problems, float* d_kf_Tcw, const uint8_t* d_kf_mode,

@@ -315,7 +315,7 @@ __device__ __forceinline__ PtRef ptrec(const Problem& pb, int p) {
 // keyframe (psorted). Per S block (kh >= kl): the list of its point pairs in point order, built
 // with wave ballots and prefix counts (no atomics on positions). A diagonal block (k, k) lists
 // (edge, point): it doubles as keyframe k's edge list.
-__device__ void build_structure(BaShared& sh, const Problem& pb) {
+__device__ void build_structure(BaShared& sh, const Problem& pb, bool diag_only = false) {
   const int tid = threadIdx.x, lane = tid & 63, w = wave_id(), K = sh.K;
   const int nblk = K * (K + 1) / 2;
   for (int b = tid; b < nblk; b += kThreads) {
@@ -354,7 +354,7 @@ __device__ void build_structure(BaShared& sh, const Problem& pb) {
     for (int k = 0; k < K; k++) om |= __ballot((mask >> k) & 1) ? (1u << k) : 0u;
     for (uint32_t a = om; a; a &= a - 1) {
       const int kh = __builtin_ctz(a);
-      for (uint32_t c = om & ((2u << kh) - 1); c; c &= c - 1) {
+      for (uint32_t c = diag_only ? (1u << kh) : om & ((2u << kh) - 1); c; c &= c - 1) {
         const int kl = __builtin_ctz(c);
         const uint64_t bal = __ballot(((mask >> kh) & 1) && ((mask >> kl) & 1));
         if (lane == 0 && bal) atomicAdd(&sh.blk_cnt[tri(kh) + kl], __popcll(bal));
@@ -384,7 +384,7 @@ __device__ void build_structure(BaShared& sh, const Problem& pb) {
     for (int k = 0; k < K; k++) om |= __ballot((mask >> k) & 1) ? (1u << k) : 0u;
     for (uint32_t a = om; a; a &= a - 1) {
       const int kh = __builtin_ctz(a);
-      for (uint32_t c = om & ((2u << kh) - 1); c; c &= c - 1) {
+      for (uint32_t c = diag_only ? (1u << kh) : om & ((2u << kh) - 1); c; c &= c - 1) {
         const int kl = __builtin_ctz(c);
         const uint64_t bal = __ballot(((mask >> kh) & 1) && ((mask >> kl) & 1));
         if (lane == 0) sh.wcnt[w][tri(kh) + kl] = __popcll(bal);
@@ -404,7 +404,7 @@ __device__ void build_structure(BaShared& sh, const Problem& pb) {
     const int s = p < pb.n_pts ? pb.pstart[pb.p0 + p] - pb.o0 : 0;
     for (uint32_t a = om; a; a &= a - 1) {
       const int kh = __builtin_ctz(a);
-      for (uint32_t c = om & ((2u << kh) - 1); c; c &= c - 1) {
+      for (uint32_t c = diag_only ? (1u << kh) : om & ((2u << kh) - 1); c; c &= c - 1) {
         const int kl = __builtin_ctz(c);
         const bool mine = ((mask >> kh) & 1) && ((mask >> kl) & 1);
         const uint64_t bal = __ballot(mine);
@@ -741,18 +741,14 @@ __device__ void factor_solve(BaShared& sh) {
 }
 
 // ---- kernel -----------------------------------------------------------------------------------
-__global__ __launch_bounds__(kThreads) void local_ba_kernel(
-    PoseParams P, const slamgpu_ba_problem* __restrict__ problems, float* __restrict__ kf_Tcw,
-    const uint8_t* __restrict__ kf_mode, float* __restrict__ points,
-    const int32_t* __restrict__ pstart, const slamgpu_ba_obs* __restrict__ obs,
-    uint8_t* __restrict__ erase, int32_t* __restrict__ status, BaWorkspace ws,
-    const int32_t* stop_flag) {
-#pragma clang fp contract(fast)  // tolerance-compared FP64 path
-  __shared__ BaShared sh;
-  __shared__ float isig[SLAMGPU_MAX_LEVELS];
+// Problem setup shared by the kernels: local-keyframe map, validation (status < 0 on error),
+// initial estimates (Converter::toSE3Quat / toVector3d), every edge active.
+__device__ bool ba_setup(BaShared& sh, Problem& pb, float* isig, const PoseParams& P,
+                         const slamgpu_ba_problem* problems, const float* kf_Tcw,
+                         const uint8_t* kf_mode, const float* points, const int32_t* pstart,
+                         const slamgpu_ba_obs* obs, int32_t* status, const BaWorkspace& ws) {
   const int tid = threadIdx.x;
   const slamgpu_ba_problem pr = problems[blockIdx.x];
-  Problem pb;
   pb.obs = obs;
   pb.pstart = pstart;
   pb.p0 = pr.point_begin;
@@ -799,14 +795,8 @@ __global__ __launch_bounds__(kThreads) void local_ba_kernel(
   __syncthreads();
   if (sh.err != 0) {
     if (tid == 0) status[blockIdx.x] = sh.err;
-    return;
+    return false;
   }
-  if (stop_flag && __atomic_load_n(stop_flag, __ATOMIC_RELAXED)) {  // optimizer.cpp:616-618
-    for (int e = tid; e < pb.n_obs; e += kThreads) erase[pb.o0 + e] = 0;
-    if (tid == 0) status[blockIdx.x] = 0;
-    return;
-  }
-  // initial estimates (Converter::toSE3Quat / toVector3d)
   for (int k = tid; k < pb.n_kf; k += kThreads) {
     const float* T = kf_Tcw + (size_t)(pb.k0 + k) * 16;
     double R[9];
@@ -831,6 +821,29 @@ __global__ __launch_bounds__(kThreads) void local_ba_kernel(
   }
   if (tid < kMaxN) sh.xp[tid] = 0.0;
   __syncthreads();
+  return true;
+}
+
+__global__ __launch_bounds__(kThreads) void local_ba_kernel(
+    PoseParams P, const slamgpu_ba_problem* __restrict__ problems, float* __restrict__ kf_Tcw,
+    const uint8_t* __restrict__ kf_mode, float* __restrict__ points,
+    const int32_t* __restrict__ pstart, const slamgpu_ba_obs* __restrict__ obs,
+    uint8_t* __restrict__ erase, int32_t* __restrict__ status, BaWorkspace ws,
+    const int32_t* stop_flag) {
+#pragma clang fp contract(fast)  // tolerance-compared FP64 path
+  __shared__ BaShared sh;
+  __shared__ float isig[SLAMGPU_MAX_LEVELS];
+  const int tid = threadIdx.x;
+  if (stop_flag && __atomic_load_n(stop_flag, __ATOMIC_RELAXED)) {  // optimizer.cpp:616-618
+    const int32_t o0 = pstart[problems[blockIdx.x].point_begin];
+    const int32_t o1 = pstart[problems[blockIdx.x].point_begin + problems[blockIdx.x].n_points];
+    for (int e = o0 + tid; e < o1; e += kThreads) erase[e] = 0;
+    if (tid == 0) status[blockIdx.x] = 0;
+    return;
+  }
+  Problem pb;
+  if (!ba_setup(sh, pb, isig, P, problems, kf_Tcw, kf_mode, points, pstart, obs, status, ws))
+    return;
 
   const int K = sh.K, n = 6 * K;
   int lm_total = 0;
@@ -1060,6 +1073,52 @@ __global__ __launch_bounds__(kThreads) void local_ba_kernel(
   (void)n;
 }
 
+// computeActiveErrors + activeRobustChi2 + buildSystem of LocalBundleAdjustment's first optimize()
+// (every edge at level 0, Huber kernels on) at the input estimates, per problem: the reprojection
+// residual / Jacobian / normal-equation build the LM iterations repeat, on its own.
+__global__ __launch_bounds__(kThreads) void local_ba_linearize_kernel(
+    PoseParams P, const slamgpu_ba_problem* __restrict__ problems,
+    const float* __restrict__ kf_Tcw, const uint8_t* __restrict__ kf_mode,
+    const float* __restrict__ points, const int32_t* __restrict__ pstart,
+    const slamgpu_ba_obs* __restrict__ obs, int32_t* __restrict__ status, BaWorkspace ws,
+    BaLinearOut out) {
+#pragma clang fp contract(fast)
+  __shared__ BaShared sh;
+  __shared__ float isig[SLAMGPU_MAX_LEVELS];
+  const int tid = threadIdx.x;
+  Problem pb;
+  if (!ba_setup(sh, pb, isig, P, problems, kf_Tcw, kf_mode, points, pstart, obs, status, ws))
+    return;
+  build_structure(sh, pb, true);
+  double chi = 0.0, maxd = 0.0, zero = 0.0;
+  linearise_edges(sh, pb, P, isig, true, chi);
+  linearise_keyframes(sh, pb, P, isig, true, maxd);
+  __syncthreads();
+  sum_points(pb, maxd);
+  block_sum2(sh, chi, zero);
+  for (int e = tid; e < pb.n_obs; e += kThreads) {
+    const int ge = pb.o0 + e;
+    out.chi2[ge] = ws.chi2[ge];
+    const bool fr = sh.free_of_kf[obs[ge].keyframe] >= 0;
+    for (int i = 0; i < 18; i++) out.hpl[(size_t)ge * 18 + i] = fr ? ws.hpl[(size_t)ge * 18 + i] : 0.0;
+  }
+  for (int p = tid; p < pb.n_pts; p += kThreads) {
+    const PtRef r = ptrec(pb, p);
+    for (int i = 0; i < 6; i++) out.hll[(size_t)(pb.p0 + p) * 6 + i] = r[PH + i];
+    for (int i = 0; i < 3; i++) out.bl[(size_t)(pb.p0 + p) * 3 + i] = r[PB + i];
+  }
+  for (int k = tid; k < pb.n_kf; k += kThreads) {
+    const double* kr = kfrec(pb, k);
+    const bool fr = sh.free_of_kf[k] >= 0;
+    for (int i = 0; i < 21; i++) out.hpp[(size_t)(pb.k0 + k) * 21 + i] = fr ? kr[KH + i] : 0.0;
+    for (int i = 0; i < 6; i++) out.bp[(size_t)(pb.k0 + k) * 6 + i] = fr ? kr[KB + i] : 0.0;
+  }
+  if (tid == 0) {
+    out.chi[blockIdx.x] = chi;
+    status[blockIdx.x] = 0;
+  }
+}
+
 }  // namespace
 
 BaWorkspace ba_workspace_layout(void* base, int total_kf, int total_points, int total_obs,
@@ -1087,6 +1146,19 @@ BaWorkspace ba_workspace_layout(void* base, int total_kf, int total_points, int 
   w.kf = reinterpret_cast<double*>(take(sizeof(double) * 64 * (size_t)total_kf));
   if (bytes) *bytes = off + 256;
   return w;
+}
+
+hipError_t launch_local_ba_linearize(const PoseParams& P, const slamgpu_ba_problem* d_problems,
+                                     int n_problems, const float* d_kf_Tcw,
+                                     const uint8_t* d_kf_mode, const float* d_points,
+                                     const int32_t* d_pstart, const slamgpu_ba_obs* d_obs,
+                                     int32_t* d_status, const BaWorkspace& ws,
+                                     const BaLinearOut& out, hipStream_t st) {
+  if (n_problems <= 0) return hipSuccess;
+  SLAMGPU_LAUNCH("local_ba_linearize", st, local_ba_linearize_kernel, dim3(n_problems),
+                 dim3(kThreads), 0, st, P, d_problems, d_kf_Tcw, d_kf_mode, d_points, d_pstart,
+                 d_obs, d_status, ws, out);
+  return hipGetLastError();
 }
 
 hipError_t launch_local_ba(const PoseParams& P, const slamgpu_ba_problem* d_problems,

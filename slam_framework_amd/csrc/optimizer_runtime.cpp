@@ -182,6 +182,34 @@ int slamgpu_local_bundle_adjustment_device(
   return 0;
 }
 
+int slamgpu_local_ba_linearize_device(
+    const slamgpu_camera* cam, const float* inv_sigma2, int nlevels,
+    const slamgpu_ba_problem* d_problems, int n_problems, const float* d_kf_Tcw,
+    const uint8_t* d_kf_mode, const float* d_points, const int32_t* d_point_obs_start,
+    const slamgpu_ba_obs* d_obs, const slamgpu_ba_linear* out, int32_t* d_status,
+    void* d_workspace, size_t workspace_bytes, int total_kf, int total_points, int total_obs,
+    void* stream) {
+  PoseParams P;
+  if (int r = make_params(cam, inv_sigma2, nlevels, &P)) return r;
+  if (n_problems < 0 || total_kf < 0 || total_points < 0 || total_obs < 0 || !out)
+    return fail(SLAMGPU_EINVAL, "bad arguments");
+  if (n_problems == 0) return 0;
+  if (!d_problems || !d_kf_Tcw || !d_kf_mode || !d_point_obs_start || !d_status || !out->chi ||
+      (total_points > 0 && (!d_points || !out->hll || !out->bl)) ||
+      (total_obs > 0 && (!d_obs || !out->chi2 || !out->hpl)) || !out->hpp || !out->bp)
+    return fail(SLAMGPU_EINVAL, "null device buffer");
+  size_t need = 0;
+  ba_workspace_layout(nullptr, total_kf, total_points, total_obs, &need);
+  if (!d_workspace || workspace_bytes < need)
+    return fail(SLAMGPU_ECAP, "workspace of %zu bytes < %zu needed", workspace_bytes, need);
+  const BaWorkspace ws = ba_workspace_layout(d_workspace, total_kf, total_points, total_obs, nullptr);
+  const BaLinearOut o{out->chi2, out->hpl, out->hll, out->bl, out->hpp, out->bp, out->chi};
+  OPT_HIPCHECK(launch_local_ba_linearize(P, d_problems, n_problems, d_kf_Tcw, d_kf_mode, d_points,
+                                         d_point_obs_start, d_obs, d_status, ws, o,
+                                         static_cast<hipStream_t>(stream)));
+  return 0;
+}
+
 int slamgpu_local_bundle_adjustment(const slamgpu_camera* cam, const float* inv_sigma2,
                                     int nlevels, float* kf_Tcw, const uint8_t* kf_mode, int n_kf,
                                     float* points, int n_points, const int32_t* point_obs_start,

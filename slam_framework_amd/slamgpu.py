@@ -54,6 +54,7 @@ EXPORTS = [
     "slamgpu_timing_read", "slamgpu_pose_optimization", "slamgpu_pose_optimization_device",
     "slamgpu_optimizer_last_error", "slamgpu_local_bundle_adjustment",
     "slamgpu_local_bundle_adjustment_device", "slamgpu_local_ba_workspace_bytes",
+    "slamgpu_local_ba_linearize_device",
 ]
 
 
@@ -70,6 +71,11 @@ class Camera(C.Structure):
 class DeviceView(C.Structure):
     _fields_ = [("kps", C.c_void_p), ("desc", C.c_void_p), ("nkps", C.c_void_p),
                 ("u_right", C.c_void_p), ("depth", C.c_void_p), ("kp_cap", C.c_int)]
+
+
+class BaLinear(C.Structure):
+    """slamgpu_ba_linear: device pointers of the linearisation outputs."""
+    _fields_ = [(n, C.c_void_p) for n in ("chi2", "hpl", "hll", "bl", "hpp", "bp", "chi")]
 
 
 class SlamGpuError(RuntimeError):
@@ -134,6 +140,9 @@ def lib():
         L.slamgpu_local_bundle_adjustment_device.argtypes = [
             C.POINTER(Camera), vp, ip, vp, ip, vp, vp, vp, vp, vp, vp, vp, vp, sz, ip, ip, ip, vp,
             vp]
+        L.slamgpu_local_ba_linearize_device.argtypes = [
+            C.POINTER(Camera), vp, ip, vp, ip, vp, vp, vp, vp, vp, C.POINTER(BaLinear), vp, vp, sz,
+            ip, ip, ip, vp]
         L.slamgpu_optimizer_last_error.argtypes = []
         L.slamgpu_optimizer_last_error.restype = C.c_char_p
         _lib = L
@@ -447,3 +456,19 @@ def local_bundle_adjustment_device(cam, inv_sigma2, d_problems, n_problems, d_kf
         _ptr(d_erase), _ptr(d_status), _ptr(d_workspace),
         int(d_workspace.numel() * d_workspace.element_size()), total_kf, total_points, total_obs,
         _ptr(d_stop_flag), C.c_void_p(stream) if stream else None))
+
+
+def local_ba_linearize_device(cam, inv_sigma2, d_problems, n_problems, d_kf_Tcw, d_kf_mode,
+                              d_points, d_point_obs_start, d_obs, out, d_status, d_workspace,
+                              total_kf, total_points, total_obs, stream=None):
+    """slamgpu_local_ba_linearize_device. `out`: dict of device tensors chi2, hpl, hll, bl, hpp,
+    bp, chi (float64)."""
+    isig = np.ascontiguousarray(inv_sigma2, np.float32)
+    lin = BaLinear(*[int(out[n].data_ptr()) for n in ("chi2", "hpl", "hll", "bl", "hpp", "bp",
+                                                      "chi")])
+    _opt_check(lib().slamgpu_local_ba_linearize_device(
+        C.byref(Camera(*cam)), _ptr(isig), len(isig), _ptr(d_problems), n_problems,
+        _ptr(d_kf_Tcw), _ptr(d_kf_mode), _ptr(d_points), _ptr(d_point_obs_start), _ptr(d_obs),
+        C.byref(lin), _ptr(d_status), _ptr(d_workspace),
+        int(d_workspace.numel() * d_workspace.element_size()), total_kf, total_points, total_obs,
+        C.c_void_p(stream) if stream else None))

@@ -303,6 +303,8 @@ def _ba_lib():
         L.oc_local_bundle_adjustment.argtypes = [vp, vp, vp, vp, ip, vp, ip, vp, vp, vp,
                                                  C.POINTER(ip)]
         L.oc_ba_edge_eval.argtypes = [vp, vp, vp, vp, vp, C.c_float, vp, vp, vp]
+        L.oc_ba_linearize.argtypes = [vp, vp, vp, vp, ip, vp, ip, vp, vp, vp, vp, vp, vp, vp, vp]
+        L.oc_ba_linearize.restype = C.c_double
         L.oc_ba_edge_eval.restype = C.c_double
         L._ba_bound = True
     return L
@@ -336,3 +338,25 @@ def ba_edge_eval(cam, R, t, X, ob, inv_sigma2):
     c = _ba_lib().oc_ba_edge_eval(ptr(cam), ptr(R), ptr(t), ptr(X), ptr(o1), float(inv_sigma2),
                                   ptr(err), ptr(Jl), ptr(Jp))
     return c, err, Jl.reshape(3, 3), Jp.reshape(3, 6)
+
+
+def ba_linearize(cam, prob):
+    """computeActiveErrors + buildSystem of LocalBundleAdjustment's first optimize() at the input
+    estimates (slamgpu_ba_linear layout). Returns a dict of arrays + the robust chi2."""
+    cam = np.asarray(cam, np.float32)
+    kf = np.ascontiguousarray(prob["kf_Tcw"], np.float32)
+    pts = np.ascontiguousarray(prob["points"], np.float32)
+    mode = np.ascontiguousarray(prob["kf_mode"], np.uint8)
+    start = np.ascontiguousarray(prob["point_obs_start"], np.int32)
+    obs = np.ascontiguousarray(prob["obs"]).view(BA_OBS_DTYPE)
+    isig = np.ascontiguousarray(prob["inv_sigma2"], np.float32)
+    no, npn, nk = len(obs), len(pts), len(mode)
+    out = {"chi2": np.zeros(max(no, 1)), "hpl": np.zeros((max(no, 1), 18)),
+           "hll": np.zeros((max(npn, 1), 6)), "bl": np.zeros((max(npn, 1), 3)),
+           "hpp": np.zeros((max(nk, 1), 21)), "bp": np.zeros((max(nk, 1), 6))}
+    chi = _ba_lib().oc_ba_linearize(ptr(cam), ptr(isig), ptr(kf), ptr(mode), nk, ptr(pts), npn,
+                                    ptr(start), ptr(obs), *[ptr(out[k]) for k in
+                                                            ("chi2", "hpl", "hll", "bl", "hpp",
+                                                             "bp")])
+    out["chi"] = chi
+    return out

@@ -129,3 +129,50 @@ def test_local_ba_device_batch_matches_oracle(oracle, gpu_lib):
         assert np.array_equal(er_g[o0:o0 + len(p["obs"])], er_o), f"problem {i}"
         assert_close(kf_g[k0:k0 + nk], kf_o, p["kf_Tcw"], f"problem {i} poses")
         assert_close(pts_g[p0:p0 + npn], pts_o, p["points"], f"problem {i} points")
+
+
+def test_local_ba_linearize_matches_oracle(oracle, gpu_lib):
+    """slamgpu_local_ba_linearize_device (configs[4]'s batched residual / Jacobian / normal-equation
+    build) on a batch of problems vs the oracle's computeActiveErrors + buildSystem. FP64 sums in
+    another order: 1e-9 relative to each array's scale."""
+    import torch
+
+    G = gpu_lib
+    probs = [S.c5_problem(11), S.ba_problem(30, n_local=6, n_fixed=2, n_points=300),
+             S.ba_problem(31, n_local=3, n_fixed=0, n_points=40, stereo_frac=1.0)]
+    B = len(probs)
+    desc, starts, ko, po, oo = np.zeros((B, 4), np.int32), [], 0, 0, 0
+    for i, p in enumerate(probs):
+        desc[i] = (ko, len(p["kf_mode"]), po, len(p["points"]))
+        starts.append(p["point_obs_start"][:-1] + oo)
+        ko, po, oo = ko + len(p["kf_mode"]), po + len(p["points"]), oo + len(p["obs"])
+    start = np.concatenate(starts + [np.array([oo], np.int32)]).astype(np.int32)
+    dev = torch.device("cuda", 0)
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a).view(np.uint8).copy()).to(dev)
+    d_desc, d_start = t(desc), t(start)
+    d_kf = t(np.concatenate([p["kf_Tcw"] for p in probs]))
+    d_mode = t(np.concatenate([p["kf_mode"] for p in probs]))
+    d_pts = t(np.concatenate([p["points"] for p in probs]))
+    d_obs = t(np.concatenate([p["obs"] for p in probs]))
+    f64 = lambda *sh: torch.full(sh, np.nan, dtype=torch.float64, device=dev)
+    out = {"chi2": f64(oo), "hpl": f64(oo, 18), "hll": f64(po, 6), "bl": f64(po, 3),
+           "hpp": f64(ko, 21), "bp": f64(ko, 6), "chi": f64(B)}
+    d_st = torch.full((B,), -9, dtype=torch.int32, device=dev)
+    d_ws = torch.empty(G.local_ba_workspace_bytes(ko, po, oo), dtype=torch.uint8, device=dev)
+    G.local_ba_linearize_device(CAM, probs[0]["inv_sigma2"], d_desc, B, d_kf, d_mode, d_pts,
+                                d_start, d_obs, out, d_st, d_ws, ko, po, oo)
+    torch.cuda.synchronize()
+    o = {k: v.cpu().numpy() for k, v in out.items()}
+    assert (d_st.cpu().numpy() == 0).all()
+    for i, p in enumerate(probs):
+        k0, nk, p0, npn = desc[i]
+        e0, ne = start[p0], len(p["obs"])
+        ref = oracle.ba_linearize(CAM, p)
+        got = {"chi2": o["chi2"][e0:e0 + ne], "hpl": o["hpl"][e0:e0 + ne],
+               "hll": o["hll"][p0:p0 + npn], "bl": o["bl"][p0:p0 + npn],
+               "hpp": o["hpp"][k0:k0 + nk], "bp": o["bp"][k0:k0 + nk]}
+        for k, g in got.items():
+            r = ref[k][:len(g)]
+            np.testing.assert_allclose(g, r, rtol=1e-9, atol=1e-9 * np.abs(r).max(),
+                                       err_msg=f"problem {i} {k}")
+        assert o["chi"][i] == pytest.approx(ref["chi"], rel=1e-10)
