@@ -64,6 +64,7 @@ typedef struct {
 int slamgpu_create(int device, const slamgpu_orb_params* params, int cols, int rows,
                    int max_frames, slamgpu_ctx** out);
 void slamgpu_destroy(slamgpu_ctx* ctx);
+/* The context's last error; with ctx == NULL, why the last slamgpu_create on this thread failed. */
 const char* slamgpu_last_error(const slamgpu_ctx* ctx);
 /* Max keypoints one image can produce (sum over levels of the octree list bound). */
 int slamgpu_kp_capacity(const slamgpu_ctx* ctx);

@@ -112,12 +112,22 @@ __device__ __forceinline__ void huber_rho01(double e, double delta, double& r0, 
 struct PassPose {
   double R[9], t[3];
 };
+// A double every lane holds the same bits of, moved to a scalar register pair (the passes read
+// the pose through SGPR operands instead of 24 replicated VGPRs).
+__device__ __forceinline__ double uniform_f64(double v) {
+  const uint64_t b = __builtin_bit_cast(uint64_t, v);
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)b);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(b >> 32));
+  return __builtin_bit_cast(double, (uint64_t)hi << 32 | lo);
+}
+
 __device__ __forceinline__ PassPose pass_pose(const SE3& T) {
   PassPose p;
   quat_to_R(T.r, p.R);
-  p.t[0] = T.t[0];
-  p.t[1] = T.t[1];
-  p.t[2] = T.t[2];
+  for (int i = 0; i < 9; i++) p.R[i] = uniform_f64(p.R[i]);
+  p.t[0] = uniform_f64(T.t[0]);
+  p.t[1] = uniform_f64(T.t[1]);
+  p.t[2] = uniform_f64(T.t[2]);
   return p;
 }
 

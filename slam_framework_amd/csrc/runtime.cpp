@@ -98,6 +98,18 @@ static int fail(slamgpu_ctx* c, int code, const char* fmt, ...) {
   return code;
 }
 
+// Why the last slamgpu_create on this thread failed (no context exists to hold the message).
+thread_local std::string t_create_err;
+static int create_fail(int code, const char* fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof(buf), fmt, ap);
+  va_end(ap);
+  t_create_err = buf;
+  return code;
+}
+
 #define HIPCHECK(c, x)                                                                 \
   do {                                                                                 \
     hipError_t e_ = (x);                                                               \
@@ -169,19 +181,30 @@ int slamgpu_create(int device, const slamgpu_orb_params* p, int cols, int rows, 
                         std::min(std::max(p->min_th_fast, 0), 255)};
   std::vector<ResizeX> rx;
   std::vector<ResizeY> ry;
-  if (compute_geometry(c->params, cols, rows, &c->geom, &rx, &ry) != 0) {
+  if (int gr = compute_geometry(c->params, cols, rows, &c->geom, &rx, &ry)) {
+    static const char* why[] = {
+        "", "bad parameters",
+        "image too small: a pyramid level is under 2*19+8 pixels (the reference's FAST cell grid "
+        "would be empty, orb_extractor.cpp:712-733)",
+        "a pyramid level yields no initial octree node (orb_extractor.cpp:484-486)",
+        "FAST cell wider than 64 pixels", "resize span exceeds the pyr_down window",
+        "unsupported Gaussian kernel or octree LDS budget"};
     delete c;
-    return SLAMGPU_EINVAL;
+    return create_fail(SLAMGPU_EINVAL, "slamgpu_create(%dx%d, nlevels %d, scale %g): %s", cols,
+                       rows, p->nlevels, (double)p->scale_factor,
+                       why[std::min(std::max(-gr, 0), 6)]);
   }
   compute_tables(c->params, &c->tables);
   if (c->geom.kp_cap > 4096) {  // matcher keys carry a 12-bit keypoint index
     delete c;
-    return SLAMGPU_EINVAL;
+    return create_fail(SLAMGPU_EINVAL, "slamgpu_create: nfeatures %d gives %d keypoints per image "
+                       "> 4096", p->nfeatures, 0);
   }
   for (int l = 0; l < c->geom.nlevels; l++)
     if (c->geom.lv[l].node_cap > 1024) {
       delete c;
-      return SLAMGPU_EINVAL;  // octree LDS arrays hold <= 2048 list nodes
+      return create_fail(SLAMGPU_EINVAL, "slamgpu_create: level %d needs %d octree nodes > 1024",
+                         l, 0);  // octree LDS arrays hold <= 2048 list nodes
     }
   c->device = device;
   c->max_frames = max_frames;
@@ -257,7 +280,9 @@ void slamgpu_destroy(slamgpu_ctx* c) {
   delete c;
 }
 
-const char* slamgpu_last_error(const slamgpu_ctx* c) { return c ? c->err.c_str() : "null ctx"; }
+const char* slamgpu_last_error(const slamgpu_ctx* c) {
+  return c ? c->err.c_str() : t_create_err.c_str();
+}
 
 int slamgpu_kp_capacity(const slamgpu_ctx* c) { return c ? c->geom.kp_cap : 0; }
 

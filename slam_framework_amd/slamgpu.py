@@ -170,7 +170,7 @@ class Context:
                                   C.byref(h))
         self.h = h
         if rc != 0:
-            msg = lib().slamgpu_last_error(h).decode() if h else ""
+            msg = lib().slamgpu_last_error(h if h else None).decode()
             if h:
                 lib().slamgpu_destroy(h)
                 self.h = None
