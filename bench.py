@@ -99,10 +99,12 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--batch", type=int, default=128, help="stereo frames per GPU per step")
+    ap.add_argument("--batch", type=int, default=256, help="stereo frames per GPU per step")
     ap.add_argument("--distinct", type=int, default=16, help="distinct synthetic frames per rank")
     ap.add_argument("--cpu-frames", type=int, default=0, help="oracle sample size (0 = auto)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--streams", type=int, default=1,
+                    help="split each step's batch over this many contexts on their own HIP streams")
     ap.add_argument("--no-optimizer", action="store_true",
                     help="skip the PoseOptimization / LocalBundleAdjustment measurements")
     args = ap.parse_args()
@@ -145,32 +147,57 @@ def main():
     poses["check_ori"] = 1
     d_poses = torch.from_numpy(poses.view(np.uint8).copy()).to(dev)
 
-    ctx = G.Context(cols, rows, 2000, 1.2, 8, 20, 7, max_frames=B, device=local)
+    # NS contexts, each with its own HIP stream and Bs consecutive frames of the batch (its first
+    # frame is the halo of its second): the launches of one half fill the other's tails.
+    NS = max(1, args.streams)
+    Bs = B // NS
+    assert Bs >= 2 and Bs * NS == B, "--batch must split into --streams parts of >= 2 frames"
+    ctxs = [G.Context(cols, rows, 2000, 1.2, 8, 20, 7, max_frames=Bs, device=local)
+            for _ in range(NS)]
+    ctx = ctxs[0]
     kc = ctx.kp_cap
-    d_q = torch.empty(B * kc * G.F2F_QUERY_DTYPE.itemsize, dtype=torch.uint8, device=dev)
-    d_qs = torch.empty(B, dtype=torch.int32, device=dev)
-    d_qc = torch.empty(B, dtype=torch.int32, device=dev)
-    d_mp = torch.empty(B * kc, dtype=torch.int32, device=dev)
-    d_blk = torch.empty(B * kc, dtype=torch.uint8, device=dev)
-    d_nm = torch.empty(B, dtype=torch.int32, device=dev)
+    main = torch.cuda.current_stream()
+    streams = [main] + [torch.cuda.Stream(device=dev) for _ in range(NS - 1)]
+    parts = []
+    for si in range(NS):
+        parts.append({
+            "q": torch.empty(Bs * kc * G.F2F_QUERY_DTYPE.itemsize, dtype=torch.uint8, device=dev),
+            "qs": torch.empty(Bs, dtype=torch.int32, device=dev),
+            "qc": torch.empty(Bs, dtype=torch.int32, device=dev),
+            "mp": torch.empty(Bs * kc, dtype=torch.int32, device=dev),
+            "blk": torch.empty(Bs * kc, dtype=torch.uint8, device=dev),
+            "nm": torch.empty(Bs, dtype=torch.int32, device=dev),
+            "poses": d_poses[si * Bs * G.F2F_POSE_DTYPE.itemsize:
+                             (si + 1) * Bs * G.F2F_POSE_DTYPE.itemsize]})
 
     def step():
-        st = torch.cuda.current_stream().cuda_stream
-        ctx.frontend_device(int(d_l.data_ptr()), int(d_r.data_ptr()), stride, pitch, B, cam, st)
-        ctx.make_vo_queries_device(d_poses, 1, d_q, d_qs, d_qc, B, st)
-        d_mp.fill_(-1)
-        d_blk.zero_()
-        ctx.search_by_projection_frame_device(d_q, B * kc, d_qs, d_qc, kc, d_poses, d_mp, d_blk,
-                                              kc, d_nm, B, st)
+        for si in range(NS):
+            st_ = streams[si]
+            if si:
+                st_.wait_stream(main)
+            with torch.cuda.stream(st_):
+                c, pt, h = ctxs[si], parts[si], st_.cuda_stream
+                off = si * Bs * stride
+                c.frontend_device(int(d_l.data_ptr()) + off, int(d_r.data_ptr()) + off, stride,
+                                  pitch, Bs, cam, h)
+                c.make_vo_queries_device(pt["poses"], 1, pt["q"], pt["qs"], pt["qc"], Bs, h)
+                pt["mp"].fill_(-1)
+                pt["blk"].zero_()
+                c.search_by_projection_frame_device(pt["q"], Bs * kc, pt["qs"], pt["qc"], kc,
+                                                    pt["poses"], pt["mp"], pt["blk"], kc,
+                                                    pt["nm"], Bs, h)
+        for si in range(1, NS):
+            main.wait_stream(streams[si])
 
     for _ in range(max(1, args.warmup)):
         step()
     torch.cuda.synchronize()
-    ctx.sync()
+    for c in ctxs:
+        c.sync()
     # sanity of what the timed steps compute (not timed)
-    nk = np.array([ctx.keypoints(i)[0].shape[0] for i in range(min(4, 2 * B))])
-    nm = d_nm.cpu().numpy()
-    nq = d_qc.cpu().numpy()
+    nk = np.array([ctx.keypoints(i)[0].shape[0] for i in range(min(4, 2 * Bs))])
+    nm = np.concatenate([pt["nm"].cpu().numpy() for pt in parts])
+    nq = np.concatenate([pt["qc"].cpu().numpy() for pt in parts])
     print(f"[rank {rank}] keypoints/image {nk.tolist()} queries/frame {nq[1:5].tolist()} "
           f"matches/frame {nm[1:5].tolist()}", file=sys.stderr)
 
@@ -201,14 +228,15 @@ def main():
         dist.barrier()
     t1 = time.perf_counter()
     ctx.timing_stop()
-    ctx.sync()
+    for c in ctxs:
+        c.sync()
     from slam_framework_amd import dist as SD
     elapsed = SD.max_over_ranks(t1 - t0, dev)
     dom_ms, dom_n = ctx.timing_read(dominant)
     # per-rank result summary gathered to every rank (validation, outside the timed region)
-    summ = SD.gather_summary([int(nk.sum()), int(d_nm.sum().item()), int(d_qc.sum().item())], dev)
+    summ = SD.gather_summary([int(nk.sum()), int(nm.sum()), int(nq.sum())], dev)
 
-    frames = world * (B - 1) * args.steps
+    frames = world * NS * (Bs - 1) * args.steps
     value = frames / elapsed
     ms_per_step = 1000.0 * elapsed / args.steps
 
@@ -216,7 +244,7 @@ def main():
         level_px = [ctx.pyramid_level(0, l).size for l in range(8)]
         kp_img = float(nk.mean())
         nqueries = int(nq.sum())
-        dom_bytes = kernel_bytes(dominant, 2 * B, B, kp_img, level_px, nqueries)
+        dom_bytes = kernel_bytes(dominant, 2 * Bs, Bs, kp_img, level_px, nqueries // NS)
         avg_launch_s = dom_ms / 1000.0 / max(1, dom_n)
         per_launch_bytes = dom_bytes / max(1, launches_per_step) if dom_bytes else None
         achieved = (per_launch_bytes / avg_launch_s / 1e9) if per_launch_bytes else None
@@ -257,7 +285,8 @@ def main():
             "data": "synthetic (seeded rectangles scene, pure-rotation sequence)",
             "config": {"workload": "configs[1]: synthetic 1241x376 stereo stream, 2000 kp/frame, "
                                    "extract L+R + stereo match + frame-to-frame match",
-                       "frames_per_gpu_per_step": B - 1, "batch": B, "nfeatures": 2000,
+                       "frames_per_gpu_per_step": NS * (Bs - 1), "batch": B, "streams": NS,
+                       "nfeatures": 2000,
                        "nlevels": 8, "scale_factor": 1.2, "fast_th": [20, 7],
                        "parallelism": f"frame-sharded x{world}"},
             "roofline": roofline,

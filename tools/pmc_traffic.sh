@@ -5,7 +5,8 @@
 set -e
 export TMPDIR=/tmp
 OUT=${OUT:-gpurun_out/traffic}
-ARGS=${ARGS:-"--steps 3 --warmup 1 --no-cpu-baseline"}
+ARGS=${ARGS:-"--steps 3 --warmup 1 --no-cpu-baseline --no-optimizer"}  # recorded by traffic.py via ARGS
+export ARGS
 mkdir -p $OUT
 for c in FETCH_SIZE WRITE_SIZE; do
   lc=$(echo $c | tr A-Z a-z | cut -d_ -f1)

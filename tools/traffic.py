@@ -4,7 +4,7 @@ Calibration (MI355X_MICROARCH.md, HBM section): on gfx950 FETCH_SIZE counts half
 16-B-per-lane streaming read; other widths are uncalibrated, so the membench kernels copy16
 (16 B/lane) and copy4 (4 B/lane, the width the ORB kernels use) are profiled beside the bench and
 their known byte counts give the read factor per width. Writes are taken as reported.
-Usage: python tools/traffic.py gpurun_out/traffic [kernel]
+Usage: python tools/traffic.py gpurun_out/traffic [kernel|-] [batch] > profiles/traffic.json
 """
 import collections
 import csv
@@ -30,7 +30,8 @@ def per_kernel(d, counter):
 
 def main():
     base = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/traffic"
-    want = sys.argv[2] if len(sys.argv) > 2 else None
+    want = sys.argv[2] if len(sys.argv) > 2 and sys.argv[2] != "-" else None
+    batch = int(sys.argv[3]) if len(sys.argv) > 3 else None
     mb_f = per_kernel(os.path.join(base, "membench_fetch"), "FETCH_SIZE")
     mb_w = per_kernel(os.path.join(base, "membench_write"), "WRITE_SIZE")
     known = 512 << 20  # membench: each copy reads and writes 512 MiB
@@ -41,7 +42,13 @@ def main():
     f = per_kernel(os.path.join(base, "bench_fetch"), "FETCH_SIZE")
     w = per_kernel(os.path.join(base, "bench_write"), "WRITE_SIZE")
     read_factor = cal.get("copy4", 2.0)
-    res = {"calibration_read_factor": cal, "write_calibration": {k: known / (v * 1024.0) for k, v in mb_w.items()
+    res = {"batch": batch,
+           "command": "python3 bench.py " + os.environ.get("ARGS", "") + " (tools/pmc_traffic.sh)",
+           "source": "tools/pmc_traffic.sh + tools/traffic.py",
+           "method": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes, "
+                     "kernel-trace only; FETCH_SIZE (KB) x read factor calibrated on membench "
+                     "copy4/copy16 (known 512 MiB) + WRITE_SIZE (KB)",
+           "calibration_read_factor": cal, "write_calibration": {k: known / (v * 1024.0) for k, v in mb_w.items()
                                                                 if k.startswith("copy")},
            "kernels": {}}
     for k in sorted(set(f) | set(w)):
