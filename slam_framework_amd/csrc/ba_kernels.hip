@@ -55,7 +55,7 @@ using se3::SE3;
   } while (0)
 #endif
 
-constexpr int kThreads = 1024;
+constexpr int kThreads = 512;
 constexpr int kWaves = kThreads / 64;
 constexpr int kMaxK = SLAMGPU_BA_MAX_LOCAL_KF;
 constexpr int kMaxN = 6 * kMaxK;
@@ -586,36 +586,39 @@ __device__ void assemble_S(BaShared& sh, const Problem& pb, double lambda) {
     const int cnt = sh.blk_cnt[b], off = sh.blk_off[b];
     const bool diag = kh == kl;
     const double* kr = kfrec(pb, sh.kf_of_free[kh]);
-    for (int half = 0; half < 2; half++) {
-      double acc[32];
+    // one pass over the block's pairs: 36 accumulators (rows 0-5 x columns 0-5)
+    double acc[64];
 #pragma unroll
-      for (int i = 0; i < 32; i++) acc[i] = 0.0;
-      for (int h = lane; h < cnt; h += 64) {
-        const int2 ep = hits[off + h];
-        const int eh = pb.o0 + ep.x, el = pb.o0 + (diag ? ep.x : ep.y);
-        const double* bd = pb.ws.bdinv + (size_t)eh * 18 + 9 * half;
-        const double* hp = pb.ws.hpl + (size_t)el * 18;
-        double B[9], Hl[18];
+    for (int i = 0; i < 64; i++) acc[i] = 0.0;
+    for (int h = lane; h < cnt; h += 64) {
+      const int2 ep = hits[off + h];
+      const int eh = pb.o0 + ep.x, el = pb.o0 + (diag ? ep.x : ep.y);
+      const double* bd = pb.ws.bdinv + (size_t)eh * 18;
+      const double* hp = pb.ws.hpl + (size_t)el * 18;
+      double B[18], Hl[18];
 #pragma unroll
-        for (int i = 0; i < 9; i++) B[i] = bd[i];
+      for (int i = 0; i < 18; i++) B[i] = bd[i];
 #pragma unroll
-        for (int i = 0; i < 18; i++) Hl[i] = hp[i];
+      for (int i = 0; i < 18; i++) Hl[i] = hp[i];
 #pragma unroll
-        for (int r = 0; r < 3; r++)
+      for (int r = 0; r < 6; r++)
 #pragma unroll
-          for (int c = 0; c < 6; c++)
-            acc[6 * r + c] += B[3 * r] * Hl[3 * c] + B[3 * r + 1] * Hl[3 * c + 1] +
-                              B[3 * r + 2] * Hl[3 * c + 2];
-      }
-      const double s = wave_reduce_scatter32(acc);
-      const int idx = lane >> 1;
-      if ((lane & 1) == 0 && idx < 18) {
-        const int r = 3 * half + idx / 6, c = idx % 6;
+        for (int c = 0; c < 6; c++)
+          acc[6 * r + c] += B[3 * r] * Hl[3 * c] + B[3 * r + 1] * Hl[3 * c + 1] +
+                            B[3 * r + 2] * Hl[3 * c + 2];
+    }
+    const double s0 = wave_reduce_scatter32(acc), s1 = wave_reduce_scatter32(acc + 32);
+    const int idx = lane >> 1;
+#pragma unroll
+    for (int part = 0; part < 2; part++) {
+      const int id = idx + 32 * part;
+      if ((lane & 1) == 0 && id < 36) {
+        const int r = id / 6, c = id % 6;
         const int i = 6 * kh + r, j = 6 * kl + c;
         if (!diag || j <= i) {
           double base = 0.0;
           if (diag) base = kr[KH + hidx(c, r)] + (r == c ? lambda : 0.0);
-          sh.S[sidx(i, j)] = base - s;
+          sh.S[sidx(i, j)] = base - (part ? s1 : s0);
         }
       }
     }
