@@ -14,7 +14,6 @@ static_assert(sizeof(slamgpu_ba_obs) == 20, "ba observation layout");
 struct BaWorkspace {
   double* chi2;      // [obs] last computed chi2 (g2o keeps the last error per edge)
   double* hpl;       // [obs][6 x 3] Hpl block of a local-keyframe edge
-  double* bdinv;     // [obs][6 x 3] Hpl Dinv of the current trial
   uint8_t* act;      // [obs] edge at level 0
   int32_t* psorted;  // [obs] a point's active local-keyframe edges sorted by keyframe
   int2* hits;        // [obs * ((MAX_LOCAL_KF + 2) / 2)] S-block point pairs

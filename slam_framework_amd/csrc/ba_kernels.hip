@@ -5,10 +5,9 @@
 // Every LM trial solves the full system by the Schur complement on the points, as g2o's
 // BlockSolver does (block_solver.hpp:351-497):
 //
-//   point pass   (thread per point)   Dinv_p = (Hll_p + lambda I)^-1, db_p = Dinv_p bl_p and
-//                                     BDinv_e = Hpl_e Dinv_p for the point's free-keyframe edges
+//   point pass   (thread per point)   Dinv_p = (Hll_p + lambda I)^-1, db_p = Dinv_p bl_p
 //   S assembly   (wave per 6x6 block) S(kh, kl) = [kh == kl](Hpp + lambda I)
-//                                       - sum over the points seen by both BDinv_e(kh) Hpl_e(kl)^T
+//                                       - sum over the points seen by both Hpl_e(kh) Dinv_p Hpl_e(kl)^T
 //                                     lanes over the block's point pairs, deterministic wave sums
 //   reduced rhs  (wave per keyframe)  bs_k = bp_k - sum_e Hpl_e db_p
 //   LDLT         (whole workgroup)    S in LDS (lower triangle, 6K <= 144), 6x6-blocked
@@ -559,25 +558,6 @@ __device__ void schur_points(const Problem& pb, double lambda) {
   }
 }
 
-// BDinv_e = Hpl_e Dinv_p for every active local-keyframe edge (edge-parallel).
-__device__ void schur_edges(BaShared& sh, const Problem& pb) {
-  for (int e = threadIdx.x; e < pb.n_obs; e += kThreads) {
-    const int ge = pb.o0 + e;
-    if (!pb.ws.act[ge] || sh.free_of_kf[pb.obs[ge].keyframe] < 0) continue;
-    const PtRef pr = ptrec(pb, pb.ws.opoint[ge]);
-    double Di[6];
-    for (int i = 0; i < 6; i++) Di[i] = pr[PD + i];
-    const double* hp = pb.ws.hpl + (size_t)ge * 18;
-    double* bd = pb.ws.bdinv + (size_t)ge * 18;
-    for (int i = 0; i < 6; i++) {
-      const double h0 = hp[3 * i], h1 = hp[3 * i + 1], h2 = hp[3 * i + 2];
-      bd[3 * i] = h0 * Di[0] + h1 * Di[1] + h2 * Di[2];
-      bd[3 * i + 1] = h0 * Di[1] + h1 * Di[3] + h2 * Di[4];
-      bd[3 * i + 2] = h0 * Di[2] + h1 * Di[4] + h2 * Di[5];
-    }
-  }
-}
-
 __device__ void assemble_S(BaShared& sh, const Problem& pb, double lambda) {
   const int lane = threadIdx.x & 63, w = wave_id(), K = sh.K, nblk = K * (K + 1) / 2;
   const int2* hits = pb.ws.hits + (size_t)pb.o0 * kPairsPerObs;
@@ -593,13 +573,23 @@ __device__ void assemble_S(BaShared& sh, const Problem& pb, double lambda) {
     for (int h = lane; h < cnt; h += 64) {
       const int2 ep = hits[off + h];
       const int eh = pb.o0 + ep.x, el = pb.o0 + (diag ? ep.x : ep.y);
-      const double* bd = pb.ws.bdinv + (size_t)eh * 18;
+      // B = Hpl_eh Dinv_p, formed here rather than stored per edge (the kernel is bound by
+      // the bytes it moves, not by these 54 FMAs)
+      const double* hh = pb.ws.hpl + (size_t)eh * 18;
       const double* hp = pb.ws.hpl + (size_t)el * 18;
-      double B[18], Hl[18];
+      const PtRef pr = ptrec(pb, pb.ws.opoint[eh]);
+      double Di[6], B[18], Hl[18];
 #pragma unroll
-      for (int i = 0; i < 18; i++) B[i] = bd[i];
+      for (int i = 0; i < 6; i++) Di[i] = pr[PD + i];
 #pragma unroll
-      for (int i = 0; i < 18; i++) Hl[i] = hp[i];
+      for (int i = 0; i < 6; i++) {
+        const double h0 = hh[3 * i], h1 = hh[3 * i + 1], h2 = hh[3 * i + 2];
+        B[3 * i] = h0 * Di[0] + h1 * Di[1] + h2 * Di[2];
+        B[3 * i + 1] = h0 * Di[1] + h1 * Di[3] + h2 * Di[4];
+        B[3 * i + 2] = h0 * Di[2] + h1 * Di[4] + h2 * Di[5];
+      }
+#pragma unroll
+      for (int i = 0; i < 18; i++) Hl[i] = diag ? hh[i] : hp[i];
 #pragma unroll
       for (int r = 0; r < 6; r++)
 #pragma unroll
@@ -893,8 +883,6 @@ __global__ __launch_bounds__(kThreads) void local_ba_kernel(
         BA_TICK(7);
         schur_points(pb, lambda);
         __syncthreads();
-        schur_edges(sh, pb);
-        __syncthreads();
         BA_TICK(2);
         assemble_S(sh, pb, lambda);
         __syncthreads();
@@ -1137,7 +1125,6 @@ BaWorkspace ba_workspace_layout(void* base, int total_kf, int total_points, int 
   };
   w.chi2 = reinterpret_cast<double*>(take(sizeof(double) * (size_t)total_obs));
   w.hpl = reinterpret_cast<double*>(take(sizeof(double) * 18 * (size_t)total_obs));
-  w.bdinv = reinterpret_cast<double*>(take(sizeof(double) * 18 * (size_t)total_obs));
   w.act = reinterpret_cast<uint8_t*>(take((size_t)total_obs));
   w.psorted = reinterpret_cast<int32_t*>(take(sizeof(int32_t) * (size_t)total_obs));
   w.hits = reinterpret_cast<int2*>(take(sizeof(int2) * kPairsPerObs * (size_t)total_obs));
