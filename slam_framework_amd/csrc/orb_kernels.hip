@@ -367,6 +367,12 @@ __global__ __launch_bounds__(64) void blur7_edges_kernel(ImageBatch b, const Orb
 // NMS is strict '>' against the 8 neighbours' scores at that t, zero outside the detect area
 // (cell-local, as cv::FAST sees only the cell view). Survivors are written in row-major order.
 constexpr int kCellWaves = 4;
+#ifndef FAST_PRE2
+#define FAST_PRE2 1  // opposite-pair pre-test on (0,8),(4,12) only (0: all four pairs)
+#endif
+#ifndef FAST_MINW
+#define FAST_MINW 1  // A/B: __launch_bounds__ minimum waves per SIMD
+#endif
 
 // max over the 16 contiguous 9-arcs of min(v - ring) ("darker" strength) and of min(ring - v)
 // ("brighter"); p is a FAST-9 corner at threshold t iff the result is > t.
@@ -473,6 +479,7 @@ struct CellView {
   bool aligned;
 };
 
+template <int kAlign = 4>
 __device__ __forceinline__ CellView cell_view(const ImageBatch& b, const OrbGeom* g, int img,
                                               int in_pitch, const uint4& d) {
   CellView v;
@@ -484,7 +491,7 @@ __device__ __forceinline__ CellView cell_view(const ImageBatch& b, const OrbGeom
   const LevelGeom& L = g->lv[v.level];
   v.pitch = v.level == 0 ? in_pitch : L.pitch;
   v.base = v.level == 0 ? batch_image(b, img) : b.pyr + (int64_t)img * g->pyr_bytes + L.offset;
-  v.ax = v.ini_x & ~3;
+  v.ax = v.ini_x & -kAlign;
   v.off = v.ini_x - v.ax;
   v.nd = (v.vw + v.off + 3) >> 2;  // dwords per tile row (<= 18)
   v.aligned = (((uintptr_t)v.base | (uintptr_t)v.pitch) & 3) == 0;
@@ -496,8 +503,13 @@ __device__ __forceinline__ uint4 readlane4(const uint4& x, int j) {
                     __builtin_amdgcn_readlane(x.z, j), __builtin_amdgcn_readlane(x.w, j));
 }
 
-template <int TS>
-__global__ __launch_bounds__(256) void fast_cells_kernel(ImageBatch b,
+// GLDS: every cell view of the launch is 16-byte aligned (pyramid levels, and a caller image
+// with 16-byte base/pitch/stride): tiles go HBM -> LDS by global_load_lds_dwordx4 (no VGPRs, one
+// instruction per 1 KiB = 1024/TS tile rows), double-buffered so the next cell's tile streams in
+// while this one is processed. Otherwise dword loads staged through registers (4-byte aligned)
+// or a byte copy.
+template <int TS, bool GLDS>
+__global__ __launch_bounds__(256, FAST_MINW) void fast_cells_kernel(ImageBatch b,
                                                          const OrbGeom* __restrict__ g,
                                                          const CellDesc* __restrict__ cells,
                                                          uint32_t* __restrict__ cell_keys,
@@ -508,6 +520,9 @@ __global__ __launch_bounds__(256) void fast_cells_kernel(ImageBatch b,
   constexpr int kTileStride = TS, kScoreStride = TS;  // == g->fast_tile_stride
   constexpr int kLpr = TS / 4, kRps = 64 / kLpr;        // tile copy: lanes per row, rows per step
   constexpr int kTileSteps = (70 + kRps - 1) / kRps;    // cell views are <= 70 rows
+  constexpr int kGLpr = TS / 16, kGRows = 64 / kGLpr;   // glds: lanes per row, rows per instr.
+  constexpr int kGSteps = (70 + kGRows - 1) / kGRows;
+  constexpr int kAlign = GLDS ? 16 : 4;
   const int img = blockIdx.y;
   const int ncells = g->cells_per_image;
   const int c0 = (blockIdx.x * kCellWaves + wid) * kCellsPerWave;
@@ -516,8 +531,9 @@ __global__ __launch_bounds__(256) void fast_cells_kernel(ImageBatch b,
   const uint4 my_desc = lane < nc ? reinterpret_cast<const uint4*>(cells)[c0 + lane]
                                   : make_uint4(0, 0, 0, 0);
   const int in_pitch = __builtin_amdgcn_readfirstlane(b.in_pitch);
-  uint8_t* tile = s_fast + wid * g->fast_lds_per_wave;
-  uint8_t* sc = tile + ((kTileStride * g->fast_tile_rows + 15) & ~15);
+  const int tile_bytes = (kTileStride * g->fast_tile_rows + 15) & ~15;
+  uint8_t* tile0 = s_fast + wid * g->fast_lds_per_wave;
+  uint8_t* sc = tile0 + (GLDS ? 2 : 1) * tile_bytes;
   uint16_t* cand =
       reinterpret_cast<uint16_t*>(sc + ((kScoreStride * g->fast_score_rows + 15) & ~15));
 
@@ -525,7 +541,7 @@ __global__ __launch_bounds__(256) void fast_cells_kernel(ImageBatch b,
   // into registers, lane = (row within a step, dword): each element is a scalar row base plus a
   // per-lane offset. Tile column c = image column ax + c.
   const int plr = lane / kLpr, pld = lane % kLpr;
-  uint32_t tv[kTileSteps];
+  uint32_t tv[GLDS ? 1 : kTileSteps];
   int tn = 0;
   auto prefetch = [&](const CellView& v) {
     tn = v.aligned ? (v.vh + kRps - 1) / kRps : 0;  // wave-uniform
@@ -537,16 +553,65 @@ __global__ __launch_bounds__(256) void fast_cells_kernel(ImageBatch b,
       if (k < tn && dok && k * kRps + plr < v.vh)
         tv[k] = *reinterpret_cast<const uint32_t*>(src + (int64_t)(k * kRps) * v.pitch + goff);
   };
-  CellView nxt = cell_view(b, g, img, in_pitch, readlane4(my_desc, 0));
-  if (nxt.vh > 0) prefetch(nxt);
+  // glds: tile row r of the view = image row ini_y + min(r, vh - 1) (rows past the view repeat
+  // its last row; they are never read), 16-byte chunk lane % kGLpr of [ax, ax + TS). The view
+  // ends >= 16 rows above the level's last row, so the TS-byte row reads stay in the image.
+  const int glr = lane / kGLpr, glc = 16 * (lane % kGLpr);
+  auto issue = [&](const CellView& v, uint8_t* buf) -> int {
+    const int n = (v.vh + kGRows - 1) / kGRows;  // wave-uniform
+    const uint8_t* src = v.base + (int64_t)v.ini_y * v.pitch + v.ax + glc;
+#pragma unroll
+    for (int k = 0; k < kGSteps; k++)
+      if (k < n)
+        __builtin_amdgcn_global_load_lds(
+            (const __attribute__((address_space(1))) void*)(
+                src + (int64_t)min(k * kGRows + glr, v.vh - 1) * v.pitch),
+            (__attribute__((address_space(3))) void*)(buf + 1024 * k), 16, 0, 0);
+    return n;
+  };
+  CellView nxt = cell_view<kAlign>(b, g, img, in_pitch, readlane4(my_desc, 0));
+  if constexpr (GLDS) {
+    if (nxt.vh > 0) issue(nxt, tile0);
+  } else {
+    if (nxt.vh > 0) prefetch(nxt);
+  }
 
   for (int ci = 0; ci < nc; ci++) {
     const CellView v = nxt;
     const int64_t slot = (int64_t)img * ncells + c0 + ci;
+    uint8_t* tile = tile0;
+    if constexpr (GLDS) {
+      tile = tile0 + (ci & 1) * tile_bytes;
+      int n_next = 0;
+      if (ci + 1 < nc) {
+        nxt = cell_view<kAlign>(b, g, img, in_pitch, readlane4(my_desc, ci + 1));
+        // the other buffer's last reader was cell ci - 1, whose LDS reads have all returned
+        if (nxt.vh > 0) n_next = issue(nxt, tile0 + ((ci + 1) & 1) * tile_bytes);
+      }
+      if (v.vh == 0) {  // empty cell (:737, :745)
+        if (lane == 0) cell_count[slot] = 0;
+        continue;
+      }
+      // this cell's glds have landed once at most the next cell's n_next are outstanding
+      switch (n_next) {
+        case 0: __builtin_amdgcn_s_waitcnt(0x0F70); break;
+        case 1: __builtin_amdgcn_s_waitcnt(0x0F71); break;
+        case 2: __builtin_amdgcn_s_waitcnt(0x0F72); break;
+        case 3: __builtin_amdgcn_s_waitcnt(0x0F73); break;
+        case 4: __builtin_amdgcn_s_waitcnt(0x0F74); break;
+        case 5: __builtin_amdgcn_s_waitcnt(0x0F75); break;
+        case 6: __builtin_amdgcn_s_waitcnt(0x0F76); break;
+        case 7: __builtin_amdgcn_s_waitcnt(0x0F77); break;
+        case 8: __builtin_amdgcn_s_waitcnt(0x0F78); break;
+        default: __builtin_amdgcn_s_waitcnt(0x0F79); break;
+      }
+      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+    } else {
     if (v.vh == 0) {  // empty cell (:737, :745)
       if (lane == 0) cell_count[slot] = 0;
       if (ci + 1 < nc) {
-        nxt = cell_view(b, g, img, in_pitch, readlane4(my_desc, ci + 1));
+        nxt = cell_view<kAlign>(b, g, img, in_pitch, readlane4(my_desc, ci + 1));
         if (nxt.vh > 0) prefetch(nxt);
       }
       continue;
@@ -565,11 +630,12 @@ __global__ __launch_bounds__(256) void fast_cells_kernel(ImageBatch b,
           tile[r * kTileStride + x] = v.base[(int64_t)(v.ini_y + r) * v.pitch + v.ax + x];
     }
     if (ci + 1 < nc) {  // next cell's loads fly while this one is processed
-      nxt = cell_view(b, g, img, in_pitch, readlane4(my_desc, ci + 1));
+      nxt = cell_view<kAlign>(b, g, img, in_pitch, readlane4(my_desc, ci + 1));
       if (nxt.vh > 0) prefetch(nxt);
     }
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     __builtin_amdgcn_wave_barrier();
+    }
     const int off = v.off;
     const int dh = v.vh - 6, dw = v.vw - 6;  // detect area [3, vh-3) x [3, vw-3)
     // ---- score map: rows -1 .. dh of the detect area, all zero (a zero frame around the detect
@@ -603,8 +669,10 @@ __global__ __launch_bounds__(256) void fast_cells_kernel(ImageBatch b,
             return *reinterpret_cast<const uint32_t*>(row + dy * kTileStride + 4 * dq);
           };
           const uint32_t c = rd(0, 0), cm = rd(0, qm), cp = rd(0, 1);
+#if !FAST_PRE2
           const uint32_t u2 = rd(2, 0), u2m = rd(2, qm), u2p = rd(2, 1);
           const uint32_t d2 = rd(-2, 0), d2m = rd(-2, qm), d2p = rd(-2, 1);
+#endif
           const uint32_t p0 = rd(3, 0), p8 = rd(-3, 0);
           // even pixels (bytes 0, 2) and odd pixels (bytes 1, 3) of each ring position as u16
           // pairs; v_perm picks the shifted bytes straight out of two adjacent dwords
@@ -622,6 +690,12 @@ __global__ __launch_bounds__(256) void fast_cells_kernel(ImageBatch b,
             const u16x2_t a8 = U(__builtin_amdgcn_perm(p8, p8, s0));      // (0, -3)
             const u16x2_t a4 = U(__builtin_amdgcn_perm(cp, c, s3));       // (+3, 0)
             const u16x2_t a12 = U(__builtin_amdgcn_perm(c, cm, s1));      // (-3, 0)
+#if FAST_PRE2
+            const u16x2_t D = __builtin_elementwise_max(__builtin_elementwise_min(a0, a8),
+                                                        __builtin_elementwise_min(a4, a12));
+            const u16x2_t B = __builtin_elementwise_min(__builtin_elementwise_max(a0, a8),
+                                                        __builtin_elementwise_max(a4, a12));
+#else
             const u16x2_t a2 = U(__builtin_amdgcn_perm(u2p, u2, s2));     // (+2, +2)
             const u16x2_t a14 = U(__builtin_amdgcn_perm(u2, u2m, s2));    // (-2, +2)
             const u16x2_t a6 = U(__builtin_amdgcn_perm(d2p, d2, s2));     // (+2, -2)
@@ -634,6 +708,7 @@ __global__ __launch_bounds__(256) void fast_cells_kernel(ImageBatch b,
             const u16x2_t B = __builtin_elementwise_min(
                 __builtin_elementwise_min(__builtin_elementwise_max(a0, a8), __builtin_elementwise_max(a4, a12)),
                 __builtin_elementwise_min(__builtin_elementwise_max(a2, a10), __builtin_elementwise_max(a6, a14)));
+#endif
             const u16x2_t lo = __builtin_elementwise_sub_sat(v, tt2), hi = v + tt2;
             any[h] = __builtin_bit_cast(uint32_t, __builtin_elementwise_sub_sat(lo, D)) |
                      __builtin_bit_cast(uint32_t, __builtin_elementwise_sub_sat(B, hi));
@@ -1968,20 +2043,28 @@ void launch_extract(const ImageBatch& b, const OrbGeomDev& gd, int n_images, hip
     SLAMGPU_LAUNCH("blur7_edges", st, blur7_edges_kernel, dim3(strips, n_images), dim3(64), 0, st,
                    b, gd.dev);
   }
-  if (g.fast_tile_stride == 64)
-    SLAMGPU_LAUNCH("fast_cells", st, fast_cells_kernel<64>,
-                 dim3((g.cells_per_image + kCellWaves * kCellsPerWave - 1) /
-                          (kCellWaves * kCellsPerWave), n_images),
-                 dim3(64 * kCellWaves), (size_t)kCellWaves * g.fast_lds_per_wave, st, b,
-                 gd.dev, gd.cells, gd.ws.cell_keys,
-                     gd.ws.cell_count, gd.ws.err);
-  else
-    SLAMGPU_LAUNCH("fast_cells", st, fast_cells_kernel<128>,
-                 dim3((g.cells_per_image + kCellWaves * kCellsPerWave - 1) /
-                          (kCellWaves * kCellsPerWave), n_images),
-                 dim3(64 * kCellWaves), (size_t)kCellWaves * g.fast_lds_per_wave, st, b,
-                 gd.dev, gd.cells, gd.ws.cell_keys,
-                     gd.ws.cell_count, gd.ws.err);
+  {
+    // glds tiles need every cell view 16-byte aligned: the caller's level-0 images included
+    const bool glds = ((reinterpret_cast<uintptr_t>(b.in_l) | reinterpret_cast<uintptr_t>(b.in_r) |
+                        (uintptr_t)b.in_stride | (uintptr_t)b.in_pitch |
+                        reinterpret_cast<uintptr_t>(b.pyr) | (uintptr_t)g.pyr_bytes) & 15) == 0;
+    const dim3 grid((g.cells_per_image + kCellWaves * kCellsPerWave - 1) /
+                        (kCellWaves * kCellsPerWave), n_images);
+    const dim3 block(64 * kCellWaves);
+    const size_t lds = (size_t)kCellWaves * g.fast_lds_per_wave;
+#define SLAMGPU_FAST(TS, GL)                                                                \
+  do {                                                                                      \
+    auto* kfn = &fast_cells_kernel<TS, GL>;                                                 \
+    SLAMGPU_LAUNCH("fast_cells", st, kfn, grid, block, lds, st, b, gd.dev, gd.cells,        \
+                   gd.ws.cell_keys, gd.ws.cell_count, gd.ws.err);                           \
+  } while (0)
+    if (g.fast_tile_stride == 64) {
+      if (glds) SLAMGPU_FAST(64, true); else SLAMGPU_FAST(64, false);
+    } else {
+      if (glds) SLAMGPU_FAST(128, true); else SLAMGPU_FAST(128, false);
+    }
+#undef SLAMGPU_FAST
+  }
   SLAMGPU_LAUNCH("octree", st, octree_img_kernel, dim3(n_images), dim3(64 * g.nlevels),
                  (size_t)g.oct_lds_bytes, st, gd.dev, gd.ws.cell_keys, gd.ws.cell_count,
                  gd.ws.key_scratch, gd.ws.oct_keys, gd.ws.oct_count, gd.ws.err);
