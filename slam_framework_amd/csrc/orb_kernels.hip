@@ -366,7 +366,10 @@ __global__ __launch_bounds__(64) void blur7_edges_kernel(ImageBatch b, const Orb
 // serves both passes: NMS at iniTh, and again at minTh if nothing survived (:753-757).
 // NMS is strict '>' against the 8 neighbours' scores at that t, zero outside the detect area
 // (cell-local, as cv::FAST sees only the cell view). Survivors are written in row-major order.
-constexpr int kCellWaves = 4;
+#ifndef FAST_CELL_WAVES
+#define FAST_CELL_WAVES 1
+#endif
+constexpr int kCellWaves = FAST_CELL_WAVES;  // waves per work-group
 #ifndef FAST_PRE2
 #define FAST_PRE2 1  // opposite-pair pre-test on (0,8),(4,12) only (0: all four pairs)
 #endif
@@ -471,7 +474,10 @@ constexpr uint32_t kH = 0x80808080u;
 
 // A wave runs kCellsPerWave consecutive cells of one image: the next cell's tile is loaded
 // into registers while the current one is processed from LDS.
-constexpr int kCellsPerWave = 4;
+#ifndef FAST_CELLS_PER_WAVE
+#define FAST_CELLS_PER_WAVE 4
+#endif
+constexpr int kCellsPerWave = FAST_CELLS_PER_WAVE;
 
 struct CellView {
   int level, ini_x, ini_y, vw, vh, pitch, ax, off, nd;
@@ -509,7 +515,7 @@ __device__ __forceinline__ uint4 readlane4(const uint4& x, int j) {
 // while this one is processed. Otherwise dword loads staged through registers (4-byte aligned)
 // or a byte copy.
 template <int TS, bool GLDS>
-__global__ __launch_bounds__(256, FAST_MINW) void fast_cells_kernel(ImageBatch b,
+__global__ __launch_bounds__(64 * kCellWaves, FAST_MINW) void fast_cells_kernel(ImageBatch b,
                                                          const OrbGeom* __restrict__ g,
                                                          const CellDesc* __restrict__ cells,
                                                          uint32_t* __restrict__ cell_keys,
