@@ -125,6 +125,22 @@ __device__ __forceinline__ int wave_id() {
   return __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
 }
 
+// XCD-aware (image, block) of a (blocks per image, images) grid: workgroups are dealt
+// round-robin over the 8 XCDs by linear id, so give every block of one image the same
+// (linear id % 8) -- an image's rows then stay in one XCD's L2, where neighbouring blocks share
+// their halo lines. Bijective when the image count is a multiple of 8; otherwise natural order.
+__device__ __forceinline__ void xcd_image_block(int* img, int* bx) {
+  const int bpi = gridDim.x;
+  *img = blockIdx.y;
+  *bx = blockIdx.x;
+  if ((gridDim.y & 7) == 0) {
+    const int lin = blockIdx.x + blockIdx.y * bpi;
+    const int j = lin >> 3;
+    *img = (lin & 7) + 8 * (j / bpi);
+    *bx = j % bpi;
+  }
+}
+
 template <typename T>
 __device__ __forceinline__ T wave_min(T v) {
 #pragma unroll

@@ -56,12 +56,13 @@ __global__ __launch_bounds__(256) void pyr_down_kernel(ImageBatch b, const OrbGe
                                                        int level,
                                                        const ResizeX* __restrict__ rxt,
                                                        const ResizeY* __restrict__ ryt) {
-  const int img = blockIdx.y;
+  int img, bx;
+  xcd_image_block(&img, &bx);
   const int lane = threadIdx.x & 63, wid = wave_id();
   const LevelGeom& D = g->lv[level];
   const LevelGeom& S = g->lv[level - 1];
   const int tiles_x = (D.w + 255) >> 8;
-  const int tx = blockIdx.x % tiles_x, ty = blockIdx.x / tiles_x;
+  const int tx = bx % tiles_x, ty = bx / tiles_x;
   const int dy0 = (ty * 4 + wid) * kPyrStrip;
   if (dy0 >= D.h) return;
   const int nrows = min(kPyrStrip, D.h - dy0);
@@ -184,8 +185,8 @@ __device__ __forceinline__ int reflect101(int i, int n) {
 constexpr int kBlurTileW = 256, kBlurTileH = 128, kBlurStrip = 32;
 
 __global__ __launch_bounds__(256) void blur7_kernel(ImageBatch b, const OrbGeom* __restrict__ g) {
-  const int img = blockIdx.y;
-  int tile = blockIdx.x;
+  int img, tile;
+  xcd_image_block(&img, &tile);
   int level = 0;
   while (level + 1 < g->nlevels && tile >= g->lv[level + 1].blur_tile_base) level++;
   const LevelGeom& L = g->lv[level];
@@ -529,9 +530,10 @@ __global__ __launch_bounds__(64 * kCellWaves, FAST_MINW) void fast_cells_kernel(
   constexpr int kGLpr = TS / 16, kGRows = 64 / kGLpr;   // glds: lanes per row, rows per instr.
   constexpr int kGSteps = (70 + kGRows - 1) / kGRows;
   constexpr int kAlign = GLDS ? 16 : 4;
-  const int img = blockIdx.y;
+  int img, bx;
+  xcd_image_block(&img, &bx);
   const int ncells = g->cells_per_image;
-  const int c0 = (blockIdx.x * kCellWaves + wid) * kCellsPerWave;
+  const int c0 = (bx * kCellWaves + wid) * kCellsPerWave;
   if (c0 >= ncells) return;
   const int nc = min(kCellsPerWave, ncells - c0);
   const uint4 my_desc = lane < nc ? reinterpret_cast<const uint4*>(cells)[c0 + lane]
@@ -1849,14 +1851,8 @@ __global__ __launch_bounds__(256) void orient_desc_kernel(
   // XCD-aware mapping: blocks are dealt round-robin over the 8 XCDs, so give every block of one
   // image the same (linear id % 8) -- an image's pyramid then stays in one XCD's L2
   // (bijective when the image count is a multiple of 8; otherwise the natural order is used).
-  const int bpi = gridDim.x;
-  int img = blockIdx.y, bx = blockIdx.x;
-  if ((gridDim.y & 7) == 0) {
-    const int lin = blockIdx.x + blockIdx.y * bpi;
-    const int xcd = lin & 7, j = lin >> 3;
-    img = xcd + 8 * (j / bpi);
-    bx = j % bpi;
-  }
+  int img, bx;
+  xcd_image_block(&img, &bx);
   const int lane = threadIdx.x & 63, wid = wave_id();
   int lcount[kMaxLevels];
   int total = 0;
