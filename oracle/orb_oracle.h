@@ -197,6 +197,37 @@ double oc_ba_edge_eval(const float cam[5], const double R[9], const double t[3],
                        const oc_ba_obs* o, float inv_sigma2, double err[3], double Jl[9],
                        double Jp[18]);
 
+/* ---- DBoW2 vocabulary, SearchByBoW, ComputeDistinctiveDescriptors, cvtColor (bow_oracle.c) - */
+/* The arrays TemplatedVocabulary::loadFromTextFile builds (TemplatedVocabulary.h:1335-1421):
+ * node 0 = root; node i >= 1 has parent[i] < i, the file's leaf flag, a descriptor and a weight.
+ * scoring / weighting are DBoW2's ScoringType / WeightingType values. */
+typedef struct {
+  int k, L, scoring, weighting;
+  int n_nodes;
+  const int32_t* parent;
+  const uint8_t* leaf_flag;
+  const uint8_t* desc; /* [n_nodes][32] */
+  const double* weight;
+} oc_vocab_arrays;
+typedef struct oc_vocab oc_vocab;
+oc_vocab* oc_vocab_build(const oc_vocab_arrays* a);
+void oc_vocab_free(oc_vocab* v);
+void oc_vocab_transform_one(const oc_vocab* v, const uint8_t d[32], int levelsup, uint32_t* word,
+                            double* weight, uint32_t* nid, uint32_t* leaf);
+int oc_bow_transform(const oc_vocab* v, const uint8_t* desc, int n, int levelsup, uint32_t* words,
+                     double* values, int* n_words, uint32_t* nodes, int32_t* node_start,
+                     uint32_t* node_feats, int* n_nodes);
+int oc_search_by_bow(const uint8_t* a_desc, const oc_keypoint* a_kps, const uint8_t* a_valid,
+                     int n_a, const uint32_t* a_nodes, const int32_t* a_start,
+                     const uint32_t* a_feats, int a_nn, const uint8_t* b_desc,
+                     const oc_keypoint* b_kps, const uint8_t* b_valid, int n_b,
+                     const uint32_t* b_nodes, const int32_t* b_start, const uint32_t* b_feats,
+                     int b_nn, int strict_lt, float nnratio, int check_ori, int32_t* match_a);
+void oc_distinctive_descriptors(const uint8_t* desc, const int32_t* start, int n_points,
+                                int32_t* best);
+void oc_cvt_gray(const uint8_t* src, size_t sstep, int cn, int rgb, int cols, int rows,
+                 uint8_t* dst, size_t dstep);
+
 #ifdef __cplusplus
 }
 #endif

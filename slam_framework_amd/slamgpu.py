@@ -55,6 +55,12 @@ EXPORTS = [
     "slamgpu_optimizer_last_error", "slamgpu_local_bundle_adjustment",
     "slamgpu_local_bundle_adjustment_device", "slamgpu_local_ba_workspace_bytes",
     "slamgpu_local_ba_linearize_device",
+    # include/slamgpu_bow.h
+    "slamgpu_bow_last_error", "slamgpu_vocab_load_text", "slamgpu_vocab_create",
+    "slamgpu_vocab_destroy", "slamgpu_vocab_info", "slamgpu_vocab_nodes", "slamgpu_bow_transform",
+    "slamgpu_bow_transform_device", "slamgpu_search_by_bow", "slamgpu_search_by_bow_device",
+    "slamgpu_distinctive_descriptors", "slamgpu_distinctive_descriptors_device", "slamgpu_gray",
+    "slamgpu_gray_device",
 ]
 
 
@@ -377,6 +383,36 @@ class OrbMatcher:
         a = np.ascontiguousarray(a, dtype=np.uint8)
         b = np.ascontiguousarray(b, dtype=np.uint8)
         return lib().slamgpu_descriptor_distance(_ptr(a), _ptr(b))
+
+    def SearchByBoW(self, kf, F):
+        """SearchByBoW(KeyFrame* pKF, Frame& F, vpMapPointMatches) (orb_matcher.cpp:133-262).
+        kf: .descriptors, .keypoints, .feature_vec (bow.FeatureVector), .map_points (map point id
+        per keypoint, -1 = none; a bad point counts as none); F: .descriptors, .keypoints,
+        .feature_vec. Returns (nmatches, vpMapPointMatches as ids per F keypoint, -1 = none)."""
+        from . import bow
+        mps = np.asarray(kf.map_points, np.int64)
+        nm, m = bow.search_by_bow(kf.descriptors, kf.keypoints, mps >= 0, kf.feature_vec,
+                                  F.descriptors, F.keypoints, F.feature_vec, kf_kf=False,
+                                  nnratio=self.mfNNratio, check_ori=self.mbCheckOrientation)
+        out = np.full(len(F.descriptors), -1, np.int64)
+        sel = m >= 0
+        out[m[sel]] = mps[sel]
+        return nm, out
+
+    def SearchByBoWKeyFrames(self, kf1, kf2):
+        """SearchByBoW(KeyFrame* pKF1, KeyFrame* pKF2, vpMatches12) (orb_matcher.cpp:499-632).
+        Returns (nmatches, vpMatches12 as kf2 map point ids per kf1 keypoint, -1 = none)."""
+        from . import bow
+        mp1 = np.asarray(kf1.map_points, np.int64)
+        mp2 = np.asarray(kf2.map_points, np.int64)
+        nm, m = bow.search_by_bow(kf1.descriptors, kf1.keypoints, mp1 >= 0, kf1.feature_vec,
+                                  kf2.descriptors, kf2.keypoints, kf2.feature_vec,
+                                  b_valid=mp2 >= 0, kf_kf=True, nnratio=self.mfNNratio,
+                                  check_ori=self.mbCheckOrientation)
+        out = np.full(len(kf1.descriptors), -1, np.int64)
+        sel = m >= 0
+        out[sel] = mp2[m[sel]]
+        return nm, out
 
 
 def _opt_check(rc):

@@ -326,3 +326,78 @@ def ba_problem(seed: int, n_local: int = 20, n_fixed: int = 6, n_points: int = 3
             "point_obs_start": start, "obs": obs,
             "inv_sigma2": level_inv_sigma2(scale_factor, nlevels),
             "kf_true": T_true, "points_true": np.array(pts)}
+
+
+# ---- DBoW2 vocabularies: ORBvoc.txt is not in the reference ------
+def vocabulary(seed: int, k: int = 10, L: int = 6, pool=None, scoring: int = 0,
+               weighting: int = 0, stop_frac: float = 0.02):
+    """A DBoW2 vocabulary as the arrays TemplatedVocabulary::loadFromTextFile builds
+    (TemplatedVocabulary.h:1335-1421): a complete k-ary tree of depth L in breadth-first node order
+    (parent < child, node 0 = root), the depth-L leaves flagged as words (ORBvoc.txt's shape is
+    k = 10, L = 6, L1_NORM / TF_IDF). Level-1 and level-2 centres are drawn from `pool` (real ORB
+    descriptors) when it is large enough, so that similar descriptors descend alike; otherwise,
+    and deeper, a child flips each bit of its parent's descriptor with probability 1/2 (levels
+    1-2), 1/8 (level 3) or 1/16. Word weights are idf-like U(0.1, 8), stop_frac of them 0
+    (stopped words); internal nodes weigh 0."""
+    rng = np.random.default_rng(seed)
+    sizes = [k ** l for l in range(L + 1)]
+    n = sum(sizes)
+    parent = np.zeros(n, np.int32)
+    leaf = np.zeros(n, np.uint8)
+    desc = np.zeros((n, 32), np.uint8)
+    weight = np.zeros(n, np.float64)
+    prev, start = 0, 1
+    for lvl in range(1, L + 1):
+        cnt = sizes[lvl]
+        par = prev + np.arange(cnt) // k
+        parent[start:start + cnt] = par
+        if pool is not None and lvl <= 2 and len(pool) >= cnt:
+            d = np.asarray(pool, np.uint8).reshape(-1, 32)[rng.choice(len(pool), cnt,
+                                                                      replace=False)]
+        else:
+            m = rng.integers(0, 256, (cnt, 32), dtype=np.uint8)
+            for _ in range(0 if lvl <= 2 else (2 if lvl == 3 else 3)):
+                m &= rng.integers(0, 256, (cnt, 32), dtype=np.uint8)
+            d = desc[par] ^ m
+        desc[start:start + cnt] = d
+        prev, start = start, start + cnt
+    leaf[prev:] = 1
+    w = rng.uniform(0.1, 8.0, sizes[L])
+    w[rng.random(sizes[L]) < stop_frac] = 0.0
+    weight[prev:] = w
+    return dict(k=k, L=L, scoring=scoring, weighting=weighting, parent=parent, leaf=leaf,
+                desc=desc, weight=weight)
+
+
+def random_tree_vocabulary(seed: int, n_nodes: int = 300, scoring: int = 0, weighting: int = 0,
+                           unflagged_frac: float = 0.1, stop_frac: float = 0.1):
+    """An unbalanced vocabulary tree (every node's parent a uniformly chosen earlier node):
+    leaves at mixed depths, childless nodes without the leaf flag (word id 0 with their own
+    weight, the Node() default), stopped words. L = the tree's depth."""
+    rng = np.random.default_rng(seed)
+    parent = np.zeros(n_nodes, np.int32)
+    depth = np.zeros(n_nodes, np.int32)
+    for i in range(1, n_nodes):
+        parent[i] = rng.integers(0, i)
+        depth[i] = depth[parent[i]] + 1
+    has_child = np.zeros(n_nodes, bool)
+    has_child[parent[1:]] = True
+    leaf = (~has_child).astype(np.uint8)
+    leaf[0] = 0
+    leaf[(rng.random(n_nodes) < unflagged_frac)] = 0
+    desc = rng.integers(0, 256, (n_nodes, 32), dtype=np.uint8)
+    weight = rng.uniform(0.1, 5.0, n_nodes)
+    weight[rng.random(n_nodes) < stop_frac] = 0.0
+    weight[0] = 0.0
+    return dict(k=min(20, int(np.bincount(parent[1:]).max())), L=int(depth.max()), scoring=scoring,
+                weighting=weighting, parent=parent, leaf=leaf, desc=desc, weight=weight)
+
+
+def vocabulary_text(V, trailing_newline: bool = True) -> str:
+    """V in the text format loadFromTextFile reads (saveToTextFile's layout, :1426-1446)."""
+    lines = [f"{V['k']} {V['L']}  {V['scoring']} {V['weighting']}"]
+    for i in range(1, len(V["parent"])):
+        lines.append(f"{int(V['parent'][i])} {int(V['leaf'][i])} "
+                     + " ".join(str(int(b)) for b in V["desc"][i])
+                     + f"  {repr(float(V['weight'][i]))}")
+    return "\n".join(lines) + ("\n" if trailing_newline else "")

@@ -360,3 +360,117 @@ def ba_linearize(cam, prob):
                                                              "bp")])
     out["chi"] = chi
     return out
+
+
+# ---- DBoW2 transform, SearchByBoW, ComputeDistinctiveDescriptors, cvtColor (bow_oracle.c) ------
+class VocabArrays(C.Structure):
+    _fields_ = [("k", C.c_int), ("L", C.c_int), ("scoring", C.c_int), ("weighting", C.c_int),
+                ("n_nodes", C.c_int), ("parent", C.c_void_p), ("leaf_flag", C.c_void_p),
+                ("desc", C.c_void_p), ("weight", C.c_void_p)]
+
+
+def _bow_lib():
+    L = lib()
+    if not getattr(L, "_bow_bound", False):
+        vp, ip = C.c_void_p, C.c_int
+        L.oc_vocab_build.argtypes = [C.POINTER(VocabArrays)]
+        L.oc_vocab_build.restype = vp
+        L.oc_vocab_free.argtypes = [vp]
+        L.oc_vocab_free.restype = None
+        L.oc_vocab_transform_one.argtypes = [vp, vp, ip, vp, vp, vp, vp]
+        L.oc_vocab_transform_one.restype = None
+        L.oc_bow_transform.argtypes = [vp, vp, ip, ip, vp, vp, C.POINTER(ip), vp, vp, vp,
+                                       C.POINTER(ip)]
+        L.oc_search_by_bow.argtypes = [vp, vp, vp, ip, vp, vp, vp, ip, vp, vp, vp, ip, vp, vp, vp,
+                                       ip, ip, C.c_float, ip, vp]
+        L.oc_distinctive_descriptors.argtypes = [vp, vp, ip, vp]
+        L.oc_distinctive_descriptors.restype = None
+        L.oc_cvt_gray.argtypes = [vp, C.c_size_t, ip, ip, ip, ip, vp, C.c_size_t]
+        L.oc_cvt_gray.restype = None
+        L._bow_bound = True
+    return L
+
+
+class OracleVocab:
+    """oc_vocab built from a vocabulary dict (synthetic.vocabulary layout)."""
+
+    def __init__(self, V):
+        self.keep = [np.ascontiguousarray(V["parent"], np.int32),
+                     np.ascontiguousarray(V["leaf"], np.uint8),
+                     np.ascontiguousarray(V["desc"], np.uint8).reshape(-1, 32),
+                     np.ascontiguousarray(V["weight"], np.float64)]
+        a = VocabArrays(int(V["k"]), int(V["L"]), int(V["scoring"]), int(V["weighting"]),
+                        len(self.keep[0]), *[x.ctypes.data for x in self.keep])
+        self.h = _bow_lib().oc_vocab_build(C.byref(a))
+        if not self.h:
+            raise ValueError("oc_vocab_build rejected the arrays")
+
+    def __del__(self):
+        try:
+            _bow_lib().oc_vocab_free(self.h)
+        except Exception:
+            pass
+
+
+def transform_one(ov, d, levelsup=4):
+    """(word, weight, nid, leaf) of one descriptor."""
+    d = np.ascontiguousarray(d, np.uint8)
+    w, n, f = (np.zeros(1, np.uint32) for _ in range(3))
+    wt = np.zeros(1)
+    _bow_lib().oc_vocab_transform_one(ov.h, ptr(d), levelsup, ptr(w), ptr(wt), ptr(n), ptr(f))
+    return int(w[0]), float(wt[0]), int(n[0]), int(f[0])
+
+
+def bow_transform(ov, desc, levelsup=4):
+    """transform(features, BowVector, FeatureVector, levelsup) ->
+    (words, values, nodes, node_start, node_feats)."""
+    d = np.ascontiguousarray(desc, np.uint8).reshape(-1, 32)
+    n = len(d)
+    m = max(n, 1)
+    words, vals = np.zeros(m, np.uint32), np.zeros(m)
+    nodes, feats = np.zeros(m, np.uint32), np.zeros(m, np.uint32)
+    start = np.zeros(m + 1, np.int32)
+    nw, nn = C.c_int(), C.c_int()
+    _bow_lib().oc_bow_transform(ov.h, ptr(d), n, levelsup, ptr(words), ptr(vals), C.byref(nw),
+                                ptr(nodes), ptr(start), ptr(feats), C.byref(nn))
+    nw, nn = nw.value, nn.value
+    return (words[:nw].copy(), vals[:nw].copy(), nodes[:nn].copy(), start[:nn + 1].copy(),
+            feats[:start[nn]].copy())
+
+
+def search_by_bow(a_desc, a_kps, a_valid, a_fv, b_desc, b_kps, b_valid, b_fv, strict_lt, nnratio,
+                  check_ori):
+    """a_fv / b_fv = (nodes, node_start, node_feats); b_valid None = every B feature.
+    Returns (nmatches, match_a)."""
+    def arrs(desc, kps, valid, fv):
+        return (np.ascontiguousarray(desc, np.uint8).reshape(-1, 32),
+                np.ascontiguousarray(kps).view(KP_DTYPE) if len(kps) else np.zeros(1, KP_DTYPE),
+                None if valid is None else np.ascontiguousarray(valid, np.uint8),
+                np.ascontiguousarray(fv[0], np.uint32), np.ascontiguousarray(fv[1], np.int32),
+                np.ascontiguousarray(fv[2], np.uint32))
+    A = arrs(a_desc, a_kps, a_valid, a_fv)
+    B = arrs(b_desc, b_kps, b_valid, b_fv)
+    na = len(A[0])
+    match = np.zeros(max(na, 1), np.int32)
+    p = lambda x: None if x is None else ptr(x)  # noqa: E731
+    nm = _bow_lib().oc_search_by_bow(p(A[0]), p(A[1]), p(A[2]), na, p(A[3]), p(A[4]), p(A[5]),
+                                     len(A[3]), p(B[0]), p(B[1]), p(B[2]), len(B[0]), p(B[3]),
+                                     p(B[4]), p(B[5]), len(B[3]), int(bool(strict_lt)),
+                                     float(nnratio), int(bool(check_ori)), ptr(match))
+    return nm, match[:na]
+
+
+def distinctive(desc, start):
+    d = np.ascontiguousarray(desc, np.uint8).reshape(-1, 32)
+    st = np.ascontiguousarray(start, np.int32)
+    best = np.zeros(max(len(st) - 1, 1), np.int32)
+    _bow_lib().oc_distinctive_descriptors(ptr(d), ptr(st), len(st) - 1, ptr(best))
+    return best[:len(st) - 1]
+
+
+def cvt_gray(img, rgb=True):
+    a = np.ascontiguousarray(img, np.uint8)
+    rows, cols, cn = a.shape
+    out = np.zeros((rows, cols), np.uint8)
+    _bow_lib().oc_cvt_gray(ptr(a), a.strides[0], cn, int(bool(rgb)), cols, rows, ptr(out), cols)
+    return out
