@@ -107,6 +107,8 @@ def main():
                     help="split each step's batch over this many contexts on their own HIP streams")
     ap.add_argument("--no-optimizer", action="store_true",
                     help="skip the PoseOptimization / LocalBundleAdjustment measurements")
+    ap.add_argument("--no-bow", action="store_true",
+                    help="skip the ComputeBoW / SearchByBoW measurement")
     args = ap.parse_args()
 
     import torch
@@ -277,6 +279,9 @@ def main():
         if not args.no_optimizer:
             opt = {"pose_optimization": bench_pose(dev, not args.no_cpu_baseline),
                    "local_bundle_adjustment": bench_local_ba(dev, not args.no_cpu_baseline)}
+        bow_leg = None
+        if not args.no_bow:
+            bow_leg = bench_bow(ctx, Bs, dev, not args.no_cpu_baseline)
         line = {
             "metric": "stereo frames/sec ORB extract+match @1241x376, 2000 kp/frame",
             "value": round(value, 2), "unit": "stereo frames/s", "n_gpus": world,
@@ -293,6 +298,7 @@ def main():
             "cpu_baseline": cpu,
             "kernel_ms_per_step": {n: round(brk[n][0], 4) for n in names},
             "optimizer": opt,
+            "bow": bow_leg,
             "per_rank_matches_per_step": summ[:, 1].tolist(),
         }
         print(json.dumps(line))
@@ -493,6 +499,110 @@ def bench_local_ba(dev, with_cpu):
                                "cores": threads, "kind": "port",
                                "sample": f"{done} problems ({threads} threads x {per}); "
                                          "oracle/ba_oracle.c FP64 restatement"}
+    return out
+
+
+# Algorithmic bytes of one descriptor through Frame::ComputeBoW on an ORBvoc-shaped vocabulary
+# (k = 10, L = 6): the descriptor (32 B), per level the k children's descriptors and slots
+# (10 x (32 + 16) B), the per-feature leaf / node out and back in (16 B), the feature's word,
+# weight, value, node and feature-list entries (28 B).
+BOW_BYTES_PER_DESC = 32 + 6 * 10 * 48 + 16 + 28
+
+
+def bench_bow(ctx, Bs, dev, with_cpu):
+    """SURVEY.md section 8(f) row 1 on the batch the timed step just extracted: Frame::ComputeBoW
+    (DBoW2 transform, levelsup 4) of every left view straight from the frontend's device outputs,
+    then OrbMatcher::SearchByBoW(KeyFrame = frame f, whose stereo keypoints carry map points;
+    Frame = frame f + 1) for every consecutive pair. The vocabulary is ORBvoc.txt's shape (k 10,
+    L 6, 1.1M nodes, L1 / TF-IDF), seeded, its top two levels from real descriptors: the reference
+    ships none."""
+    import torch
+    from slam_framework_amd import bow
+    from slam_framework_amd import synthetic as S
+
+    V = S.vocabulary(31, k=10, L=6, pool=ctx.keypoints(0)[1])
+    voc = bow.ORBVocabulary.from_arrays(V, device=dev.index)
+    view = ctx.device_results()
+    kc = view.kp_cap
+    cap = min(kc, bow.MAX_FEATURES)
+    sets = bow.DeviceBowSets(Bs, cap, dev)
+    stream = torch.cuda.current_stream()
+
+    def transform():
+        voc.transform_device(view.desc, 2 * kc, view.nkps, 2, Bs, 4, sets, stream.cuda_stream)
+    transform()
+    # SearchByBoW views: A = left view of frame f (valid = has stereo depth), B = frame f + 1
+    valid = np.zeros((Bs, kc), np.uint8)
+    for f in range(Bs):
+        d = ctx.stereo(f)[1]
+        valid[f, :len(d)] = d > 0
+    d_valid = torch.from_numpy(valid).to(dev)
+    va = np.zeros(Bs - 1, bow.VIEW_DTYPE)
+    vb = np.zeros(Bs - 1, bow.VIEW_DTYPE)
+    for f in range(Bs - 1):
+        for rec, fr, vld in ((va, f, int(d_valid.data_ptr()) + f * kc), (vb, f + 1, 0)):
+            rec["desc"][f] = view.desc + 2 * fr * kc * 32
+            rec["kps"][f] = view.kps + 2 * fr * kc * 28
+            rec["valid"][f] = vld
+            rec["n"][f] = view.nkps + 4 * 2 * fr
+            for k, a in sets.view_of(fr).items():
+                rec[k][f] = a
+    d_va = torch.from_numpy(va.view(np.uint8).copy()).to(dev)
+    d_vb = torch.from_numpy(vb.view(np.uint8).copy()).to(dev)
+    d_match = torch.empty((Bs - 1, cap), dtype=torch.int32, device=dev)
+    d_nm = torch.empty(Bs - 1, dtype=torch.int32, device=dev)
+
+    def search():
+        bow.search_by_bow_device(d_va, d_vb, Bs - 1, False, 0.7, True, d_match, cap, d_nm,
+                                 stream.cuda_stream)
+    search()
+    torch.cuda.synchronize()
+    t_ms = _events_ms(transform, stream, 5)
+    s_ms = _events_ms(search, stream, 5)
+    n_desc = sum(ctx.keypoints(2 * f)[0].shape[0] for f in range(Bs))
+    nm = d_nm.cpu().numpy()
+    gbs = n_desc * BOW_BYTES_PER_DESC / (t_ms * 1e-3) / 1e9
+    out = {"workload": "SURVEY 8(f) row 1: Frame::ComputeBoW (DBoW2 transform, levelsup 4, "
+                       "ORBvoc-shaped k 10 / L 6 vocabulary) of each frame's left view + "
+                       "SearchByBoW(KeyFrame f, Frame f+1), from the frontend's device outputs",
+           "frames": Bs, "transform_ms": round(t_ms, 3),
+           "transform_frames_per_s": round(Bs / t_ms * 1e3, 1),
+           "search_ms": round(s_ms, 3), "search_pairs_per_s": round((Bs - 1) / s_ms * 1e3, 1),
+           "matches_per_pair": round(float(nm.mean()), 1),
+           "roofline": {"kernel": "bow_descend + bow_vectors", "bound": "hbm",
+                        "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                        "frac": round(gbs / HBM_PEAK_GBS, 4),
+                        "algorithmic_bytes_per_descriptor": BOW_BYTES_PER_DESC,
+                        "note": "vocabulary reads are mostly L2/MALL hits; the descent is a "
+                                "6-level dependent chain per descriptor"},
+           "cpu_baseline": None}
+    if with_cpu:
+        import concurrent.futures as cf
+        sys.path.insert(0, os.path.join(ROOT, "tests"))
+        import oracle_lib as O
+        O.build()
+        ov = O.OracleVocab(V)
+        frames = [ctx.keypoints(2 * f) for f in range(min(Bs, 17))]
+        threads = min(16, os.cpu_count() or 1)
+        per = 4
+
+        def work(tid):
+            for i in range(per):
+                f = (tid + i) % (len(frames) - 1)
+                wa = O.bow_transform(ov, frames[f][1], 4)
+                wb = O.bow_transform(ov, frames[f + 1][1], 4)
+                O.search_by_bow(frames[f][1], frames[f][0], valid[f][:len(frames[f][1])],
+                                wa[2:], frames[f + 1][1], frames[f + 1][0], None, wb[2:], False,
+                                0.7, True)
+            return per
+        t0 = time.perf_counter()
+        with cf.ThreadPoolExecutor(threads) as ex:
+            done = sum(ex.map(work, range(threads)))
+        wall = time.perf_counter() - t0
+        out["cpu_baseline"] = {"value": round(done / wall, 1), "unit": "frames/s",
+                               "cores": threads, "kind": "port",
+                               "sample": f"{done} frames ({threads} threads x {per}): transform "
+                                         "of two frames + SearchByBoW; oracle/bow_oracle.c"}
     return out
 
 

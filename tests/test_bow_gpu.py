@@ -290,7 +290,8 @@ def test_cvt_gray_device_batch(oracle, B, torch_dev):
 
 def test_vocab_text_roundtrip(oracle, B, tmp_path):
     """loadFromTextFile on saveToTextFile's layout (TemplatedVocabulary.h:1335-1446)."""
-    V = S.random_tree_vocabulary(13, 400, scoring=1, weighting=0)
+    V = S.vocabulary(13, k=5, L=4, scoring=1, weighting=0)  # the header allows L <= 10 (:1356)
+    V["leaf"][np.random.default_rng(1).choice(len(V["leaf"]), 40)] = 0  # unflagged nodes
     p = tmp_path / "voc.txt"
     p.write_text(S.vocabulary_text(V) + "\n  \n")  # trailing blank lines add no node
     gv = B.ORBVocabulary()
