@@ -411,3 +411,49 @@ int oc_fast16(const uint8_t* img, int w, int h, size_t step, int threshold, int 
   free(cpmem);
   return nout;
 }
+
+/* ---- glibc 2.35 logf, x86-64 FMA ifunc variant (__logf_fma: sysdeps/ieee754/flt-32/e_logf.c
+ * compiled with -mfma -mavx2). MapPoint::PredictScale calls std::log(float) (map_point.cpp:372).
+ * Table and polynomial = __logf_data of this host's libm (16 {invc, logc} records, ln2, poly).
+ * Pinned bit-exactly against host logf on every positive float (oracle/check_logf.c). */
+static const double kLogfTab[16][2] = {
+    {0x1.661ec79f8f3bep+0, -0x1.57bf7808caadep-2}, {0x1.571ed4aaf883dp+0, -0x1.2bef0a7c06ddbp-2},
+    {0x1.49539f0f010b0p+0, -0x1.01eae7f513a67p-2}, {0x1.3c995b0b80385p+0, -0x1.b31d8a68224e9p-3},
+    {0x1.30d190c8864a5p+0, -0x1.6574f0ac07758p-3}, {0x1.25e227b0b8ea0p+0, -0x1.1aa2bc79c8100p-3},
+    {0x1.1bb4a4a1a343fp+0, -0x1.a4e76ce8c0e5ep-4}, {0x1.12358f08ae5bap+0, -0x1.1973c5a611cccp-4},
+    {0x1.0953f419900a7p+0, -0x1.252f438e10c1ep-5}, {0x1.0000000000000p+0, 0x0.0p+0},
+    {0x1.e608cfd9a47acp-1, 0x1.aa5aa5df25984p-5}, {0x1.ca4b31f026aa0p-1, 0x1.c5e53aa362eb4p-4},
+    {0x1.b2036576afce6p-1, 0x1.526e57720db08p-3}, {0x1.9c2d163a1aa2dp-1, 0x1.bc2860d224770p-3},
+    {0x1.886e6037841edp-1, 0x1.1058bc8a07ee1p-2}, {0x1.767dcf5534862p-1, 0x1.4043057b6ee09p-2}};
+static const double kLogfLn2 = 0x1.62e42fefa39efp-1;
+static const double kLogfPoly[3] = {-0x1.00ea348b88334p-2, 0x1.5575b0be00b6ap-2,
+                                    -0x1.ffffef20a4123p-2};
+
+float oc_logf(float x) {
+  uint32_t ix;
+  memcpy(&ix, &x, 4);
+  if (ix == 0x3f800000u) return 0.0f;
+  if (ix - 0x00800000u >= 0x7f800000u - 0x00800000u) {
+    /* x < 0x1p-126 or inf or nan */
+    if (ix * 2 == 0) return -INFINITY;
+    if (ix == 0x7f800000u) return x;
+    if ((ix & 0x80000000u) || ix * 2 >= 0xff000000u) return (x - x) / (x - x);
+    const float xs = x * 0x1p23f; /* subnormal: normalise */
+    memcpy(&ix, &xs, 4);
+    ix -= 23u << 23;
+  }
+  const uint32_t tmp = ix - 0x3f330000u;
+  const int i = (int)((tmp >> (23 - 4)) % 16);
+  const int k = (int32_t)tmp >> 23;
+  const uint32_t iz = ix - (tmp & 0xff800000u);
+  float zf;
+  memcpy(&zf, &iz, 4);
+  const double invc = kLogfTab[i][0], logc = kLogfTab[i][1], z = (double)zf;
+  const double r = fma(z, invc, -1.0);
+  const double y0 = fma((double)k, kLogfLn2, logc);
+  const double r2 = r * r;
+  double y = fma(kLogfPoly[1], r, kLogfPoly[2]);
+  y = fma(kLogfPoly[0], r2, y);
+  y = fma(y, r2, y0 + r);
+  return (float)y;
+}

@@ -80,6 +80,7 @@ int oc_cv_round(float v);                              /* cvRound(float): half-t
 float oc_fast_atan2(float y, float x);                 /* cv::fastAtan2, degrees [0,360)    */
 float oc_sinf(float x);                                /* glibc 2.35 __sinf_fma             */
 float oc_cosf(float x);                                /* glibc 2.35 __cosf_fma             */
+float oc_logf(float x);                                /* glibc 2.35 __logf_fma             */
 void oc_resize_linear_u8(const uint8_t* src, int sw, int sh, size_t sstep, uint8_t* dst, int dw,
                          int dh, size_t dstep);
 void oc_gaussian_blur7_u8(const uint8_t* src, int w, int h, size_t sstep, uint8_t* dst,
@@ -227,6 +228,36 @@ void oc_distinctive_descriptors(const uint8_t* desc, const int32_t* start, int n
                                 int32_t* best);
 void oc_cvt_gray(const uint8_t* src, size_t sstep, int cn, int rgb, int cols, int rows,
                  uint8_t* dst, size_t dstep);
+
+/* ---- keyframe-rate matchers (kfmatch_oracle.c) ---------------------------------------- */
+typedef struct {
+  float xyz[3];      /* GetWorldPos()                                              */
+  float normal[3];   /* GetNormal()                                                */
+  float min_dist;    /* min_dist_ (GetMinDistanceInvariance() = 0.8f * min_dist_)  */
+  float max_dist;    /* max_dist_ (GetMaxDistanceInvariance() = 1.2f * max_dist_)  */
+  int32_t skip;      /* !pMP || isBad() || IsInKeyFrame(pKF)                       */
+  int32_t pad[3];
+  uint8_t desc[32];  /* GetDescriptor()                                            */
+} oc_fuse_point;     /* 80 B, == slamgpu_fuse_point */
+
+int oc_check_dist_epipolar(const oc_keypoint* kp1, const oc_keypoint* kp2, const float* F,
+                           const float* sigma2);
+void oc_epipole(const float* C1w, const float* T2w, float fx, float fy, float cx, float cy,
+                float* ex, float* ey);
+int oc_search_for_triangulation(
+    const oc_keypoint* k1, const uint8_t* d1, const float* ur1, const uint8_t* mp1, int n1,
+    const uint32_t* nodes1, const int32_t* start1, const uint32_t* feats1, int nn1,
+    const oc_keypoint* k2, const uint8_t* d2, const float* ur2, const uint8_t* mp2,
+    const uint32_t* nodes2, const int32_t* start2, const uint32_t* feats2, int nn2,
+    const float* C1w, const float* T2w, float fx, float fy, float cx, float cy,
+    const float* scale, const float* sigma2, const float* F12, int only_stereo, int check_ori,
+    int32_t* match12);
+int oc_predict_scale(float max_dist, float dist, float log_scale_factor, int nlevels);
+int oc_fuse(const oc_keypoint* kps, const uint8_t* desc, const float* ur, int n,
+            const oc_grid_geom* g, const float* Rcw, const float* tcw, const float* Ow, float fx,
+            float fy, float cx, float cy, float bf, const float* scale, const float* inv_sigma2,
+            int nlevels, float log_scale_factor, const oc_fuse_point* pts, int n_pts, float th,
+            int32_t* best_idx, int32_t* best_dist);
 
 #ifdef __cplusplus
 }

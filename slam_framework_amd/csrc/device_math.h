@@ -117,6 +117,41 @@ __device__ __forceinline__ uint32_t mulhi24(uint32_t a, uint32_t b) {
   return (uint32_t)(((uint64_t)(a & 0xffffffu) * (uint64_t)(b & 0xffffffu)) >> 32);
 }
 
+// glibc 2.35 logf, x86-64 FMA variant (__logf_fma; reference: std::log(float) in
+// MapPoint::PredictScale, src/data/map_point.cpp:372). Same table and polynomial as libm's
+// __logf_data; oracle/oc_logf is pinned against host logf on every positive float. Inputs here
+// are finite and positive (max_dist / dist); 0, inf and nan follow glibc too.
+__device__ __forceinline__ float glibc_logf(float x) {
+  static __device__ __constant__ double tab[16][2] = {
+      {0x1.661ec79f8f3bep+0, -0x1.57bf7808caadep-2}, {0x1.571ed4aaf883dp+0, -0x1.2bef0a7c06ddbp-2},
+      {0x1.49539f0f010b0p+0, -0x1.01eae7f513a67p-2}, {0x1.3c995b0b80385p+0, -0x1.b31d8a68224e9p-3},
+      {0x1.30d190c8864a5p+0, -0x1.6574f0ac07758p-3}, {0x1.25e227b0b8ea0p+0, -0x1.1aa2bc79c8100p-3},
+      {0x1.1bb4a4a1a343fp+0, -0x1.a4e76ce8c0e5ep-4}, {0x1.12358f08ae5bap+0, -0x1.1973c5a611cccp-4},
+      {0x1.0953f419900a7p+0, -0x1.252f438e10c1ep-5}, {0x1.0000000000000p+0, 0x0.0p+0},
+      {0x1.e608cfd9a47acp-1, 0x1.aa5aa5df25984p-5}, {0x1.ca4b31f026aa0p-1, 0x1.c5e53aa362eb4p-4},
+      {0x1.b2036576afce6p-1, 0x1.526e57720db08p-3}, {0x1.9c2d163a1aa2dp-1, 0x1.bc2860d224770p-3},
+      {0x1.886e6037841edp-1, 0x1.1058bc8a07ee1p-2}, {0x1.767dcf5534862p-1, 0x1.4043057b6ee09p-2}};
+  uint32_t ix = __float_as_uint(x);
+  if (ix == 0x3f800000u) return 0.0f;
+  if (ix - 0x00800000u >= 0x7f800000u - 0x00800000u) {
+    if (ix * 2 == 0) return -__builtin_inff();
+    if (ix == 0x7f800000u) return x;
+    if ((ix & 0x80000000u) || ix * 2 >= 0xff000000u) return __builtin_nanf("");
+    ix = __float_as_uint(x * 0x1p23f) - (23u << 23);
+  }
+  const uint32_t tmp = ix - 0x3f330000u;
+  const int i = (int)((tmp >> 19) & 15);
+  const int k = (int32_t)tmp >> 23;
+  const double z = (double)__uint_as_float(ix - (tmp & 0xff800000u));
+  const double r = fma(z, tab[i][0], -1.0);
+  const double y0 = fma((double)k, 0x1.62e42fefa39efp-1, tab[i][1]);
+  const double r2 = r * r;
+  double y = fma(0x1.5575b0be00b6ap-2, r, -0x1.ffffef20a4123p-2);
+  y = fma(-0x1.00ea348b88334p-2, r2, y);
+  y = fma(y, r2, y0 + r);
+  return (float)y;
+}
+
 // ---- wavefront (64-lane) helpers --------------------------------------------------------
 __device__ __forceinline__ int lane_id() { return __lane_id(); }
 // Wave index inside the workgroup, as a scalar (the compiler cannot prove threadIdx.x >> 6 is

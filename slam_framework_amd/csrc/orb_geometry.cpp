@@ -12,6 +12,10 @@
 #include <cmath>
 #include <cstring>
 
+#ifndef BLUR_STRIP
+#define BLUR_STRIP 32  // == orb_kernels.hip's blur7 rows per wave
+#endif
+
 namespace slamgpu {
 
 static inline int cv_round_h(float v) { return (int)std::lrintf(v); }
@@ -177,7 +181,7 @@ int compute_geometry(const OrbParams& p, int cols, int rows, OrbGeom* g,
     boff += (int64_t)L.pitch * L.h;
     boff = (boff + 255) & ~(int64_t)255;
     L.blur_tile_base = btiles;
-    btiles += ((L.w + 255) / 256) * ((L.h + 127) / 128);  // blur7 tiles: 256 x 128
+    btiles += ((L.w + 255) / 256) * ((L.h + 4 * BLUR_STRIP - 1) / (4 * BLUR_STRIP));  // 256 x 4 strips
   }
   g->blur_bytes = boff;
   g->blur_tiles = btiles;

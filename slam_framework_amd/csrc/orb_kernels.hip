@@ -49,8 +49,14 @@ __device__ __forceinline__ uint32_t dot2u(uint32_t a, uint32_t b, uint32_t c) {
                                 false);
 }
 
-constexpr int kPyrStrip = 16;  // output rows per wave
-constexpr int kPyrChunk = 4;   // source rows fetched per batch
+#ifndef PYR_STRIP
+#define PYR_STRIP 16
+#endif
+#ifndef PYR_CHUNK
+#define PYR_CHUNK 4
+#endif
+constexpr int kPyrStrip = PYR_STRIP;  // output rows per wave
+constexpr int kPyrChunk = PYR_CHUNK;  // source rows fetched per batch
 
 __global__ __launch_bounds__(256) void pyr_down_kernel(ImageBatch b, const OrbGeom* __restrict__ g,
                                                        int level,
@@ -182,7 +188,10 @@ __device__ __forceinline__ int reflect101(int i, int n) {
   return i;
 }
 
-constexpr int kBlurTileW = 256, kBlurTileH = 128, kBlurStrip = 32;
+#ifndef BLUR_STRIP
+#define BLUR_STRIP 32
+#endif
+constexpr int kBlurTileW = 256, kBlurStrip = BLUR_STRIP, kBlurTileH = 4 * kBlurStrip;
 
 __global__ __launch_bounds__(256) void blur7_kernel(ImageBatch b, const OrbGeom* __restrict__ g) {
   int img, tile;

@@ -61,6 +61,9 @@ EXPORTS = [
     "slamgpu_bow_transform_device", "slamgpu_search_by_bow", "slamgpu_search_by_bow_device",
     "slamgpu_distinctive_descriptors", "slamgpu_distinctive_descriptors_device", "slamgpu_gray",
     "slamgpu_gray_device",
+    # include/slamgpu_kfmatch.h
+    "slamgpu_kfmatch_last_error", "slamgpu_search_for_triangulation",
+    "slamgpu_search_for_triangulation_device", "slamgpu_fuse", "slamgpu_fuse_device",
 ]
 
 
@@ -413,6 +416,30 @@ class OrbMatcher:
         sel = m >= 0
         out[sel] = mp2[m[sel]]
         return nm, out
+
+
+    def SearchForTriangulation(self, kf1, kf2, F12, cam, levels, bOnlyStereo=False):
+        """SearchForTriangulation(pKF1, pKF2, F12, vMatchedPairs, bOnlyStereo)
+        (orb_matcher.cpp:634-802). kf: .keypoints, .descriptors, .u_right, .map_points (-1 =
+        none), .feature_vec, .Tcw. Returns (nmatches, vMatchedPairs as an (n, 2) array)."""
+        from . import kfmatch as K
+        a = K.host_kf(kf1.keypoints, kf1.descriptors, kf1.u_right, kf1.Tcw,
+                      np.asarray(kf1.map_points) >= 0, kf1.feature_vec)
+        b = K.host_kf(kf2.keypoints, kf2.descriptors, kf2.u_right, kf2.Tcw,
+                      np.asarray(kf2.map_points) >= 0, kf2.feature_vec)
+        nm, m = K.search_for_triangulation(a, b, F12, cam, levels, bOnlyStereo,
+                                           self.mbCheckOrientation)
+        i = np.nonzero(m >= 0)[0]
+        return nm, np.stack([i, m[i]], 1)
+
+    def Fuse(self, kf, points, th, cam, levels, grid):
+        """Fuse(pKF, vpMapPoints, th) (orb_matcher.cpp:804-954): the per-point candidate search
+        on the device; returns (nfused, best_idx) -- kfmatch.fuse_apply walks it as the
+        reference does."""
+        from . import kfmatch as K
+        k = K.host_kf(kf.keypoints, kf.descriptors, kf.u_right, kf.Tcw)
+        nf, bi, _ = K.fuse(k, points, th, cam, levels, grid)
+        return nf, bi
 
 
 def _opt_check(rc):

@@ -474,3 +474,63 @@ def cvt_gray(img, rgb=True):
     out = np.zeros((rows, cols), np.uint8)
     _bow_lib().oc_cvt_gray(ptr(a), a.strides[0], cn, int(bool(rgb)), cols, rows, ptr(out), cols)
     return out
+
+
+# ---- SearchForTriangulation, Fuse (kfmatch_oracle.c) -------------------------------------------
+def _kf_lib():
+    L = lib()
+    if not getattr(L, "_kf_bound", False):
+        vp, ip, fp = C.c_void_p, C.c_int, C.c_float
+        L.oc_search_for_triangulation.argtypes = [vp, vp, vp, vp, ip, vp, vp, vp, ip,
+                                                  vp, vp, vp, vp, vp, vp, vp, ip,
+                                                  vp, vp, fp, fp, fp, fp, vp, vp, vp, ip, ip, vp]
+        L.oc_fuse.argtypes = [vp, vp, vp, ip, C.POINTER(GridGeom), vp, vp, vp, fp, fp, fp, fp, fp,
+                              vp, vp, ip, fp, vp, ip, fp, vp, vp]
+        L.oc_predict_scale.argtypes = [fp, fp, fp, ip]
+        L.oc_logf.argtypes = [fp]
+        L.oc_logf.restype = fp
+        L._kf_bound = True
+    return L
+
+
+def search_for_triangulation(kf1, kf2, C1w, T2w, cam4, scale, sigma2, F12, only_stereo,
+                             check_ori):
+    """kf = dict(kps, desc, ur, mp (u8), fv=(nodes, start, feats)). T2w = R (row-major) + t.
+    Returns (nmatches, match12)."""
+    def arrs(k):
+        return (np.ascontiguousarray(k["kps"]).view(KP_DTYPE) if len(k["kps"]) else
+                np.zeros(1, KP_DTYPE),
+                np.ascontiguousarray(k["desc"], np.uint8).reshape(-1, 32),
+                np.ascontiguousarray(k["ur"], np.float32), np.ascontiguousarray(k["mp"], np.uint8),
+                np.ascontiguousarray(k["fv"][0], np.uint32),
+                np.ascontiguousarray(k["fv"][1], np.int32),
+                np.ascontiguousarray(k["fv"][2], np.uint32))
+    A, B = arrs(kf1), arrs(kf2)
+    n1 = len(A[1])
+    m = np.zeros(max(n1, 1), np.int32)
+    f = lambda a: np.ascontiguousarray(a, np.float32).reshape(-1)  # noqa: E731
+    keep = [f(C1w), f(T2w), f(scale), f(sigma2), f(F12)]
+    nm = _kf_lib().oc_search_for_triangulation(
+        ptr(A[0]), ptr(A[1]), ptr(A[2]), ptr(A[3]), n1, ptr(A[4]), ptr(A[5]), ptr(A[6]), len(A[4]),
+        ptr(B[0]), ptr(B[1]), ptr(B[2]), ptr(B[3]), ptr(B[4]), ptr(B[5]), ptr(B[6]), len(B[4]),
+        ptr(keep[0]), ptr(keep[1]), *[float(np.float32(c)) for c in cam4], ptr(keep[2]),
+        ptr(keep[3]), ptr(keep[4]), int(bool(only_stereo)), int(bool(check_ori)), ptr(m))
+    return nm, m[:n1]
+
+
+def fuse(kps, desc, ur, grid, Rcw, tcw, Ow, cam, scale, inv_sigma2, log_scale_factor, points, th):
+    """Fuse's candidate search; grid = GridGeom; points = FUSE_POINT records (80 B).
+    Returns (nfused, best_idx, best_dist)."""
+    k = np.ascontiguousarray(kps).view(KP_DTYPE)
+    d = np.ascontiguousarray(desc, np.uint8).reshape(-1, 32)
+    u = np.ascontiguousarray(ur, np.float32)
+    f = lambda a: np.ascontiguousarray(a, np.float32).reshape(-1)  # noqa: E731
+    keep = [f(Rcw), f(tcw), f(Ow), f(scale), f(inv_sigma2)]
+    pts = np.ascontiguousarray(points)
+    n = len(pts)
+    bi, bd = np.zeros(max(n, 1), np.int32), np.zeros(max(n, 1), np.int32)
+    nf = _kf_lib().oc_fuse(ptr(k), ptr(d), ptr(u), len(d), C.byref(grid), ptr(keep[0]),
+                           ptr(keep[1]), ptr(keep[2]), *[float(np.float32(c)) for c in cam],
+                           ptr(keep[3]), ptr(keep[4]), len(keep[3]), float(log_scale_factor),
+                           ptr(pts), n, float(th), ptr(bi), ptr(bd))
+    return nf, bi[:n], bd[:n]
