@@ -607,6 +607,129 @@ def bench_bow(ctx, Bs, dev, with_cpu):
                                "cores": threads, "kind": "port",
                                "sample": f"{done} frames ({threads} threads x {per}): transform "
                                          "of two frames + SearchByBoW; oracle/bow_oracle.c"}
+    out["keyframe_matchers"] = bench_kfmatch(ctx, Bs, dev, view, sets, with_cpu)
+    return out
+
+
+def bench_kfmatch(ctx, Bs, dev, view, sets, with_cpu):
+    """SURVEY.md section 8(f) row 3 on the same batch, every frame taken as a keyframe (for the
+    triangulation search the sequence rotation plus a 0.4 m step along x per frame, so that F12
+    is well defined; for Fuse the pure rotations the frames were rendered at):
+    SearchForTriangulation(KF f, KF f+1) with 30% of the keypoints already carrying map points,
+    and Fuse of KF f's stereo points (unprojected from its depths) into KF f+1, th = 3."""
+    import torch
+    from slam_framework_amd import kfmatch as K
+    from slam_framework_amd import synthetic as S
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import kf_scenario as KS
+
+    kc = view.kp_cap
+    D = 16
+    Ts = [KS.pose(f % D, (-0.4 * (f % D), 0.0, 0.0)) for f in range(Bs)]
+    host = [ctx.keypoints(2 * f) for f in range(Bs)]
+    depth = [ctx.stereo(f)[1] for f in range(Bs)]
+    nn = sets.n_nodes.cpu().numpy()
+    rng = np.random.default_rng(5)
+    has_mp = torch.from_numpy((rng.random((Bs, kc)) < 0.3).astype(np.uint8)).to(dev)
+    kfs = np.zeros(Bs, K.KF_DTYPE)
+    for f in range(Bs):
+        h = K.host_kf(host[f][0][:1], host[f][1][:1], np.zeros(1, np.float32), Ts[f])[0]
+        kfs[f]["kps"] = view.kps + 2 * f * kc * 28
+        kfs[f]["desc"] = view.desc + 2 * f * kc * 32
+        kfs[f]["u_right"] = view.u_right + f * kc * 4
+        kfs[f]["has_mp"] = int(has_mp.data_ptr()) + f * kc
+        for k, a in sets.view_of(f).items():
+            if k != "n_nodes":
+                kfs[f][k] = a
+        kfs[f]["n"], kfs[f]["n_nodes"] = len(host[f][1]), nn[f]
+        kfs[f]["Rcw"], kfs[f]["tcw"], kfs[f]["Ow"] = list(h.Rcw), list(h.tcw), list(h.Ow)
+    d_kfs = torch.from_numpy(kfs.view(np.uint8).copy()).to(dev)
+    # Fuse uses the poses the images were rendered at (pure rotation), so that points re-project
+    kfs_r = kfs.copy()
+    Tr = [KS.pose(f % D) for f in range(Bs)]
+    for f in range(Bs):
+        kfs_r[f]["tcw"], kfs_r[f]["Ow"] = 0.0, 0.0
+        kfs_r[f]["Rcw"] = Tr[f][:3, :3].reshape(-1)
+    d_kfs_r = torch.from_numpy(kfs_r.view(np.uint8).copy()).to(dev)
+    pairs = np.zeros(Bs - 1, K.TRI_PAIR_DTYPE)
+    for f in range(Bs - 1):
+        pairs[f] = (f, f + 1, KS.fundamental(Ts[f], Ts[f + 1]).reshape(-1), 0)
+    d_pairs = torch.from_numpy(pairs.view(np.uint8).copy()).to(dev)
+    d_m = torch.empty((Bs - 1, kc), dtype=torch.int32, device=dev)
+    d_nm = torch.empty(Bs - 1, dtype=torch.int32, device=dev)
+    lv = K.levels()
+    stream = torch.cuda.current_stream()
+
+    def tri():
+        K.search_for_triangulation_device(d_kfs, d_pairs, Bs - 1, S.KITTI_CAM, lv, True, d_m, kc,
+                                          d_nm, stream.cuda_stream)
+    # Fuse points of KF f into KF f + 1
+    pts, pkf = [], []
+    for f in range(Bs - 1):
+        p = KS.fuse_points({"kps": host[f][0], "desc": host[f][1], "depth": depth[f]}, Tr[f],
+                           n_extra=0)
+        pts.append(p)
+        pkf.append(np.full(len(p), f + 1, np.int32))
+    pts, pkf = np.concatenate(pts), np.concatenate(pkf)
+    d_pts = torch.from_numpy(pts.view(np.uint8).copy()).to(dev)
+    d_pkf = torch.from_numpy(pkf).to(dev)
+    d_bi = torch.empty(len(pts), dtype=torch.int32, device=dev)
+    d_bd = torch.empty(len(pts), dtype=torch.int32, device=dev)
+    grid = K.kf_grid(S.KITTI_COLS, S.KITTI_ROWS)
+
+    def fuse():
+        K.fuse_device(d_kfs_r, d_pts, d_pkf, len(pts), 3.0, S.KITTI_CAM, lv, grid, d_bi, d_bd,
+                      stream.cuda_stream)
+    tri()
+    fuse()
+    torch.cuda.synchronize()
+    t_ms, f_ms = _events_ms(tri, stream, 5), _events_ms(fuse, stream, 5)
+    nm, bi = d_nm.cpu().numpy(), d_bi.cpu().numpy()
+    out = {"workload": "SURVEY 8(f) row 3: SearchForTriangulation(KF f, KF f+1) and Fuse(KF f+1, "
+                       "KF f's stereo points, th 3) over the batch, from the frontend's device "
+                       "outputs and the BoW leg's FeatureVectors",
+           "pairs": Bs - 1, "triangulation_ms": round(t_ms, 3),
+           "triangulation_pairs_per_s": round((Bs - 1) / t_ms * 1e3, 1),
+           "triangulation_matches_per_pair": round(float(nm.mean()), 1),
+           "fuse_points": int(len(pts)), "fuse_ms": round(f_ms, 3),
+           "fuse_points_per_s": round(len(pts) / f_ms * 1e3),
+           "fused_per_keyframe": round(float((bi >= 0).sum()) / (Bs - 1), 1),
+           "cpu_baseline": None}
+    if with_cpu:
+        import concurrent.futures as cf
+        import oracle_lib as O
+        O.build()
+        sc, s2, isg, _ = KS.levels_arrays()
+        g = O.grid_geom(S.KITTI_COLS, S.KITTI_ROWS)
+        ur = [ctx.stereo(f)[0] for f in range(min(Bs, 17))]
+        mp = has_mp.cpu().numpy()
+        fvs = [sets.host(f)[1].arrays() for f in range(min(Bs, 17))]
+        kd = [dict(kps=host[f][0], desc=host[f][1], ur=ur[f], mp=mp[f][:len(host[f][1])],
+                   fv=fvs[f]) for f in range(min(Bs, 17))]
+        threads = min(16, os.cpu_count() or 1)
+        per = 4
+
+        def work(tid):
+            for i in range(per):
+                f = (tid + i) % (len(kd) - 1)
+                T2 = Ts[f + 1]
+                T2w = np.concatenate([T2[:3, :3].reshape(-1), T2[:3, 3]]).astype(np.float32)
+                O.search_for_triangulation(kd[f], kd[f + 1], kfs[f]["Ow"], T2w, S.KITTI_CAM[:4],
+                                           sc, s2, pairs[f]["F12"], 0, 1)
+                sel = pkf == f + 1
+                O.fuse(kd[f + 1]["kps"], kd[f + 1]["desc"], kd[f + 1]["ur"], g,
+                       Tr[f + 1][:3, :3].reshape(-1), Tr[f + 1][:3, 3], kfs_r[f + 1]["Ow"],
+                       S.KITTI_CAM, sc, isg,
+                       float(lv.log_scale_factor), pts[sel], 3.0)
+            return per
+        t0 = time.perf_counter()
+        with cf.ThreadPoolExecutor(threads) as ex:
+            done = sum(ex.map(work, range(threads)))
+        wall = time.perf_counter() - t0
+        out["cpu_baseline"] = {"value": round(done / wall, 1), "unit": "keyframe pairs/s",
+                               "cores": threads, "kind": "port",
+                               "sample": f"{done} pairs ({threads} threads x {per}): "
+                                         "SearchForTriangulation + Fuse; oracle/kfmatch_oracle.c"}
     return out
 
 
