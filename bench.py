@@ -403,7 +403,7 @@ def bench_pose(dev, with_cpu):
 def bench_local_ba(dev, with_cpu):
     """configs[4]: Optimizer::LocalBundleAdjustment on SURVEY.md section 8(d) C5 (20 local + 5
     fixed keyframes at 1 m spacing, 3000 map points seen by 2-6 keyframes, ~12k observations;
-    seed 11), one problem and a batch of 64; the oracle on host cores."""
+    seed 11), one problem and a batch of 256 (one per CU); the oracle on host cores."""
     import torch
     from slam_framework_amd import slamgpu as G
     from slam_framework_amd import synthetic as S
@@ -412,7 +412,8 @@ def bench_local_ba(dev, with_cpu):
     nk, npn, no = len(P["kf_mode"]), len(P["points"]), len(P["obs"])
     stream = torch.cuda.current_stream()
     res = {}
-    for B in (1, 64):
+    BB = 256  # one problem per CU: a workgroup runs a whole problem
+    for B in (1, BB):
         desc = np.array([(i * nk, nk, i * npn, npn) for i in range(B)], np.int32)
         start = np.concatenate([P["point_obs_start"][:-1] + i * no for i in range(B)] +
                                [[B * no]]).astype(np.int32)
@@ -475,7 +476,7 @@ def bench_local_ba(dev, with_cpu):
            "workload": "configs[4]: LocalBundleAdjustment on SURVEY 8(d) C5, 20 local + 5 fixed "
                        f"keyframes x 3000 map points ({no} observations), 5 robust + 10 LM "
                        "iterations (FP64)",
-           "problems_per_s": round(64 / res[64][0] * 1e3, 1), "batch_problems": 64,
+           "problems_per_s": round(BB / res[BB][0] * 1e3, 1), "batch_problems": BB,
            "single_problem_ms": round(res[1][0], 3), "lm_iterations": res[1][1],
            "cpu_baseline": None}
     if with_cpu:

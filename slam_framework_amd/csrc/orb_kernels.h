@@ -57,6 +57,15 @@ struct OrbGeomDev {
   ExtractOutput out;
 };
 
-void launch_extract(const ImageBatch& b, const OrbGeomDev& g, int n_images, hipStream_t st);
+// Optional side streams of the extraction (all null: everything on `st`):
+//   side0: FAST of level 0 (reads only the caller's images) beside the pyramid, joined before
+//          the octree;
+//   side:  the blur (descriptor input) beside fast_cells + octree, joined before orient_desc.
+struct ExtractStreams {
+  hipStream_t side0 = nullptr, side = nullptr;
+  hipEvent_t fork0 = nullptr, join0 = nullptr, fork = nullptr, join = nullptr;
+};
+void launch_extract(const ImageBatch& b, const OrbGeomDev& g, int n_images, hipStream_t st,
+                    const ExtractStreams& fx = ExtractStreams());
 
 }  // namespace slamgpu

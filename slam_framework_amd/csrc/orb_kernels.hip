@@ -530,7 +530,8 @@ __global__ __launch_bounds__(64 * kCellWaves, FAST_MINW) void fast_cells_kernel(
                                                          const CellDesc* __restrict__ cells,
                                                          uint32_t* __restrict__ cell_keys,
                                                          int* __restrict__ cell_count,
-                                                         uint32_t* __restrict__ err) {
+                                                         uint32_t* __restrict__ err,
+                                                         int cell_lo, int cell_hi) {
   extern __shared__ __attribute__((aligned(16))) uint8_t s_fast[];
   const int wid = wave_id(), lane = threadIdx.x & 63;
   constexpr int kTileStride = TS, kScoreStride = TS;  // == g->fast_tile_stride
@@ -541,10 +542,10 @@ __global__ __launch_bounds__(64 * kCellWaves, FAST_MINW) void fast_cells_kernel(
   constexpr int kAlign = GLDS ? 16 : 4;
   int img, bx;
   xcd_image_block(&img, &bx);
-  const int ncells = g->cells_per_image;
-  const int c0 = (bx * kCellWaves + wid) * kCellsPerWave;
-  if (c0 >= ncells) return;
-  const int nc = min(kCellsPerWave, ncells - c0);
+  const int ncells = g->cells_per_image;  // per-image stride; this launch runs [cell_lo, cell_hi)
+  const int c0 = cell_lo + (bx * kCellWaves + wid) * kCellsPerWave;
+  if (c0 >= cell_hi) return;
+  const int nc = min(kCellsPerWave, cell_hi - c0);
   const uint4 my_desc = lane < nc ? reinterpret_cast<const uint4*>(cells)[c0 + lane]
                                   : make_uint4(0, 0, 0, 0);
   const int in_pitch = __builtin_amdgcn_readfirstlane(b.in_pitch);
@@ -1435,6 +1436,9 @@ __global__ __launch_bounds__(64 * kMaxLevels) void octree_img_kernel(
   }
   __syncthreads();
   if (!active) return;
+#ifdef OCT_LEVEL_MASK  // timing ablation only: skip the levels not in the mask
+  if (!((OCT_LEVEL_MASK >> level) & 1)) return;
+#endif
   int* const outc = oct_count + img * nlev + level;
   uint32_t* const outk = oct_keys + (int64_t)img * g->out_per_image + L.out_base;
   const int nIni = L.n_ini;
@@ -2040,41 +2044,91 @@ __global__ __launch_bounds__(256) void orient_desc_kernel(
 
 // ---------------------------------------------------------------------------------------
 // Host-side launchers.
-void launch_extract(const ImageBatch& b, const OrbGeomDev& gd, int n_images, hipStream_t st) {
+void launch_extract(const ImageBatch& b, const OrbGeomDev& gd, int n_images, hipStream_t st,
+                    const ExtractStreams& fx) {
   const OrbGeom& g = *gd.host;
+  // glds tiles need every cell view 16-byte aligned: the caller's level-0 images included
+  const bool glds = ((reinterpret_cast<uintptr_t>(b.in_l) | reinterpret_cast<uintptr_t>(b.in_r) |
+                      (uintptr_t)b.in_stride | (uintptr_t)b.in_pitch |
+                      reinterpret_cast<uintptr_t>(b.pyr) | (uintptr_t)g.pyr_bytes) & 15) == 0;
+  // FAST of level 0 reads only the caller's images: with a second side stream it runs beside
+  // the pyramid (whose small levels leave the chip mostly idle)
+  const bool split0 = fx.side0 && fx.fork0 && fx.join0 && g.nlevels > 1;
+  if (split0) {
+    (void)hipEventRecord(fx.fork0, st);
+    (void)hipStreamWaitEvent(fx.side0, fx.fork0, 0);
+  }
+  auto fast_level0 = [&]() {
+    const dim3 block(64 * kCellWaves);
+    const size_t lds = (size_t)kCellWaves * g.fast_lds_per_wave;
+    const int lo = 0, hi = g.lv[1].cell_base;
+    const dim3 grid((hi - lo + kCellWaves * kCellsPerWave - 1) / (kCellWaves * kCellsPerWave),
+                    n_images);
+    hipStream_t fs = fx.side0;
+    if (g.fast_tile_stride == 64) {
+      if (glds)
+        SLAMGPU_LAUNCH("fast_cells", fs, (fast_cells_kernel<64, true>), grid, block, lds, fs, b,
+                       gd.dev, gd.cells, gd.ws.cell_keys, gd.ws.cell_count, gd.ws.err, lo, hi);
+      else
+        SLAMGPU_LAUNCH("fast_cells", fs, (fast_cells_kernel<64, false>), grid, block, lds, fs, b,
+                       gd.dev, gd.cells, gd.ws.cell_keys, gd.ws.cell_count, gd.ws.err, lo, hi);
+    } else {
+      if (glds)
+        SLAMGPU_LAUNCH("fast_cells", fs, (fast_cells_kernel<128, true>), grid, block, lds, fs, b,
+                       gd.dev, gd.cells, gd.ws.cell_keys, gd.ws.cell_count, gd.ws.err, lo, hi);
+      else
+        SLAMGPU_LAUNCH("fast_cells", fs, (fast_cells_kernel<128, false>), grid, block, lds, fs,
+                       b, gd.dev, gd.cells, gd.ws.cell_keys, gd.ws.cell_count, gd.ws.err, lo, hi);
+    }
+    (void)hipEventRecord(fx.join0, fs);
+  };
+  if (split0) fast_level0();
   for (int l = 1; l < g.nlevels; l++) {
     const int tiles = ((g.lv[l].w + 255) >> 8) * ((g.lv[l].h + 4 * kPyrStrip - 1) / (4 * kPyrStrip));
     SLAMGPU_LAUNCH("pyr_down", st, pyr_down_kernel, dim3(tiles, n_images), dim3(256), 0, st, b,
                    gd.dev, l, gd.rx, gd.ry);
   }
-  SLAMGPU_LAUNCH("blur7", st, blur7_kernel, dim3(g.blur_tiles, n_images), dim3(256), 0, st, b, gd.dev);
+  // the blurred pyramid only feeds orient_desc: with a side stream it overlaps fast_cells +
+  // octree (the octree's long level-0 waves leave most SIMDs idle)
+  hipStream_t bs = st;
+  if (fx.side && fx.fork && fx.join) {
+    (void)hipEventRecord(fx.fork, st);
+    (void)hipStreamWaitEvent(fx.side, fx.fork, 0);
+    bs = fx.side;
+  }
+  SLAMGPU_LAUNCH("blur7", bs, blur7_kernel, dim3(g.blur_tiles, n_images), dim3(256), 0, bs, b, gd.dev);
   {
     int strips = 0;
     for (int l = 0; l < g.nlevels; l++) strips += (g.lv[l].h + kEdgeStrip - 1) / kEdgeStrip;
-    SLAMGPU_LAUNCH("blur7_edges", st, blur7_edges_kernel, dim3(strips, n_images), dim3(64), 0, st,
+    SLAMGPU_LAUNCH("blur7_edges", bs, blur7_edges_kernel, dim3(strips, n_images), dim3(64), 0, bs,
                    b, gd.dev);
   }
+  if (bs != st) (void)hipEventRecord(fx.join, bs);
   {
-    // glds tiles need every cell view 16-byte aligned: the caller's level-0 images included
-    const bool glds = ((reinterpret_cast<uintptr_t>(b.in_l) | reinterpret_cast<uintptr_t>(b.in_r) |
-                        (uintptr_t)b.in_stride | (uintptr_t)b.in_pitch |
-                        reinterpret_cast<uintptr_t>(b.pyr) | (uintptr_t)g.pyr_bytes) & 15) == 0;
-    const dim3 grid((g.cells_per_image + kCellWaves * kCellsPerWave - 1) /
-                        (kCellWaves * kCellsPerWave), n_images);
     const dim3 block(64 * kCellWaves);
     const size_t lds = (size_t)kCellWaves * g.fast_lds_per_wave;
+    auto fast = [&](int lo, int hi, hipStream_t fs) {
+      const dim3 grid((hi - lo + kCellWaves * kCellsPerWave - 1) / (kCellWaves * kCellsPerWave),
+                      n_images);
 #define SLAMGPU_FAST(TS, GL)                                                                \
   do {                                                                                      \
     auto* kfn = &fast_cells_kernel<TS, GL>;                                                 \
-    SLAMGPU_LAUNCH("fast_cells", st, kfn, grid, block, lds, st, b, gd.dev, gd.cells,        \
-                   gd.ws.cell_keys, gd.ws.cell_count, gd.ws.err);                           \
+    SLAMGPU_LAUNCH("fast_cells", fs, kfn, grid, block, lds, fs, b, gd.dev, gd.cells,        \
+                   gd.ws.cell_keys, gd.ws.cell_count, gd.ws.err, lo, hi);                   \
   } while (0)
-    if (g.fast_tile_stride == 64) {
-      if (glds) SLAMGPU_FAST(64, true); else SLAMGPU_FAST(64, false);
-    } else {
-      if (glds) SLAMGPU_FAST(128, true); else SLAMGPU_FAST(128, false);
-    }
+      if (g.fast_tile_stride == 64) {
+        if (glds) SLAMGPU_FAST(64, true); else SLAMGPU_FAST(64, false);
+      } else {
+        if (glds) SLAMGPU_FAST(128, true); else SLAMGPU_FAST(128, false);
+      }
 #undef SLAMGPU_FAST
+    };
+    if (split0) {  // level 0 already ran beside the pyramid
+      fast(g.lv[1].cell_base, g.cells_per_image, st);
+      (void)hipStreamWaitEvent(st, fx.join0, 0);
+    } else {
+      fast(0, g.cells_per_image, st);
+    }
   }
   SLAMGPU_LAUNCH("octree", st, octree_img_kernel, dim3(n_images), dim3(64 * g.nlevels),
                  (size_t)g.oct_lds_bytes, st, gd.dev, gd.ws.cell_keys, gd.ws.cell_count,
@@ -2082,6 +2136,7 @@ void launch_extract(const ImageBatch& b, const OrbGeomDev& gd, int n_images, hip
   SLAMGPU_LAUNCH("octree_global", st, octree_kernel, dim3(g.nlevels, n_images), dim3(kOctThreads), 0, st, gd.dev,
                      gd.ws.cell_keys, gd.ws.cell_count, gd.ws.key_scratch, gd.ws.node_scratch,
                      gd.ws.oct_keys, gd.ws.oct_count, gd.ws.err);
+  if (bs != st) (void)hipStreamWaitEvent(st, fx.join, 0);
   SLAMGPU_LAUNCH("orient_desc", st, orient_desc_kernel,
                  dim3((g.kp_cap + 4 * kKpPerWave - 1) / (4 * kKpPerWave), n_images), dim3(256), 0,
                  st, b, gd.dev, gd.ws.oct_keys, gd.ws.oct_count, gd.out.kps, gd.out.desc,

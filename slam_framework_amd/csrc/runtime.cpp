@@ -9,6 +9,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdarg>
+#include <cstdlib>
 #include <cstdio>
 #include <cstring>
 #include <string>
@@ -29,6 +30,7 @@ thread_local KernelTimer* g_timer = nullptr;
 struct slamgpu_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
+  ExtractStreams fx;  // side streams of the extraction (launch_extract)
   OrbParams params{};
   OrbTables tables{};
   OrbGeom geom{};
@@ -221,6 +223,23 @@ int slamgpu_create(int device, const slamgpu_orb_params* p, int cols, int rows, 
   TRY(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) == hipSuccess
           ? 0
           : fail(c, SLAMGPU_EHIP, "hipStreamCreate"));
+  {  // the side stream of launch_extract's blur branch (SLAMGPU_FORK=0 disables it)
+    const char* e = getenv("SLAMGPU_FORK");  // 0: none, 1: blur only, default: blur + FAST-0
+    const int mode = e ? atoi(e) : 2;
+    ExtractStreams& fx = c->fx;
+    if (mode >= 1)
+      TRY(hipStreamCreateWithFlags(&fx.side, hipStreamNonBlocking) == hipSuccess &&
+                  hipEventCreateWithFlags(&fx.fork, hipEventDisableTiming) == hipSuccess &&
+                  hipEventCreateWithFlags(&fx.join, hipEventDisableTiming) == hipSuccess
+              ? 0
+              : fail(c, SLAMGPU_EHIP, "side stream / events"));
+    if (mode >= 2)
+      TRY(hipStreamCreateWithFlags(&fx.side0, hipStreamNonBlocking) == hipSuccess &&
+                  hipEventCreateWithFlags(&fx.fork0, hipEventDisableTiming) == hipSuccess &&
+                  hipEventCreateWithFlags(&fx.join0, hipEventDisableTiming) == hipSuccess
+              ? 0
+              : fail(c, SLAMGPU_EHIP, "side stream / events"));
+  }
   const OrbGeom& g = c->geom;
   const int n = c->max_images;
   TRY(dalloc(c, &c->d_geom, 1));
@@ -277,6 +296,10 @@ void slamgpu_destroy(slamgpu_ctx* c) {
   for (hipEvent_t e : c->timer.pool) (void)hipEventDestroy(e);
   for (void* p : c->allocs) (void)hipFree(p);
   if (c->stream) (void)hipStreamDestroy(c->stream);
+  for (hipStream_t s : {c->fx.side0, c->fx.side})
+    if (s) (void)hipStreamDestroy(s);
+  for (hipEvent_t e : {c->fx.fork0, c->fx.join0, c->fx.fork, c->fx.join})
+    if (e) (void)hipEventDestroy(e);
   delete c;
 }
 
@@ -306,7 +329,7 @@ static int run_frontend(slamgpu_ctx* c, const ImageBatch& b, int n_frames, int n
   c->n_frames_last = n_frames;
   c->n_images_last = n_images;
   OrbGeomDev g = c->gd();
-  launch_extract(b, g, n_images, st);
+  launch_extract(b, g, n_images, st, c->fx);
   if (stereo) {
     launch_stereo(b, g, c->cam, n_frames, c->sws, c->sout, st);
     FrameKps cur{c->out.kps, c->out.desc, c->out.nkps, 2 * (int64_t)c->geom.kp_cap, 2};
