@@ -1284,7 +1284,10 @@ __global__ __launch_bounds__(kOctThreads) void octree_kernel(
 // vPrev, whose nodes were all created in the same pass -- in push order, i.e. ascending list
 // position -- so nodes carry no sequence number. Levels whose keys do not fit set
 // oct_count = -1 and octree_kernel (global memory) redoes them.
-constexpr int kOctLaneKeys = 32;  // <= 255 (8-bit packed quadrant counts)
+#ifndef OCT_LANE_KEYS
+#define OCT_LANE_KEYS 64
+#endif
+constexpr int kOctLaneKeys = OCT_LANE_KEYS;  // <= 255 (8-bit packed quadrant counts)
 constexpr int kOctDivRegs = 16;
 
 struct OctNodeS {
@@ -1439,6 +1442,11 @@ __global__ __launch_bounds__(64 * kMaxLevels) void octree_img_kernel(
 #ifdef OCT_LEVEL_MASK  // timing ablation only: skip the levels not in the mask
   if (!((OCT_LEVEL_MASK >> level) & 1)) return;
 #endif
+#ifdef OCT_PROFILE  // phase timing (timing builds only): wall clock at 100 MHz
+  const uint64_t oct_t0 = wall_clock64();
+  uint64_t oct_t1 = 0, oct_t2 = 0, oct_tp[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  int oct_passes = 0, oct_sz[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#endif
   int* const outc = oct_count + img * nlev + level;
   uint32_t* const outk = oct_keys + (int64_t)img * g->out_per_image + L.out_base;
   const int nIni = L.n_ini;
@@ -1476,32 +1484,24 @@ __global__ __launch_bounds__(64 * kMaxLevels) void octree_img_kernel(
   const float hX = L.hx;
   constexpr int kGatherChunks = 8, kGatherRegs = 48;
   int bcnt = 0;  // lane b < nIni: keys in bucket b
-  if (ncell <= 64 * kGatherChunks && K <= 64 * kGatherRegs) {
+  if (ncell <= 64 * kGatherChunks && K <= 64 * kGatherRegs && ncell + 1 <= NC) {
+    // cell prefix in LDS (the level's sort scratch, free until the passes), then every key
+    // slot finds its cell by a binary search and all key loads are issued at once
+    int* const cpre = reinterpret_cast<int*>(sortk);
     int ccnt[kGatherChunks];
 #pragma unroll
     for (int ch = 0; ch < kGatherChunks; ch++) {
       const int c = 64 * ch + lane;
       ccnt[ch] = c < ncell ? cell_count[cbase + c] : 0;
     }
-    int kb = 0;
+    int carry = 0;
 #pragma unroll
     for (int ch = 0; ch < kGatherChunks; ch++) {
       if (64 * ch < ncell) {
         int ctot;
         const int cex = wave_excl_scan(ccnt[ch], lane, &ctot);
-        for (int r0 = 0; r0 < ctot; r0 += 64) {
-          const int r = r0 + lane;
-          int lo = 0;
-#pragma unroll
-          for (int step = 32; step >= 1; step >>= 1) {
-            const int cand = lo + step;
-            const int pv = __shfl(cex, cand & 63, 64);
-            if (cand < 64 && pv <= r) lo = cand;
-          }
-          const int base = __shfl(cex, lo, 64);
-          if (r < ctot) keys[kb + r] = cell_keys[(cbase + 64 * ch + lo) * g->cell_cap + (r - base)];
-        }
-        kb += ctot;
+        if (64 * ch + lane < ncell) cpre[64 * ch + lane] = carry + cex;
+        carry += ctot;
       }
     }
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
@@ -1512,8 +1512,20 @@ __global__ __launch_bounds__(64 * kMaxLevels) void octree_img_kernel(
 #pragma unroll
     for (int r = 0; r < kGatherRegs; r++) {
       br[r] = -1;
+      const int s = 64 * r + lane;
+      if (r < R && s < K) {
+        int lo = 0, hi = ncell;  // largest c with cpre[c] <= s: the non-empty cell holding s
+        while (hi - lo > 1) {
+          const int mid = (lo + hi) >> 1;
+          if (cpre[mid] <= s) lo = mid;
+          else hi = mid;
+        }
+        kr[r] = cell_keys[(cbase + lo) * g->cell_cap + (s - cpre[lo])];
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < kGatherRegs; r++) {
       if (r < R && 64 * r + lane < K) {
-        kr[r] = keys[64 * r + lane];
         br[r] = (int)((float)key_x(kr[r]) / hX);
         if (br[r] >= nIni) br[r] = -1;
       }
@@ -1601,7 +1613,15 @@ __global__ __launch_bounds__(64 * kMaxLevels) void octree_img_kernel(
   const int N = L.budget;
   int cur = 0, nexp = 0;
   bool outer = true;
+#ifdef OCT_PROFILE
+  oct_t1 = wall_clock64();
+#endif
   while (true) {
+#ifdef OCT_PROFILE
+    if (oct_passes < 8) oct_tp[oct_passes] = wall_clock64();
+    if (oct_passes < 8) oct_sz[oct_passes] = (outer ? 1 : -1) * m;
+    oct_passes++;
+#endif
     const OctNodeS* Lc = lists + cur * NC;
     OctNodeS* Ln = lists + (cur ^ 1) * NC;
     const int V = outer ? m : nexp;
@@ -1789,6 +1809,9 @@ __global__ __launch_bounds__(64 * kMaxLevels) void octree_img_kernel(
     if (newm >= N || newm == mprev) break;
     if (outer && newm + E * 3 > N) outer = false;
   }
+#ifdef OCT_PROFILE
+  oct_t2 = wall_clock64();
+#endif
   // ---- 4. retain the best key of each node (:682-701): strict '>' keeps the first maximum
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
   __builtin_amdgcn_wave_barrier();
@@ -1808,6 +1831,17 @@ __global__ __launch_bounds__(64 * kMaxLevels) void octree_img_kernel(
     if (m > L.out_cap) atomicOr(err, kErrNodeOverflow);
     *outc = mout;
   }
+#ifdef OCT_PROFILE
+  if (lane == 0 && img < 2 && (level == 0 || level == 7)) {
+    const uint64_t t3 = wall_clock64();
+    printf("oct img %d lvl %d K %d gather %d passes %d (%d) retain %d x10ns | %d:%d %d:%d %d:%d %d:%d %d:%d\n",
+           img, level, K, (int)(oct_t1 - oct_t0), (int)(oct_t2 - oct_t1), oct_passes,
+           (int)(t3 - oct_t2), oct_sz[0], (int)(oct_tp[1] - oct_tp[0]), oct_sz[1],
+           (int)(oct_tp[2] - oct_tp[1]), oct_sz[2], (int)(oct_tp[3] - oct_tp[2]), oct_sz[3],
+           (int)((oct_passes > 4 ? oct_tp[4] : oct_t2) - oct_tp[3]), oct_sz[4],
+           (int)(oct_t2 - oct_tp[oct_passes > 4 ? 4 : 3]));
+  }
+#endif
 }
 
 // ---------------------------------------------------------------------------------------
