@@ -188,18 +188,51 @@ __global__ __launch_bounds__(256) void stereo_match_kernel(ImageBatch b,
   const uint8_t* IR = level_img(b, g, ir, levelL, &pr);
   // SAD of the 11 window offsets: the 121 (offset, row) pairs are spread over the wave (two
   // rounds), each lane summing one 11-pixel row; rows are then summed per offset through LDS.
+  // The window bytes (left: columns xcl-5..xcl+5, right: xcr-10..xcr+10, rows yc-5..yc+5) are
+  // first staged into LDS with dword loads (11 dwords per row: 4 left + 7 right); dwords past a
+  // row's last byte are clamped to it (their bytes are never used). Caller images with an odd
+  // base or pitch take byte loads instead (wave-uniform).
   __shared__ int s_part[4][128];
+  __shared__ uint32_t s_win[4][11][11];
   int* part = s_part[wave_id()];
+  uint32_t(*win)[11] = s_win[wave_id()];
+  const int al = (xcl - w) & ~3, ar = (xcr - L - w) & ~3;
+  const bool dw = ((((uintptr_t)IL | (uintptr_t)IR) | (uintptr_t)(pl | pr)) & 3) == 0;
+  const int lastw = (LG.w - 1) >> 2;
+#pragma unroll
+  for (int rnd = 0; rnd < 2; rnd++) {
+    const int p = lane + 64 * rnd;
+    if (p < 121) {
+      const int r = p / 11, d = p - 11 * r;  // window row, dword slot (0-3 left, 4-10 right)
+      const bool left = d < 4;
+      const uint8_t* img = left ? IL : IR;
+      const int pitch = left ? pl : pr;
+      const int x0 = left ? al + 4 * d : ar + 4 * (d - 4);
+      const uint8_t* row = img + (int64_t)(yc - w + r) * pitch;
+      uint32_t v;
+      if (dw) {
+        v = reinterpret_cast<const uint32_t*>(row)[min(x0 >> 2, lastw)];
+      } else {
+        v = 0;
+        for (int j = 0; j < 4; j++)
+          v |= (uint32_t)row[min(x0 + j, LG.w - 1)] << (8 * j);
+      }
+      win[r][d] = v;
+    }
+  }
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  const uint8_t* wb = reinterpret_cast<const uint8_t*>(&win[0][0]);  // row r at 44 r
 #pragma unroll
   for (int rnd = 0; rnd < 2; rnd++) {
     const int p = lane + 64 * rnd;
     if (p < 121) {
       const int k = p / 11, yy = p - 11 * k - w;
       const int incR = k - L;
-      const int cl = IL[(int64_t)yc * pl + xcl];
-      const int cr = IR[(int64_t)yc * pr + xcr + incR];
-      const uint8_t* rl = IL + (int64_t)(yc + yy) * pl + xcl - w;
-      const uint8_t* rr = IR + (int64_t)(yc + yy) * pr + xcr + incR - w;
+      const int cl = wb[44 * w + (xcl - al)];
+      const int cr = wb[44 * w + 16 + (xcr + incR - ar)];
+      const uint8_t* rl = wb + 44 * (yy + w) + (xcl - w - al);
+      const uint8_t* rr = wb + 44 * (yy + w) + 16 + (xcr + incR - w - ar);
       int acc = 0;
 #pragma unroll
       for (int xx = 0; xx < 2 * w + 1; xx++) acc += abs((rl[xx] - cl) - (rr[xx] - cr));
