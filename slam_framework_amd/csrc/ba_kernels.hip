@@ -1078,7 +1078,12 @@ __global__ __launch_bounds__(kThreads) void local_ba_linearize_kernel(
   __shared__ float isig[SLAMGPU_MAX_LEVELS];
   const int tid = threadIdx.x;
   Problem pb;
-  if (!ba_setup(sh, pb, isig, P, problems, kf_Tcw, kf_mode, points, pstart, obs, status, ws))
+  // the edge pass writes chi2 and the Hpl blocks straight into the outputs (same global edge
+  // indexing as the workspace; nothing else in this kernel reads them back)
+  BaWorkspace wso = ws;
+  wso.chi2 = out.chi2;
+  wso.hpl = out.hpl;
+  if (!ba_setup(sh, pb, isig, P, problems, kf_Tcw, kf_mode, points, pstart, obs, status, wso))
     return;
   build_structure(sh, pb, true);
   double chi = 0.0, maxd = 0.0, zero = 0.0;
@@ -1087,11 +1092,10 @@ __global__ __launch_bounds__(kThreads) void local_ba_linearize_kernel(
   __syncthreads();
   sum_points(pb, maxd);
   block_sum2(sh, chi, zero);
-  for (int e = tid; e < pb.n_obs; e += kThreads) {
+  for (int e = tid; e < pb.n_obs; e += kThreads) {  // edges to fixed cameras have no Hpl block
     const int ge = pb.o0 + e;
-    out.chi2[ge] = ws.chi2[ge];
-    const bool fr = sh.free_of_kf[obs[ge].keyframe] >= 0;
-    for (int i = 0; i < 18; i++) out.hpl[(size_t)ge * 18 + i] = fr ? ws.hpl[(size_t)ge * 18 + i] : 0.0;
+    if (sh.free_of_kf[obs[ge].keyframe] < 0)
+      for (int i = 0; i < 18; i++) out.hpl[(size_t)ge * 18 + i] = 0.0;
   }
   for (int p = tid; p < pb.n_pts; p += kThreads) {
     const PtRef r = ptrec(pb, p);
