@@ -412,7 +412,7 @@ def bench_local_ba(dev, with_cpu):
     nk, npn, no = len(P["kf_mode"]), len(P["points"]), len(P["obs"])
     stream = torch.cuda.current_stream()
     res = {}
-    BB = 256  # one problem per CU: a workgroup runs a whole problem
+    BB = int(os.environ.get("SLAMGPU_BA_BATCH", "256"))  # problems per batch (a workgroup each)
     for B in (1, BB):
         desc = np.array([(i * nk, nk, i * npn, npn) for i in range(B)], np.int32)
         start = np.concatenate([P["point_obs_start"][:-1] + i * no for i in range(B)] +
