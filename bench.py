@@ -8,9 +8,15 @@ frame's stereo points as visual-odometry map points, and OrbMatcher::SearchByPro
 CurrentFrame, LastFrame, th=7) -- the tracker's per-frame motion-model search. Frame 0 of a batch
 is the halo frame of frame 1's search, so a step completes B-1 frames.
 
-Multi-GPU (python -m torch.distributed.run --nproc-per-node N bench.py --gpus N): every rank
-processes its own batch of frames (frames are independent units: weak scaling, no data-path
-collective); the barrier and the max-over-ranks timing use the RCCL process group.
+Multi-GPU (configs[2]; `python -m torch.distributed.run --nproc-per-node N bench.py --gpus N`,
+or `python bench.py --gpus N`, which starts the N ranks itself before touching the GPU): ONE
+contiguous synthetic sequence is sharded over the ranks -- rank r owns frames
+[r*F + 1, (r+1)*F + 1) (F = frames completed per rank per step) and recomputes frame r*F, the halo
+its first frame-to-frame search reads. Inside every timed step each rank packs its owned frames'
+results (keypoints + descriptors of both views, stereo u_right/depth, frame-to-frame map-point ids
+and match counts; slamgpu_pack_frame_records_device) and RCCL-gathers them to rank 0 on the
+collective's own stream, double-buffered so the gather of step k overlaps the compute of k+1
+(slam_framework_amd.dist.FrameGather). Weak scaling: F is fixed per rank.
 
 Prints ONE JSON line on rank 0 (driver contract), with `roofline` for the dominant kernel
 (HIP-event timed inside the timed region) and `cpu_baseline` (the oracle/ restatement on host
@@ -100,7 +106,7 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--batch", type=int, default=256, help="stereo frames per GPU per step")
-    ap.add_argument("--distinct", type=int, default=16, help="distinct synthetic frames per rank")
+    ap.add_argument("--distinct", type=int, default=16, help="distinct synthetic renders of the sequence")
     ap.add_argument("--cpu-frames", type=int, default=0, help="oracle sample size (0 = auto)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--streams", type=int, default=1,
@@ -111,12 +117,16 @@ def main():
                     help="skip the ComputeBoW / SearchByBoW measurement")
     args = ap.parse_args()
 
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(spawn_ranks(args.gpus))
     import torch
     import torch.distributed as dist
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        sys.exit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}")
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     # One explicit stream for torch ops and library launches alike: a null stream handle would
@@ -124,26 +134,40 @@ def main():
     torch.cuda.set_stream(torch.cuda.Stream(device=dev))
     if world > 1:
         dist.init_process_group("nccl", device_id=dev)
+        world = dist.get_world_size()
+        # the CPU baseline and the optimizer / BoW legs are N=1 measurements
+        args.no_cpu_baseline = args.no_optimizer = args.no_bow = True
 
     from slam_framework_amd import slamgpu as G
     from slam_framework_amd import synthetic as S
 
     cols, rows, B, D = S.KITTI_COLS, S.KITTI_ROWS, args.batch, args.distinct
     cam = S.KITTI_CAM
-    # ---- synthetic input, uploaded once (resident in HBM before the timed region)
-    Ls, Rs = S.sequence(1000 + rank, D)
+    NS = max(1, args.streams)
+    Bs = B // NS
+    assert Bs >= 2 and Bs * NS == B, "--batch must split into --streams parts of >= 2 frames"
+    F = NS * (Bs - 1)   # frames this rank completes (owns) per step
+    # ---- ONE synthetic sequence for the whole job (D distinct renders, frame g = render g % D),
+    # sharded contiguously with a one-frame halo; uploaded once (resident in HBM before timing)
+    Ls, Rs = S.sequence(1000, D)
+    from slam_framework_amd import dist as SD
+    first, lo, hi = SD.shard_with_halo(world * F, rank, world, first=1)
+    assert hi - lo == F and first == lo - 1
+    # context si computes global frames lo - 1 + si*(Bs-1) + [0, Bs): its slot 0 is the halo of
+    # its slot 1 (the previous context's last frame, or the previous rank's for si = 0)
+    gframe = np.array([first + si * (Bs - 1) + i for si in range(NS) for i in range(Bs)])
     pitch = 1280
     host_l = np.zeros((B, rows, pitch), np.uint8)
     host_r = np.zeros((B, rows, pitch), np.uint8)
     for f in range(B):
-        host_l[f, :, :cols] = Ls[f % D]
-        host_r[f, :, :cols] = Rs[f % D]
+        host_l[f, :, :cols] = Ls[gframe[f] % D]
+        host_r[f, :, :cols] = Rs[gframe[f] % D]
     d_l = torch.from_numpy(host_l).to(dev)
     d_r = torch.from_numpy(host_r).to(dev)
     stride = rows * pitch
     poses = np.zeros(B, G.F2F_POSE_DTYPE)
     for f in range(B):
-        poses["Rcw"][f] = S.rotation(f % D).astype(np.float32).reshape(-1)
+        poses["Rcw"][f] = S.rotation(gframe[f] % D).astype(np.float32).reshape(-1)
     poses["baseline"] = np.float32(cam[4]) / np.float32(cam[0])
     poses["th"] = 7.0
     poses["check_ori"] = 1
@@ -151,9 +175,6 @@ def main():
 
     # NS contexts, each with its own HIP stream and Bs consecutive frames of the batch (its first
     # frame is the halo of its second): the launches of one half fill the other's tails.
-    NS = max(1, args.streams)
-    Bs = B // NS
-    assert Bs >= 2 and Bs * NS == B, "--batch must split into --streams parts of >= 2 frames"
     ctxs = [G.Context(cols, rows, 2000, 1.2, 8, 20, 7, max_frames=Bs, device=local)
             for _ in range(NS)]
     ctx = ctxs[0]
@@ -172,7 +193,15 @@ def main():
             "poses": d_poses[si * Bs * G.F2F_POSE_DTYPE.itemsize:
                              (si + 1) * Bs * G.F2F_POSE_DTYPE.itemsize]})
 
+    # per-frame results of the owned frames -> rank 0 (world > 1 only)
+    rec_b = ctx.record_bytes
+    # (SLAMGPU_BENCH_GATHER=1 runs the pack + gather path at world 1 too, as a local copy)
+    gat = SD.FrameGather({"frontend": rec_b, "map_point": kc * 4, "nmatches": 4}, F, dev) \
+        if world > 1 or os.environ.get("SLAMGPU_BENCH_GATHER") == "1" else None
+
     def step():
+        if gat is not None:
+            gat.begin()
         for si in range(NS):
             st_ = streams[si]
             if si:
@@ -188,8 +217,17 @@ def main():
                 c.search_by_projection_frame_device(pt["q"], Bs * kc, pt["qs"], pt["qc"], kc,
                                                     pt["poses"], pt["mp"], pt["blk"], kc,
                                                     pt["nm"], Bs, h)
+                if gat is not None:   # owned frames = slots 1..Bs-1 of this context
+                    o = si * (Bs - 1)
+                    c.pack_frame_records_device(1, Bs - 1, gat.slab("frontend")[o:o + Bs - 1], h)
+                    gat.slab("map_point")[o:o + Bs - 1].view(-1).copy_(
+                        pt["mp"][kc:].view(torch.uint8))
+                    gat.slab("nmatches")[o:o + Bs - 1].view(-1).copy_(
+                        pt["nm"][1:].view(torch.uint8))
         for si in range(1, NS):
             main.wait_stream(streams[si])
+        if gat is not None:
+            gat.start()
 
     for _ in range(max(1, args.warmup)):
         step()
@@ -225,6 +263,8 @@ def main():
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
+    if gat is not None:
+        gat.wait_all()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -232,7 +272,6 @@ def main():
     ctx.timing_stop()
     for c in ctxs:
         c.sync()
-    from slam_framework_amd import dist as SD
     elapsed = SD.max_over_ranks(t1 - t0, dev)
     dom_ms, dom_n = ctx.timing_read(dominant)
     # per-rank result summary gathered to every rank (validation, outside the timed region)
@@ -242,6 +281,11 @@ def main():
     value = frames / elapsed
     ms_per_step = 1000.0 * elapsed / args.steps
 
+    gather_info = None
+    if gat is not None:
+        torch.cuda.synchronize()
+        gather_info = check_gather(gat, ctxs, parts, gframe, Bs, kc, D, world, F) \
+            if rank == 0 else None
     if rank == 0:
         level_px = [ctx.pyramid_level(0, l).size for l in range(8)]
         kp_img = float(nk.mean())
@@ -287,13 +331,17 @@ def main():
             "value": round(value, 2), "unit": "stereo frames/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 3),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u8",
-            "data": "synthetic (seeded rectangles scene, pure-rotation sequence)",
+            "data": "synthetic (seeded rectangles scene, one pure-rotation sequence sharded "
+                    "over the ranks)",
             "config": {"workload": "configs[1]: synthetic 1241x376 stereo stream, 2000 kp/frame, "
                                    "extract L+R + stereo match + frame-to-frame match",
                        "frames_per_gpu_per_step": NS * (Bs - 1), "batch": B, "streams": NS,
                        "nfeatures": 2000,
                        "nlevels": 8, "scale_factor": 1.2, "fast_th": [20, 7],
-                       "parallelism": f"frame-sharded x{world}"},
+                       "parallelism": f"frame-sharded x{world}" + (
+                           ", contiguous shards + 1 halo frame, RCCL gather to rank 0"
+                           if world > 1 else "")},
+            "gather": gather_info,
             "roofline": roofline,
             "cpu_baseline": cpu,
             "kernel_ms_per_step": {n: round(brk[n][0], 4) for n in names},
@@ -305,6 +353,64 @@ def main():
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
+
+
+def spawn_ranks(n):
+    """`bench.py --gpus N` without a launcher: start N rank processes of this script (RANK /
+    LOCAL_RANK / WORLD_SIZE, rendezvous on 127.0.0.1) before this process makes any GPU call,
+    wait for all of them and return the worst exit code. Only rank 0 prints the JSON line."""
+    import socket
+    import subprocess
+    sk = socket.socket()
+    sk.bind(("127.0.0.1", 0))
+    port = sk.getsockname()[1]
+    sk.close()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
+                   LOCAL_WORLD_SIZE=str(n), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:],
+                                      env=env))
+    return max(abs(p.wait()) for p in procs)
+
+
+def check_gather(gat, ctxs, parts, gframe, Bs, kc, D, world, F):
+    """Rank 0, after timing: every frame gathered from the other ranks must equal, byte for byte
+    (trimmed to its keypoint count), rank 0's own result for the same sequence frame modulo the
+    D distinct renders -- the frontend output depends only on the frame, the frame-to-frame
+    search only on (t-1, t)."""
+    import torch
+    from slam_framework_amd import slamgpu as G
+    slot = (gat.k - 1) % len(gat.send)
+    recs = gat.field(slot, "frontend").cpu().numpy()
+    mps = gat.field(slot, "map_point").cpu().numpy().view(np.int32)
+    nms = gat.field(slot, "nmatches").cpu().numpy().view(np.int32).reshape(-1)
+    # rank 0's own owned frames, by residue
+    own = {}
+    for si, c in enumerate(ctxs):
+        rec = torch.empty((Bs - 1, c.record_bytes), dtype=torch.uint8, device=gat.device)
+        c.pack_frame_records_device(1, Bs - 1, rec, torch.cuda.current_stream().cuda_stream)
+        torch.cuda.synchronize()
+        rec = rec.cpu().numpy()
+        mp = parts[si]["mp"].cpu().numpy().reshape(Bs, kc)
+        nm = parts[si]["nm"].cpu().numpy()
+        for i in range(1, Bs):
+            own.setdefault(int(gframe[si * Bs + i]) % D, (rec[i - 1], mp[i], nm[i]))
+    checked = 0
+    j0 = F if world > 1 else 0   # the frames of ranks 1..world-1 (at world 1: rank 0's own)
+    for j in range(j0, world * F, max(1, (world * F - j0) // 64)):
+        g = j + 1
+        r_own, mp_own, nm_own = own[g % D]
+        a, b = G.unpack_frame_record(recs[j], kc), G.unpack_frame_record(r_own, kc)
+        n = len(a["kps_left"])
+        ok = all(a[k].tobytes() == b[k].tobytes() for k in a) and nms[j] == nm_own and \
+            np.array_equal(mps[j][:n], mp_own[:n])
+        if not ok:
+            raise SystemExit(f"bench.py: gathered frame {g} differs from rank 0's own result")
+        checked += 1
+    return {"bytes_per_rank_per_step": gat.nbytes, "frames_per_rank_per_step": F,
+            "record_bytes_per_frame": int(gat.fields["frontend"]) + 4 * kc + 4,
+            "frames_checked_vs_rank0": checked, "identical": True}
 
 
 FP64_VALU_PEAK_TFLOPS = 78.6  # MI355X FP64 vector peak (MI355X_MICROARCH.md)

@@ -127,6 +127,23 @@ typedef struct {
 } slamgpu_device_view;
 int slamgpu_device_results(const slamgpu_ctx* ctx, slamgpu_device_view* out);
 
+/* Per-frame result record of the last frontend call, for gathering a frame-sharded job's
+ * results to one rank (the stereo Frame ctor's outputs, frame.cpp:61-111 --
+ * left/right keypoints and descriptors, Frame::ComputeStereoMatches' u_right/depth). Record
+ * layout (kc = kp_cap; entries past nkps[v] are stale and must be ignored):
+ *   [0, 56 kc)            slamgpu_keypoint kps[2][kc]   (left, right)
+ *   [56 kc, 120 kc)       uint8_t desc[2][kc][32]
+ *   [120 kc, 124 kc)      float u_right[kc]
+ *   [124 kc, 128 kc)      float depth[kc]
+ *   [128 kc, 128 kc + 8)  int32_t nkps[2]
+ * padded to a multiple of 256 bytes (slamgpu_frame_record_bytes). */
+size_t slamgpu_frame_record_bytes(const slamgpu_ctx* ctx);
+/* Device-to-device copy of frames [first, first + n) of the last frontend call into n
+ * consecutive records at d_dst, ordered on `stream` (NULL = the context's stream) after the
+ * frontend's launches. Never allocates; graph-capturable. */
+int slamgpu_pack_frame_records_device(slamgpu_ctx* ctx, int first, int n, void* d_dst,
+                                      void* stream);
+
 /* ---- OrbMatcher ---------------------------------------------------------------------------- */
 /* Replaces: OrbMatcher::DescriptorDistance (orb_matcher.cpp:1630-1646). Host, pure. */
 int slamgpu_descriptor_distance(const uint8_t* a, const uint8_t* b);

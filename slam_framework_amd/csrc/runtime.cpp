@@ -488,6 +488,34 @@ int slamgpu_device_results(const slamgpu_ctx* c, slamgpu_device_view* v) {
   return 0;
 }
 
+size_t slamgpu_frame_record_bytes(const slamgpu_ctx* c) {
+  if (!c) return 0;
+  return ((size_t)128 * c->geom.kp_cap + 8 + 255) / 256 * 256;
+}
+
+int slamgpu_pack_frame_records_device(slamgpu_ctx* c, int first, int n, void* d_dst,
+                                      void* stream) {
+  if (!c || !d_dst || n < 0 || first < 0 || first + n > c->n_frames_last)
+    return fail(c, SLAMGPU_EINVAL, "pack_frame_records_device: frames [%d, %d) of %d", first,
+                first + n, c->n_frames_last);
+  if (n == 0) return 0;
+  const size_t kc = c->geom.kp_cap, rec = slamgpu_frame_record_bytes(c);
+  uint8_t* d = static_cast<uint8_t*>(d_dst);
+  hipStream_t s = pick_stream(c, stream);
+  // one strided copy per field: source rows are frames (pitch = the field's bytes per frame),
+  // destination rows are records
+  struct { size_t dst_off; const void* src; size_t width; } f[5] = {
+      {0, c->out.kps + 2 * kc * first, 56 * kc},
+      {56 * kc, c->out.desc + 64 * kc * first, 64 * kc},
+      {120 * kc, c->sout.u_right + kc * first, 4 * kc},
+      {124 * kc, c->sout.depth + kc * first, 4 * kc},
+      {128 * kc, c->out.nkps + 2 * first, 8}};
+  for (auto& x : f)
+    HIPCHECK(c, hipMemcpy2DAsync(d + x.dst_off, rec, x.src, x.width, x.width, (size_t)n,
+                                 hipMemcpyDeviceToDevice, s));
+  return 0;
+}
+
 int slamgpu_make_vo_queries_device(slamgpu_ctx* c, const slamgpu_f2f_pose* d_poses, int blocks,
                                    slamgpu_f2f_query* d_queries, int* d_q_start, int* d_q_count,
                                    int n_frames, void* stream) {

@@ -47,6 +47,7 @@ EXPORTS = [
     "slamgpu_scale_tables", "slamgpu_extract", "slamgpu_get_pyramid_level",
     "slamgpu_frame_stereo", "slamgpu_frontend_device", "slamgpu_sync",
     "slamgpu_download_keypoints", "slamgpu_download_stereo", "slamgpu_device_results",
+    "slamgpu_frame_record_bytes", "slamgpu_pack_frame_records_device",
     "slamgpu_descriptor_distance", "slamgpu_search_by_projection_frame",
     "slamgpu_search_by_projection_mps", "slamgpu_search_by_projection_frame_device",
     "slamgpu_search_by_projection_mps_device", "slamgpu_debug_level_keys",
@@ -65,6 +66,19 @@ EXPORTS = [
     "slamgpu_kfmatch_last_error", "slamgpu_search_for_triangulation",
     "slamgpu_search_for_triangulation_device", "slamgpu_fuse", "slamgpu_fuse_device",
 ]
+
+
+def unpack_frame_record(rec, kp_cap):
+    """Host view of one slamgpu_pack_frame_records_device record (uint8 array) -> dict of the
+    left/right keypoints and descriptors, u_right and depth, trimmed to the keypoint counts."""
+    rec = np.asarray(rec, np.uint8).reshape(-1)
+    kc = kp_cap
+    nl, nr = rec[128 * kc:128 * kc + 8].view(np.int32)
+    kps = rec[:56 * kc].view(KP_DTYPE).reshape(2, kc)
+    desc = rec[56 * kc:120 * kc].reshape(2, kc, 32)
+    return {"kps_left": kps[0, :nl], "kps_right": kps[1, :nr], "desc_left": desc[0, :nl],
+            "desc_right": desc[1, :nr], "u_right": rec[120 * kc:124 * kc].view(np.float32)[:nl],
+            "depth": rec[124 * kc:128 * kc].view(np.float32)[:nl]}
 
 
 class OrbParams(C.Structure):
@@ -124,6 +138,9 @@ def lib():
         L.slamgpu_download_keypoints.argtypes = [vp, ip, vp, vp, ip, C.POINTER(ip)]
         L.slamgpu_download_stereo.argtypes = [vp, ip, vp, vp, ip, C.POINTER(ip)]
         L.slamgpu_device_results.argtypes = [vp, C.POINTER(DeviceView)]
+        L.slamgpu_frame_record_bytes.argtypes = [vp]
+        L.slamgpu_frame_record_bytes.restype = sz
+        L.slamgpu_pack_frame_records_device.argtypes = [vp, ip, ip, vp, vp]
         L.slamgpu_descriptor_distance.argtypes = [vp, vp]
         L.slamgpu_search_by_projection_frame.argtypes = [vp, ip, vp, ip, vp, vp, vp, ip,
                                                          C.POINTER(ip)]
@@ -274,6 +291,16 @@ class Context:
         v = DeviceView()
         self.check(lib().slamgpu_device_results(self.h, C.byref(v)))
         return v
+
+    @property
+    def record_bytes(self):
+        """Bytes of one per-frame result record (include/slamgpu.h)."""
+        return lib().slamgpu_frame_record_bytes(self.h)
+
+    def pack_frame_records_device(self, first, n, d_dst, stream=None):
+        """Frames [first, first + n) of the last frontend call -> n records at d_dst."""
+        self.check(lib().slamgpu_pack_frame_records_device(self.h, first, n, _ptr(d_dst),
+                                                           C.c_void_p(stream or 0)))
 
     # ---- batched device path (torch CUDA tensors or raw device pointers) ----
     def make_vo_queries_device(self, d_poses, blocks, d_queries, d_q_start, d_q_count, n_frames,
