@@ -60,7 +60,8 @@ typedef struct {
 
 /* ---- lifecycle ---------------------------------------------------------------------------- */
 /* Replaces: ORBextractor::ORBextractor (orb_extractor.cpp:351-411) for images of cols x rows,
- * batched up to max_frames stereo pairs (2 * max_frames images). */
+ * batched up to max_frames stereo pairs (2 * max_frames images). Returns 0 and *out, or a
+ * negative code with *out = NULL (nothing to destroy; the reason: slamgpu_last_error(NULL)). */
 int slamgpu_create(int device, const slamgpu_orb_params* params, int cols, int rows,
                    int max_frames, slamgpu_ctx** out);
 void slamgpu_destroy(slamgpu_ctx* ctx);

@@ -78,7 +78,8 @@ typedef struct {
 } slamgpu_tri_pair;
 
 /* Pair p writes d_match12 + p * match_stride and d_nmatches[p] (-1 if a keyframe exceeds
- * SLAMGPU_KF_MAX_FEATURES). */
+ * SLAMGPU_KF_MAX_FEATURES, or its FeatureVector names a feature >= n, or a candidate keypoint's
+ * octave is outside [0, nlevels): such a pair's match row is left partly written). */
 int slamgpu_search_for_triangulation_device(const slamgpu_kf* d_kfs,
                                             const slamgpu_tri_pair* d_pairs, int n_pairs,
                                             const slamgpu_camera* cam, const slamgpu_levels* lv,

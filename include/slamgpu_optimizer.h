@@ -19,6 +19,7 @@
 #ifndef SLAMGPU_OPTIMIZER_H_
 #define SLAMGPU_OPTIMIZER_H_
 
+#include <stdbool.h>
 #include <stddef.h>
 #include <stdint.h>
 
@@ -86,13 +87,21 @@ typedef struct {
  * (optimizer.cpp:413-716) after its graph gathering: kf_Tcw[16 n_kf] (row-major f32, updated for
  * modes 0 and 1), points[3 n_points] (MapPoint::GetWorldPos, all updated), the observations, and
  * erase[n_obs]: 1 where the reference puts (keyframe, point) in vToErase (the caller then runs
- * EraseMapPointMatch / EraseObservation and MapPoint::UpdateNormalAndDepth). stop_flag (may be
- * NULL) is read once before the optimisation starts, as the reference checks it
- * (optimizer.cpp:616-618). *lm_iterations (may be NULL): LM iterations run. Synchronous. */
+ * EraseMapPointMatch / EraseObservation and MapPoint::UpdateNormalAndDepth).
+ * stop_flag (may be NULL) is the reference's bool* (LocalMapper::abort_BA_): it is live for the
+ * whole call, as g2o's force-stop flag is (optimizer.cpp:474-476). It is read before optimising
+ * (:616-618: raised -> return with nothing written and no erasures), and while the kernel runs
+ * this thread mirrors it into host-mapped memory that the device polls at every point g2o calls
+ * terminate(): each LM iteration (sparse_optimizer.cpp:376), each failed Levenberg trial
+ * (optimization_algorithm_levenberg.cpp:149) and before the second optimize() (:625-627). So a
+ * flag raised by another thread mid-run (LocalMapper::InsertKeyFrame, local_mapper.cpp:89-93;
+ * RequestStop :95-100; InterruptBA :165-166) ends the optimisation within one LM iteration, and
+ * the erase list and write-back use the state at that point, as in the reference.
+ * *lm_iterations (may be NULL): LM iterations run. Synchronous. */
 int slamgpu_local_bundle_adjustment(const slamgpu_camera* cam, const float* inv_sigma2,
                                     int nlevels, float* kf_Tcw, const uint8_t* kf_mode, int n_kf,
                                     float* points, int n_points, const int32_t* point_obs_start,
-                                    const slamgpu_ba_obs* obs, const int* stop_flag,
+                                    const slamgpu_ba_obs* obs, const volatile bool* stop_flag,
                                     uint8_t* erase, int* lm_iterations);
 
 /* A problem of a batch: its keyframes d_kf_*[kf_begin, kf_begin + n_kf) and points
@@ -111,8 +120,9 @@ size_t slamgpu_local_ba_workspace_bytes(int total_kf, int total_points, int tota
  * or -1 more than SLAMGPU_BA_MAX_LOCAL_KF local keyframes, -2 a point observed twice by one
  * keyframe, -3 a keyframe index outside the problem or more than SLAMGPU_BA_MAX_KF keyframes
  * (the problem's outputs are then untouched). d_stop_flag (may be NULL; may be host-mapped
- * memory): polled before every LM iteration -- a non-zero value ends the optimisation as
- * g2o's force-stop flag does (SparseOptimizer::terminate). */
+ * memory): polled (one read per work-group, system scope) wherever g2o calls terminate() -- see
+ * slamgpu_local_bundle_adjustment; a non-zero value ends the optimisation as g2o's force-stop
+ * flag does. */
 int slamgpu_local_bundle_adjustment_device(
     const slamgpu_camera* cam, const float* inv_sigma2, int nlevels,
     const slamgpu_ba_problem* d_problems, int n_problems, float* d_kf_Tcw,

@@ -52,7 +52,19 @@ typedef struct {
   double* Hpl;  // [n_obs][18] (6 x 3, pose rows x point columns)
   int* kf_nact;   // active edges per KF
   int* pt_nact;   // active edges per point
+  // g2o's force-stop flag (optimizer.cpp:474-476): reads false for the first stop_after polls
+  // and true from then on (stop_after < 0: never raised)
+  int stop_after, polls;
 } ba;
+
+// SparseOptimizer::terminate() (sparse_optimizer.h:188), polled where g2o and the reference poll
+// *stop_flag: the optimize() loop condition (sparse_optimizer.cpp:376), the Levenberg trial loop
+// (optimization_algorithm_levenberg.cpp:149), before optimising and before the second
+// optimize() (optimizer.cpp:616-627).
+static int terminate_(ba* B) {
+  if (B->stop_after < 0) return 0;
+  return B->polls++ >= B->stop_after;
+}
 
 static int is_stereo(const oc_ba_obs* o) { return o->ur >= 0; }
 
@@ -341,7 +353,7 @@ static void optimize(ba* B, int iterations, int* lm_iters) {
   count_active(B);
   double lambda = 0;
   int ni = 2, nbad = 0;
-  for (int it = 0; it < iterations; it++) {
+  for (int it = 0; it < iterations && !terminate_(B); it++) {
     compute_active_errors(B);
     double currentChi = active_robust_chi2(B);
     const double iniChi = currentChi;
@@ -399,7 +411,7 @@ static void optimize(ba* B, int iterations, int* lm_iters) {
         memcpy(B->X, Xb, sizeof(double) * 3 * B->n_pts);
       }
       qmax++;
-    } while (rho < 0 && qmax < 10);
+    } while (rho < 0 && qmax < 10 && !terminate_(B));
     if (lm_iters) (*lm_iters)++;
     if (qmax == 10 || rho == 0) break;
     if ((iniChi - currentChi) * 1e3 < iniChi) nbad++;
@@ -425,6 +437,7 @@ static void ba_init(ba* B, const float cam[5], const float* inv_sigma2, const fl
                     const int32_t* point_obs_start, const oc_ba_obs* obs) {
   const int n_obs = point_obs_start[n_points];
   memset(B, 0, sizeof(*B));
+  B->stop_after = -1;
   B->n_kf = n_kf;
   B->n_pts = n_points;
   B->n_obs = n_obs;
@@ -483,21 +496,38 @@ int oc_local_bundle_adjustment(const float cam[5], const float* inv_sigma2, floa
                                const uint8_t* kf_mode, int n_kf, float* points, int n_points,
                                const int32_t* point_obs_start, const oc_ba_obs* obs,
                                uint8_t* erase, int* lm_iterations) {
+  return oc_local_bundle_adjustment_stop(cam, inv_sigma2, kf_Tcw, kf_mode, n_kf, points, n_points,
+                                         point_obs_start, obs, -1, erase, lm_iterations);
+}
+
+int oc_local_bundle_adjustment_stop(const float cam[5], const float* inv_sigma2, float* kf_Tcw,
+                                    const uint8_t* kf_mode, int n_kf, float* points, int n_points,
+                                    const int32_t* point_obs_start, const oc_ba_obs* obs,
+                                    int stop_after, uint8_t* erase, int* lm_iterations) {
   if (lm_iterations) *lm_iterations = 0;
   if (n_kf < 0 || n_points < 0 || point_obs_start[0] != 0) return -1;
   const int n_obs = point_obs_start[n_points];
   ba B;
   ba_init(&B, cam, inv_sigma2, kf_Tcw, kf_mode, n_kf, points, n_points, point_obs_start, obs);
+  B.stop_after = stop_after;
+  B.polls = 0;
+  if (terminate_(&B)) {  // optimizer.cpp:616-618: return before optimising, nothing written
+    for (int e = 0; e < n_obs; e++) erase[e] = 0;
+    ba_free(&B);
+    return 0;
+  }
 
   B.robust = 1;
   optimize(&B, 5, lm_iterations);  // optimizer.cpp:622-623
-  // optimizer.cpp:632-665: outliers to level 1, robust kernels off
-  for (int e = 0; e < n_obs; e++) {
-    const double thr = is_stereo(&obs[e]) ? 7.815 : 5.991;
-    if (B.chi2[e] > thr || !depth_positive(&B, e)) B.active[e] = 0;
+  if (!terminate_(&B)) {           // :625-627 do_more
+    // optimizer.cpp:632-665: outliers to level 1, robust kernels off
+    for (int e = 0; e < n_obs; e++) {
+      const double thr = is_stereo(&obs[e]) ? 7.815 : 5.991;
+      if (B.chi2[e] > thr || !depth_positive(&B, e)) B.active[e] = 0;
+    }
+    B.robust = 0;
+    optimize(&B, 10, lm_iterations);  // :668-669
   }
-  B.robust = 0;
-  optimize(&B, 10, lm_iterations);  // :668-669
   // :672-700: erase list over every edge (level-1 edges keep their last computed chi2)
   for (int e = 0; e < n_obs; e++) {
     const double thr = is_stereo(&obs[e]) ? 7.815 : 5.991;

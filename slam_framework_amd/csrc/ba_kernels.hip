@@ -236,7 +236,22 @@ struct BaShared {
   int kf_of_free[kMaxK];
   int K, err, ok;
   int rb;
+  int stop;  // the last stop-flag poll (one read per poll, by thread 0)
 };
+
+// g2o's SparseOptimizer::terminate() (*forceStopFlag, sparse_optimizer.h:188) for the whole
+// work-group: thread 0 reads the flag once (system scope: the flag may be host-mapped memory a
+// host thread raises while the kernel runs) and every thread takes that one value, so a flag
+// raised mid-poll cannot split the work-group's control flow. Contains a barrier.
+__device__ __forceinline__ bool poll_stop(BaShared& sh, const int32_t* stop_flag) {
+  if (!stop_flag) return false;
+  if (threadIdx.x == 0)
+    sh.stop = __hip_atomic_load(stop_flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0;
+  __syncthreads();
+  const bool r = sh.stop != 0;
+  __syncthreads();  // sh.stop is not rewritten before every thread has read it
+  return r;
+}
 
 // Deterministic block sum of two values: wave butterflies (bitwise identical in every lane), wave
 // partials summed in wave order by every thread.
@@ -827,7 +842,7 @@ __global__ __launch_bounds__(kThreads) void local_ba_kernel(
   __shared__ BaShared sh;
   __shared__ float isig[SLAMGPU_MAX_LEVELS];
   const int tid = threadIdx.x;
-  if (stop_flag && __atomic_load_n(stop_flag, __ATOMIC_RELAXED)) {  // optimizer.cpp:616-618
+  if (poll_stop(sh, stop_flag)) {  // optimizer.cpp:616-618: return before optimising
     const int32_t o0 = pstart[problems[blockIdx.x].point_begin];
     const int32_t o1 = pstart[problems[blockIdx.x].point_begin + problems[blockIdx.x].n_points];
     for (int e = o0 + tid; e < o1; e += kThreads) erase[e] = 0;
@@ -854,7 +869,7 @@ __global__ __launch_bounds__(kThreads) void local_ba_kernel(
     double lambda = 0.0;
     int ni = 2, nbad = 0;
     for (int it = 0; it < iterations; it++) {
-      if (stop_flag && __atomic_load_n(stop_flag, __ATOMIC_RELAXED)) {
+      if (poll_stop(sh, stop_flag)) {  // optimize(): i < iterations && !terminate() && ok
         stopped = true;
         break;
       }
@@ -1008,7 +1023,9 @@ __global__ __launch_bounds__(kThreads) void local_ba_kernel(
           __syncthreads();
         }
         qmax++;
-      } while (rho < 0 && qmax < 10);
+        // levenberg.cpp:149: while (rho < 0 && qmax < maxTrials && !terminate()); rho and qmax
+        // are work-group uniform
+      } while (rho < 0 && qmax < 10 && !poll_stop(sh, stop_flag));
       lm_total++;
       if (qmax == 10 || rho == 0) break;
       if ((iniChi - currentChi) * 1e3 < iniChi) nbad++;
@@ -1016,7 +1033,7 @@ __global__ __launch_bounds__(kThreads) void local_ba_kernel(
       if (nbad >= 3) break;
     }
     if (phase == 0) {
-      if (stop_flag && __atomic_load_n(stop_flag, __ATOMIC_RELAXED)) stopped = true;  // do_more
+      if (poll_stop(sh, stop_flag)) stopped = true;  // optimizer.cpp:625-627: do_more
       if (stopped) break;
       // optimizer.cpp:632-665: chi2 > threshold or depth <= 0 -> level 1
       for (int e = tid; e < pb.n_obs; e += kThreads) {

@@ -66,7 +66,7 @@ __global__ __launch_bounds__(64 * kTriWaves) void search_tri_kernel(
     int64_t match_stride, int32_t* __restrict__ nmatches) {
   __shared__ int8_t s_bin[kMaxFeat];
   __shared__ int s_hist[kHisto];
-  __shared__ int s_acc[kTriWaves], s_rem[kTriWaves], s_ind[3];
+  __shared__ int s_acc[kTriWaves], s_rem[kTriWaves], s_ind[3], s_bad;
   const int pair = blockIdx.x, tid = threadIdx.x, lane = lane_id(), wid = wave_id();
   const slamgpu_tri_pair P = pairs[pair];
   const slamgpu_kf& A = kfs[P.kf1];
@@ -82,6 +82,7 @@ __global__ __launch_bounds__(64 * kTriWaves) void search_tri_kernel(
     s_bin[i] = -1;
   }
   if (tid < kHisto) s_hist[tid] = 0;
+  if (tid == 0) s_bad = 0;
   // epipole of pKF1's centre in pKF2 (:643-649)
   const float c2x = gemm_row(B.Rcw, A.Ow, B.tcw[0]);
   const float c2y = gemm_row(B.Rcw + 3, A.Ow, B.tcw[1]);
@@ -102,6 +103,10 @@ __global__ __launch_bounds__(64 * kTriWaves) void search_tri_kernel(
     const int ib = node_find(B.nodes, B.n_nodes, A.nodes[lo]);
     if (ib < 0) continue;
     const int idx1 = (int)A.node_feats[p];
+    if ((unsigned)idx1 >= (unsigned)na) {  // malformed FeatureVector: flag the pair, touch nothing
+      s_bad = 1;
+      continue;
+    }
     if (A.has_mp[idx1]) continue;
     const bool st1 = A.u_right[idx1] >= 0;
     if (P.only_stereo && !st1) continue;
@@ -116,12 +121,20 @@ __global__ __launch_bounds__(64 * kTriWaves) void search_tri_kernel(
     uint32_t best = 0xffffffffu;
     for (int c = lane; c < nbn; c += 64) {
       const int idx2 = (int)B.node_feats[b0 + c];
+      if ((unsigned)idx2 >= (unsigned)nb) {
+        s_bad = 1;
+        continue;
+      }
       if (B.has_mp[idx2]) continue;
       const bool st2 = B.u_right[idx2] >= 0;
       if (P.only_stereo && !st2) continue;
       const int dist = hamming32(d1, B.desc + (int64_t)idx2 * 32);
       if (dist > kThLow) continue;
       const slamgpu_keypoint kp2 = B.kps[idx2];
+      if ((unsigned)kp2.octave >= (unsigned)lv.nlevels) {
+        s_bad = 1;
+        continue;
+      }
       if (!st1 && !st2) {
         const float dx = ex - kp2.x, dy = ey - kp2.y;
         if (fmaf(dx, dx, dy * dy) < 100.0f * lv.scale[kp2.octave]) continue;
@@ -193,7 +206,7 @@ __global__ __launch_bounds__(64 * kTriWaves) void search_tri_kernel(
   if (tid == 0) {
     int nm = 0;
     for (int w = 0; w < kTriWaves; w++) nm += s_acc[w] - s_rem[w];
-    nmatches[pair] = nm;
+    nmatches[pair] = s_bad ? -1 : nm;
   }
 }
 

@@ -6,6 +6,9 @@
 // on a per-thread stream and synchronises.
 #include <hip/hip_runtime.h>
 
+#include <chrono>
+#include <thread>
+
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
@@ -58,8 +61,12 @@ struct HostStage {
   hipStream_t stream = nullptr;
   void* buf = nullptr;
   size_t bytes = 0;
+  // host-mapped mirror of a caller's stop flag, polled by the local BA kernel
+  int32_t* stop_host = nullptr;
+  int32_t* stop_dev = nullptr;
   ~HostStage() {
     if (buf) (void)hipFree(buf);
+    if (stop_host) (void)hipHostFree(stop_host);
     if (stream) (void)hipStreamDestroy(stream);
   }
 };
@@ -70,8 +77,10 @@ int stage_reserve(HostStage& S, size_t need) {
   OPT_HIPCHECK(hipGetDevice(&dev));
   if (S.device != dev) {
     if (S.buf) (void)hipFree(S.buf);
+    if (S.stop_host) (void)hipHostFree(S.stop_host);
     if (S.stream) (void)hipStreamDestroy(S.stream);
     S.buf = nullptr;
+    S.stop_host = S.stop_dev = nullptr;
     S.stream = nullptr;
     S.bytes = 0;
     OPT_HIPCHECK(hipStreamCreateWithFlags(&S.stream, hipStreamNonBlocking));
@@ -213,7 +222,7 @@ int slamgpu_local_ba_linearize_device(
 int slamgpu_local_bundle_adjustment(const slamgpu_camera* cam, const float* inv_sigma2,
                                     int nlevels, float* kf_Tcw, const uint8_t* kf_mode, int n_kf,
                                     float* points, int n_points, const int32_t* point_obs_start,
-                                    const slamgpu_ba_obs* obs, const int* stop_flag,
+                                    const slamgpu_ba_obs* obs, const volatile bool* stop_flag,
                                     uint8_t* erase, int* lm_iterations) {
   PoseParams P;
   if (int r = make_params(cam, inv_sigma2, nlevels, &P)) return r;
@@ -268,12 +277,35 @@ int slamgpu_local_bundle_adjustment(const slamgpu_camera* cam, const float* inv_
     OPT_HIPCHECK(hipMemcpyAsync(b + o_obs, obs, sizeof(slamgpu_ba_obs) * (size_t)n_obs,
                                 hipMemcpyHostToDevice, S.stream));
   const BaWorkspace ws = ba_workspace_layout(b + o_ws, n_kf, n_points, n_obs, nullptr);
+  volatile int32_t* mirror = nullptr;
+  if (stop_flag) {
+    if (!S.stop_host) {
+      void* h = nullptr;
+      OPT_HIPCHECK(hipHostMalloc(&h, 64, hipHostMallocMapped | hipHostMallocCoherent));
+      S.stop_host = static_cast<int32_t*>(h);
+      void* d = nullptr;
+      OPT_HIPCHECK(hipHostGetDevicePointer(&d, h, 0));
+      S.stop_dev = static_cast<int32_t*>(d);
+    }
+    mirror = S.stop_host;
+    *mirror = *stop_flag ? 1 : 0;
+  }
   OPT_HIPCHECK(launch_local_ba(P, reinterpret_cast<slamgpu_ba_problem*>(b + o_prob), 1,
                                reinterpret_cast<float*>(b + o_T), reinterpret_cast<uint8_t*>(b + o_mode),
                                reinterpret_cast<float*>(b + o_pts), reinterpret_cast<int32_t*>(b + o_ps),
                                reinterpret_cast<slamgpu_ba_obs*>(b + o_obs),
                                reinterpret_cast<uint8_t*>(b + o_er), reinterpret_cast<int32_t*>(b + o_st),
-                               ws, nullptr, S.stream));
+                               ws, stop_flag ? S.stop_dev : nullptr, S.stream));
+  if (mirror) {  // keep the device's view of the caller's flag live until the kernel is done
+    // (nothing pageable may be queued behind the kernel here: a copy to pageable memory would
+    // block this thread until the kernel ends)
+    hipError_t q;
+    while ((q = hipStreamQuery(S.stream)) == hipErrorNotReady) {
+      *mirror = *stop_flag ? 1 : 0;
+      std::this_thread::sleep_for(std::chrono::microseconds(20));
+    }
+    if (q != hipSuccess) return fail(SLAMGPU_EHIP, "local BA: %s", hipGetErrorString(q));
+  }
   int32_t st = 0;
   OPT_HIPCHECK(hipMemcpyAsync(&st, b + o_st, 4, hipMemcpyDeviceToHost, S.stream));
   OPT_HIPCHECK(hipStreamSynchronize(S.stream));

@@ -198,26 +198,31 @@ int slamgpu_create(int device, const slamgpu_orb_params* p, int cols, int rows, 
   }
   compute_tables(c->params, &c->tables);
   if (c->geom.kp_cap > 4096) {  // matcher keys carry a 12-bit keypoint index
+    const int kpc = c->geom.kp_cap;
     delete c;
     return create_fail(SLAMGPU_EINVAL, "slamgpu_create: nfeatures %d gives %d keypoints per image "
-                       "> 4096", p->nfeatures, 0);
+                       "> 4096", p->nfeatures, kpc);
   }
   for (int l = 0; l < c->geom.nlevels; l++)
     if (c->geom.lv[l].node_cap > 1024) {
+      const int need = c->geom.lv[l].node_cap;
       delete c;
       return create_fail(SLAMGPU_EINVAL, "slamgpu_create: level %d needs %d octree nodes > 1024",
-                         l, 0);  // octree LDS arrays hold <= 2048 list nodes
+                         l, need);  // octree LDS arrays hold <= 2048 list nodes
     }
   c->device = device;
   c->max_frames = max_frames;
   c->max_images = 2 * max_frames;
   int rc = 0;
-#define TRY(x)             \
-  do {                     \
-    if ((rc = (x)) != 0) { \
-      *out = c;            \
-      return rc;           \
-    }                      \
+  // on failure the partial context is destroyed here and its message kept for
+  // slamgpu_last_error(NULL); *out stays NULL
+#define TRY(x)                           \
+  do {                                   \
+    if ((rc = (x)) != 0) {               \
+      t_create_err = c->err;             \
+      slamgpu_destroy(c);                \
+      return rc;                         \
+    }                                    \
   } while (0)
   TRY(hipSetDevice(device) == hipSuccess ? 0 : fail(c, SLAMGPU_EHIP, "hipSetDevice"));
   TRY(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) == hipSuccess

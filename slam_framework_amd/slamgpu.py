@@ -196,10 +196,9 @@ class Context:
                                   C.byref(h))
         self.h = h
         if rc != 0:
-            msg = lib().slamgpu_last_error(h if h else None).decode()
-            if h:
-                lib().slamgpu_destroy(h)
-                self.h = None
+            assert not h, "slamgpu_create returns no context on failure"
+            self.h = None
+            msg = lib().slamgpu_last_error(None).decode()
             raise SlamGpuError(f"slamgpu_create failed ({rc}): {msg}")
         self.kp_cap = lib().slamgpu_kp_capacity(self.h)
 
@@ -502,8 +501,9 @@ class Optimizer:
                               stop_flag=False):
         """Optimizer::LocalBundleAdjustment (optimizer.cpp:413-716) on the gathered graph.
         kf_mode per keyframe: 0 local, 1 local fixed (id 0), 2 fixed camera; observations
-        grouped by point (CSR point_obs_start). Returns (kf_Tcw', points', erase,
-        lm_iterations); erase marks the reference's vToErase observations."""
+        grouped by point (CSR point_obs_start). stop_flag: a bool, or a ctypes.c_bool that
+        another thread may raise mid-run (the reference's bool* stop_flag). Returns (kf_Tcw',
+        points', erase, lm_iterations); erase marks the reference's vToErase observations."""
         kf = np.ascontiguousarray(np.asarray(kf_Tcw, np.float32).reshape(-1, 4, 4)).copy()
         mode = np.ascontiguousarray(kf_mode, np.uint8)
         pts = np.ascontiguousarray(np.asarray(points, np.float32).reshape(-1, 3)).copy()
@@ -512,7 +512,8 @@ class Optimizer:
         isig = np.ascontiguousarray(inv_sigma2, np.float32)
         erase = np.zeros(max(len(ob), 1), np.uint8)
         its = C.c_int()
-        stop = C.c_int(1 if stop_flag else 0)
+        # a ctypes.c_bool stays live: another thread may raise it while the call runs
+        stop = stop_flag if isinstance(stop_flag, C.c_bool) else C.c_bool(bool(stop_flag))
         _opt_check(lib().slamgpu_local_bundle_adjustment(
             C.byref(Camera(*cam)), _ptr(isig), len(isig), _ptr(kf), _ptr(mode), len(mode),
             _ptr(pts), len(pts), _ptr(start), _ptr(ob), C.byref(stop), _ptr(erase),

@@ -302,6 +302,8 @@ def _ba_lib():
         vp, ip = C.c_void_p, C.c_int
         L.oc_local_bundle_adjustment.argtypes = [vp, vp, vp, vp, ip, vp, ip, vp, vp, vp,
                                                  C.POINTER(ip)]
+        L.oc_local_bundle_adjustment_stop.argtypes = [vp, vp, vp, vp, ip, vp, ip, vp, vp, ip,
+                                                      vp, C.POINTER(ip)]
         L.oc_ba_edge_eval.argtypes = [vp, vp, vp, vp, vp, C.c_float, vp, vp, vp]
         L.oc_ba_linearize.argtypes = [vp, vp, vp, vp, ip, vp, ip, vp, vp, vp, vp, vp, vp, vp, vp]
         L.oc_ba_linearize.restype = C.c_double
@@ -310,8 +312,9 @@ def _ba_lib():
     return L
 
 
-def local_ba(cam, prob):
-    """Optimizer::LocalBundleAdjustment restated on a synthetic.ba_problem dict. Returns
+def local_ba(cam, prob, stop_after=-1):
+    """Optimizer::LocalBundleAdjustment restated on a synthetic.ba_problem dict, with the
+    reference's stop_flag raised after `stop_after` polls of it (< 0: never). Returns
     (kf_Tcw', points', erase, lm_iterations)."""
     cam = np.asarray(cam, np.float32)
     kf = np.ascontiguousarray(prob["kf_Tcw"], np.float32).copy()
@@ -322,9 +325,9 @@ def local_ba(cam, prob):
     isig = np.ascontiguousarray(prob["inv_sigma2"], np.float32)
     erase = np.zeros(max(len(obs), 1), np.uint8)
     it = C.c_int()
-    r = _ba_lib().oc_local_bundle_adjustment(ptr(cam), ptr(isig), ptr(kf), ptr(mode), len(mode),
-                                             ptr(pts), len(pts), ptr(start), ptr(obs),
-                                             ptr(erase), C.byref(it))
+    r = _ba_lib().oc_local_bundle_adjustment_stop(ptr(cam), ptr(isig), ptr(kf), ptr(mode),
+                                                  len(mode), ptr(pts), len(pts), ptr(start),
+                                                  ptr(obs), stop_after, ptr(erase), C.byref(it))
     assert r == 0
     return kf, pts, erase[:len(obs)].astype(bool), it.value
 

@@ -72,6 +72,35 @@ def test_local_ba_stop_flag_leaves_inputs(gpu_lib):
     assert np.array_equal(kf, P["kf_Tcw"]) and np.array_equal(pts, P["points"])
 
 
+def test_local_ba_interrupted_mid_run(oracle, gpu_lib):
+    """The reference's stop_flag raised by another thread while the optimisation runs
+    (LocalMapper::InsertKeyFrame -> abort_BA_, local_mapper.cpp:89-93): the device stops at its
+    next terminate() poll, and its poses, points, erase list and LM count are the oracle's with
+    the flag raised at one of its polls (oracle.local_ba(stop_after=c), some c)."""
+    import ctypes
+    import threading
+    P = S.c5_problem(11)
+    _, _, _, its_full = run_host(gpu_lib, P)
+    for delay in (0.002, 0.003, 0.005, 0.001):
+        flag = ctypes.c_bool(False)
+        t = threading.Timer(delay, lambda: setattr(flag, "value", True))
+        t.start()
+        kf, pts, er, its = run_host(gpu_lib, P, stop=flag)
+        t.join()
+        if 0 < its < its_full:
+            break
+    assert 0 < its < its_full, (its, its_full)
+    for c in range(1, 4 * its_full + 40):
+        kf_o, pts_o, er_o, its_o = oracle.local_ba(CAM, P, stop_after=c)
+        if its_o > its:
+            break
+        if its_o == its and np.array_equal(er, er_o):
+            assert_close(kf, kf_o, P["kf_Tcw"], "interrupted poses")
+            assert_close(pts, pts_o, P["points"], "interrupted points")
+            return
+    raise AssertionError(f"no oracle stop position reproduces the device's {its} iterations")
+
+
 def test_local_ba_rejects_bad_graphs(gpu_lib):
     P = S.ba_problem(8, n_local=25, n_fixed=1, n_points=200)
     with pytest.raises(gpu_lib.SlamGpuError):

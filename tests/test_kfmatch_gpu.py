@@ -187,3 +187,53 @@ def test_errors_are_loud(K, scene):
     b = K.host_kf(k1["kps"], k1["desc"], k1["ur"], KS.pose(0))
     with pytest.raises(SlamGpuError):
         K.fuse(b, KS.fuse_points(k1, KS.pose(0))[:4], 3.0, KS.CAM, lv, K.kf_grid(1241, 376))
+
+
+def test_device_malformed_keyframe_flags_pair(K, scene):
+    """Batched SearchForTriangulation with a FeatureVector entry naming a feature >= n, and with a
+    keypoint octave outside [0, nlevels): the pair reports -1 and nothing outside its match row
+    (or the LDS bin table) is written; a well-formed pair of the same launch is unaffected."""
+    import torch
+    dev = torch.device("cuda", 0)
+    k0, k1 = scene
+    T0, T1 = KS.pose(0), KS.pose(1, (-0.4, 0.02, 0.1))
+    keep = []
+
+    def dev_arr(a):
+        t = torch.from_numpy(np.ascontiguousarray(a).view(np.uint8).copy()).to(dev)
+        keep.append(t)
+        return int(t.data_ptr())
+
+    bad_feats = k0["fv"][2].astype(np.uint32).copy()
+    bad_feats[len(bad_feats) // 2] = 60000            # feature index far past n
+    bad_kps = k1["kps"].copy()
+    bad_kps["octave"][:] = 31                         # >= nlevels (8)
+    variants = [(k0, k0["fv"][2], k0["kps"]), (k0, bad_feats, k0["kps"]), (k1, k1["fv"][2], bad_kps),
+                (k1, k1["fv"][2], k1["kps"])]
+    kfs = np.zeros(len(variants), K.KF_DTYPE)
+    for i, (k, feats, kps) in enumerate(variants):
+        T = T0 if k is k0 else T1
+        h = K.host_kf(k["kps"], k["desc"], k["ur"], T, k["mp"], _fv(None, k))[0]
+        kfs[i]["kps"], kfs[i]["desc"] = dev_arr(kps), dev_arr(k["desc"])
+        kfs[i]["u_right"], kfs[i]["has_mp"] = dev_arr(k["ur"]), dev_arr(k["mp"])
+        kfs[i]["nodes"] = dev_arr(k["fv"][0].astype(np.uint32))
+        kfs[i]["node_start"] = dev_arr(k["fv"][1].astype(np.int32))
+        kfs[i]["node_feats"] = dev_arr(feats.astype(np.uint32))
+        kfs[i]["n"], kfs[i]["n_nodes"] = len(k["desc"]), len(k["fv"][0])
+        kfs[i]["Rcw"], kfs[i]["tcw"], kfs[i]["Ow"] = list(h.Rcw), list(h.tcw), list(h.Ow)
+    d_kfs = torch.from_numpy(kfs.view(np.uint8).copy()).to(dev)
+    plist = [(0, 3), (1, 3), (0, 2)]                  # good, bad FeatureVector in kf1, bad octaves in kf2
+    pairs = np.zeros(len(plist), K.TRI_PAIR_DTYPE)
+    for p, (a, b) in enumerate(plist):
+        pairs[p] = (a, b, KS.fundamental(T0, T1).reshape(-1), 0)
+    d_pairs = torch.from_numpy(pairs.view(np.uint8).copy()).to(dev)
+    cap = 2100
+    guard = 64
+    d_m = torch.full((len(plist) * cap + guard,), -9, dtype=torch.int32, device=dev)
+    d_nm = torch.zeros(len(plist), dtype=torch.int32, device=dev)
+    K.search_for_triangulation_device(d_kfs, d_pairs, len(plist), KS.CAM, K.levels(), True, d_m,
+                                      cap, d_nm, torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    nm, m = d_nm.cpu().numpy(), d_m.cpu().numpy()
+    assert nm[0] > 20 and nm[1] == -1 and nm[2] == -1
+    assert (m[len(plist) * cap:] == -9).all(), "wrote past the last match row"
