@@ -115,6 +115,8 @@ def main():
                     help="skip the PoseOptimization / LocalBundleAdjustment measurements")
     ap.add_argument("--no-bow", action="store_true",
                     help="skip the ComputeBoW / SearchByBoW measurement")
+    ap.add_argument("--no-latency", action="store_true",
+                    help="skip the single-frame drop-in latency and the PCIe-inclusive rate")
     args = ap.parse_args()
 
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
@@ -136,7 +138,7 @@ def main():
         dist.init_process_group("nccl", device_id=dev)
         world = dist.get_world_size()
         # the CPU baseline and the optimizer / BoW legs are N=1 measurements
-        args.no_cpu_baseline = args.no_optimizer = args.no_bow = True
+        args.no_cpu_baseline = args.no_optimizer = args.no_bow = args.no_latency = True
 
     from slam_framework_amd import slamgpu as G
     from slam_framework_amd import synthetic as S
@@ -326,6 +328,10 @@ def main():
         bow_leg = None
         if not args.no_bow:
             bow_leg = bench_bow(ctx, Bs, dev, not args.no_cpu_baseline)
+        drop_in = None
+        if not args.no_latency:
+            drop_in = {"single_frame": bench_frame_latency(Ls, Rs, cam, local),
+                       "batched_h2d": bench_h2d(ctxs[0], host_l, host_r, poses, cam, dev, args)}
         line = {
             "metric": "stereo frames/sec ORB extract+match @1241x376, 2000 kp/frame",
             "value": round(value, 2), "unit": "stereo frames/s", "n_gpus": world,
@@ -347,6 +353,7 @@ def main():
             "kernel_ms_per_step": {n: round(brk[n][0], 4) for n in names},
             "optimizer": opt,
             "bow": bow_leg,
+            "drop_in": drop_in,
             "per_rank_matches_per_step": summ[:, 1].tolist(),
         }
         print(json.dumps(line))
@@ -411,6 +418,87 @@ def check_gather(gat, ctxs, parts, gframe, Bs, kc, D, world, F):
     return {"bytes_per_rank_per_step": gat.nbytes, "frames_per_rank_per_step": F,
             "record_bytes_per_frame": int(gat.fields["frontend"]) + 4 * kc + 4,
             "frames_checked_vs_rank0": checked, "identical": True}
+
+
+def bench_frame_latency(Ls, Rs, cam, device, reps=40):
+    """The unmodified Tracker's call pattern (tracker.cpp:104-141 -> the stereo Frame ctor,
+    frame.cpp:61-111): ONE frame per call from host images -- slamgpu_frame_stereo (H2D of both
+    views, extract L+R, stereo, grid) plus the download of both views' keypoints + descriptors
+    and the stereo coordinates the Frame holds. Median wall time per frame."""
+    from slam_framework_amd import slamgpu as G
+    from slam_framework_amd import synthetic as S
+    c = G.Context(S.KITTI_COLS, S.KITTI_ROWS, 2000, 1.2, 8, 20, 7, max_frames=1, device=device)
+    ms = []
+    for i in range(reps + 3):
+        f = i % len(Ls)
+        t0 = time.perf_counter()
+        c.frame_stereo(Ls[f], Rs[f], cam)
+        c.keypoints(0)
+        c.keypoints(1)
+        c.stereo(0)
+        ms.append(1e3 * (time.perf_counter() - t0))
+    c.close()
+    ms = np.array(ms[3:])
+    return {"workload": "one stereo frame per call from host memory (slamgpu_frame_stereo + "
+                        "download of keypoints, descriptors, u_right/depth)",
+            "median_ms": round(float(np.median(ms)), 3), "p90_ms": round(float(np.percentile(ms, 90)), 3),
+            "frames_per_s": round(1e3 / float(np.median(ms)), 1), "calls": reps}
+
+
+def bench_h2d(ctx, host_l, host_r, poses, cam, dev, args, steps=10):
+    """Batched throughput with the input crossing PCIe inside the timed region: every step's B
+    stereo frames are copied from pinned host memory on a copy stream into one of two device
+    buffers while the previous step computes on the other (the same step as the headline)."""
+    import torch
+    from slam_framework_amd import slamgpu as G
+    B, rows, pitch = host_l.shape
+    stride = rows * pitch
+    kc = ctx.kp_cap
+    pin = [torch.from_numpy(h).pin_memory() for h in (host_l, host_r)]
+    bufs = [[torch.empty_like(p, device=dev) for p in pin] for _ in range(2)]
+    main = torch.cuda.current_stream()
+    cp = torch.cuda.Stream(device=dev)
+    d_poses = torch.from_numpy(poses.view(np.uint8).copy()).to(dev)
+    q = torch.empty(B * kc * G.F2F_QUERY_DTYPE.itemsize, dtype=torch.uint8, device=dev)
+    qs, qc, nm = (torch.empty(B, dtype=torch.int32, device=dev) for _ in range(3))
+    mp = torch.empty(B * kc, dtype=torch.int32, device=dev)
+    blk = torch.empty(B * kc, dtype=torch.uint8, device=dev)
+    done = [torch.cuda.Event(), torch.cuda.Event()]
+    for e in done:
+        e.record(main)
+
+    def step(k):
+        dl, dr = bufs[k % 2]
+        cp.wait_event(done[k % 2])           # the step that last read this buffer is done
+        with torch.cuda.stream(cp):
+            dl.copy_(pin[0], non_blocking=True)
+            dr.copy_(pin[1], non_blocking=True)
+        main.wait_stream(cp)
+        h = main.cuda_stream
+        ctx.frontend_device(dl, dr, stride, pitch, B, cam, h)
+        ctx.make_vo_queries_device(d_poses, 1, q, qs, qc, B, h)
+        mp.fill_(-1)
+        blk.zero_()
+        ctx.search_by_projection_frame_device(q, B * kc, qs, qc, kc, d_poses, mp, blk, kc, nm,
+                                              B, h)
+        done[k % 2].record(main)
+    for k in range(2):
+        step(k)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for k in range(steps):
+        step(k)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    from slam_framework_amd import synthetic as S
+    pair_bytes = 2 * S.KITTI_COLS * S.KITTI_ROWS
+    return {"workload": "the headline step with both views copied from pinned host memory each "
+                        "step (copy stream, double-buffered)",
+            "value": round(steps * (B - 1) / dt, 1), "unit": "stereo frames/s",
+            "ms_per_step": round(1e3 * dt / steps, 3),
+            "h2d_bytes_per_step": int(2 * host_l.nbytes),
+            "h2d_GBps": round(2 * host_l.nbytes * steps / dt / 1e9, 2),
+            "image_bytes_per_pair": pair_bytes}
 
 
 FP64_VALU_PEAK_TFLOPS = 78.6  # MI355X FP64 vector peak (MI355X_MICROARCH.md)
@@ -840,10 +928,25 @@ def bench_kfmatch(ctx, Bs, dev, view, sets, with_cpu):
     return out
 
 
+def cpu_model():
+    """The host CPU's model name (lscpu's "Model name") and logical CPU count."""
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip(), os.cpu_count()
+    except OSError:
+        pass
+    return None, os.cpu_count()
+
+
 def cpu_baseline(Ls, Rs, n_frames):
-    """The oracle/ restatement (scalar C) on host threads: extract L+R, stereo, frame-to-frame
-    search against the previous frame's stereo points. Each thread runs its own consecutive
-    frames; wall time over all threads."""
+    """The oracle/ restatement (C, the -O3 x86-64-v3 build oracle/liborb_oracle_fast.so, checked
+    byte-identical to the test oracle by tests/test_oracle.py) on host threads, two ways:
+    throughput -- each of 16 threads runs its own consecutive frames (extract L+R, stereo,
+    frame-to-frame search against the previous frame's stereo points), wall time over all;
+    reference threading -- one frame at a time, its left and right extraction on two threads as
+    the stereo Frame ctor runs them (frame.cpp:86-89), then stereo and search."""
     import concurrent.futures as cf
 
     sys.path.insert(0, os.path.join(ROOT, "tests"))
@@ -852,12 +955,22 @@ def cpu_baseline(Ls, Rs, n_frames):
     from slam_framework_amd import synthetic as S
 
     O.build()
+    if O._lib is None:
+        O.use_fast()
     t = O.tables()
     g = O.grid_geom(S.KITTI_COLS, S.KITTI_ROWS)
     cam = S.KITTI_CAM
     threads = min(16, os.cpu_count() or 1)
     per_thread = max(2, (n_frames or 16 * threads) // threads)
     D = len(Ls)
+
+    def search(f, kl, dl, ur, prev):
+        q, lmp, lout, xyz, md, nobs = scenario.vo_queries(prev[0], prev[1], prev[2], prev[3])
+        p = scenario.pose(f)
+        mp = np.full(len(kl), -1, np.int32)
+        O.search_frame(t, g, kl, dl, ur, mp, prev[0], lmp, lout, xyz, md, nobs,
+                       p["Rcw"][0].reshape(3, 3), p["tcw"][0], 0.0,
+                       float(p["baseline"][0]), cam, 7.0, 0, 1)
 
     def run(tid):
         prev = None
@@ -867,13 +980,7 @@ def cpu_baseline(Ls, Rs, n_frames):
             kr, dr, pr = O.extract(t, Rs[f], True)
             ur, depth, _ = O.stereo(t, kl, dl, kr, dr, pl, pr, cam[0], cam[4])
             if prev is not None:
-                q, lmp, lout, xyz, md, nobs = scenario.vo_queries(prev[0], prev[1], prev[2],
-                                                                  prev[3])
-                p = scenario.pose(f)
-                mp = np.full(len(kl), -1, np.int32)
-                O.search_frame(t, g, kl, dl, ur, mp, prev[0], lmp, lout, xyz, md, nobs,
-                               p["Rcw"][0].reshape(3, 3), p["tcw"][0], 0.0,
-                               float(p["baseline"][0]), cam, 7.0, 0, 1)
+                search(f, kl, dl, ur, prev)
             prev = (kl, dl, depth, f)
         return per_thread
 
@@ -881,11 +988,33 @@ def cpu_baseline(Ls, Rs, n_frames):
     with cf.ThreadPoolExecutor(threads) as ex:
         done = sum(ex.map(run, range(threads)))
     wall = time.perf_counter() - t0
+
+    # the reference's own threading: frames in sequence, L and R extracted concurrently
+    n_seq = 24
+    prev = None
+    t1 = time.perf_counter()
+    with cf.ThreadPoolExecutor(2) as ex:
+        for k in range(n_seq):
+            f = k % D
+            fl, fr = ex.submit(O.extract, t, Ls[f], True), ex.submit(O.extract, t, Rs[f], True)
+            (kl, dl, pl), (kr, dr, pr) = fl.result(), fr.result()
+            ur, depth, _ = O.stereo(t, kl, dl, kr, dr, pl, pr, cam[0], cam[4])
+            if prev is not None:
+                search(f, kl, dl, ur, prev)
+            prev = (kl, dl, depth, f)
+    seq = time.perf_counter() - t1
+    model, ncpu = cpu_model()
     return {"value": round(done / wall, 2), "unit": "stereo frames/s", "cores": threads,
-            "kind": "port",
+            "kind": "port", "cpu_model": model, "host_logical_cpus": ncpu,
+            "build": "oracle/liborb_oracle_fast.so: gcc -O3 -march=x86-64-v3 -ffp-contract=off",
             "sample": f"{done} synthetic stereo frames ({threads} threads x {per_thread}); "
-                      f"oracle/ scalar C restatement: extract L+R + stereo + frame-to-frame",
-            "wall_s": round(wall, 2)}
+                      f"oracle/ C restatement: extract L+R + stereo + frame-to-frame",
+            "wall_s": round(wall, 2),
+            "reference_threading": {
+                "value": round(n_seq / seq, 2), "unit": "stereo frames/s", "cores": 2,
+                "ms_per_frame": round(1e3 * seq / n_seq, 2),
+                "sample": f"{n_seq} frames in sequence, left/right extraction on 2 threads "
+                          "(frame.cpp:86-89), then stereo + frame-to-frame search"}}
 
 
 if __name__ == "__main__":

@@ -36,6 +36,7 @@ def _stale() -> bool:
 
 def build(force: bool = False, verbose: bool = False) -> str:
     if not force and not _stale():
+        build_capi_check()
         return LIB
     objdir = os.path.join(PKG, "build")
     os.makedirs(objdir, exist_ok=True)
@@ -60,7 +61,25 @@ def build(force: bool = False, verbose: bool = False) -> str:
     subprocess.run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp, *objs],
                    check=True)
     os.replace(tmp, LIB)
+    build_capi_check()
     return LIB
+
+
+ROOT = os.path.dirname(PKG)
+CAPI_SRC = os.path.join(ROOT, "tests", "capi_check.cpp")
+CAPI_BIN = os.path.join(ROOT, "tests", "capi_check")
+
+
+def build_capi_check() -> str:
+    """g++ build of tests/capi_check.cpp against include/*.h, linked to libslamgpu.so: the C++
+    caller side of the drop-in boundary, with no HIP or Python in between."""
+    if os.path.exists(CAPI_BIN) and os.path.getmtime(CAPI_BIN) >= max(
+            os.path.getmtime(CAPI_SRC), os.path.getmtime(LIB)):
+        return CAPI_BIN
+    subprocess.run(["g++", "-O2", "-std=c++17", "-Wall", "-I", os.path.join(ROOT, "include"),
+                    CAPI_SRC, "-L", PKG, "-lslamgpu",
+                    "-Wl,-rpath,$ORIGIN/../slam_framework_amd", "-o", CAPI_BIN], check=True)
+    return CAPI_BIN
 
 
 if __name__ == "__main__":

@@ -43,6 +43,7 @@ struct slamgpu_ctx {
   CellDesc* d_cells = nullptr;
   // images staged by the host-buffer calls (left at d_in, right at d_in + in_stride)
   uint8_t* d_in = nullptr;
+  uint8_t* h_in = nullptr;  // pinned twin of d_in: one DMA per call instead of per-row copies
   int in_pitch = 0;
   int64_t in_stride = 0;
   // batch state
@@ -261,6 +262,8 @@ int slamgpu_create(int device, const slamgpu_orb_params* p, int cols, int rows, 
   c->in_pitch = (cols + 63) / 64 * 64;
   c->in_stride = (int64_t)c->in_pitch * rows;
   TRY(dalloc(c, &c->d_in, 2 * (size_t)c->in_stride));
+  TRY(hcheck(c, hipHostMalloc(reinterpret_cast<void**>(&c->h_in), 2 * (size_t)c->in_stride,
+                              hipHostMallocDefault)));
   TRY(dalloc(c, &c->d_pyr, (size_t)n * g.pyr_bytes));
   TRY(dalloc(c, &c->d_blur, (size_t)n * g.blur_bytes));
   TRY(dalloc(c, &c->ws.cell_keys, (size_t)n * g.cells_per_image * g.cell_cap));
@@ -300,6 +303,7 @@ void slamgpu_destroy(slamgpu_ctx* c) {
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   for (hipEvent_t e : c->timer.pool) (void)hipEventDestroy(e);
   for (void* p : c->allocs) (void)hipFree(p);
+  if (c->h_in) (void)hipHostFree(c->h_in);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   for (hipStream_t s : {c->fx.side0, c->fx.side})
     if (s) (void)hipStreamDestroy(s);
@@ -344,12 +348,24 @@ static int run_frontend(slamgpu_ctx* c, const ImageBatch& b, int n_frames, int n
   return 0;
 }
 
+// Host images -> d_in: rows packed into the pinned staging buffer at the device pitch, then one
+// DMA of the whole buffer (pageable 2-D copies go row by row: ~5 ms for a stereo pair). The
+// previous call on this context has synchronised, so the staging buffer is free.
+static int stage_images(slamgpu_ctx* c, const uint8_t* const* imgs, int n, size_t step) {
+  const int cols = c->geom.cols, rows = c->geom.rows;
+  for (int i = 0; i < n; i++)
+    for (int y = 0; y < rows; y++)
+      std::memcpy(c->h_in + i * c->in_stride + (int64_t)y * c->in_pitch, imgs[i] + y * step, cols);
+  HIPCHECK(c, hipMemcpyAsync(c->d_in, c->h_in, (size_t)n * c->in_stride, hipMemcpyHostToDevice,
+                             c->stream));
+  return 0;
+}
+
 int slamgpu_extract(slamgpu_ctx* c, const uint8_t* img, size_t step, slamgpu_keypoint* kps,
                     uint8_t* desc, int cap, int* n_out) {
   if (!c || !img) return SLAMGPU_EINVAL;
   HIPCHECK(c, hipSetDevice(c->device));
-  HIPCHECK(c, hipMemcpy2DAsync(c->d_in, c->in_pitch, img, step, c->geom.cols, c->geom.rows,
-                               hipMemcpyHostToDevice, c->stream));
+  if (int r = stage_images(c, &img, 1, step)) return r;
   ImageBatch b{c->d_in, c->d_in + c->in_stride, 2 * c->in_stride, c->in_pitch, c->d_pyr,
                c->d_blur};
   int rc = run_frontend(c, b, 1, 1, false, c->stream);
@@ -422,10 +438,8 @@ int slamgpu_frame_stereo(slamgpu_ctx* c, const uint8_t* left, const uint8_t* rig
   if (!c || !left || !right || !cam) return SLAMGPU_EINVAL;
   HIPCHECK(c, hipSetDevice(c->device));
   set_camera(c, cam);
-  HIPCHECK(c, hipMemcpy2DAsync(c->d_in, c->in_pitch, left, step, c->geom.cols, c->geom.rows,
-                               hipMemcpyHostToDevice, c->stream));
-  HIPCHECK(c, hipMemcpy2DAsync(c->d_in + c->in_stride, c->in_pitch, right, step, c->geom.cols,
-                               c->geom.rows, hipMemcpyHostToDevice, c->stream));
+  const uint8_t* imgs[2] = {left, right};
+  if (int r = stage_images(c, imgs, 2, step)) return r;
   ImageBatch b{c->d_in, c->d_in + c->in_stride, 2 * c->in_stride, c->in_pitch, c->d_pyr,
                c->d_blur};
   int rc = run_frontend(c, b, 1, 2, true, c->stream);

@@ -51,7 +51,16 @@ class FrameView(C.Structure):
 
 
 def build() -> None:
-    subprocess.run(["make", "-s", "-C", ORACLE_DIR, "liborb_oracle.so"], check=True)
+    subprocess.run(["make", "-s", "-C", ORACLE_DIR, "liborb_oracle.so", "liborb_oracle_fast.so"],
+                   check=True)
+
+
+def use_fast() -> None:
+    """Load the -O3 x86-64-v3 build (oracle/Makefile liborb_oracle_fast.so) instead: the CPU
+    baseline's library. Must run before the first lib() call of the process."""
+    global LIB_PATH
+    assert _lib is None, "oracle library already loaded"
+    LIB_PATH = os.path.join(ORACLE_DIR, "liborb_oracle_fast.so")
 
 
 _lib = None
