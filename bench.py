@@ -151,7 +151,7 @@ def main():
     F = NS * (Bs - 1)   # frames this rank completes (owns) per step
     # ---- ONE synthetic sequence for the whole job (D distinct renders, frame g = render g % D),
     # sharded contiguously with a one-frame halo; uploaded once (resident in HBM before timing)
-    Ls, Rs = S.sequence(1000, D)
+    Ls, Rs = S.layered_sequence(1000, D)
     from slam_framework_amd import dist as SD
     first, lo, hi = SD.shard_with_halo(world * F, rank, world, first=1)
     assert hi - lo == F and first == lo - 1
@@ -169,7 +169,12 @@ def main():
     stride = rows * pitch
     poses = np.zeros(B, G.F2F_POSE_DTYPE)
     for f in range(B):
-        poses["Rcw"][f] = S.rotation(gframe[f] % D).astype(np.float32).reshape(-1)
+        t, tl = gframe[f] % D, (gframe[f] - 1) % D
+        Rf, tf = S.layered_pose(t)
+        poses["Rcw"][f] = Rf.astype(np.float32).reshape(-1)
+        poses["tcw"][f] = tf.astype(np.float32)
+        poses["tlc_z"][f] = np.float32((S.rotation(tl) @ (S.camera_center(t) -
+                                                          S.camera_center(tl)))[2])
     poses["baseline"] = np.float32(cam[4]) / np.float32(cam[0])
     poses["th"] = 7.0
     poses["check_ori"] = 1
@@ -337,8 +342,9 @@ def main():
             "value": round(value, 2), "unit": "stereo frames/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 3),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u8",
-            "data": "synthetic (seeded rectangles scene, one pure-rotation sequence sharded "
-                    "over the ranks)",
+            "data": "synthetic (seeded layered-surfaces scene: ~50% of keypoints with stereo "
+                    "depth, ~1000 frame-to-frame queries/frame; camera turning + 0.3 m/frame "
+                    "forward; one sequence of 16 renders, sharded over the ranks)",
             "config": {"workload": "configs[1]: synthetic 1241x376 stereo stream, 2000 kp/frame, "
                                    "extract L+R + stereo match + frame-to-frame match",
                        "frames_per_gpu_per_step": NS * (Bs - 1), "batch": B, "streams": NS,
@@ -807,9 +813,8 @@ def bench_bow(ctx, Bs, dev, with_cpu):
 
 
 def bench_kfmatch(ctx, Bs, dev, view, sets, with_cpu):
-    """SURVEY.md section 8(f) row 3 on the same batch, every frame taken as a keyframe (for the
-    triangulation search the sequence rotation plus a 0.4 m step along x per frame, so that F12
-    is well defined; for Fuse the pure rotations the frames were rendered at):
+    """SURVEY.md section 8(f) row 3 on the same batch, every frame taken as a keyframe at the
+    pose it was rendered at (synthetic.layered_pose: turning + 0.3 m forward per frame):
     SearchForTriangulation(KF f, KF f+1) with 30% of the keypoints already carrying map points,
     and Fuse of KF f's stereo points (unprojected from its depths) into KF f+1, th = 3."""
     import torch
@@ -820,7 +825,13 @@ def bench_kfmatch(ctx, Bs, dev, view, sets, with_cpu):
 
     kc = view.kp_cap
     D = 16
-    Ts = [KS.pose(f % D, (-0.4 * (f % D), 0.0, 0.0)) for f in range(Bs)]
+
+    def layered_T(t):
+        R, tc = S.layered_pose(t)
+        T = np.eye(4, dtype=np.float32)
+        T[:3, :3], T[:3, 3] = R, tc
+        return T
+    Ts = [layered_T(f % D) for f in range(Bs)]
     host = [ctx.keypoints(2 * f) for f in range(Bs)]
     depth = [ctx.stereo(f)[1] for f in range(Bs)]
     nn = sets.n_nodes.cpu().numpy()
@@ -839,13 +850,9 @@ def bench_kfmatch(ctx, Bs, dev, view, sets, with_cpu):
         kfs[f]["n"], kfs[f]["n_nodes"] = len(host[f][1]), nn[f]
         kfs[f]["Rcw"], kfs[f]["tcw"], kfs[f]["Ow"] = list(h.Rcw), list(h.tcw), list(h.Ow)
     d_kfs = torch.from_numpy(kfs.view(np.uint8).copy()).to(dev)
-    # Fuse uses the poses the images were rendered at (pure rotation), so that points re-project
-    kfs_r = kfs.copy()
-    Tr = [KS.pose(f % D) for f in range(Bs)]
-    for f in range(Bs):
-        kfs_r[f]["tcw"], kfs_r[f]["Ow"] = 0.0, 0.0
-        kfs_r[f]["Rcw"] = Tr[f][:3, :3].reshape(-1)
-    d_kfs_r = torch.from_numpy(kfs_r.view(np.uint8).copy()).to(dev)
+    # Fuse projects KF f's points with the poses the frames were rendered at
+    Tr = Ts
+    d_kfs_r = d_kfs
     pairs = np.zeros(Bs - 1, K.TRI_PAIR_DTYPE)
     for f in range(Bs - 1):
         pairs[f] = (f, f + 1, KS.fundamental(Ts[f], Ts[f + 1]).reshape(-1), 0)
@@ -913,7 +920,7 @@ def bench_kfmatch(ctx, Bs, dev, view, sets, with_cpu):
                                            sc, s2, pairs[f]["F12"], 0, 1)
                 sel = pkf == f + 1
                 O.fuse(kd[f + 1]["kps"], kd[f + 1]["desc"], kd[f + 1]["ur"], g,
-                       Tr[f + 1][:3, :3].reshape(-1), Tr[f + 1][:3, 3], kfs_r[f + 1]["Ow"],
+                       Tr[f + 1][:3, :3].reshape(-1), Tr[f + 1][:3, 3], kfs[f + 1]["Ow"],
                        S.KITTI_CAM, sc, isg,
                        float(lv.log_scale_factor), pts[sel], 3.0)
             return per
@@ -965,11 +972,12 @@ def cpu_baseline(Ls, Rs, n_frames):
     D = len(Ls)
 
     def search(f, kl, dl, ur, prev):
-        q, lmp, lout, xyz, md, nobs = scenario.vo_queries(prev[0], prev[1], prev[2], prev[3])
-        p = scenario.pose(f)
+        q, lmp, lout, xyz, md, nobs = scenario.vo_queries(prev[0], prev[1], prev[2], prev[3],
+                                                          layered=True)
+        p = scenario.pose(f, layered=True, t_last=prev[3])
         mp = np.full(len(kl), -1, np.int32)
         O.search_frame(t, g, kl, dl, ur, mp, prev[0], lmp, lout, xyz, md, nobs,
-                       p["Rcw"][0].reshape(3, 3), p["tcw"][0], 0.0,
+                       p["Rcw"][0].reshape(3, 3), p["tcw"][0], float(p["tlc_z"][0]),
                        float(p["baseline"][0]), cam, 7.0, 0, 1)
 
     def run(tid):

@@ -104,6 +104,88 @@ def sequence(seed: int, n: int, cols: int = KITTI_COLS, rows: int = KITTI_ROWS):
     return L, R
 
 
+# ---- the bench's KITTI-like sequence ---------------------------------------------------------
+# 200-320 fronto-parallel surfaces (side 30-220 x 20-160 px at frame 0, one disparity each,
+# U[3, 50] px), each carrying 4-12 small patches (3-24 px) at its own depth, over a U[60, 200]
+# background, N(0, 3) noise per view. Corners mostly lie INSIDE a surface (patch corners), so
+# the right view sees them unchanged, as on KITTI's textured road and facades: ~45-50 % of the
+# left keypoints get stereo depth (the rectangles scene above: ~17 %), ~950 frame-to-frame
+# queries and ~700 matches per frame. The camera moves forward FORWARD_M per frame and turns as
+# rotation(t) (about 3 px / -1 px of image motion and 0.5 deg of roll), so near surfaces grow
+# and move faster than far ones (parallax), as in SURVEY.md section 8(d)'s motion model.
+FORWARD_M = 0.3
+
+
+def camera_center(t: int) -> np.ndarray:
+    return np.array([0.0, 0.0, FORWARD_M * t])
+
+
+def layered_pose(t: int):
+    """(Rcw, tcw) of frame t of layered_sequence: Rcw = rotation(t), tcw = -Rcw C(t)."""
+    R = rotation(t)
+    return R, -R @ camera_center(t)
+
+
+def _layered_scene(rng: np.random.Generator, cols: int, rows: int):
+    items = []  # (x, y, w, h, val, disparity, surface, patch index)
+    ns = int(rng.integers(200, 321))
+    for i in range(ns):
+        w, h = int(rng.integers(30, 220)), int(rng.integers(20, 160))
+        x, y = int(rng.integers(-60, cols)), int(rng.integers(-40, rows))
+        d = float(rng.uniform(3.0, 50.0))
+        items.append((x, y, w, h, int(rng.integers(0, 256)), d, i, 0))
+        for j in range(int(rng.integers(4, 13))):
+            pw = int(rng.integers(3, max(4, min(24, w // 2))))
+            ph = int(rng.integers(3, max(4, min(24, h // 2))))
+            px = x + int(rng.integers(0, max(1, w - pw)))
+            py = y + int(rng.integers(0, max(1, h - ph)))
+            items.append((px, py, pw, ph, int(rng.integers(0, 256)), d, i, j + 1))
+    return int(rng.integers(60, 201)), items
+
+
+def layered_pair(seed: int, t: int = 0, cols: int = KITTI_COLS, rows: int = KITTI_ROWS):
+    """Left/right u8 images of frame t of the layered scene `seed` (pose layered_pose(t))."""
+    rng = np.random.Generator(np.random.PCG64([seed, 23]))
+    bg, items = _layered_scene(rng, cols, rows)
+    fx, fy, cx0, cy0, bf = KITTI_CAM
+    R, C = rotation(t), camera_center(t)
+    draw = []
+    for (x, y, w, h, val, d, surf, j) in items:
+        z0 = bf / d
+        cx, cy = x + 0.5 * w, y + 0.5 * h
+        Xw = np.array([(cx - cx0) * z0 / fx, (cy - cy0) * z0 / fy, z0])
+        Xc = R @ (Xw - C)
+        if Xc[2] < 1.0:
+            continue
+        sc = z0 / Xc[2]
+        u, v = fx * Xc[0] / Xc[2] + cx0, fy * Xc[1] / Xc[2] + cy0
+        draw.append((bf / Xc[2], surf, j, u, v, w * sc, h * sc, val))
+    draw.sort(key=lambda e: (e[0], e[1], e[2]))  # far to near; a surface before its patches
+    noise = np.random.Generator(np.random.PCG64([seed, t, 29]))
+    out = []
+    for right in (False, True):
+        img = np.full((rows, cols), float(bg), dtype=np.float32)
+        for (disp, _, _, u, v, w, h, val) in draw:
+            x0 = int(round(u - (disp if right else 0.0) - 0.5 * w))
+            y0 = int(round(v - 0.5 * h))
+            x1, y1 = max(0, x0), max(0, y0)
+            x2, y2 = min(cols, x0 + max(1, int(round(w)))), min(rows, y0 + max(1, int(round(h))))
+            if x1 < x2 and y1 < y2:
+                img[y1:y2, x1:x2] = val
+        img += noise.normal(0.0, 3.0, size=img.shape).astype(np.float32)
+        out.append(np.clip(np.rint(img), 0, 255).astype(np.uint8))
+    return out[0], out[1]
+
+
+def layered_sequence(seed: int, n: int, cols: int = KITTI_COLS, rows: int = KITTI_ROWS):
+    """n consecutive stereo frames of the layered scene: (left[n], right[n])."""
+    L = np.empty((n, rows, cols), np.uint8)
+    R = np.empty_like(L)
+    for t in range(n):
+        L[t], R[t] = layered_pair(seed, t, cols, rows)
+    return L, R
+
+
 def _rodrigues(w: np.ndarray) -> np.ndarray:
     th = float(np.linalg.norm(w))
     if th == 0.0:

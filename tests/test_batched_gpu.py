@@ -23,10 +23,18 @@ CAM = S.KITTI_CAM
 COLS, ROWS, PITCH = S.KITTI_COLS, S.KITTI_ROWS, 1280
 
 
-def _poses(G, B, t_of):
+def _poses(G, B, t_of, layered=False):
     poses = np.zeros(B, G.F2F_POSE_DTYPE)
     for f in range(B):
-        poses["Rcw"][f] = S.rotation(t_of(f)).astype(np.float32).reshape(-1)
+        if layered:  # rotation + forward motion (synthetic.layered_pose); tlc_z vs frame f - 1
+            t, tl = t_of(f), t_of(f - 1) if f else t_of(f)
+            R, tc = S.layered_pose(t)
+            poses["Rcw"][f] = R.astype(np.float32).reshape(-1)
+            poses["tcw"][f] = tc.astype(np.float32)
+            poses["tlc_z"][f] = np.float32((S.rotation(tl) @ (S.camera_center(t) -
+                                                              S.camera_center(tl)))[2])
+        else:
+            poses["Rcw"][f] = S.rotation(t_of(f)).astype(np.float32).reshape(-1)
     poses["baseline"] = np.float32(CAM[4]) / np.float32(CAM[0])
     poses["th"] = 7.0
     poses["check_ori"] = 1
@@ -58,7 +66,7 @@ class _Part:
                                                    Bs, s)
 
 
-def run_batch(G, L, R, t_of, n_parts=1):
+def run_batch(G, L, R, t_of, n_parts=1, layered=False):
     """Two back-to-back device steps over the batch, split over n_parts contexts on their own
     streams (each part's first frame is the halo of its second, as in bench.py)."""
     import torch
@@ -68,7 +76,7 @@ def run_batch(G, L, R, t_of, n_parts=1):
     hr = np.zeros((B, ROWS, PITCH), np.uint8)
     hl[:, :, :COLS] = L
     hr[:, :, :COLS] = R
-    poses = _poses(G, B, t_of)
+    poses = _poses(G, B, t_of, layered)
     Bs = B // n_parts
     main = torch.cuda.Stream(device=dev)
     streams = [main] + [torch.cuda.Stream(device=dev) for _ in range(n_parts - 1)]
@@ -144,8 +152,9 @@ def check_frames(G, oracle, parts, poses, L, R, frames):
         mp_o = np.full(len(kl), -1, np.int32)
         nm_o = oracle.search_frame(t, g, kl, dl, ur, mp_o, pkl, last_mp,
                                    np.zeros(n_last, np.uint8), xyz, mdesc, nobs,
-                                   poses["Rcw"][f].reshape(3, 3), poses["tcw"][f], 0.0,
-                                   float(poses["baseline"][f]), CAM, 7.0, 0, 1)
+                                   poses["Rcw"][f].reshape(3, 3), poses["tcw"][f],
+                                   float(poses["tlc_z"][f]), float(poses["baseline"][f]), CAM,
+                                   7.0, 0, 1)
         assert nm_all[i] == nm_o, f"frame {f}"
         np.testing.assert_array_equal(p.mp.cpu().numpy()[i * kc:i * kc + len(kl)], mp_o)
         total += nm_o
@@ -158,6 +167,16 @@ def test_batched_device_path_matches_oracle(oracle, gpu_lib, B):
     parts, poses = run_batch(gpu_lib, L, R, lambda f: f)
     total = check_frames(gpu_lib, oracle, parts, poses, L, R, range(B))
     assert total > 100, "scenario should produce real frame-to-frame matches"
+
+
+def test_layered_scene_with_forward_motion(oracle, gpu_lib):
+    """The bench's scene (synthetic.layered_sequence: ~50 % stereo yield, turning + 0.3 m/frame
+    forward, so the queries' map points are unprojected with a translation) in an 8-frame batch."""
+    B = 8
+    L, R = S.layered_sequence(1000, B)
+    parts, poses = run_batch(gpu_lib, L, R, lambda f: f, layered=True)
+    total = check_frames(gpu_lib, oracle, parts, poses, L, R, range(B))
+    assert total > 500 * (B - 1), "the layered scene should give ~700-800 matches per frame"
 
 
 def test_batch64_spread_frames(oracle, gpu_lib):
