@@ -111,6 +111,9 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--streams", type=int, default=1,
                     help="split each step's batch over this many contexts on their own HIP streams")
+    ap.add_argument("--inflight", type=int, default=int(os.environ.get("SLAMGPU_INFLIGHT", "2")),
+                    help="batches in flight: consecutive steps alternate between this many "
+                         "context groups, each on its own streams")
     ap.add_argument("--no-optimizer", action="store_true",
                     help="skip the PoseOptimization / LocalBundleAdjustment measurements")
     ap.add_argument("--no-bow", action="store_true",
@@ -182,39 +185,54 @@ def main():
 
     # NS contexts, each with its own HIP stream and Bs consecutive frames of the batch (its first
     # frame is the halo of its second): the launches of one half fill the other's tails.
-    ctxs = [G.Context(cols, rows, 2000, 1.2, 8, 20, 7, max_frames=Bs, device=local)
-            for _ in range(NS)]
+    # INF groups of them take the steps in turn, each group on streams of its own, so up to INF
+    # batches are in flight: the matcher tail of step k (latency-bound: one wave per frame in
+    # search_resolve) runs beside the pyramid of step k + 1.
+    INF = max(1, args.inflight)
+    groups = []
+    for gi in range(INF):
+        g_ctxs = [G.Context(cols, rows, 2000, 1.2, 8, 20, 7, max_frames=Bs, device=local)
+                  for _ in range(NS)]
+        g_streams = [torch.cuda.Stream(device=dev) for _ in range(NS)]
+        g_parts = []
+        kc_ = g_ctxs[0].kp_cap
+        for si in range(NS):
+            g_parts.append({
+                "q": torch.empty(Bs * kc_ * G.F2F_QUERY_DTYPE.itemsize, dtype=torch.uint8,
+                                 device=dev),
+                "qs": torch.empty(Bs, dtype=torch.int32, device=dev),
+                "qc": torch.empty(Bs, dtype=torch.int32, device=dev),
+                "mp": torch.empty(Bs * kc_, dtype=torch.int32, device=dev),
+                "blk": torch.empty(Bs * kc_, dtype=torch.uint8, device=dev),
+                "nm": torch.empty(Bs, dtype=torch.int32, device=dev),
+                "poses": d_poses[si * Bs * G.F2F_POSE_DTYPE.itemsize:
+                                 (si + 1) * Bs * G.F2F_POSE_DTYPE.itemsize]})
+        groups.append((g_ctxs, g_streams, g_parts))
+    ctxs, _, parts = groups[0]
     ctx = ctxs[0]
     kc = ctx.kp_cap
-    main = torch.cuda.current_stream()
-    streams = [main] + [torch.cuda.Stream(device=dev) for _ in range(NS - 1)]
-    parts = []
-    for si in range(NS):
-        parts.append({
-            "q": torch.empty(Bs * kc * G.F2F_QUERY_DTYPE.itemsize, dtype=torch.uint8, device=dev),
-            "qs": torch.empty(Bs, dtype=torch.int32, device=dev),
-            "qc": torch.empty(Bs, dtype=torch.int32, device=dev),
-            "mp": torch.empty(Bs * kc, dtype=torch.int32, device=dev),
-            "blk": torch.empty(Bs * kc, dtype=torch.uint8, device=dev),
-            "nm": torch.empty(Bs, dtype=torch.int32, device=dev),
-            "poses": d_poses[si * Bs * G.F2F_POSE_DTYPE.itemsize:
-                             (si + 1) * Bs * G.F2F_POSE_DTYPE.itemsize]})
 
     # per-frame results of the owned frames -> rank 0 (world > 1 only)
     rec_b = ctx.record_bytes
     # (SLAMGPU_BENCH_GATHER=1 runs the pack + gather path at world 1 too, as a local copy)
     gat = SD.FrameGather({"frontend": rec_b, "map_point": kc * 4, "nmatches": 4}, F, dev) \
         if world > 1 or os.environ.get("SLAMGPU_BENCH_GATHER") == "1" else None
+    k_step = [0]
 
-    def step():
-        if gat is not None:
-            gat.begin()
+    def step(group=None):
+        gi = k_step[0] % INF if group is None else group
+        k_step[0] += 1
+        g_ctxs, g_streams, g_parts = groups[gi]
+        gmain = g_streams[0]
+        with torch.cuda.stream(gmain):
+            if gat is not None:
+                gat.begin()
         for si in range(NS):
-            st_ = streams[si]
+            st_ = g_streams[si]
             if si:
-                st_.wait_stream(main)
+                st_.wait_stream(gmain)
             with torch.cuda.stream(st_):
-                c, pt, h = ctxs[si], parts[si], st_.cuda_stream
+                c, pt, h = g_ctxs[si], g_parts[si], st_.cuda_stream
                 off = si * Bs * stride
                 c.frontend_device(int(d_l.data_ptr()) + off, int(d_r.data_ptr()) + off, stride,
                                   pitch, Bs, cam, h)
@@ -232,15 +250,17 @@ def main():
                     gat.slab("nmatches")[o:o + Bs - 1].view(-1).copy_(
                         pt["nm"][1:].view(torch.uint8))
         for si in range(1, NS):
-            main.wait_stream(streams[si])
+            gmain.wait_stream(g_streams[si])
         if gat is not None:
-            gat.start()
+            with torch.cuda.stream(gmain):
+                gat.start()
 
-    for _ in range(max(1, args.warmup)):
+    for _ in range(max(1, args.warmup) * INF):
         step()
     torch.cuda.synchronize()
-    for c in ctxs:
-        c.sync()
+    for gc in groups:
+        for c in gc[0]:
+            c.sync()
     # sanity of what the timed steps compute (not timed)
     nk = np.array([ctx.keypoints(i)[0].shape[0] for i in range(min(4, 2 * Bs))])
     nm = np.concatenate([pt["nm"].cpu().numpy() for pt in parts])
@@ -252,8 +272,9 @@ def main():
     names = ["pyr_down", "blur7", "blur7_edges", "fast_cells", "octree", "octree_global", "orient_desc", "stereo_rows",
              "stereo_match", "stereo_median", "grid_build", "vo_queries", "search_cand",
              "search_resolve"]
+    torch.cuda.synchronize()
     ctx.timing_start("*", 4096)
-    step()
+    step(group=0)
     ctx.timing_stop()
     brk = {n: ctx.timing_read(n) for n in names}
     tot = sum(v[0] for v in brk.values())
@@ -277,8 +298,9 @@ def main():
         dist.barrier()
     t1 = time.perf_counter()
     ctx.timing_stop()
-    for c in ctxs:
-        c.sync()
+    for gc in groups:
+        for c in gc[0]:
+            c.sync()
     elapsed = SD.max_over_ranks(t1 - t0, dev)
     dom_ms, dom_n = ctx.timing_read(dominant)
     # per-rank result summary gathered to every rank (validation, outside the timed region)
@@ -348,6 +370,7 @@ def main():
             "config": {"workload": "configs[1]: synthetic 1241x376 stereo stream, 2000 kp/frame, "
                                    "extract L+R + stereo match + frame-to-frame match",
                        "frames_per_gpu_per_step": NS * (Bs - 1), "batch": B, "streams": NS,
+                       "batches_in_flight": INF,
                        "nfeatures": 2000,
                        "nlevels": 8, "scale_factor": 1.2, "fast_th": [20, 7],
                        "parallelism": f"frame-sharded x{world}" + (
