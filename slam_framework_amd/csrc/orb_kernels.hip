@@ -549,6 +549,11 @@ __global__ __launch_bounds__(64 * kCellWaves, FAST_MINW) void fast_cells_kernel(
   const uint4 my_desc = lane < nc ? reinterpret_cast<const uint4*>(cells)[c0 + lane]
                                   : make_uint4(0, 0, 0, 0);
   const int in_pitch = __builtin_amdgcn_readfirstlane(b.in_pitch);
+  // configuration scalars read once (the stores below would otherwise make the compiler reload
+  // them inside the NMS loop, each behind a scalar-load wait)
+  const int cell_cap = __builtin_amdgcn_readfirstlane(g->cell_cap);
+  const int ini_th = __builtin_amdgcn_readfirstlane(g->ini_th);
+  const int min_th = __builtin_amdgcn_readfirstlane(g->min_th);
   const int tile_bytes = (kTileStride * g->fast_tile_rows + 15) & ~15;
   uint8_t* tile0 = s_fast + wid * g->fast_lds_per_wave;
   uint8_t* sc = tile0 + (GLDS ? 2 : 1) * tile_bytes;
@@ -656,28 +661,30 @@ __global__ __launch_bounds__(64 * kCellWaves, FAST_MINW) void fast_cells_kernel(
     }
     const int off = v.off;
     const int dh = v.vh - 6, dw = v.vw - 6;  // detect area [3, vh-3) x [3, vw-3)
-    // ---- score map: rows -1 .. dh of the detect area, all zero (a zero frame around the detect
-    // area lets the NMS read 3x3 neighbourhoods without bounds checks); sc1 = row 0.
+    // ---- score map: rows -1 .. dh of the detect area, zeroed before each pass's scores (a zero
+    // frame around the detect area lets the NMS read 3x3 neighbourhoods without bounds checks);
+    // sc1 = row 0. Until then the pass keeps its prefilter records in the same bytes.
     uint8_t* sc1 = sc + kScoreStride;
-#pragma unroll 4
-    for (int rz = plr - 1; rz <= dh; rz += kRps)
-      *reinterpret_cast<uint32_t*>(sc1 + rz * kScoreStride + 4 * pld) = 0;
+    uint32_t* const recs = reinterpret_cast<uint32_t*>(sc);
     // ---- one FAST pass at threshold th: prefilter every detect pixel (4 pixels, one tile dword,
-    // per lane; survivors compacted in row-major order), exact score of the survivors into the
-    // score map, NMS at th, survivors out in row-major order. The score map keeps the scores of
-    // earlier passes (same values: s does not depend on the threshold).
+    // per lane), exact score of the survivors into the score map, NMS at th, survivors out in
+    // row-major order.
     // Detect pixel (rr, col): tile row rr + 3, tile column col in [off + 3, off + 3 + dw).
     const int q_lo = (off + 3) >> 2, q_hi = (off + 2 + dw) >> 2;
     const int nq = q_hi - q_lo + 1;
-    const int rows_per = 64 / nq;
-    const int lr = lane / nq, Q = q_lo + (lane - lr * nq);
+    // lane / nq by a reciprocal (exact for lane < 64, nq < 64): no integer division
+    const int inv_nq = (int)ceilf(4096.0f / (float)nq);
+    const int rows_per = (64 * inv_nq) >> 12;
+    const int lr = (lane * inv_nq) >> 12, Q = q_lo + (lane - lr * nq);
     const int blo = max(0, off + 3 - 4 * Q), bhi = min(4, off + 3 + dw - 4 * Q);
     const uint32_t vmask =
         (uint32_t)(((1ull << (8 * bhi)) - 1) & ~((1ull << (8 * blo)) - 1)) & kH;
     const int qm = max(Q - 1, 0) - Q;  // dword step left (clamped at the tile edge)
-    uint32_t* out = cell_keys + slot * g->cell_cap;
+    uint32_t* out = cell_keys + slot * cell_cap;
     auto fast_pass = [&](int th) -> int {
-      int ncand = 0;
+      // prefilter: a lane with any surviving pixel appends one record (its tile dword's pixel
+      // index | 4-bit survivor mask << 16); records come out in row-major order (row, dword)
+      int nrec = 0;
       for (int r0 = 0; r0 < dh; r0 += rows_per) {
         const int rr = r0 + lr;
         uint32_t m = 0;
@@ -735,16 +742,36 @@ __global__ __launch_bounds__(64 * kCellWaves, FAST_MINW) void fast_cells_kernel(
           m = ((((any[0] + 0x7fff7fffu) & 0x80008000u) >> 8) | ((any[1] + 0x7fff7fffu) & 0x80008000u)) &
               vmask;
         }
-        // row-major compaction: exclusive prefix of per-lane counts (0..4) via 3 ballots
-        const int cnt = __popc(m);
+        const uint64_t act = __ballot(m != 0);
+        if (m) {  // bits 7, 15, 23, 31 -> bits 16..19
+          const uint32_t bits = ((m >> 7) & 1u) | ((m >> 14) & 2u) | ((m >> 21) & 4u) |
+                                ((m >> 28) & 8u);
+          recs[nrec + lanes_below(act)] = (uint32_t)(rr * kScoreStride + 4 * Q) | bits << 16;
+        }
+        nrec += __popcll(act);
+      }
+      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      // records -> one candidate per surviving pixel, row-major (exclusive prefix of the
+      // per-record counts via 3 ballots)
+      int ncand = 0;
+      for (int i0 = 0; i0 < nrec; i0 += 64) {
+        const int i = i0 + lane;
+        const uint32_t rec = i < nrec ? recs[i] : 0u;
+        const int cnt = __popc(rec >> 16);
         const uint64_t b0 = __ballot(cnt & 1), b1 = __ballot(cnt & 2), b2 = __ballot(cnt & 4);
         int pos = ncand + lanes_below(b0) + 2 * lanes_below(b1) + 4 * lanes_below(b2);
-        const int pix0 = rr * kScoreStride + 4 * Q;
+        const uint32_t pix0 = rec & 0xffffu;
 #pragma unroll
         for (int bb = 0; bb < 4; bb++)
-          if (m & (0x80u << (8 * bb))) cand[pos++] = (uint16_t)(pix0 + bb);
+          if (rec & (0x10000u << bb)) cand[pos++] = (uint16_t)(pix0 + bb);
         ncand += __popcll(b0) + 2 * __popcll(b1) + 4 * __popcll(b2);
       }
+      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+#pragma unroll 4
+      for (int rz = plr - 1; rz <= dh; rz += kRps)
+        *reinterpret_cast<uint32_t*>(sc1 + rz * kScoreStride + 4 * pld) = 0;
       __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
       __builtin_amdgcn_wave_barrier();
       // exact FAST score of the survivors
@@ -759,7 +786,8 @@ __global__ __launch_bounds__(64 * kCellWaves, FAST_MINW) void fast_cells_kernel(
       // NMS at th: cv::FAST keeps p iff s - 1 > ns for all 8 neighbours, ns = (q > th ? q - 1 :
       // 0), zero outside the detect area. With Q = max of the 8 neighbours' s that is
       //   s > th  &&  s >= 2  &&  Q < max(s, th + 1),
-      // and a neighbour this pass did not score has s <= th < s_p, so it cannot change the test.
+      // and a neighbour this pass did not score has s <= th < s_p (the pre-test is necessary),
+      // so it cannot change the test.
       int count = 0;
       for (int i0 = 0; i0 < ncand; i0 += 64) {
         const int i = i0 + lane;
@@ -785,7 +813,7 @@ __global__ __launch_bounds__(64 * kCellWaves, FAST_MINW) void fast_cells_kernel(
         const uint64_t mk = __ballot(keep);
         if (keep) {
           const int pos = count + lanes_below(mk);
-          if (pos < g->cell_cap) out[pos] = pack_key(v.ax + cc - kMinBorder, v.ini_y + 3 + r - kMinBorder, sv - 1);
+          if (pos < cell_cap) out[pos] = pack_key(v.ax + cc - kMinBorder, v.ini_y + 3 + r - kMinBorder, sv - 1);
         }
         count += __popcll(mk);
       }
@@ -793,16 +821,16 @@ __global__ __launch_bounds__(64 * kCellWaves, FAST_MINW) void fast_cells_kernel(
     };
     // FAST at iniTh; the reference re-runs the whole cell at minTh when the iniTh output (after
     // NMS) is empty (:753-757)
-    int count = fast_pass(g->ini_th);
+    int count = fast_pass(ini_th);
     if (count == 0) {
       __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
       __builtin_amdgcn_wave_barrier();
-      count = fast_pass(g->min_th);
+      count = fast_pass(min_th);
     }
     if (lane == 0) {
-      if (count > g->cell_cap) {
+      if (count > cell_cap) {
         atomicOr(err, kErrCellOverflow);
-        count = g->cell_cap;
+        count = cell_cap;
       }
       cell_count[slot] = count;
     }
