@@ -53,7 +53,8 @@ typedef struct {
 } slamgpu_orb_params;
 
 /* Pinhole stereo camera as the Frame sees it (tracker.cpp:29-70): K entries and bf. Image
- * bounds are 0..cols x 0..rows (k1 == 0, Frame::ComputeImageBounds frame.cpp:678-703). */
+ * bounds are 0..cols x 0..rows, or the undistorted corners once slamgpu_set_distortion gave a
+ * DistCoef with k1 != 0 (Frame::ComputeImageBounds frame.cpp:644-675). */
 typedef struct {
   float fx, fy, cx, cy, bf;
 } slamgpu_camera;
@@ -125,8 +126,33 @@ typedef struct {
   const float* u_right;        /* [max_frames][kp_cap]          */
   const float* depth;          /* [max_frames][kp_cap]          */
   int kp_cap;
+  const slamgpu_keypoint* kps_un; /* [2 * max_frames][kp_cap]: undistorted left views (= kps
+                                     when k1 == 0; right-view slots unused)                   */
 } slamgpu_device_view;
 int slamgpu_device_results(const slamgpu_ctx* ctx, slamgpu_device_view* out);
+
+/* ---- Frame: distortion (Frame::UndistortKeyPoints / ComputeImageBounds) ------------------ */
+/* Sets the Frame's DistCoef (tracker.cpp:41-51: k1 k2 p1 p2 [k3]; n = 4 or 5, n = 0 clears).
+ * With k1 != 0 every following frame call undistorts the left keypoints on the device after
+ * ComputeStereoMatches (frame.cpp:96, :614-641), and the grid, the projection searches and
+ * slamgpu_make_vo_queries_device read the undistorted keypoints (undistorted_keypoints_), the
+ * image bounds are the undistorted corners. k1 == 0 is the reference's identity case. */
+int slamgpu_set_distortion(slamgpu_ctx* ctx, const float* dist_coef, int n);
+/* Replaces cv::undistortPoints(src, dst, K, DistCoef, noArray(), K) as the reference calls it
+ * (frame.cpp:630, :659; OpenCV 3.3.1 semantics, undistort.h). Host, pure; n = 0: copy. */
+int slamgpu_undistort_points(const slamgpu_camera* cam, const float* dist_coef, int n,
+                             const float* xy_in, float* xy_out, int n_points);
+/* Batched device Frame::UndistortKeyPoints: set f's d_counts[f * counts_stride] keypoints at
+ * d_in + f * in_stride -> d_out + f * out_stride (pt undistorted, other fields copied; k1 == 0
+ * copies). max_kps >= every count. Asynchronous on `stream`. */
+int slamgpu_undistort_keypoints_device(const slamgpu_camera* cam, const float* dist_coef, int n,
+                                       const slamgpu_keypoint* d_in, int64_t in_stride,
+                                       const int* d_counts, int counts_stride,
+                                       slamgpu_keypoint* d_out, int64_t out_stride, int n_sets,
+                                       int max_kps, void* stream);
+/* Frame f's undistorted left keypoints (GetUndistortedKeys) of the last frame/frontend call. */
+int slamgpu_download_undistorted_keypoints(slamgpu_ctx* ctx, int frame, slamgpu_keypoint* kps,
+                                           int cap, int* n_out);
 
 /* Per-frame result record of the last frontend call, for gathering a frame-sharded job's
  * results to one rank (the stereo Frame ctor's outputs, frame.cpp:61-111 --

@@ -422,3 +422,68 @@ int oc_search_by_projection_mps(const oc_grid_geom* g, const oc_orb_tables* t,
   free(cand);
   return nmatches;
 }
+
+/* ---- Frame::UndistortKeyPoints / ComputeImageBounds ------------------------------------------ */
+/* OpenCV 3.3.1 cvUndistortPoints (imgproc/src/undistort.cpp) for the reference's call
+ * cv::undistortPoints(mat, mat, K, DistCoef, cv::Mat(), K) (frame.cpp:630, :659): K and the
+ * coefficients converted to double (k[14], unset entries 0); iters = 5 because D is given; the
+ * tilt matrix for tau = 0 is the identity; RR = P * R = K * I. Evaluation order as written there
+ * (left to right, no contraction: this file is built -ffp-contract=off). */
+void oc_undistort_points(const float cam[4], const float* dist, int ndist, const float* xy_in,
+                         float* xy_out, int n) {
+  double k[14] = {0};
+  for (int i = 0; i < ndist && i < 14; i++) k[i] = (double)dist[i];
+  const double A00 = cam[0], A11 = cam[1], A02 = cam[2], A12 = cam[3];
+  const double fx = A00, fy = A11, ifx = 1. / fx, ify = 1. / fy, cx = A02, cy = A12;
+  /* RR = PP * I (cvMatMul of the 3x3 K with the identity): rows (fx 0 cx) (0 fy cy) (0 0 1) */
+  const double RR[3][3] = {{A00, 0., A02}, {0., A11, A12}, {0., 0., 1.}};
+  for (int i = 0; i < n; i++) {
+    double x = xy_in[2 * i], y = xy_in[2 * i + 1], x0, y0;
+    x = (x - cx) * ifx;
+    y = (y - cy) * ify;
+    /* tilt compensation: vecUntilt = I * (x, y, 1), invProj = 1 */
+    x0 = x;
+    y0 = y;
+    for (int j = 0; j < 5; j++) {
+      double r2 = x * x + y * y;
+      double icdist = (1 + ((k[7] * r2 + k[6]) * r2 + k[5]) * r2) /
+                      (1 + ((k[4] * r2 + k[1]) * r2 + k[0]) * r2);
+      double deltaX = 2 * k[2] * x * y + k[3] * (r2 + 2 * x * x) + k[8] * r2 + k[9] * r2 * r2;
+      double deltaY = k[2] * (r2 + 2 * y * y) + 2 * k[3] * x * y + k[10] * r2 + k[11] * r2 * r2;
+      x = (x0 - deltaX) * icdist;
+      y = (y0 - deltaY) * icdist;
+    }
+    double xx = RR[0][0] * x + RR[0][1] * y + RR[0][2];
+    double yy = RR[1][0] * x + RR[1][1] * y + RR[1][2];
+    double ww = 1. / (RR[2][0] * x + RR[2][1] * y + RR[2][2]);
+    xy_out[2 * i] = (float)(xx * ww);
+    xy_out[2 * i + 1] = (float)(yy * ww);
+  }
+}
+
+void oc_undistort_keypoints(const float cam[4], const float* dist, int ndist,
+                            const oc_keypoint* in, oc_keypoint* out, int n) {
+  for (int i = 0; i < n; i++) out[i] = in[i];
+  if (dist[0] == 0.0f) return; /* frame.cpp:616-619 */
+  for (int i = 0; i < n; i++) {
+    float p[2] = {in[i].x, in[i].y};
+    oc_undistort_points(cam, dist, ndist, p, p, 1);
+    out[i].x = p[0];
+    out[i].y = p[1];
+  }
+}
+
+void oc_grid_geom_init_dist(oc_grid_geom* g, int cols, int rows, const float cam[4],
+                            const float* dist, int ndist) {
+  oc_grid_geom_init(g, cols, rows);
+  if (dist[0] != 0.0) { /* frame.cpp:646-667: corners (0,0) (cols,0) (0,rows) (cols,rows) */
+    float m[8] = {0.0f, 0.0f, (float)cols, 0.0f, 0.0f, (float)rows, (float)cols, (float)rows};
+    oc_undistort_points(cam, dist, ndist, m, m, 4);
+    g->min_x = fminf(m[0], m[4]);
+    g->max_x = fmaxf(m[2], m[6]);
+    g->min_y = fminf(m[1], m[3]);
+    g->max_y = fmaxf(m[5], m[7]);
+    g->cell_w = (float)(g->max_x - g->min_x) / (GRID_COLS);
+    g->cell_h = (float)(g->max_y - g->min_y) / (GRID_ROWS);
+  }
+}

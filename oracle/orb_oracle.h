@@ -125,6 +125,17 @@ typedef struct {
   float cell_w, cell_h; /* grid_element_width_/height_ */
 } oc_grid_geom;
 void oc_grid_geom_init(oc_grid_geom* g, int cols, int rows);
+/* Frame::ComputeImageBounds (frame.cpp:644-675) with DistCoef dist[ndist] (ndist 4 or 5): the
+ * undistorted image corners when dist[0] != 0, else 0..cols x 0..rows; then the grid cell size. */
+void oc_grid_geom_init_dist(oc_grid_geom* g, int cols, int rows, const float cam[4],
+                            const float* dist, int ndist);
+/* cv::undistortPoints(src, dst, K, D, noArray(), K) on n CV_32FC2 points (OpenCV 3.3.1
+ * cvUndistortPoints); cam = fx, fy, cx, cy (f32 K), dist = k1 k2 p1 p2 [k3]. In place allowed. */
+void oc_undistort_points(const float cam[4], const float* dist, int ndist, const float* xy_in,
+                         float* xy_out, int n);
+/* Frame::UndistortKeyPoints (frame.cpp:614-641): copies when dist[0] == 0, else undistorts pt. */
+void oc_undistort_keypoints(const float cam[4], const float* dist, int ndist,
+                            const oc_keypoint* in, oc_keypoint* out, int n);
 /* Frame::GetFeaturesInArea; returns count (<= cap written), reference order. */
 int oc_features_in_area(const oc_grid_geom* g, const oc_keypoint* kps, int n, float x, float y,
                         float r, int min_level, int max_level, int* out, int cap);

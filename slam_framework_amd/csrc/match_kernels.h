@@ -42,6 +42,12 @@ struct StereoOut {
 void launch_stereo(const ImageBatch& b, const OrbGeomDev& g, const Camera& cam, int n_frames,
                    const StereoWorkspace& ws, const StereoOut& out, hipStream_t st);
 
+// Frame::UndistortKeyPoints of n_sets keypoint sets (set f: src.kps + f * src.stride, count
+// src.n[f * src.n_stride]) into dst + f * dst_stride.
+struct Distortion;
+void launch_undistort(const FrameKps& src, KeyPoint* dst, int64_t dst_stride, const Camera& cam,
+                      const Distortion& dc, int n_sets, int kp_cap, hipStream_t st);
+
 // Per-frame keypoint grid (AssignFeaturesToGrid), CSR over the 64x48 cells.
 struct GridWorkspace {
   int* cell_start;     // [frame][kGridCells + 1]

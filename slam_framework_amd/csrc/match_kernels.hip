@@ -17,6 +17,7 @@
 #include "device_math.h"
 #include "timing.h"
 #include "match_kernels.h"
+#include "undistort.h"
 
 namespace slamgpu {
 
@@ -379,6 +380,26 @@ __global__ __launch_bounds__(256) void grid_build_kernel(FrameKps cur, Camera ca
 void launch_grid(const FrameKps& cur, const Camera& cam, int n_frames, int kp_cap,
                  const GridWorkspace& gw, hipStream_t st) {
   SLAMGPU_LAUNCH("grid_build", st, grid_build_kernel, dim3(n_frames), dim3(256), 0, st, cur, cam, kp_cap, gw);
+}
+
+// ---------------------------------------------------------------------------------------
+// Frame::UndistortKeyPoints (frame.cpp:614-641): a thread per keypoint of every set, the
+// keypoint copied with pt replaced by cv::undistortPoints (undistort.h; IEEE double, no
+// contraction, bit-identical to the oracle). dist k1 == 0 copies (:616-619).
+__global__ __launch_bounds__(256) void undistort_kernel(FrameKps src, KeyPoint* __restrict__ dst,
+                                                        int64_t dst_stride, float fx, float fy,
+                                                        float cx, float cy, Distortion dc) {
+  const int f = blockIdx.y, i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= src.n[f * src.n_stride]) return;
+  KeyPoint kp = src.kps[f * src.stride + i];
+  if (dc.k[0] != 0.0f) undistort_point(fx, fy, cx, cy, dc, kp.x, kp.y, &kp.x, &kp.y);
+  dst[f * dst_stride + i] = kp;
+}
+
+void launch_undistort(const FrameKps& src, KeyPoint* dst, int64_t dst_stride, const Camera& cam,
+                      const Distortion& dc, int n_sets, int kp_cap, hipStream_t st) {
+  SLAMGPU_LAUNCH("undistort", st, undistort_kernel, dim3((kp_cap + 255) / 256, n_sets), dim3(256),
+                 0, st, src, dst, dst_stride, cam.fx, cam.fy, cam.cx, cam.cy, dc);
 }
 
 // ---------------------------------------------------------------------------------------

@@ -17,6 +17,7 @@
 
 #include "../../include/slamgpu.h"
 #include "match_kernels.h"
+#include "undistort.h"
 #include "orb_kernels.h"
 #include "orb_tables.h"
 #include "timing.h"
@@ -51,6 +52,12 @@ struct slamgpu_ctx {
   int n_frames_last = 0, n_images_last = 0;
   Camera cam{};
   bool have_cam = false;
+  // Frame::dist_coeff_ (k1 k2 p1 p2 k3); with k1 != 0 the left keypoints are undistorted into
+  // kps_un ([2 * max_frames][kp_cap], left views only) and the grid / matchers read those
+  Distortion dist{};
+  int ndist = 0;
+  bool dist_on = false;
+  KeyPoint* kps_un = nullptr;
   // extractor buffers
   uint8_t* d_pyr = nullptr;
   uint8_t* d_blur = nullptr;
@@ -152,14 +159,28 @@ static void set_camera(slamgpu_ctx* c, const slamgpu_camera* cam) {
   k.max_x = (float)c->geom.cols;
   k.min_y = 0.0f;
   k.max_y = (float)c->geom.rows;
+  if (c->dist_on) {  // the undistorted corners (frame.cpp:646-667)
+    const float cols = (float)c->geom.cols, rows = (float)c->geom.rows;
+    const float cx[4] = {0.0f, cols, 0.0f, cols}, cy[4] = {0.0f, 0.0f, rows, rows};
+    float ux[4], uy[4];
+    for (int i = 0; i < 4; i++)
+      undistort_point(cam->fx, cam->fy, cam->cx, cam->cy, c->dist, cx[i], cy[i], &ux[i], &uy[i]);
+    k.min_x = std::min(ux[0], ux[2]);
+    k.max_x = std::max(ux[1], ux[3]);
+    k.min_y = std::min(uy[0], uy[1]);
+    k.max_y = std::max(uy[2], uy[3]);
+  }
   k.cell_w = (float)(k.max_x - k.min_x) / (kGridCols);
   k.cell_h = (float)(k.max_y - k.min_y) / (kGridRows);
   c->cam = k;
   c->have_cam = true;
 }
 
+// The left views as the matchers see them: Frame::undistorted_keypoints_ (== the keypoints when
+// k1 == 0), the descriptors and counts of the extraction.
 static FrameKps left_views(const slamgpu_ctx* c) {
-  return FrameKps{c->out.kps, c->out.desc, c->out.nkps, 2 * (int64_t)c->geom.kp_cap, 2};
+  return FrameKps{c->dist_on ? c->kps_un : c->out.kps, c->out.desc, c->out.nkps,
+                  2 * (int64_t)c->geom.kp_cap, 2};
 }
 
 static int check_device_err(slamgpu_ctx* c) {
@@ -341,8 +362,11 @@ static int run_frontend(slamgpu_ctx* c, const ImageBatch& b, int n_frames, int n
   launch_extract(b, g, n_images, st, c->fx);
   if (stereo) {
     launch_stereo(b, g, c->cam, n_frames, c->sws, c->sout, st);
-    FrameKps cur{c->out.kps, c->out.desc, c->out.nkps, 2 * (int64_t)c->geom.kp_cap, 2};
-    launch_grid(cur, c->cam, n_frames, c->geom.kp_cap, c->gws, st);
+    if (c->dist_on)  // Frame ctor: UndistortKeyPoints after ComputeStereoMatches (frame.cpp:96)
+      launch_undistort(FrameKps{c->out.kps, c->out.desc, c->out.nkps, 2 * (int64_t)c->geom.kp_cap, 2},
+                       c->kps_un, 2 * (int64_t)c->geom.kp_cap, c->cam, c->dist, n_frames,
+                       c->geom.kp_cap, st);
+    launch_grid(left_views(c), c->cam, n_frames, c->geom.kp_cap, c->gws, st);
   }
   HIPCHECK(c, hipGetLastError());
   return 0;
@@ -504,6 +528,81 @@ int slamgpu_device_results(const slamgpu_ctx* c, slamgpu_device_view* v) {
   v->u_right = c->sout.u_right;
   v->depth = c->sout.depth;
   v->kp_cap = c->geom.kp_cap;
+  v->kps_un = reinterpret_cast<const slamgpu_keypoint*>(c->dist_on ? c->kps_un : c->out.kps);
+  return 0;
+}
+
+static int parse_dist(const float* dist, int n, Distortion* d) {
+  if (n != 0 && n != 4 && n != 5) return -1;
+  if (n && !dist) return -1;
+  *d = Distortion{};
+  for (int i = 0; i < n; i++) d->k[i] = dist[i];
+  return 0;
+}
+
+int slamgpu_set_distortion(slamgpu_ctx* c, const float* dist, int n) {
+  if (!c) return SLAMGPU_EINVAL;
+  Distortion d;
+  if (parse_dist(dist, n, &d)) return fail(c, SLAMGPU_EINVAL, "DistCoef needs 4 or 5 values");
+  if (d.k[0] != 0.0f && !c->kps_un) {
+    HIPCHECK(c, hipSetDevice(c->device));
+    if (int rc = dalloc(c, &c->kps_un, (size_t)c->max_images * c->geom.kp_cap)) return rc;
+  }
+  c->dist = d;
+  c->ndist = n;
+  c->dist_on = d.k[0] != 0.0f;  // Frame::UndistortKeyPoints tests k1 only (frame.cpp:616)
+  c->have_cam = false;          // image bounds follow the distortion: set again by the next call
+  return 0;
+}
+
+int slamgpu_undistort_points(const slamgpu_camera* cam, const float* dist, int n,
+                             const float* xy_in, float* xy_out, int n_points) {
+  Distortion d;
+  if (!cam || parse_dist(dist, n, &d) || n_points < 0 || (n_points && (!xy_in || !xy_out)))
+    return SLAMGPU_EINVAL;
+  for (int i = 0; i < n_points; i++) {
+    float u = xy_in[2 * i], v = xy_in[2 * i + 1];
+    if (n) undistort_point(cam->fx, cam->fy, cam->cx, cam->cy, d, u, v, &u, &v);
+    xy_out[2 * i] = u;
+    xy_out[2 * i + 1] = v;
+  }
+  return 0;
+}
+
+int slamgpu_undistort_keypoints_device(const slamgpu_camera* cam, const float* dist, int n,
+                                       const slamgpu_keypoint* d_in, int64_t in_stride,
+                                       const int* d_counts, int counts_stride,
+                                       slamgpu_keypoint* d_out, int64_t out_stride, int n_sets,
+                                       int max_kps, void* stream) {
+  Distortion d;
+  if (!cam || parse_dist(dist, n, &d) || !d_in || !d_out || !d_counts || n_sets < 0 ||
+      max_kps < 0 || counts_stride < 1)
+    return SLAMGPU_EINVAL;
+  if (n_sets == 0 || max_kps == 0) return 0;
+  Camera k{};
+  k.fx = cam->fx;
+  k.fy = cam->fy;
+  k.cx = cam->cx;
+  k.cy = cam->cy;
+  launch_undistort(FrameKps{reinterpret_cast<const KeyPoint*>(d_in), nullptr, d_counts, in_stride,
+                            counts_stride},
+                   reinterpret_cast<KeyPoint*>(d_out), out_stride, k, d, n_sets, max_kps,
+                   static_cast<hipStream_t>(stream));
+  return hipGetLastError() == hipSuccess ? 0 : SLAMGPU_EHIP;
+}
+
+int slamgpu_download_undistorted_keypoints(slamgpu_ctx* c, int frame, slamgpu_keypoint* kps,
+                                           int cap, int* n_out) {
+  if (!c || frame < 0 || frame >= c->n_frames_last) return SLAMGPU_EINVAL;
+  if (!c->dist_on) return slamgpu_download_keypoints(c, 2 * frame, kps, nullptr, cap, n_out);
+  int n = 0;
+  HIPCHECK(c, hipStreamSynchronize(c->stream));
+  HIPCHECK(c, hipMemcpy(&n, c->out.nkps + 2 * frame, sizeof(int), hipMemcpyDeviceToHost));
+  if (n_out) *n_out = n;
+  if (n > cap) return fail(c, SLAMGPU_ECAP, "need %d keypoints, cap %d", n, cap);
+  if (kps && n)
+    HIPCHECK(c, hipMemcpy(kps, c->kps_un + (int64_t)2 * frame * c->geom.kp_cap,
+                          sizeof(KeyPoint) * n, hipMemcpyDeviceToHost));
   return 0;
 }
 
@@ -687,8 +786,8 @@ static int host_search(slamgpu_ctx* c, int frame, const QT* queries, int nq, int
     HIPCHECK(c, hipMemcpyAsync(c->d_blk, blocked, n, hipMemcpyHostToDevice, st));
   }
   const int64_t kc = c->geom.kp_cap;
-  FrameKps cur{c->out.kps + 2 * frame * kc, c->out.desc + 2 * frame * kc * 32,
-               c->out.nkps + 2 * frame, 2 * kc, 2};
+  FrameKps cur{(c->dist_on ? c->kps_un : c->out.kps) + 2 * frame * kc,
+               c->out.desc + 2 * frame * kc * 32, c->out.nkps + 2 * frame, 2 * kc, 2};
   GridWorkspace gw = c->gws;
   gw.cell_start += (int64_t)frame * (kGridCells + 1);
   gw.cell_items += (int64_t)frame * kc;

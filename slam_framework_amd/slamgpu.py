@@ -55,7 +55,8 @@ EXPORTS = [
     "slamgpu_timing_read", "slamgpu_pose_optimization", "slamgpu_pose_optimization_device",
     "slamgpu_optimizer_last_error", "slamgpu_local_bundle_adjustment",
     "slamgpu_local_bundle_adjustment_device", "slamgpu_local_ba_workspace_bytes",
-    "slamgpu_local_ba_linearize_device",
+    "slamgpu_local_ba_linearize_device", "slamgpu_set_distortion", "slamgpu_undistort_points",
+    "slamgpu_undistort_keypoints_device", "slamgpu_download_undistorted_keypoints",
     # include/slamgpu_bow.h
     "slamgpu_bow_last_error", "slamgpu_vocab_load_text", "slamgpu_vocab_create",
     "slamgpu_vocab_destroy", "slamgpu_vocab_info", "slamgpu_vocab_nodes", "slamgpu_bow_transform",
@@ -93,7 +94,8 @@ class Camera(C.Structure):
 
 class DeviceView(C.Structure):
     _fields_ = [("kps", C.c_void_p), ("desc", C.c_void_p), ("nkps", C.c_void_p),
-                ("u_right", C.c_void_p), ("depth", C.c_void_p), ("kp_cap", C.c_int)]
+                ("u_right", C.c_void_p), ("depth", C.c_void_p), ("kp_cap", C.c_int),
+                ("kps_un", C.c_void_p)]
 
 
 class BaLinear(C.Structure):
@@ -169,6 +171,11 @@ def lib():
         L.slamgpu_local_ba_linearize_device.argtypes = [
             C.POINTER(Camera), vp, ip, vp, ip, vp, vp, vp, vp, vp, C.POINTER(BaLinear), vp, vp, sz,
             ip, ip, ip, vp]
+        L.slamgpu_set_distortion.argtypes = [vp, vp, ip]
+        L.slamgpu_undistort_points.argtypes = [C.POINTER(Camera), vp, ip, vp, vp, ip]
+        L.slamgpu_undistort_keypoints_device.argtypes = [
+            C.POINTER(Camera), vp, ip, vp, C.c_int64, vp, ip, vp, C.c_int64, ip, ip, vp]
+        L.slamgpu_download_undistorted_keypoints.argtypes = [vp, ip, vp, ip, C.POINTER(ip)]
         L.slamgpu_optimizer_last_error.argtypes = []
         L.slamgpu_optimizer_last_error.restype = C.c_char_p
         _lib = L
@@ -267,6 +274,18 @@ class Context:
                                                  frame_stride, pitch, n_frames,
                                                  C.byref(self.cam), C.c_void_p(stream or 0)))
 
+    def set_distortion(self, dist_coef):
+        """Frame DistCoef k1 k2 p1 p2 [k3] (None or [] clears)."""
+        d = np.ascontiguousarray(dist_coef if dist_coef is not None else [], np.float32)
+        self.check(lib().slamgpu_set_distortion(self.h, _ptr(d) if d.size else None, d.size))
+
+    def undistorted_keypoints(self, frame):
+        kps = np.zeros(self.kp_cap, KP_DTYPE)
+        n = C.c_int()
+        self.check(lib().slamgpu_download_undistorted_keypoints(self.h, frame, _ptr(kps),
+                                                                self.kp_cap, C.byref(n)))
+        return kps[:n.value].copy()
+
     def sync(self, stream=None):
         self.check(lib().slamgpu_sync(self.h, C.c_void_p(stream or 0)))
 
@@ -345,6 +364,33 @@ class Context:
             self.h, frame, _ptr(queries), len(queries), nnratio, th, _ptr(map_point),
             _ptr(blocked), len(map_point), C.byref(nm)))
         return nm.value
+
+
+def undistort_points(cam, dist_coef, xy):
+    """cv::undistortPoints(xy, ., K, DistCoef, noArray(), K) (host entry point)."""
+    xy = np.ascontiguousarray(xy, np.float32).reshape(-1, 2)
+    d = np.ascontiguousarray(dist_coef, np.float32)
+    out = np.zeros_like(xy)
+    cm = Camera(*cam)
+    rc = lib().slamgpu_undistort_points(C.byref(cm), _ptr(d), d.size, _ptr(xy), _ptr(out),
+                                        len(xy))
+    if rc != 0:
+        raise SlamGpuError(f"slamgpu_undistort_points: {rc}")
+    return out
+
+
+def undistort_keypoints_device(cam, dist_coef, d_in, in_stride, d_counts, counts_stride, d_out,
+                               out_stride, n_sets, max_kps, stream=None):
+    """Batched device Frame::UndistortKeyPoints over n_sets keypoint sets (torch tensors or
+    device pointers)."""
+    d = np.ascontiguousarray(dist_coef, np.float32)
+    cm = Camera(*cam)
+    rc = lib().slamgpu_undistort_keypoints_device(C.byref(cm), _ptr(d), d.size, _ptr(d_in),
+                                                  in_stride, _ptr(d_counts), counts_stride,
+                                                  _ptr(d_out), out_stride, n_sets, max_kps,
+                                                  C.c_void_p(stream or 0))
+    if rc != 0:
+        raise SlamGpuError(f"slamgpu_undistort_keypoints_device: {rc}")
 
 
 class ORBextractor:

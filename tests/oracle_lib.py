@@ -98,6 +98,9 @@ def lib():
         L.oc_stereo_match.argtypes = [C.POINTER(OrbTables), vp, vp, ip, vp, vp, ip,
                                       C.POINTER(Pyramid), C.POINTER(Pyramid), fp, fp, vp, vp, vp]
         L.oc_grid_geom_init.argtypes = [C.POINTER(GridGeom), ip, ip]
+        L.oc_grid_geom_init_dist.argtypes = [C.POINTER(GridGeom), ip, ip, vp, vp, ip]
+        L.oc_undistort_points.argtypes = [vp, vp, ip, vp, vp, ip]
+        L.oc_undistort_keypoints.argtypes = [vp, vp, ip, vp, vp, ip]
         L.oc_features_in_area.argtypes = [C.POINTER(GridGeom), vp, ip, fp, fp, fp, ip, ip, vp, ip]
         L.oc_search_by_projection_frame.argtypes = [
             C.POINTER(GridGeom), C.POINTER(OrbTables), C.POINTER(FrameView), vp, vp, vp, ip,
@@ -176,10 +179,37 @@ def stereo(t, kl, dl, kr, dr, pyr_l, pyr_r, fx, bf):
     return ur, depth, sad
 
 
-def grid_geom(cols, rows) -> GridGeom:
+def grid_geom(cols, rows, cam=None, dist=None) -> GridGeom:
+    """Frame image bounds + grid cell size; with cam (fx, fy, cx, cy, ...) and DistCoef `dist`,
+    the undistorted bounds of Frame::ComputeImageBounds."""
     g = GridGeom()
-    lib().oc_grid_geom_init(C.byref(g), cols, rows)
+    if dist is None:
+        lib().oc_grid_geom_init(C.byref(g), cols, rows)
+    else:
+        k = np.ascontiguousarray(cam[:4], np.float32)
+        d = np.ascontiguousarray(dist, np.float32)
+        lib().oc_grid_geom_init_dist(C.byref(g), cols, rows, ptr(k), ptr(d), d.size)
     return g
+
+
+def undistort_points(cam, dist, xy):
+    """cv::undistortPoints(xy, ., K, DistCoef, noArray(), K) restated (oc_undistort_points)."""
+    xy = np.ascontiguousarray(xy, np.float32).reshape(-1, 2)
+    out = np.zeros_like(xy)
+    k = np.ascontiguousarray(cam[:4], np.float32)
+    d = np.ascontiguousarray(dist, np.float32)
+    lib().oc_undistort_points(ptr(k), ptr(d), d.size, ptr(xy), ptr(out), len(xy))
+    return out
+
+
+def undistort_keypoints(cam, dist, kps):
+    """Frame::UndistortKeyPoints restated (oc_undistort_keypoints)."""
+    kps = np.ascontiguousarray(kps)
+    out = np.zeros_like(kps)
+    k = np.ascontiguousarray(cam[:4], np.float32)
+    d = np.ascontiguousarray(dist, np.float32)
+    lib().oc_undistort_keypoints(ptr(k), ptr(d), d.size, ptr(kps), ptr(out), len(kps))
+    return out
 
 
 def pack_keys(kps) -> np.ndarray:
