@@ -79,12 +79,18 @@ typedef struct {
 #define SLAMGPU_KF_LOCAL 0        /* local keyframe: optimised, pose written back */
 #define SLAMGPU_KF_LOCAL_FIXED 1  /* local keyframe with id 0: fixed, pose written back */
 #define SLAMGPU_KF_FIXED 2        /* fixed camera (sees a local point): neither */
-/* Largest local (optimised) window and keyframe count per problem the device solver takes. */
+/* Largest local (optimised) window and keyframe count per problem of the BATCHED device solver
+ * (slamgpu_local_bundle_adjustment_device: one work-group per problem, S in LDS). */
 #define SLAMGPU_BA_MAX_LOCAL_KF 24
 #define SLAMGPU_BA_MAX_KF 256
+/* Largest optimised window of the single-problem calls (slamgpu_local_bundle_adjustment,
+ * slamgpu_global_bundle_adjustment: one problem over a cooperative grid, S dense in HBM). */
+#define SLAMGPU_BA_COOP_MAX_KF 1024
 
 /* Replaces: void Optimizer::LocalBundleAdjustment(KeyFrame*, bool* stop_flag, const Map&)
- * (optimizer.cpp:413-716) after its graph gathering: kf_Tcw[16 n_kf] (row-major f32, updated for
+ * (optimizer.cpp:413-716) after its graph gathering -- any local window (up to
+ * SLAMGPU_BA_COOP_MAX_KF optimised keyframes), one problem spread over the GPU's CUs for
+ * latency: kf_Tcw[16 n_kf] (row-major f32, updated for
  * modes 0 and 1), points[3 n_points] (MapPoint::GetWorldPos, all updated), the observations, and
  * erase[n_obs]: 1 where the reference puts (keyframe, point) in vToErase (the caller then runs
  * EraseMapPointMatch / EraseObservation and MapPoint::UpdateNormalAndDepth).
@@ -103,6 +109,23 @@ int slamgpu_local_bundle_adjustment(const slamgpu_camera* cam, const float* inv_
                                     float* points, int n_points, const int32_t* point_obs_start,
                                     const slamgpu_ba_obs* obs, const volatile bool* stop_flag,
                                     uint8_t* erase, int* lm_iterations);
+
+/* Replaces: void Optimizer::BundleAdjustment(vpKFs, vpMP, nIterations, pbStopFlag, nLoopKF,
+ * bRobust) (optimizer.cpp:33-207; GlobalBundleAdjustemnt :18-31 passes every keyframe and map
+ * point) after its graph gathering: the keyframes (kf_mode SLAMGPU_KF_LOCAL, or
+ * SLAMGPU_KF_LOCAL_FIXED for the keyframe with id 0, :53), the points and their observations in
+ * the reference's edge order (bad keyframes / points left out by the caller, as :47-49, :82-84,
+ * :95-97 skip them; a point with no observation is not optimised, :149-152). n_iterations
+ * Levenberg-Marquardt iterations of one optimize() (:159-160), Huber kernels (deltas sqrt(5.99) /
+ * sqrt(7.815)) when robust. kf_Tcw and points are updated in place: the caller stores them as
+ * the pose / position or, for a loop-closure GBA (nLoopKF != 0), as Tcw_global_bundle_adj /
+ * position_global_bundle_adj (:170-206). stop_flag: as slamgpu_local_bundle_adjustment's.
+ * *lm_iterations (may be NULL): iterations run. Synchronous. */
+int slamgpu_global_bundle_adjustment(const slamgpu_camera* cam, const float* inv_sigma2,
+                                     int nlevels, float* kf_Tcw, const uint8_t* kf_mode, int n_kf,
+                                     float* points, int n_points, const int32_t* point_obs_start,
+                                     const slamgpu_ba_obs* obs, int n_iterations, int robust,
+                                     const volatile bool* stop_flag, int* lm_iterations);
 
 /* A problem of a batch: its keyframes d_kf_*[kf_begin, kf_begin + n_kf) and points
  * d_points[point_begin, point_begin + n_points); observations are

@@ -42,6 +42,7 @@ typedef struct {
   double* X;              // [n_pts][3]
   uint8_t* active;        // level 0
   int robust;
+  double delta_mono, delta_stereo;  // Huber deltas of the robust kernels
   double* err;            // [n_obs][3] last computed error
   double* chi2;           // [n_obs]
   // linear system
@@ -146,8 +147,8 @@ static void compute_active_errors(ba* B) {
     if (B->active[e]) B->chi2[e] = ba_error(B, e, &B->err[3 * e], Xc);
 }
 
-static double delta_of(const oc_ba_obs* o) {  // const float huber_thresh = std::sqrt(double)
-  return is_stereo(o) ? (double)(float)sqrt(7.815) : (double)(float)sqrt(5.991);
+static double delta_of(const ba* B, const oc_ba_obs* o) {
+  return is_stereo(o) ? B->delta_stereo : B->delta_mono;
 }
 
 static double active_robust_chi2(const ba* B) {
@@ -156,7 +157,7 @@ static double active_robust_chi2(const ba* B) {
     if (!B->active[e]) continue;
     if (B->robust) {
       double rho[3];
-      huber(B->chi2[e], delta_of(&B->obs[e]), rho);
+      huber(B->chi2[e], delta_of(B, &B->obs[e]), rho);
       chi += rho[0];
     } else {
       chi += B->chi2[e];
@@ -180,7 +181,7 @@ static void build_system(ba* B) {
     double w = 1.0;
     if (B->robust) {
       double rho[3];
-      huber(B->chi2[e], delta_of(o), rho);
+      huber(B->chi2[e], delta_of(B, o), rho);
       w = rho[1];
     }
     const double* er = &B->err[3 * e];
@@ -438,6 +439,9 @@ static void ba_init(ba* B, const float cam[5], const float* inv_sigma2, const fl
   const int n_obs = point_obs_start[n_points];
   memset(B, 0, sizeof(*B));
   B->stop_after = -1;
+  // LocalBundleAdjustment's const float thresholds sqrt(5.991) / sqrt(7.815) (optimizer.cpp:556,598)
+  B->delta_mono = (double)(float)sqrt(5.991);
+  B->delta_stereo = (double)(float)sqrt(7.815);
   B->n_kf = n_kf;
   B->n_pts = n_points;
   B->n_obs = n_obs;
@@ -611,4 +615,40 @@ double oc_ba_linearize(const float cam[5], const float* inv_sigma2, const float*
   }
   ba_free(&B);
   return chi;
+}
+
+/* Optimizer::BundleAdjustment (optimizer.cpp:33-207) after its graph gathering: keyframe id 0
+ * fixed (kf_mode 1), every other keyframe optimised (mode 0), every point; one
+ * optimize(n_iterations) with Huber kernels (deltas sqrt(5.99) / sqrt(7.815) as float,
+ * :69-70) when robust; poses and points written back (:163-206). stop_after as above (< 0:
+ * never raised); g2o polls it at each iteration and failed trial only (no check before). */
+int oc_global_bundle_adjustment_stop(const float cam[5], const float* inv_sigma2, float* kf_Tcw,
+                                     const uint8_t* kf_mode, int n_kf, float* points,
+                                     int n_points, const int32_t* point_obs_start,
+                                     const oc_ba_obs* obs, int n_iterations, int robust,
+                                     int stop_after, int* lm_iterations) {
+  if (lm_iterations) *lm_iterations = 0;
+  if (n_kf < 0 || n_points < 0 || point_obs_start[0] != 0) return -1;
+  ba B;
+  ba_init(&B, cam, inv_sigma2, kf_Tcw, kf_mode, n_kf, points, n_points, point_obs_start, obs);
+  B.stop_after = stop_after;
+  B.polls = 0;
+  B.delta_mono = (double)(float)sqrt(5.99);
+  B.delta_stereo = (double)(float)sqrt(7.815);
+  B.robust = robust;
+  optimize(&B, n_iterations, lm_iterations);
+  for (int k = 0; k < n_kf; k++) {
+    if (kf_mode[k] == 2) continue;
+    double R[9];
+    quat_to_R(B.T[k].r, R);
+    for (int i = 0; i < 3; i++) {
+      for (int j = 0; j < 3; j++) kf_Tcw[16 * k + 4 * i + j] = (float)R[3 * i + j];
+      kf_Tcw[16 * k + 4 * i + 3] = (float)B.T[k].t[i];
+    }
+    kf_Tcw[16 * k + 12] = kf_Tcw[16 * k + 13] = kf_Tcw[16 * k + 14] = 0.f;
+    kf_Tcw[16 * k + 15] = 1.f;
+  }
+  for (int i = 0; i < 3 * n_points; i++) points[i] = (float)B.X[i];
+  ba_free(&B);
+  return 0;
 }

@@ -207,6 +207,11 @@ int oc_local_bundle_adjustment_stop(const float cam[5], const float* inv_sigma2,
                                     const uint8_t* kf_mode, int n_kf, float* points, int n_points,
                                     const int32_t* point_obs_start, const oc_ba_obs* obs,
                                     int stop_after, uint8_t* erase, int* lm_iterations);
+int oc_global_bundle_adjustment_stop(const float cam[5], const float* inv_sigma2, float* kf_Tcw,
+                                     const uint8_t* kf_mode, int n_kf, float* points,
+                                     int n_points, const int32_t* point_obs_start,
+                                     const oc_ba_obs* obs, int n_iterations, int robust,
+                                     int stop_after, int* lm_iterations);
 double oc_ba_linearize(const float cam[5], const float* inv_sigma2, const float* kf_Tcw,
                        const uint8_t* kf_mode, int n_kf, const float* points, int n_points,
                        const int32_t* point_obs_start, const oc_ba_obs* obs, double* chi2,

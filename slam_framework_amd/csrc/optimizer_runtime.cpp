@@ -11,10 +11,15 @@
 
 #include <cstdarg>
 #include <cstdio>
+#include <algorithm>
+#include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <string>
+#include <vector>
 
 #include "../../include/slamgpu_optimizer.h"
+#include "ba_coop.h"
 #include "ba_kernels.h"
 #include "pose_kernels.h"
 
@@ -219,54 +224,96 @@ int slamgpu_local_ba_linearize_device(
   return 0;
 }
 
-int slamgpu_local_bundle_adjustment(const slamgpu_camera* cam, const float* inv_sigma2,
-                                    int nlevels, float* kf_Tcw, const uint8_t* kf_mode, int n_kf,
-                                    float* points, int n_points, const int32_t* point_obs_start,
-                                    const slamgpu_ba_obs* obs, const volatile bool* stop_flag,
-                                    uint8_t* erase, int* lm_iterations) {
+}  // extern "C"
+
+namespace {
+
+// Work-groups of the cooperative single-problem solver: one per CU up to 64 (SLAMGPU_BA_WGS
+// overrides), never more than can be resident at once.
+int coop_grid(int device) {
+  static int cached_dev = -1, cached = 0;
+  if (cached_dev == device) return cached;
+  hipDeviceProp_t prop{};
+  int g = 64;
+  if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 0)
+    g = std::min(g, prop.multiProcessorCount);
+  if (const char* e = getenv("SLAMGPU_BA_WGS")) g = std::max(1, atoi(e));
+  int per_cu = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, coop_kernel_ptr(), kCoopThreads, 0) ==
+          hipSuccess &&
+      per_cu > 0 && prop.multiProcessorCount > 0)
+    g = std::min(g, per_cu * prop.multiProcessorCount);
+  cached_dev = device;
+  cached = g;
+  return g;
+}
+
+// One problem (LocalBundleAdjustment after its graph gathering, or the global BundleAdjustment)
+// on the cooperative solver: validate, stage, run the schedule asynchronously while mirroring the
+// caller's stop flag into host-mapped memory, read back.
+int coop_host(const char* what, const slamgpu_camera* cam, const float* inv_sigma2, int nlevels,
+              float* kf_Tcw, const uint8_t* kf_mode, int n_kf, float* points, int n_points,
+              const int32_t* point_obs_start, const slamgpu_ba_obs* obs,
+              const volatile bool* stop_flag, uint8_t* erase, const CoopPhase* phases,
+              int n_phases, bool local, int* lm_iterations) {
   PoseParams P;
   if (int r = make_params(cam, inv_sigma2, nlevels, &P)) return r;
   if (lm_iterations) *lm_iterations = 0;
   if (n_kf < 0 || n_points < 0 || !kf_Tcw || !kf_mode || !point_obs_start || (n_points && !points))
-    return fail(SLAMGPU_EINVAL, "bad arguments");
+    return fail(SLAMGPU_EINVAL, "%s: bad arguments", what);
   if (point_obs_start[0] != 0) return fail(SLAMGPU_EINVAL, "point_obs_start[0] must be 0");
   const int n_obs = point_obs_start[n_points];
-  if (n_obs < 0 || (n_obs > 0 && (!obs || !erase))) return fail(SLAMGPU_EINVAL, "bad observations");
-  if (n_kf > SLAMGPU_BA_MAX_KF)
-    return fail(SLAMGPU_ECAP, "%d keyframes > SLAMGPU_BA_MAX_KF (%d)", n_kf, SLAMGPU_BA_MAX_KF);
-  int n_local = 0;
+  if (n_obs < 0 || (n_obs > 0 && !obs) || (local && n_obs > 0 && !erase))
+    return fail(SLAMGPU_EINVAL, "%s: bad observations", what);
+  std::vector<int32_t> free_of(n_kf, -1), kf_of;
   for (int k = 0; k < n_kf; k++) {
     if (kf_mode[k] > SLAMGPU_KF_FIXED) return fail(SLAMGPU_EINVAL, "kf_mode[%d] = %d", k, kf_mode[k]);
-    n_local += kf_mode[k] == SLAMGPU_KF_LOCAL;
+    if (kf_mode[k] == SLAMGPU_KF_LOCAL) {
+      free_of[k] = (int32_t)kf_of.size();
+      kf_of.push_back(k);
+    }
   }
-  if (n_local > SLAMGPU_BA_MAX_LOCAL_KF)
-    return fail(SLAMGPU_ECAP, "%d local keyframes > SLAMGPU_BA_MAX_LOCAL_KF (%d)", n_local,
-                SLAMGPU_BA_MAX_LOCAL_KF);
-  for (int p = 0; p < n_points; p++)
-    if (point_obs_start[p + 1] < point_obs_start[p])
-      return fail(SLAMGPU_EINVAL, "point_obs_start not monotone at %d", p);
-  for (int e = 0; e < n_obs; e++) {
-    if (obs[e].keyframe < 0 || obs[e].keyframe >= n_kf)
-      return fail(SLAMGPU_EINVAL, "observation %d: keyframe %d outside [0, %d)", e, obs[e].keyframe, n_kf);
-    if (obs[e].octave < 0 || obs[e].octave >= nlevels)
-      return fail(SLAMGPU_EINVAL, "observation %d: octave %d outside [0, %d)", e, obs[e].octave, nlevels);
+  const int K = (int)kf_of.size();
+  if (K > SLAMGPU_BA_COOP_MAX_KF)
+    return fail(SLAMGPU_ECAP, "%s: %d optimised keyframes > SLAMGPU_BA_COOP_MAX_KF (%d)", what, K,
+                SLAMGPU_BA_COOP_MAX_KF);
+  long long pairs = 0;
+  std::vector<int> seen(n_kf, -1);
+  for (int p = 0; p < n_points; p++) {
+    const int s = point_obs_start[p], e1 = point_obs_start[p + 1];
+    if (e1 < s) return fail(SLAMGPU_EINVAL, "point_obs_start not monotone at %d", p);
+    long long m = 0;
+    for (int e = s; e < e1; e++) {
+      const int k = obs[e].keyframe;
+      if (k < 0 || k >= n_kf)
+        return fail(SLAMGPU_EINVAL, "observation %d: keyframe %d outside [0, %d)", e, k, n_kf);
+      if (obs[e].octave < 0 || obs[e].octave >= nlevels)
+        return fail(SLAMGPU_EINVAL, "observation %d: octave %d outside [0, %d)", e, obs[e].octave, nlevels);
+      if (seen[k] == p) return fail(SLAMGPU_EINVAL, "a map point is observed twice by one keyframe");
+      seen[k] = p;
+      m += free_of[k] >= 0;
+    }
+    pairs += m * (m + 1) / 2;
   }
-  if (stop_flag && *stop_flag) {  // optimizer.cpp:616-618: return before optimising
+  if (pairs > (1ll << 30)) return fail(SLAMGPU_ECAP, "%s: %lld Schur pairs", what, pairs);
+  if (local && stop_flag && *stop_flag) {  // optimizer.cpp:616-618: return before optimising
     for (int e = 0; e < n_obs; e++) erase[e] = 0;
     return 0;
   }
+  int dev = 0;
+  OPT_HIPCHECK(hipGetDevice(&dev));
+  const int G = coop_grid(dev);
   size_t wsb = 0;
-  ba_workspace_layout(nullptr, n_kf, n_points, n_obs, &wsb);
-  const size_t o_prob = 0, o_T = 256, o_mode = o_T + al256(64 * (size_t)n_kf);
-  const size_t o_pts = o_mode + al256(n_kf), o_ps = o_pts + al256(12 * (size_t)n_points);
+  coop_layout(nullptr, n_kf, n_points, n_obs, K, (int)pairs, G, &wsb);
+  const size_t o_T = 0, o_mode = o_T + al256(64 * (size_t)n_kf);
+  const size_t o_pts = o_mode + al256(n_kf + 1), o_ps = o_pts + al256(12 * (size_t)n_points + 4);
   const size_t o_obs = o_ps + al256(4 * ((size_t)n_points + 1));
-  const size_t o_er = o_obs + al256(sizeof(slamgpu_ba_obs) * (size_t)n_obs);
-  const size_t o_st = o_er + al256((size_t)n_obs), o_ws = o_st + 256;
+  const size_t o_er = o_obs + al256(sizeof(slamgpu_ba_obs) * (size_t)n_obs + 4);
+  const size_t o_ws = o_er + al256((size_t)n_obs + 4);
   HostStage& S = t_stage;
   if (int r = stage_reserve(S, o_ws + wsb)) return r;
   char* b = static_cast<char*>(S.buf);
-  const slamgpu_ba_problem prob = {0, n_kf, 0, n_points};
-  OPT_HIPCHECK(hipMemcpyAsync(b + o_prob, &prob, sizeof(prob), hipMemcpyHostToDevice, S.stream));
+  const CoopWs w = coop_layout(b + o_ws, n_kf, n_points, n_obs, K, (int)pairs, G, nullptr);
   OPT_HIPCHECK(hipMemcpyAsync(b + o_T, kf_Tcw, 64 * (size_t)n_kf, hipMemcpyHostToDevice, S.stream));
   OPT_HIPCHECK(hipMemcpyAsync(b + o_mode, kf_mode, n_kf, hipMemcpyHostToDevice, S.stream));
   if (n_points)
@@ -276,7 +323,19 @@ int slamgpu_local_bundle_adjustment(const slamgpu_camera* cam, const float* inv_
   if (n_obs)
     OPT_HIPCHECK(hipMemcpyAsync(b + o_obs, obs, sizeof(slamgpu_ba_obs) * (size_t)n_obs,
                                 hipMemcpyHostToDevice, S.stream));
-  const BaWorkspace ws = ba_workspace_layout(b + o_ws, n_kf, n_points, n_obs, nullptr);
+  if (n_kf)
+    OPT_HIPCHECK(hipMemcpyAsync(const_cast<int32_t*>(w.free_of_kf), free_of.data(), 4 * (size_t)n_kf,
+                                hipMemcpyHostToDevice, S.stream));
+  if (K)
+    OPT_HIPCHECK(hipMemcpyAsync(const_cast<int32_t*>(w.kf_of_free), kf_of.data(), 4 * (size_t)K,
+                                hipMemcpyHostToDevice, S.stream));
+  CoopProblem pb{reinterpret_cast<const slamgpu_ba_obs*>(b + o_obs),
+                 reinterpret_cast<const int32_t*>(b + o_ps),
+                 reinterpret_cast<const uint8_t*>(b + o_mode),
+                 reinterpret_cast<float*>(b + o_T),
+                 reinterpret_cast<float*>(b + o_pts),
+                 local ? reinterpret_cast<uint8_t*>(b + o_er) : nullptr,
+                 n_obs, n_points, n_kf, K};
   volatile int32_t* mirror = nullptr;
   if (stop_flag) {
     if (!S.stop_host) {
@@ -290,36 +349,61 @@ int slamgpu_local_bundle_adjustment(const slamgpu_camera* cam, const float* inv_
     mirror = S.stop_host;
     *mirror = *stop_flag ? 1 : 0;
   }
-  OPT_HIPCHECK(launch_local_ba(P, reinterpret_cast<slamgpu_ba_problem*>(b + o_prob), 1,
-                               reinterpret_cast<float*>(b + o_T), reinterpret_cast<uint8_t*>(b + o_mode),
-                               reinterpret_cast<float*>(b + o_pts), reinterpret_cast<int32_t*>(b + o_ps),
-                               reinterpret_cast<slamgpu_ba_obs*>(b + o_obs),
-                               reinterpret_cast<uint8_t*>(b + o_er), reinterpret_cast<int32_t*>(b + o_st),
-                               ws, stop_flag ? S.stop_dev : nullptr, S.stream));
-  if (mirror) {  // keep the device's view of the caller's flag live until the kernel is done
-    // (nothing pageable may be queued behind the kernel here: a copy to pageable memory would
-    // block this thread until the kernel ends)
+  OPT_HIPCHECK(launch_coop_ba(P, pb, w, phases, n_phases, local, stop_flag ? S.stop_dev : nullptr,
+                              G, S.stream));
+  int32_t ctl[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  // keep the device's view of the caller's flag live until the work is done (nothing pageable
+  // may be queued behind the kernels: a copy to pageable memory would block this thread)
+  if (mirror) {
     hipError_t q;
     while ((q = hipStreamQuery(S.stream)) == hipErrorNotReady) {
       *mirror = *stop_flag ? 1 : 0;
       std::this_thread::sleep_for(std::chrono::microseconds(20));
     }
-    if (q != hipSuccess) return fail(SLAMGPU_EHIP, "local BA: %s", hipGetErrorString(q));
+    if (q != hipSuccess) return fail(SLAMGPU_EHIP, "%s: %s", what, hipGetErrorString(q));
   }
-  int32_t st = 0;
-  OPT_HIPCHECK(hipMemcpyAsync(&st, b + o_st, 4, hipMemcpyDeviceToHost, S.stream));
+  OPT_HIPCHECK(hipMemcpyAsync(ctl, w.ctl, sizeof(ctl), hipMemcpyDeviceToHost, S.stream));
   OPT_HIPCHECK(hipStreamSynchronize(S.stream));
-  if (st < 0) {
-    if (st == -2) return fail(SLAMGPU_EINVAL, "a map point is observed twice by one keyframe");
-    return fail(SLAMGPU_EDEVICE, "local BA kernel status %d", st);
-  }
+  if (ctl[CTL_ERR]) return fail(SLAMGPU_EDEVICE, "%s: grid barrier timed out", what);
   OPT_HIPCHECK(hipMemcpyAsync(kf_Tcw, b + o_T, 64 * (size_t)n_kf, hipMemcpyDeviceToHost, S.stream));
   if (n_points)
     OPT_HIPCHECK(hipMemcpyAsync(points, b + o_pts, 12 * (size_t)n_points, hipMemcpyDeviceToHost, S.stream));
-  if (n_obs) OPT_HIPCHECK(hipMemcpyAsync(erase, b + o_er, n_obs, hipMemcpyDeviceToHost, S.stream));
+  if (local && n_obs)
+    OPT_HIPCHECK(hipMemcpyAsync(erase, b + o_er, n_obs, hipMemcpyDeviceToHost, S.stream));
   OPT_HIPCHECK(hipStreamSynchronize(S.stream));
-  if (lm_iterations) *lm_iterations = st;
+  if (lm_iterations) *lm_iterations = ctl[CTL_LM];
   return 0;
+}
+
+}  // namespace
+
+extern "C" {
+
+int slamgpu_local_bundle_adjustment(const slamgpu_camera* cam, const float* inv_sigma2,
+                                    int nlevels, float* kf_Tcw, const uint8_t* kf_mode, int n_kf,
+                                    float* points, int n_points, const int32_t* point_obs_start,
+                                    const slamgpu_ba_obs* obs, const volatile bool* stop_flag,
+                                    uint8_t* erase, int* lm_iterations) {
+  // optimizer.cpp:611-613 optimize(5) with Huber kernels (deltas sqrt(5.991) / sqrt(7.815) as
+  // float, :556 / :598), the outlier pass, then optimize(10) without them (:667-670)
+  const CoopPhase ph[2] = {{5, 1, (double)(float)sqrt(5.991), (double)(float)sqrt(7.815)},
+                           {10, 0, 0.0, 0.0}};
+  return coop_host("local BA", cam, inv_sigma2, nlevels, kf_Tcw, kf_mode, n_kf, points, n_points,
+                   point_obs_start, obs, stop_flag, erase, ph, 2, true, lm_iterations);
+}
+
+int slamgpu_global_bundle_adjustment(const slamgpu_camera* cam, const float* inv_sigma2,
+                                     int nlevels, float* kf_Tcw, const uint8_t* kf_mode, int n_kf,
+                                     float* points, int n_points, const int32_t* point_obs_start,
+                                     const slamgpu_ba_obs* obs, int n_iterations, int robust,
+                                     const volatile bool* stop_flag, int* lm_iterations) {
+  if (n_iterations < 0) return fail(SLAMGPU_EINVAL, "n_iterations %d < 0", n_iterations);
+  // optimizer.cpp:69-70 huber_thresh_2d = sqrt(5.99), huber_thresh_3d = sqrt(7.815) (float);
+  // one optimize(num_iter) (:159-160)
+  const CoopPhase ph[1] = {{n_iterations, robust ? 1 : 0, (double)(float)sqrt(5.99),
+                            (double)(float)sqrt(7.815)}};
+  return coop_host("global BA", cam, inv_sigma2, nlevels, kf_Tcw, kf_mode, n_kf, points, n_points,
+                   point_obs_start, obs, stop_flag, nullptr, ph, 1, false, lm_iterations);
 }
 
 }  // extern "C"

@@ -55,6 +55,7 @@ EXPORTS = [
     "slamgpu_timing_read", "slamgpu_pose_optimization", "slamgpu_pose_optimization_device",
     "slamgpu_optimizer_last_error", "slamgpu_local_bundle_adjustment",
     "slamgpu_local_bundle_adjustment_device", "slamgpu_local_ba_workspace_bytes",
+    "slamgpu_global_bundle_adjustment",
     "slamgpu_local_ba_linearize_device", "slamgpu_set_distortion", "slamgpu_undistort_points",
     "slamgpu_undistort_keypoints_device", "slamgpu_download_undistorted_keypoints",
     # include/slamgpu_bow.h
@@ -163,6 +164,8 @@ def lib():
                                                        vp, vp, vp, vp]
         L.slamgpu_local_bundle_adjustment.argtypes = [C.POINTER(Camera), vp, ip, vp, vp, ip, vp,
                                                       ip, vp, vp, vp, vp, C.POINTER(ip)]
+        L.slamgpu_global_bundle_adjustment.argtypes = [C.POINTER(Camera), vp, ip, vp, vp, ip, vp,
+                                                       ip, vp, vp, ip, ip, vp, C.POINTER(ip)]
         L.slamgpu_local_ba_workspace_bytes.argtypes = [ip, ip, ip]
         L.slamgpu_local_ba_workspace_bytes.restype = sz
         L.slamgpu_local_bundle_adjustment_device.argtypes = [
@@ -565,6 +568,26 @@ class Optimizer:
             _ptr(pts), len(pts), _ptr(start), _ptr(ob), C.byref(stop), _ptr(erase),
             C.byref(its)))
         return kf, pts, erase[:len(ob)].astype(bool), its.value
+
+    @staticmethod
+    def BundleAdjustment(kf_Tcw, kf_mode, points, point_obs_start, obs, cam, inv_sigma2,
+                         n_iterations=10, robust=True, stop_flag=False):
+        """Optimizer::BundleAdjustment / GlobalBundleAdjustemnt (optimizer.cpp:18-207) on the
+        gathered graph: kf_mode 1 for the keyframe with id 0 (fixed), 0 for the others. Returns
+        (kf_Tcw', points', lm_iterations)."""
+        kf = np.ascontiguousarray(np.asarray(kf_Tcw, np.float32).reshape(-1, 4, 4)).copy()
+        mode = np.ascontiguousarray(kf_mode, np.uint8)
+        pts = np.ascontiguousarray(np.asarray(points, np.float32).reshape(-1, 3)).copy()
+        start = np.ascontiguousarray(point_obs_start, np.int32)
+        ob = np.ascontiguousarray(obs, dtype=BA_OBS_DTYPE)
+        isig = np.ascontiguousarray(inv_sigma2, np.float32)
+        its = C.c_int()
+        stop = stop_flag if isinstance(stop_flag, C.c_bool) else C.c_bool(bool(stop_flag))
+        _opt_check(lib().slamgpu_global_bundle_adjustment(
+            C.byref(Camera(*cam)), _ptr(isig), len(isig), _ptr(kf), _ptr(mode), len(mode),
+            _ptr(pts), len(pts), _ptr(start), _ptr(ob), int(n_iterations), int(bool(robust)),
+            C.byref(stop), C.byref(its)))
+        return kf, pts, its.value
 
 
 def pose_optimization_device(cam, inv_sigma2, d_edges, d_edge_start, n_frames, d_Tcw, d_outlier,

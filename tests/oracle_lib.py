@@ -343,6 +343,8 @@ def _ba_lib():
                                                  C.POINTER(ip)]
         L.oc_local_bundle_adjustment_stop.argtypes = [vp, vp, vp, vp, ip, vp, ip, vp, vp, ip,
                                                       vp, C.POINTER(ip)]
+        L.oc_global_bundle_adjustment_stop.argtypes = [vp, vp, vp, vp, ip, vp, ip, vp, vp, ip,
+                                                       ip, ip, C.POINTER(ip)]
         L.oc_ba_edge_eval.argtypes = [vp, vp, vp, vp, vp, C.c_float, vp, vp, vp]
         L.oc_ba_linearize.argtypes = [vp, vp, vp, vp, ip, vp, ip, vp, vp, vp, vp, vp, vp, vp, vp]
         L.oc_ba_linearize.restype = C.c_double
@@ -369,6 +371,25 @@ def local_ba(cam, prob, stop_after=-1):
                                                   ptr(obs), stop_after, ptr(erase), C.byref(it))
     assert r == 0
     return kf, pts, erase[:len(obs)].astype(bool), it.value
+
+
+def global_ba(cam, prob, n_iterations=10, robust=True, stop_after=-1):
+    """Optimizer::BundleAdjustment restated on a synthetic problem dict (kf_mode 1 = the fixed
+    keyframe id 0, 0 = optimised). Returns (kf_Tcw', points', lm_iterations)."""
+    cam = np.asarray(cam, np.float32)
+    kf = np.ascontiguousarray(prob["kf_Tcw"], np.float32).copy()
+    pts = np.ascontiguousarray(prob["points"], np.float32).copy()
+    mode = np.ascontiguousarray(prob["kf_mode"], np.uint8)
+    start = np.ascontiguousarray(prob["point_obs_start"], np.int32)
+    obs = np.ascontiguousarray(prob["obs"]).view(BA_OBS_DTYPE)
+    isig = np.ascontiguousarray(prob["inv_sigma2"], np.float32)
+    it = C.c_int()
+    r = _ba_lib().oc_global_bundle_adjustment_stop(ptr(cam), ptr(isig), ptr(kf), ptr(mode),
+                                                   len(mode), ptr(pts), len(pts), ptr(start),
+                                                   ptr(obs), n_iterations, int(robust),
+                                                   stop_after, C.byref(it))
+    assert r == 0
+    return kf, pts, it.value
 
 
 def ba_edge_eval(cam, R, t, X, ob, inv_sigma2):

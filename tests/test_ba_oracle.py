@@ -132,3 +132,30 @@ def test_stop_flag_polls(oracle):
         prev = its_c
     # stopping in the first optimize() skips the second one (do_more = false)
     assert oracle.local_ba(S.KITTI_CAM, P, stop_after=2)[3] <= 5
+
+
+@pytest.mark.parametrize("robust", [True, False])
+def test_global_ba_noise_free_converges(robust):
+    """Optimizer::BundleAdjustment restated (oc_global_bundle_adjustment_stop): keyframe 0 fixed,
+    every other keyframe and every point perturbed; noise-free observations pull them back."""
+    P = S.ba_problem(41, n_local=12, n_fixed=0, n_points=900, noise_px=0.0, outlier_frac=0.0,
+                     first_local_fixed=True, spacing=0.8)
+    kf, pts, its = O.global_ba(S.KITTI_CAM, P, 20, robust)
+    assert its > 0
+    assert np.abs(kf[1:, :3, :] - P["kf_true"][1:, :3, :]).max() < 1e-3
+    err = np.abs(pts - P["points_true"]).max(1)
+    e0 = np.abs(P["points"] - P["points_true"]).max(1)
+    assert np.percentile(err, 99) < 1e-3 and np.median(err) < 0.01 * np.median(e0)
+    assert np.array_equal(kf[0], O.global_ba(S.KITTI_CAM, P, 0, robust)[0][0])
+
+
+def test_global_ba_stop_polls():
+    """No stop check before optimize() in the global BA: stop_after=0 runs no iteration but still
+    writes back (Converter round trip); stop_after=1 runs exactly one."""
+    P = S.ba_problem(42, n_local=6, n_fixed=0, n_points=300, first_local_fixed=True)
+    kf0, pts0, its0 = O.global_ba(S.KITTI_CAM, P, 10, True, stop_after=0)
+    assert its0 == 0
+    np.testing.assert_allclose(kf0, P["kf_Tcw"], atol=1e-6)
+    np.testing.assert_array_equal(pts0, P["points"])
+    _, _, its1 = O.global_ba(S.KITTI_CAM, P, 10, True, stop_after=1)
+    assert its1 == 1
