@@ -695,12 +695,40 @@ def bench_local_ba(dev, with_cpu):
                             "frac": round(lin_gbs / HBM_PEAK_GBS, 4),
                             "algorithmic_bytes_per_launch": lin_bytes}}
     del d_ws, lin
-    out = {"linearize": out_lin,
+    # the drop-in calls (host buffers in and out, synchronous): slamgpu_local_bundle_adjustment
+    # and slamgpu_global_bundle_adjustment, one problem spread over the CUs (csrc/ba_coop.hip)
+    def wall_ms(fn, reps=10):
+        fn()
+        ts = []
+        for _ in range(reps):
+            t0 = time.perf_counter()
+            r = fn()
+            ts.append(1e3 * (time.perf_counter() - t0))
+        return float(np.median(ts)), r
+    drop = {}
+    P48 = S.ba_problem(12, n_local=48, n_fixed=6, n_points=5000, spacing=0.6)
+    for name, PP in (("C5", P), ("local_window_48", P48)):
+        ms, r = wall_ms(lambda: G.Optimizer.LocalBundleAdjustment(
+            PP["kf_Tcw"], PP["kf_mode"], PP["points"], PP["point_obs_start"], PP["obs"],
+            S.KITTI_CAM, PP["inv_sigma2"]))
+        drop[name] = {"ms": round(ms, 3), "lm_iterations": r[3],
+                      "keyframes": int(len(PP["kf_mode"])), "points": int(len(PP["points"])),
+                      "observations": int(len(PP["obs"]))}
+    for nkf, npt in ((30, 4000), (100, 12000)):
+        PG = S.ba_problem(34, n_local=nkf, n_fixed=0, n_points=npt, first_local_fixed=True,
+                          spacing=0.8)
+        ms, r = wall_ms(lambda: G.Optimizer.BundleAdjustment(
+            PG["kf_Tcw"], PG["kf_mode"], PG["points"], PG["point_obs_start"], PG["obs"],
+            S.KITTI_CAM, PG["inv_sigma2"], n_iterations=10), reps=5)
+        drop[f"global_ba_{nkf}kf"] = {"ms": round(ms, 3), "lm_iterations": r[2], "keyframes": nkf,
+                                      "points": npt, "observations": int(len(PG["obs"]))}
+    out = {"linearize": out_lin, "drop_in": drop,
            "workload": "configs[4]: LocalBundleAdjustment on SURVEY 8(d) C5, 20 local + 5 fixed "
                        f"keyframes x 3000 map points ({no} observations), 5 robust + 10 LM "
                        "iterations (FP64)",
            "problems_per_s": round(BB / res[BB][0] * 1e3, 1), "batch_problems": BB,
-           "single_problem_ms": round(res[1][0], 3), "lm_iterations": res[1][1],
+           "single_problem_ms": drop["C5"]["ms"],
+           "batched_kernel_one_problem_ms": round(res[1][0], 3), "lm_iterations": res[1][1],
            "cpu_baseline": None}
     if with_cpu:
         import concurrent.futures as cf

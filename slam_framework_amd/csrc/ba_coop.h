@@ -17,6 +17,7 @@ struct CoopProblem {
   float* kf_Tcw;               // [n_kf][16]
   float* points;               // [n_pts][3]
   uint8_t* erase;              // [n_obs] or nullptr (global BA)
+  int32_t* ctl_out;            // [8] copy of the control words at the end, or nullptr
   int n_obs, n_pts, n_kf;
   int K;                       // optimised keyframes (mode SLAMGPU_KF_LOCAL)
 };
@@ -43,14 +44,23 @@ struct CoopWs {
   int32_t* n_runs;     // [1]
   int32_t* diag_run;   // [K] run of block (f, f) or -1
   double* hpp_part;    // [K][nch][27] Hpp (21) + bp (6) partial sums
-  int nch;
-  double* S;           // [n][n] reduced camera system (dense; lower blocks written)
+  double* hpp_tot;     // [K][27] their totals (the keyframe's last chunk, chunk order)
+  int32_t* kf_arrive;  // [K] chunk arrival counters
+  int32_t* run_arrive; // [pairs_cap] chunk arrival counters per run
+  double* S;           // [n][n] reduced camera system (dense; the lower blocks of each run)
   double* bs;          // [n] reduced right-hand side
-  double* fac;         // factor scratch when n > kCoopLdsN: packed L (n(n+1)/2), V (6n), dg, rhs
+  int nch;
+  int32_t* run_nch;    // [pairs_cap] assembly chunks per run
+  int32_t* run_ch0;    // [pairs_cap] first chunk of each run
+  int32_t* chunk_run;  // [chunks] run of each chunk
+  int32_t* n_chunks;   // [1]
+  double* chunk_part;  // [chunks][42] partial S block (36) and reduced rhs (6) sums
+  double* fac;         // factor storage when n > kCoopLdsN: packed L (n(n+1)/2), V (6n), dg, rhs
   double* xp;          // [n] pose step of the last successful solve
   double* part;        // [G][8] work-group partials + [8] scalars of work-group 0
   uint32_t* bar;       // grid barrier: [0] arrivals, [1] generation
   int32_t* ctl;        // control words (CTL_*)
+  double* prof;        // [8] per-phase wall time (us) of work-group 0, or nullptr
   void* cub_tmp;
   size_t cub_bytes;
   int pairs_cap;
@@ -64,6 +74,13 @@ struct CoopPhase {
   int iterations;
   int robust;
   double delta_mono, delta_stereo;  // Huber deltas (float sqrt of the thresholds, as g2o gets)
+};
+
+// The schedule: one or two optimize() calls (LocalBA: robust 5, outlier pass, plain 10).
+struct CoopSchedule {
+  CoopPhase ph[2];
+  int n_phases;
+  int outlier_pass;
 };
 
 constexpr int kCoopThreads = 512;

@@ -34,7 +34,10 @@ namespace {
 using namespace ba;
 
 constexpr int kT = kCoopThreads, kW = kT / 64;
+constexpr int kMaxGrid = 256;  // work-groups of a cooperative launch (<= one per CU)
 constexpr uint32_t kPadKey = 0xFFFFFFFFu;
+constexpr int kChunk = 64;  // S-block pairs per assembly task (one per lane)
+constexpr int kCP = 42;     // per-chunk partials: 36 of the 6x6 block + 6 of the reduced rhs
 
 struct CoopShared {
   double S[kCoopLdsN * (kCoopLdsN + 1) / 2];  // packed lower L of the factorisation
@@ -42,6 +45,10 @@ struct CoopShared {
   double dg[kCoopLdsN];
   double V[kCoopLdsN * 6];
   double red[kW];
+  double gpart[4][kMaxGrid];  // per-work-group partials staged for the grid totals
+  double tot[4];
+  int iscan[kT];
+  int itot;
   float isig[SLAMGPU_MAX_LEVELS];
   int ok;
 };
@@ -85,7 +92,8 @@ __device__ void grid_sync(const CoopWs& w, const int32_t* stop_flag, bool poll) 
       } else {
         uint32_t spins = 0;
         while (__hip_atomic_load(&w.bar[1], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) == g) {
-          __builtin_amdgcn_s_sleep(2);
+          if (spins < 256) __builtin_amdgcn_s_sleep(1);  // short waits: poll fast
+          else __builtin_amdgcn_s_sleep(16);             // then back off (~1k cycles)
           if (++spins > (1u << 22)) {
             __hip_atomic_store(&w.ctl[CTL_ERR], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             break;
@@ -114,14 +122,39 @@ __device__ void wg_part(CoopShared& sh, const CoopWs& w, double v, int slot, boo
   }
   __syncthreads();
 }
-// The grid total of a slot, in work-group order (identical in every work-group).
-__device__ double grid_total(const CoopWs& w, int slot, bool is_max) {
-  double s = w.part[slot];
-  for (int g = 1; g < (int)gridDim.x; g++) {
-    const double v = w.part[(size_t)g * 8 + slot];
-    s = is_max ? fmax(s, v) : s + v;
+// Grid totals of partial slots slot0 .. slot0 + ns - 1 (ns <= 4), each summed (or max-ed) in
+// work-group order, identical in every work-group: the partials are loaded in parallel into LDS,
+// then thread 0 reduces them. Results in sh.tot[0 .. ns). Contains barriers.
+__device__ void grid_totals(CoopShared& sh, const CoopWs& w, int slot0, int ns, bool is_max) {
+  const int G = gridDim.x;
+  for (int t = threadIdx.x; t < G * ns; t += kT) {
+    const int g = t / ns, k = t - g * ns;
+    sh.gpart[k][g] = w.part[(size_t)g * 8 + slot0 + k];
   }
-  return s;
+  __syncthreads();
+  if (threadIdx.x < ns) {
+    const int k = threadIdx.x;
+    double v = sh.gpart[k][0];
+    for (int g = 1; g < G; g++) v = is_max ? fmax(v, sh.gpart[k][g]) : v + sh.gpart[k][g];
+    sh.tot[k] = v;
+  }
+  __syncthreads();
+}
+
+// A wave that has just stored its partial of a reduction with `total` contributors: releases the
+// stores at device scope and counts itself in at `counter`; returns true (wave-uniform) in the
+// wave that arrived last, which then sees every partial (acquire) and resets the counter.
+__device__ __forceinline__ bool last_arriver(int32_t* counter, int total) {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+  int a = 0;
+  if ((threadIdx.x & 63) == 0)
+    a = __hip_atomic_fetch_add(counter, 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+  a = __builtin_amdgcn_readfirstlane(a);
+  if (a != total - 1) return false;
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  if ((threadIdx.x & 63) == 0)
+    __hip_atomic_store(counter, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  return true;
 }
 
 // ---- setup and structure kernels -------------------------------------------------------------
@@ -153,6 +186,7 @@ __global__ __launch_bounds__(256) void coop_setup_kernel(CoopProblem pb, CoopWs 
   if (i < 6 * pb.K) w.xp[i] = 0.0;
   if (i < 8) w.ctl[i] = 0;
   if (i < 2) w.bar[i] = 0u;
+  if (w.prof && i < 16) w.prof[i] = 0.0;
 }
 
 // Per point: its active edges to optimised keyframes, sorted by keyframe, and its pair count.
@@ -205,10 +239,23 @@ __global__ __launch_bounds__(256) void coop_runs_kernel(CoopWs w) {
   const int r = blockIdx.x * 256 + threadIdx.x;
   if (r >= *w.n_runs) return;
   const uint32_t key = w.run_key[r];
-  if (key == kPadKey) return;
+  if (key == kPadKey) {
+    w.run_nch[r] = 0;
+    return;
+  }
   int kh, kl;
   decode_key(key, kh, kl);
   if (kh == kl) w.diag_run[kh] = r;
+  w.run_nch[r] = (w.run_cnt[r] + kChunk - 1) / kChunk;
+}
+
+// chunk -> run map (chunks of a run are consecutive, in pair order) and the chunk total.
+__global__ __launch_bounds__(256) void coop_chunks_kernel(CoopWs w) {
+  const int r = blockIdx.x * 256 + threadIdx.x, nr = *w.n_runs;
+  if (r >= nr) return;
+  const int c0 = w.run_ch0[r], nc = w.run_nch[r];
+  for (int k = 0; k < nc; k++) w.chunk_run[c0 + k] = r;
+  if (r == nr - 1) *w.n_chunks = c0 + nc;
 }
 
 // ---- the cooperative LM kernel ----------------------------------------------------------------
@@ -306,13 +353,23 @@ __device__ void lin_keyframes(const CoopWs& w, const CoopProblem& pb, const Pose
     }
     const double s = wave_reduce_scatter32(acc);
     if ((lane & 1) == 0 && (lane >> 1) < 27) w.hpp_part[((size_t)f * w.nch + c) * 27 + (lane >> 1)] = s;
+    if (last_arriver(&w.kf_arrive[f], w.nch) && lane < 27) {  // Hpp / bp totals, chunk order
+      const double* pp = w.hpp_part + (size_t)f * w.nch * 27 + lane;
+      double v[8];
+#pragma unroll
+      for (int k = 0; k < 8; k++) v[k] = k < w.nch ? pp[(size_t)k * 27] : 0.0;
+      double t = v[0];
+#pragma unroll
+      for (int k = 1; k < 8; k++) t = k < w.nch ? t + v[k] : t;
+      w.hpp_tot[(size_t)f * 27 + lane] = t;
+    }
   }
 }
 
-__device__ __forceinline__ double hpp_sum(const CoopWs& w, int f, int i) {
-  double s = 0.0;
-  for (int c = 0; c < w.nch; c++) s += w.hpp_part[((size_t)f * w.nch + c) * 27 + i];
-  return s;
+// An optimised keyframe with active edges in the current phase (a vertex of g2o's system).
+__device__ __forceinline__ bool kf_active(const CoopWs& w, int f) {
+  const int r = w.diag_run[f];
+  return r >= 0 && w.run_cnt[r] > 0;
 }
 
 __device__ __forceinline__ void dinv_point(const CoopWs& w, int p, double lambda, double Di[6]) {
@@ -324,174 +381,378 @@ __device__ __forceinline__ void dinv_point(const CoopWs& w, int p, double lambda
   inverse3_sym(D, Di);
 }
 
-// S blocks (a wave per distinct block, over its pairs in point order) and the reduced rhs of the
-// diagonal blocks: S(kh, kl) = [kh == kl](Hpp + lambda I) - sum Hpl_eh Dinv_p Hpl_el^T,
-// bs_k = bp_k - sum_e Hpl_e Dinv_p bl_p.
-__device__ void assemble(const CoopWs& w, const CoopProblem& pb, double lambda, int n_runs) {
-  const int lane = threadIdx.x & 63, n = 6 * pb.K;
+// S-block partial sums: a wave per chunk of kChunk pairs of one block (one pair per lane, in
+// point order), sum Hpl_eh Dinv_p Hpl_el^T and, on a diagonal block, sum Hpl_e Dinv_p bl_p; the
+// point's Dinv = (Hll + lambda I)^-1 formed on the fly. Work-group 0 adds a block's chunk
+// partials in chunk order when it builds S (build_S), so every sum has a fixed order.
+__device__ void assemble(const CoopWs& w, int K, double lambda, int n_chunks) {
+  const int lane = threadIdx.x & 63;
   const int nw = gridDim.x * kW;
-  for (int r = blockIdx.x * kW + (threadIdx.x >> 6); r < n_runs; r += nw) {
+  for (int ch = blockIdx.x * kW + (threadIdx.x >> 6); ch < n_chunks; ch += nw) {
+    const int r = w.chunk_run[ch];
+    int kh, kl;
+    decode_key(w.run_key[r], kh, kl);
+    const bool diag = kh == kl;
+    const int h = (ch - w.run_ch0[r]) * kChunk + lane;
+    // one pair per lane: B = Hpl_eh Dinv_p, then the block rows in two halves (rows 0-2 with
+    // the rhs terms, rows 3-5), each reduced across the wave by a 32-value reduce-scatter
+    double B[18], hp[18], db[3] = {0, 0, 0};
+    const bool valid = h < w.run_cnt[r];
+    int eh = 0, el = 0, p = 0;
+    if (valid) {
+      const int2 ep = w.vals[1][w.run_off[r] + h];
+      eh = ep.x;
+      el = diag ? ep.x : ep.y;
+      p = diag ? ep.y : w.opoint[ep.x];
+    }
+    {
+      double Di[6] = {0, 0, 0, 0, 0, 0};
+      if (valid) dinv_point(w, p, lambda, Di);
+      const double* hh = w.hpl + (size_t)eh * 18;
+#pragma unroll
+      for (int i = 0; i < 6; i++) {
+        const double h0 = valid ? hh[3 * i] : 0.0, h1 = valid ? hh[3 * i + 1] : 0.0,
+                     h2 = valid ? hh[3 * i + 2] : 0.0;
+        B[3 * i] = h0 * Di[0] + h1 * Di[1] + h2 * Di[2];
+        B[3 * i + 1] = h0 * Di[1] + h1 * Di[3] + h2 * Di[4];
+        B[3 * i + 2] = h0 * Di[2] + h1 * Di[4] + h2 * Di[5];
+      }
+      if (diag && valid) {  // Hpl_e Dinv_p bl_p = B bl_p
+        const double b0 = ptf(w, p, PB), b1 = ptf(w, p, PB + 1), b2 = ptf(w, p, PB + 2);
+        db[0] = b0;
+        db[1] = b1;
+        db[2] = b2;
+      }
+      const double* hpl = w.hpl + (size_t)el * 18;
+#pragma unroll
+      for (int i = 0; i < 18; i++) hp[i] = valid ? hpl[i] : 0.0;
+    }
+    double* out = w.chunk_part + (size_t)ch * kCP;
+    const int id = lane >> 1;
+#pragma unroll
+    for (int half = 0; half < 2; half++) {
+      double acc[32];
+#pragma unroll
+      for (int i = 0; i < 32; i++) acc[i] = 0.0;
+#pragma unroll
+      for (int rr = 0; rr < 3; rr++)
+#pragma unroll
+        for (int c = 0; c < 6; c++) {
+          const int ro = 3 * half + rr;
+          acc[6 * rr + c] = B[3 * ro] * hp[3 * c] + B[3 * ro + 1] * hp[3 * c + 1] +
+                            B[3 * ro + 2] * hp[3 * c + 2];
+        }
+      if (half == 0 && diag) {
+#pragma unroll
+        for (int i = 0; i < 6; i++) acc[18 + i] = B[3 * i] * db[0] + B[3 * i + 1] * db[1] + B[3 * i + 2] * db[2];
+      }
+      const double sv = wave_reduce_scatter32(acc);
+      // partial layout: [0, 36) the block row-major, [36, 42) the rhs terms
+      if ((lane & 1) == 0) {
+        if (id < 18) out[18 * half + id] = sv;
+        else if (half == 0 && id < 24) out[36 + id - 18] = sv;
+      }
+    }
+    // the run's last chunk to finish sums the run's chunk partials in chunk order and writes
+    // S(kh, kl) = [kh == kl](Hpp + lambda I) - sum, bs = bp - sum into the dense S / bs
+    const int nch = w.run_nch[r];
+    if (!last_arriver(&w.run_arrive[r], nch) || lane >= kCP) continue;
+    if (!diag && lane >= 36) continue;
+    const int rr = lane / 6, c = lane % 6;
+    if (lane < 36 && diag && c > rr) continue;
+    const double* pp = w.chunk_part + (size_t)w.run_ch0[r] * kCP + lane;
+    double sv = 0.0;
+    int k = 0;
+    for (; k + 4 <= nch; k += 4) {  // four loads in flight per step
+      const double a0 = pp[(size_t)k * kCP], a1 = pp[(size_t)(k + 1) * kCP];
+      const double a2 = pp[(size_t)(k + 2) * kCP], a3 = pp[(size_t)(k + 3) * kCP];
+      sv = (((sv + a0) + a1) + a2) + a3;
+    }
+    for (; k < nch; k++) sv += pp[(size_t)k * kCP];
+    const int n = 6 * K;
+    if (lane < 36) {
+      double base = 0.0;
+      if (diag) base = w.hpp_tot[(size_t)kh * 27 + hidx(c, rr)] + (rr == c ? lambda : 0.0);
+      w.S[(size_t)(6 * kh + rr) * n + 6 * kl + c] = base - sv;
+    } else {
+      w.bs[6 * kh + lane - 36] = w.hpp_tot[(size_t)kh * 27 + 21 + lane - 36] - sv;
+    }
+  }
+}
+
+// Work-group 0: S (packed lower, at Lp) and the reduced rhs from the dense S / bs the runs'
+// last chunks wrote (8 loads in flight per thread); the rows of an optimised keyframe left
+// without active edges (not in g2o's system) become I with rhs 0.
+template <typename PtrT>
+__device__ __forceinline__ void build_S(const CoopWs& w, int K, double lambda, PtrT Lp, PtrT rhs) {
+  const int tid = threadIdx.x, n = 6 * K, nl = n * (n + 1) / 2;
+  for (int q0 = tid; q0 < nl; q0 += 8 * kT) {
+    double v[8];
+#pragma unroll
+    for (int u = 0; u < 8; u++) {
+      const int q = q0 + u * kT;
+      int i = 0, j = 0;
+      if (q < nl) {
+        i = (int)((sqrt(8.0 * (double)q + 1.0) - 1.0) * 0.5);
+        while (tri(i + 1) <= q) i++;
+        while (tri(i) > q) i--;
+        j = q - tri(i);
+      }
+      v[u] = q < nl ? w.S[(size_t)i * n + j] : 0.0;
+    }
+#pragma unroll
+    for (int u = 0; u < 8; u++)
+      if (q0 + u * kT < nl) Lp[q0 + u * kT] = v[u];
+  }
+  for (int i = tid; i < n; i += kT) rhs[i] = w.bs[i];
+  __syncthreads();
+  for (int t = tid; t < 6 * K; t += kT) {
+    const int f = t / 6, i = t - 6 * f;
+    if (kf_active(w, f)) continue;
+    Lp[sidx(6 * f + i, 6 * f + i)] = 1.0;
+    rhs[6 * f + i] = 0.0;
+  }
+  __syncthreads();
+}
+
+__device__ __forceinline__ double rl64(double x, int l) {  // v_readlane of a double
+  const uint64_t u = __builtin_bit_cast(uint64_t, x);
+  const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)u, l);
+  const uint32_t hi = __builtin_amdgcn_readlane((uint32_t)(u >> 32), l);
+  return __builtin_bit_cast(double, (uint64_t)hi << 32 | lo);
+}
+
+// LDLT of S (6x6 block columns, right-looking, forward solve fused) by work-group 0. L is packed
+// lower at Lp (LDS, or the global scratch for 6K > kCoopLdsN), row i at offset tri(i). Per block
+// column J: wave 0 factors the 6x6 diagonal block (lanes 0-5 hold its rows; one reciprocal per
+// pivot, multipliers exchanged by v_readlane), a thread per row
+// below forms V = A_iJ L_JJ^-T and L_iJ = V D_J^-1 and updates the rhs, then a wave per group of
+// 4 trailing rows (lanes over the columns k <= i) subtracts L_iJ V_kJ^T. Then z = D^-1 y and the
+// backward solve L^T x = z, a 6x6 block at a time. Sets sh.ok (0 on an exact zero pivot, as
+// Eigen's SimplicialLDLT fails); on success writes the solution to w.xp (a failed solve keeps the
+// previous step, which g2o applies anyway: optimization_algorithm_levenberg.cpp:107-109).
+template <typename PtrT>
+__device__ __forceinline__ void factor_solve(CoopShared& sh, const CoopWs& w, int K, PtrT Lp,
+                                             PtrT rhs, PtrT dg, PtrT V) {
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, n = 6 * K;
+  if (tid == 0) sh.ok = 1;
+  __syncthreads();
+  for (int J = 0; J < K; J++) {
+    const int j0 = 6 * J;
+    if (wid == 0) {  // diagonal block: lane r < 6 holds row r; pivots and multipliers by readlane
+      const bool row = lane < 6;
+      const int ro = tri(j0 + (row ? lane : 0)) + j0;
+      double A[6], y = row ? rhs[j0 + lane] : 0.0;
+#pragma unroll
+      for (int k = 0; k < 6; k++) A[k] = row && k <= lane ? Lp[ro + k] : 0.0;
+      bool good = true;
+#pragma unroll
+      for (int c = 0; c < 6; c++) {
+        const double d = rl64(A[c], c);
+        good = good && d != 0.0;
+        const double rd = d != 0.0 ? 1.0 / d : 0.0;
+        const bool below = row && lane > c;
+        const double l = below ? A[c] * rd : 0.0;
+        const double yc = rl64(y, c);
+        if (below) {
+          y -= l * yc;
+          A[c] = l;
+        }
+        const double ld = l * d;
+#pragma unroll
+        for (int k = c + 1; k < 6; k++) {
+          const double lk = rl64(l, k);
+          if (row && lane >= k) A[k] -= ld * lk;
+        }
+      }
+      if (row) {
+        double dr = A[0];
+#pragma unroll
+        for (int k = 0; k < 6; k++) {
+          if (k < lane) Lp[ro + k] = A[k];
+          if (k == lane) dr = A[k];
+        }
+        dg[j0 + lane] = dr;
+        rhs[j0 + lane] = y;
+      }
+      if (lane == 0 && !good) sh.ok = 0;
+    }
+    __syncthreads();
+    if (!sh.ok) return;
+    {  // panel rows below the diagonal block
+      double Ljj[15], idg[6], yj[6];
+      int q = 0;
+#pragma unroll
+      for (int c = 1; c < 6; c++)
+#pragma unroll
+        for (int k = 0; k < c; k++) Ljj[q++] = Lp[tri(j0 + c) + j0 + k];
+#pragma unroll
+      for (int c = 0; c < 6; c++) {
+        idg[c] = 1.0 / dg[j0 + c];
+        yj[c] = rhs[j0 + c];
+      }
+      for (int i = j0 + 6 + tid; i < n; i += kT) {
+        const int ro = tri(i) + j0;
+        double v[6];
+        q = 0;
+#pragma unroll
+        for (int c = 0; c < 6; c++) {
+          double s = Lp[ro + c];
+#pragma unroll
+          for (int k = 0; k < c; k++) s -= v[k] * Ljj[q++];
+          v[c] = s;
+        }
+        double r = rhs[i];
+#pragma unroll
+        for (int c = 0; c < 6; c++) {
+          V[(size_t)i * 6 + c] = v[c];
+          const double l = v[c] * idg[c];
+          Lp[ro + c] = l;
+          r -= l * yj[c];
+        }
+        rhs[i] = r;
+      }
+    }
+    __syncthreads();
+    // trailing update: a wave per group of 4 rows (i, i + kW, i + 2 kW, i + 3 kW), lanes over
+    // the columns k <= i; the rows' independent chains interleave and V_k is read once per group
+    for (int i = j0 + 6 + wid; i < n; i += 4 * kW) {
+      int ro[4];
+      double l[4][6];
+#pragma unroll
+      for (int a = 0; a < 4; a++) {
+        const int ia = i + a * kW;
+        ro[a] = ia < n ? tri(ia) : 0;
+#pragma unroll
+        for (int c = 0; c < 6; c++) l[a][c] = ia < n ? Lp[ro[a] + j0 + c] : 0.0;
+      }
+      const int imax = min(i + 3 * kW, n - 1);
+      for (int k = j0 + 6 + lane; k <= imax; k += 64) {
+        double v[6];
+#pragma unroll
+        for (int c = 0; c < 6; c++) v[c] = V[(size_t)k * 6 + c];
+        double s[4];
+#pragma unroll
+        for (int a = 0; a < 4; a++) s[a] = k <= i + a * kW && i + a * kW < n ? Lp[ro[a] + k] : 0.0;
+#pragma unroll
+        for (int a = 0; a < 4; a++) {
+#pragma unroll
+          for (int c = 0; c < 6; c++) s[a] -= l[a][c] * v[c];
+          if (k <= i + a * kW && i + a * kW < n) Lp[ro[a] + k] = s[a];
+        }
+      }
+    }
+    __syncthreads();
+  }
+  if (wid == 0) {  // z = D^-1 y; L^T x = z from the last 6x6 block up
+    for (int i = lane; i < n; i += 64) rhs[i] /= dg[i];
+    for (int J = K - 1; J >= 0; J--) {
+      const int j0 = 6 * J;
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+      // within the block: lane r < 6 holds x_r; x_c final when c is reached (descending)
+      double xv = lane < 6 ? rhs[j0 + lane] : 0.0;
+#pragma unroll
+      for (int c = 5; c >= 0; c--) {
+        const double xc = rl64(xv, c);
+        if (lane < c) xv -= Lp[tri(j0 + c) + j0 + lane] * xc;
+      }
+      if (lane < 6) rhs[j0 + lane] = xv;
+      double x[6];
+#pragma unroll
+      for (int c = 0; c < 6; c++) x[c] = rl64(xv, c);
+      for (int i = lane; i < j0; i += 64) {  // earlier rows: z_i -= sum_c L(j0 + c, i) x_c
+        double sx = rhs[i];
+#pragma unroll
+        for (int c = 0; c < 6; c++) sx -= Lp[tri(j0 + c) + i] * x[c];
+        rhs[i] = sx;
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    for (int i = lane; i < n; i += 64) w.xp[i] = rhs[i];
+  }
+  __syncthreads();
+}
+
+// optimizer.cpp:632-665 between the two optimize() calls: chi2 > threshold or depth <= 0 ->
+// level 1 (edge-parallel over the grid).
+__device__ void mark_outliers(const CoopWs& w, const CoopProblem& pb, const PoseParams& P,
+                              const float* isig) {
+  for (int ge = blockIdx.x * kT + threadIdx.x; ge < pb.n_obs; ge += gridDim.x * kT) {
+    const int p = w.opoint[ge];
+    const double X[3] = {ptf(w, p, PX), ptf(w, p, PX + 1), ptf(w, p, PX + 2)};
+    const slamgpu_ba_obs o = pb.obs[ge];
+    ObsEval v;
+    eval_obs(o, P, isig, kfr(w, o.keyframe), X, v);
+    if (w.chi2[ge] > (o.ur >= 0 ? 7.815 : 5.991) || !(v.z > 0.0)) w.act[ge] = 0;
+  }
+}
+
+// The next phase's S-block pair lists: each run's pairs filtered to the active edges in place,
+// in order (a wave per run, ballot prefix counts), so the block structure needs no new sort.
+__device__ void compact_runs(const CoopWs& w, int n_runs, int n) {
+  const int lane = threadIdx.x & 63;
+  for (int r = blockIdx.x * kW + (threadIdx.x >> 6); r < n_runs; r += gridDim.x * kW) {
     const uint32_t key = w.run_key[r];
     if (key == kPadKey) continue;
     int kh, kl;
     decode_key(key, kh, kl);
     const bool diag = kh == kl;
-    const int cnt = w.run_cnt[r], off = w.run_off[r];
-    double acc[64];
-#pragma unroll
-    for (int i = 0; i < 64; i++) acc[i] = 0.0;
-    for (int h = lane; h < cnt; h += 64) {
-      const int2 ep = w.vals[1][off + h];
-      const int eh = ep.x, el = diag ? ep.x : ep.y, p = diag ? ep.y : w.opoint[ep.x];
-      double Di[6];
-      dinv_point(w, p, lambda, Di);
-      const double* hh = w.hpl + (size_t)eh * 18;
-      const double* hp = w.hpl + (size_t)el * 18;
-      double B[18];
-#pragma unroll
-      for (int i = 0; i < 6; i++) {
-        const double h0 = hh[3 * i], h1 = hh[3 * i + 1], h2 = hh[3 * i + 2];
-        B[3 * i] = h0 * Di[0] + h1 * Di[1] + h2 * Di[2];
-        B[3 * i + 1] = h0 * Di[1] + h1 * Di[3] + h2 * Di[4];
-        B[3 * i + 2] = h0 * Di[2] + h1 * Di[4] + h2 * Di[5];
+    const int off = w.run_off[r], cnt = w.run_cnt[r];
+    int kept = 0;
+    for (int h0 = 0; h0 < cnt; h0 += 64) {
+      const int h = h0 + lane;
+      int2 ep = make_int2(0, 0);
+      bool keep = false;
+      if (h < cnt) {
+        ep = w.vals[1][off + h];
+        keep = w.act[ep.x] && (diag || w.act[ep.y]);
       }
-#pragma unroll
-      for (int rr = 0; rr < 6; rr++)
-#pragma unroll
-        for (int c = 0; c < 6; c++)
-          acc[6 * rr + c] += B[3 * rr] * hp[3 * c] + B[3 * rr + 1] * hp[3 * c + 1] +
-                             B[3 * rr + 2] * hp[3 * c + 2];
-      if (diag) {
-        const double b0 = ptf(w, p, PB), b1 = ptf(w, p, PB + 1), b2 = ptf(w, p, PB + 2);
-        const double d0 = Di[0] * b0 + Di[1] * b1 + Di[2] * b2;
-        const double d1 = Di[1] * b0 + Di[3] * b1 + Di[4] * b2;
-        const double d2 = Di[2] * b0 + Di[4] * b1 + Di[5] * b2;
-#pragma unroll
-        for (int i = 0; i < 6; i++) acc[36 + i] += hh[3 * i] * d0 + hh[3 * i + 1] * d1 + hh[3 * i + 2] * d2;
-      }
+      const uint64_t bal = __ballot(keep);
+      if (keep) w.vals[1][off + kept + lanes_below(bal)] = ep;  // in place: never past h
+      kept += __popcll(bal);
     }
-    const double s0 = wave_reduce_scatter32(acc), s1 = wave_reduce_scatter32(acc + 32);
-    const int idx = lane >> 1;
-#pragma unroll
-    for (int part = 0; part < 2; part++) {
-      const int id = idx + 32 * part;
-      if ((lane & 1) != 0) continue;
-      const double sv = part ? s1 : s0;
-      if (id < 36) {
-        const int rr = id / 6, c = id % 6;
-        const int i = 6 * kh + rr, j = 6 * kl + c;
-        if (!diag || j <= i) {
-          double base = 0.0;
-          if (diag) base = hpp_sum(w, kh, hidx(c < rr ? c : rr, c < rr ? rr : c)) + (rr == c ? lambda : 0.0);
-          w.S[(size_t)i * n + j] = base - sv;
-        }
-      } else if (diag && id < 42) {
-        const int i = id - 36;
-        w.bs[6 * kh + i] = hpp_sum(w, kh, 21 + i) - sv;
-      }
+    if (lane == 0) {
+      w.run_cnt[r] = kept;
+      w.run_nch[r] = (kept + kChunk - 1) / kChunk;
     }
+    if (kept == 0 && cnt > 0 && lane < 36)  // the block left the system: no chunk rewrites it
+      w.S[(size_t)(6 * kh + lane / 6) * n + 6 * kl + lane % 6] = 0.0;
   }
 }
 
-// LDLT of S (6x6 block columns, right-looking, forward solve fused) by work-group 0, the same
-// algorithm as ba_kernels.hip's factor_solve. L is packed lower at Lp (LDS or the global
-// scratch). Sets sh.ok; on success writes the solution to w.xp (a failed solve keeps the previous
-// step, which g2o applies anyway: optimization_algorithm_levenberg.cpp:107-109).
-__device__ void factor_solve(CoopShared& sh, const CoopWs& w, int K, double* Lp, double* rhs,
-                             double* dg, double* V) {
-  const int tid = threadIdx.x, lane = tid & 63, n = 6 * K;
-  for (int i = tid; i < n; i += kT) {
-    rhs[i] = w.bs[i];
-    for (int j = 0; j <= i; j++) Lp[sidx(i, j)] = w.S[(size_t)i * n + j];
-  }
-  if (tid == 0) sh.ok = 1;
+// Work-group 0: chunk offsets (exclusive scan of run_nch over the runs: a contiguous segment per
+// thread, then the segment sums in order) and the chunk -> run map; returns the chunk count.
+__device__ int rebuild_chunks(CoopShared& sh, const CoopWs& w, int n_runs) {
+  const int tid = threadIdx.x, seg = (n_runs + kT - 1) / kT;
+  const int r0 = min(tid * seg, n_runs), r1 = min(r0 + seg, n_runs);
+  int sum = 0;
+  for (int r = r0; r < r1; r++) sum += w.run_nch[r];
+  sh.iscan[tid] = sum;
   __syncthreads();
-  for (int J = 0; J < K; J++) {
-    const int j0 = 6 * J;
-    if (tid == 0) {
-      double A[6][6], d[6], y[6];
-#pragma unroll
-      for (int i = 0; i < 6; i++) {
-#pragma unroll
-        for (int j = 0; j <= i; j++) A[i][j] = Lp[sidx(j0 + i, j0 + j)];
-        y[i] = rhs[j0 + i];
-      }
-      bool good = true;
-#pragma unroll
-      for (int j = 0; j < 6; j++) {
-        double dj = A[j][j];
-#pragma unroll
-        for (int k = 0; k < j; k++) dj -= A[j][k] * A[j][k] * d[k];
-        good = good && dj != 0.0;
-        d[j] = dj;
-#pragma unroll
-        for (int i = j + 1; i < 6; i++) {
-          double s = A[i][j];
-#pragma unroll
-          for (int k = 0; k < j; k++) s -= A[i][k] * A[j][k] * d[k];
-          A[i][j] = dj != 0.0 ? s / dj : 0.0;
-        }
-      }
-#pragma unroll
-      for (int i = 0; i < 6; i++) {
-#pragma unroll
-        for (int k = 0; k < i; k++) y[i] -= A[i][k] * y[k];
-      }
-#pragma unroll
-      for (int i = 0; i < 6; i++) {
-        dg[j0 + i] = d[i];
-        rhs[j0 + i] = y[i];
-#pragma unroll
-        for (int j = 0; j < i; j++) Lp[sidx(j0 + i, j0 + j)] = A[i][j];
-      }
-      if (!good) sh.ok = 0;
+  if (tid == 0) {
+    int acc = 0;
+    for (int t = 0; t < kT; t++) {
+      const int v = sh.iscan[t];
+      sh.iscan[t] = acc;
+      acc += v;
     }
-    __syncthreads();
-    if (!sh.ok) return;
-    for (int i = j0 + 6 + tid; i < n; i += kT) {
-      double v[6];
-      for (int c = 0; c < 6; c++) {
-        double s = Lp[sidx(i, j0 + c)];
-        for (int k = 0; k < c; k++) s -= v[k] * Lp[sidx(j0 + c, j0 + k)];
-        v[c] = s;
-      }
-      double r = rhs[i];
-      for (int c = 0; c < 6; c++) {
-        V[(size_t)i * 6 + c] = v[c];
-        const double l = v[c] / dg[j0 + c];
-        Lp[sidx(i, j0 + c)] = l;
-        r -= l * rhs[j0 + c];
-      }
-      rhs[i] = r;
-    }
-    __syncthreads();
-    const int m = n - j0 - 6;
-    for (int q = tid; q < m * m; q += kT) {
-      const int ii = q / m, kk = q - ii * m;
-      if (kk > ii) continue;
-      const int i = j0 + 6 + ii, k = j0 + 6 + kk;
-      double s = Lp[sidx(i, k)];
-#pragma unroll
-      for (int c = 0; c < 6; c++) s -= Lp[sidx(i, j0 + c)] * V[(size_t)k * 6 + c];
-      Lp[sidx(i, k)] = s;
-    }
-    __syncthreads();
-  }
-  if ((tid >> 6) == 0) {
-    for (int i = lane; i < n; i += 64) rhs[i] /= dg[i];
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-    for (int k = n - 1; k > 0; k--) {
-      const double xk = rhs[k];
-      for (int i = lane; i < k; i += 64) rhs[i] -= Lp[sidx(k, i)] * xk;
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-    }
-    for (int i = lane; i < n; i += 64) w.xp[i] = rhs[i];
+    sh.itot = acc;
   }
   __syncthreads();
+  int c = sh.iscan[tid];
+  for (int r = r0; r < r1; r++) {
+    const int nc = w.run_nch[r];
+    w.run_ch0[r] = c;
+    for (int k = 0; k < nc; k++) w.chunk_run[c + k] = r;
+    c += nc;
+  }
+  const int total = sh.itot;
+  __syncthreads();
+  return total;
 }
 
 __device__ void restore_estimates(const CoopWs& w, const CoopProblem& pb) {
@@ -499,7 +760,7 @@ __device__ void restore_estimates(const CoopWs& w, const CoopProblem& pb) {
   for (int p = blockIdx.x * kT + threadIdx.x; p < pb.n_pts; p += GT)
     for (int i = 0; i < 3; i++) ptf(w, p, PX + i) = ptf(w, p, PXB + i);
   for (int f = blockIdx.x * kT + threadIdx.x; f < pb.K; f += GT) {
-    if (w.diag_run[f] < 0) continue;
+    if (!kf_active(w, f)) continue;
     double* kr = kfr(w, w.kf_of_free[f]);
     SE3 T;
     T.r.x = kr[KBQ];
@@ -512,7 +773,7 @@ __device__ void restore_estimates(const CoopWs& w, const CoopProblem& pb) {
 }
 
 __global__ __launch_bounds__(kT) void ba_coop_kernel(PoseParams P, CoopProblem pb, CoopWs w,
-                                                     CoopPhase ph, const int32_t* stop_flag) {
+                                                     CoopSchedule sch, const int32_t* stop_flag) {
 #pragma clang fp contract(fast)  // tolerance-compared FP64 path
   __shared__ CoopShared sh;
   const int tid = threadIdx.x, wg = blockIdx.x, GT = gridDim.x * kT;
@@ -520,15 +781,53 @@ __global__ __launch_bounds__(kT) void ba_coop_kernel(PoseParams P, CoopProblem p
   if (tid < SLAMGPU_MAX_LEVELS) sh.isig[tid] = P.inv_sigma2[tid];
   const int K = pb.K, n = 6 * K;
   const int n_runs = *w.n_runs;
-  double* Lp = n <= kCoopLdsN ? sh.S : w.fac;
-  double* Vp = n <= kCoopLdsN ? sh.V : w.fac + (size_t)n * (n + 1) / 2;
-  double* dgp = n <= kCoopLdsN ? sh.dg : Vp + (size_t)6 * n;
-  double* rhsp = n <= kCoopLdsN ? sh.rhs : dgp + n;
+  int n_chunks = *w.n_chunks;
+  // factor storage: LDS (explicit address space, so every access is a ds_ op) or the global
+  // scratch for systems past kCoopLdsN
+  typedef __attribute__((address_space(3))) double* LdsPtr;
+  const bool in_lds = n <= kCoopLdsN;
+  double* const Gp = w.fac;
+  double* const Gv = Gp + (size_t)n * (n + 1) / 2;
+  double* const Gd = Gv + (size_t)6 * n;
+  double* const Gr = Gd + n;
+  // optional per-phase wall clock of work-group 0 (s_memrealtime: 100 MHz)
+  double pacc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  uint64_t pt0 = __builtin_amdgcn_s_memrealtime();
+  auto tick = [&](int slot) {
+    if (w.prof && wg == 0) {
+      const uint64_t t = __builtin_amdgcn_s_memrealtime();
+      pacc[slot] += 0.01 * (double)(t - pt0);
+      pt0 = t;
+    }
+  };
+  int lm_total = 0;
+  bool stopped = false;
+  for (int phs = 0; phs < sch.n_phases; phs++) {
+  const CoopPhase ph = sch.ph[phs];
+  if (phs > 0) {
+    grid_sync(w, stop_flag, true);  // optimizer.cpp:625-627: do_more
+    if (ctl_load(w, CTL_POLL)) {
+      stopped = true;
+      break;
+    }
+    if (sch.outlier_pass) {  // level-1 outliers, then the next phase's block pair lists
+      mark_outliers(w, pb, P, sh.isig);
+      grid_sync(w, stop_flag, false);
+      compact_runs(w, n_runs, n);
+      grid_sync(w, stop_flag, false);
+      if (wg == 0) {
+        const int nc = rebuild_chunks(sh, w, n_runs);
+        if (tid == 0) *w.n_chunks = nc;
+      }
+      grid_sync(w, stop_flag, false);
+      n_chunks = *w.n_chunks;
+    }
+  }
   grid_sync(w, stop_flag, true);  // the first iteration's terminate() poll
+  tick(7);
   bool stop = ctl_load(w, CTL_POLL) != 0;
   double lambda = 0.0;
-  int ni = 2, nbad = 0, lm_total = 0;
-  bool stopped = false;
+  int ni = 2, nbad = 0;
   for (int it = 0; it < ph.iterations; it++) {
     if (stop) {  // optimize(): i < iterations && !terminate()
       stopped = true;
@@ -540,16 +839,25 @@ __global__ __launch_bounds__(kT) void ba_coop_kernel(PoseParams P, CoopProblem p
     lin_keyframes(w, pb, P, sh.isig, ph);
     wg_part(sh, w, chi, 0, false);
     wg_part(sh, w, maxd, 1, true);
+    tick(0);
     grid_sync(w, stop_flag, false);
-    double currentChi = grid_total(w, 0, false);
+    tick(1);
+    grid_totals(sh, w, 0, 1, false);
+    double currentChi = sh.tot[0];
     const double iniChi = currentChi;
     if (it == 0) {  // computeLambdaInit over the active vertices
-      double m = grid_total(w, 1, true);
-      for (int f = 0; f < K; f++) {
-        if (w.diag_run[f] < 0) continue;
+      double m = 0.0;
+      for (int t = tid; t < 6 * K; t += kT) {
+        const int f = t / 6, i = t - 6 * f;
         const int dgi[6] = {0, 6, 11, 15, 18, 20};
-        for (int i = 0; i < 6; i++) m = fmax(m, fabs(hpp_sum(w, f, dgi[i])));
+        if (kf_active(w, f)) m = fmax(m, fabs(w.hpp_tot[(size_t)f * 27 + dgi[i]]));
       }
+      m = wave_max(m);
+      if ((tid & 63) == 0) sh.red[tid >> 6] = m;
+      grid_totals(sh, w, 1, 1, true);  // (its barriers also publish sh.red)
+      m = sh.tot[0];
+      for (int k = 0; k < kW; k++) m = fmax(m, sh.red[k]);
+      __syncthreads();
       lambda = 1e-5 * m;
       ni = 2;
       nbad = 0;
@@ -559,20 +867,31 @@ __global__ __launch_bounds__(kT) void ba_coop_kernel(PoseParams P, CoopProblem p
     bool rejected = false;
     do {
       // ---- S, reduced rhs (and the pop of a rejected trial's estimates) ----
-      assemble(w, pb, lambda, n_runs);
+      assemble(w, K, lambda, n_chunks);
       if (rejected) restore_estimates(w, pb);
+      tick(2);
       grid_sync(w, stop_flag, false);
+      tick(1);
       // ---- work-group 0: factor + solve, keyframe update (backup first) ----
       if (wg == 0) {
-        factor_solve(sh, w, K, Lp, rhsp, dgp, Vp);
+        if (in_lds) {
+          build_S(w, K, lambda, (LdsPtr)sh.S, (LdsPtr)sh.rhs);
+          tick(5);
+          factor_solve(sh, w, K, (LdsPtr)sh.S, (LdsPtr)sh.rhs, (LdsPtr)sh.dg, (LdsPtr)sh.V);
+        } else {
+          build_S(w, K, lambda, Gp, Gr);
+          tick(5);
+          factor_solve(sh, w, K, Gp, Gr, Gd, Gv);
+        }
+        tick(6);
         double sc = 0.0;
         for (int f = tid; f < K; f += kT) {
-          if (w.diag_run[f] < 0) continue;
+          if (!kf_active(w, f)) continue;
           double* kr = kfr(w, w.kf_of_free[f]);
           double x[6];
           for (int i = 0; i < 6; i++) {
             x[i] = w.xp[6 * f + i];
-            sc += x[i] * (lambda * x[i] + hpp_sum(w, f, 21 + i));
+            sc += x[i] * (lambda * x[i] + w.hpp_tot[(size_t)f * 27 + 21 + i]);
           }
           SE3 T;
           load_T(kr, T);
@@ -583,7 +902,9 @@ __global__ __launch_bounds__(kT) void ba_coop_kernel(PoseParams P, CoopProblem p
         wg_part(sh, w, sc, 4, false);  // work-group 0's slot 4: the keyframe share of `scale`
         if (tid == 0) w.ctl[CTL_OK] = sh.ok;
       }
+      tick(3);
       grid_sync(w, stop_flag, false);
+      tick(1);
       const bool ok = ctl_load(w, CTL_OK) != 0;
       // ---- points: back-substitution, update (backup first), errors of their edges ----
       double scale = 0.0, temp = 0.0;
@@ -636,10 +957,13 @@ __global__ __launch_bounds__(kT) void ba_coop_kernel(PoseParams P, CoopProblem p
       }
       wg_part(sh, w, temp, 2, false);
       wg_part(sh, w, scale, 3, false);
+      tick(4);
       grid_sync(w, stop_flag, true);  // carries the trial loop's terminate() poll
+      tick(1);
       stop = ctl_load(w, CTL_POLL) != 0;
-      const double tempChi = ok ? grid_total(w, 2, false) : DBL_MAX;
-      double sc = grid_total(w, 3, false) + w.part[4];
+      grid_totals(sh, w, 2, 2, false);
+      const double tempChi = ok ? sh.tot[0] : DBL_MAX;
+      double sc = sh.tot[1] + w.part[4];
       sc += 1e-3;
       rho = (currentChi - tempChi) / sc;
       if (rho > 0 && isfinite(tempChi)) {
@@ -666,37 +990,21 @@ __global__ __launch_bounds__(kT) void ba_coop_kernel(PoseParams P, CoopProblem p
     else nbad = 0;
     if (nbad >= 3) break;
   }
+  if (stopped) break;
+  }  // phases
+  if (w.prof && wg == 0 && tid == 0)
+    for (int i = 0; i < 8; i++) w.prof[i] += pacc[i];
   if (wg == 0 && tid == 0) {
     w.ctl[CTL_LM] += lm_total;
     if (stopped) w.ctl[CTL_STOPPED] = 1;
   }
 }
 
-// ---- between the phases and after ------------------------------------------------------------
-// optimizer.cpp:625-627: the stop flag is read once more before the second optimize().
-__global__ void coop_poll_kernel(CoopWs w, const int32_t* stop_flag) {
-  if (threadIdx.x == 0 && stop_flag &&
-      __hip_atomic_load(stop_flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0)
-    w.ctl[CTL_STOPPED] = 1;
-}
-
-// optimizer.cpp:632-665: chi2 > threshold or depth <= 0 -> level 1 (unless stopped).
-__global__ __launch_bounds__(256) void coop_outlier_kernel(PoseParams P, CoopProblem pb, CoopWs w) {
-  const int ge = blockIdx.x * 256 + threadIdx.x;
-  if (ge >= pb.n_obs || w.ctl[CTL_STOPPED] || w.ctl[CTL_ERR]) return;
-  float isig[SLAMGPU_MAX_LEVELS];
-  for (int i = 0; i < P.nlevels; i++) isig[i] = P.inv_sigma2[i];
-  const int p = w.opoint[ge];
-  const double X[3] = {ptf(w, p, PX), ptf(w, p, PX + 1), ptf(w, p, PX + 2)};
-  const slamgpu_ba_obs o = pb.obs[ge];
-  ObsEval v;
-  eval_obs(o, P, isig, kfr(w, o.keyframe), X, v);
-  if (w.chi2[ge] > (o.ur >= 0 ? 7.815 : 5.991) || !(v.z > 0.0)) w.act[ge] = 0;
-}
-
+// ---- after the schedule ----------------------------------------------------------------------
 // optimizer.cpp:672-700 erase list (LocalBA), :702-716 / :170-206 write-back.
 __global__ __launch_bounds__(256) void coop_finish_kernel(PoseParams P, CoopProblem pb, CoopWs w) {
   const int i = blockIdx.x * 256 + threadIdx.x;
+  if (pb.ctl_out && i < 8) pb.ctl_out[i] = w.ctl[i];  // next to the outputs: one readback
   if (w.ctl[CTL_ERR]) return;
   if (pb.erase && i < pb.n_obs) {
     float isig[SLAMGPU_MAX_LEVELS];
@@ -776,8 +1084,17 @@ CoopWs coop_layout(void* base, int n_kf, int n_pts, int n_obs, int K, int pairs_
   w.run_off = reinterpret_cast<int32_t*>(take(4 * (size_t)pc));
   w.n_runs = reinterpret_cast<int32_t*>(take(4));
   w.diag_run = reinterpret_cast<int32_t*>(take(4 * (size_t)K + 4));
-  w.nch = std::max(1, std::min(32, (G * kW) / std::max(K, 1)));
+  w.run_nch = reinterpret_cast<int32_t*>(take(4 * (size_t)pc));
+  w.run_ch0 = reinterpret_cast<int32_t*>(take(4 * (size_t)pc));
+  w.n_chunks = reinterpret_cast<int32_t*>(take(4));
+  const size_t chunk_cap = std::min<size_t>((size_t)pc, (size_t)K * (K + 1) / 2 + pc / kChunk + 1);
+  w.chunk_run = reinterpret_cast<int32_t*>(take(4 * chunk_cap));
+  w.chunk_part = reinterpret_cast<double*>(take(8 * kCP * chunk_cap));
+  w.nch = std::max(1, std::min(8, (G * kW) / std::max(K, 1)));
   w.hpp_part = reinterpret_cast<double*>(take(8 * 27 * (size_t)K * w.nch + 8));
+  w.hpp_tot = reinterpret_cast<double*>(take(8 * 27 * (size_t)K + 8));
+  w.kf_arrive = reinterpret_cast<int32_t*>(take(4 * (size_t)K + 4));
+  w.run_arrive = reinterpret_cast<int32_t*>(take(4 * (size_t)pc));
   w.S = reinterpret_cast<double*>(take(8 * (size_t)n * n + 8));
   w.bs = reinterpret_cast<double*>(take(8 * (size_t)n + 8));
   w.fac = reinterpret_cast<double*>(
@@ -786,6 +1103,7 @@ CoopWs coop_layout(void* base, int n_kf, int n_pts, int n_obs, int K, int pairs_
   w.part = reinterpret_cast<double*>(take(8 * 8 * (size_t)(G + 1)));
   w.bar = reinterpret_cast<uint32_t*>(take(64));
   w.ctl = reinterpret_cast<int32_t*>(take(64));
+  w.prof = reinterpret_cast<double*>(take(128));
   w.pairs_cap = pc;
   w.end_bit = key_bits(K);
   w.cub_bytes = cub_bytes_needed(pc, w.end_bit);
@@ -802,15 +1120,9 @@ hipError_t launch_coop_ba(const PoseParams& P, const CoopProblem& pb, const Coop
   auto blocks = [](int n) { return dim3((unsigned)std::max(1, (n + 255) / 256)); };
   const int nmax = std::max(std::max(pb.n_kf, pb.n_pts), std::max(pb.n_obs, 6 * pb.K + 8));
   SLAMGPU_LAUNCH("ba_coop_setup", st, coop_setup_kernel, blocks(nmax), dim3(256), 0, st, pb, w);
-  for (int ph = 0; ph < n_phases; ph++) {
-    if (ph > 0) {
-      if (outlier_pass) {
-        SLAMGPU_LAUNCH("ba_coop_poll", st, coop_poll_kernel, dim3(1), dim3(64), 0, st, w, d_stop);
-        SLAMGPU_LAUNCH("ba_coop_outlier", st, coop_outlier_kernel, blocks(pb.n_obs), dim3(256), 0,
-                       st, P, pb, w);
-      }
-    }
-    // structure of the active edge set: pairs per point -> offsets -> keys -> sorted runs
+  {
+    // structure of the first phase's active edge set: pairs per point -> offsets -> keys ->
+    // sorted runs -> chunks (the second phase filters these lists in the kernel)
     SLAMGPU_LAUNCH("ba_coop_sort", st, coop_sort_kernel, blocks(pb.n_pts + 1), dim3(256), 0, st,
                    pb, w);
     size_t tb = w.cub_bytes;
@@ -833,14 +1145,24 @@ hipError_t launch_coop_ba(const PoseParams& P, const CoopProblem& pb, const Coop
     if (e != hipSuccess) return e;
     if ((e = hipMemsetAsync(w.diag_run, 0xff, 4 * (size_t)pb.K + 4, st)) != hipSuccess) return e;
     if ((e = hipMemsetAsync(w.S, 0, 8 * 36 * (size_t)pb.K * pb.K + 8, st)) != hipSuccess) return e;
+    if ((e = hipMemsetAsync(w.run_arrive, 0, 4 * (size_t)w.pairs_cap, st)) != hipSuccess) return e;
+    if ((e = hipMemsetAsync(w.kf_arrive, 0, 4 * (size_t)pb.K + 4, st)) != hipSuccess) return e;
     SLAMGPU_LAUNCH("ba_coop_runs", st, coop_runs_kernel, blocks(w.pairs_cap), dim3(256), 0, st, w);
-    // the LM iterations: one cooperative launch (every work-group resident)
-    CoopPhase cp = phases[ph];
+    tb = w.cub_bytes;
+    e = hipcub::DeviceScan::ExclusiveSum(w.cub_tmp, tb, w.run_nch, w.run_ch0, w.pairs_cap, st);
+    if (e != hipSuccess) return e;
+    SLAMGPU_LAUNCH("ba_coop_chunks", st, coop_chunks_kernel, blocks(w.pairs_cap), dim3(256), 0, st,
+                   w);
+    // the whole LM schedule: one cooperative launch (every work-group resident)
+    CoopSchedule sch{};
+    sch.n_phases = n_phases;
+    sch.outlier_pass = outlier_pass ? 1 : 0;
+    for (int ph = 0; ph < n_phases && ph < 2; ph++) sch.ph[ph] = phases[ph];
     PoseParams Pc = P;
     CoopProblem pbc = pb;
     CoopWs wc = w;
     const int32_t* stop = d_stop;
-    void* args[] = {&Pc, &pbc, &wc, &cp, &stop};
+    void* args[] = {&Pc, &pbc, &wc, &sch, &stop};
     if (g_timer) g_timer->begin("ba_coop", st);
     e = hipLaunchCooperativeKernel(reinterpret_cast<const void*>(&ba_coop_kernel), dim3(G),
                                    dim3(kT), args, 0, st);

@@ -69,8 +69,12 @@ struct HostStage {
   // host-mapped mirror of a caller's stop flag, polled by the local BA kernel
   int32_t* stop_host = nullptr;
   int32_t* stop_dev = nullptr;
+  // pinned host twin of the inputs / outputs region of the single-problem BA calls
+  char* pin = nullptr;
+  size_t pin_bytes = 0;
   ~HostStage() {
     if (buf) (void)hipFree(buf);
+    if (pin) (void)hipHostFree(pin);
     if (stop_host) (void)hipHostFree(stop_host);
     if (stream) (void)hipStreamDestroy(stream);
   }
@@ -237,7 +241,7 @@ int coop_grid(int device) {
   int g = 64;
   if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 0)
     g = std::min(g, prop.multiProcessorCount);
-  if (const char* e = getenv("SLAMGPU_BA_WGS")) g = std::max(1, atoi(e));
+  if (const char* e = getenv("SLAMGPU_BA_WGS")) g = std::min(256, std::max(1, atoi(e)));
   int per_cu = 0;
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, coop_kernel_ptr(), kCoopThreads, 0) ==
           hipSuccess &&
@@ -300,78 +304,105 @@ int coop_host(const char* what, const slamgpu_camera* cam, const float* inv_sigm
     for (int e = 0; e < n_obs; e++) erase[e] = 0;
     return 0;
   }
+  using clk = std::chrono::steady_clock;
+  const auto t_host0 = clk::now();
   int dev = 0;
   OPT_HIPCHECK(hipGetDevice(&dev));
   const int G = coop_grid(dev);
   size_t wsb = 0;
   coop_layout(nullptr, n_kf, n_points, n_obs, K, (int)pairs, G, &wsb);
+  // inputs and outputs in one region (one DMA each way through a pinned twin), then workspace
   const size_t o_T = 0, o_mode = o_T + al256(64 * (size_t)n_kf);
   const size_t o_pts = o_mode + al256(n_kf + 1), o_ps = o_pts + al256(12 * (size_t)n_points + 4);
   const size_t o_obs = o_ps + al256(4 * ((size_t)n_points + 1));
-  const size_t o_er = o_obs + al256(sizeof(slamgpu_ba_obs) * (size_t)n_obs + 4);
-  const size_t o_ws = o_er + al256((size_t)n_obs + 4);
+  const size_t o_free = o_obs + al256(sizeof(slamgpu_ba_obs) * (size_t)n_obs + 4);
+  const size_t o_kof = o_free + al256(4 * (size_t)n_kf + 4);
+  const size_t o_er = o_kof + al256(4 * (size_t)K + 4);
+  const size_t o_ctl = o_er + al256((size_t)n_obs + 4);
+  const size_t o_io = o_ctl + 256, o_ws = o_io;
   HostStage& S = t_stage;
   if (int r = stage_reserve(S, o_ws + wsb)) return r;
+  if (S.pin_bytes < o_io) {
+    if (S.pin) OPT_HIPCHECK(hipHostFree(S.pin));
+    S.pin = nullptr;
+    S.pin_bytes = 0;
+    OPT_HIPCHECK(hipHostMalloc(reinterpret_cast<void**>(&S.pin), o_io, hipHostMallocDefault));
+    S.pin_bytes = o_io;
+  }
   char* b = static_cast<char*>(S.buf);
-  const CoopWs w = coop_layout(b + o_ws, n_kf, n_points, n_obs, K, (int)pairs, G, nullptr);
-  OPT_HIPCHECK(hipMemcpyAsync(b + o_T, kf_Tcw, 64 * (size_t)n_kf, hipMemcpyHostToDevice, S.stream));
-  OPT_HIPCHECK(hipMemcpyAsync(b + o_mode, kf_mode, n_kf, hipMemcpyHostToDevice, S.stream));
-  if (n_points)
-    OPT_HIPCHECK(hipMemcpyAsync(b + o_pts, points, 12 * (size_t)n_points, hipMemcpyHostToDevice, S.stream));
-  OPT_HIPCHECK(hipMemcpyAsync(b + o_ps, point_obs_start, 4 * ((size_t)n_points + 1),
-                              hipMemcpyHostToDevice, S.stream));
-  if (n_obs)
-    OPT_HIPCHECK(hipMemcpyAsync(b + o_obs, obs, sizeof(slamgpu_ba_obs) * (size_t)n_obs,
-                                hipMemcpyHostToDevice, S.stream));
-  if (n_kf)
-    OPT_HIPCHECK(hipMemcpyAsync(const_cast<int32_t*>(w.free_of_kf), free_of.data(), 4 * (size_t)n_kf,
-                                hipMemcpyHostToDevice, S.stream));
-  if (K)
-    OPT_HIPCHECK(hipMemcpyAsync(const_cast<int32_t*>(w.kf_of_free), kf_of.data(), 4 * (size_t)K,
-                                hipMemcpyHostToDevice, S.stream));
+  char* h = S.pin;
+  std::memcpy(h + o_T, kf_Tcw, 64 * (size_t)n_kf);
+  std::memcpy(h + o_mode, kf_mode, n_kf);
+  if (n_points) std::memcpy(h + o_pts, points, 12 * (size_t)n_points);
+  std::memcpy(h + o_ps, point_obs_start, 4 * ((size_t)n_points + 1));
+  if (n_obs) std::memcpy(h + o_obs, obs, sizeof(slamgpu_ba_obs) * (size_t)n_obs);
+  if (n_kf) std::memcpy(h + o_free, free_of.data(), 4 * (size_t)n_kf);
+  if (K) std::memcpy(h + o_kof, kf_of.data(), 4 * (size_t)K);
+  OPT_HIPCHECK(hipMemcpyAsync(b, h, o_er, hipMemcpyHostToDevice, S.stream));
+  CoopWs w = coop_layout(b + o_ws, n_kf, n_points, n_obs, K, (int)pairs, G, nullptr);
+  w.free_of_kf = reinterpret_cast<const int32_t*>(b + o_free);
+  w.kf_of_free = reinterpret_cast<const int32_t*>(b + o_kof);
+  static const bool prof = getenv("SLAMGPU_BA_PROFILE") != nullptr;
+  if (!prof) w.prof = nullptr;
   CoopProblem pb{reinterpret_cast<const slamgpu_ba_obs*>(b + o_obs),
                  reinterpret_cast<const int32_t*>(b + o_ps),
                  reinterpret_cast<const uint8_t*>(b + o_mode),
                  reinterpret_cast<float*>(b + o_T),
                  reinterpret_cast<float*>(b + o_pts),
                  local ? reinterpret_cast<uint8_t*>(b + o_er) : nullptr,
+                 reinterpret_cast<int32_t*>(b + o_ctl),
                  n_obs, n_points, n_kf, K};
   volatile int32_t* mirror = nullptr;
   if (stop_flag) {
     if (!S.stop_host) {
-      void* h = nullptr;
-      OPT_HIPCHECK(hipHostMalloc(&h, 64, hipHostMallocMapped | hipHostMallocCoherent));
-      S.stop_host = static_cast<int32_t*>(h);
+      void* hm = nullptr;
+      OPT_HIPCHECK(hipHostMalloc(&hm, 64, hipHostMallocMapped | hipHostMallocCoherent));
+      S.stop_host = static_cast<int32_t*>(hm);
       void* d = nullptr;
-      OPT_HIPCHECK(hipHostGetDevicePointer(&d, h, 0));
+      OPT_HIPCHECK(hipHostGetDevicePointer(&d, hm, 0));
       S.stop_dev = static_cast<int32_t*>(d);
     }
     mirror = S.stop_host;
     *mirror = *stop_flag ? 1 : 0;
   }
+  const auto t_launch0 = clk::now();
   OPT_HIPCHECK(launch_coop_ba(P, pb, w, phases, n_phases, local, stop_flag ? S.stop_dev : nullptr,
                               G, S.stream));
-  int32_t ctl[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  // keep the device's view of the caller's flag live until the work is done (nothing pageable
-  // may be queued behind the kernels: a copy to pageable memory would block this thread)
+  // the outputs and the control words come back in the same region (pinned: asynchronous)
+  OPT_HIPCHECK(hipMemcpyAsync(h, b, o_io, hipMemcpyDeviceToHost, S.stream));
+  const auto t_launch1 = clk::now();
+  // keep the device's view of the caller's flag live until the work is done
   if (mirror) {
     hipError_t q;
     while ((q = hipStreamQuery(S.stream)) == hipErrorNotReady) {
       *mirror = *stop_flag ? 1 : 0;
-      std::this_thread::sleep_for(std::chrono::microseconds(20));
+      std::this_thread::sleep_for(std::chrono::microseconds(5));
     }
     if (q != hipSuccess) return fail(SLAMGPU_EHIP, "%s: %s", what, hipGetErrorString(q));
   }
-  OPT_HIPCHECK(hipMemcpyAsync(ctl, w.ctl, sizeof(ctl), hipMemcpyDeviceToHost, S.stream));
   OPT_HIPCHECK(hipStreamSynchronize(S.stream));
+  const auto t_done = clk::now();
+  int32_t ctl[8];
+  std::memcpy(ctl, h + o_ctl, sizeof(ctl));
   if (ctl[CTL_ERR]) return fail(SLAMGPU_EDEVICE, "%s: grid barrier timed out", what);
-  OPT_HIPCHECK(hipMemcpyAsync(kf_Tcw, b + o_T, 64 * (size_t)n_kf, hipMemcpyDeviceToHost, S.stream));
-  if (n_points)
-    OPT_HIPCHECK(hipMemcpyAsync(points, b + o_pts, 12 * (size_t)n_points, hipMemcpyDeviceToHost, S.stream));
-  if (local && n_obs)
-    OPT_HIPCHECK(hipMemcpyAsync(erase, b + o_er, n_obs, hipMemcpyDeviceToHost, S.stream));
-  OPT_HIPCHECK(hipStreamSynchronize(S.stream));
+  std::memcpy(kf_Tcw, h + o_T, 64 * (size_t)n_kf);
+  if (n_points) std::memcpy(points, h + o_pts, 12 * (size_t)n_points);
+  if (local && n_obs) std::memcpy(erase, h + o_er, n_obs);
+  if (prof) {
+    auto us = [](clk::time_point a, clk::time_point b2) {
+      return std::chrono::duration<double, std::micro>(b2 - a).count();
+    };
+    fprintf(stderr, "[%s] host us: stage %.0f enqueue %.0f device-wait %.0f\n", what,
+            us(t_host0, t_launch0), us(t_launch0, t_launch1), us(t_launch1, t_done));
+  }
   if (lm_iterations) *lm_iterations = ctl[CTL_LM];
+  if (w.prof) {  // SLAMGPU_BA_PROFILE: work-group 0's per-phase wall time
+    double pr[16];
+    OPT_HIPCHECK(hipMemcpy(pr, w.prof, sizeof(pr), hipMemcpyDeviceToHost));
+    fprintf(stderr, "[%s] us: lin %.0f barrier %.0f assemble %.0f build_S %.0f factor %.0f "
+            "kf_update %.0f points %.0f first-sync %.0f (G %d, K %d)\n", what, pr[0], pr[1],
+            pr[2], pr[5], pr[6], pr[3], pr[4], pr[7], G, K);
+  }
   return 0;
 }
 
