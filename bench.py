@@ -85,12 +85,11 @@ def kernel_bytes(name, n_images, n_frames, kp_per_image, level_px, n_queries):
     px = sum(level_px)
     if name == "pyr_down":       # read level l-1, write level l
         return n_images * sum(level_px[l - 1] + level_px[l] for l in range(1, len(level_px)))
-    if name == "blur7":          # read + write every level
-        return n_images * 2 * px
     if name == "fast_cells":     # read every level once (+ small candidate writes)
         return n_images * px
-    if name == "orient_desc":    # 749-px disc + 37x37 blurred window + 60 B out per keypoint
-        return n_images * kp_per_image * (749 + 37 * 37 + 60)
+    if name == "orient_desc":    # 43x43 raw window (the 7x7-blurred samples' support; it holds
+        # the 749-px IC_Angle disc) + 60 B out per keypoint
+        return n_images * kp_per_image * (43 * 43 + 60)
     if name == "stereo_match":   # left+right kps/desc (60 B each) + SAD windows (11x11 + 11x21)
         return n_frames * kp_per_image * (2 * 60 + 121 + 231)
     if name == "search_cand":    # query (64 B) + window candidates' kps/desc (~60 B each, ~8)
@@ -269,7 +268,7 @@ def main():
           f"matches/frame {nm[1:5].tolist()}", file=sys.stderr)
 
     # ---- per-kernel breakdown pass (untimed) to pick the dominant kernel
-    names = ["pyr_down", "blur7", "blur7_edges", "fast_cells", "octree", "octree_global", "orient_desc", "stereo_rows",
+    names = ["pyr_down", "fast_cells", "octree", "octree_global", "orient_desc", "stereo_rows",
              "stereo_match", "stereo_median", "grid_build", "vo_queries", "search_cand",
              "search_resolve"]
     torch.cuda.synchronize()

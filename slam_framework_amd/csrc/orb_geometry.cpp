@@ -12,10 +12,6 @@
 #include <cmath>
 #include <cstring>
 
-#ifndef BLUR_STRIP
-#define BLUR_STRIP 32  // == orb_kernels.hip's blur7 rows per wave
-#endif
-
 namespace slamgpu {
 
 static inline int cv_round_h(float v) { return (int)std::lrintf(v); }
@@ -173,20 +169,8 @@ int compute_geometry(const OrbParams& p, int cols, int rows, OrbGeom* g,
     }
   }
   g->cells_per_image = cell_base;
-  int64_t boff = 0;
-  int btiles = 0;
-  for (int l = 0; l < p.nlevels; l++) {
-    LevelGeom& L = g->lv[l];
-    L.blur_offset = boff;
-    boff += (int64_t)L.pitch * L.h;
-    boff = (boff + 255) & ~(int64_t)255;
-    L.blur_tile_base = btiles;
-    btiles += ((L.w + 255) / 256) * ((L.h + 4 * BLUR_STRIP - 1) / (4 * BLUR_STRIP));  // 256 x 4 strips
-  }
-  g->blur_bytes = boff;
-  g->blur_tiles = btiles;
   gauss_kernel_int(g->gauss);
-  {  // blur7_kernel packs taps into bytes and row sums into u16 (sum of taps <= 257)
+  {  // orient_desc packs taps into bytes and row sums into u16 (sum of taps <= 257)
     int sum = 0;
     for (int i = 0; i < 7; i++) {
       if (g->gauss[i] < 0 || g->gauss[i] > 255 || g->gauss[i] != g->gauss[6 - i]) return -6;

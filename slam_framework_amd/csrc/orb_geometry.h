@@ -27,7 +27,6 @@ struct LevelGeom {
   int w, h;             // level image size
   int pitch;            // row pitch of this level in the pyramid buffers (level >= 1)
   int64_t offset;       // byte offset of this level inside one image's pyramid buffer
-  int64_t blur_offset;  // byte offset of this level inside one image's blurred buffer
   // FAST cell grid (ComputeKeyPointsOctTree :712-733)
   int max_bx, max_by;   // maxBorderX/Y
   int ncols, nrows;     // cells
@@ -48,7 +47,6 @@ struct LevelGeom {
   int oct_work_off;     //   byte offset of sort keys / prefix arrays / flags
   // resize tables (level >= 1) in the shared table buffer
   int rx_base, ry_base; // offsets into the x (per dst column) / y (per dst row) tables
-  int blur_tile_base;   // first 256x128 blur tile of this level
   int xmax;             // first dst column that copies S[sx] * 2048 (resize HResizeLinear)
   float scale, inv_scale;
   float patch_size;     // (float)(int)(PATCH_SIZE * scale) (:778)
@@ -64,8 +62,6 @@ struct OrbGeom {
   int fast_score_stride, fast_score_rows;  // detect area
   int fast_lds_per_wave;                   // bytes (tile + score + u16 candidate list)
   int64_t pyr_bytes;     // bytes of one image's pyramid (levels >= 1) buffer
-  int64_t blur_bytes;    // bytes of one image's blurred pyramid (levels >= 0) buffer
-  int blur_tiles;        // 256x128 blur tiles over all levels of one image
   int gauss[7];          // GaussianBlur 7x7 sigma 2 integer kernel (x256)
   int64_t keys_per_image;
   int64_t nodes_per_image;

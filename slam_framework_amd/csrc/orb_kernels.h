@@ -17,14 +17,13 @@ static_assert(sizeof(KeyPoint) == 28, "cv::KeyPoint layout");
 // A batch of u8 images already in device memory. Image 2f is the left view of frame f at
 // in_l + f * in_stride, image 2f+1 the right view at in_r + f * in_stride; rows are in_pitch
 // bytes apart. (n mono images at base + i*s: in_l = base, in_r = base + s, in_stride = 2s.)
-// pyr/blur are the per-image pyramid (levels >= 1) and blurred pyramids.
+// pyr is the per-image pyramid (levels >= 1).
 struct ImageBatch {
   const uint8_t* in_l;
   const uint8_t* in_r;
   int64_t in_stride;
   int in_pitch;
   uint8_t* pyr;
-  uint8_t* blur;
 };
 
 __device__ __forceinline__ const uint8_t* batch_image(const ImageBatch& b, int img) {
@@ -60,10 +59,9 @@ struct OrbGeomDev {
 // Optional side streams of the extraction (all null: everything on `st`):
 //   side0: FAST of level 0 (reads only the caller's images) beside the pyramid, joined before
 //          the octree;
-//   side:  the blur (descriptor input) beside fast_cells + octree, joined before orient_desc.
 struct ExtractStreams {
-  hipStream_t side0 = nullptr, side = nullptr;
-  hipEvent_t fork0 = nullptr, join0 = nullptr, fork = nullptr, join = nullptr;
+  hipStream_t side0 = nullptr;
+  hipEvent_t fork0 = nullptr, join0 = nullptr;
 };
 void launch_extract(const ImageBatch& b, const OrbGeomDev& g, int n_images, hipStream_t st,
                     const ExtractStreams& fx = ExtractStreams());

@@ -2,10 +2,10 @@
 //
 // Pipeline for a batch of n images (all levels of all images in flight together):
 //   pyr_down      level l from level l-1 (resize INTER_LINEAR 8U)        one launch per level
-//   blur7         7x7 Gaussian of every level (descriptor input)         one launch
 //   fast_cells    per-cell FAST-9 score, threshold fallback, cell NMS    one wave per cell
 //   octree        DistributeOctTree, exact list / pointer-order semantics one workgroup per level
-//   orient_desc   IC_Angle + rBRIEF, output in ORBextractor::Compute order one wave per keypoint
+//   orient_desc   IC_Angle + 7x7-blurred rBRIEF (the blur at the samples), output in
+//                 ORBextractor::Compute order                            8 keypoints per wave
 // Reference: src/orb_features/orb_extractor.cpp (citations per kernel). Built with
 // -ffp-contract=off; fused multiply-adds are explicit where the reference's Release build fuses.
 #include <hip/hip_runtime.h>
@@ -172,200 +172,10 @@ __global__ __launch_bounds__(256) void pyr_down_kernel(ImageBatch b, const OrbGe
 }
 
 // ---------------------------------------------------------------------------------------
-// blur7: Compute (:1029-1030) clone + GaussianBlur(7x7, 2, 2, BORDER_REFLECT_101) per level.
-// Row pass: exact int sums over the reflect-101 extended row. Column pass: OpenCV 3.3.1's
-// SymmColumnVec_32s8u covers x < w - w%4 and rounds V/65536 half-to-even; the scalar tail rounds
-// (V + 32768) >> 16. Each thread owns 4 adjacent columns of a 32-row strip and slides a 7-row
-// window of row sums down it in registers (one aligned 12-byte read per input row, no LDS);
-// a 256-thread block covers 256 columns x 128 rows.
-// All sums are exact integers, so they map onto the dot-product ALU: a row sum is two
-// v_dot4_u32_u8 (taps 0-3 and 4-6 of the byte window), and since the taps {18,34,49,55,49,34,18}
-// sum to 257 a row sum is <= 65535, so the column sum is three v_dot2_u32_u16 over packed pairs
-// of consecutive row sums plus one multiply-add. The host checks those bounds (orb_geometry.cpp).
-__device__ __forceinline__ int reflect101(int i, int n) {
+__device__ __forceinline__ int reflect101(int i, int n) {  // cv::BORDER_REFLECT_101, |overshoot| < n
   if (i < 0) i = -i;
   if (i >= n) i = 2 * n - 2 - i;
   return i;
-}
-
-#ifndef BLUR_STRIP
-#define BLUR_STRIP 32
-#endif
-constexpr int kBlurTileW = 256, kBlurStrip = BLUR_STRIP, kBlurTileH = 4 * kBlurStrip;
-
-__global__ __launch_bounds__(256) void blur7_kernel(ImageBatch b, const OrbGeom* __restrict__ g) {
-  int img, tile;
-  xcd_image_block(&img, &tile);
-  int level = 0;
-  while (level + 1 < g->nlevels && tile >= g->lv[level + 1].blur_tile_base) level++;
-  const LevelGeom& L = g->lv[level];
-  tile -= L.blur_tile_base;
-  const int tiles_x = (L.w + kBlurTileW - 1) / kBlurTileW;
-  const int lane = threadIdx.x & 63, wid = wave_id();
-  const int x = (tile % tiles_x) * kBlurTileW + 4 * lane;
-  const int y0 = (tile / tiles_x) * kBlurTileH + wid * kBlurStrip;
-  if (x >= L.w || y0 >= L.h) return;
-  int spitch;
-  const uint8_t* src = level_ptr(b, g, img, level, &spitch);
-  uint8_t* dst = b.blur + (int64_t)img * g->blur_bytes + L.blur_offset;
-  const int w = L.w, h = L.h;
-  // Dword path for every lane of a 4-aligned image; lanes whose taps cross the left/right image
-  // border (x < 4 or x + 8 > w) load clamped in-bounds dwords and leave their columns to
-  // blur7_edges_kernel. Caller images with an odd base/pitch take the byte path everywhere
-  // (wave-uniform).
-  const bool fast = (((uintptr_t)src | (uintptr_t)spitch) & 3) == 0;
-  const bool edge = fast && (x < 4 || x + 8 > w);
-  const int xl = edge ? min(max(x, 4), (w - 8) & ~3) : x;
-  const uint32_t k0 = g->gauss[0], k1 = g->gauss[1], k2 = g->gauss[2], k3 = g->gauss[3];
-  const uint32_t KA = k0 | k1 << 8 | k2 << 16 | k3 << 24;  // taps 0..3
-  const uint32_t KB = k2 | k1 << 8 | k0 << 16;             // taps 4..6
-  const uint32_t K01 = k0 | k1 << 16, K23 = k2 | k3 << 16, K21 = k2 | k1 << 16;
-  // rounding: half-to-even inside the vector span, half-up in the scalar tail
-  const bool vec_round = x < w - (w % 4);  // whole 4-column group on one side of xvec
-  const uint32_t rbias = vec_round ? 0x7fffu : 0x8000u, rodd = vec_round ? 1u : 0u;
-  const int y1 = min(y0 + kBlurStrip, h);
-  // pr[s][j]: (row sum of ring slot s, row sum of slot s+1) packed as u16 pairs
-  uint32_t pr[7][4], prev[4] = {0, 0, 0, 0};
-  // Rows are fetched a 7-row group at a time, branch-free (rows past the strip reflect back
-  // into the image and are never output), and the next group is in flight while the current
-  // one is filtered.
-  uint32_t cur[7][3], nxt[7][3];
-  auto fetch = [&](int r0, uint32_t (&buf)[7][3]) {
-#pragma unroll
-    for (int k = 0; k < 7; k++) {
-      const uint8_t* row = src + (int64_t)reflect101(r0 + k, h) * spitch;
-      if (fast) {
-        buf[k][0] = *reinterpret_cast<const uint32_t*>(row + xl - 4);
-        buf[k][1] = *reinterpret_cast<const uint32_t*>(row + xl);
-        buf[k][2] = *reinterpret_cast<const uint32_t*>(row + xl + 4);
-      } else {  // bytes x-3 .. x+6 with reflect-101 columns
-        uint32_t wv[3] = {0, 0, 0};
-#pragma unroll
-        for (int i = 1; i <= 10; i++)
-          wv[i >> 2] |= (uint32_t)row[reflect101(x - 4 + i, w)] << (8 * (i & 3));
-        buf[k][0] = wv[0];
-        buf[k][1] = wv[1];
-        buf[k][2] = wv[2];
-      }
-    }
-  };
-  fetch(y0 - 3, cur);
-  // input rows y0-3 .. y1+2; output row r-3 once 7 rows are in the ring
-  for (int r0 = y0 - 3; r0 < y1 + 3; r0 += 7) {
-    if (r0 + 7 < y1 + 3) fetch(r0 + 7, nxt);
-#pragma unroll
-    for (int k = 0; k < 7; k++) {
-      const int r = r0 + k;
-      if (r < y1 + 3) {
-        const uint32_t w0 = cur[k][0], w1 = cur[k][1], w2 = cur[k][2];  // bytes x-4 .. x+7
-        uint32_t n[4];
-#pragma unroll
-        for (int j = 0; j < 4; j++) {  // 7-tap window starts at byte x - 3 + j
-          const uint32_t lo = j == 3 ? w1 : __builtin_amdgcn_alignbyte(w1, w0, j + 1);
-          const uint32_t hi = j == 3 ? w2 : __builtin_amdgcn_alignbyte(w2, w1, j + 1);
-          n[j] = __builtin_amdgcn_udot4(lo, KA, __builtin_amdgcn_udot4(hi, KB, 0u, false), false);
-          pr[(k + 6) % 7][j] = prev[j] | n[j] << 16;
-          prev[j] = n[j];
-        }
-        const int yo = r - 3;  // output row whose window ends at input row r
-        if (yo >= y0) {
-          uint32_t packed = 0;
-#pragma unroll
-          for (int j = 0; j < 4; j++) {
-            // window rows w0..w6 = slots k+1 .. k: (w0,w1), (w2,w3), (w4,w5) pairs, then w6
-            uint32_t v = dot2u(pr[(k + 1) % 7][j], K01, 0u);
-            v = dot2u(pr[(k + 3) % 7][j], K23, v);
-            v = dot2u(pr[(k + 5) % 7][j], K21, v);
-            v += k0 * n[j];
-            uint32_t o = (v + rbias + __builtin_amdgcn_ubfe(v, 16, rodd)) >> 16;
-            o = o > 255u ? 255u : o;
-            packed |= o << (8 * j);
-          }
-          uint8_t* drow = dst + (int64_t)yo * L.pitch;
-          if (!edge) {
-            if (x + 4 <= w) {
-              *reinterpret_cast<uint32_t*>(drow + x) = packed;
-            } else {
-              for (int j = 0; x + j < w; j++) drow[x + j] = (uint8_t)(packed >> (8 * j));
-            }
-          }
-        }
-      }
-    }
-#pragma unroll
-    for (int k = 0; k < 7; k++)
-#pragma unroll
-      for (int e = 0; e < 3; e++) cur[k][e] = nxt[k][e];
-  }
-}
-
-// blur7_edges: the columns blur7_kernel's dword path leaves out (the 4-column groups with
-// x < 4 or x + 8 > w), reflect-101 in both directions. One wave per (image, level, 32-row
-// strip): the 38 input rows' reflected edge bytes (13 per row and side) are staged in LDS with
-// coalesced loads, then lane (row, side) filters its <= 7 columns from registers.
-constexpr int kEdgeStrip = 32;
-
-__global__ __launch_bounds__(64) void blur7_edges_kernel(ImageBatch b, const OrbGeom* __restrict__ g) {
-  __shared__ __attribute__((aligned(16))) uint8_t s_e[kEdgeStrip + 6][2][16];
-  const int img = blockIdx.y, lane = threadIdx.x;
-  int strip = blockIdx.x, level = 0;
-  while (level < g->nlevels && strip >= (g->lv[level].h + kEdgeStrip - 1) / kEdgeStrip) {
-    strip -= (g->lv[level].h + kEdgeStrip - 1) / kEdgeStrip;
-    level++;
-  }
-  if (level >= g->nlevels) return;
-  const LevelGeom& L = g->lv[level];
-  const int w = L.w, h = L.h;
-  int spitch;
-  const uint8_t* src = level_ptr(b, g, img, level, &spitch);
-  if ((((uintptr_t)src | (uintptr_t)spitch) & 3) != 0) return;  // byte path covered it
-  const int y0 = strip * kEdgeStrip;
-  const int xr = ((w - 8) & ~3) + 4;  // first 4-aligned group with x + 8 > w
-  // stage: element j -> (row j / 26, side (j / 13) & 1, byte j % 13) = column c0 - 3 + byte
-  for (int j = lane; j < (kEdgeStrip + 6) * 26; j += 64) {
-    const int r = j / 26, rem = j - r * 26, side = rem >= 13, bt = rem - 13 * side;
-    const int c0 = side ? xr : 0;
-    const uint8_t* row = src + (int64_t)reflect101(y0 - 3 + r, h) * spitch;
-    s_e[r][side][bt] = row[reflect101(c0 - 3 + bt, w)];
-  }
-  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
-  __syncthreads();
-  const int r = lane >> 1, side = lane & 1, y = y0 + r;
-  if (y >= h) return;
-  const int c0 = side ? xr : 0, nc = side ? w - xr : 4;  // nc <= 7
-  uint32_t pk[7][4];
-#pragma unroll
-  for (int dy = 0; dy < 7; dy++) {
-    const uint4 q = *reinterpret_cast<const uint4*>(&s_e[r + dy][side][0]);
-    pk[dy][0] = q.x;
-    pk[dy][1] = q.y;
-    pk[dy][2] = q.z;
-    pk[dy][3] = q.w & 0xffu;  // byte 12 only
-  }
-  const uint32_t k0 = g->gauss[0], k1 = g->gauss[1], k2 = g->gauss[2], k3 = g->gauss[3];
-  const uint32_t KA = k0 | k1 << 8 | k2 << 16 | k3 << 24, KB = k2 | k1 << 8 | k0 << 16;
-  const uint32_t kv[7] = {k0, k1, k2, k3, k2, k1, k0};
-  uint8_t* drow = b.blur + (int64_t)img * g->blur_bytes + L.blur_offset + (int64_t)y * L.pitch;
-#pragma unroll
-  for (int m = 0; m < 7; m++) {  // output column c0 + m: taps at local bytes m .. m+6
-    if (m < nc) {
-      uint32_t v = 0;
-#pragma unroll
-      for (int dy = 0; dy < 7; dy++) {
-        const uint32_t lo = (m & 3) == 0 ? pk[dy][m >> 2]
-                                         : __builtin_amdgcn_alignbyte(pk[dy][(m >> 2) + 1],
-                                                                      pk[dy][m >> 2], m & 3);
-        const uint32_t hi = (m & 3) == 0 ? pk[dy][(m >> 2) + 1]
-                                         : __builtin_amdgcn_alignbyte(pk[dy][(m >> 2) + 2],
-                                                                      pk[dy][(m >> 2) + 1], m & 3);
-        v += kv[dy] * __builtin_amdgcn_udot4(lo, KA, __builtin_amdgcn_udot4(hi, KB, 0u, false), false);
-      }
-      const int c = c0 + m;
-      const uint32_t o = (c & ~3) < w - (w % 4) ? (v + 0x7fffu + ((v >> 16) & 1u)) >> 16
-                                                : (v + 0x8000u) >> 16;
-      drow[c] = (uint8_t)(o > 255u ? 255u : o);
-    }
-  }
 }
 
 // ---------------------------------------------------------------------------------------
@@ -1873,23 +1683,7 @@ __global__ __launch_bounds__(64 * kMaxLevels) void octree_img_kernel(
 }
 
 // ---------------------------------------------------------------------------------------
-// orient_desc: computeOrientation/IC_Angle (:413-420, :18-45) on the unblurred level, then
-// computeOrbDescriptor (:49-88) on the blurred level. Output order is ORBextractor::Compute's:
-// levels 0..L-1 concatenated, each in octree list order (:1020-1048). Descriptor sample offsets
-// use the Release-build FMA association (g++ -O3 -march=native):
-// row = cvRound(fma(px, b, py*a)), col = cvRound(fma(px, a, -(py*b))).
-// Each wave handles kKpPerWave consecutive keypoints in three phases, so the per-keypoint scalar
-// work (atan2, sincos) runs once for all of them and every load is in flight at once:
-//  1. issue all loads: each keypoint's 31x31 raw patch into registers (lane = half a patch row,
-//     5 dwords), its 37x37 blurred window (samples reach |offset| <= 18)
-//     straight into LDS with global_load_lds;
-//  2. IC_Angle moments with v_dot4_u32_u8 against per-lane disc weights (u+20 / 1 inside
-//     umax, 0 outside; sum(u*I) = sum((u+20)*I) - 20*sum(I), exact), a 16-value reduce-scatter
-//     across the wave, and one fastAtan2 + sincosf pass for the 8 keypoints;
-//  3. rBRIEF: 4 tests per lane per keypoint with packed-fp32 offsets; cvRound(v) == bits of
-//     (v + 1.5*2^23) for |v| < 2^22 (round-half-even in the add), which feeds the LDS address.
 constexpr int kKpPerWave = 8;
-constexpr int kBlurStride = 40, kBlurWin = 37 * kBlurStride;
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 
 // Sum of the 16 per-lane values v[] over the wave; value i ends up in lanes 4i..4i+3.
@@ -1918,14 +1712,43 @@ __device__ __forceinline__ int reduce_scatter16(int (&v)[16], int lane) {
   return z;
 }
 
+// ---------------------------------------------------------------------------------------
+// orient_desc: computeOrientation/IC_Angle (:413-420, :18-45) on the unblurred level, then
+// computeOrbDescriptor (:49-88) on the level blurred by cv::GaussianBlur(7x7, sigma 2) (:1029-1030),
+// with the blur folded in: no blurred pyramid is written or read back. The blur is separable
+// with exact integer sums: a pixel is round(sum_i k_i R_i / 2^16), R_i = the row
+// sums sum_j k_j I(y+i-3, x+j-3) <= 255 * 257 (u16). Per keypoint a wave forms the row sums of
+// the 43 x 37 window the samples' columns need (rows y-21..y+21, columns x-18..x+18: 430 lane
+// tasks of 4 columns, one dwordx4 load of the raw row + 2 v_dot4_u32_u8 per column, stored
+// TRANSPOSED as u16 in LDS), then each of the 512 samples takes its 7 vertical row sums as 4
+// dwords of its column (v_alignbit for an odd start) and 4 v_dot2_u32_u16, and rounds with the
+// column's rule (half to even inside the SSE span x < W - W%4, half up in the scalar tail).
+// Border keypoints (the window leaves the image: reflect-101 columns) load bytes one by one.
+// Keypoints are processed kFG at a time per wave (LDS: kFG x 40 x 44 u16 per wave).
+constexpr int kRtCols = 40, kRtRows = 44;
+#ifndef FUSED_GROUP
+#define FUSED_GROUP 1
+#endif
+constexpr int kFG = FUSED_GROUP;  // keypoints per row-sum pass (LDS: kFG x 3.5 KB per wave)
+
+__device__ __forceinline__ uint32_t rt_tap(const uint16_t* rt, int sy, int sx, uint32_t K01,
+                                           uint32_t K23, uint32_t K21, uint32_t K0) {
+  const int e0 = (sx + 18) * kRtRows + sy + 18;  // rows sy - 3 .. sy + 3 of column sx
+  const uint32_t* rw = reinterpret_cast<const uint32_t*>(rt) + (e0 >> 1);
+  const uint32_t sh = (uint32_t)(e0 & 1) << 4;
+  const uint32_t w0 = rw[0], w1 = rw[1], w2 = rw[2], w3 = rw[3];
+  const uint32_t p0 = __builtin_amdgcn_alignbit(w1, w0, sh);
+  const uint32_t p1 = __builtin_amdgcn_alignbit(w2, w1, sh);
+  const uint32_t p2 = __builtin_amdgcn_alignbit(w3, w2, sh);
+  const uint32_t p3 = __builtin_amdgcn_alignbit(0u, w3, sh);
+  return dot2u(p0, K01, dot2u(p1, K23, dot2u(p2, K21, dot2u(p3, K0, 0u))));
+}
+
 __global__ __launch_bounds__(256) void orient_desc_kernel(
     ImageBatch b, const OrbGeom* __restrict__ g, const uint32_t* __restrict__ oct_keys,
     const int* __restrict__ oct_count, KeyPoint* __restrict__ kps, uint8_t* __restrict__ desc,
     int* __restrict__ nkps) {
-  __shared__ __attribute__((aligned(16))) uint8_t s_blur[4][kKpPerWave][kBlurWin];
-  // XCD-aware mapping: blocks are dealt round-robin over the 8 XCDs, so give every block of one
-  // image the same (linear id % 8) -- an image's pyramid then stays in one XCD's L2
-  // (bijective when the image count is a multiple of 8; otherwise the natural order is used).
+  __shared__ __attribute__((aligned(16))) uint16_t s_rt[4][kFG][kRtCols * kRtRows];
   int img, bx;
   xcd_image_block(&img, &bx);
   const int lane = threadIdx.x & 63, wid = wave_id();
@@ -1939,7 +1762,6 @@ __global__ __launch_bounds__(256) void orient_desc_kernel(
   const int k0 = (bx * 4 + wid) * kKpPerWave;
   if (k0 >= total) return;
   const int nk = min(kKpPerWave, total - k0);
-  // lane j < nk: level / key of keypoint k0 + j
   int my_level = 0, my_key = 0;
   if (lane < nk) {
     int t = k0 + lane, l = 0;
@@ -1950,8 +1772,6 @@ __global__ __launch_bounds__(256) void orient_desc_kernel(
     my_level = l;
     my_key = (int)oct_keys[(int64_t)img * g->out_per_image + g->lv[l].out_base + t];
   }
-  // Per-lane IC_Angle geometry: lane = (patch row hr, half hh); dword k covers
-  // u = 16*hh + 4k + (0..3) - 15 of row v = hr - 15.
   const int hr = lane >> 1, hh = lane & 1, hv = hr - 15;
   const int hd = hr < 31 ? g->umax[hv < 0 ? -hv : hv] : -1;
   uint32_t wt[4], one[4];
@@ -1968,8 +1788,6 @@ __global__ __launch_bounds__(256) void orient_desc_kernel(
       }
     }
   }
-  // Keys of the wave's keypoints as scalars; slots j >= nk repeat the last keypoint so that
-  // every phase is branch-free (their results are never stored).
   uint32_t kkey[kKpPerWave];
   int klev[kKpPerWave];
 #pragma unroll
@@ -1978,16 +1796,8 @@ __global__ __launch_bounds__(256) void orient_desc_kernel(
     kkey[j] = (uint32_t)__builtin_amdgcn_readlane(my_key, jj);
     klev[j] = __builtin_amdgcn_readlane(my_level, jj);
   }
-  // Phase 1: all loads. Keypoint bases are wave-uniform (scalar); lane offsets are 24-bit.
-  int br[6], bq[6];
-#pragma unroll
-  for (int k = 0; k < 6; k++) {
-    const int i = lane + 64 * k;
-    br[k] = i / 10;
-    bq[k] = 4 * (i - br[k] * 10);
-  }
   const int in_pitch = __builtin_amdgcn_readfirstlane(b.in_pitch);
-  const uint8_t* blur_img = b.blur + (int64_t)img * g->blur_bytes;
+  // Phase 1: the IC_Angle patches (raw level, registers)
   uint32_t raw[kKpPerWave][5];
 #pragma unroll
   for (int j = 0; j < kKpPerWave; j++) {
@@ -2005,21 +1815,13 @@ __global__ __launch_bounds__(256) void orient_desc_kernel(
       if ((((uintptr_t)im | (uintptr_t)pitch) & 3) == 0) {
 #pragma unroll
         for (int k = 0; k < 5; k++) raw[j][k] = reinterpret_cast<const uint32_t*>(rp)[k];
-      } else {  // caller image with an odd pitch/base
+      } else {
 #pragma unroll
         for (int k = 0; k < 20; k++) raw[j][k >> 2] |= (uint32_t)rp[k] << (8 * (k & 3));
       }
     }
-    const int bp = L.pitch;
-    const uint8_t* bl = blur_img + L.blur_offset + (int64_t)(y - 18) * bp + ((x - 18) & ~3);
-#pragma unroll
-    for (int k = 0; k < 6; k++)
-      if (lane + 64 * k < 37 * 10)
-        __builtin_amdgcn_global_load_lds(
-            (const __attribute__((address_space(1))) void*)(bl + (__umul24(br[k], bp) + bq[k])),
-            (__attribute__((address_space(3))) void*)(&s_blur[wid][j][256 * k]), 4, 0, 0);
   }
-  // Phase 2: moments -> angle, sin, cos (lane 8j holds keypoint j's).
+  // Phase 2: moments -> angle, sin, cos (lane 8j holds keypoint j's)
   int mv[16];
 #pragma unroll
   for (int j = 0; j < kKpPerWave; j++) {
@@ -2031,8 +1833,8 @@ __global__ __launch_bounds__(256) void orient_desc_kernel(
       s = __builtin_amdgcn_udot4(e, one[k], s, false);
       t = __builtin_amdgcn_udot4(e, wt[k], t, false);
     }
-    mv[2 * j] = (int)t - 20 * (int)s;  // m10 part
-    mv[2 * j + 1] = hv * (int)s;       // m01 part
+    mv[2 * j] = (int)t - 20 * (int)s;
+    mv[2 * j + 1] = hv * (int)s;
   }
   int mom = reduce_scatter16(mv, lane);
   const int m01 = __builtin_amdgcn_mov_dpp(mom, 0x104, 0xf, 0xf, false);  // row_shl:4
@@ -2040,7 +1842,7 @@ __global__ __launch_bounds__(256) void orient_desc_kernel(
   const float factorPI = (float)(3.14159265358979323846 / 180.0);
   float sa, ca;
   glibc_sincosf(angle * factorPI, &sa, &ca);
-  // Phase 3: descriptors. Pattern test t = r*64 + lane.
+  // Phase 3: per 4 keypoints, the row-summed windows (LDS) then the 512 blurred samples each
   f32x2 ppx[4][2], ppy[4][2];
 #pragma unroll
   for (int r = 0; r < 4; r++) {
@@ -2052,27 +1854,84 @@ __global__ __launch_bounds__(256) void orient_desc_kernel(
       ppy[r][e] = (f32x2){py, py};
     }
   }
-  __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): the global_load_lds windows have landed
+  const uint32_t q0 = g->gauss[0], q1 = g->gauss[1], q2 = g->gauss[2], q3 = g->gauss[3];
+  const uint32_t KA = q0 | q1 << 8 | q2 << 16 | q3 << 24, KB = q2 | q1 << 8 | q0 << 16;
+  const uint32_t K01 = q0 | q1 << 16, K23 = q2 | q3 << 16, K21 = q2 | q1 << 16, K0 = q0;
   const f32x2 magic = {12582912.0f, 12582912.0f};
   uint32_t dlo = 0, dhi = 0;
 #pragma unroll
-  for (int j = 0; j < kKpPerWave; j++) {
-    {
-      const int x = key_x(kkey[j]) + kMinBorder;
+  for (int half = 0; half < kKpPerWave / kFG; half++) {
+#pragma unroll
+    for (int jj = 0; jj < kFG; jj++) {  // row sums of keypoint kFG half + jj
+      const int j = kFG * half + jj;
+      const int level = klev[j];
+      const int kx = key_x(kkey[j]) + kMinBorder, ky = key_y(kkey[j]) + kMinBorder;
+      const LevelGeom& L = g->lv[level];
+      const int w = L.w, h = L.h;
+      const int pitch = level == 0 ? in_pitch : L.pitch;
+      const uint8_t* im = level == 0 ? batch_image(b, img)
+                                     : b.pyr + (int64_t)img * g->pyr_bytes + L.offset;
+      const bool fastp = kx >= 21 && kx <= w - 31 && ((((uintptr_t)im | (uintptr_t)pitch) & 3) == 0);
+      const uint32_t sft = (uint32_t)((kx - 21) & 3);
+      uint16_t* rt = &s_rt[wid][jj][0];
+#pragma unroll
+      for (int i = 0; i < 7; i++) {
+        const int t = lane + 64 * i;
+        if (t < 43 * 10) {
+          const int r = t / 10, gq = t - r * 10;
+          const int y = reflect101(ky - 21 + r, h);
+          const uint8_t* row = im + (int64_t)y * pitch;
+          const int x0 = kx - 18 + 4 * gq;
+          uint32_t u0, u1, u2;
+          if (fastp) {
+            const uint4 q = *reinterpret_cast<const uint4*>(row + ((x0 - 3) & ~3));
+            u0 = __builtin_amdgcn_alignbyte(q.y, q.x, sft);
+            u1 = __builtin_amdgcn_alignbyte(q.z, q.y, sft);
+            u2 = __builtin_amdgcn_alignbyte(q.w, q.z, sft);
+          } else {
+            uint32_t wv[3] = {0, 0, 0};
+#pragma unroll
+            for (int k = 0; k < 10; k++)
+              wv[k >> 2] |= (uint32_t)row[reflect101(x0 - 3 + k, w)] << (8 * (k & 3));
+            u0 = wv[0];
+            u1 = wv[1];
+            u2 = wv[2];
+          }
+#pragma unroll
+          for (int jx = 0; jx < 4; jx++) {
+            const uint32_t lo = jx == 0 ? u0 : __builtin_amdgcn_alignbyte(u1, u0, jx);
+            const uint32_t hi = jx == 0 ? u1 : __builtin_amdgcn_alignbyte(u2, u1, jx);
+            const uint32_t R = __builtin_amdgcn_udot4(lo, KA, __builtin_amdgcn_udot4(hi, KB, 0u, false), false);
+            rt[(4 * gq + jx) * kRtRows + r] = (uint16_t)R;
+          }
+        }
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+#pragma unroll
+    for (int jj = 0; jj < kFG; jj++) {  // the 256 tests of keypoint kFG half + jj
+      const int j = kFG * half + jj;
+      const int kx = key_x(kkey[j]) + kMinBorder;
+      const int w = g->lv[klev[j]].w, xvec = w - (w & 3);
+      const bool tail_possible = kx + 18 >= xvec;
       const float cj = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(ca), 8 * j));
       const float sj = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(sa), 8 * j));
       const f32x2 ab = {sj, cj}, nab = {cj, -sj};
-      // LDS byte address of window(ry, rx) = base + (0x400000+ry)*40 + 0x4B400000+rx - C
-      const uint8_t* bc = &s_blur[wid][j][0] + 18 * kBlurStride + 18 + ((x - 18) & 3) -
-                          (int32_t)0x55400000u;
+      const uint16_t* rt = &s_rt[wid][jj][0];
 #pragma unroll
       for (int r = 0; r < 4; r++) {
-        int v[2];
+        uint32_t v[2];
 #pragma unroll
         for (int e = 0; e < 2; e++) {
           const f32x2 q = __builtin_elementwise_fma(ppx[r][e], ab, ppy[r][e] * nab) + magic;
-          const uint32_t yb = __float_as_uint(q.x), xb = __float_as_uint(q.y);
-          v[e] = bc[(int32_t)((yb & 0xFFFFFFu) * (uint32_t)kBlurStride + xb)];
+          const int sy = (int)__float_as_uint(q.x) - 0x4B400000;
+          const int sx = (int)__float_as_uint(q.y) - 0x4B400000;
+          const uint32_t s = rt_tap(rt, sy, sx, K01, K23, K21, K0);
+          const bool tail = tail_possible && kx + sx >= xvec;
+          uint32_t o = (s + (tail ? 0x8000u : 0x7fffu + ((s >> 16) & 1u))) >> 16;
+          v[e] = o > 255u ? 255u : o;
         }
         const uint64_t word = __ballot(v[0] < v[1]);
         if (lane == 4 * j + r) {
@@ -2081,6 +1940,9 @@ __global__ __launch_bounds__(256) void orient_desc_kernel(
         }
       }
     }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
   }
   const int64_t o = (int64_t)img * g->kp_cap + k0;
   if (lane < 4 * nk)
@@ -2150,22 +2012,6 @@ void launch_extract(const ImageBatch& b, const OrbGeomDev& gd, int n_images, hip
     SLAMGPU_LAUNCH("pyr_down", st, pyr_down_kernel, dim3(tiles, n_images), dim3(256), 0, st, b,
                    gd.dev, l, gd.rx, gd.ry);
   }
-  // the blurred pyramid only feeds orient_desc: with a side stream it overlaps fast_cells +
-  // octree (the octree's long level-0 waves leave most SIMDs idle)
-  hipStream_t bs = st;
-  if (fx.side && fx.fork && fx.join) {
-    (void)hipEventRecord(fx.fork, st);
-    (void)hipStreamWaitEvent(fx.side, fx.fork, 0);
-    bs = fx.side;
-  }
-  SLAMGPU_LAUNCH("blur7", bs, blur7_kernel, dim3(g.blur_tiles, n_images), dim3(256), 0, bs, b, gd.dev);
-  {
-    int strips = 0;
-    for (int l = 0; l < g.nlevels; l++) strips += (g.lv[l].h + kEdgeStrip - 1) / kEdgeStrip;
-    SLAMGPU_LAUNCH("blur7_edges", bs, blur7_edges_kernel, dim3(strips, n_images), dim3(64), 0, bs,
-                   b, gd.dev);
-  }
-  if (bs != st) (void)hipEventRecord(fx.join, bs);
   {
     const dim3 block(64 * kCellWaves);
     const size_t lds = (size_t)kCellWaves * g.fast_lds_per_wave;
@@ -2198,7 +2044,6 @@ void launch_extract(const ImageBatch& b, const OrbGeomDev& gd, int n_images, hip
   SLAMGPU_LAUNCH("octree_global", st, octree_kernel, dim3(g.nlevels, n_images), dim3(kOctThreads), 0, st, gd.dev,
                      gd.ws.cell_keys, gd.ws.cell_count, gd.ws.key_scratch, gd.ws.node_scratch,
                      gd.ws.oct_keys, gd.ws.oct_count, gd.ws.err);
-  if (bs != st) (void)hipStreamWaitEvent(st, fx.join, 0);
   SLAMGPU_LAUNCH("orient_desc", st, orient_desc_kernel,
                  dim3((g.kp_cap + 4 * kKpPerWave - 1) / (4 * kKpPerWave), n_images), dim3(256), 0,
                  st, b, gd.dev, gd.ws.oct_keys, gd.ws.oct_count, gd.out.kps, gd.out.desc,

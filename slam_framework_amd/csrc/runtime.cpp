@@ -60,7 +60,6 @@ struct slamgpu_ctx {
   KeyPoint* kps_un = nullptr;
   // extractor buffers
   uint8_t* d_pyr = nullptr;
-  uint8_t* d_blur = nullptr;
   ExtractWorkspace ws{};
   ExtractOutput out{};
   // stereo
@@ -250,17 +249,11 @@ int slamgpu_create(int device, const slamgpu_orb_params* p, int cols, int rows, 
   TRY(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) == hipSuccess
           ? 0
           : fail(c, SLAMGPU_EHIP, "hipStreamCreate"));
-  {  // the side stream of launch_extract's blur branch (SLAMGPU_FORK=0 disables it)
-    const char* e = getenv("SLAMGPU_FORK");  // 0: none, 1: blur only, default: blur + FAST-0
-    const int mode = e ? atoi(e) : 2;
+  {  // the side stream of launch_extract's level-0 FAST (SLAMGPU_FORK=0 disables it)
+    const char* e = getenv("SLAMGPU_FORK");
+    const int mode = e ? atoi(e) : 1;
     ExtractStreams& fx = c->fx;
     if (mode >= 1)
-      TRY(hipStreamCreateWithFlags(&fx.side, hipStreamNonBlocking) == hipSuccess &&
-                  hipEventCreateWithFlags(&fx.fork, hipEventDisableTiming) == hipSuccess &&
-                  hipEventCreateWithFlags(&fx.join, hipEventDisableTiming) == hipSuccess
-              ? 0
-              : fail(c, SLAMGPU_EHIP, "side stream / events"));
-    if (mode >= 2)
       TRY(hipStreamCreateWithFlags(&fx.side0, hipStreamNonBlocking) == hipSuccess &&
                   hipEventCreateWithFlags(&fx.fork0, hipEventDisableTiming) == hipSuccess &&
                   hipEventCreateWithFlags(&fx.join0, hipEventDisableTiming) == hipSuccess
@@ -286,7 +279,6 @@ int slamgpu_create(int device, const slamgpu_orb_params* p, int cols, int rows, 
   TRY(hcheck(c, hipHostMalloc(reinterpret_cast<void**>(&c->h_in), 2 * (size_t)c->in_stride,
                               hipHostMallocDefault)));
   TRY(dalloc(c, &c->d_pyr, (size_t)n * g.pyr_bytes));
-  TRY(dalloc(c, &c->d_blur, (size_t)n * g.blur_bytes));
   TRY(dalloc(c, &c->ws.cell_keys, (size_t)n * g.cells_per_image * g.cell_cap));
   TRY(dalloc(c, &c->ws.cell_count, (size_t)n * g.cells_per_image));
   TRY(dalloc(c, &c->ws.key_scratch, (size_t)n * g.keys_per_image));
@@ -326,9 +318,8 @@ void slamgpu_destroy(slamgpu_ctx* c) {
   for (void* p : c->allocs) (void)hipFree(p);
   if (c->h_in) (void)hipHostFree(c->h_in);
   if (c->stream) (void)hipStreamDestroy(c->stream);
-  for (hipStream_t s : {c->fx.side0, c->fx.side})
-    if (s) (void)hipStreamDestroy(s);
-  for (hipEvent_t e : {c->fx.fork0, c->fx.join0, c->fx.fork, c->fx.join})
+  if (c->fx.side0) (void)hipStreamDestroy(c->fx.side0);
+  for (hipEvent_t e : {c->fx.fork0, c->fx.join0})
     if (e) (void)hipEventDestroy(e);
   delete c;
 }
@@ -390,8 +381,7 @@ int slamgpu_extract(slamgpu_ctx* c, const uint8_t* img, size_t step, slamgpu_key
   if (!c || !img) return SLAMGPU_EINVAL;
   HIPCHECK(c, hipSetDevice(c->device));
   if (int r = stage_images(c, &img, 1, step)) return r;
-  ImageBatch b{c->d_in, c->d_in + c->in_stride, 2 * c->in_stride, c->in_pitch, c->d_pyr,
-               c->d_blur};
+  ImageBatch b{c->d_in, c->d_in + c->in_stride, 2 * c->in_stride, c->in_pitch, c->d_pyr};
   int rc = run_frontend(c, b, 1, 1, false, c->stream);
   if (rc) return rc;
   HIPCHECK(c, hipStreamSynchronize(c->stream));
@@ -464,8 +454,7 @@ int slamgpu_frame_stereo(slamgpu_ctx* c, const uint8_t* left, const uint8_t* rig
   set_camera(c, cam);
   const uint8_t* imgs[2] = {left, right};
   if (int r = stage_images(c, imgs, 2, step)) return r;
-  ImageBatch b{c->d_in, c->d_in + c->in_stride, 2 * c->in_stride, c->in_pitch, c->d_pyr,
-               c->d_blur};
+  ImageBatch b{c->d_in, c->d_in + c->in_stride, 2 * c->in_stride, c->in_pitch, c->d_pyr};
   int rc = run_frontend(c, b, 1, 2, true, c->stream);
   if (rc) return rc;
   return slamgpu_sync(c, nullptr);
@@ -478,7 +467,7 @@ int slamgpu_frontend_device(slamgpu_ctx* c, const uint8_t* d_left, const uint8_t
       pitch < (size_t)c->geom.cols)
     return fail(c, SLAMGPU_EINVAL, "slamgpu_frontend_device: bad arguments");
   set_camera(c, cam);
-  ImageBatch b{d_left, d_right, (int64_t)frame_stride, (int)pitch, c->d_pyr, c->d_blur};
+  ImageBatch b{d_left, d_right, (int64_t)frame_stride, (int)pitch, c->d_pyr};
   return run_frontend(c, b, n_frames, 2 * n_frames, true, pick_stream(c, stream));
 }
 

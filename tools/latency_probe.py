@@ -27,7 +27,7 @@ for i in range(30):
     w["kps"].append(t2 - t1)
     w["stereo"].append(t3 - t2)
 print({k: round(1e3 * float(np.median(v)), 3) for k, v in w.items()})
-names = ["pyr_down", "blur7", "blur7_edges", "fast_cells", "octree", "octree_global", "orient_desc",
+names = ["pyr_down", "fast_cells", "octree", "octree_global", "orient_desc",
          "stereo_rows", "stereo_match", "stereo_median", "grid_build"]
 c.timing_start("*", 4096)
 for i in range(10):

@@ -5,7 +5,7 @@
 set -e
 export TMPDIR=/tmp
 OUT=${OUT:-gpurun_out/pmc_stalls}
-RE=${RE:-"fast_cells|blur7|orient_desc|pyr_down|octree|stereo_match"}
+RE=${RE:-"fast_cells|orient_desc|pyr_down|octree|stereo_match"}
 ARGS=${ARGS:-"--steps 2 --warmup 1 --no-cpu-baseline --no-optimizer --no-bow"}
 mkdir -p $OUT
 i=0
