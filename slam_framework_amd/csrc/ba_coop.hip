@@ -8,7 +8,7 @@
 //     only its structurally non-zero 6x6 blocks are listed, found per phase by a radix sort of the
 //     (block, point-pair) keys every point contributes (hipcub, stable: each block's pairs stay in
 //     point order, so every sum has a fixed order and the solver is deterministic);
-//   * one problem over G work-groups (one per CU) of a cooperative launch, synchronised by a
+//   * one problem over G work-groups (16 by default, all resident at once), synchronised by a
 //     grid barrier at each data dependency. Per LM iteration: the linearisation (a thread per
 //     point over its edges: errors, Hll, bl, the 6x3 Hpl blocks; a wave per (keyframe, chunk):
 //     partial Hpp, bp) -> barrier; per LM trial: the S blocks (a wave per block over its point
@@ -1153,7 +1153,12 @@ hipError_t launch_coop_ba(const PoseParams& P, const CoopProblem& pb, const Coop
     if (e != hipSuccess) return e;
     SLAMGPU_LAUNCH("ba_coop_chunks", st, coop_chunks_kernel, blocks(w.pairs_cap), dim3(256), 0, st,
                    w);
-    // the whole LM schedule: one cooperative launch (every work-group resident)
+    // the whole LM schedule in one launch. Its G work-groups (16 by default, at most the number
+    // the device holds resident at once, optimizer_runtime.cpp coop_grid) are all dispatched
+    // while the first spin at a grid barrier: they only wait for CUs that non-spinning kernels
+    // free, and a barrier that still does not fill raises CTL_ERR (bounded spin) rather than
+    // hanging. A plain launch: under rocprofv3 the HIP runtime's cooperative-launch path leaves
+    // the process to crash in its own teardown at exit (r2s/r2t), and costs ~50 us per call.
     CoopSchedule sch{};
     sch.n_phases = n_phases;
     sch.outlier_pass = outlier_pass ? 1 : 0;
@@ -1164,8 +1169,8 @@ hipError_t launch_coop_ba(const PoseParams& P, const CoopProblem& pb, const Coop
     const int32_t* stop = d_stop;
     void* args[] = {&Pc, &pbc, &wc, &sch, &stop};
     if (g_timer) g_timer->begin("ba_coop", st);
-    e = hipLaunchCooperativeKernel(reinterpret_cast<const void*>(&ba_coop_kernel), dim3(G),
-                                   dim3(kT), args, 0, st);
+    e = hipLaunchKernel(reinterpret_cast<const void*>(&ba_coop_kernel), dim3(G), dim3(kT), args, 0,
+                        st);
     if (g_timer) g_timer->end("ba_coop", st);
     if (e != hipSuccess) return e;
   }

@@ -72,14 +72,14 @@ struct HostStage {
   // pinned host twin of the inputs / outputs region of the single-problem BA calls
   char* pin = nullptr;
   size_t pin_bytes = 0;
-  ~HostStage() {
-    if (buf) (void)hipFree(buf);
-    if (pin) (void)hipHostFree(pin);
-    if (stop_host) (void)hipHostFree(stop_host);
-    if (stream) (void)hipStreamDestroy(stream);
-  }
 };
-thread_local HostStage t_stage;
+// One per calling thread, never destroyed: its device / pinned buffers and stream live until the
+// process ends (the runtime reclaims them); freeing them from a thread-exit destructor at process
+// exit would run after the HIP runtime's own teardown has begun.
+HostStage& thread_stage() {
+  thread_local HostStage* s = new HostStage();
+  return *s;
+}
 
 int stage_reserve(HostStage& S, size_t need) {
   int dev = 0;
@@ -142,7 +142,7 @@ int slamgpu_pose_optimization(const slamgpu_camera* cam, const float* inv_sigma2
   for (int i = 0; i < n; i++)
     if (edges[i].octave < 0 || edges[i].octave >= nlevels)
       return fail(SLAMGPU_EINVAL, "edge %d: octave %d outside [0, %d)", i, edges[i].octave, nlevels);
-  HostStage& S = t_stage;
+  HostStage& S = thread_stage();
   const size_t off_e = 256, off_T = off_e + al256((size_t)n * sizeof(slamgpu_pose_edge));
   const size_t off_o = off_T + 256, off_r = off_o + al256((size_t)n);
   if (int r = stage_reserve(S, off_r + 256)) return r;
@@ -232,13 +232,13 @@ int slamgpu_local_ba_linearize_device(
 
 namespace {
 
-// Work-groups of the cooperative single-problem solver: one per CU up to 64 (SLAMGPU_BA_WGS
+// Work-groups of the cooperative single-problem solver: 16 (SLAMGPU_BA_WGS
 // overrides), never more than can be resident at once.
 int coop_grid(int device) {
   static int cached_dev = -1, cached = 0;
   if (cached_dev == device) return cached;
   hipDeviceProp_t prop{};
-  int g = 64;
+  int g = 16;
   if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 0)
     g = std::min(g, prop.multiProcessorCount);
   if (const char* e = getenv("SLAMGPU_BA_WGS")) g = std::min(256, std::max(1, atoi(e)));
@@ -320,7 +320,7 @@ int coop_host(const char* what, const slamgpu_camera* cam, const float* inv_sigm
   const size_t o_er = o_kof + al256(4 * (size_t)K + 4);
   const size_t o_ctl = o_er + al256((size_t)n_obs + 4);
   const size_t o_io = o_ctl + 256, o_ws = o_io;
-  HostStage& S = t_stage;
+  HostStage& S = thread_stage();
   if (int r = stage_reserve(S, o_ws + wsb)) return r;
   if (S.pin_bytes < o_io) {
     if (S.pin) OPT_HIPCHECK(hipHostFree(S.pin));
