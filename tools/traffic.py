@@ -14,17 +14,33 @@ import os
 import sys
 
 
+def kernel_key(name):
+    """Short kernel name; anonymous-namespace kernels keep their own name."""
+    n = name.replace("void ", "").replace("slamgpu::", "").replace("(anonymous namespace)::", "")
+    return n.split("(")[0]
+
+
 def per_kernel(d, counter):
+    """Mean counter value per dispatch of each kernel, over its batch dispatches only (grid at least
+    1/32 of its largest): the launches the bench line describes (the same kernels also run at B=1 for the drop-in
+    latency figures, and those would drag a plain average down)."""
     acc = collections.defaultdict(list)
+    grid = {}
     for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
         for r in csv.DictReader(open(f)):
             if r["Counter_Name"] != counter:
                 continue
-            k = r["Kernel_Name"].split("(")[0].replace("void ", "").replace("slamgpu::", "")
-            acc[(k, r.get("Dispatch_Id", r.get("Correlation_Id", "")))].append(float(r["Counter_Value"]))
+            k = kernel_key(r["Kernel_Name"])
+            did = r.get("Dispatch_Id", r.get("Correlation_Id", ""))
+            acc[(k, did)].append(float(r["Counter_Value"]))
+            grid[(k, did)] = int(r.get("Grid_Size", 0) or 0)
+    gmax = collections.defaultdict(int)
+    for (k, did), g in grid.items():
+        gmax[k] = max(gmax[k], g)
     out = collections.defaultdict(list)
-    for (k, _), v in acc.items():
-        out[k].append(sum(v))  # sum over dimensions of one dispatch
+    for (k, did), v in acc.items():
+        if 32 * grid[(k, did)] >= gmax[k]:
+            out[k].append(sum(v))  # sum over dimensions of one dispatch
     return {k: sum(v) / len(v) for k, v in out.items()}
 
 
@@ -46,7 +62,7 @@ def main():
            "command": "python3 bench.py " + os.environ.get("ARGS", "") + " (tools/pmc_traffic.sh)",
            "source": "tools/pmc_traffic.sh + tools/traffic.py",
            "method": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes, "
-                     "kernel-trace only; FETCH_SIZE (KB) x read factor calibrated on membench "
+                     "kernel-trace only; each kernel's batch dispatches (grid >= 1/32 of its largest); FETCH_SIZE (KB) x read factor calibrated on membench "
                      "copy4/copy16 (known 512 MiB) + WRITE_SIZE (KB)",
            "calibration_read_factor": cal, "write_calibration": {k: known / (v * 1024.0) for k, v in mb_w.items()
                                                                 if k.startswith("copy")},
