@@ -21,6 +21,10 @@
 
 namespace slamgpu {
 
+#ifndef MATCH_XCD
+#define MATCH_XCD 1
+#endif
+
 constexpr int TH_HIGH = 100, TH_LOW = 50, HISTO_LENGTH = 30;
 constexpr uint64_t kNoKey = ~0ull;
 
@@ -125,9 +129,14 @@ __global__ __launch_bounds__(256) void stereo_match_kernel(ImageBatch b,
                                                            const OrbGeom* __restrict__ g,
                                                            FrameKps ext, Camera cam, int nrows,
                                                            StereoWorkspace ws, StereoOut out) {
-  const int f = blockIdx.y;
+#if MATCH_XCD
+  int f, bx;
+  xcd_image_block(&f, &bx);  // a frame's work-groups share one XCD's L2 (its right keypoints)
+#else
+  const int f = blockIdx.y, bx = blockIdx.x;
+#endif
   const int lane = threadIdx.x & 63;
-  const int iL = blockIdx.x * 4 + wave_id();
+  const int iL = bx * 4 + wave_id();
   const int il = 2 * f, ir = 2 * f + 1;
   const int nl = ext.n[il * ext.n_stride];
   if (iL >= nl) return;
@@ -555,9 +564,14 @@ __global__ __launch_bounds__(256) void search_cand_kernel(
     FrameKps cur, const float* __restrict__ u_right, int64_t ur_stride, Camera cam,
     const OrbGeom* __restrict__ g, const Q* __restrict__ queries, const F2FPose* __restrict__ poses,
     int th, GridWorkspace gw, MatchWorkspace mw, MatchIO io) {
-  const int f = blockIdx.y;
+#if MATCH_XCD
+  int f, bx;
+  xcd_image_block(&f, &bx);  // a frame's work-groups share one XCD's L2 (its grid and keypoints)
+#else
+  const int f = blockIdx.y, bx = blockIdx.x;
+#endif
   const int lane = threadIdx.x & 63;
-  const int qi = blockIdx.x * 4 + wave_id();
+  const int qi = bx * 4 + wave_id();
   if (qi >= io.q_count[f]) return;
   const int q = io.q_start[f] + qi;
   FrameView F;

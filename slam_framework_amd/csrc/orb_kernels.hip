@@ -18,7 +18,7 @@
 
 namespace slamgpu {
 
-__constant__ int8_t c_pattern[1024] = {
+__constant__ __attribute__((aligned(16))) int8_t c_pattern[1024] = {
 #include "orb_pattern.inc"
 };
 
@@ -1724,12 +1724,23 @@ __device__ __forceinline__ int reduce_scatter16(int (&v)[16], int lane) {
 // dwords of its column (v_alignbit for an odd start) and 4 v_dot2_u32_u16, and rounds with the
 // column's rule (half to even inside the SSE span x < W - W%4, half up in the scalar tail).
 // Border keypoints (the window leaves the image: reflect-101 columns) load bytes one by one.
-// Keypoints are processed kFG at a time per wave (LDS: kFG x 40 x 44 u16 per wave).
-constexpr int kRtCols = 40, kRtRows = 44;
-#ifndef FUSED_GROUP
-#define FUSED_GROUP 1
+// LDS: one 40 x 44 u16 window per wave.
+#ifndef RT_ROWS
+#define RT_ROWS 44
 #endif
-constexpr int kFG = FUSED_GROUP;  // keypoints per row-sum pass (LDS: kFG x 3.5 KB per wave)
+#ifndef RS_PREFETCH
+#define RS_PREFETCH 1
+#endif
+#ifndef OD_FENCE
+#define OD_FENCE 0
+#endif
+#ifndef OD_UNROLL_J
+#define OD_UNROLL_J 1
+#endif
+#ifndef PAT_PACKED
+#define PAT_PACKED 1
+#endif
+constexpr int kRtCols = 40, kRtRows = RT_ROWS;  // u16 per transposed column (even)
 
 __device__ __forceinline__ uint32_t rt_tap(const uint16_t* rt, int sy, int sx, uint32_t K01,
                                            uint32_t K23, uint32_t K21, uint32_t K0) {
@@ -1744,11 +1755,16 @@ __device__ __forceinline__ uint32_t rt_tap(const uint16_t* rt, int sy, int sx, u
   return dot2u(p0, K01, dot2u(p1, K23, dot2u(p2, K21, dot2u(p3, K0, 0u))));
 }
 
-__global__ __launch_bounds__(256) void orient_desc_kernel(
+#ifdef OD_WAVES
+#define OD_ATTR __attribute__((amdgpu_waves_per_eu(OD_WAVES)))
+#else
+#define OD_ATTR
+#endif
+__global__ __launch_bounds__(256) OD_ATTR void orient_desc_kernel(
     ImageBatch b, const OrbGeom* __restrict__ g, const uint32_t* __restrict__ oct_keys,
     const int* __restrict__ oct_count, KeyPoint* __restrict__ kps, uint8_t* __restrict__ desc,
     int* __restrict__ nkps) {
-  __shared__ __attribute__((aligned(16))) uint16_t s_rt[4][kFG][kRtCols * kRtRows];
+  __shared__ __attribute__((aligned(16))) uint16_t s_rt[4][1][kRtCols * kRtRows];
   int img, bx;
   xcd_image_block(&img, &bx);
   const int lane = threadIdx.x & 63, wid = wave_id();
@@ -1797,44 +1813,53 @@ __global__ __launch_bounds__(256) void orient_desc_kernel(
     klev[j] = __builtin_amdgcn_readlane(my_level, jj);
   }
   const int in_pitch = __builtin_amdgcn_readfirstlane(b.in_pitch);
-  // Phase 1: the IC_Angle patches (raw level, registers)
-  uint32_t raw[kKpPerWave][5];
-#pragma unroll
-  for (int j = 0; j < kKpPerWave; j++) {
-#pragma unroll
-    for (int k = 0; k < 5; k++) raw[j][k] = 0;
-    const int level = klev[j];
-    const int x = key_x(kkey[j]) + kMinBorder, y = key_y(kkey[j]) + kMinBorder;
-    const LevelGeom& L = g->lv[level];
-    const int pitch = level == 0 ? in_pitch : L.pitch;
-    const uint8_t* im = level == 0 ? batch_image(b, img)
-                                   : b.pyr + (int64_t)img * g->pyr_bytes + L.offset;
-    const uint8_t* rbase = im + (int64_t)(y - 15) * pitch + ((x - 15) & ~3);
-    const uint8_t* rp = rbase + (__umul24(hr, pitch) + 16 * hh);
-    if (hr < 31) {
-      if ((((uintptr_t)im | (uintptr_t)pitch) & 3) == 0) {
-#pragma unroll
-        for (int k = 0; k < 5; k++) raw[j][k] = reinterpret_cast<const uint32_t*>(rp)[k];
-      } else {
-#pragma unroll
-        for (int k = 0; k < 20; k++) raw[j][k >> 2] |= (uint32_t)rp[k] << (8 * (k & 3));
-      }
-    }
-  }
-  // Phase 2: moments -> angle, sin, cos (lane 8j holds keypoint j's)
+  // Phases 1-2: the IC_Angle patches (raw level, registers), PH12_SPLIT keypoints at a time,
+  // then their moments (lane 8j ends up with keypoint j's)
+#ifndef PH12_SPLIT
+#define PH12_SPLIT 4
+#endif
   int mv[16];
 #pragma unroll
-  for (int j = 0; j < kKpPerWave; j++) {
-    const int a = (key_x(kkey[j]) + kMinBorder - 15) & 3;
-    uint32_t s = 0, t = 0;
+  for (int j0 = 0; j0 < kKpPerWave; j0 += PH12_SPLIT) {
+    uint32_t raw[PH12_SPLIT][5];
 #pragma unroll
-    for (int k = 0; k < 4; k++) {
-      const uint32_t e = __builtin_amdgcn_alignbyte(raw[j][k + 1], raw[j][k], a);
-      s = __builtin_amdgcn_udot4(e, one[k], s, false);
-      t = __builtin_amdgcn_udot4(e, wt[k], t, false);
+    for (int jj = 0; jj < PH12_SPLIT; jj++) {
+      const int j = j0 + jj;
+#pragma unroll
+      for (int k = 0; k < 5; k++) raw[jj][k] = 0;
+      const int level = klev[j];
+      const int x = key_x(kkey[j]) + kMinBorder, y = key_y(kkey[j]) + kMinBorder;
+      const LevelGeom& L = g->lv[level];
+      const int pitch = level == 0 ? in_pitch : L.pitch;
+      const uint8_t* im = level == 0 ? batch_image(b, img)
+                                     : b.pyr + (int64_t)img * g->pyr_bytes + L.offset;
+      const uint8_t* rbase = im + (int64_t)(y - 15) * pitch + ((x - 15) & ~3);
+      const uint8_t* rp = rbase + (__umul24(hr, pitch) + 16 * hh);
+      if (hr < 31) {
+        if ((((uintptr_t)im | (uintptr_t)pitch) & 3) == 0) {
+#pragma unroll
+          for (int k = 0; k < 5; k++) raw[jj][k] = reinterpret_cast<const uint32_t*>(rp)[k];
+        } else {
+#pragma unroll
+          for (int k = 0; k < 20; k++) raw[jj][k >> 2] |= (uint32_t)rp[k] << (8 * (k & 3));
+        }
+      }
     }
-    mv[2 * j] = (int)t - 20 * (int)s;
-    mv[2 * j + 1] = hv * (int)s;
+#pragma unroll
+    for (int jj = 0; jj < PH12_SPLIT; jj++) {
+      const int j = j0 + jj;
+      const int a = (key_x(kkey[j]) + kMinBorder - 15) & 3;
+      uint32_t s = 0, t = 0;
+#pragma unroll
+      for (int k = 0; k < 4; k++) {
+        const uint32_t e = __builtin_amdgcn_alignbyte(raw[jj][k + 1], raw[jj][k], a);
+        s = __builtin_amdgcn_udot4(e, one[k], s, false);
+        t = __builtin_amdgcn_udot4(e, wt[k], t, false);
+      }
+      mv[2 * j] = (int)t - 20 * (int)s;
+      mv[2 * j + 1] = hv * (int)s;
+    }
+    if (PH12_SPLIT < kKpPerWave) __asm__ volatile("" ::: "memory");
   }
   int mom = reduce_scatter16(mv, lane);
   const int m01 = __builtin_amdgcn_mov_dpp(mom, 0x104, 0xf, 0xf, false);  // row_shl:4
@@ -1843,6 +1868,13 @@ __global__ __launch_bounds__(256) void orient_desc_kernel(
   float sa, ca;
   glibc_sincosf(angle * factorPI, &sa, &ca);
   // Phase 3: per 4 keypoints, the row-summed windows (LDS) then the 512 blurred samples each
+#if PAT_PACKED
+  // the lane's 4 tests (8 points) as int8 (x0, y0, x1, y1) words: 4 VGPRs instead of 32
+  uint32_t pat[4];
+#pragma unroll
+  for (int r = 0; r < 4; r++)
+    pat[r] = reinterpret_cast<const uint32_t*>(c_pattern)[r * 64 + lane];
+#else
   f32x2 ppx[4][2], ppy[4][2];
 #pragma unroll
   for (int r = 0; r < 4; r++) {
@@ -1854,80 +1886,134 @@ __global__ __launch_bounds__(256) void orient_desc_kernel(
       ppy[r][e] = (f32x2){py, py};
     }
   }
+#endif
   const uint32_t q0 = g->gauss[0], q1 = g->gauss[1], q2 = g->gauss[2], q3 = g->gauss[3];
   const uint32_t KA = q0 | q1 << 8 | q2 << 16 | q3 << 24, KB = q2 | q1 << 8 | q0 << 16;
   const uint32_t K01 = q0 | q1 << 16, K23 = q2 | q3 << 16, K21 = q2 | q1 << 16, K0 = q0;
   const f32x2 magic = {12582912.0f, 12582912.0f};
   uint32_t dlo = 0, dhi = 0;
+  // Per keypoint: its row-summed window into LDS, then its 256 tests from LDS. The window's raw
+  // rows (one 16-byte load per lane task, 7 tasks per lane) of keypoint j + 1 are in flight
+  // while keypoint j's tests run (RS_PREFETCH). LDS hand-offs are within the wave (LDS executes
+  // a wave's instructions in order): only compiler ordering is needed between the passes.
+  struct RsGeo {
+    const uint8_t* im;
+    int pitch, w, h, kx, ky;
+    bool fastp;
+  };
+  auto rs_geo = [&](int j) {
+    RsGeo G;
+    const int jj = min(j, nk - 1);
+    const int level = __builtin_amdgcn_readlane(my_level, jj);
+    const uint32_t key = (uint32_t)__builtin_amdgcn_readlane(my_key, jj);
+    const LevelGeom& L = g->lv[level];
+    G.kx = key_x(key) + kMinBorder;
+    G.ky = key_y(key) + kMinBorder;
+    G.w = L.w;
+    G.h = L.h;
+    G.pitch = level == 0 ? in_pitch : L.pitch;
+    G.im = level == 0 ? batch_image(b, img) : b.pyr + (int64_t)img * g->pyr_bytes + L.offset;
+    G.fastp = G.kx >= 21 && G.kx <= G.w - 31 && ((((uintptr_t)G.im | (uintptr_t)G.pitch) & 3) == 0);
+    return G;
+  };
+  auto rs_load = [&](const RsGeo& G, uint4 (&q)[7]) {
+    if (!G.fastp) return;
 #pragma unroll
-  for (int half = 0; half < kKpPerWave / kFG; half++) {
+    for (int i = 0; i < 7; i++) {
+      const int t = lane + 64 * i;
+      if (t < 43 * 10) {
+        const int r = t / 10, gq = t - r * 10;
+        const uint8_t* row = G.im + (int64_t)reflect101(G.ky - 21 + r, G.h) * G.pitch;
+        q[i] = *reinterpret_cast<const uint4*>(row + ((G.kx - 21 + 4 * gq) & ~3));
+      }
+    }
+  };
+  uint16_t* rtw = &s_rt[wid][0][0];
+  RsGeo gn = rs_geo(0);
+#if RS_PREFETCH
+  uint4 qn[7];
+  rs_load(gn, qn);
+#endif
+#if OD_UNROLL_J
 #pragma unroll
-    for (int jj = 0; jj < kFG; jj++) {  // row sums of keypoint kFG half + jj
-      const int j = kFG * half + jj;
-      const int level = klev[j];
-      const int kx = key_x(kkey[j]) + kMinBorder, ky = key_y(kkey[j]) + kMinBorder;
-      const LevelGeom& L = g->lv[level];
-      const int w = L.w, h = L.h;
-      const int pitch = level == 0 ? in_pitch : L.pitch;
-      const uint8_t* im = level == 0 ? batch_image(b, img)
-                                     : b.pyr + (int64_t)img * g->pyr_bytes + L.offset;
-      const bool fastp = kx >= 21 && kx <= w - 31 && ((((uintptr_t)im | (uintptr_t)pitch) & 3) == 0);
-      const uint32_t sft = (uint32_t)((kx - 21) & 3);
-      uint16_t* rt = &s_rt[wid][jj][0];
+#else
+#pragma unroll 1
+#endif
+  for (int j = 0; j < kKpPerWave; j++) {
+    const RsGeo G = gn;
+    uint4 q[7];
+#if RS_PREFETCH
 #pragma unroll
-      for (int i = 0; i < 7; i++) {
-        const int t = lane + 64 * i;
-        if (t < 43 * 10) {
-          const int r = t / 10, gq = t - r * 10;
-          const int y = reflect101(ky - 21 + r, h);
-          const uint8_t* row = im + (int64_t)y * pitch;
-          const int x0 = kx - 18 + 4 * gq;
-          uint32_t u0, u1, u2;
-          if (fastp) {
-            const uint4 q = *reinterpret_cast<const uint4*>(row + ((x0 - 3) & ~3));
-            u0 = __builtin_amdgcn_alignbyte(q.y, q.x, sft);
-            u1 = __builtin_amdgcn_alignbyte(q.z, q.y, sft);
-            u2 = __builtin_amdgcn_alignbyte(q.w, q.z, sft);
-          } else {
-            uint32_t wv[3] = {0, 0, 0};
+    for (int i = 0; i < 7; i++) q[i] = qn[i];
+#else
+    rs_load(G, q);
+#endif
+    const uint32_t sft = (uint32_t)((G.kx - 21) & 3);
 #pragma unroll
-            for (int k = 0; k < 10; k++)
-              wv[k >> 2] |= (uint32_t)row[reflect101(x0 - 3 + k, w)] << (8 * (k & 3));
-            u0 = wv[0];
-            u1 = wv[1];
-            u2 = wv[2];
-          }
+    for (int i = 0; i < 7; i++) {
+      const int t = lane + 64 * i;
+      if (t < 43 * 10) {
+        const int r = t / 10, gq = t - r * 10;
+        uint32_t u0, u1, u2;
+        if (G.fastp) {
+          u0 = __builtin_amdgcn_alignbyte(q[i].y, q[i].x, sft);
+          u1 = __builtin_amdgcn_alignbyte(q[i].z, q[i].y, sft);
+          u2 = __builtin_amdgcn_alignbyte(q[i].w, q[i].z, sft);
+        } else {  // the window leaves the image: reflect-101 columns, byte loads
+          const uint8_t* row = G.im + (int64_t)reflect101(G.ky - 21 + r, G.h) * G.pitch;
+          const int x0 = G.kx - 18 + 4 * gq;
+          uint32_t wv[3] = {0, 0, 0};
 #pragma unroll
-          for (int jx = 0; jx < 4; jx++) {
-            const uint32_t lo = jx == 0 ? u0 : __builtin_amdgcn_alignbyte(u1, u0, jx);
-            const uint32_t hi = jx == 0 ? u1 : __builtin_amdgcn_alignbyte(u2, u1, jx);
-            const uint32_t R = __builtin_amdgcn_udot4(lo, KA, __builtin_amdgcn_udot4(hi, KB, 0u, false), false);
-            rt[(4 * gq + jx) * kRtRows + r] = (uint16_t)R;
-          }
+          for (int k = 0; k < 10; k++)
+            wv[k >> 2] |= (uint32_t)row[reflect101(x0 - 3 + k, G.w)] << (8 * (k & 3));
+          u0 = wv[0];
+          u1 = wv[1];
+          u2 = wv[2];
+        }
+#pragma unroll
+        for (int jx = 0; jx < 4; jx++) {
+          const uint32_t lo = jx == 0 ? u0 : __builtin_amdgcn_alignbyte(u1, u0, jx);
+          const uint32_t hi = jx == 0 ? u1 : __builtin_amdgcn_alignbyte(u2, u1, jx);
+          const uint32_t R = __builtin_amdgcn_udot4(lo, KA, __builtin_amdgcn_udot4(hi, KB, 0u, false), false);
+          rtw[(4 * gq + jx) * kRtRows + r] = (uint16_t)R;
         }
       }
     }
+#if OD_FENCE
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-#pragma unroll
-    for (int jj = 0; jj < kFG; jj++) {  // the 256 tests of keypoint kFG half + jj
-      const int j = kFG * half + jj;
-      const int kx = key_x(kkey[j]) + kMinBorder;
-      const int w = g->lv[klev[j]].w, xvec = w - (w & 3);
+#else
+    __asm__ volatile("" ::: "memory");
+#endif
+    if (j + 1 < kKpPerWave) {
+      gn = rs_geo(j + 1);
+#if RS_PREFETCH
+      rs_load(gn, qn);
+#endif
+    }
+    {
+      const int kx = G.kx;
+      const int w = G.w, xvec = w - (w & 3);
       const bool tail_possible = kx + 18 >= xvec;
       const float cj = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(ca), 8 * j));
       const float sj = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(sa), 8 * j));
       const f32x2 ab = {sj, cj}, nab = {cj, -sj};
-      const uint16_t* rt = &s_rt[wid][jj][0];
+      const uint16_t* rt = &s_rt[wid][0][0];
 #pragma unroll
       for (int r = 0; r < 4; r++) {
         uint32_t v[2];
 #pragma unroll
         for (int e = 0; e < 2; e++) {
-          const f32x2 q = __builtin_elementwise_fma(ppx[r][e], ab, ppy[r][e] * nab) + magic;
-          const int sy = (int)__float_as_uint(q.x) - 0x4B400000;
-          const int sx = (int)__float_as_uint(q.y) - 0x4B400000;
+#if PAT_PACKED
+          const float px = (float)(int)(int8_t)(pat[r] >> (16 * e));
+          const float py = (float)(int)(int8_t)(pat[r] >> (16 * e + 8));
+          const f32x2 sp = __builtin_elementwise_fma((f32x2){px, px}, ab, (f32x2){py, py} * nab) + magic;
+#else
+          const f32x2 sp = __builtin_elementwise_fma(ppx[r][e], ab, ppy[r][e] * nab) + magic;
+#endif
+          const int sy = (int)__float_as_uint(sp.x) - 0x4B400000;
+          const int sx = (int)__float_as_uint(sp.y) - 0x4B400000;
           const uint32_t s = rt_tap(rt, sy, sx, K01, K23, K21, K0);
           const bool tail = tail_possible && kx + sx >= xvec;
           uint32_t o = (s + (tail ? 0x8000u : 0x7fffu + ((s >> 16) & 1u))) >> 16;
@@ -1940,9 +2026,13 @@ __global__ __launch_bounds__(256) void orient_desc_kernel(
         }
       }
     }
+#if OD_FENCE
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+#else
+    __asm__ volatile("" ::: "memory");
+#endif
   }
   const int64_t o = (int64_t)img * g->kp_cap + k0;
   if (lane < 4 * nk)

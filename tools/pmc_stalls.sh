@@ -6,7 +6,7 @@ set -e
 export TMPDIR=/tmp
 OUT=${OUT:-gpurun_out/pmc_stalls}
 RE=${RE:-"fast_cells|orient_desc|pyr_down|octree|stereo_match"}
-ARGS=${ARGS:-"--steps 2 --warmup 1 --no-cpu-baseline --no-optimizer --no-bow"}
+ARGS=${ARGS:-"--steps 2 --warmup 1 --no-cpu-baseline --no-optimizer --no-bow --no-latency --inflight 1"}
 mkdir -p $OUT
 i=0
 while read -r grp; do
