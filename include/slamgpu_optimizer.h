@@ -8,6 +8,9 @@
  *   slamgpu_pose_optimization_device  the same, batched over frames, inputs resident in HBM
  *   slamgpu_local_bundle_adjustment   Optimizer::LocalBundleAdjustment     optimizer.cpp:413-716
  *   slamgpu_local_bundle_adjustment_device   the same, batched over independent problems
+ *   slamgpu_global_bundle_adjustment  Optimizer::BundleAdjustment          optimizer.cpp:18-207
+ *   slamgpu_optimize_sim3             Optimizer::OptimizeSim3              optimizer.cpp:962-1152
+ *   slamgpu_optimize_sim3_device      the same, batched over loop candidates
  * These calls hold no state, so they take no handle. Every function returns 0 or a negative
  * SLAMGPU_E* code (slamgpu.h) with a message in slamgpu_optimizer_last_error() (per thread).
  *
@@ -182,6 +185,49 @@ int slamgpu_local_ba_linearize_device(
     const slamgpu_ba_obs* d_obs, const slamgpu_ba_linear* out, int32_t* d_status,
     void* d_workspace, size_t workspace_bytes, int total_kf, int total_points, int total_obs,
     void* stream);
+
+/* ---- OptimizeSim3 ------------------------------------------------------------------------ */
+/* One correspondence of Optimizer::OptimizeSim3 (optimizer.cpp:1020-1096), for a match i whose
+ * map points are both good and seen by KF2 (:1033-1055; the caller skips the others): the
+ * points in their keyframes' camera frames as the reference forms them (P3D1c = R1w * P3D1w +
+ * t1w, P3D2c = R2w * P3D2w + t2w, f32 cv::Mat arithmetic), KF1's undistorted keypoint i, KF2's
+ * undistorted keypoint GetIndexInKeyFrame(pKF2), and their octaves. 48 bytes. */
+typedef struct {
+  float x1c[3];
+  float x2c[3];
+  float u1, v1;
+  float u2, v2;
+  int32_t octave1, octave2;
+} slamgpu_sim3_match;
+
+/* Largest correspondence count per OptimizeSim3 problem. */
+#define SLAMGPU_SIM3_MAX_MATCHES 4096
+
+/* Replaces: int Optimizer::OptimizeSim3(KeyFrame* pKF1, KeyFrame* pKF2, vector<MapPoint*>&
+ * vpMatches1, g2o::Sim3& g2oS12, float th2, bool bFixScale)  optimizer.cpp:962-1152.
+ * K1 / K2: fx, fy, cx, cy of the keyframes' calib_mat; inv_sigma2_1 / _2[nlevels]: their
+ * inv_level_sigma_sq. S12: the g2o::Sim3 as (qx, qy, qz, qw, tx, ty, tz, s) -- Sim3::operator[]
+ * order -- updated in place unless the reference returns early. inlier[n]: 0 where the reference
+ * sets vpMatches1[i] = NULL (pairs whose chi2 exceeds th2 after the first or the second
+ * optimisation), 1 elsewhere. *n_inliers: the reference's return value (0 on its early return,
+ * :1122-1125). Synchronous. */
+int slamgpu_optimize_sim3(const float K1[4], const float K2[4], const float* inv_sigma2_1,
+                          const float* inv_sigma2_2, int nlevels,
+                          const slamgpu_sim3_match* matches, int n, float th2, int fix_scale,
+                          double S12[8], uint8_t* inlier, int* n_inliers);
+
+/* Batched (LoopCloser::ComputeSim3 tries its candidates in order and keeps the first with >= 20
+ * inliers, loop_closer.cpp; every candidate can run at once and the caller takes the first),
+ * asynchronous on `stream`, pointers device memory: problem p owns
+ * d_matches[d_match_start[p] .. d_match_start[p+1]), d_S12[8 p ...] (in/out), inlier flags at
+ * the matches' positions, d_n_inliers[p] (-1 when it exceeds SLAMGPU_SIM3_MAX_MATCHES, S12 then
+ * untouched) and, if not NULL, d_lm_iterations[p]. The keyframe cameras / levels are shared. */
+int slamgpu_optimize_sim3_device(const float K1[4], const float K2[4], const float* inv_sigma2_1,
+                                 const float* inv_sigma2_2, int nlevels,
+                                 const slamgpu_sim3_match* d_matches,
+                                 const int32_t* d_match_start, int n_problems, float th2,
+                                 int fix_scale, double* d_S12, uint8_t* d_inlier,
+                                 int32_t* d_n_inliers, int32_t* d_lm_iterations, void* stream);
 
 const char* slamgpu_optimizer_last_error(void);
 

@@ -281,6 +281,28 @@ int oc_fuse(const oc_keypoint* kps, const uint8_t* desc, const float* ur, int n,
             int nlevels, float log_scale_factor, const oc_fuse_point* pts, int n_pts, float th,
             int32_t* best_idx, int32_t* best_dist);
 
+/* ---- OptimizeSim3 (sim3_oracle.c) ------------------------------------------------------ */
+/* One correspondence of OptimizeSim3 (optimizer.cpp:1020-1096): the two map points in their
+ * keyframes' camera frames (f32, as cv::Mat R*X + t gives them), the undistorted keypoints and
+ * their octaves. 48 B, == slamgpu_sim3_match. */
+typedef struct {
+  float x1c[3], x2c[3];
+  float u1, v1, u2, v2;
+  int32_t octave1, octave2;
+} oc_sim3_match;
+/* S12: g2o::Sim3 as (qx, qy, qz, qw, tx, ty, tz, s); returns nIn (0 on the early return, S12
+ * then untouched); inlier[i] = 0 where the reference nulls vpMatches1. */
+int oc_optimize_sim3(const float K1[4], const float K2[4], const float* inv_sigma2_1,
+                     const float* inv_sigma2_2, int nlevels, const oc_sim3_match* m, int n,
+                     float th2, int fix_scale, double S12[8], uint8_t* inlier, int* lm_iterations);
+void oc_sim3_exp(const double u[7], double out[8]);
+void oc_sim3_log(const double in[8], double u[7]);
+void oc_sim3_mul(const double a[8], const double b[8], double out[8]);
+void oc_sim3_inverse(const double a[8], double out[8]);
+void oc_sim3_map(const double a[8], const double x[3], double o[3]);
+void oc_sim3_pair_eval(const float K1[4], const float K2[4], const oc_sim3_match* m,
+                       const double S12[8], int fix_scale, double e[4], double J[28]);
+
 #ifdef __cplusplus
 }
 #endif

@@ -22,6 +22,7 @@
 #include "ba_coop.h"
 #include "ba_kernels.h"
 #include "pose_kernels.h"
+#include "sim3_kernels.h"
 
 using namespace slamgpu;
 
@@ -107,6 +108,29 @@ int stage_reserve(HostStage& S, size_t need) {
 }
 
 size_t al256(size_t x) { return (x + 255) / 256 * 256; }
+
+int make_sim3_params(const float K1[4], const float K2[4], const float* isig1, const float* isig2,
+                     int nlevels, float th2, int fix_scale, Sim3Params* P) {
+  if (!K1 || !K2 || !isig1 || !isig2)
+    return fail(SLAMGPU_EINVAL, "calibrations and inv_sigma2 arrays are required");
+  if (nlevels < 1 || nlevels > SLAMGPU_MAX_LEVELS)
+    return fail(SLAMGPU_EINVAL, "nlevels %d outside [1, %d]", nlevels, SLAMGPU_MAX_LEVELS);
+  if (!(th2 >= 0.f)) return fail(SLAMGPU_EINVAL, "th2 %g is not a threshold", (double)th2);
+  std::memset(P, 0, sizeof(*P));
+  for (int i = 0; i < 4; i++) {
+    P->K1[i] = (double)K1[i];
+    P->K2[i] = (double)K2[i];
+  }
+  for (int i = 0; i < nlevels; i++) {
+    P->isig1[i] = isig1[i];
+    P->isig2[i] = isig2[i];
+  }
+  P->nlevels = nlevels;
+  P->th2 = th2;
+  P->delta = (double)std::sqrt(th2);  // const float deltaHuber = sqrt(th2) (optimizer.cpp:1017)
+  P->fix_scale = fix_scale ? 1 : 0;
+  return 0;
+}
 
 }  // namespace
 
@@ -435,6 +459,64 @@ int slamgpu_global_bundle_adjustment(const slamgpu_camera* cam, const float* inv
                             (double)(float)sqrt(7.815)}};
   return coop_host("global BA", cam, inv_sigma2, nlevels, kf_Tcw, kf_mode, n_kf, points, n_points,
                    point_obs_start, obs, stop_flag, nullptr, ph, 1, false, lm_iterations);
+}
+
+int slamgpu_optimize_sim3_device(const float K1[4], const float K2[4], const float* inv_sigma2_1,
+                                 const float* inv_sigma2_2, int nlevels,
+                                 const slamgpu_sim3_match* d_matches,
+                                 const int32_t* d_match_start, int n_problems, float th2,
+                                 int fix_scale, double* d_S12, uint8_t* d_inlier,
+                                 int32_t* d_n_inliers, int32_t* d_lm_iterations, void* stream) {
+  Sim3Params P;
+  if (int r = make_sim3_params(K1, K2, inv_sigma2_1, inv_sigma2_2, nlevels, th2, fix_scale, &P))
+    return r;
+  if (n_problems < 0) return fail(SLAMGPU_EINVAL, "n_problems %d < 0", n_problems);
+  if (n_problems > 0 && (!d_match_start || !d_S12 || !d_n_inliers || !d_matches || !d_inlier))
+    return fail(SLAMGPU_EINVAL, "null device buffer");
+  OPT_HIPCHECK(launch_optimize_sim3(d_matches, d_match_start, n_problems, P, d_S12, d_inlier,
+                                    d_n_inliers, d_lm_iterations,
+                                    static_cast<hipStream_t>(stream)));
+  return 0;
+}
+
+int slamgpu_optimize_sim3(const float K1[4], const float K2[4], const float* inv_sigma2_1,
+                          const float* inv_sigma2_2, int nlevels,
+                          const slamgpu_sim3_match* matches, int n, float th2, int fix_scale,
+                          double S12[8], uint8_t* inlier, int* n_inliers) {
+  Sim3Params P;
+  if (int r = make_sim3_params(K1, K2, inv_sigma2_1, inv_sigma2_2, nlevels, th2, fix_scale, &P))
+    return r;
+  if (!S12 || !n_inliers || n < 0 || (n > 0 && (!matches || !inlier)))
+    return fail(SLAMGPU_EINVAL, "bad arguments");
+  if (n > SLAMGPU_SIM3_MAX_MATCHES)
+    return fail(SLAMGPU_ECAP, "%d matches > SLAMGPU_SIM3_MAX_MATCHES (%d)", n,
+                SLAMGPU_SIM3_MAX_MATCHES);
+  for (int i = 0; i < n; i++)
+    if (matches[i].octave1 < 0 || matches[i].octave1 >= nlevels || matches[i].octave2 < 0 ||
+        matches[i].octave2 >= nlevels)
+      return fail(SLAMGPU_EINVAL, "match %d: octave outside [0, %d)", i, nlevels);
+  HostStage& S = thread_stage();
+  const size_t off_m = 256, off_S = off_m + al256((size_t)n * sizeof(slamgpu_sim3_match));
+  const size_t off_i = off_S + 256, off_r = off_i + al256((size_t)n);
+  if (int r = stage_reserve(S, off_r + 256)) return r;
+  char* b = static_cast<char*>(S.buf);
+  const int32_t start[2] = {0, n};
+  OPT_HIPCHECK(hipMemcpyAsync(b, start, sizeof(start), hipMemcpyHostToDevice, S.stream));
+  if (n > 0)
+    OPT_HIPCHECK(hipMemcpyAsync(b + off_m, matches, (size_t)n * sizeof(slamgpu_sim3_match),
+                                hipMemcpyHostToDevice, S.stream));
+  OPT_HIPCHECK(hipMemcpyAsync(b + off_S, S12, 8 * sizeof(double), hipMemcpyHostToDevice, S.stream));
+  OPT_HIPCHECK(launch_optimize_sim3(
+      reinterpret_cast<const slamgpu_sim3_match*>(b + off_m), reinterpret_cast<int32_t*>(b), 1, P,
+      reinterpret_cast<double*>(b + off_S), reinterpret_cast<uint8_t*>(b + off_i),
+      reinterpret_cast<int32_t*>(b + off_r), nullptr, S.stream));
+  int32_t res = 0;
+  OPT_HIPCHECK(hipMemcpyAsync(&res, b + off_r, sizeof(res), hipMemcpyDeviceToHost, S.stream));
+  OPT_HIPCHECK(hipMemcpyAsync(S12, b + off_S, 8 * sizeof(double), hipMemcpyDeviceToHost, S.stream));
+  if (n > 0) OPT_HIPCHECK(hipMemcpyAsync(inlier, b + off_i, n, hipMemcpyDeviceToHost, S.stream));
+  OPT_HIPCHECK(hipStreamSynchronize(S.stream));
+  *n_inliers = res;
+  return 0;
 }
 
 }  // extern "C"

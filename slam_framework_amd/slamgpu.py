@@ -32,6 +32,10 @@ MPS_QUERY_DTYPE = np.dtype([("proj_x", "<f4"), ("proj_y", "<f4"), ("proj_xr", "<
                             ("view_cos", "<f4"), ("level", "<i4"), ("in_view", "<i4"),
                             ("is_bad", "<i4"), ("mp_id", "<i4"), ("blocks", "<i4"),
                             ("pad", "<i4", (3,)), ("desc", "u1", (32,))])
+# slamgpu_sim3_match (include/slamgpu_optimizer.h): one OptimizeSim3 correspondence.
+SIM3_MATCH_DTYPE = np.dtype([("x1c", "<f4", (3,)), ("x2c", "<f4", (3,)), ("u1", "<f4"),
+                             ("v1", "<f4"), ("u2", "<f4"), ("v2", "<f4"), ("octave1", "<i4"),
+                             ("octave2", "<i4")])
 # slamgpu_pose_edge (include/slamgpu_optimizer.h): one PoseOptimization correspondence.
 POSE_EDGE_DTYPE = np.dtype([("xw", "<f4", (3,)), ("u", "<f4"), ("v", "<f4"), ("ur", "<f4"),
                             ("octave", "<i4")])
@@ -55,7 +59,7 @@ EXPORTS = [
     "slamgpu_timing_read", "slamgpu_pose_optimization", "slamgpu_pose_optimization_device",
     "slamgpu_optimizer_last_error", "slamgpu_local_bundle_adjustment",
     "slamgpu_local_bundle_adjustment_device", "slamgpu_local_ba_workspace_bytes",
-    "slamgpu_global_bundle_adjustment",
+    "slamgpu_global_bundle_adjustment", "slamgpu_optimize_sim3", "slamgpu_optimize_sim3_device",
     "slamgpu_local_ba_linearize_device", "slamgpu_set_distortion", "slamgpu_undistort_points",
     "slamgpu_undistort_keypoints_device", "slamgpu_download_undistorted_keypoints",
     # include/slamgpu_bow.h
@@ -166,6 +170,10 @@ def lib():
                                                       ip, vp, vp, vp, vp, C.POINTER(ip)]
         L.slamgpu_global_bundle_adjustment.argtypes = [C.POINTER(Camera), vp, ip, vp, vp, ip, vp,
                                                        ip, vp, vp, ip, ip, vp, C.POINTER(ip)]
+        L.slamgpu_optimize_sim3.argtypes = [vp, vp, vp, vp, ip, vp, ip, fp, ip, vp, vp,
+                                            C.POINTER(ip)]
+        L.slamgpu_optimize_sim3_device.argtypes = [vp, vp, vp, vp, ip, vp, vp, ip, fp, ip, vp, vp,
+                                                   vp, vp, vp]
         L.slamgpu_local_ba_workspace_bytes.argtypes = [ip, ip, ip]
         L.slamgpu_local_ba_workspace_bytes.restype = sz
         L.slamgpu_local_bundle_adjustment_device.argtypes = [
@@ -570,6 +578,23 @@ class Optimizer:
         return kf, pts, erase[:len(ob)].astype(bool), its.value
 
     @staticmethod
+    def OptimizeSim3(matches, S12, K1, K2, inv_sigma2_1, inv_sigma2_2, th2=10.0, fix_scale=False):
+        """Optimizer::OptimizeSim3 (optimizer.cpp:962-1152) on the gathered correspondences
+        (SIM3_MATCH_DTYPE: both points in their cameras' frames, both undistorted keypoints and
+        octaves). S12: the g2o::Sim3 as (qx, qy, qz, qw, tx, ty, tz, s). Returns (n_inliers,
+        S12', inlier): the reference's return value, the optimised Sim3 (the input one on the
+        early return) and False where the reference nulls vpMatches1."""
+        K1, K2, i1, i2 = _sim3_args(K1, K2, inv_sigma2_1, inv_sigma2_2)
+        m = np.ascontiguousarray(matches, dtype=SIM3_MATCH_DTYPE)
+        S = np.ascontiguousarray(S12, np.float64).copy()
+        inl = np.zeros(max(len(m), 1), np.uint8)
+        n_in = C.c_int()
+        _opt_check(lib().slamgpu_optimize_sim3(_ptr(K1), _ptr(K2), _ptr(i1), _ptr(i2), len(i1),
+                                               _ptr(m), len(m), float(th2), int(bool(fix_scale)),
+                                               _ptr(S), _ptr(inl), C.byref(n_in)))
+        return n_in.value, S, inl[:len(m)].astype(bool)
+
+    @staticmethod
     def BundleAdjustment(kf_Tcw, kf_mode, points, point_obs_start, obs, cam, inv_sigma2,
                          n_iterations=10, robust=True, stop_flag=False):
         """Optimizer::BundleAdjustment / GlobalBundleAdjustemnt (optimizer.cpp:18-207) on the
@@ -588,6 +613,27 @@ class Optimizer:
             _ptr(pts), len(pts), _ptr(start), _ptr(ob), int(n_iterations), int(bool(robust)),
             C.byref(stop), C.byref(its)))
         return kf, pts, its.value
+
+
+def _sim3_args(K1, K2, inv_sigma2_1, inv_sigma2_2):
+    K1 = np.ascontiguousarray(np.asarray(K1, np.float32)[:4])
+    K2 = np.ascontiguousarray(np.asarray(K2, np.float32)[:4])
+    i1 = np.ascontiguousarray(inv_sigma2_1, np.float32)
+    i2 = np.ascontiguousarray(inv_sigma2_2, np.float32)
+    if len(i1) != len(i2):
+        raise ValueError("both keyframes need the same number of levels")
+    return K1, K2, i1, i2
+
+
+def optimize_sim3_device(K1, K2, inv_sigma2_1, inv_sigma2_2, d_matches, d_match_start,
+                         n_problems, d_S12, d_inlier, d_n_inliers, th2=10.0, fix_scale=False,
+                         d_lm_iterations=None, stream=None):
+    """slamgpu_optimize_sim3_device: OptimizeSim3 for a batch of loop candidates in HBM."""
+    K1, K2, i1, i2 = _sim3_args(K1, K2, inv_sigma2_1, inv_sigma2_2)
+    _opt_check(lib().slamgpu_optimize_sim3_device(
+        _ptr(K1), _ptr(K2), _ptr(i1), _ptr(i2), len(i1), _ptr(d_matches), _ptr(d_match_start),
+        n_problems, float(th2), int(bool(fix_scale)), _ptr(d_S12), _ptr(d_inlier),
+        _ptr(d_n_inliers), _ptr(d_lm_iterations), C.c_void_p(stream) if stream else None))
 
 
 def pose_optimization_device(cam, inv_sigma2, d_edges, d_edge_start, n_frames, d_Tcw, d_outlier,

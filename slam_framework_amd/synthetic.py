@@ -255,6 +255,71 @@ def pose_problem(seed: int, n: int = 2000, stereo_frac: float = 0.6, outlier_fra
     return edges, T0.astype(np.float32), T_true, level_inv_sigma2(scale_factor, nlevels), bad
 
 
+def sim3_problem(seed: int, n: int = 300, outlier_frac: float = 0.1, noise_px: float = 0.7,
+                 scale: float = 1.3, rot_err: float = 0.03, trans_err: float = 0.2,
+                 scale_err: float = 0.05, fix_scale: bool = False, cam1=KITTI_CAM, cam2=KITTI_CAM,
+                 cols: int = KITTI_COLS, rows: int = KITTI_ROWS, nlevels: int = 8,
+                 scale_factor: float = 1.2):
+    """One OptimizeSim3 input (optimizer.cpp:962-1152): n matched map points between a loop
+    keyframe pair. The true S12 maps camera-2 coordinates into camera 1: X1c = s R X2c + t
+    (scale 1 when fix_scale, as the stereo loop closer uses it). Points are drawn in camera 2's
+    view at depth U[3, 40] m; each is observed by keyframe 1 at project(K1, X1c) and keyframe 2
+    at project(K2, X2c) with N(0, noise_px * 1.2^octave) pixel noise; outlier_frac of the pairs
+    get a uniform keyframe-1 pixel. The initial S12 (the RANSAC Sim3Solver's) is the truth
+    perturbed by rot_err rad, trans_err m and exp(N(0, scale_err)). Returns (matches
+    [SIM3_MATCH_DTYPE], S12_init f64[8] (qx, qy, qz, qw, t, s), S12_true, inv_sigma2, bad)."""
+    rng = np.random.default_rng(seed)
+    s_true = 1.0 if fix_scale else float(scale)
+    R = _rodrigues(rng.normal(0, 0.15, 3))
+    t = rng.normal(0, 1.5, 3)
+    fx2, fy2, cx2, cy2 = cam2[:4]
+    fx1, fy1, cx1, cy1 = cam1[:4]
+    u2 = rng.uniform(0, cols, n)
+    v2 = rng.uniform(0, rows, n)
+    z2 = rng.uniform(3.0, 40.0, n)
+    X2 = np.stack([(u2 - cx2) / fx2 * z2, (v2 - cy2) / fy2 * z2, z2], 1)
+    X1 = s_true * X2 @ R.T + t
+    keep = X1[:, 2] > 0.5
+    X1, X2, u2, v2 = X1[keep], X2[keep], u2[keep], v2[keep]
+    n = len(X1)
+    o1 = np.minimum(rng.geometric(0.45, n) - 1, nlevels - 1).astype(np.int32)
+    o2 = np.minimum(rng.geometric(0.45, n) - 1, nlevels - 1).astype(np.int32)
+    u1 = X1[:, 0] / X1[:, 2] * fx1 + cx1 + rng.normal(0, 1, n) * noise_px * scale_factor ** o1
+    v1 = X1[:, 1] / X1[:, 2] * fy1 + cy1 + rng.normal(0, 1, n) * noise_px * scale_factor ** o1
+    u2o = u2 + rng.normal(0, 1, n) * noise_px * scale_factor ** o2
+    v2o = v2 + rng.normal(0, 1, n) * noise_px * scale_factor ** o2
+    bad = rng.uniform(0, 1, n) < outlier_frac
+    u1 = np.where(bad, rng.uniform(0, cols, n), u1)
+    v1 = np.where(bad, rng.uniform(0, rows, n), v1)
+    from .slamgpu import SIM3_MATCH_DTYPE
+    m = np.zeros(n, SIM3_MATCH_DTYPE)
+    m["x1c"] = X1.astype(np.float32)
+    m["x2c"] = X2.astype(np.float32)
+    m["u1"], m["v1"] = u1.astype(np.float32), v1.astype(np.float32)
+    m["u2"], m["v2"] = u2o.astype(np.float32), v2o.astype(np.float32)
+    m["octave1"], m["octave2"] = o1, o2
+
+    def pack(Rm, tv, sv):
+        q = _quat_from_R(Rm)
+        return np.array([q[0], q[1], q[2], q[3], tv[0], tv[1], tv[2], sv], np.float64)
+
+    S_true = pack(R, t, s_true)
+    R0 = _rodrigues(rng.normal(0, rot_err / np.sqrt(3), 3)) @ R
+    t0 = t + rng.normal(0, trans_err / np.sqrt(3), 3)
+    s0 = s_true if fix_scale else s_true * float(np.exp(rng.normal(0, scale_err)))
+    return m, pack(R0, t0, s0), S_true, level_inv_sigma2(scale_factor, nlevels), bad
+
+
+def _quat_from_R(R: np.ndarray) -> np.ndarray:
+    """(x, y, z, w) of a rotation matrix, w >= 0."""
+    w = np.sqrt(max(0.0, 1.0 + R[0, 0] + R[1, 1] + R[2, 2])) / 2
+    x = np.copysign(np.sqrt(max(0.0, 1.0 + R[0, 0] - R[1, 1] - R[2, 2])) / 2, R[2, 1] - R[1, 2])
+    y = np.copysign(np.sqrt(max(0.0, 1.0 - R[0, 0] + R[1, 1] - R[2, 2])) / 2, R[0, 2] - R[2, 0])
+    z = np.copysign(np.sqrt(max(0.0, 1.0 - R[0, 0] - R[1, 1] + R[2, 2])) / 2, R[1, 0] - R[0, 1])
+    q = np.array([x, y, z, w])
+    return q / np.linalg.norm(q)
+
+
 def c4_problem(seed: int = 7, n: int = 2000, cam=KITTI_CAM, nlevels: int = 8,
                scale_factor: float = 1.2):
     """SURVEY.md section 8(d) C4, the PoseOptimization bench workload: n world points uniform in
