@@ -11,6 +11,7 @@
  *   slamgpu_global_bundle_adjustment  Optimizer::BundleAdjustment          optimizer.cpp:18-207
  *   slamgpu_optimize_sim3             Optimizer::OptimizeSim3              optimizer.cpp:962-1152
  *   slamgpu_optimize_sim3_device      the same, batched over loop candidates
+ *   slamgpu_optimize_essential_graph  Optimizer::OptimizeEssentialGraph    optimizer.cpp:718-960
  * These calls hold no state, so they take no handle. Every function returns 0 or a negative
  * SLAMGPU_E* code (slamgpu.h) with a message in slamgpu_optimizer_last_error() (per thread).
  *
@@ -228,6 +229,32 @@ int slamgpu_optimize_sim3_device(const float K1[4], const float K2[4], const flo
                                  const int32_t* d_match_start, int n_problems, float th2,
                                  int fix_scale, double* d_S12, uint8_t* d_inlier,
                                  int32_t* d_n_inliers, int32_t* d_lm_iterations, void* stream);
+
+/* ---- OptimizeEssentialGraph --------------------------------------------------------------- */
+/* One EdgeSim3 of the essential graph (optimizer.cpp:784-909): _vertices[0] = keyframe i,
+ * _vertices[1] = keyframe j (indices into the call's keyframe arrays), measurement Sji (the
+ * reference's Sjw * Swi, computed from vScw or the non-corrected poses as :789-898 do; same layout
+ * as S12 above). Edges in the reference's insertion order. 80 bytes. */
+typedef struct {
+  int32_t i, j;
+  int32_t pad[2];
+  double Sji[8];
+} slamgpu_sim3_edge;
+
+/* Replaces: void Optimizer::OptimizeEssentialGraph(pMap, pLoopKF, pCurKF, NonCorrectedSim3,
+ * CorrectedSim3, LoopConnections, bFixScale)  optimizer.cpp:718-960, after its graph gathering.
+ * Scw[8 n_kf] (in/out): the vertices' vScw (the corrected Sim3 of the current keyframe's
+ * neighbourhood, Sim3(R, t, 1) of the others), in keyframe id order; on return the optimised
+ * CorrectedSiw. fixed[n_kf]: 1 for the loop keyframe. n_iterations: 20 in the reference.
+ * Tcw[16 n_kf] (may be NULL): the recovered SE3 poses [R t/s; 0 1] for KeyFrame::SetPose.
+ * points[3 n_points] (may be NULL), point_ref[n_points]: the map points (GetWorldPos) and the
+ * keyframe index whose vScw / optimised Sim3 correct them (:941-947: corrected_reference when
+ * the point was corrected by the current keyframe, else its reference keyframe); updated in place
+ * (the caller then runs UpdateNormalAndDepth). *lm_iterations (may be NULL). Synchronous. */
+int slamgpu_optimize_essential_graph(int n_kf, double* Scw, const uint8_t* fixed,
+                                     const slamgpu_sim3_edge* edges, int n_edges, int fix_scale,
+                                     int n_iterations, float* Tcw, float* points,
+                                     const int32_t* point_ref, int n_points, int* lm_iterations);
 
 const char* slamgpu_optimizer_last_error(void);
 

@@ -303,6 +303,22 @@ void oc_sim3_map(const double a[8], const double x[3], double o[3]);
 void oc_sim3_pair_eval(const float K1[4], const float K2[4], const oc_sim3_match* m,
                        const double S12[8], int fix_scale, double e[4], double J[28]);
 
+/* ---- OptimizeEssentialGraph (eg_oracle.c) ---------------------------------------------- */
+/* One EdgeSim3 of the essential graph (optimizer.cpp:784-909): _vertices[0] = i, [1] = j,
+ * measurement Sji (qx, qy, qz, qw, t, s). 80 B, == slamgpu_sim3_edge. */
+typedef struct {
+  int32_t i, j;
+  int32_t pad[2];
+  double Sji[8];
+} oc_sim3_edge;
+int oc_optimize_essential_graph(int n, double* Scw, const uint8_t* fixed, const oc_sim3_edge* edges,
+                                int n_edges, int fix_scale, int n_iterations, float* Tcw_out,
+                                int* lm_iterations);
+void oc_correct_points_sim3(const double* Scw_before, const double* Scw_after, const int32_t* ref,
+                            float* points, int n_points);
+double oc_sim3_edge_eval(const double Si[8], const double Sj[8], const double Sji[8], int fix_scale,
+                         double e[7], double Ji[49], double Jj[49]);
+
 #ifdef __cplusplus
 }
 #endif

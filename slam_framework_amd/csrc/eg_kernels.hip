@@ -1,0 +1,425 @@
+// eg_kernels.hip -- Optimizer::OptimizeEssentialGraph (optimizer.cpp:718-960) on the device.
+//
+// The graph: a g2o::VertexSim3Expmap per keyframe (the loop keyframe fixed) and an EdgeSim3 per
+// spanning-tree / loop / covisibility link, error log(Sji Si Sj^-1), identity information, no
+// robust kernel; Levenberg-Marquardt with user lambda 1e-16, 20 iterations; the linear system
+// (7 x 7 blocks, BlockSolver_7_3 + LinearSolverEigen) solved by sparse LDLT.
+//
+// Device split (the host drives the LM loop: one synchronisation per trial for the chi2 and the
+// solve status, optimizer_runtime.cpp):
+//   eg_linearize   a thread per edge: error, chi2, g2o's numeric Jacobians of both vertices
+//                  (central differences, delta 1e-9: 14 error evaluations per free vertex), and
+//                  the edge's contributions Ji'Ji, Jj'Jj, Ji'Jj, -Ji'e, -Jj'e
+//   eg_assemble    a wave per block of the system that an edge touches: the contributions summed
+//                  in edge order (g2o's buildSystem order), so the sums are deterministic
+//   eg_factor_solve one work-group: the LDLT of H + lambda I in the profile (skyline) storage of
+//                  the vertex order -- keyframe ids order the graph along the trajectory, so the
+//                  profile is a band plus the few long rows of loop edges -- right-looking by
+//                  block column (diagonal block LDLT, panel, trailing update of the column's
+//                  extent), then the forward / diagonal / backward solves and g2o's scale term
+//   eg_update      a thread per vertex: Sim3(dx) * S (dx[6] = 0 with a fixed scale)
+//   eg_errors, eg_chi2_sum  the trial's errors and their fixed-order sum
+//   eg_finish      SE3 pose recovery [R t/s] (:917-931) and the map point correction (:933-959)
+// The reference's Eigen sparse LDLT orders the unknowns by AMD; the profile LDLT in vertex order
+// computes the same factorisation up to rounding.
+#include <hip/hip_runtime.h>
+
+#include <cfloat>
+#include <cmath>
+
+#include "device_math.h"
+#include "eg_kernels.h"
+#include "sim3_device.h"
+
+namespace slamgpu {
+namespace {
+
+using sim3::Sim3;
+
+__device__ __forceinline__ double edge_error(const Sim3& M, const Sim3& Si, const Sim3& Sj,
+                                             double e[7]) {
+  const Sim3 a = sim3::sim3_mul(M, Si);
+  const Sim3 err = sim3::sim3_mul(a, sim3::sim3_inverse(Sj));
+  sim3::sim3_log(err, e);
+  double c = 0.0;
+#pragma unroll
+  for (int r = 0; r < 7; r++) c += e[r] * e[r];
+  return c;
+}
+
+__device__ __forceinline__ Sim3 oplus_axis(const Sim3& S, int d, double h, int fix_scale) {
+  double u[7];
+#pragma unroll
+  for (int i = 0; i < 7; i++) u[i] = i == d ? h : 0.0;
+  if (fix_scale) u[6] = 0;
+  return sim3::sim3_mul(sim3::sim3_exp(u), S);
+}
+
+__global__ __launch_bounds__(256) void eg_linearize_kernel(EgGraph G, EgState W) {
+  const int k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= G.n_edges) return;
+  const slamgpu_sim3_edge ed = G.edges[k];
+  const int fi = G.fidx[ed.i], fj = G.fidx[ed.j];
+  const Sim3 Si = sim3::sim3_load(W.S + 8 * ed.i), Sj = sim3::sim3_load(W.S + 8 * ed.j);
+  const Sim3 M = sim3::sim3_load(ed.Sji);
+  double e[7];
+  W.chi2[k] = edge_error(M, Si, Sj, e);
+#pragma unroll
+  for (int r = 0; r < 7; r++) W.err[7 * k + r] = e[r];
+  double* c = W.contrib + (int64_t)k * kEgContrib;
+  // Jacobian columns go through the contribution slots (Hii <- Ji, Hjj <- Jj; row-major 7x7),
+  // then the products overwrite them
+  const double delta = 1e-9, scalar = 1.0 / (2 * delta);
+  for (int which = 0; which < 2; which++) {
+    if ((which ? fj : fi) < 0) continue;
+    double* J = c + 49 * which;
+#pragma unroll 1
+    for (int d = 0; d < 7; d++) {
+      double ep[7], em[7];
+      if (which == 0) {
+        edge_error(M, oplus_axis(Si, d, delta, G.fix_scale), Sj, ep);
+        edge_error(M, oplus_axis(Si, d, -delta, G.fix_scale), Sj, em);
+      } else {
+        edge_error(M, Si, oplus_axis(Sj, d, delta, G.fix_scale), ep);
+        edge_error(M, Si, oplus_axis(Sj, d, -delta, G.fix_scale), em);
+      }
+#pragma unroll
+      for (int r = 0; r < 7; r++) J[7 * r + d] = scalar * (ep[r] - em[r]);
+    }
+  }
+  // b += J' omega_r (omega_r = -e), H += J' J (base_binary_edge.hpp:55-121, Omega = I)
+  double Ja[49], Jb[49];
+  if (fi >= 0)
+    for (int q = 0; q < 49; q++) Ja[q] = c[q];
+  if (fj >= 0)
+    for (int q = 0; q < 49; q++) Jb[q] = c[49 + q];
+  if (fi >= 0) {
+#pragma unroll 1
+    for (int a = 0; a < 7; a++) {
+      double s = 0.0;
+      for (int q = 0; q < 7; q++) s += Ja[7 * q + a] * -e[q];
+      c[147 + a] = s;
+      for (int cc = 0; cc < 7; cc++) {
+        double h = 0.0;
+        for (int q = 0; q < 7; q++) h += Ja[7 * q + a] * Ja[7 * q + cc];
+        c[7 * a + cc] = h;
+      }
+    }
+    if (fj >= 0) {
+#pragma unroll 1
+      for (int a = 0; a < 7; a++)
+        for (int cc = 0; cc < 7; cc++) {
+          double h = 0.0;
+          for (int q = 0; q < 7; q++) h += Ja[7 * q + a] * Jb[7 * q + cc];
+          c[98 + 7 * a + cc] = h;
+        }
+    }
+  }
+  if (fj >= 0) {
+#pragma unroll 1
+    for (int a = 0; a < 7; a++) {
+      double s = 0.0;
+      for (int q = 0; q < 7; q++) s += Jb[7 * q + a] * -e[q];
+      c[154 + a] = s;
+      for (int cc = 0; cc < 7; cc++) {
+        double h = 0.0;
+        for (int q = 0; q < 7; q++) h += Jb[7 * q + a] * Jb[7 * q + cc];
+        c[49 + 7 * a + cc] = h;
+      }
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void eg_errors_kernel(EgGraph G, const double* S, EgState W) {
+  const int k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= G.n_edges) return;
+  const slamgpu_sim3_edge ed = G.edges[k];
+  double e[7];
+  W.chi2[k] = edge_error(sim3::sim3_load(ed.Sji), sim3::sim3_load(S + 8 * ed.i),
+                         sim3::sim3_load(S + 8 * ed.j), e);
+}
+
+// Deterministic sum of v[0..n): thread t sums v[t], v[t + 256], ... then a fixed tree.
+__device__ double block_sum256(const double* v, int n, double* red) {
+  double s = 0.0;
+  for (int i = threadIdx.x; i < n; i += 256) s += v[i];
+  red[threadIdx.x] = s;
+  __syncthreads();
+  for (int h = 128; h >= 1; h >>= 1) {
+    if ((int)threadIdx.x < h) red[threadIdx.x] += red[threadIdx.x + h];
+    __syncthreads();
+  }
+  const double t = red[0];
+  __syncthreads();
+  return t;
+}
+
+__global__ __launch_bounds__(256) void eg_chi2_sum_kernel(EgGraph G, EgState W) {
+  __shared__ double red[256];
+  const double t = block_sum256(W.chi2, G.n_edges, red);
+  if (threadIdx.x == 0) W.out[0] = t;
+}
+
+__global__ __launch_bounds__(64) void eg_assemble_kernel(EgGraph G, EgState W) {
+  const int t = blockIdx.x, lane = threadIdx.x;
+  const int blk = G.tgt_block[t], f = G.tgt_vertex[t];
+  const int i0 = G.tgt_ptr[t], i1 = G.tgt_ptr[t + 1];
+  const bool is_b = lane >= 49 && lane < 56 && f >= 0;
+  if (lane >= 49 && !is_b) return;
+  const int r = lane / 7, cc = lane % 7, rb = lane - 49;
+  double s = 0.0;
+  for (int q = i0; q < i1; q++) {
+    const int item = G.tgt_items[q];
+    const double* c = W.contrib + (int64_t)(item >> 2) * kEgContrib;
+    const int kind = item & 3;
+    if (is_b) s += c[(kind == 0 ? 147 : 154) + rb];
+    else if (kind == 0) s += c[lane];
+    else if (kind == 1) s += c[49 + lane];
+    else if (kind == 2) s += c[98 + lane];
+    else s += c[98 + 7 * cc + r];
+  }
+  if (is_b) W.b[7 * f + rb] = s;
+  else W.H[(int64_t)blk * 49 + lane] = s;
+}
+
+constexpr int kFacThreads = 1024;
+
+__global__ __launch_bounds__(kFacThreads) void eg_factor_solve_kernel(EgGraph G, EgState W,
+                                                                      int64_t n_blocks,
+                                                                      double lambda) {
+  __shared__ int s_ok;
+  __shared__ double red[256];
+  const int tid = threadIdx.x, F = G.F;
+  double* L = W.L;
+  for (int64_t q = tid; q < n_blocks * 49; q += kFacThreads) L[q] = W.H[q];
+  if (tid == 0) s_ok = 1;
+  __syncthreads();
+  for (int f = tid; f < 7 * F; f += kFacThreads) {
+    const int v = f / 7, r = f % 7;
+    L[(G.off[v] + (v - G.start[v])) * 49 + 8 * r] += lambda;  // setLambda: H + lambda I
+  }
+  __syncthreads();
+  auto blkp = [&](int i, int j) { return L + (G.off[i] + (j - G.start[i])) * 49; };
+  // ---- factorisation, right-looking by block column ----
+  for (int k = 0; k < F; k++) {
+    double* Akk = blkp(k, k);
+    if (tid == 0) {  // the diagonal block: scalar LDLT (lower L, D on the diagonal)
+      for (int j = 0; j < 7; j++) {
+        double d = Akk[8 * j];
+        for (int m = 0; m < j; m++) d -= Akk[7 * j + m] * Akk[7 * j + m] * Akk[8 * m];
+        Akk[8 * j] = d;
+        if (d == 0.0) s_ok = 0;
+        for (int i = j + 1; i < 7; i++) {
+          double s = Akk[7 * i + j];
+          for (int m = 0; m < j; m++) s -= Akk[7 * i + m] * Akk[7 * j + m] * Akk[8 * m];
+          Akk[7 * i + j] = s / d;
+        }
+      }
+    }
+    __syncthreads();
+    const int e0 = G.ext_ptr[k], ne = G.ext_ptr[k + 1] - e0;
+    for (int q = tid; q < 7 * ne; q += kFacThreads) {  // panel: L_ik = A_ik L_kk^-T D_k^-1
+      const int i = G.ext_rows[e0 + q / 7], r = q % 7;
+      double* Aik = blkp(i, k) + 7 * r;
+      for (int c = 0; c < 7; c++) {
+        double s = Aik[c];
+        for (int m = 0; m < c; m++) s -= Aik[m] * Akk[8 * m] * Akk[7 * c + m];
+        Aik[c] = s / Akk[8 * c];
+      }
+    }
+    __syncthreads();
+    const int npairs = ne * (ne + 1) / 2;
+    for (int q = tid; q < npairs * 49; q += kFacThreads) {  // trailing: A_ij -= L_ik D_k L_jk'
+      const int pair = q / 49, ent = q % 49;
+      int ti = (int)((sqrtf(8.0f * (float)pair + 1.0f) - 1.0f) * 0.5f);
+      while ((ti + 1) * (ti + 2) / 2 <= pair) ti++;
+      while (ti * (ti + 1) / 2 > pair) ti--;
+      const int tj = pair - ti * (ti + 1) / 2;
+      const int i = G.ext_rows[e0 + ti], j = G.ext_rows[e0 + tj];
+      const int r = ent / 7, c = ent % 7;
+      const double* Lik = blkp(i, k) + 7 * r;
+      const double* Ljk = blkp(j, k) + 7 * c;
+      double s = 0.0;
+#pragma unroll
+      for (int m = 0; m < 7; m++) s += Lik[m] * Akk[8 * m] * Ljk[m];
+      blkp(i, j)[ent] -= s;
+    }
+    __syncthreads();
+  }
+  // ---- solve L D L' y = b ----
+  double* y = W.y;
+  for (int q = tid; q < 7 * F; q += kFacThreads) y[q] = W.b[q];
+  __syncthreads();
+  for (int k = 0; k < F; k++) {
+    const double* Lkk = blkp(k, k);
+    if (tid == 0)
+      for (int r = 1; r < 7; r++) {
+        double s = y[7 * k + r];
+        for (int m = 0; m < r; m++) s -= Lkk[7 * r + m] * y[7 * k + m];
+        y[7 * k + r] = s;
+      }
+    __syncthreads();
+    const int e0 = G.ext_ptr[k], ne = G.ext_ptr[k + 1] - e0;
+    for (int q = tid; q < 7 * ne; q += kFacThreads) {
+      const int i = G.ext_rows[e0 + q / 7], r = q % 7;
+      const double* Lik = blkp(i, k) + 7 * r;
+      double s = 0.0;
+      for (int m = 0; m < 7; m++) s += Lik[m] * y[7 * k + m];
+      y[7 * i + r] -= s;
+    }
+    __syncthreads();
+  }
+  for (int q = tid; q < 7 * F; q += kFacThreads) y[q] /= blkp(q / 7, q / 7)[8 * (q % 7)];
+  __syncthreads();
+  for (int k = F - 1; k >= 0; k--) {
+    const int e0 = G.ext_ptr[k], ne = G.ext_ptr[k + 1] - e0;
+    if (tid < 7) {  // y_k -= sum over the later rows i of L_ik' x_i
+      double s = 0.0;
+      for (int t = 0; t < ne; t++) {
+        const int i = G.ext_rows[e0 + t];
+        const double* Lik = blkp(i, k);
+        for (int r = 0; r < 7; r++) s += Lik[7 * r + tid] * y[7 * i + r];
+      }
+      y[7 * k + tid] -= s;
+    }
+    __syncthreads();
+    if (tid == 0) {
+      const double* Lkk = blkp(k, k);
+      for (int r = 5; r >= 0; r--) {
+        double s = y[7 * k + r];
+        for (int m = r + 1; m < 7; m++) s -= Lkk[7 * m + r] * y[7 * k + m];
+        y[7 * k + r] = s;
+      }
+    }
+    __syncthreads();
+  }
+  // LinearSolverEigen: a failed factorisation leaves x as it was; the vertex oplus zeroes the
+  // scale coordinate of the solver's x when the scale is fixed
+  const bool ok = s_ok != 0;
+  if (ok)
+    for (int q = tid; q < 7 * F; q += kFacThreads) W.x[q] = (G.fix_scale && q % 7 == 6) ? 0.0 : y[q];
+  __syncthreads();
+  // computeScale: sum x (lambda x + b)
+  double s = 0.0;
+  if (tid < 256)
+    for (int q = tid; q < 7 * F; q += 256) s += W.x[q] * (lambda * W.x[q] + W.b[q]);
+  if (tid < 256) red[tid] = s;
+  __syncthreads();
+  for (int h = 128; h >= 1; h >>= 1) {
+    if (tid < h) red[tid] += red[tid + h];
+    __syncthreads();
+  }
+  if (tid == 0) {
+    W.out[1] = red[0];
+    W.out[2] = ok ? 1.0 : 0.0;
+  }
+}
+
+__global__ __launch_bounds__(256) void eg_update_kernel(EgGraph G, EgState W) {
+  const int v = blockIdx.x * blockDim.x + threadIdx.x;
+  if (v >= G.n) return;
+  const int f = G.fidx[v];
+  double* o = W.S_trial + 8 * v;
+  const double* s = W.S + 8 * v;
+  if (f < 0) {
+    for (int q = 0; q < 8; q++) o[q] = s[q];
+    return;
+  }
+  double u[7];
+  for (int q = 0; q < 7; q++) u[q] = W.x[7 * f + q];
+  if (G.fix_scale) u[6] = 0;
+  const Sim3 N = sim3::sim3_mul(sim3::sim3_exp(u), sim3::sim3_load(s));
+  sim3::sim3_store(N, o);
+}
+
+__global__ __launch_bounds__(256) void eg_finish_kernel(EgGraph G, const double* S_final,
+                                                        const double* S_init, float* Tcw,
+                                                        float* points, const int32_t* ref,
+                                                        int n_points) {
+  const int q = blockIdx.x * blockDim.x + threadIdx.x;
+  if (q < G.n) {
+    if (!Tcw) return;
+    const Sim3 S = sim3::sim3_load(S_final + 8 * q);
+    double R[9];
+    se3::quat_to_R(S.r, R);
+    const double is = 1. / S.s;
+    float* T = Tcw + 16 * q;
+    for (int i = 0; i < 3; i++) {
+      for (int j = 0; j < 3; j++) T[4 * i + j] = (float)R[3 * i + j];
+      T[4 * i + 3] = (float)(S.t[i] * is);
+    }
+    T[12] = T[13] = T[14] = 0.f;
+    T[15] = 1.f;
+    return;
+  }
+  const int p = q - G.n;
+  if (p >= n_points) return;
+  const int v = ref[p];
+  const Sim3 Srw = sim3::sim3_load(S_init + 8 * v);
+  const Sim3 Swr = sim3::sim3_inverse(sim3::sim3_load(S_final + 8 * v));
+  const double X[3] = {points[3 * p], points[3 * p + 1], points[3 * p + 2]};
+  double Y[3], Z[3], r1[3], r2[3];
+  se3::quat_rotate(Srw.r, X, r1);
+  for (int i = 0; i < 3; i++) Y[i] = Srw.s * r1[i] + Srw.t[i];
+  se3::quat_rotate(Swr.r, Y, r2);
+  for (int i = 0; i < 3; i++) Z[i] = Swr.s * r2[i] + Swr.t[i];
+  for (int i = 0; i < 3; i++) points[3 * p + i] = (float)Z[i];
+}
+
+int blocks_of(int n, int t) { return (n + t - 1) / t; }
+
+}  // namespace
+
+hipError_t launch_eg_linearize(const EgGraph& G, const EgState& W, hipStream_t st) {
+  if (G.n_edges <= 0) return hipSuccess;
+  SLAMGPU_LAUNCH("eg_linearize", st, eg_linearize_kernel, dim3(blocks_of(G.n_edges, 256)),
+                 dim3(256), 0, st, G, W);
+  return hipGetLastError();
+}
+
+hipError_t launch_eg_errors(const EgGraph& G, const double* S, const EgState& W, hipStream_t st) {
+  if (G.n_edges <= 0) return hipSuccess;
+  SLAMGPU_LAUNCH("eg_errors", st, eg_errors_kernel, dim3(blocks_of(G.n_edges, 256)), dim3(256), 0,
+                 st, G, S, W);
+  return hipGetLastError();
+}
+
+hipError_t launch_eg_chi2_sum(const EgGraph& G, const EgState& W, hipStream_t st) {
+  SLAMGPU_LAUNCH("eg_chi2_sum", st, eg_chi2_sum_kernel, dim3(1), dim3(256), 0, st, G, W);
+  return hipGetLastError();
+}
+
+hipError_t launch_eg_assemble(const EgGraph& G, const EgState& W, int64_t n_blocks,
+                              hipStream_t st) {
+  hipError_t e = hipMemsetAsync(W.H, 0, (size_t)n_blocks * 49 * sizeof(double), st);
+  if (e != hipSuccess) return e;
+  if (G.n_targets <= 0) return hipSuccess;
+  SLAMGPU_LAUNCH("eg_assemble", st, eg_assemble_kernel, dim3(G.n_targets), dim3(64), 0, st, G, W);
+  return hipGetLastError();
+}
+
+hipError_t launch_eg_factor_solve(const EgGraph& G, const EgState& W, int64_t n_blocks,
+                                  double lambda, hipStream_t st) {
+  SLAMGPU_LAUNCH("eg_factor_solve", st, eg_factor_solve_kernel, dim3(1), dim3(kFacThreads), 0, st,
+                 G, W, n_blocks, lambda);
+  return hipGetLastError();
+}
+
+hipError_t launch_eg_update(const EgGraph& G, const EgState& W, hipStream_t st) {
+  if (G.n <= 0) return hipSuccess;
+  SLAMGPU_LAUNCH("eg_update", st, eg_update_kernel, dim3(blocks_of(G.n, 256)), dim3(256), 0, st,
+                 G, W);
+  return hipGetLastError();
+}
+
+hipError_t launch_eg_finish(const EgGraph& G, const double* S_final, const double* S_init,
+                            float* Tcw, float* points, const int32_t* point_ref, int n_points,
+                            hipStream_t st) {
+  const int total = G.n + (points ? n_points : 0);
+  if (total <= 0) return hipSuccess;
+  SLAMGPU_LAUNCH("eg_finish", st, eg_finish_kernel, dim3(blocks_of(total, 256)), dim3(256), 0, st,
+                 G, S_final, S_init, Tcw, points, point_ref, points ? n_points : 0);
+  return hipGetLastError();
+}
+
+}  // namespace slamgpu

@@ -9,6 +9,7 @@
 #include <chrono>
 #include <thread>
 
+#include <cfloat>
 #include <cstdarg>
 #include <cstdio>
 #include <algorithm>
@@ -21,6 +22,7 @@
 #include "../../include/slamgpu_optimizer.h"
 #include "ba_coop.h"
 #include "ba_kernels.h"
+#include "eg_kernels.h"
 #include "pose_kernels.h"
 #include "sim3_kernels.h"
 
@@ -516,6 +518,223 @@ int slamgpu_optimize_sim3(const float K1[4], const float K2[4], const float* inv
   if (n > 0) OPT_HIPCHECK(hipMemcpyAsync(inlier, b + off_i, n, hipMemcpyDeviceToHost, S.stream));
   OPT_HIPCHECK(hipStreamSynchronize(S.stream));
   *n_inliers = res;
+  return 0;
+}
+
+int slamgpu_optimize_essential_graph(int n_kf, double* Scw, const uint8_t* fixed,
+                                     const slamgpu_sim3_edge* edges, int n_edges, int fix_scale,
+                                     int n_iterations, float* Tcw, float* points,
+                                     const int32_t* point_ref, int n_points, int* lm_iterations) {
+  if (lm_iterations) *lm_iterations = 0;
+  if (n_kf < 0 || n_edges < 0 || n_points < 0 || n_iterations < 0)
+    return fail(SLAMGPU_EINVAL, "negative sizes");
+  if ((n_kf > 0 && (!Scw || !fixed)) || (n_edges > 0 && !edges) ||
+      (n_points > 0 && points && !point_ref))
+    return fail(SLAMGPU_EINVAL, "null buffer");
+  for (int k = 0; k < n_edges; k++)
+    if (edges[k].i < 0 || edges[k].i >= n_kf || edges[k].j < 0 || edges[k].j >= n_kf ||
+        edges[k].i == edges[k].j)
+      return fail(SLAMGPU_EINVAL, "edge %d: keyframes (%d, %d) invalid for %d keyframes", k,
+                  edges[k].i, edges[k].j, n_kf);
+  if (points)
+    for (int q = 0; q < n_points; q++)
+      if (point_ref[q] < 0 || point_ref[q] >= n_kf)
+        return fail(SLAMGPU_EINVAL, "point %d: reference keyframe %d outside [0, %d)", q,
+                    point_ref[q], n_kf);
+  if (n_kf == 0) return 0;
+  // ---- the graph's structure (host): free vertices, profile, assembly targets, extents ----
+  std::vector<int32_t> fidx(n_kf);
+  int F = 0;
+  for (int v = 0; v < n_kf; v++) fidx[v] = fixed[v] ? -1 : F++;
+  std::vector<int32_t> start(F);
+  for (int f = 0; f < F; f++) start[f] = f;
+  for (int k = 0; k < n_edges; k++) {
+    const int a = fidx[edges[k].i], b = fidx[edges[k].j];
+    if (a < 0 || b < 0) continue;
+    const int hi = std::max(a, b), lo = std::min(a, b);
+    start[hi] = std::min(start[hi], lo);
+  }
+  std::vector<int64_t> off(F + 1, 0);
+  for (int f = 0; f < F; f++) off[f + 1] = off[f] + (f - start[f] + 1);
+  const int64_t n_blocks = off[F];
+  std::vector<std::vector<int32_t>> items(F);
+  std::vector<int32_t> tgt_block, tgt_vertex;
+  std::vector<std::vector<int32_t>> off_items;
+  std::vector<std::pair<int64_t, int32_t>> off_key;  // (block, target) of off-diagonal targets
+  std::vector<int32_t> block_target;
+  {
+    std::vector<int32_t> blk2t((size_t)n_blocks, -1);
+    for (int k = 0; k < n_edges; k++) {
+      const int a = fidx[edges[k].i], b = fidx[edges[k].j];
+      if (a >= 0) items[a].push_back(4 * k + 0);
+      if (b >= 0) items[b].push_back(4 * k + 1);
+      if (a >= 0 && b >= 0) {
+        const int hi = std::max(a, b), lo = std::min(a, b);
+        const int64_t blk = off[hi] + (lo - start[hi]);
+        if (blk2t[blk] < 0) {
+          blk2t[blk] = (int32_t)off_items.size();
+          off_items.emplace_back();
+          off_key.emplace_back(blk, 0);
+        }
+        off_items[blk2t[blk]].push_back(4 * k + (a > b ? 2 : 3));
+      }
+    }
+  }
+  std::vector<int32_t> tgt_ptr(1, 0), tgt_items;
+  for (int f = 0; f < F; f++) {
+    tgt_block.push_back((int32_t)(off[f] + (f - start[f])));
+    tgt_vertex.push_back(f);
+    tgt_items.insert(tgt_items.end(), items[f].begin(), items[f].end());
+    tgt_ptr.push_back((int32_t)tgt_items.size());
+  }
+  for (size_t t = 0; t < off_items.size(); t++) {
+    tgt_block.push_back((int32_t)off_key[t].first);
+    tgt_vertex.push_back(-1);
+    tgt_items.insert(tgt_items.end(), off_items[t].begin(), off_items[t].end());
+    tgt_ptr.push_back((int32_t)tgt_items.size());
+  }
+  const int n_targets = (int)tgt_block.size();
+  std::vector<std::vector<int32_t>> ext(F);
+  for (int i = 0; i < F; i++)
+    for (int k = start[i]; k < i; k++) ext[k].push_back(i);
+  std::vector<int32_t> ext_ptr(1, 0), ext_rows;
+  for (int k = 0; k < F; k++) {
+    ext_rows.insert(ext_rows.end(), ext[k].begin(), ext[k].end());
+    ext_ptr.push_back((int32_t)ext_rows.size());
+  }
+  // ---- one device region: inputs, structure, state ----
+  const size_t E = (size_t)n_edges, N = (size_t)n_kf, P7 = 7 * (size_t)F;
+  size_t o = 0;
+  auto take = [&](size_t bytes) {
+    const size_t at = o;
+    o += al256(bytes + 1);
+    return at;
+  };
+  const size_t o_edges = take(E * sizeof(slamgpu_sim3_edge)), o_fidx = take(4 * N);
+  const size_t o_start = take(4 * (size_t)F), o_off = take(8 * ((size_t)F + 1));
+  const size_t o_tb = take(4 * (size_t)n_targets), o_tv = take(4 * (size_t)n_targets);
+  const size_t o_tp = take(4 * ((size_t)n_targets + 1)), o_ti = take(4 * tgt_items.size());
+  const size_t o_ep = take(4 * ((size_t)F + 1)), o_er = take(4 * ext_rows.size());
+  const size_t o_S = take(8 * 8 * N), o_S2 = take(8 * 8 * N), o_S0 = take(8 * 8 * N);
+  const size_t o_err = take(8 * 7 * E), o_chi = take(8 * E), o_con = take(8 * kEgContrib * E);
+  const size_t o_H = take(8 * 49 * (size_t)n_blocks), o_b = take(8 * P7);
+  const size_t o_L = take(8 * 49 * (size_t)n_blocks), o_x = take(8 * P7), o_y = take(8 * P7);
+  const size_t o_out = take(64), o_T = take(Tcw ? 64 * N : 0);
+  const size_t o_pts = take(points ? 12 * (size_t)n_points : 0);
+  const size_t o_ref = take(points ? 4 * (size_t)n_points : 0);
+  HostStage& HS = thread_stage();
+  if (int r = stage_reserve(HS, o)) return r;
+  char* d = static_cast<char*>(HS.buf);
+  hipStream_t st = HS.stream;
+  auto up = [&](size_t at, const void* src, size_t bytes) -> hipError_t {
+    return bytes ? hipMemcpyAsync(d + at, src, bytes, hipMemcpyHostToDevice, st) : hipSuccess;
+  };
+  OPT_HIPCHECK(up(o_edges, edges, E * sizeof(slamgpu_sim3_edge)));
+  OPT_HIPCHECK(up(o_fidx, fidx.data(), 4 * N));
+  OPT_HIPCHECK(up(o_start, start.data(), 4 * (size_t)F));
+  OPT_HIPCHECK(up(o_off, off.data(), 8 * ((size_t)F + 1)));
+  OPT_HIPCHECK(up(o_tb, tgt_block.data(), 4 * (size_t)n_targets));
+  OPT_HIPCHECK(up(o_tv, tgt_vertex.data(), 4 * (size_t)n_targets));
+  OPT_HIPCHECK(up(o_tp, tgt_ptr.data(), 4 * ((size_t)n_targets + 1)));
+  OPT_HIPCHECK(up(o_ti, tgt_items.data(), 4 * tgt_items.size()));
+  OPT_HIPCHECK(up(o_ep, ext_ptr.data(), 4 * ((size_t)F + 1)));
+  OPT_HIPCHECK(up(o_er, ext_rows.data(), 4 * ext_rows.size()));
+  OPT_HIPCHECK(up(o_S, Scw, 64 * N));
+  OPT_HIPCHECK(up(o_S0, Scw, 64 * N));
+  OPT_HIPCHECK(hipMemsetAsync(d + o_x, 0, 8 * P7 + 1, st));
+  if (points) {
+    OPT_HIPCHECK(up(o_pts, points, 12 * (size_t)n_points));
+    OPT_HIPCHECK(up(o_ref, point_ref, 4 * (size_t)n_points));
+  }
+  EgGraph G;
+  G.n = n_kf;
+  G.n_edges = n_edges;
+  G.F = F;
+  G.fix_scale = fix_scale ? 1 : 0;
+  G.edges = reinterpret_cast<const slamgpu_sim3_edge*>(d + o_edges);
+  G.fidx = reinterpret_cast<const int32_t*>(d + o_fidx);
+  G.start = reinterpret_cast<const int32_t*>(d + o_start);
+  G.off = reinterpret_cast<const int64_t*>(d + o_off);
+  G.n_targets = n_targets;
+  G.tgt_block = reinterpret_cast<const int32_t*>(d + o_tb);
+  G.tgt_vertex = reinterpret_cast<const int32_t*>(d + o_tv);
+  G.tgt_ptr = reinterpret_cast<const int32_t*>(d + o_tp);
+  G.tgt_items = reinterpret_cast<const int32_t*>(d + o_ti);
+  G.ext_ptr = reinterpret_cast<const int32_t*>(d + o_ep);
+  G.ext_rows = reinterpret_cast<const int32_t*>(d + o_er);
+  EgState W;
+  W.S = reinterpret_cast<double*>(d + o_S);
+  W.S_trial = reinterpret_cast<double*>(d + o_S2);
+  W.err = reinterpret_cast<double*>(d + o_err);
+  W.chi2 = reinterpret_cast<double*>(d + o_chi);
+  W.contrib = reinterpret_cast<double*>(d + o_con);
+  W.H = reinterpret_cast<double*>(d + o_H);
+  W.b = reinterpret_cast<double*>(d + o_b);
+  W.L = reinterpret_cast<double*>(d + o_L);
+  W.x = reinterpret_cast<double*>(d + o_x);
+  W.y = reinterpret_cast<double*>(d + o_y);
+  W.out = reinterpret_cast<double*>(d + o_out);
+  auto read_out = [&](double* h) -> hipError_t {
+    hipError_t e = hipMemcpyAsync(h, W.out, 3 * sizeof(double), hipMemcpyDeviceToHost, st);
+    if (e != hipSuccess) return e;
+    return hipStreamSynchronize(st);
+  };
+  // ---- SparseOptimizer::optimize(n_iterations), OptimizationAlgorithmLevenberg ----
+  double lambda = 1e-16;  // setUserLambdaInit(1e-16) (:732)
+  int ni = 2, nbad = 0, its = 0;
+  for (int it = 0; it < n_iterations && F > 0; it++) {
+    OPT_HIPCHECK(launch_eg_linearize(G, W, st));
+    OPT_HIPCHECK(launch_eg_chi2_sum(G, W, st));
+    OPT_HIPCHECK(launch_eg_assemble(G, W, n_blocks, st));
+    double h[3];
+    OPT_HIPCHECK(read_out(h));
+    double currentChi = h[0];
+    const double iniChi = currentChi;
+    if (it == 0) {
+      lambda = 1e-16;
+      ni = 2;
+      nbad = 0;
+    }
+    double rho = 0;
+    int qmax = 0;
+    do {
+      OPT_HIPCHECK(launch_eg_factor_solve(G, W, n_blocks, lambda, st));
+      OPT_HIPCHECK(launch_eg_update(G, W, st));
+      OPT_HIPCHECK(launch_eg_errors(G, W.S_trial, W, st));
+      OPT_HIPCHECK(launch_eg_chi2_sum(G, W, st));
+      OPT_HIPCHECK(read_out(h));
+      double tempChi = h[0];
+      if (h[2] == 0.0) tempChi = DBL_MAX;
+      rho = (currentChi - tempChi) / (h[1] + 1e-3);
+      if (rho > 0 && std::isfinite(tempChi)) {
+        double alpha = 1. - std::pow(2 * rho - 1, 3.0);
+        alpha = std::min(alpha, 2. / 3.);
+        lambda *= std::max(1. / 3., alpha);
+        ni = 2;
+        currentChi = tempChi;
+        std::swap(W.S, W.S_trial);  // accept
+      } else {
+        lambda *= ni;
+        ni *= 2;
+      }
+      qmax++;
+    } while (rho < 0 && qmax < 10);
+    its++;
+    if (qmax == 10 || rho == 0) break;
+    if ((iniChi - currentChi) * 1e3 < iniChi) nbad++;
+    else nbad = 0;
+    if (nbad >= 3) break;
+  }
+  OPT_HIPCHECK(launch_eg_finish(G, W.S, reinterpret_cast<double*>(d + o_S0),
+                                Tcw ? reinterpret_cast<float*>(d + o_T) : nullptr,
+                                points ? reinterpret_cast<float*>(d + o_pts) : nullptr,
+                                reinterpret_cast<const int32_t*>(d + o_ref), n_points, st));
+  OPT_HIPCHECK(hipMemcpyAsync(Scw, W.S, 64 * N, hipMemcpyDeviceToHost, st));
+  if (Tcw) OPT_HIPCHECK(hipMemcpyAsync(Tcw, d + o_T, 64 * N, hipMemcpyDeviceToHost, st));
+  if (points && n_points)
+    OPT_HIPCHECK(hipMemcpyAsync(points, d + o_pts, 12 * (size_t)n_points, hipMemcpyDeviceToHost, st));
+  OPT_HIPCHECK(hipStreamSynchronize(st));
+  if (lm_iterations) *lm_iterations = its;
   return 0;
 }
 

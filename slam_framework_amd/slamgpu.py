@@ -36,6 +36,8 @@ MPS_QUERY_DTYPE = np.dtype([("proj_x", "<f4"), ("proj_y", "<f4"), ("proj_xr", "<
 SIM3_MATCH_DTYPE = np.dtype([("x1c", "<f4", (3,)), ("x2c", "<f4", (3,)), ("u1", "<f4"),
                              ("v1", "<f4"), ("u2", "<f4"), ("v2", "<f4"), ("octave1", "<i4"),
                              ("octave2", "<i4")])
+# slamgpu_sim3_edge (include/slamgpu_optimizer.h): one EdgeSim3 of the essential graph.
+SIM3_EDGE_DTYPE = np.dtype([("i", "<i4"), ("j", "<i4"), ("pad", "<i4", (2,)), ("Sji", "<f8", (8,))])
 # slamgpu_pose_edge (include/slamgpu_optimizer.h): one PoseOptimization correspondence.
 POSE_EDGE_DTYPE = np.dtype([("xw", "<f4", (3,)), ("u", "<f4"), ("v", "<f4"), ("ur", "<f4"),
                             ("octave", "<i4")])
@@ -60,6 +62,7 @@ EXPORTS = [
     "slamgpu_optimizer_last_error", "slamgpu_local_bundle_adjustment",
     "slamgpu_local_bundle_adjustment_device", "slamgpu_local_ba_workspace_bytes",
     "slamgpu_global_bundle_adjustment", "slamgpu_optimize_sim3", "slamgpu_optimize_sim3_device",
+    "slamgpu_optimize_essential_graph",
     "slamgpu_local_ba_linearize_device", "slamgpu_set_distortion", "slamgpu_undistort_points",
     "slamgpu_undistort_keypoints_device", "slamgpu_download_undistorted_keypoints",
     # include/slamgpu_bow.h
@@ -174,6 +177,8 @@ def lib():
                                             C.POINTER(ip)]
         L.slamgpu_optimize_sim3_device.argtypes = [vp, vp, vp, vp, ip, vp, vp, ip, fp, ip, vp, vp,
                                                    vp, vp, vp]
+        L.slamgpu_optimize_essential_graph.argtypes = [ip, vp, vp, vp, ip, ip, ip, vp, vp, vp, ip,
+                                                       C.POINTER(ip)]
         L.slamgpu_local_ba_workspace_bytes.argtypes = [ip, ip, ip]
         L.slamgpu_local_ba_workspace_bytes.restype = sz
         L.slamgpu_local_bundle_adjustment_device.argtypes = [
@@ -593,6 +598,28 @@ class Optimizer:
                                                _ptr(m), len(m), float(th2), int(bool(fix_scale)),
                                                _ptr(S), _ptr(inl), C.byref(n_in)))
         return n_in.value, S, inl[:len(m)].astype(bool)
+
+    @staticmethod
+    def OptimizeEssentialGraph(Scw, fixed, edges, fix_scale=True, n_iterations=20, points=None,
+                               point_ref=None):
+        """Optimizer::OptimizeEssentialGraph (optimizer.cpp:718-960) on the gathered graph:
+        Scw [n][8] the vertices' vScw (keyframe id order), fixed [n] (1 for the loop keyframe),
+        edges SIM3_EDGE_DTYPE in the reference's insertion order. points [m][3] / point_ref [m]
+        (optional): map points and the keyframe index that corrects each. Returns (Scw' [n][8]
+        the optimised CorrectedSiw, Tcw' [n][4][4] f32 [R t/s], points' or None,
+        lm_iterations)."""
+        S = np.ascontiguousarray(np.asarray(Scw, np.float64).reshape(-1, 8)).copy()
+        fx = np.ascontiguousarray(fixed, np.uint8)
+        E = np.ascontiguousarray(edges, dtype=SIM3_EDGE_DTYPE)
+        T = np.zeros((max(len(S), 1), 4, 4), np.float32)
+        P = None if points is None else \
+            np.ascontiguousarray(np.asarray(points, np.float32).reshape(-1, 3)).copy()
+        ref = None if points is None else np.ascontiguousarray(point_ref, np.int32)
+        its = C.c_int()
+        _opt_check(lib().slamgpu_optimize_essential_graph(
+            len(S), _ptr(S), _ptr(fx), _ptr(E), len(E), int(bool(fix_scale)), int(n_iterations),
+            _ptr(T), _ptr(P), _ptr(ref), 0 if P is None else len(P), C.byref(its)))
+        return S, T[:len(S)], P, its.value
 
     @staticmethod
     def BundleAdjustment(kf_Tcw, kf_mode, points, point_obs_start, obs, cam, inv_sigma2,

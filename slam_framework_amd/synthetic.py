@@ -310,6 +310,123 @@ def sim3_problem(seed: int, n: int = 300, outlier_frac: float = 0.1, noise_px: f
     return m, pack(R0, t0, s0), S_true, level_inv_sigma2(scale_factor, nlevels), bad
 
 
+def _sim3_pack(R, t, s):
+    q = _quat_from_R(R)
+    return np.array([q[0], q[1], q[2], q[3], t[0], t[1], t[2], s], np.float64)
+
+
+def _sim3_mat(S8):
+    x, y, z, w = S8[:4]
+    R = np.array([[1 - 2 * (y * y + z * z), 2 * (x * y - z * w), 2 * (x * z + y * w)],
+                  [2 * (x * y + z * w), 1 - 2 * (x * x + z * z), 2 * (y * z - x * w)],
+                  [2 * (x * z - y * w), 2 * (y * z + x * w), 1 - 2 * (x * x + y * y)]])
+    M = np.eye(4)
+    M[:3, :3] = S8[7] * R
+    M[:3, 3] = S8[4:7]
+    return M
+
+
+def _sim3_from_mat(M):
+    s = float(np.cbrt(np.linalg.det(M[:3, :3])))
+    return _sim3_pack(M[:3, :3] / s, M[:3, 3], s)
+
+
+def essential_graph_problem(seed: int, n_kf: int = 60, fix_scale: bool = True,
+                            drift_rot: float = 0.004, drift_trans: float = 0.02,
+                            drift_scale: float = 0.01, meas_noise=None,
+                            covis: int = 3, neighbourhood: int = 4, loop_kf: int = 1,
+                            old_loop=None):
+    """One OptimizeEssentialGraph input (optimizer.cpp:718-960) for a loop closure: n_kf
+    keyframes on a circle (truth), their drifted estimates (rotation / translation / scale random
+    walks; scale kept at 1 when fix_scale, the stereo case), and the graph the reference builds:
+      1. loop connections (:784-812): each keyframe of the current keyframe's neighbourhood
+         (the last `neighbourhood` ones) to the loop keyframe's (loop_kf - 1 .. loop_kf + 2),
+         measured from the corrected poses vScw;
+      2. per keyframe in id order (:815-909): the spanning-tree edge to its parent (the previous
+         keyframe), loop edges to older keyframes (old_loop = (a, b), a > b), covisibility edges
+         to the `covis` previous keyframes that are not its parent and not already a loop
+         connection, measured from the non-corrected poses.
+    The current keyframe's neighbourhood is corrected to the truth (what ComputeSim3 + the loop
+    correction give, corrected_sim3); non_corrected keeps their drifted poses. meas_noise None:
+    measurements Sjw * Swi from those estimates, as the reference forms them; a float: the true
+    relative Sim3s perturbed by that much (0: a consistent graph whose optimum is the truth).
+    Returns (Scw_init [n][8], fixed [n] u8, edges [SIM3_EDGE_DTYPE], Scw_true [n][8],
+    Scw_drift [n][8])."""
+    rng = np.random.default_rng(seed)
+    from .slamgpu import SIM3_EDGE_DTYPE
+    n = n_kf
+    radius = 30.0
+    truth, drift = [], []
+    D = np.eye(4)
+    for k in range(n):
+        a = 2 * np.pi * k / n
+        Rwc = _rodrigues(np.array([0.0, -a, 0.0]))
+        twc = np.array([radius * np.sin(a), 0.0, radius * (1 - np.cos(a))])
+        Tcw = np.eye(4)
+        Tcw[:3, :3] = Rwc.T
+        Tcw[:3, 3] = -Rwc.T @ twc
+        truth.append(Tcw)
+        if k == 0:
+            D = Tcw.copy()
+        else:
+            rel = truth[k] @ np.linalg.inv(truth[k - 1])  # T_k,k-1
+            N = np.eye(4)
+            N[:3, :3] = _rodrigues(rng.normal(0, drift_rot, 3))
+            N[:3, 3] = rng.normal(0, drift_trans, 3)
+            sc = 1.0 if fix_scale else float(np.exp(rng.normal(0, drift_scale)))
+            D = N @ rel @ D
+            if not fix_scale:
+                D = np.diag([sc, sc, sc, 1.0]) @ D
+        drift.append(D.copy())
+    S_true = np.stack([_sim3_from_mat(T) for T in truth])
+    S_drift = np.stack([_sim3_from_mat(T) for T in drift])
+    cur = n - 1
+    hood = list(range(n - neighbourhood, n))
+    S_cw = S_drift.copy()
+    for k in hood:
+        S_cw[k] = S_true[k]  # corrected_sim3
+    S_cw[loop_kf] = S_true[loop_kf]
+    S_drift[loop_kf] = S_true[loop_kf]
+    fixed = np.zeros(n, np.uint8)
+    fixed[loop_kf] = 1
+    noncorr = {k: S_drift[k] for k in hood}
+
+    def meas(j, i, Sj, Si):
+        if meas_noise is None:  # the reference: Sji = Sjw * Swi from the estimates
+            return _sim3_from_mat(_sim3_mat(Sj) @ np.linalg.inv(_sim3_mat(Si)))
+        M = truth[j] @ np.linalg.inv(truth[i])
+        if meas_noise > 0:
+            N = np.eye(4)
+            N[:3, :3] = _rodrigues(rng.normal(0, meas_noise, 3))
+            N[:3, 3] = rng.normal(0, 10 * meas_noise, 3)
+            M = N @ M
+        return _sim3_from_mat(M)
+
+    edges = []
+    inserted = set()
+    loop_hood = [k for k in range(loop_kf - 1, loop_kf + 3) if 0 <= k < n]
+    for i in hood:
+        for j in loop_hood:
+            edges.append((i, j, meas(j, i, S_cw[j], S_cw[i])))
+            inserted.add((min(i, j), max(i, j)))
+    for i in range(n):
+        Si = noncorr.get(i, S_cw[i])
+        if i > 0:
+            p = i - 1
+            edges.append((i, p, meas(p, i, noncorr.get(p, S_cw[p]), Si)))
+        loops = [old_loop[1]] if old_loop is not None and i == old_loop[0] else []
+        for l in loops:
+            edges.append((i, l, meas(l, i, noncorr.get(l, S_cw[l]), Si)))
+        for j in range(max(0, i - covis), i - 1):
+            if j in loops or (min(i, j), max(i, j)) in inserted:
+                continue
+            edges.append((i, j, meas(j, i, noncorr.get(j, S_cw[j]), Si)))
+    E = np.zeros(len(edges), SIM3_EDGE_DTYPE)
+    for k, (i, j, M) in enumerate(edges):
+        E[k]["i"], E[k]["j"], E[k]["Sji"] = i, j, M
+    return S_cw, fixed, E, S_true, S_drift
+
+
 def _quat_from_R(R: np.ndarray) -> np.ndarray:
     """(x, y, z, w) of a rotation matrix, w >= 0."""
     w = np.sqrt(max(0.0, 1.0 + R[0, 0] + R[1, 1] + R[2, 2])) / 2
