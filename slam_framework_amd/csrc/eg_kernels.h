@@ -43,6 +43,7 @@ struct EgState {
   double* err;      // [n_edges][7]
   double* chi2;     // [n_edges]
   double* contrib;  // [n_edges][kEgContrib]
+  double* J;        // [n_edges][98] numeric Jacobians Ji, Jj
   double* H;        // [blocks][49] assembled system
   double* b;        // [7F]
   double* L;        // [blocks][49] factor (copy of H)

@@ -67,12 +67,12 @@ __global__ __launch_bounds__(256) void eg_linearize_kernel(EgGraph G, EgState W)
 #pragma unroll
   for (int r = 0; r < 7; r++) W.err[7 * k + r] = e[r];
   double* c = W.contrib + (int64_t)k * kEgContrib;
-  // Jacobian columns go through the contribution slots (Hii <- Ji, Hjj <- Jj; row-major 7x7),
-  // then the products overwrite them
+  // Jacobian columns (Ji, Jj row-major 7x7) into the edge's Jacobian slots, then the products
+  double* Jk = W.J + (int64_t)k * 98;
   const double delta = 1e-9, scalar = 1.0 / (2 * delta);
   for (int which = 0; which < 2; which++) {
     if ((which ? fj : fi) < 0) continue;
-    double* J = c + 49 * which;
+    double* J = Jk + 49 * which;
 #pragma unroll 1
     for (int d = 0; d < 7; d++) {
       double ep[7], em[7];
@@ -88,11 +88,8 @@ __global__ __launch_bounds__(256) void eg_linearize_kernel(EgGraph G, EgState W)
     }
   }
   // b += J' omega_r (omega_r = -e), H += J' J (base_binary_edge.hpp:55-121, Omega = I)
-  double Ja[49], Jb[49];
-  if (fi >= 0)
-    for (int q = 0; q < 49; q++) Ja[q] = c[q];
-  if (fj >= 0)
-    for (int q = 0; q < 49; q++) Jb[q] = c[49 + q];
+  const double* Ja = Jk;
+  const double* Jb = Jk + 49;
   if (fi >= 0) {
 #pragma unroll 1
     for (int a = 0; a < 7; a++) {
@@ -182,13 +179,45 @@ __global__ __launch_bounds__(64) void eg_assemble_kernel(EgGraph G, EgState W) {
   else W.H[(int64_t)blk * 49 + lane] = s;
 }
 
-constexpr int kFacThreads = 1024;
+constexpr int kFacThreads = 256;
+
+// In-register LDLT of a 7x7 block (lower triangle + diagonal of A, row-major): L below the
+// diagonal, D on it. Returns false on a zero pivot.
+__device__ __forceinline__ bool ldlt7_inplace(double* A) {
+  double a[7][7];
+#pragma unroll
+  for (int r = 0; r < 7; r++)
+#pragma unroll
+    for (int c = 0; c <= r; c++) a[r][c] = A[7 * r + c];
+  bool ok = true;
+#pragma unroll
+  for (int j = 0; j < 7; j++) {
+    double d = a[j][j];
+#pragma unroll
+    for (int m = 0; m < j; m++) d -= a[j][m] * a[j][m] * a[m][m];
+    a[j][j] = d;
+    ok = ok && d != 0.0;
+#pragma unroll
+    for (int i = j + 1; i < 7; i++) {
+      double t = a[i][j];
+#pragma unroll
+      for (int m = 0; m < j; m++) t -= a[i][m] * a[j][m] * a[m][m];
+      a[i][j] = t / d;
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < 7; r++)
+#pragma unroll
+    for (int c = 0; c <= r; c++) A[7 * r + c] = a[r][c];
+  return ok;
+}
 
 __global__ __launch_bounds__(kFacThreads) void eg_factor_solve_kernel(EgGraph G, EgState W,
                                                                       int64_t n_blocks,
                                                                       double lambda) {
   __shared__ int s_ok;
   __shared__ double red[256];
+  __shared__ double s_kk[49];  // the current diagonal block (L below, D on the diagonal)
   const int tid = threadIdx.x, F = G.F;
   double* L = W.L;
   for (int64_t q = tid; q < n_blocks * 49; q += kFacThreads) L[q] = W.H[q];
@@ -203,29 +232,27 @@ __global__ __launch_bounds__(kFacThreads) void eg_factor_solve_kernel(EgGraph G,
   // ---- factorisation, right-looking by block column ----
   for (int k = 0; k < F; k++) {
     double* Akk = blkp(k, k);
-    if (tid == 0) {  // the diagonal block: scalar LDLT (lower L, D on the diagonal)
-      for (int j = 0; j < 7; j++) {
-        double d = Akk[8 * j];
-        for (int m = 0; m < j; m++) d -= Akk[7 * j + m] * Akk[7 * j + m] * Akk[8 * m];
-        Akk[8 * j] = d;
-        if (d == 0.0) s_ok = 0;
-        for (int i = j + 1; i < 7; i++) {
-          double s = Akk[7 * i + j];
-          for (int m = 0; m < j; m++) s -= Akk[7 * i + m] * Akk[7 * j + m] * Akk[8 * m];
-          Akk[7 * i + j] = s / d;
-        }
-      }
-    }
+    if (tid < 49) s_kk[tid] = Akk[tid];
     __syncthreads();
+    if (tid == 0 && !ldlt7_inplace(s_kk)) s_ok = 0;  // the diagonal block
+    __syncthreads();
+    if (tid < 49) Akk[tid] = s_kk[tid];
     const int e0 = G.ext_ptr[k], ne = G.ext_ptr[k + 1] - e0;
     for (int q = tid; q < 7 * ne; q += kFacThreads) {  // panel: L_ik = A_ik L_kk^-T D_k^-1
       const int i = G.ext_rows[e0 + q / 7], r = q % 7;
       double* Aik = blkp(i, k) + 7 * r;
+      double a[7];
+#pragma unroll
+      for (int c = 0; c < 7; c++) a[c] = Aik[c];
+#pragma unroll
       for (int c = 0; c < 7; c++) {
-        double s = Aik[c];
-        for (int m = 0; m < c; m++) s -= Aik[m] * Akk[8 * m] * Akk[7 * c + m];
-        Aik[c] = s / Akk[8 * c];
+        double t = a[c];
+#pragma unroll
+        for (int m = 0; m < c; m++) t -= a[m] * s_kk[8 * m] * s_kk[7 * c + m];
+        a[c] = t / s_kk[8 * c];
       }
+#pragma unroll
+      for (int c = 0; c < 7; c++) Aik[c] = a[c];
     }
     __syncthreads();
     const int npairs = ne * (ne + 1) / 2;
@@ -239,10 +266,10 @@ __global__ __launch_bounds__(kFacThreads) void eg_factor_solve_kernel(EgGraph G,
       const int r = ent / 7, c = ent % 7;
       const double* Lik = blkp(i, k) + 7 * r;
       const double* Ljk = blkp(j, k) + 7 * c;
-      double s = 0.0;
+      double t = 0.0;
 #pragma unroll
-      for (int m = 0; m < 7; m++) s += Lik[m] * Akk[8 * m] * Ljk[m];
-      blkp(i, j)[ent] -= s;
+      for (int m = 0; m < 7; m++) t += Lik[m] * s_kk[8 * m] * Ljk[m];
+      blkp(i, j)[ent] -= t;
     }
     __syncthreads();
   }
@@ -252,12 +279,17 @@ __global__ __launch_bounds__(kFacThreads) void eg_factor_solve_kernel(EgGraph G,
   __syncthreads();
   for (int k = 0; k < F; k++) {
     const double* Lkk = blkp(k, k);
-    if (tid == 0)
-      for (int r = 1; r < 7; r++) {
-        double s = y[7 * k + r];
-        for (int m = 0; m < r; m++) s -= Lkk[7 * r + m] * y[7 * k + m];
-        y[7 * k + r] = s;
-      }
+    if (tid == 0) {
+      double v[7];
+#pragma unroll
+      for (int r = 0; r < 7; r++) v[r] = y[7 * k + r];
+#pragma unroll
+      for (int r = 1; r < 7; r++)
+#pragma unroll
+        for (int m = 0; m < r; m++) v[r] -= Lkk[7 * r + m] * v[m];
+#pragma unroll
+      for (int r = 1; r < 7; r++) y[7 * k + r] = v[r];
+    }
     __syncthreads();
     const int e0 = G.ext_ptr[k], ne = G.ext_ptr[k + 1] - e0;
     for (int q = tid; q < 7 * ne; q += kFacThreads) {
@@ -285,11 +317,15 @@ __global__ __launch_bounds__(kFacThreads) void eg_factor_solve_kernel(EgGraph G,
     __syncthreads();
     if (tid == 0) {
       const double* Lkk = blkp(k, k);
-      for (int r = 5; r >= 0; r--) {
-        double s = y[7 * k + r];
-        for (int m = r + 1; m < 7; m++) s -= Lkk[7 * m + r] * y[7 * k + m];
-        y[7 * k + r] = s;
-      }
+      double v[7];
+#pragma unroll
+      for (int r = 0; r < 7; r++) v[r] = y[7 * k + r];
+#pragma unroll
+      for (int r = 5; r >= 0; r--)
+#pragma unroll
+        for (int m = r + 1; m < 7; m++) v[r] -= Lkk[7 * m + r] * v[m];
+#pragma unroll
+      for (int r = 0; r < 6; r++) y[7 * k + r] = v[r];
     }
     __syncthreads();
   }
@@ -301,9 +337,8 @@ __global__ __launch_bounds__(kFacThreads) void eg_factor_solve_kernel(EgGraph G,
   __syncthreads();
   // computeScale: sum x (lambda x + b)
   double s = 0.0;
-  if (tid < 256)
-    for (int q = tid; q < 7 * F; q += 256) s += W.x[q] * (lambda * W.x[q] + W.b[q]);
-  if (tid < 256) red[tid] = s;
+  for (int q = tid; q < 7 * F; q += 256) s += W.x[q] * (lambda * W.x[q] + W.b[q]);
+  red[tid] = s;
   __syncthreads();
   for (int h = 128; h >= 1; h >>= 1) {
     if (tid < h) red[tid] += red[tid + h];

@@ -617,6 +617,7 @@ int slamgpu_optimize_essential_graph(int n_kf, double* Scw, const uint8_t* fixed
   const size_t o_ep = take(4 * ((size_t)F + 1)), o_er = take(4 * ext_rows.size());
   const size_t o_S = take(8 * 8 * N), o_S2 = take(8 * 8 * N), o_S0 = take(8 * 8 * N);
   const size_t o_err = take(8 * 7 * E), o_chi = take(8 * E), o_con = take(8 * kEgContrib * E);
+  const size_t o_J = take(8 * 98 * E);
   const size_t o_H = take(8 * 49 * (size_t)n_blocks), o_b = take(8 * P7);
   const size_t o_L = take(8 * 49 * (size_t)n_blocks), o_x = take(8 * P7), o_y = take(8 * P7);
   const size_t o_out = take(64), o_T = take(Tcw ? 64 * N : 0);
@@ -668,6 +669,7 @@ int slamgpu_optimize_essential_graph(int n_kf, double* Scw, const uint8_t* fixed
   W.err = reinterpret_cast<double*>(d + o_err);
   W.chi2 = reinterpret_cast<double*>(d + o_chi);
   W.contrib = reinterpret_cast<double*>(d + o_con);
+  W.J = reinterpret_cast<double*>(d + o_J);
   W.H = reinterpret_cast<double*>(d + o_H);
   W.b = reinterpret_cast<double*>(d + o_b);
   W.L = reinterpret_cast<double*>(d + o_L);

@@ -10,7 +10,7 @@ import numpy as np
 sys.path.insert(0, ".")
 from slam_framework_amd import slamgpu as G, synthetic as S  # noqa: E402
 
-reps = int(sys.argv[1]) if len(sys.argv) > 1 else 10
+reps = int(sys.argv[1]) if len(sys.argv) > 1 and sys.argv[1].isdigit() else 10
 CAM = S.KITTI_CAM
 out = {}
 
@@ -43,4 +43,36 @@ for nkf, npt in [(30, 4000), (100, 12000)]:
     out[key] = {"median_ms": round(med, 3), "min_ms": round(mn, 3), "lm_iterations": r[2],
                 "keyframes": nkf, "points": npt, "observations": int(len(P["obs"]))}
     print(key, out[key], flush=True)
+# OptimizeSim3: one loop candidate (SIM3 matches of a keyframe pair), and a batch of 8
+isig = S.level_inv_sigma2()
+for n in (300, 1000):
+    m, S0, _, _, _ = S.sim3_problem(40 + n, n, outlier_frac=0.2)
+    med, mn, r = timeit(lambda: G.Optimizer.OptimizeSim3(m, S0, CAM, CAM, isig, isig, 10.0, False))
+    key = f"sim3_{n}"
+    out[key] = {"median_ms": round(med, 3), "min_ms": round(mn, 3), "n_inliers": r[0],
+                "matches": int(len(m))}
+    print(key, out[key], flush=True)
+# OptimizeEssentialGraph: loop closures over n keyframes (covisibility 3, an older loop edge)
+for n in (100, 400, 1000):
+    Scw, fixed, E, _, _ = S.essential_graph_problem(60 + n, n, fix_scale=True,
+                                                    old_loop=(n // 2, n // 5))
+    med, mn, r = timeit(lambda: G.Optimizer.OptimizeEssentialGraph(Scw, fixed, E, True, 20))
+    key = f"essential_graph_{n}"
+    out[key] = {"median_ms": round(med, 3), "min_ms": round(mn, 3), "lm_iterations": r[3],
+                "keyframes": n, "edges": int(len(E))}
+    print(key, out[key], flush=True)
+if "--oracle" in sys.argv:  # the CPU restatement beside it (one thread)
+    sys.path.insert(0, "tests")
+    import oracle_lib as O
+    for n in (300, 1000):
+        m, S0, _, _, _ = S.sim3_problem(40 + n, n, outlier_frac=0.2)
+        t0 = time.perf_counter()
+        O.optimize_sim3(CAM, CAM, isig, isig, m, S0, 10.0, False)
+        out[f"sim3_{n}"]["oracle_1thread_ms"] = round(1e3 * (time.perf_counter() - t0), 3)
+    for n in (100, 400, 1000):
+        Scw, fixed, E, _, _ = S.essential_graph_problem(60 + n, n, fix_scale=True,
+                                                        old_loop=(n // 2, n // 5))
+        t0 = time.perf_counter()
+        O.optimize_essential_graph(Scw, fixed, E, True, 20)
+        out[f"essential_graph_{n}"]["oracle_1thread_ms"] = round(1e3 * (time.perf_counter() - t0), 3)
 print(json.dumps(out))
