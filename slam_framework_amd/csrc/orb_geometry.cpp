@@ -188,10 +188,11 @@ int compute_geometry(const OrbParams& p, int cols, int rows, OrbGeom* g,
   // A tile row starts at iniX & ~15 (16-byte global_load_lds chunks; up to 15 lead bytes).
   // Tiles are double-buffered and hold whole 1 KiB glds blocks (1024 / stride rows each).
   g->fast_tile_stride = max_wcell + 6 + 15 + 4 <= 64 ? 64 : 128;
-  g->fast_tile_rows = round_up(max_hcell + 6, 1024 / g->fast_tile_stride);
+  g->fast_tile_rows = FAST_EXACT_ROWS ? max_hcell + 6
+                                      : round_up(max_hcell + 6, 1024 / g->fast_tile_stride);
   g->fast_score_stride = g->fast_tile_stride;
   g->fast_score_rows = max_hcell + 2;  // detect rows + a zero row above and below
-  g->fast_lds_per_wave = 2 * round_up(g->fast_tile_stride * g->fast_tile_rows, 16) +
+  g->fast_lds_per_wave = FAST_TILE_BUFS * round_up(g->fast_tile_stride * g->fast_tile_rows, 16) +
                          round_up(g->fast_score_stride * g->fast_score_rows, 16) +
                          round_up(2 * max_wcell * max_hcell, 16);  // u16 candidate list
   if (max_wcell > 64) return -4;

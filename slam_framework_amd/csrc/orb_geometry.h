@@ -8,6 +8,17 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+// fast_cells tile buffers per wave (2: the next cell's tile streams in while this one is
+// processed; 1: more waves per CU instead -- LDS, not VGPRs, bounds its occupancy: 10.3 KB per
+// wave double-buffered, 6.6 KB single; A/B 0.966 -> 0.84 ms per step) and whether a tile holds
+// exactly the view's rows (the last global_load_lds block lane-masked) or whole 1 KiB blocks.
+#ifndef FAST_TILE_BUFS
+#define FAST_TILE_BUFS 1
+#endif
+#ifndef FAST_EXACT_ROWS
+#define FAST_EXACT_ROWS 1
+#endif
+
 namespace slamgpu {
 
 constexpr int kMaxLevels = 12;

@@ -366,7 +366,8 @@ __global__ __launch_bounds__(64 * kCellWaves, FAST_MINW) void fast_cells_kernel(
   const int min_th = __builtin_amdgcn_readfirstlane(g->min_th);
   const int tile_bytes = (kTileStride * g->fast_tile_rows + 15) & ~15;
   uint8_t* tile0 = s_fast + wid * g->fast_lds_per_wave;
-  uint8_t* sc = tile0 + (GLDS ? 2 : 1) * tile_bytes;
+  uint8_t* sc = tile0 + (GLDS ? FAST_TILE_BUFS : 1) * tile_bytes;
+  const int tile_rows = __builtin_amdgcn_readfirstlane(g->fast_tile_rows);
   uint16_t* cand =
       reinterpret_cast<uint16_t*>(sc + ((kScoreStride * g->fast_score_rows + 15) & ~15));
 
@@ -395,7 +396,7 @@ __global__ __launch_bounds__(64 * kCellWaves, FAST_MINW) void fast_cells_kernel(
     const uint8_t* src = v.base + (int64_t)v.ini_y * v.pitch + v.ax + glc;
 #pragma unroll
     for (int k = 0; k < kGSteps; k++)
-      if (k < n)
+      if (k < n && (!FAST_EXACT_ROWS || k * kGRows + glr < tile_rows))
         __builtin_amdgcn_global_load_lds(
             (const __attribute__((address_space(1))) void*)(
                 src + (int64_t)min(k * kGRows + glr, v.vh - 1) * v.pitch),
@@ -404,7 +405,7 @@ __global__ __launch_bounds__(64 * kCellWaves, FAST_MINW) void fast_cells_kernel(
   };
   CellView nxt = cell_view<kAlign>(b, g, img, in_pitch, readlane4(my_desc, 0));
   if constexpr (GLDS) {
-    if (nxt.vh > 0) issue(nxt, tile0);
+    if (FAST_TILE_BUFS == 2 && nxt.vh > 0) issue(nxt, tile0);
   } else {
     if (nxt.vh > 0) prefetch(nxt);
   }
@@ -413,7 +414,21 @@ __global__ __launch_bounds__(64 * kCellWaves, FAST_MINW) void fast_cells_kernel(
     const CellView v = nxt;
     const int64_t slot = (int64_t)img * ncells + c0 + ci;
     uint8_t* tile = tile0;
-    if constexpr (GLDS) {
+    if constexpr (GLDS && FAST_TILE_BUFS == 1) {
+      // one tile buffer: this cell's rows are loaded now (the previous cell's tile reads have
+      // all returned), other waves hide the latency
+      if (ci + 1 < nc) nxt = cell_view<kAlign>(b, g, img, in_pitch, readlane4(my_desc, ci + 1));
+      if (v.vh == 0) {  // empty cell (:737, :745)
+        if (lane == 0) cell_count[slot] = 0;
+        continue;
+      }
+      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      issue(v, tile0);
+      __builtin_amdgcn_s_waitcnt(0x0F70);
+      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+    } else if constexpr (GLDS) {
       tile = tile0 + (ci & 1) * tile_bytes;
       int n_next = 0;
       if (ci + 1 < nc) {
