@@ -358,6 +358,29 @@ def main():
         if not args.no_latency:
             drop_in = {"single_frame": bench_frame_latency(Ls, Rs, cam, local),
                        "batched_h2d": bench_h2d(ctxs[0], host_l, host_r, poses, cam, dev, args)}
+        # every frontend kernel on its roofs: standalone launch times of the breakdown pass (one
+        # batch, nothing else in flight), algorithmic bytes, PMC traffic and VALU counts
+        kernels = {}
+        for n in names:
+            ms, nl = brk[n]
+            if ms <= 0 or nl <= 0:
+                continue
+            avg_s = ms / 1000.0 / nl
+            ent = {"ms_per_step": round(ms, 4), "launches_per_step": nl,
+                   "avg_launch_us": round(avg_s * 1e6, 2)}
+            kb = kernel_bytes(n, 2 * Bs, Bs, kp_img, level_px, nqueries // NS)
+            if kb:
+                ent["algorithmic_bytes_per_launch"] = kb / nl
+                ent["hbm_frac"] = round(kb / nl / avg_s / 1e9 / HBM_PEAK_GBS, 4)
+            tr, _ = measured_traffic(n, B)
+            if tr is not None:
+                ent["traffic_bytes_per_launch"] = round(tr)
+                ent["traffic_frac"] = round(tr / avg_s / 1e9 / HBM_PEAK_GBS, 4)
+            vi, vpeak = measured_valu(n, B)
+            if vi is not None:
+                ent["valu_wave_instr_per_launch"] = round(vi)
+                ent["valu_issue_frac"] = round(vi / avg_s / vpeak, 4)
+            kernels[n] = ent
         line = {
             "metric": "stereo frames/sec ORB extract+match @1241x376, 2000 kp/frame",
             "value": round(value, 2), "unit": "stereo frames/s", "n_gpus": world,
@@ -379,6 +402,7 @@ def main():
             "roofline": roofline,
             "cpu_baseline": cpu,
             "kernel_ms_per_step": {n: round(brk[n][0], 4) for n in names},
+            "kernels_standalone": kernels,
             "optimizer": opt,
             "bow": bow_leg,
             "drop_in": drop_in,
