@@ -125,6 +125,18 @@ __global__ __launch_bounds__(256) void stereo_rows_kernel(const OrbGeom* __restr
   }
 }
 
+// One left keypoint per half-wave (32 lanes), two per wave: the kernel is a chain of dependent
+// loads per keypoint (row table -> candidates -> descriptors -> SAD windows), so two independent
+// chains per wave hide twice the latency at the same occupancy.
+__device__ __forceinline__ uint32_t half_min(uint32_t v) {
+#pragma unroll
+  for (int off = 16; off >= 1; off >>= 1) {
+    const uint32_t o = __shfl_xor(v, off, 64);
+    v = o < v ? o : v;
+  }
+  return v;
+}
+
 __global__ __launch_bounds__(256) void stereo_match_kernel(ImageBatch b,
                                                            const OrbGeom* __restrict__ g,
                                                            FrameKps ext, Camera cam, int nrows,
@@ -135,52 +147,59 @@ __global__ __launch_bounds__(256) void stereo_match_kernel(ImageBatch b,
 #else
   const int f = blockIdx.y, bx = blockIdx.x;
 #endif
-  const int lane = threadIdx.x & 63;
-  const int iL = bx * 4 + wave_id();
+  const int lane = threadIdx.x & 63, half = lane >> 5, hl = lane & 31;
+  const int iL = (bx * 4 + wave_id()) * 2 + half;
   const int il = 2 * f, ir = 2 * f + 1;
   const int nl = ext.n[il * ext.n_stride];
-  if (iL >= nl) return;
   const int64_t o = (int64_t)f * g->kp_cap + iL;
-  if (lane == 0) {
+  bool ok = iL < nl;
+  if (ok && hl == 0) {
     out.u_right[o] = -1.0f;
     out.depth[o] = -1.0f;
     ws.sad[o] = -1;
   }
-  const KeyPoint kpL = ext.kps[il * ext.stride + iL];
+  KeyPoint kpL{};
+  if (ok) kpL = ext.kps[il * ext.stride + iL];
   const KeyPoint* kr = ext.kps + ir * ext.stride;
   const int levelL = kpL.octave;
   const float vL = kpL.y, uL = kpL.x;
   const int row = (int)vL;
-  if (row < 0 || row >= nrows) return;
+  ok = ok && row >= 0 && row < nrows;
   const int* rs = ws.row_start + (int64_t)f * (nrows + 1);
   const int* items = ws.row_items + (int64_t)f * ws.row_cap;
-  const int c0 = rs[row], c1 = min(rs[row + 1], ws.row_cap);
-  if (c0 >= c1) return;
+  int c0 = 0, c1 = 0;
+  if (ok) {
+    c0 = rs[row];
+    c1 = min(rs[row + 1], ws.row_cap);
+  }
+  ok = ok && c0 < c1;
   const float baseline = cam.bf / cam.fx;  // see DESIGN.md: maxD is UB in the reference (:436)
   const float minZ = baseline, minD = 0, maxD = cam.bf / minZ;
   const float minU = uL - maxD, maxU = uL - minD;
-  if (maxU < 0) return;
-  const uint8_t* dL = ext.desc + (il * ext.stride + iL) * 32;
+  ok = ok && !(maxU < 0);
+  const uint8_t* dL = ext.desc + (il * ext.stride + (ok ? iL : 0)) * 32;
   const uint8_t* dRb = ext.desc + ir * ext.stride * 32;
   uint32_t best = ((uint32_t)TH_HIGH << 16) | 0xffffu;
-  for (int c = c0 + lane; c < c1; c += 64) {
-    const int iR = items[c];
-    const KeyPoint kpR = kr[iR];
-    if (kpR.octave < levelL - 1 || kpR.octave > levelL + 1) continue;
-    const float uR = kpR.x;
-    if (uR >= minU && uR <= maxU) {
-      const int dist = hamming32(dL, dRb + iR * 32);
-      const uint32_t key = ((uint32_t)dist << 16) | (uint32_t)iR;
-      if (dist < TH_HIGH && key < best) best = key;
+  if (ok) {
+    for (int c = c0 + hl; c < c1; c += 32) {
+      const int iR = items[c];
+      const KeyPoint kpR = kr[iR];
+      if (kpR.octave < levelL - 1 || kpR.octave > levelL + 1) continue;
+      const float uR = kpR.x;
+      if (uR >= minU && uR <= maxU) {
+        const int dist = hamming32(dL, dRb + iR * 32);
+        const uint32_t key = ((uint32_t)dist << 16) | (uint32_t)iR;
+        if (dist < TH_HIGH && key < best) best = key;
+      }
     }
   }
-  best = wave_min(best);
+  best = half_min(best);
   const int bestDist = (int)(best >> 16);
   const int thOrbDist = (TH_HIGH + TH_LOW) / 2;
-  if (bestDist >= thOrbDist) return;
-  const int bestIdxR = (int)(best & 0xffff);
+  ok = ok && bestDist < thOrbDist;
   // sliding-window SAD at the left keypoint's level (:481-531)
-  const float uR0 = kr[bestIdxR].x;
+  const int bestIdxR = ok ? (int)(best & 0xffff) : 0;
+  const float uR0 = ok ? kr[bestIdxR].x : 0.f;
   const float scaleFactor = g->lv[levelL].inv_scale;
   const float scaleduL = roundf(kpL.x * scaleFactor);
   const float scaledvL = roundf(kpL.y * scaleFactor);
@@ -189,79 +208,87 @@ __global__ __launch_bounds__(256) void stereo_match_kernel(ImageBatch b,
   const LevelGeom& LG = g->lv[levelL];
   const float iniu = scaleduR0 + L - w;
   const float endu = scaleduR0 + L + w + 1;
-  if (iniu < 0 || endu >= (float)LG.w) return;
+  ok = ok && !(iniu < 0 || endu >= (float)LG.w);
   const int yc = (int)scaledvL, xcl = (int)scaleduL, xcr = (int)scaleduR0;
   // windows the reference would reject with a cv::Mat ROI assertion are treated as no match
-  if (yc - w < 0 || yc + w >= LG.h || xcl - w < 0 || xcl + w >= LG.w || xcr - L - w < 0) return;
-  int pl, pr;
-  const uint8_t* IL = level_img(b, g, il, levelL, &pl);
-  const uint8_t* IR = level_img(b, g, ir, levelL, &pr);
-  // SAD of the 11 window offsets: the 121 (offset, row) pairs are spread over the wave (two
-  // rounds), each lane summing one 11-pixel row; rows are then summed per offset through LDS.
-  // The window bytes (left: columns xcl-5..xcl+5, right: xcr-10..xcr+10, rows yc-5..yc+5) are
-  // first staged into LDS with dword loads (11 dwords per row: 4 left + 7 right); dwords past a
-  // row's last byte are clamped to it (their bytes are never used). Caller images with an odd
-  // base or pitch take byte loads instead (wave-uniform).
-  __shared__ int s_part[4][128];
-  __shared__ uint32_t s_win[4][11][11];
-  int* part = s_part[wave_id()];
-  uint32_t(*win)[11] = s_win[wave_id()];
+  ok = ok && !(yc - w < 0 || yc + w >= LG.h || xcl - w < 0 || xcl + w >= LG.w || xcr - L - w < 0);
+  // SAD of the 11 window offsets: the 121 (offset, row) pairs over the half-wave (four rounds),
+  // each lane summing one 11-pixel row; rows are then summed per offset through LDS. The window
+  // bytes (left: columns xcl-5..xcl+5, right: xcr-10..xcr+10, rows yc-5..yc+5) are first staged
+  // into LDS with dword loads (11 dwords per row: 4 left + 7 right); dwords past a row's last byte
+  // are clamped to it (their bytes are never used). Caller images with an odd base or pitch take
+  // byte loads instead.
+  __shared__ int s_part[4][2][128];
+  __shared__ uint32_t s_win[4][2][11][11];
+  int* part = s_part[wave_id()][half];
+  uint32_t(*win)[11] = s_win[wave_id()][half];
+  int pl = 0, pr = 0;
+  const uint8_t* IL = nullptr;
+  const uint8_t* IR = nullptr;
+  if (ok) {
+    IL = level_img(b, g, il, levelL, &pl);
+    IR = level_img(b, g, ir, levelL, &pr);
+  }
   const int al = (xcl - w) & ~3, ar = (xcr - L - w) & ~3;
   const bool dw = ((((uintptr_t)IL | (uintptr_t)IR) | (uintptr_t)(pl | pr)) & 3) == 0;
   const int lastw = (LG.w - 1) >> 2;
+  if (ok) {
 #pragma unroll
-  for (int rnd = 0; rnd < 2; rnd++) {
-    const int p = lane + 64 * rnd;
-    if (p < 121) {
-      const int r = p / 11, d = p - 11 * r;  // window row, dword slot (0-3 left, 4-10 right)
-      const bool left = d < 4;
-      const uint8_t* img = left ? IL : IR;
-      const int pitch = left ? pl : pr;
-      const int x0 = left ? al + 4 * d : ar + 4 * (d - 4);
-      const uint8_t* row = img + (int64_t)(yc - w + r) * pitch;
-      uint32_t v;
-      if (dw) {
-        v = reinterpret_cast<const uint32_t*>(row)[min(x0 >> 2, lastw)];
-      } else {
-        v = 0;
-        for (int j = 0; j < 4; j++)
-          v |= (uint32_t)row[min(x0 + j, LG.w - 1)] << (8 * j);
+    for (int rnd = 0; rnd < 4; rnd++) {
+      const int p = hl + 32 * rnd;
+      if (p < 121) {
+        const int r = p / 11, d = p - 11 * r;  // window row, dword slot (0-3 left, 4-10 right)
+        const bool left = d < 4;
+        const uint8_t* img = left ? IL : IR;
+        const int pitch = left ? pl : pr;
+        const int x0 = left ? al + 4 * d : ar + 4 * (d - 4);
+        const uint8_t* rowp = img + (int64_t)(yc - w + r) * pitch;
+        uint32_t v;
+        if (dw) {
+          v = reinterpret_cast<const uint32_t*>(rowp)[min(x0 >> 2, lastw)];
+        } else {
+          v = 0;
+          for (int j = 0; j < 4; j++)
+            v |= (uint32_t)rowp[min(x0 + j, LG.w - 1)] << (8 * j);
+        }
+        win[r][d] = v;
       }
-      win[r][d] = v;
     }
   }
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
   __builtin_amdgcn_wave_barrier();
   const uint8_t* wb = reinterpret_cast<const uint8_t*>(&win[0][0]);  // row r at 44 r
+  if (ok) {
 #pragma unroll
-  for (int rnd = 0; rnd < 2; rnd++) {
-    const int p = lane + 64 * rnd;
-    if (p < 121) {
-      const int k = p / 11, yy = p - 11 * k - w;
-      const int incR = k - L;
-      const int cl = wb[44 * w + (xcl - al)];
-      const int cr = wb[44 * w + 16 + (xcr + incR - ar)];
-      const uint8_t* rl = wb + 44 * (yy + w) + (xcl - w - al);
-      const uint8_t* rr = wb + 44 * (yy + w) + 16 + (xcr + incR - w - ar);
-      int acc = 0;
+    for (int rnd = 0; rnd < 4; rnd++) {
+      const int p = hl + 32 * rnd;
+      if (p < 121) {
+        const int k = p / 11, yy = p - 11 * k - w;
+        const int incR = k - L;
+        const int cl = wb[44 * w + (xcl - al)];
+        const int cr = wb[44 * w + 16 + (xcr + incR - ar)];
+        const uint8_t* rl = wb + 44 * (yy + w) + (xcl - w - al);
+        const uint8_t* rr = wb + 44 * (yy + w) + 16 + (xcr + incR - w - ar);
+        int acc = 0;
 #pragma unroll
-      for (int xx = 0; xx < 2 * w + 1; xx++) acc += abs((rl[xx] - cl) - (rr[xx] - cr));
-      part[p] = acc;
+        for (int xx = 0; xx < 2 * w + 1; xx++) acc += abs((rl[xx] - cl) - (rr[xx] - cr));
+        part[p] = acc;
+      }
     }
   }
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
   __builtin_amdgcn_wave_barrier();
   int sad = 0x7fffffff;
-  if (lane < 2 * L + 1) {
+  if (ok && hl < 2 * L + 1) {
     int acc = 0;
 #pragma unroll
-    for (int yy = 0; yy < 2 * w + 1; yy++) acc += part[11 * lane + yy];
+    for (int yy = 0; yy < 2 * w + 1; yy++) acc += part[11 * hl + yy];
     sad = acc;
   }
   float vDists[11];
 #pragma unroll
-  for (int k = 0; k < 11; k++) vDists[k] = (float)__shfl(sad, k, 64);
-  if (lane != 0) return;
+  for (int k = 0; k < 11; k++) vDists[k] = (float)__shfl(sad, 32 * half + k, 64);
+  if (!ok || hl != 0) return;
   int bestSad = 0x7fffffff, bestincR = 0;
 #pragma unroll
   for (int k = 0; k < 11; k++) {
@@ -345,7 +372,7 @@ void launch_stereo(const ImageBatch& b, const OrbGeomDev& gd, const Camera& cam,
   const int nrows = g.lv[0].h;
   SLAMGPU_LAUNCH("stereo_rows", st, stereo_rows_kernel, dim3(n_frames), dim3(256), 0, st, gd.dev, ext, nrows,
                      ws, gd.ws.err);
-  SLAMGPU_LAUNCH("stereo_match", st, stereo_match_kernel, dim3((g.kp_cap + 3) / 4, n_frames), dim3(256), 0, st,
+  SLAMGPU_LAUNCH("stereo_match", st, stereo_match_kernel, dim3((g.kp_cap + 7) / 8, n_frames), dim3(256), 0, st,
                      b, gd.dev, ext, cam, nrows, ws, out);
   SLAMGPU_LAUNCH("stereo_median", st, stereo_median_kernel, dim3(n_frames), dim3(256), 0, st, gd.dev, ext, ws,
                      out);
