@@ -475,11 +475,41 @@ __device__ int scan_query(const ScanCtx& c, const Camera& cam, const FrameView& 
     const bool bCheckLevels = (c.min_level > 0) || (c.max_level >= 0);
     const int ny = nMaxCellY - nMinCellY + 1;
     const int total = (nMaxCellX - nMinCellX + 1) * ny;
-    for (int ci = lane; ci < total; ci += 64) {
-      const int ix = nMinCellX + ci / ny, iy = nMinCellY + ci % ny;
-      const int cell = ix * kGridRows + iy;
-      const int p1 = F.cell_start[cell + 1];
-      for (int p = F.cell_start[cell]; p < p1; p++) {
+    // The window's (cell, keypoint) pairs are spread over the lanes, one keypoint each: a lane
+    // per cell would walk its cell's keypoints as one serial chain of dependent loads while the
+    // lanes of empty or absent cells idle. Cells 64 at a time: per-lane keypoint counts, their
+    // wave prefix sum, then lane k takes pair k (its cell found by a binary search over the
+    // prefix sums). The kept candidates are an order-free minimum, so any order gives the same.
+    for (int cb = 0; cb < total; cb += 64) {
+      const int ci = cb + lane;
+      int cell = 0, q0 = 0, nq = 0;
+      if (ci < total) {
+        const int ix = nMinCellX + ci / ny, iy = nMinCellY + ci % ny;
+        cell = ix * kGridRows + iy;
+        q0 = F.cell_start[cell];
+        nq = F.cell_start[cell + 1] - q0;
+      }
+      int incl = nq;  // inclusive prefix sum over the lanes
+#pragma unroll
+      for (int off = 1; off < 64; off <<= 1) {
+        const int y = __shfl_up(incl, off, 64);
+        if (lane >= off) incl += y;
+      }
+      const int excl = incl - nq;
+      const int npairs = __shfl(incl, 63, 64);
+      // every lane takes part in the shuffles (a shuffle reads 0 from an inactive lane)
+      for (int k0 = 0; k0 < npairs; k0 += 64) {
+        const int k = k0 + lane;
+        int lo = 0;  // the last lane whose exclusive offset is <= k
+#pragma unroll
+        for (int step = 32; step >= 1; step >>= 1) {
+          const int cand = lo + step;
+          const int ec = __shfl(excl, cand & 63, 64);
+          if (cand < 64 && ec <= k) lo = cand;
+        }
+        const int p = __shfl(q0, lo, 64) + (k - __shfl(excl, lo, 64));
+        const int pcell = __shfl(cell, lo, 64);
+        if (k >= npairs) continue;
         const int i = F.cell_items[p];
         const KeyPoint kp = F.kps[i];
         if (bCheckLevels) {
@@ -494,16 +524,16 @@ __device__ int scan_query(const ScanCtx& c, const Camera& cam, const FrameView& 
         if (ur > 0 && fabsf(c.ur - ur) > c.gate) continue;
         const int dist = hamming32(c.desc, F.desc + i * 32);
         if (dist > c.max_dist) continue;
-        const uint64_t key = ((uint64_t)dist << 32) | ((uint64_t)cell << 12) | (uint64_t)i;
+        const uint64_t key = ((uint64_t)dist << 32) | ((uint64_t)pcell << 12) | (uint64_t)i;
         cnt++;
         if (key < t[kTopK - 1]) {
           t[kTopK - 1] = key;
 #pragma unroll
-          for (int k = kTopK - 1; k > 0; k--)
-            if (t[k] < t[k - 1]) {
-              const uint64_t s = t[k];
-              t[k] = t[k - 1];
-              t[k - 1] = s;
+          for (int k2 = kTopK - 1; k2 > 0; k2--)
+            if (t[k2] < t[k2 - 1]) {
+              const uint64_t s2 = t[k2];
+              t[k2] = t[k2 - 1];
+              t[k2 - 1] = s2;
             }
         }
       }
