@@ -46,6 +46,15 @@ TRAFFIC_FILE = os.path.join(ROOT, "profiles", "traffic.json")
 VALU_FILE = os.path.join(ROOT, "profiles", "valu.json")
 
 
+# bench.py's timing names -> kernel symbols where they differ (the octree timing is the per-image
+# kernel; octree_kernel is its global-memory fallback)
+KERNEL_SYMBOL = {"octree": "octree_img", "octree_global": "octree"}
+
+
+def _symbol_matches(sym, kernel):
+    return sym.split("<")[0].replace("_kernel", "") == KERNEL_SYMBOL.get(kernel, kernel)
+
+
 def measured_valu(kernel, batch):
     """SQ_INSTS_VALU per dispatch of `kernel` (tools/pmc_valu.sh + tools/valu.py, committed as
     profiles/valu.json) and the chip's VALU issue peak; (None, None) when absent or measured on
@@ -58,7 +67,7 @@ def measured_valu(kernel, batch):
     if d.get("batch") != batch:
         return None, None
     for k, v in d.get("kernels", {}).items():
-        if k.split("<")[0].replace("_kernel", "") == kernel:
+        if _symbol_matches(k, kernel):
             return v.get("sq_insts_valu_per_dispatch"), d.get("valu_issue_peak_per_s")
     return None, None
 
@@ -75,7 +84,7 @@ def measured_traffic(kernel, batch):
     if d.get("batch") != batch:
         return None, None
     for k, v in d.get("kernels", {}).items():
-        if k.split("<")[0].replace("_kernel", "") == kernel:
+        if _symbol_matches(k, kernel):
             return v.get("hbm_bytes_per_dispatch"), d.get("source")
     return None, None
 
