@@ -754,6 +754,28 @@ def bench_local_ba(dev, with_cpu):
             S.KITTI_CAM, PG["inv_sigma2"], n_iterations=10), reps=5)
         drop[f"global_ba_{nkf}kf"] = {"ms": round(ms, 3), "lm_iterations": r[2], "keyframes": nkf,
                                       "points": npt, "observations": int(len(PG["obs"]))}
+    # the loop closer's optimisers: OptimizeSim3 on one loop candidate and
+    # OptimizeEssentialGraph over a 400-keyframe loop, with the oracle on one host thread beside
+    isig = S.level_inv_sigma2()
+    m3, S3, _, _, _ = S.sim3_problem(340, 300, outlier_frac=0.2)
+    ms, r = wall_ms(lambda: G.Optimizer.OptimizeSim3(m3, S3, S.KITTI_CAM, S.KITTI_CAM, isig,
+                                                     isig, 10.0, False))
+    drop["optimize_sim3_300"] = {"ms": round(ms, 3), "n_inliers": r[0], "matches": int(len(m3))}
+    Seg, fx, Eeg, _, _ = S.essential_graph_problem(460, 400, fix_scale=True, old_loop=(200, 80))
+    ms, r = wall_ms(lambda: G.Optimizer.OptimizeEssentialGraph(Seg, fx, Eeg, True, 20), reps=5)
+    drop["essential_graph_400kf"] = {"ms": round(ms, 3), "lm_iterations": r[3], "keyframes": 400,
+                                     "edges": int(len(Eeg))}
+    if with_cpu:
+        sys.path.insert(0, os.path.join(ROOT, "tests"))
+        import oracle_lib as O
+        O.build()
+        t0 = time.perf_counter()
+        O.optimize_sim3(S.KITTI_CAM, S.KITTI_CAM, isig, isig, m3, S3, 10.0, False)
+        drop["optimize_sim3_300"]["oracle_1thread_ms"] = round(1e3 * (time.perf_counter() - t0), 3)
+        t0 = time.perf_counter()
+        O.optimize_essential_graph(Seg, fx, Eeg, True, 20)
+        drop["essential_graph_400kf"]["oracle_1thread_ms"] = round(
+            1e3 * (time.perf_counter() - t0), 3)
     out = {"linearize": out_lin, "drop_in": drop,
            "workload": "configs[4]: LocalBundleAdjustment on SURVEY 8(d) C5, 20 local + 5 fixed "
                        f"keyframes x 3000 map points ({no} observations), 5 robust + 10 LM "
