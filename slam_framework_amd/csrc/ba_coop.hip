@@ -536,48 +536,55 @@ __device__ __forceinline__ void factor_solve(CoopShared& sh, const CoopWs& w, in
                                              PtrT rhs, PtrT dg, PtrT V) {
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, n = 6 * K;
   if (tid == 0) sh.ok = 1;
+  // the diagonal block J by wave 0: lane r < 6 holds row r; pivots and multipliers by readlane
+  auto diag_factor = [&](int J) {
+    const int j0 = 6 * J;
+    const bool row = lane < 6;
+    const int ro = tri(j0 + (row ? lane : 0)) + j0;
+    double A[6], y = row ? rhs[j0 + lane] : 0.0;
+#pragma unroll
+    for (int k = 0; k < 6; k++) A[k] = row && k <= lane ? Lp[ro + k] : 0.0;
+    bool good = true;
+#pragma unroll
+    for (int c = 0; c < 6; c++) {
+      const double d = rl64(A[c], c);
+      good = good && d != 0.0;
+      const double rd = d != 0.0 ? 1.0 / d : 0.0;
+      const bool below = row && lane > c;
+      const double l = below ? A[c] * rd : 0.0;
+      const double yc = rl64(y, c);
+      if (below) {
+        y -= l * yc;
+        A[c] = l;
+      }
+      const double ld = l * d;
+#pragma unroll
+      for (int k = c + 1; k < 6; k++) {
+        const double lk = rl64(l, k);
+        if (row && lane >= k) A[k] -= ld * lk;
+      }
+    }
+    if (row) {
+      double dr = A[0];
+#pragma unroll
+      for (int k = 0; k < 6; k++) {
+        if (k < lane) Lp[ro + k] = A[k];
+        if (k == lane) dr = A[k];
+      }
+      dg[j0 + lane] = dr;
+      rhs[j0 + lane] = y;
+    }
+    if (lane == 0 && !good) sh.ok = 0;
+  };
   __syncthreads();
+  if (wid == 0) diag_factor(0);
+  __syncthreads();
+  // Look-ahead: while waves 1.. apply column J's trailing update to the rows below block J + 1,
+  // wave 0 updates block J + 1 itself and factors it, so the next column's panel can start right
+  // after one barrier (two barriers per block column instead of three, and the diagonal chain
+  // off the critical path).
   for (int J = 0; J < K; J++) {
     const int j0 = 6 * J;
-    if (wid == 0) {  // diagonal block: lane r < 6 holds row r; pivots and multipliers by readlane
-      const bool row = lane < 6;
-      const int ro = tri(j0 + (row ? lane : 0)) + j0;
-      double A[6], y = row ? rhs[j0 + lane] : 0.0;
-#pragma unroll
-      for (int k = 0; k < 6; k++) A[k] = row && k <= lane ? Lp[ro + k] : 0.0;
-      bool good = true;
-#pragma unroll
-      for (int c = 0; c < 6; c++) {
-        const double d = rl64(A[c], c);
-        good = good && d != 0.0;
-        const double rd = d != 0.0 ? 1.0 / d : 0.0;
-        const bool below = row && lane > c;
-        const double l = below ? A[c] * rd : 0.0;
-        const double yc = rl64(y, c);
-        if (below) {
-          y -= l * yc;
-          A[c] = l;
-        }
-        const double ld = l * d;
-#pragma unroll
-        for (int k = c + 1; k < 6; k++) {
-          const double lk = rl64(l, k);
-          if (row && lane >= k) A[k] -= ld * lk;
-        }
-      }
-      if (row) {
-        double dr = A[0];
-#pragma unroll
-        for (int k = 0; k < 6; k++) {
-          if (k < lane) Lp[ro + k] = A[k];
-          if (k == lane) dr = A[k];
-        }
-        dg[j0 + lane] = dr;
-        rhs[j0 + lane] = y;
-      }
-      if (lane == 0 && !good) sh.ok = 0;
-    }
-    __syncthreads();
     if (!sh.ok) return;
     {  // panel rows below the diagonal block
       double Ljj[15], idg[6], yj[6];
@@ -614,31 +621,53 @@ __device__ __forceinline__ void factor_solve(CoopShared& sh, const CoopWs& w, in
       }
     }
     __syncthreads();
-    // trailing update: a wave per group of 4 rows (i, i + kW, i + 2 kW, i + 3 kW), lanes over
-    // the columns k <= i; the rows' independent chains interleave and V_k is read once per group
-    for (int i = j0 + 6 + wid; i < n; i += 4 * kW) {
-      int ro[4];
-      double l[4][6];
+    if (wid == 0) {
+      if (J + 1 < K) {  // block J + 1's lower triangle (21 entries, a lane each), then factor it
+        if (lane < 21) {
+          int r = 0;
+          while ((r + 1) * (r + 2) / 2 <= lane) r++;
+          const int c = lane - r * (r + 1) / 2;
+          const int i = j0 + 6 + r, k = j0 + 6 + c;
+          const int ro = tri(i);
+          double s = Lp[ro + k];
 #pragma unroll
-      for (int a = 0; a < 4; a++) {
-        const int ia = i + a * kW;
-        ro[a] = ia < n ? tri(ia) : 0;
-#pragma unroll
-        for (int c = 0; c < 6; c++) l[a][c] = ia < n ? Lp[ro[a] + j0 + c] : 0.0;
+          for (int m = 0; m < 6; m++) s -= Lp[ro + j0 + m] * V[(size_t)k * 6 + m];
+          Lp[ro + k] = s;
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+        diag_factor(J + 1);
       }
-      const int imax = min(i + 3 * kW, n - 1);
-      for (int k = j0 + 6 + lane; k <= imax; k += 64) {
-        double v[6];
-#pragma unroll
-        for (int c = 0; c < 6; c++) v[c] = V[(size_t)k * 6 + c];
-        double s[4];
-#pragma unroll
-        for (int a = 0; a < 4; a++) s[a] = k <= i + a * kW && i + a * kW < n ? Lp[ro[a] + k] : 0.0;
+    } else {
+      // trailing update of the rows below block J + 1: a wave per group of 4 rows, lanes over
+      // the columns k <= i; the rows' independent chains interleave and V_k is read once per group
+      constexpr int kTW = kW - 1;
+      for (int i = j0 + 12 + (wid - 1); i < n; i += 4 * kTW) {
+        int ro[4];
+        double l[4][6];
 #pragma unroll
         for (int a = 0; a < 4; a++) {
+          const int ia = i + a * kTW;
+          ro[a] = ia < n ? tri(ia) : 0;
 #pragma unroll
-          for (int c = 0; c < 6; c++) s[a] -= l[a][c] * v[c];
-          if (k <= i + a * kW && i + a * kW < n) Lp[ro[a] + k] = s[a];
+          for (int c = 0; c < 6; c++) l[a][c] = ia < n ? Lp[ro[a] + j0 + c] : 0.0;
+        }
+        const int imax = min(i + 3 * kTW, n - 1);
+        for (int k = j0 + 6 + lane; k <= imax; k += 64) {
+          double v[6];
+#pragma unroll
+          for (int c = 0; c < 6; c++) v[c] = V[(size_t)k * 6 + c];
+          double s[4];
+#pragma unroll
+          for (int a = 0; a < 4; a++)
+            s[a] = k <= i + a * kTW && i + a * kTW < n ? Lp[ro[a] + k] : 0.0;
+#pragma unroll
+          for (int a = 0; a < 4; a++) {
+#pragma unroll
+            for (int c = 0; c < 6; c++) s[a] -= l[a][c] * v[c];
+            if (k <= i + a * kTW && i + a * kTW < n) Lp[ro[a] + k] = s[a];
+          }
         }
       }
     }
