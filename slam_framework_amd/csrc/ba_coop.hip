@@ -8,7 +8,7 @@
 //     only its structurally non-zero 6x6 blocks are listed, found per phase by a radix sort of the
 //     (block, point-pair) keys every point contributes (hipcub, stable: each block's pairs stay in
 //     point order, so every sum has a fixed order and the solver is deterministic);
-//   * one problem over G work-groups (16 by default, all resident at once), synchronised by a
+//   * one problem over G work-groups (32 by default, all resident at once), synchronised by a
 //     grid barrier at each data dependency. Per LM iteration: the linearisation (a thread per
 //     point over its edges: errors, Hll, bl, the 6x3 Hpl blocks; a wave per (keyframe, chunk):
 //     partial Hpp, bp) -> barrier; per LM trial: the S blocks (a wave per block over its point
@@ -36,6 +36,9 @@ using namespace ba;
 constexpr int kT = kCoopThreads, kW = kT / 64;
 constexpr int kMaxGrid = 256;  // work-groups of a cooperative launch (<= one per CU)
 constexpr uint32_t kPadKey = 0xFFFFFFFFu;
+#ifndef FS_PROF
+#define FS_PROF 0
+#endif
 constexpr int kChunk = 64;  // S-block pairs per assembly task (one per lane)
 constexpr int kCP = 42;     // per-chunk partials: 36 of the 6x6 block + 6 of the reduced rhs
 
@@ -43,6 +46,7 @@ struct CoopShared {
   double S[kCoopLdsN * (kCoopLdsN + 1) / 2];  // packed lower L of the factorisation
   double rhs[kCoopLdsN];
   double dg[kCoopLdsN];
+  double idg[kCoopLdsN];  // 1 / dg, formed once per pivot by the diagonal factorisation
   double V[kCoopLdsN * 6];
   double red[kW];
   double gpart[4][kMaxGrid];  // per-work-group partials staged for the grid totals
@@ -51,6 +55,8 @@ struct CoopShared {
   int itot;
   float isig[SLAMGPU_MAX_LEVELS];
   int ok;
+  double pacc[8];  // SLAMGPU_BA_PROFILE: work-group 0's per-phase wall time (LDS, not registers)
+  uint64_t pt0;
 };
 
 __device__ __forceinline__ double& ptf(const CoopWs& w, int p, int f) {
@@ -67,13 +73,19 @@ __device__ __forceinline__ void decode_key(uint32_t key, int& kh, int& kl) {
 }
 
 // ---- grid barrier --------------------------------------------------------------------------
-// Arrival counter + generation word in device memory; every thread releases its stores at
-// device scope before and acquires after. Work-group 0 can carry a poll of the caller's stop flag
+// Arrival counter + generation word in device memory. Every wave drains its own stores
+// (vmcnt(0)) before the work-group barrier; then ONE lane per work-group releases at device scope
+// (one write-back of its XCD's L2), arrives with a relaxed add, polls the generation word with
+// relaxed (L1-bypassing) loads, and acquires once for the whole CU (one L1 invalidate, waited
+// for) before the second work-group barrier -- the one-fence-per-work-group form, instead of a
+// release + acquire from every wave. Work-group 0 can carry a poll of the caller's stop flag
 // (system scope: host-mapped memory) into CTL_POLL, which every work-group reads after the
 // barrier -- so all of them take the same decision. A waiter gives up after ~2^22 sleeps and
 // raises CTL_ERR (the host then reports a device error); later barriers do not wait once it is set.
+__device__ __forceinline__ void vm_drain() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+
 __device__ void grid_sync(const CoopWs& w, const int32_t* stop_flag, bool poll) {
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+  vm_drain();  // this wave's stores have reached L2
   __syncthreads();
   if (threadIdx.x == 0) {
     if (poll && blockIdx.x == 0) {
@@ -82,16 +94,20 @@ __device__ void grid_sync(const CoopWs& w, const int32_t* stop_flag, bool poll) 
       __hip_atomic_store(&w.ctl[CTL_POLL], v != 0 ? 1 : 0, __ATOMIC_RELAXED,
                          __HIP_MEMORY_SCOPE_AGENT);
     }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    vm_drain();  // the write-back (and the CTL_POLL store) complete before the arrival
     if (__hip_atomic_load(&w.ctl[CTL_ERR], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) {
       const uint32_t g = __hip_atomic_load(&w.bar[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      vm_drain();  // the generation is read before this work-group can complete the barrier
       const uint32_t a =
-          __hip_atomic_fetch_add(&w.bar[0], 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+          __hip_atomic_fetch_add(&w.bar[0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       if (a == gridDim.x - 1) {
         __hip_atomic_store(&w.bar[0], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(&w.bar[1], g + 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        vm_drain();  // the reset lands before anyone can arrive at the next barrier
+        __hip_atomic_store(&w.bar[1], g + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       } else {
         uint32_t spins = 0;
-        while (__hip_atomic_load(&w.bar[1], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) == g) {
+        while (__hip_atomic_load(&w.bar[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == g) {
           if (spins < 256) __builtin_amdgcn_s_sleep(1);  // short waits: poll fast
           else __builtin_amdgcn_s_sleep(16);             // then back off (~1k cycles)
           if (++spins > (1u << 22)) {
@@ -101,9 +117,10 @@ __device__ void grid_sync(const CoopWs& w, const int32_t* stop_flag, bool poll) 
         }
       }
     }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // invalidates this CU's L1
+    vm_drain();  // ... and waits for it before the other waves are released
   }
   __syncthreads();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
 }
 
 __device__ __forceinline__ int ctl_load(const CoopWs& w, int i) {
@@ -141,17 +158,25 @@ __device__ void grid_totals(CoopShared& sh, const CoopWs& w, int slot0, int ns, 
   __syncthreads();
 }
 
-// A wave that has just stored its partial of a reduction with `total` contributors: releases the
-// stores at device scope and counts itself in at `counter`; returns true (wave-uniform) in the
-// wave that arrived last, which then sees every partial (acquire) and resets the counter.
+// Write-through (sc1) store / L1-bypassing (sc1) load of a hand-off partial: the reduction
+// partials below go from the waves that produce them to the last arriver without any fence.
+__device__ __forceinline__ void st_wt(double* p, double v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ double ld_wt(const double* p) {
+  return __hip_atomic_load(const_cast<double*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// A wave that has just stored its partial of a reduction with `total` contributors (st_wt):
+// drains the stores and counts itself in at `counter` (relaxed add); returns true (wave-uniform)
+// in the wave that arrived last, which then reads every partial with ld_wt and resets the counter.
 __device__ __forceinline__ bool last_arriver(int32_t* counter, int total) {
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+  vm_drain();
   int a = 0;
   if ((threadIdx.x & 63) == 0)
-    a = __hip_atomic_fetch_add(counter, 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+    a = __hip_atomic_fetch_add(counter, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   a = __builtin_amdgcn_readfirstlane(a);
   if (a != total - 1) return false;
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
   if ((threadIdx.x & 63) == 0)
     __hip_atomic_store(counter, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   return true;
@@ -274,6 +299,7 @@ __device__ __forceinline__ double huber_rho(double c2, double d, double& wgt) {
 // edge, Hll and bl summed, the Hpl block of every edge to an optimised keyframe.
 __device__ void lin_points(const CoopWs& w, const CoopProblem& pb, const PoseParams& P,
                            const float* isig, const CoopPhase& ph, double& chi, double& maxd) {
+#pragma clang fp contract(fast)  // tolerance-compared FP64 path
   const int GT = gridDim.x * kT;
   for (int p = blockIdx.x * kT + threadIdx.x; p < pb.n_pts; p += GT) {
     const double X[3] = {ptf(w, p, PX), ptf(w, p, PX + 1), ptf(w, p, PX + 2)};
@@ -318,6 +344,7 @@ __device__ void lin_points(const CoopWs& w, const CoopProblem& pb, const PosePar
 // Hpp (packed upper) and bp.
 __device__ void lin_keyframes(const CoopWs& w, const CoopProblem& pb, const PoseParams& P,
                               const float* isig, const CoopPhase& ph) {
+#pragma clang fp contract(fast)  // tolerance-compared FP64 path
   const int lane = threadIdx.x & 63;
   const int nw = gridDim.x * kW, tasks = pb.K * w.nch;
   for (int t = blockIdx.x * kW + (threadIdx.x >> 6); t < tasks; t += nw) {
@@ -352,12 +379,12 @@ __device__ void lin_keyframes(const CoopWs& w, const CoopProblem& pb, const Pose
       }
     }
     const double s = wave_reduce_scatter32(acc);
-    if ((lane & 1) == 0 && (lane >> 1) < 27) w.hpp_part[((size_t)f * w.nch + c) * 27 + (lane >> 1)] = s;
+    if ((lane & 1) == 0 && (lane >> 1) < 27) st_wt(&w.hpp_part[((size_t)f * w.nch + c) * 27 + (lane >> 1)], s);
     if (last_arriver(&w.kf_arrive[f], w.nch) && lane < 27) {  // Hpp / bp totals, chunk order
       const double* pp = w.hpp_part + (size_t)f * w.nch * 27 + lane;
       double v[8];
 #pragma unroll
-      for (int k = 0; k < 8; k++) v[k] = k < w.nch ? pp[(size_t)k * 27] : 0.0;
+      for (int k = 0; k < 8; k++) v[k] = k < w.nch ? ld_wt(pp + (size_t)k * 27) : 0.0;
       double t = v[0];
 #pragma unroll
       for (int k = 1; k < 8; k++) t = k < w.nch ? t + v[k] : t;
@@ -386,6 +413,7 @@ __device__ __forceinline__ void dinv_point(const CoopWs& w, int p, double lambda
 // point's Dinv = (Hll + lambda I)^-1 formed on the fly. Work-group 0 adds a block's chunk
 // partials in chunk order when it builds S (build_S), so every sum has a fixed order.
 __device__ void assemble(const CoopWs& w, int K, double lambda, int n_chunks) {
+#pragma clang fp contract(fast)  // tolerance-compared FP64 path
   const int lane = threadIdx.x & 63;
   const int nw = gridDim.x * kW;
   for (int ch = blockIdx.x * kW + (threadIdx.x >> 6); ch < n_chunks; ch += nw) {
@@ -449,8 +477,8 @@ __device__ void assemble(const CoopWs& w, int K, double lambda, int n_chunks) {
       const double sv = wave_reduce_scatter32(acc);
       // partial layout: [0, 36) the block row-major, [36, 42) the rhs terms
       if ((lane & 1) == 0) {
-        if (id < 18) out[18 * half + id] = sv;
-        else if (half == 0 && id < 24) out[36 + id - 18] = sv;
+        if (id < 18) st_wt(&out[18 * half + id], sv);
+        else if (half == 0 && id < 24) st_wt(&out[36 + id - 18], sv);
       }
     }
     // the run's last chunk to finish sums the run's chunk partials in chunk order and writes
@@ -464,11 +492,11 @@ __device__ void assemble(const CoopWs& w, int K, double lambda, int n_chunks) {
     double sv = 0.0;
     int k = 0;
     for (; k + 4 <= nch; k += 4) {  // four loads in flight per step
-      const double a0 = pp[(size_t)k * kCP], a1 = pp[(size_t)(k + 1) * kCP];
-      const double a2 = pp[(size_t)(k + 2) * kCP], a3 = pp[(size_t)(k + 3) * kCP];
+      const double a0 = ld_wt(pp + (size_t)k * kCP), a1 = ld_wt(pp + (size_t)(k + 1) * kCP);
+      const double a2 = ld_wt(pp + (size_t)(k + 2) * kCP), a3 = ld_wt(pp + (size_t)(k + 3) * kCP);
       sv = (((sv + a0) + a1) + a2) + a3;
     }
-    for (; k < nch; k++) sv += pp[(size_t)k * kCP];
+    for (; k < nch; k++) sv += ld_wt(pp + (size_t)k * kCP);
     const int n = 6 * K;
     if (lane < 36) {
       double base = 0.0;
@@ -533,48 +561,64 @@ __device__ __forceinline__ double rl64(double x, int l) {  // v_readlane of a do
 // previous step, which g2o applies anyway: optimization_algorithm_levenberg.cpp:107-109).
 template <typename PtrT>
 __device__ __forceinline__ void factor_solve(CoopShared& sh, const CoopWs& w, int K, PtrT Lp,
-                                             PtrT rhs, PtrT dg, PtrT V) {
+                                             PtrT rhs, PtrT dg, PtrT idg, PtrT V) {
+#pragma clang fp contract(fast)  // tolerance-compared FP64 path
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, n = 6 * K;
   if (tid == 0) sh.ok = 1;
-  // the diagonal block J by wave 0: lane r < 6 holds row r; pivots and multipliers by readlane
+#if FS_PROF  // diagnostic build: thread 0's split of the factorisation into prof[8..13]
+  uint64_t fs_t = __builtin_amdgcn_s_memrealtime();
+  auto fs_tick = [&](int slot) {
+    if (w.prof && tid == 0) {
+      const uint64_t t = __builtin_amdgcn_s_memrealtime();
+      w.prof[slot] += 0.01 * (double)(t - fs_t);
+      fs_t = t;
+    }
+  };
+  if (w.prof && tid == 0) w.prof[13] += 1.0;
+#else
+  auto fs_tick = [](int) {};
+#endif
+  // the diagonal block J by one lane (lane 0 of wave 0): its 21 entries and 6 rhs values in
+  // registers, no cross-lane traffic on the pivot chain
   auto diag_factor = [&](int J) {
+    if (lane != 0) return;
     const int j0 = 6 * J;
-    const bool row = lane < 6;
-    const int ro = tri(j0 + (row ? lane : 0)) + j0;
-    double A[6], y = row ? rhs[j0 + lane] : 0.0;
+    double A[21], y[6];
 #pragma unroll
-    for (int k = 0; k < 6; k++) A[k] = row && k <= lane ? Lp[ro + k] : 0.0;
+    for (int r = 0; r < 6; r++) {
+      y[r] = rhs[j0 + r];
+#pragma unroll
+      for (int k = 0; k <= r; k++) A[r * (r + 1) / 2 + k] = Lp[tri(j0 + r) + j0 + k];
+    }
     bool good = true;
 #pragma unroll
     for (int c = 0; c < 6; c++) {
-      const double d = rl64(A[c], c);
+      const double d = A[c * (c + 3) / 2];
       good = good && d != 0.0;
       const double rd = d != 0.0 ? 1.0 / d : 0.0;
-      const bool below = row && lane > c;
-      const double l = below ? A[c] * rd : 0.0;
-      const double yc = rl64(y, c);
-      if (below) {
-        y -= l * yc;
-        A[c] = l;
-      }
-      const double ld = l * d;
+      idg[j0 + c] = rd;
+      double l[6];
 #pragma unroll
-      for (int k = c + 1; k < 6; k++) {
-        const double lk = rl64(l, k);
-        if (row && lane >= k) A[k] -= ld * lk;
+      for (int r = c + 1; r < 6; r++) {
+        l[r] = A[r * (r + 1) / 2 + c] * rd;
+        y[r] -= l[r] * y[c];
+        A[r * (r + 1) / 2 + c] = l[r];
+      }
+#pragma unroll
+      for (int r = c + 1; r < 6; r++) {
+        const double ld = l[r] * d;
+#pragma unroll
+        for (int k = c + 1; k <= r; k++) A[r * (r + 1) / 2 + k] -= ld * l[k];
       }
     }
-    if (row) {
-      double dr = A[0];
 #pragma unroll
-      for (int k = 0; k < 6; k++) {
-        if (k < lane) Lp[ro + k] = A[k];
-        if (k == lane) dr = A[k];
-      }
-      dg[j0 + lane] = dr;
-      rhs[j0 + lane] = y;
+    for (int r = 0; r < 6; r++) {
+#pragma unroll
+      for (int k = 0; k < r; k++) Lp[tri(j0 + r) + j0 + k] = A[r * (r + 1) / 2 + k];
+      dg[j0 + r] = A[r * (r + 3) / 2];
+      rhs[j0 + r] = y[r];
     }
-    if (lane == 0 && !good) sh.ok = 0;
+    if (!good) sh.ok = 0;
   };
   __syncthreads();
   if (wid == 0) diag_factor(0);
@@ -587,7 +631,7 @@ __device__ __forceinline__ void factor_solve(CoopShared& sh, const CoopWs& w, in
     const int j0 = 6 * J;
     if (!sh.ok) return;
     {  // panel rows below the diagonal block
-      double Ljj[15], idg[6], yj[6];
+      double Ljj[15], rdg[6], yj[6];
       int q = 0;
 #pragma unroll
       for (int c = 1; c < 6; c++)
@@ -595,7 +639,7 @@ __device__ __forceinline__ void factor_solve(CoopShared& sh, const CoopWs& w, in
         for (int k = 0; k < c; k++) Ljj[q++] = Lp[tri(j0 + c) + j0 + k];
 #pragma unroll
       for (int c = 0; c < 6; c++) {
-        idg[c] = 1.0 / dg[j0 + c];
+        rdg[c] = idg[j0 + c];
         yj[c] = rhs[j0 + c];
       }
       for (int i = j0 + 6 + tid; i < n; i += kT) {
@@ -613,14 +657,16 @@ __device__ __forceinline__ void factor_solve(CoopShared& sh, const CoopWs& w, in
 #pragma unroll
         for (int c = 0; c < 6; c++) {
           V[(size_t)i * 6 + c] = v[c];
-          const double l = v[c] * idg[c];
+          const double l = v[c] * rdg[c];
           Lp[ro + c] = l;
           r -= l * yj[c];
         }
         rhs[i] = r;
       }
     }
+    fs_tick(8);
     __syncthreads();
+    fs_tick(9);
     if (wid == 0) {
       if (J + 1 < K) {  // block J + 1's lower triangle (21 entries, a lane each), then factor it
         if (lane < 21) {
@@ -644,14 +690,14 @@ __device__ __forceinline__ void factor_solve(CoopShared& sh, const CoopWs& w, in
       // the columns k <= i; the rows' independent chains interleave and V_k is read once per group
       constexpr int kTW = kW - 1;
       for (int i = j0 + 12 + (wid - 1); i < n; i += 4 * kTW) {
-        int ro[4];
+        int ro[4], ic[4];
         double l[4][6];
 #pragma unroll
-        for (int a = 0; a < 4; a++) {
-          const int ia = i + a * kTW;
-          ro[a] = ia < n ? tri(ia) : 0;
+        for (int a = 0; a < 4; a++) {  // rows past n alias row n - 1: loads stay unconditional
+          ic[a] = min(i + a * kTW, n - 1);
+          ro[a] = tri(ic[a]);
 #pragma unroll
-          for (int c = 0; c < 6; c++) l[a][c] = ia < n ? Lp[ro[a] + j0 + c] : 0.0;
+          for (int c = 0; c < 6; c++) l[a][c] = Lp[ro[a] + j0 + c];
         }
         const int imax = min(i + 3 * kTW, n - 1);
         for (int k = j0 + 6 + lane; k <= imax; k += 64) {
@@ -660,8 +706,7 @@ __device__ __forceinline__ void factor_solve(CoopShared& sh, const CoopWs& w, in
           for (int c = 0; c < 6; c++) v[c] = V[(size_t)k * 6 + c];
           double s[4];
 #pragma unroll
-          for (int a = 0; a < 4; a++)
-            s[a] = k <= i + a * kTW && i + a * kTW < n ? Lp[ro[a] + k] : 0.0;
+          for (int a = 0; a < 4; a++) s[a] = Lp[ro[a] + min(k, ic[a])];
 #pragma unroll
           for (int a = 0; a < 4; a++) {
 #pragma unroll
@@ -671,7 +716,9 @@ __device__ __forceinline__ void factor_solve(CoopShared& sh, const CoopWs& w, in
         }
       }
     }
+    fs_tick(10);
     __syncthreads();
+    fs_tick(11);
   }
   if (wid == 0) {  // z = D^-1 y; L^T x = z from the last 6x6 block up
     for (int i = lane; i < n; i += 64) rhs[i] /= dg[i];
@@ -680,17 +727,26 @@ __device__ __forceinline__ void factor_solve(CoopShared& sh, const CoopWs& w, in
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-      // within the block: lane r < 6 holds x_r; x_c final when c is reached (descending)
-      double xv = lane < 6 ? rhs[j0 + lane] : 0.0;
+      // within the block, by lane 0 in registers (x_c final when c is reached, descending);
+      // the 6 values then go to every lane by v_readlane
+      double x[6] = {0, 0, 0, 0, 0, 0};
+      if (lane == 0) {
+        double Lb[15];
 #pragma unroll
-      for (int c = 5; c >= 0; c--) {
-        const double xc = rl64(xv, c);
-        if (lane < c) xv -= Lp[tri(j0 + c) + j0 + lane] * xc;
+        for (int c = 1; c < 6; c++)
+#pragma unroll
+          for (int r = 0; r < c; r++) Lb[c * (c - 1) / 2 + r] = Lp[tri(j0 + c) + j0 + r];
+#pragma unroll
+        for (int r = 0; r < 6; r++) x[r] = rhs[j0 + r];
+#pragma unroll
+        for (int c = 5; c >= 0; c--)
+#pragma unroll
+          for (int r = 0; r < c; r++) x[r] -= Lb[c * (c - 1) / 2 + r] * x[c];
+#pragma unroll
+        for (int r = 0; r < 6; r++) rhs[j0 + r] = x[r];
       }
-      if (lane < 6) rhs[j0 + lane] = xv;
-      double x[6];
 #pragma unroll
-      for (int c = 0; c < 6; c++) x[c] = rl64(xv, c);
+      for (int c = 0; c < 6; c++) x[c] = rl64(x[c], 0);
       for (int i = lane; i < j0; i += 64) {  // earlier rows: z_i -= sum_c L(j0 + c, i) x_c
         double sx = rhs[i];
 #pragma unroll
@@ -704,6 +760,7 @@ __device__ __forceinline__ void factor_solve(CoopShared& sh, const CoopWs& w, in
     for (int i = lane; i < n; i += 64) w.xp[i] = rhs[i];
   }
   __syncthreads();
+  fs_tick(12);
 }
 
 // optimizer.cpp:632-665 between the two optimize() calls: chi2 > threshold or depth <= 0 ->
@@ -819,14 +876,15 @@ __global__ __launch_bounds__(kT) void ba_coop_kernel(PoseParams P, CoopProblem p
   double* const Gv = Gp + (size_t)n * (n + 1) / 2;
   double* const Gd = Gv + (size_t)6 * n;
   double* const Gr = Gd + n;
+  double* const Gi = Gr + n;
   // optional per-phase wall clock of work-group 0 (s_memrealtime: 100 MHz)
-  double pacc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  uint64_t pt0 = __builtin_amdgcn_s_memrealtime();
-  auto tick = [&](int slot) {
-    if (w.prof && wg == 0) {
+  if (tid < 8) sh.pacc[tid] = 0.0;
+  if (tid == 0) sh.pt0 = __builtin_amdgcn_s_memrealtime();
+  auto tick = [&](int slot) {  // thread 0 of work-group 0 only: no registers held across phases
+    if (w.prof && wg == 0 && tid == 0) {
       const uint64_t t = __builtin_amdgcn_s_memrealtime();
-      pacc[slot] += 0.01 * (double)(t - pt0);
-      pt0 = t;
+      sh.pacc[slot] += 0.01 * (double)(t - sh.pt0);
+      sh.pt0 = t;
     }
   };
   int lm_total = 0;
@@ -906,11 +964,12 @@ __global__ __launch_bounds__(kT) void ba_coop_kernel(PoseParams P, CoopProblem p
         if (in_lds) {
           build_S(w, K, lambda, (LdsPtr)sh.S, (LdsPtr)sh.rhs);
           tick(5);
-          factor_solve(sh, w, K, (LdsPtr)sh.S, (LdsPtr)sh.rhs, (LdsPtr)sh.dg, (LdsPtr)sh.V);
+          factor_solve(sh, w, K, (LdsPtr)sh.S, (LdsPtr)sh.rhs, (LdsPtr)sh.dg, (LdsPtr)sh.idg,
+                       (LdsPtr)sh.V);
         } else {
           build_S(w, K, lambda, Gp, Gr);
           tick(5);
-          factor_solve(sh, w, K, Gp, Gr, Gd, Gv);
+          factor_solve(sh, w, K, Gp, Gr, Gd, Gi, Gv);
         }
         tick(6);
         double sc = 0.0;
@@ -1022,7 +1081,7 @@ __global__ __launch_bounds__(kT) void ba_coop_kernel(PoseParams P, CoopProblem p
   if (stopped) break;
   }  // phases
   if (w.prof && wg == 0 && tid == 0)
-    for (int i = 0; i < 8; i++) w.prof[i] += pacc[i];
+    for (int i = 0; i < 8; i++) w.prof[i] += sh.pacc[i];
   if (wg == 0 && tid == 0) {
     w.ctl[CTL_LM] += lm_total;
     if (stopped) w.ctl[CTL_STOPPED] = 1;
@@ -1127,7 +1186,7 @@ CoopWs coop_layout(void* base, int n_kf, int n_pts, int n_obs, int K, int pairs_
   w.S = reinterpret_cast<double*>(take(8 * (size_t)n * n + 8));
   w.bs = reinterpret_cast<double*>(take(8 * (size_t)n + 8));
   w.fac = reinterpret_cast<double*>(
-      take(n > kCoopLdsN ? 8 * ((size_t)n * (n + 1) / 2 + 8 * (size_t)n) : 8));
+      take(n > kCoopLdsN ? 8 * ((size_t)n * (n + 1) / 2 + 9 * (size_t)n) : 8));
   w.xp = reinterpret_cast<double*>(take(8 * (size_t)n + 8));
   w.part = reinterpret_cast<double*>(take(8 * 8 * (size_t)(G + 1)));
   w.bar = reinterpret_cast<uint32_t*>(take(64));

@@ -1,6 +1,7 @@
 """Wall-clock latency of the single-problem drop-in calls (slamgpu_local_bundle_adjustment on
 SURVEY 8(d) C5 and larger windows, slamgpu_global_bundle_adjustment), host buffers in and out,
-as the LocalMapper / LoopCloser would call them. Usage: python tools/ba_latency.py [reps]"""
+as the LocalMapper / LoopCloser would call them.
+Usage: python tools/ba_latency.py [reps] [--ba-only] [--oracle]"""
 import json
 import sys
 import time
@@ -43,6 +44,9 @@ for nkf, npt in [(30, 4000), (100, 12000)]:
     out[key] = {"median_ms": round(med, 3), "min_ms": round(mn, 3), "lm_iterations": r[2],
                 "keyframes": nkf, "points": npt, "observations": int(len(P["obs"]))}
     print(key, out[key], flush=True)
+if "--ba-only" in sys.argv:
+    print(json.dumps(out))
+    sys.exit(0)
 # OptimizeSim3: one loop candidate (SIM3 matches of a keyframe pair), and a batch of 8
 isig = S.level_inv_sigma2()
 for n in (300, 1000):
