@@ -34,6 +34,7 @@ struct EgGraph {
   // column extents of the factorisation: rows i > k with start[i] <= k, increasing
   const int32_t* ext_ptr;      // [F + 1]
   const int32_t* ext_rows;
+  const int64_t* ext_base;     // per extent entry: off[row] - start[row] (block (row, j) at + j)
 };
 
 // Mutable device state of one call.

@@ -179,173 +179,226 @@ __global__ __launch_bounds__(64) void eg_assemble_kernel(EgGraph G, EgState W) {
   else W.H[(int64_t)blk * 49 + lane] = s;
 }
 
-constexpr int kFacThreads = 256;
+#ifndef EG_EXACT_ROUNDING  // 1: the round-1 kernel's operation order, bit for bit
+#define EG_EXACT_ROUNDING 1
+#endif
+constexpr int kFacThreads = 1024;
 
-// In-register LDLT of a 7x7 block (lower triangle + diagonal of A, row-major): L below the
-// diagonal, D on it. Returns false on a zero pivot.
-__device__ __forceinline__ bool ldlt7_inplace(double* A) {
-  double a[7][7];
-#pragma unroll
-  for (int r = 0; r < 7; r++)
-#pragma unroll
-    for (int c = 0; c <= r; c++) a[r][c] = A[7 * r + c];
-  bool ok = true;
-#pragma unroll
-  for (int j = 0; j < 7; j++) {
-    double d = a[j][j];
-#pragma unroll
-    for (int m = 0; m < j; m++) d -= a[j][m] * a[j][m] * a[m][m];
-    a[j][j] = d;
-    ok = ok && d != 0.0;
-#pragma unroll
-    for (int i = j + 1; i < 7; i++) {
-      double t = a[i][j];
-#pragma unroll
-      for (int m = 0; m < j; m++) t -= a[i][m] * a[j][m] * a[m][m];
-      a[i][j] = t / d;
-    }
-  }
-#pragma unroll
-  for (int r = 0; r < 7; r++)
-#pragma unroll
-    for (int c = 0; c <= r; c++) A[7 * r + c] = a[r][c];
-  return ok;
-}
-
+// The LDLT of H + lambda I (profile storage, vertex order) and the solve, by one work-group of
+// 16 waves. Right-looking by 7x7 block column k with a look-ahead: the panel (a thread per row of
+// each extent block: L_ik = A_ik L_kk^-T D_k^-1, fused with the forward solve y_i -= L_ik y_k)
+// -> barrier -> waves 1-15 apply the trailing update A_ij -= L_ik D_k L_jk' over the column's
+// extent while wave 0 applies it to the next diagonal block and lane 0 factors that block in
+// registers (pivot reciprocals, in-block forward solve) -> barrier: two barriers per column,
+// the diagonal chain off the critical path. Block (i, j) of an extent row lives at
+// ext_base[e] + j (ext_base = off[i] - start[i], precomputed on the host: one dependent load).
+// Then z = D^-1 y and the backward solve by wave 0 alone (lanes 0-6 sum a column's extent, lane 0
+// solves the block; no work-group barriers), and g2o's scale term. EG_EXACT_ROUNDING (default)
+// keeps the previous kernel's operation order (divisions, no contraction, the same sums), so the
+// results are bit-identical to it; the LM stop test of this ill-conditioned system amplifies
+// last-bit differences into different iteration counts.
 __global__ __launch_bounds__(kFacThreads) void eg_factor_solve_kernel(EgGraph G, EgState W,
                                                                       int64_t n_blocks,
                                                                       double lambda) {
+#if !EG_EXACT_ROUNDING
+#pragma clang fp contract(fast)  // tolerance-compared FP64 path
+#endif
   __shared__ int s_ok;
   __shared__ double red[256];
-  __shared__ double s_kk[49];  // the current diagonal block (L below, D on the diagonal)
-  const int tid = threadIdx.x, F = G.F;
-  double* L = W.L;
-  for (int64_t q = tid; q < n_blocks * 49; q += kFacThreads) L[q] = W.H[q];
+  __shared__ double s_kk[2][49];  // factored diagonal block of this / the next column
+  __shared__ double s_rd[2][7];   // its pivot reciprocals
+  __shared__ double s_y[2][7];    // its forward-solved rhs slice
+  __shared__ double s_nx[49];     // the next diagonal block after its last update
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, F = G.F;
+  double* L = W.L;  // a copy of H (launch_eg_factor_solve)
+  double* y = W.y;
+  for (int q = tid; q < 7 * F; q += kFacThreads) {
+    const int v = q / 7, r = q % 7;
+    L[(G.off[v] + (v - G.start[v])) * 49 + 8 * r] += lambda;  // setLambda: H + lambda I
+    y[q] = W.b[q];
+  }
   if (tid == 0) s_ok = 1;
   __syncthreads();
-  for (int f = tid; f < 7 * F; f += kFacThreads) {
-    const int v = f / 7, r = f % 7;
-    L[(G.off[v] + (v - G.start[v])) * 49 + 8 * r] += lambda;  // setLambda: H + lambda I
-  }
+  auto diag_of = [&](int k) { return L + (G.off[k] + (k - G.start[k])) * 49; };
+  // lane 0: LDLT of diagonal block k from src (lower triangle + diagonal), the forward solve of
+  // y_k; L_kk / D_k to the profile and to s_kk[buf], 1 / D_k to s_rd[buf], y_k to s_y[buf]
+  auto diag_factor = [&](int k, const double* src, int buf) {
+    double a[7][7];
+#pragma unroll
+    for (int r = 0; r < 7; r++)
+#pragma unroll
+      for (int c = 0; c <= r; c++) a[r][c] = src[7 * r + c];
+    bool ok = true;
+    double rd[7];
+#pragma unroll
+    for (int j = 0; j < 7; j++) {
+      double d = a[j][j];
+#pragma unroll
+      for (int m = 0; m < j; m++) d -= a[j][m] * a[j][m] * a[m][m];
+      a[j][j] = d;
+      ok = ok && d != 0.0;
+      rd[j] = 1.0 / d;
+#pragma unroll
+      for (int i = j + 1; i < 7; i++) {
+        double t = a[i][j];
+#pragma unroll
+        for (int m = 0; m < j; m++) t -= a[i][m] * a[j][m] * a[m][m];
+#if EG_EXACT_ROUNDING
+        a[i][j] = t / d;
+#else
+        a[i][j] = t * rd[j];
+#endif
+      }
+    }
+    double v[7];
+#pragma unroll
+    for (int r = 0; r < 7; r++) v[r] = y[7 * k + r];
+#pragma unroll
+    for (int r = 1; r < 7; r++)
+#pragma unroll
+      for (int m = 0; m < r; m++) v[r] -= a[r][m] * v[m];
+    double* Akk = diag_of(k);
+#pragma unroll
+    for (int r = 0; r < 7; r++) {
+#pragma unroll
+      for (int c = 0; c <= r; c++) {
+        Akk[7 * r + c] = a[r][c];
+        s_kk[buf][7 * r + c] = a[r][c];
+      }
+      s_rd[buf][r] = rd[r];
+      s_y[buf][r] = v[r];
+      y[7 * k + r] = v[r];
+    }
+    if (!ok) s_ok = 0;
+  };
+  if (F > 0 && tid == 0) diag_factor(0, diag_of(0), 0);
   __syncthreads();
-  auto blkp = [&](int i, int j) { return L + (G.off[i] + (j - G.start[i])) * 49; };
-  // ---- factorisation, right-looking by block column ----
+  // ---- factorisation + forward solve ----
   for (int k = 0; k < F; k++) {
-    double* Akk = blkp(k, k);
-    if (tid < 49) s_kk[tid] = Akk[tid];
-    __syncthreads();
-    if (tid == 0 && !ldlt7_inplace(s_kk)) s_ok = 0;  // the diagonal block
-    __syncthreads();
-    if (tid < 49) Akk[tid] = s_kk[tid];
+    const int cur = k & 1;
     const int e0 = G.ext_ptr[k], ne = G.ext_ptr[k + 1] - e0;
-    for (int q = tid; q < 7 * ne; q += kFacThreads) {  // panel: L_ik = A_ik L_kk^-T D_k^-1
-      const int i = G.ext_rows[e0 + q / 7], r = q % 7;
-      double* Aik = blkp(i, k) + 7 * r;
+    for (int q = tid; q < 7 * ne; q += kFacThreads) {  // panel rows
+      const int t = q / 7, r = q % 7;
+      double* Aik = L + (G.ext_base[e0 + t] + k) * 49 + 7 * r;
       double a[7];
 #pragma unroll
       for (int c = 0; c < 7; c++) a[c] = Aik[c];
 #pragma unroll
       for (int c = 0; c < 7; c++) {
-        double t = a[c];
+        double t2 = a[c];
 #pragma unroll
-        for (int m = 0; m < c; m++) t -= a[m] * s_kk[8 * m] * s_kk[7 * c + m];
-        a[c] = t / s_kk[8 * c];
+        for (int m = 0; m < c; m++) t2 -= a[m] * s_kk[cur][8 * m] * s_kk[cur][7 * c + m];
+#if EG_EXACT_ROUNDING
+        a[c] = t2 / s_kk[cur][8 * c];
+#else
+        a[c] = t2 * s_rd[cur][c];
+#endif
       }
+      double sy = 0.0;
 #pragma unroll
-      for (int c = 0; c < 7; c++) Aik[c] = a[c];
-    }
-    __syncthreads();
-    const int npairs = ne * (ne + 1) / 2;
-    for (int q = tid; q < npairs * 49; q += kFacThreads) {  // trailing: A_ij -= L_ik D_k L_jk'
-      const int pair = q / 49, ent = q % 49;
-      int ti = (int)((sqrtf(8.0f * (float)pair + 1.0f) - 1.0f) * 0.5f);
-      while ((ti + 1) * (ti + 2) / 2 <= pair) ti++;
-      while (ti * (ti + 1) / 2 > pair) ti--;
-      const int tj = pair - ti * (ti + 1) / 2;
-      const int i = G.ext_rows[e0 + ti], j = G.ext_rows[e0 + tj];
-      const int r = ent / 7, c = ent % 7;
-      const double* Lik = blkp(i, k) + 7 * r;
-      const double* Ljk = blkp(j, k) + 7 * c;
-      double t = 0.0;
-#pragma unroll
-      for (int m = 0; m < 7; m++) t += Lik[m] * s_kk[8 * m] * Ljk[m];
-      blkp(i, j)[ent] -= t;
-    }
-    __syncthreads();
-  }
-  // ---- solve L D L' y = b ----
-  double* y = W.y;
-  for (int q = tid; q < 7 * F; q += kFacThreads) y[q] = W.b[q];
-  __syncthreads();
-  for (int k = 0; k < F; k++) {
-    const double* Lkk = blkp(k, k);
-    if (tid == 0) {
-      double v[7];
-#pragma unroll
-      for (int r = 0; r < 7; r++) v[r] = y[7 * k + r];
-#pragma unroll
-      for (int r = 1; r < 7; r++)
-#pragma unroll
-        for (int m = 0; m < r; m++) v[r] -= Lkk[7 * r + m] * v[m];
-#pragma unroll
-      for (int r = 1; r < 7; r++) y[7 * k + r] = v[r];
-    }
-    __syncthreads();
-    const int e0 = G.ext_ptr[k], ne = G.ext_ptr[k + 1] - e0;
-    for (int q = tid; q < 7 * ne; q += kFacThreads) {
-      const int i = G.ext_rows[e0 + q / 7], r = q % 7;
-      const double* Lik = blkp(i, k) + 7 * r;
-      double s = 0.0;
-      for (int m = 0; m < 7; m++) s += Lik[m] * y[7 * k + m];
-      y[7 * i + r] -= s;
-    }
-    __syncthreads();
-  }
-  for (int q = tid; q < 7 * F; q += kFacThreads) y[q] /= blkp(q / 7, q / 7)[8 * (q % 7)];
-  __syncthreads();
-  for (int k = F - 1; k >= 0; k--) {
-    const int e0 = G.ext_ptr[k], ne = G.ext_ptr[k + 1] - e0;
-    if (tid < 7) {  // y_k -= sum over the later rows i of L_ik' x_i
-      double s = 0.0;
-      for (int t = 0; t < ne; t++) {
-        const int i = G.ext_rows[e0 + t];
-        const double* Lik = blkp(i, k);
-        for (int r = 0; r < 7; r++) s += Lik[7 * r + tid] * y[7 * i + r];
+      for (int c = 0; c < 7; c++) {
+        Aik[c] = a[c];
+        sy += a[c] * s_y[cur][c];
       }
-      y[7 * k + tid] -= s;
+      y[7 * G.ext_rows[e0 + t] + r] -= sy;
     }
     __syncthreads();
-    if (tid == 0) {
-      const double* Lkk = blkp(k, k);
-      double v[7];
+    const bool nxt_in = k + 1 < F && ne > 0 && G.ext_rows[e0] == k + 1;
+    if (wid == 0) {
+      if (k + 1 < F) {  // the next diagonal block: its last update, then its factorisation
+        if (lane < 49) {
+          const double* An = diag_of(k + 1);
+          double v = An[lane];
+          if (nxt_in) {
+            const int r = lane / 7, c = lane % 7;
+            const double* Ln = L + (G.ext_base[e0] + k) * 49;  // block (k + 1, k)
+            double t = 0.0;
 #pragma unroll
-      for (int r = 0; r < 7; r++) v[r] = y[7 * k + r];
+            for (int m = 0; m < 7; m++) t += Ln[7 * r + m] * s_kk[cur][8 * m] * Ln[7 * c + m];
+            v -= t;
+          }
+          s_nx[lane] = v;
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+        if (lane == 0) diag_factor(k + 1, s_nx, cur ^ 1);
+      }
+    } else {  // trailing update of the rest of the extent (pair 0 is block (k+1, k+1) if nxt_in)
+      const int npairs = ne * (ne + 1) / 2;
+      for (int q = tid - 64 + (nxt_in ? 49 : 0); q < npairs * 49; q += kFacThreads - 64) {
+        const int pair = q / 49, ent = q % 49;
+        int ti = (int)((sqrtf(8.0f * (float)pair + 1.0f) - 1.0f) * 0.5f);
+        while ((ti + 1) * (ti + 2) / 2 <= pair) ti++;
+        while (ti * (ti + 1) / 2 > pair) ti--;
+        const int tj = pair - ti * (ti + 1) / 2;
+        const int j = G.ext_rows[e0 + tj];
+        const int64_t bi = G.ext_base[e0 + ti], bj = G.ext_base[e0 + tj];
+        const int r = ent / 7, c = ent % 7;
+        const double* Lik = L + (bi + k) * 49 + 7 * r;
+        const double* Ljk = L + (bj + k) * 49 + 7 * c;
+        double t = 0.0;
 #pragma unroll
-      for (int r = 5; r >= 0; r--)
-#pragma unroll
-        for (int m = r + 1; m < 7; m++) v[r] -= Lkk[7 * m + r] * v[m];
-#pragma unroll
-      for (int r = 0; r < 6; r++) y[7 * k + r] = v[r];
+        for (int m = 0; m < 7; m++) t += Lik[m] * s_kk[cur][8 * m] * Ljk[m];
+        L[(bi + j) * 49 + ent] -= t;
+      }
     }
     __syncthreads();
   }
+  // ---- z = D^-1 y, then L' x = z by wave 0 (column k: x_k = L_kk^-T (z_k - sum L_ik' x_i)) ----
+  for (int q = tid; q < 7 * F; q += kFacThreads) y[q] /= diag_of(q / 7)[8 * (q % 7)];
+  __syncthreads();
+  if (wid == 0) {
+    for (int k = F - 1; k >= 0; k--) {
+      const int e0 = G.ext_ptr[k], ne = G.ext_ptr[k + 1] - e0;
+      if (lane < 7) {  // y_k -= sum over the later rows i of L_ik' x_i (lane c: component c)
+        double acc = 0.0;
+        for (int t = 0; t < ne; t++) {
+          const double* Lik = L + (G.ext_base[e0 + t] + k) * 49;
+          const double* xi = y + 7 * G.ext_rows[e0 + t];
+#pragma unroll
+          for (int r = 0; r < 7; r++) acc += Lik[7 * r + lane] * xi[r];
+        }
+        y[7 * k + lane] -= acc;
+      }
+      __builtin_amdgcn_s_waitcnt(0);  // the stores land before lane 0 reads them
+      __builtin_amdgcn_wave_barrier();
+      if (lane == 0) {
+        const double* Lkk = diag_of(k);
+        double v[7];
+#pragma unroll
+        for (int r = 0; r < 7; r++) v[r] = y[7 * k + r];
+#pragma unroll
+        for (int r = 5; r >= 0; r--)
+#pragma unroll
+          for (int m = r + 1; m < 7; m++) v[r] -= Lkk[7 * m + r] * v[m];
+#pragma unroll
+        for (int r = 0; r < 6; r++) y[7 * k + r] = v[r];
+      }
+      __builtin_amdgcn_s_waitcnt(0);
+      __builtin_amdgcn_wave_barrier();
+    }
+  }
+  __syncthreads();
   // LinearSolverEigen: a failed factorisation leaves x as it was; the vertex oplus zeroes the
   // scale coordinate of the solver's x when the scale is fixed
   const bool ok = s_ok != 0;
   if (ok)
     for (int q = tid; q < 7 * F; q += kFacThreads) W.x[q] = (G.fix_scale && q % 7 == 6) ? 0.0 : y[q];
   __syncthreads();
-  // computeScale: sum x (lambda x + b)
-  double s = 0.0;
-  for (int q = tid; q < 7 * F; q += 256) s += W.x[q] * (lambda * W.x[q] + W.b[q]);
-  red[tid] = s;
+  // computeScale: sum x (lambda x + b): 256 strided partials, then a fixed tree
+  double sc = 0.0;
+  if (tid < 256)
+    for (int q = tid; q < 7 * F; q += 256) sc += W.x[q] * (lambda * W.x[q] + W.b[q]);
+  if (tid < 256) red[tid] = sc;
   __syncthreads();
   for (int h = 128; h >= 1; h >>= 1) {
     if (tid < h) red[tid] += red[tid + h];
     __syncthreads();
   }
   if (tid == 0) {
-    W.out[1] = red[0];
+    const double t = red[0];
+    W.out[1] = t;
     W.out[2] = ok ? 1.0 : 0.0;
   }
 }
@@ -435,6 +488,9 @@ hipError_t launch_eg_assemble(const EgGraph& G, const EgState& W, int64_t n_bloc
 
 hipError_t launch_eg_factor_solve(const EgGraph& G, const EgState& W, int64_t n_blocks,
                                   double lambda, hipStream_t st) {
+  hipError_t e = hipMemcpyAsync(W.L, W.H, (size_t)n_blocks * 49 * sizeof(double),
+                                hipMemcpyDeviceToDevice, st);
+  if (e != hipSuccess) return e;
   SLAMGPU_LAUNCH("eg_factor_solve", st, eg_factor_solve_kernel, dim3(1), dim3(kFacThreads), 0, st,
                  G, W, n_blocks, lambda);
   return hipGetLastError();

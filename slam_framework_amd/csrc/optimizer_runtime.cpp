@@ -603,8 +603,10 @@ int slamgpu_optimize_essential_graph(int n_kf, double* Scw, const uint8_t* fixed
   for (int i = 0; i < F; i++)
     for (int k = start[i]; k < i; k++) ext[k].push_back(i);
   std::vector<int32_t> ext_ptr(1, 0), ext_rows;
+  std::vector<int64_t> ext_base;
   for (int k = 0; k < F; k++) {
     ext_rows.insert(ext_rows.end(), ext[k].begin(), ext[k].end());
+    for (int i : ext[k]) ext_base.push_back(off[i] - start[i]);
     ext_ptr.push_back((int32_t)ext_rows.size());
   }
   // ---- one device region: inputs, structure, state ----
@@ -620,6 +622,7 @@ int slamgpu_optimize_essential_graph(int n_kf, double* Scw, const uint8_t* fixed
   const size_t o_tb = take(4 * (size_t)n_targets), o_tv = take(4 * (size_t)n_targets);
   const size_t o_tp = take(4 * ((size_t)n_targets + 1)), o_ti = take(4 * tgt_items.size());
   const size_t o_ep = take(4 * ((size_t)F + 1)), o_er = take(4 * ext_rows.size());
+  const size_t o_eb = take(8 * ext_base.size());
   const size_t o_S = take(8 * 8 * N), o_S2 = take(8 * 8 * N), o_S0 = take(8 * 8 * N);
   const size_t o_err = take(8 * 7 * E), o_chi = take(8 * E), o_con = take(8 * kEgContrib * E);
   const size_t o_J = take(8 * 98 * E);
@@ -645,6 +648,7 @@ int slamgpu_optimize_essential_graph(int n_kf, double* Scw, const uint8_t* fixed
   OPT_HIPCHECK(up(o_ti, tgt_items.data(), 4 * tgt_items.size()));
   OPT_HIPCHECK(up(o_ep, ext_ptr.data(), 4 * ((size_t)F + 1)));
   OPT_HIPCHECK(up(o_er, ext_rows.data(), 4 * ext_rows.size()));
+  OPT_HIPCHECK(up(o_eb, ext_base.data(), 8 * ext_base.size()));
   OPT_HIPCHECK(up(o_S, Scw, 64 * N));
   OPT_HIPCHECK(up(o_S0, Scw, 64 * N));
   OPT_HIPCHECK(hipMemsetAsync(d + o_x, 0, 8 * P7 + 1, st));
@@ -668,6 +672,7 @@ int slamgpu_optimize_essential_graph(int n_kf, double* Scw, const uint8_t* fixed
   G.tgt_items = reinterpret_cast<const int32_t*>(d + o_ti);
   G.ext_ptr = reinterpret_cast<const int32_t*>(d + o_ep);
   G.ext_rows = reinterpret_cast<const int32_t*>(d + o_er);
+  G.ext_base = reinterpret_cast<const int64_t*>(d + o_eb);
   EgState W;
   W.S = reinterpret_cast<double*>(d + o_S);
   W.S_trial = reinterpret_cast<double*>(d + o_S2);
