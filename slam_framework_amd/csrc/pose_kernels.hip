@@ -214,6 +214,7 @@ template <int W>
 struct FrameSum {
   double red[2][W][32];  // wave partials, double-buffered: a buffer is rewritten two sums later,
   double tot[W][32];     // after a barrier every reader has passed
+  double bc[14];         // the trial step (x, T, ok) from wave 0 to the other waves
   int rb;
 
   // 32 sums (H, b, chi2) -> tot[wave][0..31]
@@ -255,6 +256,12 @@ struct FrameSum {
 // thread k % (64 W); per slot a thread keeps two bits: the edge is an outlier (level 1,
 // inactive), and the f32 test chi2 > threshold of the edge's last computed chi2 -- the only use
 // g2o's classification makes of the stored (possibly stale) error.
+#ifndef POSE_PROF
+#define POSE_PROF 0
+#endif
+#ifndef POSE_LAT_W  // waves per frame of the latency variant
+#define POSE_LAT_W 8
+#endif
 template <int W>
 __global__ __launch_bounds__(64 * W) void pose_opt_kernel(
     const slamgpu_pose_edge* __restrict__ edges, const int32_t* __restrict__ edge_start,
@@ -266,6 +273,10 @@ __global__ __launch_bounds__(64 * W) void pose_opt_kernel(
   static_assert(kEpt <= 64, "slot masks are 64-bit");
   __shared__ FrameSum<W> fs;
   __shared__ float isig[SLAMGPU_MAX_LEVELS];  // Frame::mvInvLevelSigma2
+  // the latency variant (one frame per work-group of W waves) keeps the frame's edges in LDS
+  // (4096 x 28 B): the passes then wait on LDS, not on L2, for each edge slot
+  constexpr bool kLdsEdges = W > 1;
+  __shared__ uint32_t s_edges[kLdsEdges ? SLAMGPU_POSE_MAX_EDGES * 7 : 1];
   const int f = blockIdx.x, tid = threadIdx.x;
   const int e0 = edge_start[f];
   const int n = edge_start[f + 1] - e0;
@@ -288,6 +299,20 @@ __global__ __launch_bounds__(64 * W) void pose_opt_kernel(
   }
   float* Tf = Tcw + 16 * f;
   if (tid < SLAMGPU_MAX_LEVELS) isig[tid] = P.inv_sigma2[tid];
+  if constexpr (kLdsEdges) {
+    static_assert(sizeof(slamgpu_pose_edge) == 28, "pose edge layout");
+    const uint32_t* src = reinterpret_cast<const uint32_t*>(E);
+    for (int q = tid; q < 7 * n; q += kThreads) s_edges[q] = src[q];
+  }
+  auto edge = [&](int k) -> slamgpu_pose_edge {
+    if constexpr (kLdsEdges) {
+      slamgpu_pose_edge e;
+      __builtin_memcpy(&e, &s_edges[7 * k], sizeof(e));
+      return e;
+    } else {
+      return E[k];
+    }
+  };
   fs.rb = 0;
   __syncthreads();
   const double delta_mono = (double)(float)sqrt(5.991), delta_stereo = (double)(float)sqrt(7.815);
@@ -295,6 +320,17 @@ __global__ __launch_bounds__(64 * W) void pose_opt_kernel(
 
   uint64_t outl = 0, lastbad = 0;
   int lm_total = 0, is_bad = 0;
+#if POSE_PROF  // diagnostic build: thread 0's per-phase wall time (printf at the end)
+  double pp[6] = {0, 0, 0, 0, 0, 0};
+  uint64_t pt = __builtin_amdgcn_s_memrealtime();
+  auto ptick = [&](int k) {
+    const uint64_t t = __builtin_amdgcn_s_memrealtime();
+    pp[k] += 0.01 * (double)(t - pt);
+    pt = t;
+  };
+#else
+  auto ptick = [](int) {};
+#endif
   bool robust = true;
   SE3 T;
 
@@ -322,7 +358,7 @@ __global__ __launch_bounds__(64 * W) void pose_opt_kernel(
         if ((outl >> j) & 1) continue;
         const int k = tid + j * kThreads;
         EdgeEval ev;
-        const double c2 = eval_edge(E[k], P, isig, TP, ev);
+        const double c2 = eval_edge(edge(k), P, isig, TP, ev);
         const uint64_t bit = 1ull << j;
         lastbad = ((float)c2 > (ev.stereo ? 7.815f : 5.991f)) ? (lastbad | bit) : (lastbad & ~bit);
         const double delta = ev.stereo ? delta_stereo : delta_mono;
@@ -364,7 +400,9 @@ __global__ __launch_bounds__(64 * W) void pose_opt_kernel(
           for (int c = a; c < 6; c++, h++) acc[h] += wa0 * J[0][c] + wa1 * J[1][c] + wa2 * J[2][c];
         }
       }
+      ptick(0);
       const double* S = fs.sum32(acc);
+      ptick(1);
       const double* H = S;
       const double* b = S + kNH;
       double currentChi = S[27];
@@ -381,20 +419,54 @@ __global__ __launch_bounds__(64 * W) void pose_opt_kernel(
       int qmax = 0;
       do {
         const SE3 backup = T;
-        const bool ok = ldlt_solve6(H, lambda, b, x);
-        T = se3_left_update(x, backup);
+        bool ok;
+        if constexpr (W == 1) {
+          ok = ldlt_solve6(H, lambda, b, x);
+          T = se3_left_update(x, backup);
+        } else {  // wave 0 alone (its SIMD undisturbed), then a broadcast through LDS
+          if (wave_id() == 0) {
+            ok = ldlt_solve6(H, lambda, b, x);
+            T = se3_left_update(x, backup);
+            if ((tid & 63) == 0) {
+#pragma unroll
+              for (int j = 0; j < 6; j++) fs.bc[j] = x[j];
+              fs.bc[6] = T.r.x;
+              fs.bc[7] = T.r.y;
+              fs.bc[8] = T.r.z;
+              fs.bc[9] = T.r.w;
+              fs.bc[10] = T.t[0];
+              fs.bc[11] = T.t[1];
+              fs.bc[12] = T.t[2];
+              fs.bc[13] = ok ? 1.0 : 0.0;
+            }
+          }
+          __syncthreads();  // the next write of bc follows sum1's barrier, after every read
+#pragma unroll
+          for (int j = 0; j < 6; j++) x[j] = fs.bc[j];
+          T.r.x = fs.bc[6];
+          T.r.y = fs.bc[7];
+          T.r.z = fs.bc[8];
+          T.r.w = fs.bc[9];
+          T.t[0] = fs.bc[10];
+          T.t[1] = fs.bc[11];
+          T.t[2] = fs.bc[12];
+          ok = fs.bc[13] != 0.0;
+        }
+        ptick(5);
         // ---- trial: computeActiveErrors + activeRobustChi2 at the new estimate ----
         double part = 0.0;
         const PassPose TP = pass_pose(T);
         for (int j = 0; j < nslots; j++) {
           if ((outl >> j) & 1) continue;
           EdgeEval ev;
-          const double c2 = eval_edge(E[tid + j * kThreads], P, isig, TP, ev);
+          const double c2 = eval_edge(edge(tid + j * kThreads), P, isig, TP, ev);
           const uint64_t bit = 1ull << j;
           lastbad = ((float)c2 > (ev.stereo ? 7.815f : 5.991f)) ? (lastbad | bit) : (lastbad & ~bit);
           part += robust ? huber_rho0(c2, ev.stereo ? delta_stereo : delta_mono) : c2;
         }
+        ptick(2);
         double tempChi = fs.sum1(part);
+        ptick(3);
         if (!ok) tempChi = DBL_MAX;
         double scale = 0.0;
 #pragma unroll
@@ -427,16 +499,23 @@ __global__ __launch_bounds__(64 * W) void pose_opt_kernel(
       const uint64_t bit = 1ull << j;
       if (outl & bit) {
         EdgeEval ev;
-        const double c2 = eval_edge(E[tid + j * kThreads], P, isig, TP, ev);
+        const double c2 = eval_edge(edge(tid + j * kThreads), P, isig, TP, ev);
         lastbad = ((float)c2 > (ev.stereo ? 7.815f : 5.991f)) ? (lastbad | bit) : (lastbad & ~bit);
       }
       bad += (lastbad & bit) ? 1.0 : 0.0;
     }
     outl = lastbad;
     is_bad = (int)fs.sum1(bad);
+    ptick(4);
     if (round == 2) robust = false;
     if (n < 10) break;
   }
+#if POSE_PROF
+  if (tid == 0 && f == 0)
+    printf("[pose W=%d] us: lin %.1f sum32 %.1f solve+update %.1f trial %.1f sum1 %.1f "
+           "classify %.1f, %d LM iterations\n", W, pp[0], pp[1], pp[5], pp[2], pp[3], pp[4],
+           lm_total);
+#endif
   // ---- write back: Frame::SetPose(Converter::toCvMat(SE3quat_recov)), mvbOutlier ----
   for (int j = 0; j < nslots; j++) outl_out[tid + j * kThreads] = (outl >> j) & 1;
   if (tid == 0) {
@@ -461,9 +540,10 @@ hipError_t launch_pose_optimization(const slamgpu_pose_edge* d_edges, const int3
                                     int32_t* d_lm_iterations, hipStream_t st) {
   if (n_frames <= 0) return hipSuccess;
   if (n_frames < kPoseLatencyFrames) {
-    // few frames: 8 waves per frame for latency (the per-frame tracking call)
-    SLAMGPU_LAUNCH("pose_opt", st, pose_opt_kernel<8>, dim3(n_frames), dim3(512), 0, st, d_edges,
-                   d_edge_start, P, d_Tcw, d_outlier, d_n_inliers, d_lm_iterations);
+    // few frames: POSE_LAT_W waves per frame for latency (the per-frame tracking call)
+    SLAMGPU_LAUNCH("pose_opt", st, pose_opt_kernel<POSE_LAT_W>, dim3(n_frames),
+                   dim3(64 * POSE_LAT_W), 0, st, d_edges, d_edge_start, P, d_Tcw, d_outlier,
+                   d_n_inliers, d_lm_iterations);
   } else {
     // batches: one wave per frame, many frames resident per CU
     SLAMGPU_LAUNCH("pose_opt", st, pose_opt_kernel<1>, dim3(n_frames), dim3(64), 0, st, d_edges,
