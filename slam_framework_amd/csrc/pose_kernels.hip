@@ -354,11 +354,15 @@ __global__ __launch_bounds__(64 * W) void pose_opt_kernel(
 #pragma unroll
       for (int i = 0; i < 32; i++) acc[i] = 0.0;
       const PassPose TP = pass_pose(T);
+      // batched variant: a software pipeline, the next slot's edge loads (L2) under this one
+      slamgpu_pose_edge en{};
+      if (!kLdsEdges && nslots > 0) en = edge(tid);
       for (int j = 0; j < nslots; j++) {
+        const slamgpu_pose_edge ec = kLdsEdges ? edge(tid + j * kThreads) : en;
+        if (!kLdsEdges && j + 1 < nslots) en = edge(tid + (j + 1) * kThreads);
         if ((outl >> j) & 1) continue;
-        const int k = tid + j * kThreads;
         EdgeEval ev;
-        const double c2 = eval_edge(edge(k), P, isig, TP, ev);
+        const double c2 = eval_edge(ec, P, isig, TP, ev);
         const uint64_t bit = 1ull << j;
         lastbad = ((float)c2 > (ev.stereo ? 7.815f : 5.991f)) ? (lastbad | bit) : (lastbad & ~bit);
         const double delta = ev.stereo ? delta_stereo : delta_mono;
@@ -456,10 +460,14 @@ __global__ __launch_bounds__(64 * W) void pose_opt_kernel(
         // ---- trial: computeActiveErrors + activeRobustChi2 at the new estimate ----
         double part = 0.0;
         const PassPose TP = pass_pose(T);
+        slamgpu_pose_edge en{};
+        if (!kLdsEdges && nslots > 0) en = edge(tid);
         for (int j = 0; j < nslots; j++) {
+          const slamgpu_pose_edge ec = kLdsEdges ? edge(tid + j * kThreads) : en;
+          if (!kLdsEdges && j + 1 < nslots) en = edge(tid + (j + 1) * kThreads);
           if ((outl >> j) & 1) continue;
           EdgeEval ev;
-          const double c2 = eval_edge(edge(tid + j * kThreads), P, isig, TP, ev);
+          const double c2 = eval_edge(ec, P, isig, TP, ev);
           const uint64_t bit = 1ull << j;
           lastbad = ((float)c2 > (ev.stereo ? 7.815f : 5.991f)) ? (lastbad | bit) : (lastbad & ~bit);
           part += robust ? huber_rho0(c2, ev.stereo ? delta_stereo : delta_mono) : c2;
