@@ -45,6 +45,11 @@ struct slamgpu_ctx {
   // images staged by the host-buffer calls (left at d_in, right at d_in + in_stride)
   uint8_t* d_in = nullptr;
   uint8_t* h_in = nullptr;  // pinned twin of d_in: one DMA per call instead of per-row copies
+  // pinned mirror of one stereo frame's results (counts, both views' keypoints + descriptors,
+  // u_right / depth), filled by slamgpu_frame_stereo before its synchronisation: the downloads
+  // that follow it copy host memory instead of issuing synchronous device reads
+  uint8_t* h_res = nullptr;
+  bool res_valid = false;
   int in_pitch = 0;
   int64_t in_stride = 0;
   // batch state
@@ -182,6 +187,31 @@ static FrameKps left_views(const slamgpu_ctx* c) {
                   2 * (int64_t)c->geom.kp_cap, 2};
 }
 
+// Layout of the pinned result mirror (slamgpu_frame_stereo): two counts (16 B), both views'
+// keypoints and descriptors at kp_cap each, then frame 0's u_right and depth.
+struct ResMirror {
+  int* nkps;
+  KeyPoint* kps;
+  uint8_t* desc;
+  float* u_right;
+  float* depth;
+};
+static size_t res_mirror_bytes(int kp_cap) {
+  const size_t kc = (size_t)kp_cap;
+  return 16 + 2 * kc * sizeof(KeyPoint) + 2 * kc * 32 + 2 * kc * sizeof(float);
+}
+static ResMirror res_mirror(const slamgpu_ctx* c) {
+  const size_t kc = (size_t)c->geom.kp_cap;
+  uint8_t* h = c->h_res;
+  ResMirror m;
+  m.nkps = reinterpret_cast<int*>(h);
+  m.kps = reinterpret_cast<KeyPoint*>(h + 16);
+  m.desc = h + 16 + 2 * kc * sizeof(KeyPoint);
+  m.u_right = reinterpret_cast<float*>(m.desc + 2 * kc * 32);
+  m.depth = m.u_right + kc;
+  return m;
+}
+
 static int check_device_err(slamgpu_ctx* c) {
   uint32_t e = 0;
   HIPCHECK(c, hipMemcpy(&e, c->ws.err, sizeof(e), hipMemcpyDeviceToHost));
@@ -305,6 +335,8 @@ int slamgpu_create(int device, const slamgpu_orb_params* p, int cols, int rows, 
   TRY(dalloc(c, &c->d_nm, (size_t)max_frames));
   TRY(dalloc(c, &c->d_mp, (size_t)g.kp_cap));
   TRY(dalloc(c, &c->d_blk, (size_t)g.kp_cap));
+  TRY(hcheck(c, hipHostMalloc(reinterpret_cast<void**>(&c->h_res), res_mirror_bytes(g.kp_cap),
+                              hipHostMallocDefault)));
 #undef TRY
   *out = c;
   return 0;
@@ -317,6 +349,7 @@ void slamgpu_destroy(slamgpu_ctx* c) {
   for (hipEvent_t e : c->timer.pool) (void)hipEventDestroy(e);
   for (void* p : c->allocs) (void)hipFree(p);
   if (c->h_in) (void)hipHostFree(c->h_in);
+  if (c->h_res) (void)hipHostFree(c->h_res);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   if (c->fx.side0) (void)hipStreamDestroy(c->fx.side0);
   for (hipEvent_t e : {c->fx.fork0, c->fx.join0})
@@ -346,6 +379,7 @@ int slamgpu_scale_tables(const slamgpu_ctx* c, float* scale, float* inv_scale, f
 static int run_frontend(slamgpu_ctx* c, const ImageBatch& b, int n_frames, int n_images,
                         bool stereo, hipStream_t st) {
   TimerScope ts(c);
+  c->res_valid = false;
   c->batch = b;
   c->n_frames_last = n_frames;
   c->n_images_last = n_images;
@@ -457,7 +491,21 @@ int slamgpu_frame_stereo(slamgpu_ctx* c, const uint8_t* left, const uint8_t* rig
   ImageBatch b{c->d_in, c->d_in + c->in_stride, 2 * c->in_stride, c->in_pitch, c->d_pyr};
   int rc = run_frontend(c, b, 1, 2, true, c->stream);
   if (rc) return rc;
-  return slamgpu_sync(c, nullptr);
+  // the frame's results into the pinned mirror, behind the kernels on the same stream
+  const ResMirror m = res_mirror(c);
+  const size_t kc = (size_t)c->geom.kp_cap;
+  HIPCHECK(c, hipMemcpyAsync(m.nkps, c->out.nkps, 2 * sizeof(int), hipMemcpyDeviceToHost,
+                             c->stream));
+  HIPCHECK(c, hipMemcpyAsync(m.kps, c->out.kps, 2 * kc * sizeof(KeyPoint), hipMemcpyDeviceToHost,
+                             c->stream));
+  HIPCHECK(c, hipMemcpyAsync(m.desc, c->out.desc, 2 * kc * 32, hipMemcpyDeviceToHost, c->stream));
+  HIPCHECK(c, hipMemcpyAsync(m.u_right, c->sout.u_right, kc * sizeof(float),
+                             hipMemcpyDeviceToHost, c->stream));
+  HIPCHECK(c, hipMemcpyAsync(m.depth, c->sout.depth, kc * sizeof(float), hipMemcpyDeviceToHost,
+                             c->stream));
+  rc = slamgpu_sync(c, nullptr);
+  c->res_valid = rc == 0;
+  return rc;
 }
 
 int slamgpu_frontend_device(slamgpu_ctx* c, const uint8_t* d_left, const uint8_t* d_right,
@@ -480,6 +528,16 @@ int slamgpu_sync(slamgpu_ctx* c, void* stream) {
 int slamgpu_download_keypoints(slamgpu_ctx* c, int img, slamgpu_keypoint* kps, uint8_t* desc,
                                int cap, int* n_out) {
   if (!c || img < 0 || img >= c->n_images_last) return SLAMGPU_EINVAL;
+  if (c->res_valid && img < 2) {  // slamgpu_frame_stereo's mirror
+    const ResMirror m = res_mirror(c);
+    const int n = m.nkps[img];
+    if (n_out) *n_out = n;
+    if (n > cap) return fail(c, SLAMGPU_ECAP, "need %d keypoints, cap %d", n, cap);
+    const size_t o = (size_t)img * c->geom.kp_cap;
+    if (kps && n) std::memcpy(kps, m.kps + o, sizeof(KeyPoint) * n);
+    if (desc && n) std::memcpy(desc, m.desc + o * 32, 32 * (size_t)n);
+    return 0;
+  }
   int n = 0;
   HIPCHECK(c, hipStreamSynchronize(c->stream));
   HIPCHECK(c, hipMemcpy(&n, c->out.nkps + img, sizeof(int), hipMemcpyDeviceToHost));
@@ -496,6 +554,15 @@ int slamgpu_download_keypoints(slamgpu_ctx* c, int img, slamgpu_keypoint* kps, u
 int slamgpu_download_stereo(slamgpu_ctx* c, int frame, float* u_right, float* depth, int cap,
                             int* n_out) {
   if (!c || frame < 0 || frame >= c->n_frames_last) return SLAMGPU_EINVAL;
+  if (c->res_valid && frame == 0) {
+    const ResMirror m = res_mirror(c);
+    const int n = m.nkps[0];
+    if (n_out) *n_out = n;
+    if (n > cap) return fail(c, SLAMGPU_ECAP, "need %d entries, cap %d", n, cap);
+    if (u_right && n) std::memcpy(u_right, m.u_right, 4 * (size_t)n);
+    if (depth && n) std::memcpy(depth, m.depth, 4 * (size_t)n);
+    return 0;
+  }
   int n = 0;
   HIPCHECK(c, hipStreamSynchronize(c->stream));
   HIPCHECK(c, hipMemcpy(&n, c->out.nkps + 2 * frame, sizeof(int), hipMemcpyDeviceToHost));
