@@ -58,6 +58,10 @@ __device__ __forceinline__ uint32_t dot2u(uint32_t a, uint32_t b, uint32_t c) {
 constexpr int kPyrStrip = PYR_STRIP;  // output rows per wave
 constexpr int kPyrChunk = PYR_CHUNK;  // source rows fetched per batch
 
+// kAligned: the source rows are dword-aligned (every level >= 1 source; level 0 when the caller's
+// images and pitch are) -- the instantiation without the byte-gather path needs fewer VGPRs, so
+// more waves per SIMD hide the strip's chain of row loads.
+template <bool kAligned>
 __global__ __launch_bounds__(256) void pyr_down_kernel(ImageBatch b, const OrbGeom* __restrict__ g,
                                                        int level,
                                                        const ResizeX* __restrict__ rxt,
@@ -99,7 +103,7 @@ __global__ __launch_bounds__(256) void pyr_down_kernel(ImageBatch b, const OrbGe
   const int q0 = s0 >> 2, sh = s0 & 3, qmax = (S.w - 1) >> 2;
   int spitch;
   const uint8_t* src = level_ptr(b, g, img, level - 1, &spitch);
-  const bool aligned = (((uintptr_t)src | (uintptr_t)spitch) & 3) == 0;
+  const bool aligned = kAligned;
   const int qa = min(q0, qmax), qb = min(q0 + 1, qmax), qc = min(q0 + 2, qmax);
   auto fetch = [&](int sy, uint32_t (&wv)[3]) {
     const uint8_t* row = src + (int64_t)min(sy, sy_hi) * spitch;  // wave-uniform
@@ -2112,10 +2116,16 @@ void launch_extract(const ImageBatch& b, const OrbGeomDev& gd, int n_images, hip
     (void)hipEventRecord(fx.join0, fs);
   };
   if (split0) fast_level0();
+  const bool in_aligned = (((uintptr_t)b.in_l | (uintptr_t)b.in_r | (uintptr_t)b.in_stride |
+                           (uintptr_t)b.in_pitch) & 3) == 0;
   for (int l = 1; l < g.nlevels; l++) {
     const int tiles = ((g.lv[l].w + 255) >> 8) * ((g.lv[l].h + 4 * kPyrStrip - 1) / (4 * kPyrStrip));
-    SLAMGPU_LAUNCH("pyr_down", st, pyr_down_kernel, dim3(tiles, n_images), dim3(256), 0, st, b,
-                   gd.dev, l, gd.rx, gd.ry);
+    if (l > 1 || in_aligned)
+      SLAMGPU_LAUNCH("pyr_down", st, pyr_down_kernel<true>, dim3(tiles, n_images), dim3(256), 0, st,
+                     b, gd.dev, l, gd.rx, gd.ry);
+    else
+      SLAMGPU_LAUNCH("pyr_down", st, pyr_down_kernel<false>, dim3(tiles, n_images), dim3(256), 0,
+                     st, b, gd.dev, l, gd.rx, gd.ry);
   }
   {
     const dim3 block(64 * kCellWaves);
