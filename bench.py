@@ -89,22 +89,39 @@ def measured_traffic(kernel, batch):
     return None, None
 
 
+def path_bytes_per_frame(level_px, kp_per_image):
+    """algorithmic HBM bytes of one stereo frame through the whole path --
+    both views' pyramids read once (2 * sum_l W_l H_l) + the left / right / last-frame keypoints
+    and descriptors the matchers read (3 * K * (28 + 32))."""
+    return 2 * sum(level_px) + 3 * kp_per_image * 60
+
+
 def kernel_bytes(name, n_images, n_frames, kp_per_image, level_px, n_queries):
-    """Algorithmic bytes one step moves through the named kernel (all its launches)."""
+    """Algorithmic (compulsory) HBM bytes one step moves through the named kernel (all its
+    launches): every input byte the kernel needs read once, every output written once -- the
+    per-kernel split of section 8(d)'s per-frame figure, not the bytes the kernel re-reads."""
     px = sum(level_px)
     if name == "pyr_down":       # read level l-1, write level l
         return n_images * sum(level_px[l - 1] + level_px[l] for l in range(1, len(level_px)))
     if name == "fast_cells":     # read every level once (+ small candidate writes)
         return n_images * px
-    if name == "orient_desc":    # 43x43 raw window (the 7x7-blurred samples' support; it holds
-        # the 749-px IC_Angle disc) + 60 B out per keypoint
-        return n_images * kp_per_image * (43 * 43 + 60)
+    if name == "orient_desc":    # the image's pyramid (the keypoint windows cover the levels;
+        # section 8(d) counts each level read once) + keypoint (28 B) and descriptor (32 B) out
+        return n_images * (px + kp_per_image * 60)
     if name == "stereo_match":   # left+right kps/desc (60 B each) + SAD windows (11x11 + 11x21)
         return n_frames * kp_per_image * (2 * 60 + 121 + 231)
     if name == "search_cand":    # query (64 B) + window candidates' kps/desc (~60 B each, ~8)
         return n_queries * (64 + 8 * 60)
     if name == "octree":         # FAST candidates read + kept keys written (4 B each)
         return n_images * 4 * 2 * kp_per_image
+    return None
+
+
+def working_set_bytes(name, n_images, kp_per_image):
+    """Bytes a kernel's work-items fetch counting overlaps (each keypoint's 43 x 43 raw window
+    for orient_desc): an upper bound on its L2 -> CU traffic, not HBM bytes."""
+    if name == "orient_desc":
+        return n_images * kp_per_image * (43 * 43 + 60)
     return None
 
 
@@ -156,119 +173,28 @@ def main():
 
     cols, rows, B, D = S.KITTI_COLS, S.KITTI_ROWS, args.batch, args.distinct
     cam = S.KITTI_CAM
-    NS = max(1, args.streams)
-    Bs = B // NS
-    assert Bs >= 2 and Bs * NS == B, "--batch must split into --streams parts of >= 2 frames"
-    F = NS * (Bs - 1)   # frames this rank completes (owns) per step
     # ---- ONE synthetic sequence for the whole job (D distinct renders, frame g = render g % D),
-    # sharded contiguously with a one-frame halo; uploaded once (resident in HBM before timing)
+    # sharded contiguously with a one-frame halo, resident in HBM before timing
+    # (slam_framework_amd/sharded.py; the same object tests/test_sharded_gpu.py checks)
     Ls, Rs = S.layered_sequence(1000, D)
     from slam_framework_amd import dist as SD
-    first, lo, hi = SD.shard_with_halo(world * F, rank, world, first=1)
-    assert hi - lo == F and first == lo - 1
-    # context si computes global frames lo - 1 + si*(Bs-1) + [0, Bs): its slot 0 is the halo of
-    # its slot 1 (the previous context's last frame, or the previous rank's for si = 0)
-    gframe = np.array([first + si * (Bs - 1) + i for si in range(NS) for i in range(Bs)])
-    pitch = 1280
-    host_l = np.zeros((B, rows, pitch), np.uint8)
-    host_r = np.zeros((B, rows, pitch), np.uint8)
-    for f in range(B):
-        host_l[f, :, :cols] = Ls[gframe[f] % D]
-        host_r[f, :, :cols] = Rs[gframe[f] % D]
-    d_l = torch.from_numpy(host_l).to(dev)
-    d_r = torch.from_numpy(host_r).to(dev)
-    stride = rows * pitch
-    poses = np.zeros(B, G.F2F_POSE_DTYPE)
-    for f in range(B):
-        t, tl = gframe[f] % D, (gframe[f] - 1) % D
-        Rf, tf = S.layered_pose(t)
-        poses["Rcw"][f] = Rf.astype(np.float32).reshape(-1)
-        poses["tcw"][f] = tf.astype(np.float32)
-        poses["tlc_z"][f] = np.float32((S.rotation(tl) @ (S.camera_center(t) -
-                                                          S.camera_center(tl)))[2])
-    poses["baseline"] = np.float32(cam[4]) / np.float32(cam[0])
-    poses["th"] = 7.0
-    poses["check_ori"] = 1
-    d_poses = torch.from_numpy(poses.view(np.uint8).copy()).to(dev)
-
-    # NS contexts, each with its own HIP stream and Bs consecutive frames of the batch (its first
-    # frame is the halo of its second): the launches of one half fill the other's tails.
-    # INF groups of them take the steps in turn, each group on streams of its own, so up to INF
-    # batches are in flight: the matcher tail of step k (latency-bound: one wave per frame in
-    # search_resolve) runs beside the pyramid of step k + 1.
-    INF = max(1, args.inflight)
-    groups = []
-    for gi in range(INF):
-        g_ctxs = [G.Context(cols, rows, 2000, 1.2, 8, 20, 7, max_frames=Bs, device=local)
-                  for _ in range(NS)]
-        g_streams = [torch.cuda.Stream(device=dev) for _ in range(NS)]
-        g_parts = []
-        kc_ = g_ctxs[0].kp_cap
-        for si in range(NS):
-            g_parts.append({
-                "q": torch.empty(Bs * kc_ * G.F2F_QUERY_DTYPE.itemsize, dtype=torch.uint8,
-                                 device=dev),
-                "qs": torch.empty(Bs, dtype=torch.int32, device=dev),
-                "qc": torch.empty(Bs, dtype=torch.int32, device=dev),
-                "mp": torch.empty(Bs * kc_, dtype=torch.int32, device=dev),
-                "blk": torch.empty(Bs * kc_, dtype=torch.uint8, device=dev),
-                "nm": torch.empty(Bs, dtype=torch.int32, device=dev),
-                "poses": d_poses[si * Bs * G.F2F_POSE_DTYPE.itemsize:
-                                 (si + 1) * Bs * G.F2F_POSE_DTYPE.itemsize]})
-        groups.append((g_ctxs, g_streams, g_parts))
-    ctxs, _, parts = groups[0]
+    from slam_framework_amd.sharded import ShardedFrontend
+    # per-frame results of the owned frames -> rank 0 (world > 1 only; SLAMGPU_BENCH_GATHER=1
+    # runs the pack + gather path at world 1 too, as a local copy)
+    gather = world > 1 or os.environ.get("SLAMGPU_BENCH_GATHER") == "1"
+    job = ShardedFrontend(Ls, Rs, cam, B, dev, streams=args.streams, inflight=args.inflight,
+                          rank=rank, world=world, gather=gather)
+    NS, Bs, INF = job.NS, job.Bs, job.INF
+    host_l, host_r, poses = job.host_l, job.host_r, job.poses
+    ctxs, parts = job.contexts, job.parts
     ctx = ctxs[0]
     kc = ctx.kp_cap
-
-    # per-frame results of the owned frames -> rank 0 (world > 1 only)
-    rec_b = ctx.record_bytes
-    # (SLAMGPU_BENCH_GATHER=1 runs the pack + gather path at world 1 too, as a local copy)
-    gat = SD.FrameGather({"frontend": rec_b, "map_point": kc * 4, "nmatches": 4}, F, dev) \
-        if world > 1 or os.environ.get("SLAMGPU_BENCH_GATHER") == "1" else None
-    k_step = [0]
-
-    def step(group=None):
-        gi = k_step[0] % INF if group is None else group
-        k_step[0] += 1
-        g_ctxs, g_streams, g_parts = groups[gi]
-        gmain = g_streams[0]
-        with torch.cuda.stream(gmain):
-            if gat is not None:
-                gat.begin()
-        for si in range(NS):
-            st_ = g_streams[si]
-            if si:
-                st_.wait_stream(gmain)
-            with torch.cuda.stream(st_):
-                c, pt, h = g_ctxs[si], g_parts[si], st_.cuda_stream
-                off = si * Bs * stride
-                c.frontend_device(int(d_l.data_ptr()) + off, int(d_r.data_ptr()) + off, stride,
-                                  pitch, Bs, cam, h)
-                c.make_vo_queries_device(pt["poses"], 1, pt["q"], pt["qs"], pt["qc"], Bs, h)
-                pt["mp"].fill_(-1)
-                pt["blk"].zero_()
-                c.search_by_projection_frame_device(pt["q"], Bs * kc, pt["qs"], pt["qc"], kc,
-                                                    pt["poses"], pt["mp"], pt["blk"], kc,
-                                                    pt["nm"], Bs, h)
-                if gat is not None:   # owned frames = slots 1..Bs-1 of this context
-                    o = si * (Bs - 1)
-                    c.pack_frame_records_device(1, Bs - 1, gat.slab("frontend")[o:o + Bs - 1], h)
-                    gat.slab("map_point")[o:o + Bs - 1].view(-1).copy_(
-                        pt["mp"][kc:].view(torch.uint8))
-                    gat.slab("nmatches")[o:o + Bs - 1].view(-1).copy_(
-                        pt["nm"][1:].view(torch.uint8))
-        for si in range(1, NS):
-            gmain.wait_stream(g_streams[si])
-        if gat is not None:
-            with torch.cuda.stream(gmain):
-                gat.start()
+    gat = job.gat
+    step = job.step
 
     for _ in range(max(1, args.warmup) * INF):
         step()
-    torch.cuda.synchronize()
-    for gc in groups:
-        for c in gc[0]:
-            c.sync()
+    job.sync()
     # sanity of what the timed steps compute (not timed)
     nk = np.array([ctx.keypoints(i)[0].shape[0] for i in range(min(4, 2 * Bs))])
     nm = np.concatenate([pt["nm"].cpu().numpy() for pt in parts])
@@ -306,9 +232,7 @@ def main():
         dist.barrier()
     t1 = time.perf_counter()
     ctx.timing_stop()
-    for gc in groups:
-        for c in gc[0]:
-            c.sync()
+    job.sync()
     elapsed = SD.max_over_ranks(t1 - t0, dev)
     dom_ms, dom_n = ctx.timing_read(dominant)
     # per-rank result summary gathered to every rank (validation, outside the timed region)
@@ -318,11 +242,7 @@ def main():
     value = frames / elapsed
     ms_per_step = 1000.0 * elapsed / args.steps
 
-    gather_info = None
-    if gat is not None:
-        torch.cuda.synchronize()
-        gather_info = check_gather(gat, ctxs, parts, gframe, Bs, kc, D, world, F) \
-            if rank == 0 else None
+    gather_info = job.check_gather() if gat is not None else None
     if rank == 0:
         level_px = [ctx.pyramid_level(0, l).size for l in range(8)]
         kp_img = float(nk.mean())
@@ -339,7 +259,17 @@ def main():
             "traffic": None,
             "avg_launch_us": round(avg_launch_s * 1e6, 2), "launches": dom_n,
             "algorithmic_bytes_per_launch": per_launch_bytes,
+            "bytes_model": "section 8(d): compulsory bytes (pyramid read once + outputs), see "
+                           "kernel_bytes()",
         }
+        ws = working_set_bytes(dominant, 2 * Bs, kp_img)
+        if ws:
+            roofline["working_set_bytes_per_launch"] = ws / max(1, launches_per_step)
+        # the whole path against HBM: section 8(d)'s bytes per stereo frame x frames/s
+        pbf = path_bytes_per_frame(level_px, kp_img)
+        path_roof = {"bytes_per_stereo_frame": round(pbf),
+                     "achieved": round(pbf * value / 1e9, 2), "peak": HBM_PEAK_GBS,
+                     "unit": "GB/s", "frac": round(pbf * value / 1e9 / HBM_PEAK_GBS, 5)}
         traffic, tsrc = measured_traffic(dominant, B)
         if traffic is not None:
             roofline["traffic"] = round(traffic)
@@ -355,7 +285,9 @@ def main():
                                       "source": "profiles/valu.json"}
         cpu = None
         if not args.no_cpu_baseline:
-            cpu = cpu_baseline(Ls, Rs, args.cpu_frames)
+            dk, dd = ctx.keypoints(0)   # the left view of the batch's frame 0
+            cpu = cpu_baseline(Ls, Rs, args.cpu_frames,
+                               device_check=(int(job.gframe[0]) % D, dk, dd))
         opt = None
         if not args.no_optimizer:
             opt = {"pose_optimization": bench_pose(dev, not args.no_cpu_baseline),
@@ -409,6 +341,7 @@ def main():
                            if world > 1 else "")},
             "gather": gather_info,
             "roofline": roofline,
+            "path_roofline": path_roof,
             "cpu_baseline": cpu,
             "kernel_ms_per_step": {n: round(brk[n][0], 4) for n in names},
             "kernels_standalone": kernels,
@@ -440,45 +373,6 @@ def spawn_ranks(n):
         procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:],
                                       env=env))
     return max(abs(p.wait()) for p in procs)
-
-
-def check_gather(gat, ctxs, parts, gframe, Bs, kc, D, world, F):
-    """Rank 0, after timing: every frame gathered from the other ranks must equal, byte for byte
-    (trimmed to its keypoint count), rank 0's own result for the same sequence frame modulo the
-    D distinct renders -- the frontend output depends only on the frame, the frame-to-frame
-    search only on (t-1, t)."""
-    import torch
-    from slam_framework_amd import slamgpu as G
-    slot = (gat.k - 1) % len(gat.send)
-    recs = gat.field(slot, "frontend").cpu().numpy()
-    mps = gat.field(slot, "map_point").cpu().numpy().view(np.int32)
-    nms = gat.field(slot, "nmatches").cpu().numpy().view(np.int32).reshape(-1)
-    # rank 0's own owned frames, by residue
-    own = {}
-    for si, c in enumerate(ctxs):
-        rec = torch.empty((Bs - 1, c.record_bytes), dtype=torch.uint8, device=gat.device)
-        c.pack_frame_records_device(1, Bs - 1, rec, torch.cuda.current_stream().cuda_stream)
-        torch.cuda.synchronize()
-        rec = rec.cpu().numpy()
-        mp = parts[si]["mp"].cpu().numpy().reshape(Bs, kc)
-        nm = parts[si]["nm"].cpu().numpy()
-        for i in range(1, Bs):
-            own.setdefault(int(gframe[si * Bs + i]) % D, (rec[i - 1], mp[i], nm[i]))
-    checked = 0
-    j0 = F if world > 1 else 0   # the frames of ranks 1..world-1 (at world 1: rank 0's own)
-    for j in range(j0, world * F, max(1, (world * F - j0) // 64)):
-        g = j + 1
-        r_own, mp_own, nm_own = own[g % D]
-        a, b = G.unpack_frame_record(recs[j], kc), G.unpack_frame_record(r_own, kc)
-        n = len(a["kps_left"])
-        ok = all(a[k].tobytes() == b[k].tobytes() for k in a) and nms[j] == nm_own and \
-            np.array_equal(mps[j][:n], mp_own[:n])
-        if not ok:
-            raise SystemExit(f"bench.py: gathered frame {g} differs from rank 0's own result")
-        checked += 1
-    return {"bytes_per_rank_per_step": gat.nbytes, "frames_per_rank_per_step": F,
-            "record_bytes_per_frame": int(gat.fields["frontend"]) + 4 * kc + 4,
-            "frames_checked_vs_rank0": checked, "identical": True}
 
 
 def bench_frame_latency(Ls, Rs, cam, device, reps=40):
@@ -636,7 +530,7 @@ def bench_pose(dev, with_cpu):
         sys.path.insert(0, os.path.join(ROOT, "tests"))
         import oracle_lib as O
         O.build()
-        threads = min(16, os.cpu_count() or 1)
+        threads = host_cpu_share()[0]
         per = 16
 
         def work(t):
@@ -789,7 +683,7 @@ def bench_local_ba(dev, with_cpu):
         sys.path.insert(0, os.path.join(ROOT, "tests"))
         import oracle_lib as O
         O.build()
-        threads = min(16, os.cpu_count() or 1)
+        threads = host_cpu_share()[0]
         per = 2
         probs = [S.c5_problem(11 + i) for i in range(4)]
 
@@ -893,7 +787,7 @@ def bench_bow(ctx, Bs, dev, with_cpu):
         O.build()
         ov = O.OracleVocab(V)
         frames = [ctx.keypoints(2 * f) for f in range(min(Bs, 17))]
-        threads = min(16, os.cpu_count() or 1)
+        threads = host_cpu_share()[0]
         per = 4
 
         def work(tid):
@@ -1013,7 +907,7 @@ def bench_kfmatch(ctx, Bs, dev, view, sets, with_cpu):
         fvs = [sets.host(f)[1].arrays() for f in range(min(Bs, 17))]
         kd = [dict(kps=host[f][0], desc=host[f][1], ur=ur[f], mp=mp[f][:len(host[f][1])],
                    fv=fvs[f]) for f in range(min(Bs, 17))]
-        threads = min(16, os.cpu_count() or 1)
+        threads = host_cpu_share()[0]
         per = 4
 
         def work(tid):
@@ -1052,13 +946,44 @@ def cpu_model():
     return None, os.cpu_count()
 
 
-def cpu_baseline(Ls, Rs, n_frames):
-    """The oracle/ restatement (C, the -O3 x86-64-v3 build oracle/liborb_oracle_fast.so, checked
-    byte-identical to the test oracle by tests/test_oracle.py) on host threads, two ways:
-    throughput -- each of 16 threads runs its own consecutive frames (extract L+R, stereo,
-    frame-to-frame search against the previous frame's stereo points), wall time over all;
-    reference threading -- one frame at a time, its left and right extraction on two threads as
-    the stereo Frame ctor runs them (frame.cpp:86-89), then stereo and search."""
+def host_cpu_share():
+    """(usable threads, evidence): the CPUs this process may run on (sched affinity), capped by
+    the GPU pool's per-GPU CPU share, which the box advertises through OMP_NUM_THREADS (16 per
+    GPU; os.cpu_count() there reports the whole machine); plus the cgroup CPU quota if any."""
+    aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()
+    share = int(os.environ.get("OMP_NUM_THREADS") or 0) or aff
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()
+            quota = None if q == "max" else round(int(q) / int(per), 2)
+    except (OSError, ValueError):
+        pass
+    return max(1, min(aff, share)), {"affinity_cpus": aff, "omp_num_threads": share,
+                                     "cgroup_cpu_quota": quota}
+
+
+def build_native_oracle():
+    """gcc -O3 -march=native build of oracle/ for THIS host's CPU (oracle/Makefile `native`),
+    into a temporary directory; returns its path."""
+    import subprocess
+    import tempfile
+    out = os.path.join(tempfile.mkdtemp(prefix="slamgpu_oracle_"), "liborb_oracle_native.so")
+    subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "oracle"), "native",
+                    f"NATIVE_OUT={out}"], check=True, stdout=subprocess.DEVNULL,
+                   stderr=subprocess.DEVNULL)
+    return out
+
+
+def cpu_baseline(Ls, Rs, n_frames, device_check=None):
+    """The oracle/ restatement (C) built -O3 -march=native for this host on host threads:
+    throughput -- each thread runs its own consecutive frames (extract L+R, stereo,
+    frame-to-frame search against the previous frame's stereo points), wall time over all -- at
+    the thread count a sweep over 1, 2, 4, ... up to the host's CPU share picks (the sweep is in
+    the result); reference threading -- one frame at a time, its left and right extraction on
+    two threads as the stereo Frame ctor runs them (frame.cpp:86-89), then stereo and search.
+    device_check: (render index, keypoints, descriptors) of a left view from the device, which
+    the native build must reproduce byte for byte before it is timed."""
     import concurrent.futures as cf
 
     sys.path.insert(0, os.path.join(ROOT, "tests"))
@@ -1067,14 +992,26 @@ def cpu_baseline(Ls, Rs, n_frames):
     from slam_framework_amd import synthetic as S
 
     O.build()
+    native = None
     if O._lib is None:
-        O.use_fast()
+        try:
+            native = build_native_oracle()
+            O.use_lib(native)
+        except Exception as e:  # no gcc on the host: the prebuilt x86-64-v3 build
+            print(f"cpu_baseline: native build failed ({e}); using liborb_oracle_fast.so",
+                  file=sys.stderr)
+            O.use_fast()
     t = O.tables()
     g = O.grid_geom(S.KITTI_COLS, S.KITTI_ROWS)
     cam = S.KITTI_CAM
-    threads = min(16, os.cpu_count() or 1)
-    per_thread = max(2, (n_frames or 16 * threads) // threads)
     D = len(Ls)
+    identical = None
+    if device_check is not None:
+        f, dk, dd = device_check
+        kl, dl, _ = O.extract(t, Ls[f], True)
+        identical = kl.tobytes() == dk.tobytes() and np.array_equal(dl, dd)
+        if not identical:
+            raise SystemExit("cpu_baseline: the native oracle build differs from the device")
 
     def search(f, kl, dl, ur, prev):
         q, lmp, lout, xyz, md, nobs = scenario.vo_queries(prev[0], prev[1], prev[2], prev[3],
@@ -1085,22 +1022,35 @@ def cpu_baseline(Ls, Rs, n_frames):
                        p["Rcw"][0].reshape(3, 3), p["tcw"][0], float(p["tlc_z"][0]),
                        float(p["baseline"][0]), cam, 7.0, 0, 1)
 
-    def run(tid):
-        prev = None
-        for k in range(per_thread):
-            f = (tid * per_thread + k) % D
-            kl, dl, pl = O.extract(t, Ls[f], True)
-            kr, dr, pr = O.extract(t, Rs[f], True)
-            ur, depth, _ = O.stereo(t, kl, dl, kr, dr, pl, pr, cam[0], cam[4])
-            if prev is not None:
-                search(f, kl, dl, ur, prev)
-            prev = (kl, dl, depth, f)
-        return per_thread
+    def throughput(threads, per_thread):
+        def run(tid):
+            prev = None
+            for k in range(per_thread):
+                f = (tid * per_thread + k) % D
+                kl, dl, pl = O.extract(t, Ls[f], True)
+                kr, dr, pr = O.extract(t, Rs[f], True)
+                ur, depth, _ = O.stereo(t, kl, dl, kr, dr, pl, pr, cam[0], cam[4])
+                if prev is not None:
+                    search(f, kl, dl, ur, prev)
+                prev = (kl, dl, depth, f)
+            return per_thread
+        t0 = time.perf_counter()
+        with cf.ThreadPoolExecutor(threads) as ex:
+            done = sum(ex.map(run, range(threads)))
+        return done, time.perf_counter() - t0
 
-    t0 = time.perf_counter()
-    with cf.ThreadPoolExecutor(threads) as ex:
-        done = sum(ex.map(run, range(threads)))
-    wall = time.perf_counter() - t0
+    max_threads, share = host_cpu_share()
+    sweep = {}
+    tc = 1
+    while True:
+        done, wall = throughput(tc, 3)
+        sweep[tc] = round(done / wall, 2)
+        if tc >= max_threads:
+            break
+        tc = min(2 * tc, max_threads)
+    threads = max(sweep, key=sweep.get)
+    per_thread = max(2, (n_frames or 16 * threads) // threads)
+    done, wall = throughput(threads, per_thread)
 
     # the reference's own threading: frames in sequence, L and R extracted concurrently
     n_seq = 24
@@ -1119,7 +1069,14 @@ def cpu_baseline(Ls, Rs, n_frames):
     model, ncpu = cpu_model()
     return {"value": round(done / wall, 2), "unit": "stereo frames/s", "cores": threads,
             "kind": "port", "cpu_model": model, "host_logical_cpus": ncpu,
-            "build": "oracle/liborb_oracle_fast.so: gcc -O3 -march=x86-64-v3 -ffp-contract=off",
+            "cpu_share": share,
+            "thread_sweep_frames_per_s": {str(k): v for k, v in sweep.items()},
+            "threads_chosen_by": "best of the sweep over 1..min(affinity, OMP_NUM_THREADS); the "
+                                 "GPU pool gives each GPU's jobs a 16-CPU share of the host",
+            "build": ("gcc -O3 -march=native -ffp-contract=off (oracle/Makefile native, built on "
+                      "this host)" if native else
+                      "oracle/liborb_oracle_fast.so: gcc -O3 -march=x86-64-v3 -ffp-contract=off"),
+            "native_matches_device": identical,
             "sample": f"{done} synthetic stereo frames ({threads} threads x {per_thread}); "
                       f"oracle/ C restatement: extract L+R + stereo + frame-to-frame",
             "wall_s": round(wall, 2),

@@ -75,6 +75,11 @@ int slamgpu_kp_capacity(const slamgpu_ctx* ctx);
  * nlevels entries; any pointer may be NULL. */
 int slamgpu_scale_tables(const slamgpu_ctx* ctx, float* scale, float* inv_scale, float* sigma2,
                          float* inv_sigma2, int* features_per_level);
+/* The same tables from the ctor arguments alone (orb_extractor.cpp:351-387: they do not depend on
+ * the image size), with no context and no device: what ORBextractor's getters return before the
+ * first Compute. Returns SLAMGPU_EINVAL for nlevels outside [1, 12] or scale_factor <= 1. */
+int slamgpu_orb_scale_tables(const slamgpu_orb_params* params, float* scale, float* inv_scale,
+                             float* sigma2, float* inv_sigma2, int* features_per_level);
 
 /* ---- ORBextractor ------------------------------------------------------------------------- */
 /* Replaces: ORBextractor::Compute(image, mask, keypoints, descriptors)  orb_extractor.cpp:985.

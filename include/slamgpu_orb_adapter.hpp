@@ -86,20 +86,18 @@ class ORBextractor {
     cols_ = cols;
     rows_ = rows;
   }
+  // the ctor tables do not depend on the image size: computed host-side, no device context
   std::vector<float> table(int which) const {
     std::vector<float> t(params_.nlevels);
-    slamgpu_orb_params p = params_;
-    slamgpu_ctx* c = ctx_;
-    if (!c) slamgpu_create(device_, &p, 640, 480, 1, &c);  // tables do not depend on size
     float* ptrs[4] = {nullptr, nullptr, nullptr, nullptr};
     ptrs[which] = t.data();
-    slamgpu_scale_tables(c, ptrs[0], ptrs[1], ptrs[2], ptrs[3], nullptr);
-    if (c != ctx_) slamgpu_destroy(c);
+    check(slamgpu_orb_scale_tables(&params_, ptrs[0], ptrs[1], ptrs[2], ptrs[3], nullptr));
     return t;
   }
   void check(int rc) const {
-    if (rc != SLAMGPU_OK) throw std::runtime_error(std::string("slamgpu: ") +
-                                                   slamgpu_last_error(ctx_));
+    if (rc != SLAMGPU_OK)
+      throw std::runtime_error(std::string("slamgpu: ") +
+                               (ctx_ ? slamgpu_last_error(ctx_) : "invalid ORB parameters"));
   }
 
   slamgpu_orb_params params_;

@@ -37,6 +37,7 @@ def _stale() -> bool:
 def build(force: bool = False, verbose: bool = False) -> str:
     if not force and not _stale():
         build_capi_check()
+        build_adapter_check()
         return LIB
     objdir = os.path.join(PKG, "build")
     os.makedirs(objdir, exist_ok=True)
@@ -62,6 +63,7 @@ def build(force: bool = False, verbose: bool = False) -> str:
                    check=True)
     os.replace(tmp, LIB)
     build_capi_check()
+    build_adapter_check()
     return LIB
 
 
@@ -80,6 +82,23 @@ def build_capi_check() -> str:
                     CAPI_SRC, "-L", PKG, "-lslamgpu",
                     "-Wl,-rpath,$ORIGIN/../slam_framework_amd", "-o", CAPI_BIN], check=True)
     return CAPI_BIN
+
+
+ADAPTER_SRC = os.path.join(ROOT, "tests", "adapter_check.cpp")
+ADAPTER_BIN = os.path.join(ROOT, "tests", "adapter_check")
+
+
+def build_adapter_check() -> str:
+    """g++ build of tests/adapter_check.cpp: include/slamgpu_adapters.hpp (the OpenCV-free graph
+    gathering of the reference-side adapters) compiled and driven on the CPU."""
+    deps = [ADAPTER_SRC, LIB] + glob.glob(os.path.join(ROOT, "include", "*.h*"))
+    if os.path.exists(ADAPTER_BIN) and os.path.getmtime(ADAPTER_BIN) >= max(
+            os.path.getmtime(d) for d in deps):
+        return ADAPTER_BIN
+    subprocess.run(["g++", "-O2", "-std=c++17", "-Wall", "-Wextra", "-I",
+                    os.path.join(ROOT, "include"), ADAPTER_SRC, "-L", PKG, "-lslamgpu",
+                    "-Wl,-rpath,$ORIGIN/../slam_framework_amd", "-o", ADAPTER_BIN], check=True)
+    return ADAPTER_BIN
 
 
 if __name__ == "__main__":

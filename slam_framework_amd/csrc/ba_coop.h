@@ -67,7 +67,11 @@ struct CoopWs {
   int end_bit;         // radix-sort key bits
 };
 
-enum { CTL_ERR = 0, CTL_STOPPED = 1, CTL_LM = 2, CTL_POLL = 3, CTL_OK = 4 };
+// CTL_BEAT: work-group 0's heartbeat while the others wait at a barrier (bumped per block column
+// of the factorisation); CTL_ARRIVED / CTL_GRID: on a barrier give-up, the arrivals the giving-up
+// waiter last saw and the grid size (missing work-groups vs a slow one).
+enum { CTL_ERR = 0, CTL_STOPPED = 1, CTL_LM = 2, CTL_POLL = 3, CTL_OK = 4, CTL_BEAT = 5,
+       CTL_ARRIVED = 6, CTL_GRID = 7 };
 
 // One optimize() call of the schedule.
 struct CoopPhase {

@@ -80,8 +80,12 @@ __device__ __forceinline__ void decode_key(uint32_t key, int& kh, int& kl) {
 // for) before the second work-group barrier -- the one-fence-per-work-group form, instead of a
 // release + acquire from every wave. Work-group 0 can carry a poll of the caller's stop flag
 // (system scope: host-mapped memory) into CTL_POLL, which every work-group reads after the
-// barrier -- so all of them take the same decision. A waiter gives up after ~2^22 sleeps and
-// raises CTL_ERR (the host then reports a device error); later barriers do not wait once it is set.
+// barrier -- so all of them take the same decision. A waiter gives up only when nothing moves:
+// its count of sleeps restarts whenever the arrival counter or work-group 0's heartbeat
+// (CTL_BEAT, bumped per block column while it factors S alone) changes, so a long factorisation
+// never times out; ~2^22 sleeps (~2 s) without either raise CTL_ERR with the arrivals seen
+// (CTL_ARRIVED of CTL_GRID: work-groups that never became resident). Later barriers do not wait
+// once it is set.
 __device__ __forceinline__ void vm_drain() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 
 __device__ void grid_sync(const CoopWs& w, const int32_t* stop_flag, bool poll) {
@@ -106,13 +110,30 @@ __device__ void grid_sync(const CoopWs& w, const int32_t* stop_flag, bool poll) 
         vm_drain();  // the reset lands before anyone can arrive at the next barrier
         __hip_atomic_store(&w.bar[1], g + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       } else {
-        uint32_t spins = 0;
+        uint32_t spins = 0, polls = 0, seen_a = a + 1u;
+        int32_t seen_beat = __hip_atomic_load(&w.ctl[CTL_BEAT], __ATOMIC_RELAXED,
+                                              __HIP_MEMORY_SCOPE_AGENT);
         while (__hip_atomic_load(&w.bar[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == g) {
-          if (spins < 256) __builtin_amdgcn_s_sleep(1);  // short waits: poll fast
+          if (polls < 256) __builtin_amdgcn_s_sleep(1);  // short waits: poll fast
           else __builtin_amdgcn_s_sleep(16);             // then back off (~1k cycles)
-          if (++spins > (1u << 22)) {
-            __hip_atomic_store(&w.ctl[CTL_ERR], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            break;
+          polls++;
+          if ((++spins & 1023u) == 0) {  // progress check
+            const uint32_t na =
+                __hip_atomic_load(&w.bar[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const int32_t nb =
+                __hip_atomic_load(&w.ctl[CTL_BEAT], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (na != seen_a || nb != seen_beat) {
+              seen_a = na;
+              seen_beat = nb;
+              spins = 0;
+            } else if (spins > (1u << 22)) {
+              __hip_atomic_store(&w.ctl[CTL_ARRIVED], (int32_t)na, __ATOMIC_RELAXED,
+                                 __HIP_MEMORY_SCOPE_AGENT);
+              __hip_atomic_store(&w.ctl[CTL_GRID], (int32_t)gridDim.x, __ATOMIC_RELAXED,
+                                 __HIP_MEMORY_SCOPE_AGENT);
+              __hip_atomic_store(&w.ctl[CTL_ERR], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+              break;
+            }
           }
         }
       }
@@ -717,6 +738,8 @@ __device__ __forceinline__ void factor_solve(CoopShared& sh, const CoopWs& w, in
       }
     }
     fs_tick(10);
+    if (tid == 0)  // heartbeat for the work-groups waiting at the next grid barrier
+      __hip_atomic_fetch_add(&w.ctl[CTL_BEAT], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __syncthreads();
     fs_tick(11);
   }
@@ -1257,8 +1280,18 @@ hipError_t launch_coop_ba(const PoseParams& P, const CoopProblem& pb, const Coop
     const int32_t* stop = d_stop;
     void* args[] = {&Pc, &pbc, &wc, &sch, &stop};
     if (g_timer) g_timer->begin("ba_coop", st);
-    e = hipLaunchKernel(reinterpret_cast<const void*>(&ba_coop_kernel), dim3(G), dim3(kT), args, 0,
-                        st);
+    // SLAMGPU_BA_COOP_LAUNCH=1: the runtime's cooperative launch instead (residency guaranteed
+    // by the runtime; DESIGN.md section 3 records what the A/B of the two showed)
+    static const bool coop_launch = [] {
+      const char* v = getenv("SLAMGPU_BA_COOP_LAUNCH");
+      return v && v[0] == '1';
+    }();
+    if (coop_launch)
+      e = hipLaunchCooperativeKernel(reinterpret_cast<const void*>(&ba_coop_kernel), dim3(G),
+                                     dim3(kT), args, 0, st);
+    else
+      e = hipLaunchKernel(reinterpret_cast<const void*>(&ba_coop_kernel), dim3(G), dim3(kT), args,
+                          0, st);
     if (g_timer) g_timer->end("ba_coop", st);
     if (e != hipSuccess) return e;
   }

@@ -7,6 +7,7 @@
 #include <hip/hip_runtime.h>
 
 #include <chrono>
+#include <mutex>
 #include <thread>
 
 #include <cfloat>
@@ -260,23 +261,39 @@ namespace {
 
 // Work-groups of the cooperative single-problem solver: 32 (SLAMGPU_BA_WGS overrides), never more
 // than can be resident at once. C5 LocalBA: 2.91 / 2.81 / 2.82 / 2.76 ms at 24 / 32 / 48 / 64;
-// 32 leaves 224 CUs to the tracking front end that shares the device.
+// 32 leaves 224 CUs to the tracking front end that shares the device. Computed once per device
+// (the mapping and loop-closing threads may make their first calls at the same time).
+constexpr int kMaxDevices = 64;
+
 int coop_grid(int device) {
-  static int cached_dev = -1, cached = 0;
-  if (cached_dev == device) return cached;
-  hipDeviceProp_t prop{};
-  int g = 32;
-  if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 0)
-    g = std::min(g, prop.multiProcessorCount);
-  if (const char* e = getenv("SLAMGPU_BA_WGS")) g = std::min(256, std::max(1, atoi(e)));
-  int per_cu = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, coop_kernel_ptr(), kCoopThreads, 0) ==
-          hipSuccess &&
-      per_cu > 0 && prop.multiProcessorCount > 0)
-    g = std::min(g, per_cu * prop.multiProcessorCount);
-  cached_dev = device;
-  cached = g;
-  return g;
+  static std::once_flag once[kMaxDevices];
+  static int grid[kMaxDevices];
+  if (device < 0 || device >= kMaxDevices) return 1;
+  std::call_once(once[device], [device]() {
+    hipDeviceProp_t prop{};
+    int g = 32;
+    const bool have = hipGetDeviceProperties(&prop, device) == hipSuccess &&
+                      prop.multiProcessorCount > 0;
+    if (have) g = std::min(g, prop.multiProcessorCount);
+    if (const char* e = getenv("SLAMGPU_BA_WGS")) g = std::min(256, std::max(1, atoi(e)));
+    int per_cu = 0;
+    if (have && hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, coop_kernel_ptr(),
+                                                             kCoopThreads, 0) == hipSuccess &&
+        per_cu > 0)
+      g = std::min(g, per_cu * prop.multiProcessorCount);
+    grid[device] = std::max(1, g);
+  });
+  return grid[device];
+}
+
+// One single-problem solve per device at a time: its G work-groups must all be resident for the
+// grid barriers to complete, so two of them (the LocalMapper's LocalBA and the LoopCloser's global
+// BA, local_mapper.cpp:53, loop_closer.cpp:77) never compete for residency. The front end and
+// PoseOptimization on other streams only delay residency (their work-groups finish and free
+// their CUs); the barrier waits for as long as arrivals keep coming.
+std::mutex& coop_device_mutex(int device) {
+  static std::mutex m[kMaxDevices];
+  return m[device < 0 || device >= kMaxDevices ? 0 : device];
 }
 
 // One problem (LocalBundleAdjustment after its graph gathering, or the global BundleAdjustment)
@@ -358,27 +375,20 @@ int coop_host(const char* what, const slamgpu_camera* cam, const float* inv_sigm
   }
   char* b = static_cast<char*>(S.buf);
   char* h = S.pin;
-  std::memcpy(h + o_T, kf_Tcw, 64 * (size_t)n_kf);
-  std::memcpy(h + o_mode, kf_mode, n_kf);
-  if (n_points) std::memcpy(h + o_pts, points, 12 * (size_t)n_points);
-  std::memcpy(h + o_ps, point_obs_start, 4 * ((size_t)n_points + 1));
-  if (n_obs) std::memcpy(h + o_obs, obs, sizeof(slamgpu_ba_obs) * (size_t)n_obs);
-  if (n_kf) std::memcpy(h + o_free, free_of.data(), 4 * (size_t)n_kf);
-  if (K) std::memcpy(h + o_kof, kf_of.data(), 4 * (size_t)K);
-  OPT_HIPCHECK(hipMemcpyAsync(b, h, o_er, hipMemcpyHostToDevice, S.stream));
+  std::lock_guard<std::mutex> device_lock(coop_device_mutex(dev));
+  static const bool prof = getenv("SLAMGPU_BA_PROFILE") != nullptr;
   CoopWs w = coop_layout(b + o_ws, n_kf, n_points, n_obs, K, (int)pairs, G, nullptr);
   w.free_of_kf = reinterpret_cast<const int32_t*>(b + o_free);
   w.kf_of_free = reinterpret_cast<const int32_t*>(b + o_kof);
-  static const bool prof = getenv("SLAMGPU_BA_PROFILE") != nullptr;
   if (!prof) w.prof = nullptr;
-  CoopProblem pb{reinterpret_cast<const slamgpu_ba_obs*>(b + o_obs),
-                 reinterpret_cast<const int32_t*>(b + o_ps),
-                 reinterpret_cast<const uint8_t*>(b + o_mode),
-                 reinterpret_cast<float*>(b + o_T),
-                 reinterpret_cast<float*>(b + o_pts),
-                 local ? reinterpret_cast<uint8_t*>(b + o_er) : nullptr,
-                 reinterpret_cast<int32_t*>(b + o_ctl),
-                 n_obs, n_points, n_kf, K};
+  const CoopProblem pb{reinterpret_cast<const slamgpu_ba_obs*>(b + o_obs),
+                       reinterpret_cast<const int32_t*>(b + o_ps),
+                       reinterpret_cast<const uint8_t*>(b + o_mode),
+                       reinterpret_cast<float*>(b + o_T),
+                       reinterpret_cast<float*>(b + o_pts),
+                       local ? reinterpret_cast<uint8_t*>(b + o_er) : nullptr,
+                       reinterpret_cast<int32_t*>(b + o_ctl),
+                       n_obs, n_points, n_kf, K};
   volatile int32_t* mirror = nullptr;
   if (stop_flag) {
     if (!S.stop_host) {
@@ -390,28 +400,48 @@ int coop_host(const char* what, const slamgpu_camera* cam, const float* inv_sigm
       S.stop_dev = static_cast<int32_t*>(d);
     }
     mirror = S.stop_host;
-    *mirror = *stop_flag ? 1 : 0;
   }
-  const auto t_launch0 = clk::now();
-  OPT_HIPCHECK(launch_coop_ba(P, pb, w, phases, n_phases, local, stop_flag ? S.stop_dev : nullptr,
-                              G, S.stream));
-  // the outputs and the control words come back in the same region (pinned: asynchronous)
-  OPT_HIPCHECK(hipMemcpyAsync(h, b, o_io, hipMemcpyDeviceToHost, S.stream));
-  const auto t_launch1 = clk::now();
-  // keep the device's view of the caller's flag live until the work is done
-  if (mirror) {
-    hipError_t q;
-    while ((q = hipStreamQuery(S.stream)) == hipErrorNotReady) {
-      *mirror = *stop_flag ? 1 : 0;
-      std::this_thread::sleep_for(std::chrono::microseconds(5));
-    }
-    if (q != hipSuccess) return fail(SLAMGPU_EHIP, "%s: %s", what, hipGetErrorString(q));
-  }
-  OPT_HIPCHECK(hipStreamSynchronize(S.stream));
-  const auto t_done = clk::now();
+  // A barrier that gives up (CTL_ERR) leaves the caller's arrays untouched; when work-groups were
+  // missing (never resident), the solve is staged and run once more before reporting.
   int32_t ctl[8];
-  std::memcpy(ctl, h + o_ctl, sizeof(ctl));
-  if (ctl[CTL_ERR]) return fail(SLAMGPU_EDEVICE, "%s: grid barrier timed out", what);
+  clk::time_point t_launch0, t_launch1, t_done;
+  for (int attempt = 0;; attempt++) {
+    std::memcpy(h + o_T, kf_Tcw, 64 * (size_t)n_kf);
+    std::memcpy(h + o_mode, kf_mode, n_kf);
+    if (n_points) std::memcpy(h + o_pts, points, 12 * (size_t)n_points);
+    std::memcpy(h + o_ps, point_obs_start, 4 * ((size_t)n_points + 1));
+    if (n_obs) std::memcpy(h + o_obs, obs, sizeof(slamgpu_ba_obs) * (size_t)n_obs);
+    if (n_kf) std::memcpy(h + o_free, free_of.data(), 4 * (size_t)n_kf);
+    if (K) std::memcpy(h + o_kof, kf_of.data(), 4 * (size_t)K);
+    OPT_HIPCHECK(hipMemcpyAsync(b, h, o_er, hipMemcpyHostToDevice, S.stream));
+    if (mirror) *mirror = *stop_flag ? 1 : 0;
+    t_launch0 = clk::now();
+    OPT_HIPCHECK(launch_coop_ba(P, pb, w, phases, n_phases, local,
+                                stop_flag ? S.stop_dev : nullptr, G, S.stream));
+    // the outputs and the control words come back in the same region (pinned: asynchronous)
+    OPT_HIPCHECK(hipMemcpyAsync(h, b, o_io, hipMemcpyDeviceToHost, S.stream));
+    t_launch1 = clk::now();
+    // keep the device's view of the caller's flag live until the work is done
+    if (mirror) {
+      hipError_t q;
+      while ((q = hipStreamQuery(S.stream)) == hipErrorNotReady) {
+        *mirror = *stop_flag ? 1 : 0;
+        std::this_thread::sleep_for(std::chrono::microseconds(5));
+      }
+      if (q != hipSuccess) return fail(SLAMGPU_EHIP, "%s: %s", what, hipGetErrorString(q));
+    }
+    OPT_HIPCHECK(hipStreamSynchronize(S.stream));
+    t_done = clk::now();
+    std::memcpy(ctl, h + o_ctl, sizeof(ctl));
+    if (!ctl[CTL_ERR]) break;
+    const bool missing = ctl[CTL_ARRIVED] < ctl[CTL_GRID] - 1;
+    if (!missing || attempt > 0)
+      return fail(SLAMGPU_EDEVICE, "%s: grid barrier gave up after ~2 s without progress: %d of "
+                  "%d work-groups had arrived (%s)", what, ctl[CTL_ARRIVED], ctl[CTL_GRID],
+                  missing ? "work-groups never became resident, twice" : "a work-group stalled");
+    fprintf(stderr, "slamgpu %s: %d of %d work-groups resident at a grid barrier; retrying once\n",
+            what, ctl[CTL_ARRIVED], ctl[CTL_GRID]);
+  }
   std::memcpy(kf_Tcw, h + o_T, 64 * (size_t)n_kf);
   if (n_points) std::memcpy(points, h + o_pts, 12 * (size_t)n_points);
   if (local && n_obs) std::memcpy(erase, h + o_er, n_obs);

@@ -376,6 +376,25 @@ int slamgpu_scale_tables(const slamgpu_ctx* c, float* scale, float* inv_scale, f
   return 0;
 }
 
+int slamgpu_orb_scale_tables(const slamgpu_orb_params* p, float* scale, float* inv_scale,
+                             float* sigma2, float* inv_sigma2, int* fpl) {
+  if (!p || p->nlevels < 1 || p->nlevels > kMaxLevels || !(p->scale_factor > 1.0f) ||
+      p->nfeatures < 0)
+    return SLAMGPU_EINVAL;
+  OrbTables t;
+  compute_tables(OrbParams{p->nfeatures, p->scale_factor, p->nlevels, p->ini_th_fast,
+                           p->min_th_fast},
+                 &t);
+  for (int l = 0; l < t.nlevels; l++) {
+    if (scale) scale[l] = t.scale[l];
+    if (inv_scale) inv_scale[l] = t.inv_scale[l];
+    if (sigma2) sigma2[l] = t.sigma2[l];
+    if (inv_sigma2) inv_sigma2[l] = t.inv_sigma2[l];
+    if (fpl) fpl[l] = t.features_per_level[l];
+  }
+  return 0;
+}
+
 static int run_frontend(slamgpu_ctx* c, const ImageBatch& b, int n_frames, int n_images,
                         bool stereo, hipStream_t st) {
   TimerScope ts(c);

@@ -66,9 +66,13 @@ class FrameGather:
     fields: {name: bytes per frame}; frames: frames each rank owns per gather (equal on every
     rank; the last shard of a ragged split is padded by its caller). `slots` send/receive buffers
     rotate so that gather k can still be in flight while the compute of k+1 packs the next slot
-    (gather k+slots waits for it on the compute stream, never on the host)."""
+    (gather k+slots waits for it on the compute stream, never on the host).
 
-    def __init__(self, fields: dict, frames: int, device=None, slots: int = 2):
+    host_staging: the process group's backend is a CPU one (gloo) while the producers write
+    device slots -- start() copies the slot to host memory and gathers there, synchronously."""
+
+    def __init__(self, fields: dict, frames: int, device=None, slots: int = 2,
+                 host_staging: bool = False):
         self.fields = dict(fields)
         self.frames = frames
         self.offsets, off = {}, 0
@@ -80,9 +84,11 @@ class FrameGather:
         self.world = dist.get_world_size() if self.active else 1
         self.rank = dist.get_rank() if self.active else 0
         self.device = device
+        self.host_staging = host_staging
         self.send = [torch.empty(self.nbytes, dtype=torch.uint8, device=device)
                      for _ in range(slots)]
-        self.recv = [torch.empty((self.world, self.nbytes), dtype=torch.uint8, device=device)
+        rdev = "cpu" if host_staging else device
+        self.recv = [torch.empty((self.world, self.nbytes), dtype=torch.uint8, device=rdev)
                      if self.rank == 0 else None for _ in range(slots)]
         self.work = [None] * slots
         self.k = 0
@@ -118,7 +124,14 @@ class FrameGather:
     def start(self, async_op: bool = True):
         """Gather the packed slot to rank 0; returns the slot index."""
         s = self._slot()
-        if self.world > 1:
+        if self.host_staging:
+            host = self.send[s].cpu()   # waits for the producers on the current stream
+            glist = list(self.recv[s].unbind(0)) if self.rank == 0 else None
+            if self.world > 1:
+                dist.gather(host, glist, dst=0)
+            else:
+                glist[0].copy_(host)
+        elif self.world > 1:
             glist = list(self.recv[s].unbind(0)) if self.rank == 0 else None
             self.work[s] = dist.gather(self.send[s], glist, dst=0, async_op=async_op)
             if not async_op:

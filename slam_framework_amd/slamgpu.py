@@ -50,7 +50,7 @@ assert F2F_POSE_DTYPE.itemsize == 72 and MPS_QUERY_DTYPE.itemsize == 80
 
 EXPORTS = [
     "slamgpu_create", "slamgpu_destroy", "slamgpu_last_error", "slamgpu_kp_capacity",
-    "slamgpu_scale_tables", "slamgpu_extract", "slamgpu_get_pyramid_level",
+    "slamgpu_scale_tables", "slamgpu_orb_scale_tables", "slamgpu_extract", "slamgpu_get_pyramid_level",
     "slamgpu_frame_stereo", "slamgpu_frontend_device", "slamgpu_sync",
     "slamgpu_download_keypoints", "slamgpu_download_stereo", "slamgpu_device_results",
     "slamgpu_frame_record_bytes", "slamgpu_pack_frame_records_device",
@@ -140,6 +140,7 @@ def lib():
         L.slamgpu_last_error.restype = C.c_char_p
         L.slamgpu_kp_capacity.argtypes = [vp]
         L.slamgpu_scale_tables.argtypes = [vp, vp, vp, vp, vp, vp]
+        L.slamgpu_orb_scale_tables.argtypes = [C.POINTER(OrbParams), vp, vp, vp, vp, vp]
         L.slamgpu_extract.argtypes = [vp, vp, sz, vp, vp, ip, C.POINTER(ip)]
         L.slamgpu_get_pyramid_level.argtypes = [vp, ip, ip, vp, sz, C.POINTER(ip), C.POINTER(ip)]
         L.slamgpu_frame_stereo.argtypes = [vp, vp, vp, sz, C.POINTER(Camera)]

@@ -63,6 +63,14 @@ def use_fast() -> None:
     LIB_PATH = os.path.join(ORACLE_DIR, "liborb_oracle_fast.so")
 
 
+def use_lib(path: str) -> None:
+    """Load the oracle build at `path` (e.g. bench.py's -march=native build for the CPU
+    baseline). Must run before the first lib() call of the process."""
+    global LIB_PATH
+    assert _lib is None, "oracle library already loaded"
+    LIB_PATH = path
+
+
 _lib = None
 
 

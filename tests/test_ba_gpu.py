@@ -215,3 +215,83 @@ def test_local_ba_linearize_matches_oracle(oracle, gpu_lib):
             np.testing.assert_allclose(g, r, rtol=1e-9, atol=1e-9 * np.abs(r).max(),
                                        err_msg=f"problem {i} {k}")
         assert o["chi"][i] == pytest.approx(ref["chi"], rel=1e-10)
+
+
+def test_local_ba_beside_tracking_with_stop(oracle, gpu_lib):
+    """The reference runs LocalBundleAdjustment on the LocalMapper thread while the tracking thread
+    keeps extracting and optimising poses (local_mapper.cpp:53, tracker.cpp:797,1144), and raises
+    its stop flag when a new keyframe arrives (local_mapper.cpp:89-93). Here a second host thread
+    keeps the device busy with slamgpu_frontend_device batches and single-frame PoseOptimization
+    calls on their own streams while the single-problem solver (whose work-groups must all be
+    resident for its grid barriers) runs C5: once to the end and once stopped mid-run. Both must
+    finish without a barrier give-up and match the oracle (full run; the oracle's stop position
+    reproducing the device's iteration count)."""
+    import ctypes
+    import threading
+
+    import torch
+    G = gpu_lib
+    dev = torch.device("cuda", 0)
+    B = 16
+    L, R = S.layered_sequence(1000, 4)
+    pitch = 1280
+    hl = np.zeros((B, S.KITTI_ROWS, pitch), np.uint8)
+    hr = np.zeros_like(hl)
+    for f in range(B):
+        hl[f, :, :S.KITTI_COLS], hr[f, :, :S.KITTI_COLS] = L[f % 4], R[f % 4]
+    d_l, d_r = torch.from_numpy(hl).to(dev), torch.from_numpy(hr).to(dev)
+    ctx = G.Context(S.KITTI_COLS, S.KITTI_ROWS, max_frames=B)
+    edges, T0, _, isig, _ = S.pose_problem(77, 2000)
+    done = threading.Event()
+    counts = {"frontend": 0, "pose": 0}
+    errors = []
+
+    def tracking():
+        try:
+            st = torch.cuda.Stream(device=dev)
+            while not done.is_set():
+                ctx.frontend_device(d_l, d_r, S.KITTI_ROWS * pitch, pitch, B, CAM, st.cuda_stream)
+                counts["frontend"] += 1
+                G.Optimizer.PoseOptimization(edges, T0, CAM, isig)
+                counts["pose"] += 1
+                st.synchronize()   # one batch in flight at a time
+        except Exception as e:  # reported by the main thread
+            errors.append(e)
+
+    P = S.c5_problem(11)
+    kf_o, pts_o, er_o, its_o = oracle.local_ba(CAM, P)
+    th = threading.Thread(target=tracking)
+    th.start()
+    try:
+        while counts["frontend"] < 2:  # the tracking load is on the device before the solve
+            threading.Event().wait(0.005)
+        kf, pts, er, its_full = run_host(G, P)
+        stopped = None
+        for delay in (0.004, 0.006, 0.010, 0.003, 0.015):
+            flag = ctypes.c_bool(False)
+            t = threading.Timer(delay, lambda: setattr(flag, "value", True))
+            t.start()
+            r = run_host(G, P, stop=flag)
+            t.join()
+            if 0 < r[3] < its_full:
+                stopped = r
+                break
+    finally:
+        done.set()
+        th.join()
+    assert not errors, errors
+    assert counts["frontend"] >= 3 and counts["pose"] >= 2, counts
+    assert np.array_equal(er, er_o) and its_full == its_o
+    assert_close(kf, kf_o, P["kf_Tcw"], "C5 poses beside tracking")
+    assert_close(pts, pts_o, P["points"], "C5 points beside tracking")
+    assert stopped is not None, "no stop delay landed mid-run"
+    kf_s, pts_s, er_s, its_s = stopped
+    for c in range(1, 4 * its_full + 40):
+        kf_c, pts_c, er_c, its_c = oracle.local_ba(CAM, P, stop_after=c)
+        if its_c > its_s:
+            break
+        if its_c == its_s and np.array_equal(er_s, er_c):
+            assert_close(kf_s, kf_c, P["kf_Tcw"], "interrupted poses beside tracking")
+            assert_close(pts_s, pts_c, P["points"], "interrupted points beside tracking")
+            return
+    raise AssertionError(f"no oracle stop position reproduces the device's {its_s} iterations")

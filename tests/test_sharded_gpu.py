@@ -1,0 +1,141 @@
+"""configs[2] on the GPU: the frame-sharded front-end job through its
+device half -- slamgpu_pack_frame_records_device -> FrameGather -> unpack_frame_record -- with
+the object bench.py times (slam_framework_amd.sharded.ShardedFrontend).
+
+* world 1, two contexts per step (each one's first frame the halo of its second), two batches in
+  flight, three steps: every frame rank 0 gathered equals the oracle byte for byte -- left/right
+  keypoints and descriptors, u_right / depth, the frame-to-frame map-point ids and match count
+  (frame.cpp:61-111, tracker.cpp:756-824, orb_matcher.cpp:1312-1453) -- and the bench's own
+  gather self-check (ShardedFrontend.check_gather) passes.
+* world 2 (two processes on cuda:0, gloo through host memory, since RCCL needs a GPU per rank):
+  the shards + halos gathered to rank 0 reassemble exactly the world-1 job's gathered bytes."""
+import os
+import socket
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+import sharded_gpu_job as J
+from slam_framework_amd import slamgpu as G
+from slam_framework_amd import synthetic as S
+
+pytestmark = pytest.mark.gpu
+CAM = S.KITTI_CAM
+COLS, ROWS = S.KITTI_COLS, S.KITTI_ROWS
+
+
+@pytest.fixture(scope="module")
+def world1(gpu_lib):
+    """The world-1 job over the same 8 owned frames (1..8) as the world-2 run: 2 contexts of 5."""
+    import torch
+    from slam_framework_amd.sharded import ShardedFrontend
+    dev = torch.device("cuda", 0)
+    Ls, Rs = S.layered_sequence(J.SEED, J.RENDERS)
+    with torch.cuda.stream(torch.cuda.Stream(device=dev)):
+        job = ShardedFrontend(Ls, Rs, CAM, 10, dev, streams=2, inflight=2, gather=True)
+        last = [job.step() for _ in range(J.STEPS)][-1]
+        job.sync()
+    return job, last, Ls, Rs
+
+
+def test_world1_gather_matches_oracle(oracle, world1):
+    job, last, Ls, Rs = world1
+    got = job.gathered()
+    assert [d["frame"] for d in got] == list(range(1, 9))
+    t = oracle.tables()
+    g = oracle.grid_geom(COLS, ROWS)
+    _, _, parts = job.groups[last]
+    cache = {}
+
+    def orc(f):
+        if f not in cache:
+            kl, dl, pl = oracle.extract(t, Ls[f % job.D], True)
+            kr, dr, pr = oracle.extract(t, Rs[f % job.D], True)
+            ur, depth, _ = oracle.stereo(t, kl, dl, kr, dr, pl, pr, CAM[0], CAM[4])
+            cache[f] = (kl, dl, kr, dr, ur, depth)
+        return cache[f]
+
+    for d in got:
+        f = d["frame"]
+        kl, dl, kr, dr, ur, depth = orc(f)
+        assert d["kps_left"].tobytes() == kl.tobytes(), f"frame {f} left keypoints"
+        assert d["kps_right"].tobytes() == kr.tobytes(), f"frame {f} right keypoints"
+        assert np.array_equal(d["desc_left"], dl) and np.array_equal(d["desc_right"], dr)
+        assert d["u_right"].tobytes() == ur.tobytes() and d["depth"].tobytes() == depth.tobytes()
+        # the frame-to-frame search against f - 1 on the queries the device built (batch slot i
+        # of context si holds global frame f)
+        b = int(np.nonzero(job.gframe == f)[0][-1])
+        si, i = divmod(b, job.Bs)
+        assert i >= 1, "an owned frame is never its context's halo slot"
+        pt = parts[si]
+        qs, qc = pt["qs"].cpu().numpy(), pt["qc"].cpu().numpy()
+        q = pt["q"].cpu().numpy().view(G.F2F_QUERY_DTYPE)[qs[i]:qs[i] + qc[i]]
+        pkl, pdl, _, _, _, pdepth = orc(f - 1)
+        idx = np.nonzero(pdepth > 0)[0]
+        assert np.array_equal(q["mp_id"], idx) and np.array_equal(q["desc"], pdl[idx])
+        n_last = len(pkl)
+        last_mp = np.full(n_last, -1, np.int32)
+        last_mp[idx] = idx
+        xyz = np.zeros((n_last, 3), np.float32)
+        xyz[idx] = q["xyz"]
+        mdesc = np.zeros((n_last, 32), np.uint8)
+        mdesc[idx] = q["desc"]
+        nobs = np.zeros(n_last, np.int32)
+        nobs[idx] = 1
+        p = job.poses[b]
+        mp_o = np.full(len(kl), -1, np.int32)
+        nm_o = oracle.search_frame(t, g, kl, dl, ur, mp_o, pkl, last_mp,
+                                   np.zeros(n_last, np.uint8), xyz, mdesc, nobs,
+                                   p["Rcw"].reshape(3, 3), p["tcw"], float(p["tlc_z"]),
+                                   float(p["baseline"]), CAM, 7.0, 0, 1)
+        assert d["nmatches"] == nm_o > 300, f"frame {f}: {d['nmatches']} vs {nm_o}"
+        np.testing.assert_array_equal(d["map_point"], mp_o)
+    info = job.check_gather()
+    assert info["identical"] and info["frames_checked_vs_rank0"] == 8
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def test_world2_shards_reassemble_world1(world1, tmp_path):
+    job, _, _, _ = world1
+    out = str(tmp_path / "rank0.npz")
+    port = _free_port()
+    script = os.path.join(os.path.dirname(os.path.abspath(__file__)), "sharded_gpu_job.py")
+    procs = []
+    for r in range(2):
+        env = dict(os.environ, RANK=str(r), WORLD_SIZE="2", LOCAL_RANK="0",
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, "-u", script, out], env=env))
+    rcs = []
+    for p in procs:
+        try:
+            rcs.append(p.wait(timeout=100))
+        except subprocess.TimeoutExpired:
+            for q in procs:
+                q.kill()
+            raise
+    assert rcs == [0, 0], rcs
+    w2 = np.load(out)
+    assert w2["frames"].tolist() == list(range(1, 9))
+    slot = (job.gat.k - 1) % len(job.gat.send)
+    for k in job.fields():
+        ref = job.gat.field(slot, k).cpu().numpy()
+        assert w2[k].shape == ref.shape, k
+        if k == "frontend":   # records are compared up to their padding
+            for j in range(len(ref)):
+                a, b = G.unpack_frame_record(w2[k][j], job.kc), G.unpack_frame_record(ref[j], job.kc)
+                assert all(a[n].tobytes() == b[n].tobytes() for n in a), f"frame {j + 1}"
+        elif k == "map_point":
+            nkl = [len(G.unpack_frame_record(r, job.kc)["kps_left"]) for r in ref]
+            for j, n in enumerate(nkl):
+                assert np.array_equal(w2[k][j].view(np.int32)[:n], ref[j].view(np.int32)[:n]), j
+        else:
+            assert np.array_equal(w2[k], ref), k
