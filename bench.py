@@ -959,8 +959,8 @@ def host_cpu_share():
             quota = None if q == "max" else round(int(q) / int(per), 2)
     except (OSError, ValueError):
         pass
-    return max(1, min(aff, share)), {"affinity_cpus": aff, "omp_num_threads": share,
-                                     "cgroup_cpu_quota": quota}
+    n = min(aff, share, int(quota) if quota else aff)
+    return max(1, n), {"affinity_cpus": aff, "omp_num_threads": share, "cgroup_cpu_quota": quota}
 
 
 def build_native_oracle():
@@ -1049,7 +1049,8 @@ def cpu_baseline(Ls, Rs, n_frames, device_check=None):
             break
         tc = min(2 * tc, max_threads)
     threads = max(sweep, key=sweep.get)
-    per_thread = max(2, (n_frames or 16 * threads) // threads)
+    # a ~15 s sample at the chosen thread count (n_frames overrides)
+    per_thread = max(2, (n_frames or int(15 * sweep[threads])) // threads)
     done, wall = throughput(threads, per_thread)
 
     # the reference's own threading: frames in sequence, L and R extracted concurrently
@@ -1071,8 +1072,9 @@ def cpu_baseline(Ls, Rs, n_frames, device_check=None):
             "kind": "port", "cpu_model": model, "host_logical_cpus": ncpu,
             "cpu_share": share,
             "thread_sweep_frames_per_s": {str(k): v for k, v in sweep.items()},
-            "threads_chosen_by": "best of the sweep over 1..min(affinity, OMP_NUM_THREADS); the "
-                                 "GPU pool gives each GPU's jobs a 16-CPU share of the host",
+            "threads_chosen_by": "best of the sweep over 1..min(affinity, OMP_NUM_THREADS, cgroup "
+                                 "quota): the GPU pool gives each GPU's jobs a 16-CPU share of "
+                                 "the host (cgroup cpu.max), so more threads only time-slice",
             "build": ("gcc -O3 -march=native -ffp-contract=off (oracle/Makefile native, built on "
                       "this host)" if native else
                       "oracle/liborb_oracle_fast.so: gcc -O3 -march=x86-64-v3 -ffp-contract=off"),

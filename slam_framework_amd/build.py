@@ -59,7 +59,7 @@ def build(force: bool = False, verbose: bool = False) -> str:
     if failed:
         raise RuntimeError("hipcc failed:\n" + "\n".join(failed))
     tmp = LIB + ".tmp"
-    subprocess.run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp, *objs],
+    subprocess.run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp, *objs, "-lz"],
                    check=True)
     os.replace(tmp, LIB)
     build_capi_check()

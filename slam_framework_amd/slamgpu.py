@@ -74,6 +74,9 @@ EXPORTS = [
     # include/slamgpu_kfmatch.h
     "slamgpu_kfmatch_last_error", "slamgpu_search_for_triangulation",
     "slamgpu_search_for_triangulation_device", "slamgpu_fuse", "slamgpu_fuse_device",
+    # include/slamgpu_io.h
+    "slamgpu_io_last_error", "slamgpu_kitti_load_images", "slamgpu_kitti_image_path",
+    "slamgpu_png_info", "slamgpu_png_decode", "slamgpu_imread_png",
 ]
 
 
@@ -140,7 +143,8 @@ def lib():
         L.slamgpu_last_error.restype = C.c_char_p
         L.slamgpu_kp_capacity.argtypes = [vp]
         L.slamgpu_scale_tables.argtypes = [vp, vp, vp, vp, vp, vp]
-        L.slamgpu_orb_scale_tables.argtypes = [C.POINTER(OrbParams), vp, vp, vp, vp, vp]
+        if hasattr(L, "slamgpu_orb_scale_tables"):  # absent from older A/B builds (tools/abl)
+            L.slamgpu_orb_scale_tables.argtypes = [C.POINTER(OrbParams), vp, vp, vp, vp, vp]
         L.slamgpu_extract.argtypes = [vp, vp, sz, vp, vp, ip, C.POINTER(ip)]
         L.slamgpu_get_pyramid_level.argtypes = [vp, ip, ip, vp, sz, C.POINTER(ip), C.POINTER(ip)]
         L.slamgpu_frame_stereo.argtypes = [vp, vp, vp, sz, C.POINTER(Camera)]
@@ -193,6 +197,16 @@ def lib():
         L.slamgpu_undistort_keypoints_device.argtypes = [
             C.POINTER(Camera), vp, ip, vp, C.c_int64, vp, ip, vp, C.c_int64, ip, ip, vp]
         L.slamgpu_download_undistorted_keypoints.argtypes = [vp, ip, vp, ip, C.POINTER(ip)]
+        if hasattr(L, "slamgpu_png_decode"):  # include/slamgpu_io.h (absent from older A/B builds)
+            L.slamgpu_io_last_error.argtypes = []
+            L.slamgpu_io_last_error.restype = C.c_char_p
+            L.slamgpu_kitti_load_images.argtypes = [C.c_char_p, vp, ip, C.POINTER(ip)]
+            L.slamgpu_kitti_image_path.argtypes = [C.c_char_p, ip, ip, C.c_char_p, sz]
+            L.slamgpu_png_info.argtypes = [vp, sz, C.POINTER(ip), C.POINTER(ip), C.POINTER(ip)]
+            L.slamgpu_png_decode.argtypes = [vp, sz, vp, sz, sz, C.POINTER(ip), C.POINTER(ip),
+                                             C.POINTER(ip)]
+            L.slamgpu_imread_png.argtypes = [C.c_char_p, vp, sz, sz, C.POINTER(ip), C.POINTER(ip),
+                                             C.POINTER(ip)]
         L.slamgpu_optimizer_last_error.argtypes = []
         L.slamgpu_optimizer_last_error.restype = C.c_char_p
         _lib = L
@@ -381,6 +395,54 @@ class Context:
             self.h, frame, _ptr(queries), len(queries), nnratio, th, _ptr(map_point),
             _ptr(blocked), len(map_point), C.byref(nm)))
         return nm.value
+
+
+def _io_check(rc, what):
+    if rc != 0:
+        raise SlamGpuError(f"{what} ({rc}): {lib().slamgpu_io_last_error().decode()}")
+
+
+def png_decode(data: bytes):
+    """slamgpu_png_decode: an in-memory PNG -> uint8 array (h, w) or (h, w, c), channels in
+    cv::imread(IMREAD_UNCHANGED) order (include/slamgpu_io.h)."""
+    buf = np.frombuffer(data, np.uint8)
+    w, h, c = C.c_int(), C.c_int(), C.c_int()
+    _io_check(lib().slamgpu_png_info(_ptr(buf), buf.size, C.byref(w), C.byref(h), C.byref(c)),
+              "slamgpu_png_info")
+    out = np.zeros((h.value, w.value * c.value), np.uint8)
+    _io_check(lib().slamgpu_png_decode(_ptr(buf), buf.size, _ptr(out), out.strides[0], out.size,
+                                       C.byref(w), C.byref(h), C.byref(c)), "slamgpu_png_decode")
+    return out if c.value == 1 else out.reshape(h.value, w.value, c.value)
+
+
+def imread_png(path: str):
+    """cv::imread(path, CV_LOAD_IMAGE_UNCHANGED) of a PNG file (main_stereo.cpp:105-106)."""
+    w, h, c = C.c_int(), C.c_int(), C.c_int()
+    p = path.encode()
+    _io_check(lib().slamgpu_imread_png(p, None, 0, 0, C.byref(w), C.byref(h), C.byref(c)),
+              "slamgpu_imread_png")
+    out = np.zeros((h.value, w.value * c.value), np.uint8)
+    _io_check(lib().slamgpu_imread_png(p, _ptr(out), out.strides[0], out.size, C.byref(w),
+                                       C.byref(h), C.byref(c)), "slamgpu_imread_png")
+    return out if c.value == 1 else out.reshape(h.value, w.value, c.value)
+
+
+def kitti_load_images(kitti_path: str):
+    """LoadKittiImages (main_stereo.cpp:16-49): (left paths, right paths, timestamps)."""
+    n = C.c_int()
+    p = kitti_path.encode()
+    _io_check(lib().slamgpu_kitti_load_images(p, None, 0, C.byref(n)), "slamgpu_kitti_load_images")
+    ts = np.zeros(n.value, np.float64)
+    _io_check(lib().slamgpu_kitti_load_images(p, _ptr(ts), n.value, C.byref(n)),
+              "slamgpu_kitti_load_images")
+    paths = {2: [], 3: []}
+    buf = C.create_string_buffer(len(p) + 64)
+    for cam in (2, 3):
+        for i in range(n.value):
+            _io_check(lib().slamgpu_kitti_image_path(p, cam, i, buf, len(buf)),
+                      "slamgpu_kitti_image_path")
+            paths[cam].append(buf.value.decode())
+    return paths[2], paths[3], ts
 
 
 def undistort_points(cam, dist_coef, xy):

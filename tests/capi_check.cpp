@@ -23,6 +23,7 @@
 #include <vector>
 
 #include "slamgpu.h"
+#include "slamgpu_adapters.hpp"
 #include "slamgpu_optimizer.h"
 
 namespace {
@@ -82,7 +83,8 @@ int main(int argc, char** argv) {
     return 2;
   }
   const std::string dir = argv[1];
-  for (const char* f : {"/extract.kps", "/extract.desc", "/pose.out", "/lba.out"})
+  for (const char* f : {"/extract.kps", "/extract.desc", "/core.kps", "/core.desc", "/core.pyr1",
+                        "/pose.out", "/lba.out"})
     std::remove((dir + f).c_str());
 
   // ---- ORBextractor::Compute ----
@@ -107,6 +109,22 @@ int main(int argc, char** argv) {
   spit(dir + "/extract.kps", kps.data(), sizeof(slamgpu_keypoint) * n);
   spit(dir + "/extract.desc", desc.data(), 32 * (size_t)n);
   slamgpu_destroy(ctx);
+
+  // ---- the same through the adapters' OpenCV-free ORBextractor (slamgpu_adapters.hpp) ----
+  {
+    slamgpu_adapter::OrbExtractorCore ex(nfeat, 1.2f, 8, 20, 7);
+    std::vector<slamgpu_keypoint> k2;
+    std::vector<uint8_t> d2;
+    const int n2 = ex.Compute(reinterpret_cast<const uint8_t*>(img.data()), rows, cols,
+                              (size_t)cols, k2, d2);
+    if (n2 != n || (int)k2.size() != n || d2.size() != 32 * (size_t)n) return 3;
+    spit(dir + "/core.kps", k2.data(), sizeof(slamgpu_keypoint) * n2);
+    spit(dir + "/core.desc", d2.data(), d2.size());
+    const std::vector<std::vector<uint8_t>>& pyr = ex.GetImagePyramid();
+    if ((int)pyr.size() != 8 || ex.pyramid_size(0).first != cols) return 3;
+    spit(dir + "/core.pyr1", pyr[1].data(), pyr[1].size());
+    if (ex.GetScaleFactors().size() != 8 || ex.GetInverseScaleSigmaSquares()[7] <= 0.f) return 3;
+  }
 
   // ---- Optimizer::PoseOptimization ----
   {

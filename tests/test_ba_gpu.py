@@ -228,6 +228,7 @@ def test_local_ba_beside_tracking_with_stop(oracle, gpu_lib):
     reproducing the device's iteration count)."""
     import ctypes
     import threading
+    import time
 
     import torch
     G = gpu_lib
@@ -265,14 +266,17 @@ def test_local_ba_beside_tracking_with_stop(oracle, gpu_lib):
     try:
         while counts["frontend"] < 2:  # the tracking load is on the device before the solve
             threading.Event().wait(0.005)
+        t0 = time.perf_counter()
         kf, pts, er, its_full = run_host(G, P)
-        stopped = None
-        for delay in (0.004, 0.006, 0.010, 0.003, 0.015):
+        t_full = time.perf_counter() - t0
+        stopped, tried = None, []
+        for frac in (0.5, 0.3, 0.7, 0.4, 0.6, 0.2, 0.8):   # the flag raised part-way through
             flag = ctypes.c_bool(False)
-            t = threading.Timer(delay, lambda: setattr(flag, "value", True))
+            t = threading.Timer(frac * t_full, lambda: setattr(flag, "value", True))
             t.start()
             r = run_host(G, P, stop=flag)
             t.join()
+            tried.append((round(frac * t_full * 1e3, 2), r[3]))
             if 0 < r[3] < its_full:
                 stopped = r
                 break
@@ -284,7 +288,8 @@ def test_local_ba_beside_tracking_with_stop(oracle, gpu_lib):
     assert np.array_equal(er, er_o) and its_full == its_o
     assert_close(kf, kf_o, P["kf_Tcw"], "C5 poses beside tracking")
     assert_close(pts, pts_o, P["points"], "C5 points beside tracking")
-    assert stopped is not None, "no stop delay landed mid-run"
+    assert stopped is not None, f"no stop delay landed mid-run: (ms, iterations) {tried}, full run " \
+        f"{t_full * 1e3:.2f} ms, {its_full} iterations"
     kf_s, pts_s, er_s, its_s = stopped
     for c in range(1, 4 * its_full + 40):
         kf_c, pts_c, er_c, its_c = oracle.local_ba(CAM, P, stop_after=c)

@@ -63,6 +63,14 @@ def test_cpp_caller_matches_golden_and_oracle(oracle, gpu_lib, tmp_path):
     desc = np.fromfile(os.path.join(tmp_path, "extract.desc"), np.uint8)
     assert kps.tobytes() == z["keypoints"].tobytes()
     assert desc.tobytes() == z["descriptors"].tobytes()
+    # the adapters' OpenCV-free ORBextractor (include/slamgpu_adapters.hpp): the same outputs, and
+    # GetImagePyramid's level 1 = the oracle's resize of the image
+    assert np.fromfile(os.path.join(tmp_path, "core.kps"), np.uint8).tobytes() == kps.tobytes()
+    assert np.fromfile(os.path.join(tmp_path, "core.desc"), np.uint8).tobytes() == desc.tobytes()
+    t = oracle.tables(nfeatures=500)
+    _, _, pyr = oracle.extract(t, z["image"], True)
+    assert np.fromfile(os.path.join(tmp_path, "core.pyr1"), np.uint8).tobytes() == \
+        np.ascontiguousarray(pyr.level(1)).tobytes()
     # PoseOptimization: the oracle's inlier count and outliers, pose within the tolerance
     out = np.fromfile(os.path.join(tmp_path, "pose.out"), np.uint8)
     n_inl = int(out[:4].view(np.int32)[0])

@@ -9,5 +9,5 @@ for f in $src/*.hip $src/*.cpp; do
   /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC -ffp-contract=off --offload-arch=gfx950 "$@" -c $f -o $obj/$(basename $f).o &
 done
 wait
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o tools/abl/libslamgpu_$name.so $obj/*.o
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o tools/abl/libslamgpu_$name.so $obj/*.o -lz
 echo tools/abl/libslamgpu_$name.so
