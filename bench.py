@@ -648,6 +648,15 @@ def bench_local_ba(dev, with_cpu):
             S.KITTI_CAM, PG["inv_sigma2"], n_iterations=10), reps=5)
         drop[f"global_ba_{nkf}kf"] = {"ms": round(ms, 3), "lm_iterations": r[2], "keyframes": nkf,
                                       "points": npt, "observations": int(len(PG["obs"]))}
+    # a map-scale global BA after a loop closure (GlobalBundleAdjustemnt over every keyframe,
+    # optimizer.cpp:18-31): a closed loop of 1500 keyframes, S in block-profile storage
+    PM = S.map_problem(1540, 1500)
+    ms, r = wall_ms(lambda: G.Optimizer.BundleAdjustment(
+        PM["kf_Tcw"], PM["kf_mode"], PM["points"], PM["point_obs_start"], PM["obs"],
+        S.KITTI_CAM, PM["inv_sigma2"], n_iterations=10), reps=2)
+    drop["global_ba_1500kf_loop"] = {"ms": round(ms, 3), "lm_iterations": r[2], "keyframes": 1500,
+                                     "points": int(len(PM["points"])),
+                                     "observations": int(len(PM["obs"]))}
     # the loop closer's optimisers: OptimizeSim3 on one loop candidate and
     # OptimizeEssentialGraph over a 400-keyframe loop, with the oracle on one host thread beside
     isig = S.level_inv_sigma2()
@@ -663,6 +672,10 @@ def bench_local_ba(dev, with_cpu):
         sys.path.insert(0, os.path.join(ROOT, "tests"))
         import oracle_lib as O
         O.build()
+        t0 = time.perf_counter()
+        O.global_ba(S.KITTI_CAM, PM, 10, True)
+        drop["global_ba_1500kf_loop"]["oracle_1thread_ms"] = round(
+            1e3 * (time.perf_counter() - t0), 1)
         t0 = time.perf_counter()
         O.optimize_sim3(S.KITTI_CAM, S.KITTI_CAM, isig, isig, m3, S3, 10.0, False)
         drop["optimize_sim3_300"]["oracle_1thread_ms"] = round(1e3 * (time.perf_counter() - t0), 3)

@@ -88,8 +88,10 @@ typedef struct {
 #define SLAMGPU_BA_MAX_LOCAL_KF 24
 #define SLAMGPU_BA_MAX_KF 256
 /* Largest optimised window of the single-problem calls (slamgpu_local_bundle_adjustment,
- * slamgpu_global_bundle_adjustment: one problem over a cooperative grid, S dense in HBM). */
-#define SLAMGPU_BA_COOP_MAX_KF 1024
+ * slamgpu_global_bundle_adjustment: one problem over a cooperative grid, S in block-profile
+ * storage in HBM -- its envelope follows the keyframes' co-observations, so a trajectory's map
+ * stays near-banded; the bound is the factorisation's LDS row lists). */
+#define SLAMGPU_BA_COOP_MAX_KF 4096
 
 /* Replaces: void Optimizer::LocalBundleAdjustment(KeyFrame*, bool* stop_flag, const Map&)
  * (optimizer.cpp:413-716) after its graph gathering -- any local window (up to

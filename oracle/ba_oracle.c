@@ -16,8 +16,9 @@
 //   g2o/core/block_solver.hpp:351-600               Schur complement on the points, setLambda on
 //                                                   every diagonal block, back-substitution
 //   g2o/solvers/linear_solver_eigen.h:94-120        LDLT of the reduced pose system (fails only on
-//                                                   an exact zero pivot); dense here, without the
-//                                                   AMD permutation -- the same solution to rounding
+//                                                   an exact zero pivot); in keyframe order on the
+//                                                   block profile (skyline) instead of Eigen's AMD
+//                                                   permutation -- the same solution to rounding
 //   g2o/core/optimization_algorithm_levenberg.cpp   as in pose_oracle.c
 // Eigen's 3x3 inverse (cofactors over the determinant) inverts each point block.
 #include <float.h>
@@ -238,32 +239,84 @@ static void inverse3(const double m[9], double r[9]) {
 #undef M
 }
 
-// Dense LDLT of the n x n reduced system (lower triangle used), no pivoting; fails on d == 0.
-static int ldlt_solve(double* A, int n, const double* b, double* x) {
+// The reduced system in block-profile (skyline) storage: scalar row i holds columns fc(i) ..
+// i, fc(i) = 6 * first[i / 6] (first[k] = the smallest optimised keyframe sharing a point with
+// k), at L[rb[i] + k]. The LDLT's fill-in stays inside this envelope, and the loops below are the
+// dense LDLT's with the terms outside it -- exact zeros -- skipped, in the same order: the same
+// numbers as the dense factorisation (no pivoting; fails on d == 0).
+typedef struct {
+  int n;
+  int* fc;        // [n] first column of each row
+  int64_t* rb;    // [n] row base: element (i, k) at L[rb[i] + k]
+  double* L;
+} profile_mat;
+
+static int profile_init(profile_mat* P, const ba* B) {
+  const int K = B->n_free, n = 6 * K;
+  int* first = (int*)malloc(sizeof(int) * (K > 0 ? K : 1));
+  for (int k = 0; k < K; k++) first[k] = k;
+  for (int p = 0; p < B->n_pts; p++) {
+    int mn = K;
+    for (int e = B->pstart[p]; e < B->pstart[p + 1]; e++) {
+      const int k = B->free_idx[B->obs[e].keyframe];
+      if (k >= 0 && k < mn) mn = k;
+    }
+    for (int e = B->pstart[p]; e < B->pstart[p + 1]; e++) {
+      const int k = B->free_idx[B->obs[e].keyframe];
+      if (k >= 0 && mn < first[k]) first[k] = mn;
+    }
+  }
+  P->n = n;
+  P->fc = (int*)malloc(sizeof(int) * (n > 0 ? n : 1));
+  P->rb = (int64_t*)malloc(sizeof(int64_t) * (n > 0 ? n : 1));
+  int64_t nnz = 0;
+  for (int i = 0; i < n; i++) {
+    P->fc[i] = 6 * first[i / 6];
+    P->rb[i] = nnz - P->fc[i];
+    nnz += i - P->fc[i] + 1;
+  }
+  free(first);
+  P->L = (double*)calloc((size_t)nnz + 1, sizeof(double));
+  return P->L != NULL;
+}
+
+static void profile_free(profile_mat* P) {
+  free(P->fc);
+  free(P->rb);
+  free(P->L);
+}
+
+#define PL(P, i, k) ((P)->L[(P)->rb[i] + (k)])
+
+static int ldlt_solve_profile(profile_mat* P, const double* b, double* x) {
+  const int n = P->n;
   double* d = (double*)malloc(sizeof(double) * (n > 0 ? n : 1));
   for (int j = 0; j < n; j++) {
-    double dj = A[(size_t)n * j + j];
-    for (int k = 0; k < j; k++) dj -= A[(size_t)n * j + k] * A[(size_t)n * j + k] * d[k];
+    double dj = PL(P, j, j);
+    for (int k = P->fc[j]; k < j; k++) dj -= PL(P, j, k) * PL(P, j, k) * d[k];
     if (dj == 0.0) {
       free(d);
       return 0;
     }
     d[j] = dj;
     for (int i = j + 1; i < n; i++) {
-      double s = A[(size_t)n * i + j];
-      for (int k = 0; k < j; k++) s -= A[(size_t)n * i + k] * A[(size_t)n * j + k] * d[k];
-      A[(size_t)n * i + j] = s / dj;
+      if (P->fc[i] > j) continue;  // L(i, j) = 0 outside the envelope
+      double s = PL(P, i, j);
+      const int k0 = P->fc[i] > P->fc[j] ? P->fc[i] : P->fc[j];
+      for (int k = k0; k < j; k++) s -= PL(P, i, k) * PL(P, j, k) * d[k];
+      PL(P, i, j) = s / dj;
     }
   }
   for (int i = 0; i < n; i++) {
     double s = b[i];
-    for (int k = 0; k < i; k++) s -= A[(size_t)n * i + k] * x[k];
+    for (int k = P->fc[i]; k < i; k++) s -= PL(P, i, k) * x[k];
     x[i] = s;
   }
   for (int i = 0; i < n; i++) x[i] /= d[i];
   for (int i = n - 1; i >= 0; i--) {
     double s = x[i];
-    for (int k = i + 1; k < n; k++) s -= A[(size_t)n * k + i] * x[k];
+    for (int k = i + 1; k < n; k++)
+      if (P->fc[k] <= i) s -= PL(P, k, i) * x[k];
     x[i] = s;
   }
   free(d);
@@ -273,12 +326,13 @@ static int ldlt_solve(double* A, int n, const double* b, double* x) {
 // BlockSolver::solve with lambda on every diagonal block: xp (poses), xl (points).
 static int schur_solve(ba* B, double lambda, double* xp, double* xl, double* Dinv) {
   const int n = 6 * B->n_free;
-  double* S = (double*)calloc((size_t)n * n + 1, sizeof(double));
+  profile_mat S;
+  if (!profile_init(&S, B)) return 0;
   double* bs = (double*)malloc(sizeof(double) * (n + 1));
   for (int k = 0; k < B->n_free; k++)
     for (int i = 0; i < 6; i++) {
-      for (int j = 0; j < 6; j++) S[(size_t)n * (6 * k + i) + 6 * k + j] = B->Hpp[36 * k + 6 * i + j];
-      S[(size_t)n * (6 * k + i) + 6 * k + i] += lambda;
+      for (int j = 0; j <= i; j++) PL(&S, 6 * k + i, 6 * k + j) = B->Hpp[36 * k + 6 * i + j];
+      PL(&S, 6 * k + i, 6 * k + i) += lambda;
       bs[6 * k + i] = B->bp[6 * k + i];
     }
   for (int p = 0; p < B->n_pts; p++) {
@@ -302,17 +356,19 @@ static int schur_solve(ba* B, double lambda, double* xp, double* xl, double* Din
         bs[6 * k1 + i] -= B1[3 * i] * db[0] + B1[3 * i + 1] * db[1] + B1[3 * i + 2] * db[2];
       for (int e2 = B->pstart[p]; e2 < B->pstart[p + 1]; e2++) {
         const int k2 = B->free_idx[B->obs[e2].keyframe];
-        if (!B->active[e2] || k2 < 0) continue;
+        if (!B->active[e2] || k2 < 0 || k2 > k1) continue;  // the lower part
         const double* B2 = &B->Hpl[18 * e2];
         for (int i = 0; i < 6; i++)
-          for (int j = 0; j < 6; j++)
-            S[(size_t)n * (6 * k1 + i) + 6 * k2 + j] -=
+          for (int j = 0; j < 6; j++) {
+            if (k2 == k1 && j > i) continue;
+            PL(&S, 6 * k1 + i, 6 * k2 + j) -=
                 BD[3 * i] * B2[3 * j] + BD[3 * i + 1] * B2[3 * j + 1] + BD[3 * i + 2] * B2[3 * j + 2];
+          }
       }
     }
   }
-  const int ok = ldlt_solve(S, n, bs, xp);
-  free(S);
+  const int ok = ldlt_solve_profile(&S, bs, xp);
+  profile_free(&S);
   free(bs);
   if (!ok) return 0;
   for (int p = 0; p < B->n_pts; p++) {

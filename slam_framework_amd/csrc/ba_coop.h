@@ -47,7 +47,13 @@ struct CoopWs {
   double* hpp_tot;     // [K][27] their totals (the keyframe's last chunk, chunk order)
   int32_t* kf_arrive;  // [K] chunk arrival counters
   int32_t* run_arrive; // [pairs_cap] chunk arrival counters per run
-  double* S;           // [n][n] reduced camera system (dense; the lower blocks of each run)
+  double* S;           // reduced camera system, lower part in block-profile storage (below)
+  // block profile of S (host-computed from the co-observations): block row I holds block columns
+  // pfirst[I] .. I; scalar row i holds columns 6 pfirst[i / 6] .. i at S[prow[i] + k]. Every
+  // fill-in of the LDLT stays inside this envelope.
+  const int32_t* pfirst;  // [K]
+  const int64_t* prow;    // [n]
+  int64_t pnnz;           // doubles of the profile
   double* bs;          // [n] reduced right-hand side
   int nch;
   int32_t* run_nch;    // [pairs_cap] assembly chunks per run
@@ -55,7 +61,7 @@ struct CoopWs {
   int32_t* chunk_run;  // [chunks] run of each chunk
   int32_t* n_chunks;   // [1]
   double* chunk_part;  // [chunks][42] partial S block (36) and reduced rhs (6) sums
-  double* fac;         // factor storage when n > kCoopLdsN: packed L (n(n+1)/2), V (6n), dg, rhs
+  double* fac;         // factor storage when n > kCoopLdsN: profile L (pnnz), V (6n), dg, rhs, idg
   double* xp;          // [n] pose step of the last successful solve
   double* part;        // [G][8] work-group partials + [8] scalars of work-group 0
   uint32_t* bar;       // grid barrier: [0] arrivals, [1] generation
@@ -92,7 +98,7 @@ constexpr int kCoopLdsN = 144;  // reduced systems up to 6 x 24 keyframes factor
 
 // Bytes of the workspace for a problem (base = nullptr) or lays it out.
 CoopWs coop_layout(void* base, int n_kf, int n_pts, int n_obs, int K, int pairs_cap, int G,
-                   size_t* bytes);
+                   int64_t pnnz, size_t* bytes);
 
 // Enqueues the whole schedule on `st`: setup, then per phase the structure build and the
 // cooperative LM kernel, the outlier pass between phases (LocalBA), the erase list and write-back.

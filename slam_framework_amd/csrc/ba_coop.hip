@@ -518,11 +518,10 @@ __device__ void assemble(const CoopWs& w, int K, double lambda, int n_chunks) {
       sv = (((sv + a0) + a1) + a2) + a3;
     }
     for (; k < nch; k++) sv += ld_wt(pp + (size_t)k * kCP);
-    const int n = 6 * K;
     if (lane < 36) {
       double base = 0.0;
       if (diag) base = w.hpp_tot[(size_t)kh * 27 + hidx(c, rr)] + (rr == c ? lambda : 0.0);
-      w.S[(size_t)(6 * kh + rr) * n + 6 * kl + c] = base - sv;
+      w.S[w.prow[6 * kh + rr] + 6 * kl + c] = base - sv;
     } else {
       w.bs[6 * kh + lane - 36] = w.hpp_tot[(size_t)kh * 27 + 21 + lane - 36] - sv;
     }
@@ -547,7 +546,7 @@ __device__ __forceinline__ void build_S(const CoopWs& w, int K, double lambda, P
         while (tri(i) > q) i--;
         j = q - tri(i);
       }
-      v[u] = q < nl ? w.S[(size_t)i * n + j] : 0.0;
+      v[u] = q < nl && j >= 6 * w.pfirst[i / 6] ? w.S[w.prow[i] + j] : 0.0;
     }
 #pragma unroll
     for (int u = 0; u < 8; u++)
@@ -560,6 +559,34 @@ __device__ __forceinline__ void build_S(const CoopWs& w, int K, double lambda, P
     if (kf_active(w, f)) continue;
     Lp[sidx(6 * f + i, 6 * f + i)] = 1.0;
     rhs[6 * f + i] = 0.0;
+  }
+  __syncthreads();
+}
+
+// Work-group 0, 6K > kCoopLdsN: the profile S copied to the factor storage (the same layout),
+// the reduced rhs, and I / 0 for the rows of optimised keyframes left without active edges.
+__device__ void build_S_profile(const CoopWs& w, int K, double* Lp, double* rhs) {
+  const int tid = threadIdx.x, n = 6 * K;
+  const size_t nnz = (size_t)w.pnnz;
+  size_t q = (size_t)tid * 2;
+  for (; q + 2 * kT * 3 + 1 < nnz; q += 2 * kT * 4) {  // 4 x 16 B in flight per thread
+    double2 v[4];
+#pragma unroll
+    for (int u = 0; u < 4; u++) v[u] = *reinterpret_cast<const double2*>(w.S + q + 2 * kT * u);
+#pragma unroll
+    for (int u = 0; u < 4; u++) *reinterpret_cast<double2*>(Lp + q + 2 * kT * u) = v[u];
+  }
+  for (; q < nnz; q += 2 * kT) {
+    Lp[q] = w.S[q];
+    if (q + 1 < nnz) Lp[q + 1] = w.S[q + 1];
+  }
+  for (int i = tid; i < n; i += kT) rhs[i] = w.bs[i];
+  __syncthreads();
+  for (int t = tid; t < 6 * K; t += kT) {
+    const int f = t / 6;
+    if (kf_active(w, f)) continue;
+    Lp[w.prow[t] + t] = 1.0;
+    rhs[t] = 0.0;
   }
   __syncthreads();
 }
@@ -786,6 +813,220 @@ __device__ __forceinline__ void factor_solve(CoopShared& sh, const CoopWs& w, in
   fs_tick(12);
 }
 
+// The same LDLT for 6K > kCoopLdsN on the block-profile storage (w.prow / w.pfirst): row i holds
+// columns 6 pfirst[i / 6] .. i, and every fill-in stays inside that envelope, so block column J
+// only touches the active block rows A_J = {I > J : pfirst[I] <= J} -- a band of a few dozen
+// keyframes along the trajectory, plus the rows loop closures reach back from. A_J is kept in
+// LDS (unordered: every element is updated by one lane per column, so the results do not depend
+// on the order) and A_{J+1} is collected while column J's trailing update runs. Otherwise as
+// factor_solve: thread-per-row panel with the forward solve fused, wave 0 updating and factoring
+// the next diagonal block while the other waves apply the trailing update (A_J x A_J below it),
+// two work-group barriers per block column; then D^-1 and the blocked backward solve by wave 0.
+__device__ void factor_solve_profile(CoopShared& sh, const CoopWs& w, int K, double* Lp,
+                                     double* rhs, double* dg, double* idg, double* V) {
+#pragma clang fp contract(fast)  // tolerance-compared FP64 path
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, n = 6 * K;
+  const int64_t* prow = w.prow;
+  const int32_t* pfirst = w.pfirst;
+  // A_J lists in the (unused here) LDS factor storage: two buffers of K entries + 2 counters
+  int* const lists = reinterpret_cast<int*>(sh.S);
+  int* const cnt = lists + 2 * K;
+  if (tid == 0) {
+    sh.ok = 1;
+    cnt[0] = 0;
+  }
+  auto diag_factor = [&](int J) {  // as in factor_solve, on the profile rows
+    if (lane != 0) return;
+    const int j0 = 6 * J;
+    double A[21], y[6];
+#pragma unroll
+    for (int r = 0; r < 6; r++) {
+      y[r] = rhs[j0 + r];
+#pragma unroll
+      for (int k = 0; k <= r; k++) A[r * (r + 1) / 2 + k] = Lp[prow[j0 + r] + j0 + k];
+    }
+    bool good = true;
+#pragma unroll
+    for (int c = 0; c < 6; c++) {
+      const double d = A[c * (c + 3) / 2];
+      good = good && d != 0.0;
+      const double rd = d != 0.0 ? 1.0 / d : 0.0;
+      idg[j0 + c] = rd;
+      double l[6];
+#pragma unroll
+      for (int r = c + 1; r < 6; r++) {
+        l[r] = A[r * (r + 1) / 2 + c] * rd;
+        y[r] -= l[r] * y[c];
+        A[r * (r + 1) / 2 + c] = l[r];
+      }
+#pragma unroll
+      for (int r = c + 1; r < 6; r++) {
+        const double ld = l[r] * d;
+#pragma unroll
+        for (int k = c + 1; k <= r; k++) A[r * (r + 1) / 2 + k] -= ld * l[k];
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < 6; r++) {
+#pragma unroll
+      for (int k = 0; k < r; k++) Lp[prow[j0 + r] + j0 + k] = A[r * (r + 1) / 2 + k];
+      dg[j0 + r] = A[r * (r + 3) / 2];
+      rhs[j0 + r] = y[r];
+    }
+    if (!good) sh.ok = 0;
+  };
+  __syncthreads();
+  for (int I = 1 + tid; I < K; I += kT)  // A_0
+    if (pfirst[I] <= 0) lists[atomicAdd(&cnt[0], 1)] = I;
+  if (wid == 0) diag_factor(0);
+  __syncthreads();
+  for (int J = 0; J < K; J++) {
+    const int j0 = 6 * J;
+    if (!sh.ok) return;
+    const int* act = lists + (J & 1) * K;
+    int* nxt = lists + ((J + 1) & 1) * K;
+    const int na = cnt[J & 1], nr = 6 * na;
+    {  // panel rows of the active blocks (forward solve fused)
+      double Ljj[15], rdg[6], yj[6];
+      int q = 0;
+#pragma unroll
+      for (int c = 1; c < 6; c++)
+#pragma unroll
+        for (int k = 0; k < c; k++) Ljj[q++] = Lp[prow[j0 + c] + j0 + k];
+#pragma unroll
+      for (int c = 0; c < 6; c++) {
+        rdg[c] = idg[j0 + c];
+        yj[c] = rhs[j0 + c];
+      }
+      for (int t = tid; t < nr; t += kT) {
+        const int i = 6 * act[t / 6] + t % 6;
+        const int64_t ro = prow[i] + j0;
+        double v[6];
+        q = 0;
+#pragma unroll
+        for (int c = 0; c < 6; c++) {
+          double sv = Lp[ro + c];
+#pragma unroll
+          for (int k = 0; k < c; k++) sv -= v[k] * Ljj[q++];
+          v[c] = sv;
+        }
+        double r = rhs[i];
+#pragma unroll
+        for (int c = 0; c < 6; c++) {
+          V[(size_t)i * 6 + c] = v[c];
+          const double l = v[c] * rdg[c];
+          Lp[ro + c] = l;
+          r -= l * yj[c];
+        }
+        rhs[i] = r;
+      }
+    }
+    if (tid == 0) cnt[(J + 1) & 1] = 0;
+    __syncthreads();
+    const bool next_active = J + 1 < K && pfirst[J + 1] <= J;
+    if (wid == 0) {
+      if (J + 1 < K) {  // block J + 1: its update by column J (when it is active), then its LDLT
+        if (next_active && lane < 21) {
+          int r = 0;
+          while ((r + 1) * (r + 2) / 2 <= lane) r++;
+          const int c = lane - r * (r + 1) / 2;
+          const int i = j0 + 6 + r, k = j0 + 6 + c;
+          const int64_t ro = prow[i];
+          double sv = Lp[ro + k];
+#pragma unroll
+          for (int m = 0; m < 6; m++) sv -= Lp[ro + j0 + m] * V[(size_t)k * 6 + m];
+          Lp[ro + k] = sv;
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+        diag_factor(J + 1);
+      }
+    } else {
+      // trailing update A(i, k) -= L(i, J) V(k)^T over the active rows i outside block J + 1 and
+      // the active columns k <= i: a wave per group of 4 rows, lanes over the columns
+      constexpr int kTW = kW - 1;
+      for (int t0 = wid - 1; t0 < nr; t0 += 4 * kTW) {
+        int ic[4];
+        int64_t ro[4];
+        double l[4][6];
+        bool live[4];
+#pragma unroll
+        for (int a = 0; a < 4; a++) {
+          const int t = t0 + a * kTW;
+          const int tt = t < nr ? t : nr - 1;
+          ic[a] = 6 * act[tt / 6] + tt % 6;
+          live[a] = t < nr && ic[a] >= j0 + 12;  // block J + 1 is wave 0's
+          ro[a] = prow[ic[a]];
+#pragma unroll
+          for (int c = 0; c < 6; c++) l[a][c] = Lp[ro[a] + j0 + c];
+        }
+        if (!(live[0] || live[1] || live[2] || live[3])) continue;
+        for (int m = lane; m < nr; m += 64) {
+          const int k = 6 * act[m / 6] + m % 6;
+          double v[6];
+#pragma unroll
+          for (int c = 0; c < 6; c++) v[c] = V[(size_t)k * 6 + c];
+#pragma unroll
+          for (int a = 0; a < 4; a++) {
+            if (!live[a] || k > ic[a]) continue;
+            double sv = Lp[ro[a] + k];
+#pragma unroll
+            for (int c = 0; c < 6; c++) sv -= l[a][c] * v[c];
+            Lp[ro[a] + k] = sv;
+          }
+        }
+      }
+    }
+    for (int I = J + 2 + tid; I < K; I += kT)  // A_{J+1}
+      if (pfirst[I] <= J + 1) nxt[atomicAdd(&cnt[(J + 1) & 1], 1)] = I;
+    if (tid == 0)  // heartbeat for the work-groups waiting at the next grid barrier
+      __hip_atomic_fetch_add(&w.ctl[CTL_BEAT], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
+  }
+  if (wid == 0) {  // z = D^-1 y; L^T x = z from the last 6x6 block up, over each block's envelope
+    for (int i = lane; i < n; i += 64) rhs[i] /= dg[i];
+    for (int J = K - 1; J >= 0; J--) {
+      const int j0 = 6 * J;
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+      double x[6] = {0, 0, 0, 0, 0, 0};
+      if (lane == 0) {
+        double Lb[15];
+#pragma unroll
+        for (int c = 1; c < 6; c++)
+#pragma unroll
+          for (int r = 0; r < c; r++) Lb[c * (c - 1) / 2 + r] = Lp[prow[j0 + c] + j0 + r];
+#pragma unroll
+        for (int r = 0; r < 6; r++) x[r] = rhs[j0 + r];
+#pragma unroll
+        for (int c = 5; c >= 0; c--)
+#pragma unroll
+          for (int r = 0; r < c; r++) x[r] -= Lb[c * (c - 1) / 2 + r] * x[c];
+#pragma unroll
+        for (int r = 0; r < 6; r++) rhs[j0 + r] = x[r];
+      }
+#pragma unroll
+      for (int c = 0; c < 6; c++) x[c] = rl64(x[c], 0);
+      int64_t rb[6];
+#pragma unroll
+      for (int c = 0; c < 6; c++) rb[c] = prow[j0 + c];
+      for (int i = 6 * pfirst[J] + lane; i < j0; i += 64) {
+        double sx = rhs[i];
+#pragma unroll
+        for (int c = 0; c < 6; c++) sx -= Lp[rb[c] + i] * x[c];
+        rhs[i] = sx;
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    for (int i = lane; i < n; i += 64) w.xp[i] = rhs[i];
+  }
+  __syncthreads();
+}
+
 // optimizer.cpp:632-665 between the two optimize() calls: chi2 > threshold or depth <= 0 ->
 // level 1 (edge-parallel over the grid).
 __device__ void mark_outliers(const CoopWs& w, const CoopProblem& pb, const PoseParams& P,
@@ -828,8 +1069,8 @@ __device__ void compact_runs(const CoopWs& w, int n_runs, int n) {
       w.run_cnt[r] = kept;
       w.run_nch[r] = (kept + kChunk - 1) / kChunk;
     }
-    if (kept == 0 && cnt > 0 && lane < 36)  // the block left the system: no chunk rewrites it
-      w.S[(size_t)(6 * kh + lane / 6) * n + 6 * kl + lane % 6] = 0.0;
+    if (kept == 0 && cnt > 0 && lane < 36 && (!diag || lane % 6 <= lane / 6))
+      w.S[w.prow[6 * kh + lane / 6] + 6 * kl + lane % 6] = 0.0;  // the block left the system
   }
 }
 
@@ -896,7 +1137,7 @@ __global__ __launch_bounds__(kT) void ba_coop_kernel(PoseParams P, CoopProblem p
   typedef __attribute__((address_space(3))) double* LdsPtr;
   const bool in_lds = n <= kCoopLdsN;
   double* const Gp = w.fac;
-  double* const Gv = Gp + (size_t)n * (n + 1) / 2;
+  double* const Gv = Gp + (size_t)w.pnnz;
   double* const Gd = Gv + (size_t)6 * n;
   double* const Gr = Gd + n;
   double* const Gi = Gr + n;
@@ -990,9 +1231,9 @@ __global__ __launch_bounds__(kT) void ba_coop_kernel(PoseParams P, CoopProblem p
           factor_solve(sh, w, K, (LdsPtr)sh.S, (LdsPtr)sh.rhs, (LdsPtr)sh.dg, (LdsPtr)sh.idg,
                        (LdsPtr)sh.V);
         } else {
-          build_S(w, K, lambda, Gp, Gr);
+          build_S_profile(w, K, Gp, Gr);
           tick(5);
-          factor_solve(sh, w, K, Gp, Gr, Gd, Gi, Gv);
+          factor_solve_profile(sh, w, K, Gp, Gr, Gd, Gi, Gv);
         }
         tick(6);
         double sc = 0.0;
@@ -1162,7 +1403,7 @@ int key_bits(int K) {
 }  // namespace
 
 CoopWs coop_layout(void* base, int n_kf, int n_pts, int n_obs, int K, int pairs_cap, int G,
-                   size_t* bytes) {
+                   int64_t pnnz, size_t* bytes) {
   auto al = [](size_t x) { return (x + 255) / 256 * 256; };
   size_t off = 0;
   char* b = static_cast<char*>(base);
@@ -1206,10 +1447,11 @@ CoopWs coop_layout(void* base, int n_kf, int n_pts, int n_obs, int K, int pairs_
   w.hpp_tot = reinterpret_cast<double*>(take(8 * 27 * (size_t)K + 8));
   w.kf_arrive = reinterpret_cast<int32_t*>(take(4 * (size_t)K + 4));
   w.run_arrive = reinterpret_cast<int32_t*>(take(4 * (size_t)pc));
-  w.S = reinterpret_cast<double*>(take(8 * (size_t)n * n + 8));
+  w.S = reinterpret_cast<double*>(take(8 * (size_t)pnnz + 8));
+  w.pnnz = pnnz;
   w.bs = reinterpret_cast<double*>(take(8 * (size_t)n + 8));
   w.fac = reinterpret_cast<double*>(
-      take(n > kCoopLdsN ? 8 * ((size_t)n * (n + 1) / 2 + 9 * (size_t)n) : 8));
+      take(n > kCoopLdsN ? 8 * ((size_t)pnnz + 9 * (size_t)n) : 8));
   w.xp = reinterpret_cast<double*>(take(8 * (size_t)n + 8));
   w.part = reinterpret_cast<double*>(take(8 * 8 * (size_t)(G + 1)));
   w.bar = reinterpret_cast<uint32_t*>(take(64));
@@ -1255,7 +1497,7 @@ hipError_t launch_coop_ba(const PoseParams& P, const CoopProblem& pb, const Coop
     e = hipcub::DeviceScan::ExclusiveSum(w.cub_tmp, tb, w.run_cnt, w.run_off, w.pairs_cap, st);
     if (e != hipSuccess) return e;
     if ((e = hipMemsetAsync(w.diag_run, 0xff, 4 * (size_t)pb.K + 4, st)) != hipSuccess) return e;
-    if ((e = hipMemsetAsync(w.S, 0, 8 * 36 * (size_t)pb.K * pb.K + 8, st)) != hipSuccess) return e;
+    if ((e = hipMemsetAsync(w.S, 0, 8 * (size_t)w.pnnz + 8, st)) != hipSuccess) return e;
     if ((e = hipMemsetAsync(w.run_arrive, 0, 4 * (size_t)w.pairs_cap, st)) != hipSuccess) return e;
     if ((e = hipMemsetAsync(w.kf_arrive, 0, 4 * (size_t)pb.K + 4, st)) != hipSuccess) return e;
     SLAMGPU_LAUNCH("ba_coop_runs", st, coop_runs_kernel, blocks(w.pairs_cap), dim3(256), 0, st, w);

@@ -344,6 +344,29 @@ int coop_host(const char* what, const slamgpu_camera* cam, const float* inv_sigm
     pairs += m * (m + 1) / 2;
   }
   if (pairs > (1ll << 30)) return fail(SLAMGPU_ECAP, "%s: %lld Schur pairs", what, pairs);
+  // block profile of the reduced camera system: block row f spans block columns pfirst[f] .. f,
+  // pfirst[f] = the smallest optimised keyframe sharing a map point with f (any observation: a
+  // superset of every phase's active structure). Row i of S at S[prow[i] + k], k <= i.
+  std::vector<int32_t> pfirst(K);
+  for (int f = 0; f < K; f++) pfirst[f] = f;
+  for (int p = 0; p < n_points; p++) {
+    int mn = K;
+    for (int e = point_obs_start[p]; e < point_obs_start[p + 1]; e++) {
+      const int f = free_of[obs[e].keyframe];
+      if (f >= 0 && f < mn) mn = f;
+    }
+    for (int e = point_obs_start[p]; e < point_obs_start[p + 1]; e++) {
+      const int f = free_of[obs[e].keyframe];
+      if (f >= 0 && mn < pfirst[f]) pfirst[f] = mn;
+    }
+  }
+  std::vector<int64_t> prow(6 * (size_t)K);
+  int64_t pnnz = 0;
+  for (int i = 0; i < 6 * K; i++) {
+    const int64_t fc = 6 * (int64_t)pfirst[i / 6];
+    prow[i] = pnnz - fc;
+    pnnz += i - fc + 1;
+  }
   if (local && stop_flag && *stop_flag) {  // optimizer.cpp:616-618: return before optimising
     for (int e = 0; e < n_obs; e++) erase[e] = 0;
     return 0;
@@ -354,14 +377,16 @@ int coop_host(const char* what, const slamgpu_camera* cam, const float* inv_sigm
   OPT_HIPCHECK(hipGetDevice(&dev));
   const int G = coop_grid(dev);
   size_t wsb = 0;
-  coop_layout(nullptr, n_kf, n_points, n_obs, K, (int)pairs, G, &wsb);
+  coop_layout(nullptr, n_kf, n_points, n_obs, K, (int)pairs, G, pnnz, &wsb);
   // inputs and outputs in one region (one DMA each way through a pinned twin), then workspace
   const size_t o_T = 0, o_mode = o_T + al256(64 * (size_t)n_kf);
   const size_t o_pts = o_mode + al256(n_kf + 1), o_ps = o_pts + al256(12 * (size_t)n_points + 4);
   const size_t o_obs = o_ps + al256(4 * ((size_t)n_points + 1));
   const size_t o_free = o_obs + al256(sizeof(slamgpu_ba_obs) * (size_t)n_obs + 4);
   const size_t o_kof = o_free + al256(4 * (size_t)n_kf + 4);
-  const size_t o_er = o_kof + al256(4 * (size_t)K + 4);
+  const size_t o_pf = o_kof + al256(4 * (size_t)K + 4);
+  const size_t o_prow = o_pf + al256(4 * (size_t)K + 4);
+  const size_t o_er = o_prow + al256(8 * 6 * (size_t)K + 8);
   const size_t o_ctl = o_er + al256((size_t)n_obs + 4);
   const size_t o_io = o_ctl + 256, o_ws = o_io;
   HostStage& S = thread_stage();
@@ -377,9 +402,11 @@ int coop_host(const char* what, const slamgpu_camera* cam, const float* inv_sigm
   char* h = S.pin;
   std::lock_guard<std::mutex> device_lock(coop_device_mutex(dev));
   static const bool prof = getenv("SLAMGPU_BA_PROFILE") != nullptr;
-  CoopWs w = coop_layout(b + o_ws, n_kf, n_points, n_obs, K, (int)pairs, G, nullptr);
+  CoopWs w = coop_layout(b + o_ws, n_kf, n_points, n_obs, K, (int)pairs, G, pnnz, nullptr);
   w.free_of_kf = reinterpret_cast<const int32_t*>(b + o_free);
   w.kf_of_free = reinterpret_cast<const int32_t*>(b + o_kof);
+  w.pfirst = reinterpret_cast<const int32_t*>(b + o_pf);
+  w.prow = reinterpret_cast<const int64_t*>(b + o_prow);
   if (!prof) w.prof = nullptr;
   const CoopProblem pb{reinterpret_cast<const slamgpu_ba_obs*>(b + o_obs),
                        reinterpret_cast<const int32_t*>(b + o_ps),
@@ -413,6 +440,8 @@ int coop_host(const char* what, const slamgpu_camera* cam, const float* inv_sigm
     if (n_obs) std::memcpy(h + o_obs, obs, sizeof(slamgpu_ba_obs) * (size_t)n_obs);
     if (n_kf) std::memcpy(h + o_free, free_of.data(), 4 * (size_t)n_kf);
     if (K) std::memcpy(h + o_kof, kf_of.data(), 4 * (size_t)K);
+    if (K) std::memcpy(h + o_pf, pfirst.data(), 4 * (size_t)K);
+    if (K) std::memcpy(h + o_prow, prow.data(), 8 * 6 * (size_t)K);
     OPT_HIPCHECK(hipMemcpyAsync(b, h, o_er, hipMemcpyHostToDevice, S.stream));
     if (mirror) *mirror = *stop_flag ? 1 : 0;
     t_launch0 = clk::now();

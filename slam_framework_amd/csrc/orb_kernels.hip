@@ -11,6 +11,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 #include "device_math.h"
 #include "timing.h"
 #include "orb_geometry.h"
@@ -1736,65 +1738,43 @@ __device__ __forceinline__ int reduce_scatter16(int (&v)[16], int lane) {
 // computeOrbDescriptor (:49-88) on the level blurred by cv::GaussianBlur(7x7, sigma 2) (:1029-1030),
 // with the blur folded in: no blurred pyramid is written or read back. The blur is separable
 // with exact integer sums: a pixel is round(sum_i k_i R_i / 2^16), R_i = the row
-// sums sum_j k_j I(y+i-3, x+j-3) <= 255 * 257 (u16), rounded half to even inside the SSE span
-// x < W - W%4 and half up in the scalar tail. Per keypoint, one wave:
-//   1. row sums of the raw window (rows y-21..y+22, columns x-18..x+21): 220 (row pair, column
-//      quad) tasks, each two dwordx4 loads of raw rows + 2 v_dot4_u32_u8 per sum, the two rows'
-//      sums of a column packed into one dword, one ds_write_b128 per task (table P);
-//   2. the vertical pass over the blurred window's disc only: every pixel an rBRIEF sample can hit
-//      (|p| <= 13 sqrt 2 for every pattern point, so a rounded rotated sample lies within
-//      x^2 + y^2 <= 364 of the keypoint: 1125 of the 37 x 37 pixels), 308 (column, 4-row) tasks
-//      from a compile-time table, each 5 dwords of its column's row-sum pairs, 16 v_dot2_u32_u16,
-//      the column's rounding rule, one packed ds_write_b32 (table B, one byte per pixel);
-//   3. the 512 samples: one ds_read_u8 each.
+// sums sum_j k_j I(y+i-3, x+j-3) <= 255 * 257 (u16). Per keypoint a wave forms the row sums of
+// the 43 x 37 window the samples' columns need (rows y-21..y+21, columns x-18..x+18: 430 lane
+// tasks of 4 columns, one dwordx4 load of the raw row + 2 v_dot4_u32_u8 per column, stored
+// TRANSPOSED as u16 in LDS), then each of the 512 samples takes its 7 vertical row sums as 4
+// dwords of its column (v_alignbit for an odd start) and 4 v_dot2_u32_u16, and rounds with the
+// column's rule (half to even inside the SSE span x < W - W%4, half up in the scalar tail).
 // Border keypoints (the window leaves the image: reflect-101 columns) load bytes one by one.
-// LDS (per wave): P = 10 column quads x kOdQuadStride dwords, B = 37 columns x kOdColBytes.
+// LDS: one 40 x 44 u16 window per wave.
+#ifndef RT_ROWS
+#define RT_ROWS 44
+#endif
 #ifndef RS_PREFETCH
 #define RS_PREFETCH 1
+#endif
+#ifndef OD_FENCE
+#define OD_FENCE 0
 #endif
 #ifndef OD_UNROLL_J
 #define OD_UNROLL_J 1
 #endif
-// P: dword gq * kOdQuadStride + 4 * p + jx holds R(2p, c) | R(2p + 1, c) << 16 for the window
-// column c = 4 gq + jx (23 row pairs per quad; pair 22 only feeds outputs outside the disc).
-// kOdQuadStride = 4 mod 32: a ds_write_b128 group of 8 consecutive quads covers all 32 banks.
-constexpr int kOdQuadStride = 100;
-// B: byte c * kOdColBytes + y holds the blurred pixel (x - 18 + c, y - 18 + y); 11 dwords per
-// column (odd), so a vertical-pass row of consecutive columns writes distinct banks.
-constexpr int kOdColBytes = 44;
-constexpr int kOdPWords = 10 * kOdQuadStride;
-constexpr int kOdBWords = (37 * kOdColBytes + 3) / 4 + 1;  // + a dump dword for idle task slots
-constexpr int kOdBDump = 37 * kOdColBytes;                  // byte offset of the dump dword
-constexpr int kOdWaveWords = (kOdPWords + kOdBWords + 3) & ~3;
-constexpr int kOdVSlots = 320;  // 5 vertical-pass tasks per lane
+#ifndef PAT_PACKED
+#define PAT_PACKED 1
+#endif
+constexpr int kRtCols = 40, kRtRows = RT_ROWS;  // u16 per transposed column (even)
 
-// The vertical pass's tasks, row-major (4-row band outer, column inner: a wave's lanes take
-// consecutive columns of one band, conflict-free in P and B): P dword of (c, pair 2 yq) | B byte
-// of (c, 4 yq) << 10 | c << 21. Idle slots read P's first dwords and write B's dump dword, so
-// every lane runs every slot without a branch.
-struct OdVTasks {
-  uint32_t t[kOdVSlots];
-  int n;
-};
-constexpr OdVTasks make_od_vtasks() {
-  OdVTasks v{};
-  int n = 0;
-  for (int yq = 0; yq < 10; yq++)
-    for (int c = 0; c < 37; c++) {
-      bool hit = false;
-      for (int y = 4 * yq; y < 4 * yq + 4 && y < 37; y++)
-        hit = hit || (c - 18) * (c - 18) + (y - 18) * (y - 18) <= 364;
-      if (hit && n < kOdVSlots)
-        v.t[n++] = (uint32_t)((c >> 2) * kOdQuadStride + 8 * yq + (c & 3)) |
-                   (uint32_t)(c * kOdColBytes + 4 * yq) << 10 | (uint32_t)c << 21;
-    }
-  v.n = n;
-  for (int i = n; i < kOdVSlots; i++) v.t[i] = (uint32_t)kOdBDump << 10;
-  return v;
+__device__ __forceinline__ uint32_t rt_tap(const uint16_t* rt, int sy, int sx, uint32_t K01,
+                                           uint32_t K23, uint32_t K21, uint32_t K0) {
+  const int e0 = (sx + 18) * kRtRows + sy + 18;  // rows sy - 3 .. sy + 3 of column sx
+  const uint32_t* rw = reinterpret_cast<const uint32_t*>(rt) + (e0 >> 1);
+  const uint32_t sh = (uint32_t)(e0 & 1) << 4;
+  const uint32_t w0 = rw[0], w1 = rw[1], w2 = rw[2], w3 = rw[3];
+  const uint32_t p0 = __builtin_amdgcn_alignbit(w1, w0, sh);
+  const uint32_t p1 = __builtin_amdgcn_alignbit(w2, w1, sh);
+  const uint32_t p2 = __builtin_amdgcn_alignbit(w3, w2, sh);
+  const uint32_t p3 = __builtin_amdgcn_alignbit(0u, w3, sh);
+  return dot2u(p0, K01, dot2u(p1, K23, dot2u(p2, K21, dot2u(p3, K0, 0u))));
 }
-constexpr OdVTasks kOdVTasks = make_od_vtasks();
-static_assert(kOdVTasks.n == 308 && kOdVTasks.n <= kOdVSlots, "vertical-pass task table");
-__constant__ OdVTasks c_od_vtasks = kOdVTasks;
 
 #ifdef OD_WAVES
 #define OD_ATTR __attribute__((amdgpu_waves_per_eu(OD_WAVES)))
@@ -1805,7 +1785,7 @@ __global__ __launch_bounds__(256) OD_ATTR void orient_desc_kernel(
     ImageBatch b, const OrbGeom* __restrict__ g, const uint32_t* __restrict__ oct_keys,
     const int* __restrict__ oct_count, KeyPoint* __restrict__ kps, uint8_t* __restrict__ desc,
     int* __restrict__ nkps) {
-  __shared__ __attribute__((aligned(16))) uint32_t s_od[4][kOdWaveWords];
+  __shared__ __attribute__((aligned(16))) uint16_t s_rt[4][1][kRtCols * kRtRows];
   int img, bx;
   xcd_image_block(&img, &bx);
   const int lane = threadIdx.x & 63, wid = wave_id();
@@ -1908,34 +1888,58 @@ __global__ __launch_bounds__(256) OD_ATTR void orient_desc_kernel(
   const float factorPI = (float)(3.14159265358979323846 / 180.0);
   float sa, ca;
   glibc_sincosf(angle * factorPI, &sa, &ca);
-  // Phase 3: per keypoint, the blurred window's disc in LDS (row sums, vertical pass), then its
-  // 256 tests. The lane's 4 tests (8 points) as int8 (x0, y0, x1, y1) words.
+  // Phase 3: per 4 keypoints, the row-summed windows (LDS) then the 512 blurred samples each
+#if PAT_PACKED
+  // the lane's 4 tests (8 points) as int8 (x0, y0, x1, y1) words: 4 VGPRs instead of 32
   uint32_t pat[4];
 #pragma unroll
   for (int r = 0; r < 4; r++)
     pat[r] = reinterpret_cast<const uint32_t*>(c_pattern)[r * 64 + lane];
-  uint32_t vt[kOdVSlots / 64];
+#else
+  f32x2 ppx[4][2], ppy[4][2];
 #pragma unroll
-  for (int i = 0; i < kOdVSlots / 64; i++) vt[i] = c_od_vtasks.t[lane + 64 * i];
+  for (int r = 0; r < 4; r++) {
+    const int t = r * 64 + lane;
+#pragma unroll
+    for (int e = 0; e < 2; e++) {
+      const float px = (float)c_pattern[4 * t + 2 * e], py = (float)c_pattern[4 * t + 2 * e + 1];
+      ppx[r][e] = (f32x2){px, px};
+      ppy[r][e] = (f32x2){py, py};
+    }
+  }
+#endif
   const uint32_t q0 = g->gauss[0], q1 = g->gauss[1], q2 = g->gauss[2], q3 = g->gauss[3];
-  // horizontal taps (v_dot4_u32_u8 over the 7 bytes x-3..x+3) and the vertical ones over a
-  // column's row-sum pairs: an even output row y takes rows y..y+6 as pairs (y, y+1) .. (y+6, y+7)
-  // with (k0,k1) (k2,k3) (k4,k5) (k6,0); an odd one the pairs (y-1, y) .. (y+5, y+6) with
-  // (0,k0) (k1,k2) (k3,k4) (k5,k6) (the kernel is symmetric: k4 = k2, k5 = k1, k6 = k0)
   const uint32_t KA = q0 | q1 << 8 | q2 << 16 | q3 << 24, KB = q2 | q1 << 8 | q0 << 16;
-  const uint32_t KE0 = q0 | q1 << 16, KE1 = q2 | q3 << 16, KE2 = q2 | q1 << 16, KE3 = q0;
-  const uint32_t KO0 = q0 << 16, KO1 = q1 | q2 << 16, KO2 = q3 | q2 << 16, KO3 = q1 | q0 << 16;
-  const f32x2 magic = {12582912.0f, 12582912.0f};
+  const uint32_t K01 = q0 | q1 << 16, K23 = q2 | q3 << 16, K21 = q2 | q1 << 16, K0 = q0;
+  // the horizontal taps of the four columns of a row task straight from the three dwords
+  // u0..u2 holding bytes x-3 .. x+8 (no per-column realignment): column jx weights byte jx+m by
+  // k_m (k symmetric: k4 = k2, k5 = k1, k6 = k0)
+  const uint32_t C1a = q0 << 8 | q1 << 16 | q2 << 24, C1b = q3 | q2 << 8 | q1 << 16 | q0 << 24;
+  const uint32_t C2a = q0 << 16 | q1 << 24, C2b = q2 | q3 << 8 | q2 << 16 | q1 << 24, C2c = q0;
+  const uint32_t C3a = q0 << 24, C3b = q1 | q2 << 8 | q3 << 16 | q2 << 24, C3c = q1 | q0 << 8;
+  // magic + 18: a rounded sample coordinate comes out as its window index (round(x) + 18; 18 is
+  // even, so round-half-even is unchanged)
+  const f32x2 magic = {12582930.0f, 12582930.0f};
   uint32_t dlo = 0, dhi = 0;
-  // Stage-1 task t = (row pair p = t / 10, column quad gq = t % 10): raw rows 2p and 2p + 1 of
-  // the window. The raw rows of keypoint j + 1 are in flight while keypoint j's vertical pass and
-  // tests run (RS_PREFETCH). LDS hand-offs are within the wave (LDS executes a wave's
-  // instructions in order): only compiler ordering is needed between the passes.
-  constexpr int kRsTasks = 22 * 10, kRsIters = (kRsTasks + 63) / 64;
+  // Row-sum tasks: t = lane + 64 i -> window row r = t / 10, column quad gq = t % 10; a task's
+  // raw bytes sit at r * pitch + 4 gq past the keypoint's window origin (a lane constant times
+  // the level pitch: one v_mad_u32_u24, the origin a scalar base).
+  int trow[7], tcol[7];
+#pragma unroll
+  for (int i = 0; i < 7; i++) {
+    const int t = lane + 64 * i;
+    trow[i] = t / 10;
+    tcol[i] = 4 * (t - 10 * (t / 10));
+  }
+  // Per keypoint: its row-summed window into LDS, then its 256 tests from LDS. The window's raw
+  // rows (one 16-byte load per lane task, 7 tasks per lane) of keypoint j + 1 are in flight
+  // while keypoint j's tests run (RS_PREFETCH). LDS hand-offs are within the wave (LDS executes
+  // a wave's instructions in order): only compiler ordering is needed between the passes.
   struct RsGeo {
     const uint8_t* im;
+    const uint8_t* org;  // window origin (kx - 21 rounded down to a dword, ky - 21), fast path
     int pitch, w, h, kx, ky;
-    bool fastp;
+    bool fastp;          // the whole window is inside the level: dword loads, no reflection
   };
   auto rs_geo = [&](int j) {
     RsGeo G;
@@ -1949,30 +1953,24 @@ __global__ __launch_bounds__(256) OD_ATTR void orient_desc_kernel(
     G.h = L.h;
     G.pitch = level == 0 ? in_pitch : L.pitch;
     G.im = level == 0 ? batch_image(b, img) : b.pyr + (int64_t)img * g->pyr_bytes + L.offset;
-    G.fastp = G.kx >= 21 && G.kx <= G.w - 31 && ((((uintptr_t)G.im | (uintptr_t)G.pitch) & 3) == 0);
+    G.fastp = G.kx >= 21 && G.kx <= G.w - 31 && G.ky >= 21 && G.ky + 21 < G.h &&
+              ((((uintptr_t)G.im | (uintptr_t)G.pitch) & 3) == 0);
+    G.org = G.im + (int64_t)(G.ky - 21) * G.pitch + ((G.kx - 21) & ~3);
     return G;
   };
-  auto rs_load = [&](const RsGeo& G, uint4 (&q)[kRsIters][2]) {
+  auto rs_load = [&](const RsGeo& G, uint4 (&q)[7]) {
     if (!G.fastp) return;
 #pragma unroll
-    for (int i = 0; i < kRsIters; i++) {
-      const int t = lane + 64 * i;
-      if (t < kRsTasks) {
-        const int p = t / 10, gq = t - p * 10;
-        const int x0 = (G.kx - 21 + 4 * gq) & ~3;
-#pragma unroll
-        for (int h = 0; h < 2; h++) {
-          const uint8_t* row = G.im + (int64_t)reflect101(G.ky - 21 + 2 * p + h, G.h) * G.pitch;
-          q[i][h] = *reinterpret_cast<const uint4*>(row + x0);
-        }
-      }
+    for (int i = 0; i < 7; i++) {
+      if (lane + 64 * i < 43 * 10)
+        q[i] = *reinterpret_cast<const uint4*>(
+            G.org + __umul24((uint32_t)trow[i], (uint32_t)G.pitch) + (uint32_t)tcol[i]);
     }
   };
-  uint32_t* const od = &s_od[wid][0];
-  uint8_t* const odb = reinterpret_cast<uint8_t*>(od + kOdPWords);
+  uint16_t* rtw = &s_rt[wid][0][0];
   RsGeo gn = rs_geo(0);
 #if RS_PREFETCH
-  uint4 qn[kRsIters][2];
+  uint4 qn[7];
   rs_load(gn, qn);
 #endif
 #if OD_UNROLL_J
@@ -1982,125 +1980,116 @@ __global__ __launch_bounds__(256) OD_ATTR void orient_desc_kernel(
 #endif
   for (int j = 0; j < kKpPerWave; j++) {
     const RsGeo G = gn;
-    uint4 q[kRsIters][2];
+    uint4 q[7];
 #if RS_PREFETCH
 #pragma unroll
-    for (int i = 0; i < kRsIters; i++) {
-      q[i][0] = qn[i][0];
-      q[i][1] = qn[i][1];
-    }
+    for (int i = 0; i < 7; i++) q[i] = qn[i];
 #else
     rs_load(G, q);
 #endif
-    // 1. row sums -> P
     const uint32_t sft = (uint32_t)((G.kx - 21) & 3);
 #pragma unroll
-    for (int i = 0; i < kRsIters; i++) {
+    for (int i = 0; i < 7; i++) {
       const int t = lane + 64 * i;
-      if (t < kRsTasks) {
-        const int p = t / 10, gq = t - p * 10;
-        uint32_t Rs[2][4];
+      if (t < 43 * 10) {
+        const int r = trow[i], gq = tcol[i] >> 2;
+        uint32_t u0, u1, u2;
+        if (G.fastp) {
+          u0 = __builtin_amdgcn_alignbyte(q[i].y, q[i].x, sft);
+          u1 = __builtin_amdgcn_alignbyte(q[i].z, q[i].y, sft);
+          u2 = __builtin_amdgcn_alignbyte(q[i].w, q[i].z, sft);
+        } else {  // the window leaves the level: reflect-101 rows and columns, byte loads
+          const uint8_t* row = G.im + (int64_t)reflect101(G.ky - 21 + r, G.h) * G.pitch;
+          const int x0 = G.kx - 18 + 4 * gq;
+          uint32_t wv[3] = {0, 0, 0};
 #pragma unroll
-        for (int h = 0; h < 2; h++) {
-          uint32_t u0, u1, u2;
-          if (G.fastp) {
-            u0 = __builtin_amdgcn_alignbyte(q[i][h].y, q[i][h].x, sft);
-            u1 = __builtin_amdgcn_alignbyte(q[i][h].z, q[i][h].y, sft);
-            u2 = __builtin_amdgcn_alignbyte(q[i][h].w, q[i][h].z, sft);
-          } else {  // the window leaves the image: reflect-101 columns, byte loads
-            const uint8_t* row =
-                G.im + (int64_t)reflect101(G.ky - 21 + 2 * p + h, G.h) * G.pitch;
-            const int x0 = G.kx - 18 + 4 * gq;
-            uint32_t wv[3] = {0, 0, 0};
-#pragma unroll
-            for (int k = 0; k < 10; k++)
-              wv[k >> 2] |= (uint32_t)row[reflect101(x0 - 3 + k, G.w)] << (8 * (k & 3));
-            u0 = wv[0];
-            u1 = wv[1];
-            u2 = wv[2];
-          }
-#pragma unroll
-          for (int jx = 0; jx < 4; jx++) {
-            const uint32_t lo = jx == 0 ? u0 : __builtin_amdgcn_alignbyte(u1, u0, jx);
-            const uint32_t hi = jx == 0 ? u1 : __builtin_amdgcn_alignbyte(u2, u1, jx);
-            Rs[h][jx] = __builtin_amdgcn_udot4(lo, KA, __builtin_amdgcn_udot4(hi, KB, 0u, false),
-                                               false);
-          }
+          for (int k = 0; k < 10; k++)
+            wv[k >> 2] |= (uint32_t)row[reflect101(x0 - 3 + k, G.w)] << (8 * (k & 3));
+          u0 = wv[0];
+          u1 = wv[1];
+          u2 = wv[2];
         }
-        uint4 pw;
-        pw.x = Rs[0][0] | Rs[1][0] << 16;
-        pw.y = Rs[0][1] | Rs[1][1] << 16;
-        pw.z = Rs[0][2] | Rs[1][2] << 16;
-        pw.w = Rs[0][3] | Rs[1][3] << 16;
-        *reinterpret_cast<uint4*>(od + gq * kOdQuadStride + 4 * p) = pw;
+        uint32_t R[4];
+        R[0] = __builtin_amdgcn_udot4(u0, KA, __builtin_amdgcn_udot4(u1, KB, 0u, false), false);
+        R[1] = __builtin_amdgcn_udot4(u0, C1a, __builtin_amdgcn_udot4(u1, C1b, 0u, false), false);
+        R[2] = __builtin_amdgcn_udot4(u0, C2a, __builtin_amdgcn_udot4(u1, C2b,
+                                      __builtin_amdgcn_udot4(u2, C2c, 0u, false), false), false);
+        R[3] = __builtin_amdgcn_udot4(u0, C3a, __builtin_amdgcn_udot4(u1, C3b,
+                                      __builtin_amdgcn_udot4(u2, C3c, 0u, false), false), false);
+#pragma unroll
+        for (int jx = 0; jx < 4; jx++) rtw[(4 * gq + jx) * kRtRows + r] = (uint16_t)R[jx];
       }
     }
+#if OD_FENCE
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+#else
     __asm__ volatile("" ::: "memory");
+#endif
     if (j + 1 < kKpPerWave) {
       gn = rs_geo(j + 1);
 #if RS_PREFETCH
       rs_load(gn, qn);
 #endif
     }
-    // 2. vertical pass over the disc -> B
     {
-      const int xt = G.w - (G.w & 3) - (G.kx - 18);  // columns c >= xt are in the scalar tail
-      constexpr int kV = kOdVSlots / 64;
-      uint32_t d[kV][5];
-#pragma unroll
-      for (int i = 0; i < kV; i++) {  // every slot's reads first: one LDS round trip per pass
-        const uint32_t* pc = od + (vt[i] & 1023u);
-        d[i][0] = pc[0];
-        d[i][1] = pc[4];
-        d[i][2] = pc[8];
-        d[i][3] = pc[12];
-        d[i][4] = pc[16];
-      }
-#pragma unroll
-      for (int i = 0; i < kV; i++) {
-        const uint32_t e = vt[i];
-        const bool tail = (int)(e >> 21) >= xt;
-        const uint32_t bias = tail ? 0x8000u : 0x7fffu, wid1 = tail ? 0u : 1u;
-        auto rnd = [&](uint32_t sum) {  // (sum + bias (+ bit 16 if half to even)) saturated
-          const uint32_t v = sum + bias + __builtin_amdgcn_ubfe(sum, 16, wid1);
-          return v < 0xffffffu ? v : 0xffffffu;  // byte 2 = min(v >> 16, 255)
-        };
-        const uint32_t d0 = d[i][0], d1 = d[i][1], d2 = d[i][2], d3 = d[i][3], d4 = d[i][4];
-        const uint32_t r0 = rnd(dot2u(d0, KE0, dot2u(d1, KE1, dot2u(d2, KE2, dot2u(d3, KE3, 0u)))));
-        const uint32_t r1 = rnd(dot2u(d0, KO0, dot2u(d1, KO1, dot2u(d2, KO2, dot2u(d3, KO3, 0u)))));
-        const uint32_t r2 = rnd(dot2u(d1, KE0, dot2u(d2, KE1, dot2u(d3, KE2, dot2u(d4, KE3, 0u)))));
-        const uint32_t r3 = rnd(dot2u(d1, KO0, dot2u(d2, KO1, dot2u(d3, KO2, dot2u(d4, KO3, 0u)))));
-        const uint32_t lo = __builtin_amdgcn_perm(r1, r0, 0x0c0c0602u);
-        const uint32_t hi = __builtin_amdgcn_perm(r3, r2, 0x0c0c0602u);
-        *reinterpret_cast<uint32_t*>(odb + ((e >> 10) & 2047u)) = lo | hi << 16;
-      }
-    }
-    __asm__ volatile("" ::: "memory");
-    // 3. the 256 tests, one byte read per sample
-    {
+      const int kx = G.kx;
+      const int w = G.w, xvec = w - (w & 3);
       const float cj = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(ca), 8 * j));
       const float sj = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(sa), 8 * j));
       const f32x2 ab = {sj, cj}, nab = {cj, -sj};
+      const uint32_t* rt32 = reinterpret_cast<const uint32_t*>(&s_rt[wid][0][0]);
+      // the 256 tests; kTail: the window reaches the scalar tail of the row (x >= W - W % 4,
+      // rounded half up instead of half to even) -- a wave-uniform case, so two code paths
+      auto tests = [&](auto tail_case) {
+        constexpr bool kTail = decltype(tail_case)::value;
+        const int xt = xvec - kx + 18;  // window columns c >= xt are in the tail
 #pragma unroll
-      for (int r = 0; r < 4; r++) {
-        uint32_t v[2];
+        for (int r = 0; r < 4; r++) {
+          uint32_t v[2];
 #pragma unroll
-        for (int e = 0; e < 2; e++) {
-          const float px = (float)(int)(int8_t)(pat[r] >> (16 * e));
-          const float py = (float)(int)(int8_t)(pat[r] >> (16 * e + 8));
-          const f32x2 sp = __builtin_elementwise_fma((f32x2){px, px}, ab, (f32x2){py, py} * nab) + magic;
-          const int sy = (int)__float_as_uint(sp.x) - 0x4B400000;
-          const int sx = (int)__float_as_uint(sp.y) - 0x4B400000;
-          v[e] = odb[(sx + 18) * kOdColBytes + sy + 18];
+          for (int e = 0; e < 2; e++) {
+            const float px = (float)(int)(int8_t)(pat[r] >> (16 * e));
+            const float py = (float)(int)(int8_t)(pat[r] >> (16 * e + 8));
+            const f32x2 sp = __builtin_elementwise_fma((f32x2){px, px}, ab, (f32x2){py, py} * nab) + magic;
+            const uint32_t cy = __float_as_uint(sp.x) - 0x4B400000u;  // window row of sy - 3
+            const uint32_t cx = __float_as_uint(sp.y) - 0x4B400000u;  // window column
+            const uint32_t e0 = __umul24(cx, (uint32_t)kRtRows) + cy;
+            const uint32_t* rw = rt32 + (e0 >> 1);
+            const uint32_t sh = cy << 4;  // alignbit takes it mod 32: 16 for an odd start
+            const uint32_t w0 = rw[0], w1 = rw[1], w2 = rw[2], w3 = rw[3];
+            const uint32_t p0 = __builtin_amdgcn_alignbit(w1, w0, sh);
+            const uint32_t p1 = __builtin_amdgcn_alignbit(w2, w1, sh);
+            const uint32_t p2 = __builtin_amdgcn_alignbit(w3, w2, sh);
+            const uint32_t p3 = __builtin_amdgcn_alignbit(0u, w3, sh);
+            const uint32_t sm = dot2u(p0, K01, dot2u(p1, K23, dot2u(p2, K21, dot2u(p3, K0, 0u))));
+            uint32_t o;
+            if (kTail) {
+              const bool tail = (int)cx >= xt;
+              o = (sm + (tail ? 0x8000u : 0x7fffu + ((sm >> 16) & 1u))) >> 16;
+            } else {
+              o = (sm + 0x7fffu + ((sm >> 16) & 1u)) >> 16;
+            }
+            v[e] = o > 255u ? 255u : o;
+          }
+          const uint64_t word = __ballot(v[0] < v[1]);
+          if (lane == 4 * j + r) {
+            dlo = (uint32_t)word;
+            dhi = (uint32_t)(word >> 32);
+          }
         }
-        const uint64_t word = __ballot(v[0] < v[1]);
-        if (lane == 4 * j + r) {
-          dlo = (uint32_t)word;
-          dhi = (uint32_t)(word >> 32);
-        }
-      }
+      };
+      if (kx + 18 >= xvec) tests(std::true_type{});
+      else tests(std::false_type{});
     }
+#if OD_FENCE
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+#else
     __asm__ volatile("" ::: "memory");
+#endif
   }
   const int64_t o = (int64_t)img * g->kp_cap + k0;
   if (lane < 4 * nk)

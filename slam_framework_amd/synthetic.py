@@ -592,6 +592,83 @@ def ba_problem(seed: int, n_local: int = 20, n_fixed: int = 6, n_points: int = 3
             "kf_true": T_true, "points_true": np.array(pts)}
 
 
+def map_problem(seed: int, n_kf: int = 1500, points_per_kf: int = 40, max_obs: int = 6,
+                spacing: float = 1.0, stereo_frac: float = 0.6, outlier_frac: float = 0.02,
+                noise_px: float = 0.7, rot_err: float = 0.002, trans_err: float = 0.05,
+                point_err: float = 0.05, cam=KITTI_CAM, cols: int = KITTI_COLS,
+                rows: int = KITTI_ROWS, nlevels: int = 8, scale_factor: float = 1.2):
+    """A map-scale global BundleAdjustment input (optimizer.cpp:18-207 over every keyframe): a
+    closed loop of n_kf keyframes `spacing` m apart on a circle (a KITTI-00-like drive that comes
+    back to its start), keyframe 0 fixed (kf_mode 1, Id() == 0), the others free. Each keyframe
+    spawns points_per_kf points 4-40 m ahead of it; a point is observed by up to max_obs of the
+    keyframes within +-12 of its spawner that see it in the image (vectorised: no per-keyframe
+    Python loop), so the keyframes at the end of the loop co-observe points with those at its
+    start -- the reduced camera system is a band plus the rows a loop closure reaches back from.
+    Same noise model as ba_problem; returns its dict."""
+    rng = np.random.default_rng(seed)
+    fx, fy, cx, cy, bf = cam
+    Rr = n_kf * spacing / (2 * np.pi)
+    ang = 2 * np.pi * np.arange(n_kf) / n_kf
+    C = np.stack([Rr * np.sin(ang), np.zeros(n_kf), Rr * (1 - np.cos(ang))], 1)  # centres
+    T_true = np.zeros((n_kf, 4, 4))
+    for k in range(n_kf):
+        R_wc = _rodrigues(np.array([0.0, -ang[k], 0.0]))  # heading along the tangent
+        T_true[k, :3, :3] = R_wc.T
+        T_true[k, :3, 3] = -R_wc.T @ C[k]
+        T_true[k, 3, 3] = 1.0
+    mode = np.zeros(n_kf, np.uint8)
+    mode[0] = 1
+    n_pts = n_kf * points_per_kf
+    home = np.repeat(np.arange(n_kf), points_per_kf)
+    Xc0 = np.stack([rng.uniform(-12, 12, n_pts), rng.uniform(-3, 2, n_pts),
+                    rng.uniform(4, 40, n_pts)], 1)
+    Rwc = np.transpose(T_true[home, :3, :3], (0, 2, 1))
+    X = np.einsum("nij,nj->ni", Rwc, Xc0) + C[home]
+    offs = np.arange(-12, 13)
+    cand = (home[:, None] + offs[None, :]) % n_kf                  # [n_pts, 25]
+    Rc, tc = T_true[cand, :3, :3], T_true[cand, :3, 3]
+    Xc = np.einsum("npij,nj->npi", Rc, X) + tc
+    with np.errstate(divide="ignore", invalid="ignore"):
+        u = fx * Xc[..., 0] / Xc[..., 2] + cx
+        v = fy * Xc[..., 1] / Xc[..., 2] + cy
+    vis = (Xc[..., 2] > 1.0) & (Xc[..., 2] < 60.0) & (u >= 0) & (u < cols) & (v >= 0) & (v < rows)
+    vis[:, 12] = True  # the spawner sees it (4-40 m straight ahead)
+    # up to max_obs observers per point: random order among the visible candidates
+    keys = np.where(vis, rng.random(vis.shape), 2.0)
+    order = np.argsort(keys, 1)[:, :max_obs]
+    nvis = np.minimum(vis.sum(1), max_obs)
+    keep = nvis >= 2
+    order, nvis = order[keep], nvis[keep]
+    X, cand, Xc, u, v = X[keep], cand[keep], Xc[keep], u[keep], v[keep]
+    n_pts = len(X)
+    from .slamgpu import BA_OBS_DTYPE
+    start = np.zeros(n_pts + 1, np.int32)
+    start[1:] = np.cumsum(nvis)
+    n_obs = int(start[-1])
+    rowi = np.repeat(np.arange(n_pts), nvis)
+    coli = order[np.arange(max_obs)[None, :] < nvis[:, None]]
+    kk, uu, vv, zz = cand[rowi, coli], u[rowi, coli], v[rowi, coli], Xc[rowi, coli, 2]
+    octv = np.minimum(rng.geometric(0.45, n_obs) - 1, nlevels - 1)
+    sig = noise_px * scale_factor ** octv
+    uo, vo = uu + rng.normal(0, 1, n_obs) * sig, vv + rng.normal(0, 1, n_obs) * sig
+    stereo = rng.random(n_obs) < stereo_frac
+    uro = np.where(stereo, uu - bf / zz + rng.normal(0, 1, n_obs) * sig, -1.0)
+    out = rng.random(n_obs) < outlier_frac
+    uo[out], vo[out] = rng.uniform(0, cols, out.sum()), rng.uniform(0, rows, out.sum())
+    uro[out & stereo] = np.maximum(uo[out & stereo] - rng.uniform(0, 90, (out & stereo).sum()), 0)
+    obs = np.zeros(n_obs, BA_OBS_DTYPE)
+    obs["keyframe"], obs["u"], obs["v"], obs["ur"], obs["octave"] = kk, uo, vo, uro, octv
+    kf = T_true.copy()
+    for k in range(1, n_kf):
+        kf[k, :3, :3] = _rodrigues(rng.normal(0, rot_err / np.sqrt(3), 3)) @ kf[k, :3, :3]
+        kf[k, :3, 3] += rng.normal(0, trans_err / np.sqrt(3), 3)
+    P = X + rng.normal(0, point_err / np.sqrt(3), (n_pts, 3))
+    return {"kf_Tcw": kf.astype(np.float32), "kf_mode": mode, "points": P.astype(np.float32),
+            "point_obs_start": start, "obs": obs,
+            "inv_sigma2": level_inv_sigma2(scale_factor, nlevels),
+            "kf_true": T_true, "points_true": X}
+
+
 # ---- DBoW2 vocabularies (SURVEY.md section 8(f) row 1): ORBvoc.txt is not in the reference ------
 def vocabulary(seed: int, k: int = 10, L: int = 6, pool=None, scoring: int = 0,
                weighting: int = 0, stop_frac: float = 0.02):

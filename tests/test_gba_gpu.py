@@ -62,3 +62,19 @@ def test_global_ba_stop_before_start(oracle, gpu_lib):
     kf, pts, its = run(gpu_lib, P, stop=ctypes.c_bool(True))
     assert its == its_o == 0
     assert np.array_equal(kf, kf_o) and np.array_equal(pts, pts_o)
+
+
+@pytest.mark.parametrize("n_kf", [300, 1500])
+def test_global_ba_map_scale_loop(oracle, gpu_lib, n_kf):
+    """A map-scale global BA after a loop closure (GlobalBundleAdjustemnt passes every keyframe,
+    optimizer.cpp:18-31): a closed loop of n_kf keyframes (synthetic.map_problem: ~38 points and
+    ~230 observations per keyframe; the last keyframes co-observe the first ones, so the reduced
+    camera system is a band plus rows reaching back to the start). The device factorises it in
+    block-profile storage; the oracle's profile LDLT is its dense one with the exact zeros
+    skipped. Poses and points within the tolerance of every BA test, identical LM counts."""
+    P = S.map_problem(40 + n_kf, n_kf)
+    kf_o, pts_o, its_o = oracle.global_ba(CAM, P, 10, True)
+    kf, pts, its = run(gpu_lib, P, 10, True)
+    assert its == its_o
+    assert_close(kf, kf_o, P["kf_Tcw"], f"{n_kf}-keyframe loop poses")
+    assert_close(pts, pts_o, P["points"], f"{n_kf}-keyframe loop points")

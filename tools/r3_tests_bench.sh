@@ -20,6 +20,24 @@ if [ -n "${AB:-}" ]; then  # A/B of library builds: AB="tools/abl/libslamgpu_x.s
   timeout -k 10 600 python3 tools/ab.py $AB $AB > $OUT/ab.log 2>&1
   echo "ab rc=$?"; cat $OUT/ab.log
 fi
+if [ -n "${PMC_LIBS:-}" ]; then  # one PMC pass per library over a short single-batch bench
+  i=0
+  for lib in $PMC_LIBS; do
+    i=$((i+1))
+    SLAMGPU_LIB=$PWD/$lib timeout -s KILL 120 rocprofv3 --pmc ${PMC:-SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_LDS SQ_ACTIVE_INST_LDS SQ_BUSY_CYCLES SQ_WAVE_CYCLES} \
+      --kernel-include-regex "${PMC_RE:-orient_desc}" --kernel-trace --output-format csv \
+      -d $OUT/pmc$i -o run -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline \
+      --no-optimizer --no-bow --no-latency --inflight 1 > $OUT/pmc$i.log 2>&1
+    echo "pmc $lib rc=$?"
+  done
+fi
+if [ "${LAT:-0}" = "1" ]; then  # the single-frame drop-in call: per-kernel trace
+  timeout -k 10 120 python3 tools/latency_probe.py > $OUT/lat.log 2>&1
+  echo "latency probe rc=$?"; cat $OUT/lat.log
+  timeout -k 10 120 rocprofv3 --kernel-trace --memory-copy-trace --output-format csv -d $OUT/lat -o run -- \
+    python3 tools/latency_probe.py > $OUT/lat_prof.log 2>&1
+  echo "latency trace rc=$?"
+fi
 if [ "${COOP:-0}" = "1" ]; then
   timeout -k 10 120 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/plain -o run -- \
     python3 tools/ba_latency.py 3 --ba-only > $OUT/plain.log 2>&1
