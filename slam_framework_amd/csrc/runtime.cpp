@@ -50,6 +50,13 @@ struct slamgpu_ctx {
   // that follow it copy host memory instead of issuing synchronous device reads
   uint8_t* h_res = nullptr;
   bool res_valid = false;
+  // slamgpu_frame_stereo's device work (H2D of the staged pair, the frontend, the mirror copies)
+  // as one HIP graph, re-captured when the camera or the distortion changes
+  hipGraph_t fgraph = nullptr;
+  hipGraphExec_t fexec = nullptr;
+  Camera fcam{};
+  Distortion fdist{};
+  bool fdist_on = false;
   int in_pitch = 0;
   int64_t in_stride = 0;
   // batch state
@@ -191,6 +198,7 @@ static FrameKps left_views(const slamgpu_ctx* c) {
 // keypoints and descriptors at kp_cap each, then frame 0's u_right and depth.
 struct ResMirror {
   int* nkps;
+  uint32_t* err;  // the device error word, copied behind the results
   KeyPoint* kps;
   uint8_t* desc;
   float* u_right;
@@ -205,6 +213,7 @@ static ResMirror res_mirror(const slamgpu_ctx* c) {
   uint8_t* h = c->h_res;
   ResMirror m;
   m.nkps = reinterpret_cast<int*>(h);
+  m.err = reinterpret_cast<uint32_t*>(h + 8);
   m.kps = reinterpret_cast<KeyPoint*>(h + 16);
   m.desc = h + 16 + 2 * kc * sizeof(KeyPoint);
   m.u_right = reinterpret_cast<float*>(m.desc + 2 * kc * 32);
@@ -346,6 +355,8 @@ void slamgpu_destroy(slamgpu_ctx* c) {
   if (!c) return;
   (void)hipSetDevice(c->device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
+  if (c->fexec) (void)hipGraphExecDestroy(c->fexec);
+  if (c->fgraph) (void)hipGraphDestroy(c->fgraph);
   for (hipEvent_t e : c->timer.pool) (void)hipEventDestroy(e);
   for (void* p : c->allocs) (void)hipFree(p);
   if (c->h_in) (void)hipHostFree(c->h_in);
@@ -419,11 +430,20 @@ static int run_frontend(slamgpu_ctx* c, const ImageBatch& b, int n_frames, int n
 // Host images -> d_in: rows packed into the pinned staging buffer at the device pitch, then one
 // DMA of the whole buffer (pageable 2-D copies go row by row: ~5 ms for a stereo pair). The
 // previous call on this context has synchronised, so the staging buffer is free.
-static int stage_images(slamgpu_ctx* c, const uint8_t* const* imgs, int n, size_t step) {
+static void stage_host(slamgpu_ctx* c, const uint8_t* const* imgs, int n, size_t step) {
   const int cols = c->geom.cols, rows = c->geom.rows;
-  for (int i = 0; i < n; i++)
+  for (int i = 0; i < n; i++) {
+    uint8_t* dst = c->h_in + i * c->in_stride;
+    if (step == (size_t)c->in_pitch) {  // already at the device pitch: one copy per image
+      std::memcpy(dst, imgs[i], (size_t)(rows - 1) * c->in_pitch + cols);
+      continue;
+    }
     for (int y = 0; y < rows; y++)
-      std::memcpy(c->h_in + i * c->in_stride + (int64_t)y * c->in_pitch, imgs[i] + y * step, cols);
+      std::memcpy(dst + (int64_t)y * c->in_pitch, imgs[i] + y * step, cols);
+  }
+}
+static int stage_images(slamgpu_ctx* c, const uint8_t* const* imgs, int n, size_t step) {
+  stage_host(c, imgs, n, step);
   HIPCHECK(c, hipMemcpyAsync(c->d_in, c->h_in, (size_t)n * c->in_stride, hipMemcpyHostToDevice,
                              c->stream));
   return 0;
@@ -500,17 +520,13 @@ int slamgpu_debug_level_keys(slamgpu_ctx* c, int img, int level, int stage, uint
   return 0;
 }
 
-int slamgpu_frame_stereo(slamgpu_ctx* c, const uint8_t* left, const uint8_t* right, size_t step,
-                         const slamgpu_camera* cam) {
-  if (!c || !left || !right || !cam) return SLAMGPU_EINVAL;
-  HIPCHECK(c, hipSetDevice(c->device));
-  set_camera(c, cam);
-  const uint8_t* imgs[2] = {left, right};
-  if (int r = stage_images(c, imgs, 2, step)) return r;
+// The device half of slamgpu_frame_stereo on c->stream: the staged pair's DMA, the frontend,
+// then the frame's results and the device error word into the pinned mirror.
+static int enqueue_frame_stereo(slamgpu_ctx* c) {
+  HIPCHECK(c, hipMemcpyAsync(c->d_in, c->h_in, 2 * (size_t)c->in_stride, hipMemcpyHostToDevice,
+                             c->stream));
   ImageBatch b{c->d_in, c->d_in + c->in_stride, 2 * c->in_stride, c->in_pitch, c->d_pyr};
-  int rc = run_frontend(c, b, 1, 2, true, c->stream);
-  if (rc) return rc;
-  // the frame's results into the pinned mirror, behind the kernels on the same stream
+  if (int rc = run_frontend(c, b, 1, 2, true, c->stream)) return rc;
   const ResMirror m = res_mirror(c);
   const size_t kc = (size_t)c->geom.kp_cap;
   HIPCHECK(c, hipMemcpyAsync(m.nkps, c->out.nkps, 2 * sizeof(int), hipMemcpyDeviceToHost,
@@ -522,9 +538,84 @@ int slamgpu_frame_stereo(slamgpu_ctx* c, const uint8_t* left, const uint8_t* rig
                              hipMemcpyDeviceToHost, c->stream));
   HIPCHECK(c, hipMemcpyAsync(m.depth, c->sout.depth, kc * sizeof(float), hipMemcpyDeviceToHost,
                              c->stream));
-  rc = slamgpu_sync(c, nullptr);
-  c->res_valid = rc == 0;
-  return rc;
+  HIPCHECK(c, hipMemcpyAsync(m.err, c->ws.err, sizeof(uint32_t), hipMemcpyDeviceToHost,
+                             c->stream));
+  return 0;
+}
+
+// SLAMGPU_FRAME_GRAPH=0 issues the frame call's ~25 launches and copies one by one (A/B only).
+static bool frame_graph_enabled() {
+  static const bool on = [] {
+    const char* e = std::getenv("SLAMGPU_FRAME_GRAPH");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
+static void drop_frame_graph(slamgpu_ctx* c) {
+  if (c->fexec) (void)hipGraphExecDestroy(c->fexec);
+  if (c->fgraph) (void)hipGraphDestroy(c->fgraph);
+  c->fexec = nullptr;
+  c->fgraph = nullptr;
+}
+
+// One graph launch per frame: the launch chain costs the host one call instead of ~25, and the
+// device sees the whole dependency graph at once. Captured on first use and whenever the kernels'
+// by-value arguments (camera, distortion) change; the buffers it names are the context's own.
+static int launch_frame_graph(slamgpu_ctx* c) {
+  const bool same = c->fexec && std::memcmp(&c->fcam, &c->cam, sizeof(Camera)) == 0 &&
+                    c->fdist_on == c->dist_on &&
+                    std::memcmp(&c->fdist, &c->dist, sizeof(Distortion)) == 0;
+  if (!same) {
+    drop_frame_graph(c);
+    HIPCHECK(c, hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal));
+    const int rc = enqueue_frame_stereo(c);
+    hipGraph_t g = nullptr;
+    const hipError_t e = hipStreamEndCapture(c->stream, &g);
+    if (rc || e != hipSuccess) {
+      if (g) (void)hipGraphDestroy(g);
+      return rc ? rc : fail(c, SLAMGPU_EHIP, "frame graph capture: %s", hipGetErrorString(e));
+    }
+    const hipError_t ei = hipGraphInstantiate(&c->fexec, g, nullptr, nullptr, 0);
+    if (ei != hipSuccess) {
+      (void)hipGraphDestroy(g);
+      c->fexec = nullptr;
+      return fail(c, SLAMGPU_EHIP, "frame graph instantiate: %s", hipGetErrorString(ei));
+    }
+    c->fgraph = g;
+    c->fcam = c->cam;
+    c->fdist = c->dist;
+    c->fdist_on = c->dist_on;
+  } else {  // the host-side state run_frontend records
+    c->res_valid = false;
+    c->batch = ImageBatch{c->d_in, c->d_in + c->in_stride, 2 * c->in_stride, c->in_pitch, c->d_pyr};
+    c->n_frames_last = 1;
+    c->n_images_last = 2;
+  }
+  HIPCHECK(c, hipGraphLaunch(c->fexec, c->stream));
+  return 0;
+}
+
+int slamgpu_frame_stereo(slamgpu_ctx* c, const uint8_t* left, const uint8_t* right, size_t step,
+                         const slamgpu_camera* cam) {
+  if (!c || !left || !right || !cam) return SLAMGPU_EINVAL;
+  HIPCHECK(c, hipSetDevice(c->device));
+  set_camera(c, cam);
+  const uint8_t* imgs[2] = {left, right};
+  stage_host(c, imgs, 2, step);
+  // kernel timing records events around each launch: those calls stay eager
+  const int rc = frame_graph_enabled() && !c->timer.on ? launch_frame_graph(c)
+                                                       : enqueue_frame_stereo(c);
+  if (rc) return rc;
+  HIPCHECK(c, hipStreamSynchronize(c->stream));
+  const ResMirror m = res_mirror(c);
+  if (*m.err) {
+    const uint32_t e = *m.err;
+    (void)hipMemset(c->ws.err, 0, sizeof(uint32_t));
+    return fail(c, SLAMGPU_EDEVICE, "device capacity overflow (bits 0x%x)", e);
+  }
+  c->res_valid = true;
+  return 0;
 }
 
 int slamgpu_frontend_device(slamgpu_ctx* c, const uint8_t* d_left, const uint8_t* d_right,

@@ -55,6 +55,30 @@ def test_stereo_matches_oracle(seq, ctx, i):
     assert (depth > 0).sum() > 100
 
 
+def test_frame_graph_recapture_and_eager(seq, gpu_lib, oracle):
+    """slamgpu_frame_stereo replays one captured HIP graph per (camera, distortion): a camera
+    change re-captures it (depth follows the new bf), and the eager launch chain (taken while
+    kernel timing is on) gives the same bytes."""
+    t, L, R, fr = seq
+    c = gpu_lib.Context(S.KITTI_COLS, S.KITTI_ROWS)
+    cam2 = tuple(CAM[:4]) + (CAM[4] * 1.25,)
+    kl, dl, pl = oracle.extract(t, L[1], True)
+    kr, dr, pr = oracle.extract(t, R[1], True)
+    ur2, depth2, _ = oracle.stereo(t, kl, dl, kr, dr, pl, pr, cam2[0], cam2[4])
+    for cam, ref_ur, ref_depth in ((CAM, fr[1]["ur"], fr[1]["depth"]), (cam2, ur2, depth2),
+                                   (CAM, fr[1]["ur"], fr[1]["depth"])):
+        for eager in (False, True):
+            if eager:
+                c.timing_start("*", 256)
+            c.frame_stereo(L[1], R[1], cam)
+            if eager:
+                c.timing_stop()
+            _eq_kps(c.keypoints(0)[0], fr[1]["kl"])
+            ur, depth = c.stereo(0)
+            assert ur.tobytes() == ref_ur.tobytes()
+            assert depth.tobytes() == ref_depth.tobytes()
+
+
 @pytest.mark.parametrize("blocks_frac,check_ori,th", [(1.0, 1, 7.0), (0.0, 1, 7.0), (0.5, 0, 14.0),
                                                       (0.5, 1, 7.0)])
 def test_f2f_matches_oracle(seq, ctx, oracle, blocks_frac, check_ori, th):
