@@ -117,6 +117,37 @@ def kernel_bytes(name, n_images, n_frames, kp_per_image, level_px, n_queries):
     return None
 
 
+def stereo_line_bytes(ctx, level_px, line=128, pitch0=1280):
+    """Compulsory bytes of stereo_match for the batch's frame 0 at cache-line granularity: the
+    distinct `line`-byte lines its SAD windows touch (left 11 x 11 at the keypoint, right 11 x 21
+    at u_right, both at the left keypoint's level; levels >= 1 at pitch round_up(w, 64) from
+    256-aligned bases) plus every left / right keypoint and descriptor (60 B each) and the row
+    table entries (4 B per (right keypoint, row) pair). Matches whose SAD step was rejected are
+    not counted, so this is a lower bound."""
+    kl, _ = ctx.keypoints(0)
+    kr, _ = ctx.keypoints(1)
+    ur, _ = ctx.stereo(0)
+    dims = [ctx.pyramid_level(0, l).shape for l in range(8)]
+    pitches = [pitch0] + [(w + 63) // 64 * 64 for (_, w) in dims[1:]]
+    bases, off = [0], 1 << 30
+    for l in range(1, 8):
+        bases.append(off)
+        off += (pitches[l] * dims[l][0] + 255) // 256 * 256
+    lines = set()
+    for i in np.nonzero(ur >= 0)[0]:
+        lv = int(kl["octave"][i])
+        inv = 1.0 / (1.2 ** lv)
+        xl, yc, xr = (int(round(float(kl["x"][i]) * inv)), int(round(float(kl["y"][i]) * inv)),
+                      int(round(float(ur[i]) * inv)))
+        for side, x0, x1 in ((0, xl - 5, xl + 5), (1 << 40, xr - 10, xr + 10)):
+            for y in range(yc - 5, yc + 6):
+                a = side + bases[lv] + y * pitches[lv]
+                lines.update(range((a + x0) // line, (a + x1) // line + 1))
+    rows = sum(int(np.ceil(k["y"] + 2 * 1.2 ** k["octave"])) - int(np.floor(k["y"] - 2 * 1.2 ** k["octave"])) + 1
+               for k in kr)
+    return len(lines) * line + 60 * (len(kl) + len(kr)) + 4 * rows
+
+
 def working_set_bytes(name, n_images, kp_per_image):
     """Bytes a kernel's work-items fetch counting overlaps (each keypoint's 43 x 43 raw window
     for orient_desc): an upper bound on its L2 -> CU traffic, not HBM bytes."""
@@ -322,6 +353,11 @@ def main():
                 ent["valu_wave_instr_per_launch"] = round(vi)
                 ent["valu_issue_frac"] = round(vi / avg_s / vpeak, 4)
             kernels[n] = ent
+        if "stereo_match" in kernels:
+            # HBM moves lines: the windows' distinct 128-B lines (frame 0 of the batch) + the
+            # keypoint/descriptor/row-table reads, per launch (tools/stereo_lines.py restates it)
+            lb = stereo_line_bytes(ctx, level_px)
+            kernels["stereo_match"]["line_granular_bytes_per_launch"] = lb * Bs
         line = {
             "metric": "stereo frames/sec ORB extract+match @1241x376, 2000 kp/frame",
             "value": round(value, 2), "unit": "stereo frames/s", "n_gpus": world,

@@ -39,6 +39,11 @@ struct StereoOut {
 };
 
 // Stereo: frame f uses image 2f (left) and 2f+1 (right) of the extractor batch.
+// Stereo frame 0 of ext (images 0 / 1) packed in the host mirror's layout (runtime.cpp
+// ResMirror: [nkps x2][err][pad] | kps 2 x kp_cap | desc 2 x kp_cap | u_right kp_cap | depth
+// kp_cap) at dst, valid entries only: one DMA then brings the frame's results to the host.
+void launch_frame_pack(const FrameKps& ext, const float* u_right, const float* depth,
+                       const uint32_t* err, int kp_cap, uint8_t* dst, hipStream_t st);
 void launch_stereo(const ImageBatch& b, const OrbGeomDev& g, const Camera& cam, int n_frames,
                    const StereoWorkspace& ws, const StereoOut& out, hipStream_t st);
 

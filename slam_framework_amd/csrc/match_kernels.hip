@@ -316,44 +316,69 @@ __global__ __launch_bounds__(256) void stereo_match_kernel(ImageBatch b,
   }
 }
 
-// Median SAD filter (:564-576): drop matches whose SAD >= 2.1 * median.
+// Median SAD filter (:564-576): drop matches whose SAD >= 2.1 * median. The median (element
+// n / 2 of the ascending sort, :564-566) is found by an MSB-first radix select over the SADs
+// (four 8-bit digit histograms) instead of sorting them.
 __global__ __launch_bounds__(256) void stereo_median_kernel(const OrbGeom* __restrict__ g,
                                                             FrameKps ext, StereoWorkspace ws,
                                                             StereoOut out) {
   constexpr int kCap = 4096;
-  __shared__ int vals[kCap];
-  __shared__ int n_valid;
-  const int f = blockIdx.x, tid = threadIdx.x;
+  __shared__ uint32_t vals[kCap];
+  __shared__ int hist[256];
+  __shared__ int n_valid, s_digit, s_rank;
+  const int f = blockIdx.x, tid = threadIdx.x, lane = tid & 63;
   const int nl = min(ext.n[2 * f * ext.n_stride], kCap);
   const int64_t base = (int64_t)f * g->kp_cap;
   if (tid == 0) n_valid = 0;
   __syncthreads();
   for (int i = tid; i < nl; i += 256) {
     const int s = ws.sad[base + i];
-    if (s >= 0) vals[atomicAdd(&n_valid, 1)] = s;
+    if (s >= 0) vals[atomicAdd(&n_valid, 1)] = (uint32_t)s;
   }
   __syncthreads();
   const int n = n_valid;
   if (n == 0) return;  // the reference indexes an empty vector here (UB); we skip the filter
-  int P2 = 1;
-  while (P2 < n) P2 <<= 1;
-  for (int i = n + tid; i < P2; i += 256) vals[i] = 0x7fffffff;
-  __syncthreads();
-  for (int k = 2; k <= P2; k <<= 1)
-    for (int j = k >> 1; j > 0; j >>= 1) {
-      for (int i = tid; i < P2; i += 256) {
-        const int ixj = i ^ j;
-        if (ixj > i) {
-          const int x = vals[i], y = vals[ixj];
-          if (((i & k) == 0) ? (x > y) : (x < y)) {
-            vals[i] = y;
-            vals[ixj] = x;
-          }
-        }
-      }
-      __syncthreads();
+  uint32_t prefix = 0, mask = 0;
+  int k = n / 2;  // rank of the median among the values matching prefix under mask
+  for (int shift = 24; shift >= 0; shift -= 8) {
+    hist[tid] = 0;
+    __syncthreads();
+    for (int i = tid; i < n; i += 256) {
+      const uint32_t v = vals[i];
+      if ((v & mask) == prefix) atomicAdd(&hist[(v >> shift) & 255u], 1);
     }
-  const float median = (float)vals[n / 2];
+    __syncthreads();
+    if (tid < 64) {  // the digit whose cumulative count passes k: lane owns bins 4 lane .. +3
+      int h[4], sum = 0;
+#pragma unroll
+      for (int j = 0; j < 4; j++) {
+        h[j] = hist[4 * lane + j];
+        sum += h[j];
+      }
+      int x = sum;  // inclusive scan over the wave
+#pragma unroll
+      for (int off = 1; off < 64; off <<= 1) {
+        const int y = __shfl_up(x, off, 64);
+        if (lane >= off) x += y;
+      }
+      const int before = x - sum;
+      if (before <= k && k < x) {  // exactly one lane
+        int acc = before, d = 0;
+#pragma unroll
+        for (int j = 0; j < 4; j++)
+          if (d == 0 && acc + h[j] > k) d = j + 1;
+          else if (d == 0) acc += h[j];
+        s_digit = 4 * lane + d - 1;
+        s_rank = k - acc;
+      }
+    }
+    __syncthreads();
+    prefix |= (uint32_t)s_digit << shift;
+    mask |= 255u << shift;
+    k = s_rank;
+    __syncthreads();
+  }
+  const float median = (float)(int)prefix;
   const float thDist = (1.5f * 1.4f) * median;
   for (int i = tid; i < nl; i += 256) {
     const int s = ws.sad[base + i];
@@ -363,6 +388,45 @@ __global__ __launch_bounds__(256) void stereo_median_kernel(const OrbGeom* __res
       ws.sad[base + i] = -1;
     }
   }
+}
+
+// ---------------------------------------------------------------------------------------
+// Frame results -> the host mirror's layout (see match_kernels.h), copied as dwords.
+__global__ __launch_bounds__(256) void frame_pack_kernel(FrameKps ext,
+                                                         const float* __restrict__ u_right,
+                                                         const float* __restrict__ depth,
+                                                         const uint32_t* __restrict__ err,
+                                                         int kp_cap, uint8_t* __restrict__ dst) {
+  const int gid = blockIdx.x * blockDim.x + threadIdx.x, gsz = gridDim.x * blockDim.x;
+  const int c0 = ext.n[0], c1 = ext.n[ext.n_stride];
+  const int n0 = min(max(c0, 0), kp_cap), n1 = min(max(c1, 0), kp_cap);
+  const size_t kc = (size_t)kp_cap;
+  if (gid == 0) {
+    int* h = reinterpret_cast<int*>(dst);
+    h[0] = c0;
+    h[1] = c1;
+    h[2] = (int)*err;
+  }
+  auto copy = [&](const void* src, size_t dst_off, int words) {
+    const uint32_t* s = reinterpret_cast<const uint32_t*>(src);
+    uint32_t* d = reinterpret_cast<uint32_t*>(dst + dst_off);
+    for (int i = gid; i < words; i += gsz) d[i] = s[i];
+  };
+  const size_t kps_off = 16, desc_off = kps_off + 2 * kc * sizeof(KeyPoint);
+  const size_t ur_off = desc_off + 2 * kc * 32, dp_off = ur_off + kc * sizeof(float);
+  copy(ext.kps, kps_off, 7 * n0);
+  copy(ext.kps + ext.stride, kps_off + kc * sizeof(KeyPoint), 7 * n1);
+  copy(ext.desc, desc_off, 8 * n0);
+  copy(ext.desc + 32 * ext.stride, desc_off + 32 * kc, 8 * n1);
+  copy(u_right, ur_off, n0);
+  copy(depth, dp_off, n0);
+}
+
+void launch_frame_pack(const FrameKps& ext, const float* u_right, const float* depth,
+                       const uint32_t* err, int kp_cap, uint8_t* dst, hipStream_t st) {
+  static_assert(sizeof(KeyPoint) == 28, "keypoint layout");
+  SLAMGPU_LAUNCH("frame_pack", st, frame_pack_kernel, dim3(32), dim3(256), 0, st, ext, u_right,
+                 depth, err, kp_cap, dst);
 }
 
 void launch_stereo(const ImageBatch& b, const OrbGeomDev& gd, const Camera& cam, int n_frames,

@@ -244,6 +244,26 @@ int compute_geometry(const OrbParams& p, int cols, int rows, OrbGeom* g,
     }
     g->oct_lds_bytes = off + 4 * kcap;
   }
+  {  // octree_lvl_kernel LDS (80 KB: two work-groups per CU)
+    constexpr int kLdsBudget = 80 * 1024, kNodeBytes = 12, kWorkBytesPerNode = 4 + 4 * 2 + 1;
+    int nc = 64, ccap = 0;
+    for (int l = 0; l < p.nlevels; l++) {
+      nc = std::max(nc, g->lv[l].oct_nc);
+      ccap = std::max(ccap, g->lv[l].ncols * g->lv[l].nrows + 1);
+    }
+    ccap = round_up(ccap, 4);
+    const int fixed = ccap * 4 + 2 * nc * kNodeBytes + round_up(nc * kWorkBytesPerNode, 16);
+    const int kcap = std::min((kLdsBudget - fixed) / 8 / 4 * 4, 65535);
+    if (kcap < 1024) return -7;
+    g->oct2_kcap = kcap;
+    g->oct2_ccap = ccap;
+    g->oct2_nc = nc;
+    g->oct2_tmp_off = 4 * kcap;
+    g->oct2_cpre_off = 8 * kcap;
+    g->oct2_list_off = g->oct2_cpre_off + 4 * ccap;
+    g->oct2_work_off = g->oct2_list_off + 2 * nc * kNodeBytes;
+    g->oct2_lds_bytes = g->oct2_work_off + round_up(nc * kWorkBytesPerNode, 16);
+  }
   g->out_per_image = out_off;
   g->kp_cap = out_off;
   return 0;

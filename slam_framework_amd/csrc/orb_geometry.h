@@ -78,6 +78,11 @@ struct OrbGeom {
   int64_t nodes_per_image;
   int oct_lds_bytes;     // octree_img_kernel dynamic LDS (keys + per-level lists and arrays)
   int oct_kcap;          // keys of all levels of one image that fit in that LDS
+  // octree_lvl_kernel (one work-group per level): one layout for every level
+  // [keys u32 x oct2_kcap][gather staging u32 x oct2_kcap][cell prefix int x oct2_ccap]
+  // [two node lists x oct2_nc][sort keys u32, pt / pe / pu / vnext i16, processed u8 x oct2_nc]
+  int oct2_lds_bytes, oct2_kcap, oct2_ccap, oct2_nc;
+  int oct2_tmp_off, oct2_cpre_off, oct2_list_off, oct2_work_off;
   int out_per_image;     // sum of out_cap
   int kp_cap;            // max keypoints per image after Compute (== out_per_image)
   int umax[16];

@@ -12,6 +12,7 @@
 #include <stdint.h>
 
 #include <type_traits>
+#include <cstdlib>
 
 #include "device_math.h"
 #include "timing.h"
@@ -59,11 +60,17 @@ __device__ __forceinline__ uint32_t dot2u(uint32_t a, uint32_t b, uint32_t c) {
 #endif
 constexpr int kPyrStrip = PYR_STRIP;  // output rows per wave
 constexpr int kPyrChunk = PYR_CHUNK;  // source rows fetched per batch
+#ifndef PYR_SHORT_STRIP
+#define PYR_SHORT_STRIP 4
+#endif
+constexpr int kPyrShortStrip = PYR_SHORT_STRIP, kPyrShortMaxImages = 16;
 
 // kAligned: the source rows are dword-aligned (every level >= 1 source; level 0 when the caller's
 // images and pitch are) -- the instantiation without the byte-gather path needs fewer VGPRs, so
 // more waves per SIMD hide the strip's chain of row loads.
-template <bool kAligned>
+// kStrip: output rows per wave -- kPyrStrip for batches; small launches (a single frame) take
+// short strips so that more waves share a level and each walks a shorter chain of row loads.
+template <bool kAligned, int kStrip>
 __global__ __launch_bounds__(256) void pyr_down_kernel(ImageBatch b, const OrbGeom* __restrict__ g,
                                                        int level,
                                                        const ResizeX* __restrict__ rxt,
@@ -75,9 +82,9 @@ __global__ __launch_bounds__(256) void pyr_down_kernel(ImageBatch b, const OrbGe
   const LevelGeom& S = g->lv[level - 1];
   const int tiles_x = (D.w + 255) >> 8;
   const int tx = bx % tiles_x, ty = bx / tiles_x;
-  const int dy0 = (ty * 4 + wid) * kPyrStrip;
+  const int dy0 = (ty * 4 + wid) * kStrip;
   if (dy0 >= D.h) return;
-  const int nrows = min(kPyrStrip, D.h - dy0);
+  const int nrows = min(kStrip, D.h - dy0);
   // the strip's row table, one entry per lane (read back with readlane)
   int ry_y0 = 0, ry_y1 = 0, ry_b = 0;
   if (lane < nrows) {
@@ -1704,6 +1711,450 @@ __global__ __launch_bounds__(64 * kMaxLevels) void octree_img_kernel(
 }
 
 // ---------------------------------------------------------------------------------------
+// The same DistributeOctTree (:480-704) with one work-group of kOctLvlWaves waves per (level,
+// image): the latency variant. One wave per level (octree_img_kernel) puts the level-0 wave on
+// the critical path of a single frame (0.17 ms of a 0.46 ms frame call: gather 44 us, passes
+// 120 us, profiles/r3f_lat_octprof.log); here the gather's loads, the vPrev sort, the per-node
+// divides and the big nodes' partitions are spread over the waves. Same list semantics and
+// output bytes; a level that does not fit its LDS falls back to octree_kernel as before.
+constexpr int kOctLvlWaves = 4, kOctLvlThreads = 64 * kOctLvlWaves;
+#ifndef OCT_LVL_MAX_IMAGES
+#define OCT_LVL_MAX_IMAGES 16
+#endif
+constexpr int kOctLvlMaxImages = OCT_LVL_MAX_IMAGES;
+
+__device__ __forceinline__ int lvl_block_sum(int v, int* red) {
+  v = wave_sum(v);
+  if ((threadIdx.x & 63) == 0) red[wave_id()] = v;
+  __syncthreads();
+  int t = 0;
+#pragma unroll
+  for (int k = 0; k < kOctLvlWaves; k++) t += red[k];
+  __syncthreads();
+  return t;
+}
+
+// exclusive scan of a[0..n) in place by the whole work-group
+__device__ void lvl_block_scan(int* a, int n, int* red) {
+  const int lane = threadIdx.x & 63, w = wave_id();
+  int carry = 0;
+  for (int c = 0; c < n; c += kOctLvlThreads) {
+    const int i = c + (int)threadIdx.x;
+    const int v = i < n ? a[i] : 0;
+    int wt;
+    const int ex = wave_excl_scan(v, lane, &wt);
+    if (lane == 0) red[w] = wt;
+    __syncthreads();
+    int pre = 0, tot = 0;
+#pragma unroll
+    for (int k = 0; k < kOctLvlWaves; k++) {
+      pre += k < w ? red[k] : 0;
+      tot += red[k];
+    }
+    if (i < n) a[i] = carry + pre + ex;
+    carry += tot;
+    __syncthreads();
+  }
+}
+
+__global__ __launch_bounds__(kOctLvlThreads) void octree_lvl_kernel(
+    const OrbGeom* __restrict__ g, const uint32_t* __restrict__ cell_keys,
+    const int* __restrict__ cell_count, uint32_t* __restrict__ key_scratch,
+    uint32_t* __restrict__ oct_keys, int* __restrict__ oct_count, uint32_t* __restrict__ err) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t s_lvl[];
+  __shared__ int s_red[kOctLvlWaves];
+  __shared__ int s_bc[kOctLvlWaves][16];  // per-wave bucket counts of one placement round
+  __shared__ int s_brun[16];              // next free slot of each initial bucket
+  __shared__ int s_bcnt[16];              // keys per initial bucket
+  __shared__ int s_u[4];                  // T, E, U of a pass; nproc
+  const int level = blockIdx.x, img = blockIdx.y;
+  const int tid = threadIdx.x, lane = tid & 63, w = wave_id();
+  const int nlev = g->nlevels;
+  const LevelGeom& L = g->lv[level];
+  const int ncell = L.ncols * L.nrows;
+  const int64_t cbase = (int64_t)img * g->cells_per_image + L.cell_base;
+  int* const outc = oct_count + img * nlev + level;
+  uint32_t* const outk = oct_keys + (int64_t)img * g->out_per_image + L.out_base;
+  // ---- 1. candidate count; levels that do not fit fall back to octree_kernel
+  int K = 0;
+  for (int c = tid; c < ncell; c += kOctLvlThreads) K += cell_count[cbase + c];
+  K = lvl_block_sum(K, s_red);
+  const int nIni = L.n_ini;
+  const int NC = L.oct_nc;
+  if (K > g->oct2_kcap || nIni > 16 || ncell + 1 > g->oct2_ccap || NC > g->oct2_nc) {
+    if (tid == 0) *outc = -1;
+    return;
+  }
+  if (K == 0) {
+    if (tid == 0) *outc = 0;
+    return;
+  }
+#ifdef OCT_PROFILE  // phase timing (timing builds only): wall clock at 100 MHz
+  const uint64_t oct_t0 = wall_clock64();
+  uint64_t oct_tg = 0, oct_t1 = 0, oct_t2 = 0, oct_tp[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  int oct_passes = 0, oct_sz[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#endif
+  uint32_t* const keys = reinterpret_cast<uint32_t*>(s_lvl);
+  uint32_t* const tmp = reinterpret_cast<uint32_t*>(s_lvl + g->oct2_tmp_off);
+  int* const cpre = reinterpret_cast<int*>(s_lvl + g->oct2_cpre_off);
+  OctNodeS* const lists = reinterpret_cast<OctNodeS*>(s_lvl + g->oct2_list_off);
+  uint32_t* const sortk = reinterpret_cast<uint32_t*>(s_lvl + g->oct2_work_off);
+  int16_t* const pt = reinterpret_cast<int16_t*>(sortk + NC);
+  int16_t* const pe = pt + NC;
+  int16_t* const pu = pe + NC;
+  int16_t* const vnext = pu + NC;
+  uint8_t* const processed = reinterpret_cast<uint8_t*>(vnext + NC);
+  uint32_t* const gscratch = key_scratch + img * g->keys_per_image + L.key_base;
+
+  // ---- 2. gather in cell row-major order (a key slot finds its cell by binary search over the
+  // cell prefix), then a stable placement into the initial nodes' buckets (:484-526)
+  for (int c = tid; c < ncell; c += kOctLvlThreads) cpre[c] = cell_count[cbase + c];
+  if (tid < 16) s_bcnt[tid] = 0;
+  __syncthreads();
+  lvl_block_scan(cpre, ncell, s_red);
+  const float hX = L.hx;
+  auto bucket = [&](uint32_t k) {
+    const int b = (int)((float)key_x(k) / hX);
+    return b >= nIni ? -1 : b;
+  };
+  constexpr int kGatherUnroll = 4;
+  for (int s0 = 0; s0 < K; s0 += kGatherUnroll * kOctLvlThreads) {
+    uint32_t kr[kGatherUnroll];
+    int sr[kGatherUnroll];
+#pragma unroll
+    for (int r = 0; r < kGatherUnroll; r++) {
+      const int s = s0 + r * kOctLvlThreads + tid;
+      sr[r] = s;
+      if (s < K) {
+        int lo = 0, hi = ncell;  // largest c with cpre[c] <= s: the non-empty cell holding s
+        while (hi - lo > 1) {
+          const int mid = (lo + hi) >> 1;
+          if (cpre[mid] <= s) lo = mid;
+          else hi = mid;
+        }
+        kr[r] = cell_keys[(cbase + lo) * g->cell_cap + (s - cpre[lo])];
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < kGatherUnroll; r++)
+      if (sr[r] < K) {
+        tmp[sr[r]] = kr[r];
+        const int b = bucket(kr[r]);
+        if (b >= 0) atomicAdd(&s_bcnt[b], 1);
+      }
+  }
+  __syncthreads();
+#ifdef OCT_PROFILE
+  oct_tg = wall_clock64();
+#endif
+  if (w == 0) {
+    int tot;
+    const int bb = wave_excl_scan(lane < nIni ? s_bcnt[lane] : 0, lane, &tot);
+    if (lane < 16) s_brun[lane] = bb;
+  }
+  __syncthreads();
+  // stable placement, kOctLvlThreads slots per round in slot order
+  for (int s0 = 0; s0 < K; s0 += kOctLvlThreads) {
+    const int s = s0 + tid;
+    uint32_t k = 0;
+    int b = -1;
+    if (s < K) {
+      k = tmp[s];
+      b = bucket(k);
+    }
+    int rank = 0;
+    for (int bb = 0; bb < nIni; bb++) {
+      const uint64_t m = __ballot(b == bb);
+      if (b == bb) rank = lanes_below(m);
+      if (lane == bb) s_bc[w][bb] = __popcll(m);
+    }
+    __syncthreads();
+    if (b >= 0) {
+      int pos = s_brun[b] + rank;
+      for (int k2 = 0; k2 < w; k2++) pos += s_bc[k2][b];
+      keys[pos] = k;
+    }
+    __syncthreads();
+    if (tid < nIni) {
+      int add = 0;
+#pragma unroll
+      for (int k2 = 0; k2 < kOctLvlWaves; k2++) add += s_bc[k2][tid];
+      s_brun[tid] += add;
+    }
+    __syncthreads();
+  }
+  // initial nodes: non-empty buckets in order (empty ones are erased, :513-526)
+  if (w == 0) {
+    const int bcnt = lane < nIni ? s_bcnt[lane] : 0;
+    int tot;
+    const int bbase = wave_excl_scan(bcnt, lane, &tot);
+    const bool has = lane < nIni && bcnt > 0;
+    const uint64_t hm = __ballot(has);
+    if (has) {
+      OctNodeS nd;
+      nd.x0 = (int16_t)(int)(hX * (float)lane);
+      nd.x1 = (int16_t)(int)(hX * (float)(lane + 1));
+      nd.y0 = 0;
+      nd.y1 = (int16_t)(L.max_by - kMinBorder);
+      nd.kn = (uint32_t)bbase | (uint32_t)bcnt << 16;
+      lists[lanes_below(hm)] = nd;
+    }
+    if (lane == 0) s_u[0] = __popcll(hm);
+  }
+  __syncthreads();
+  int m = s_u[0];
+  __syncthreads();
+
+  // ---- 3. passes (as octree_img_kernel; node j of a pass belongs to wave (j / 64) % W when it
+  // is divided by one lane, to wave j % W when a whole wave divides it)
+  const int N = L.budget;
+  int cur = 0, nexp = 0;
+  bool outer = true;
+  auto owner = [&](int j, int n) {
+    return (n > kOctLaneKeys ? j : (j >> 6)) % kOctLvlWaves == w;
+  };
+#ifdef OCT_PROFILE
+  oct_t1 = wall_clock64();
+#endif
+  while (true) {
+#ifdef OCT_PROFILE
+    if (oct_passes < 8) oct_tp[oct_passes] = wall_clock64();
+    if (oct_passes < 8) oct_sz[oct_passes] = (outer ? 1 : -1) * m;
+    oct_passes++;
+#endif
+    const OctNodeS* Lc = lists + cur * NC;
+    OctNodeS* Ln = lists + (cur ^ 1) * NC;
+    const int V = outer ? m : nexp;
+    if (!outer) {  // vPrev: positions in push order -> descending (n, creation order)
+      int P2 = 64;
+      while (P2 < V) P2 <<= 1;
+      for (int i = tid; i < P2; i += kOctLvlThreads) {
+        uint32_t key = 0;  // pads sort to the end
+        if (i < V) {
+          const int pos = (int)sortk[i];
+          key = (uint32_t)node_n(Lc[pos]) << 12 | (uint32_t)(4095 - pos);
+        }
+        sortk[i] = key;
+      }
+      __syncthreads();
+      for (int k = 2; k <= P2; k <<= 1)
+        for (int jj = k >> 1; jj > 0; jj >>= 1) {
+          for (int i = tid; i < P2; i += kOctLvlThreads) {
+            const int ixj = i ^ jj;
+            if (ixj > i) {
+              const uint32_t x = sortk[i], y = sortk[ixj];
+              const bool desc = (i & k) == 0;
+              if (desc ? (x < y) : (x > y)) {
+                sortk[i] = y;
+                sortk[ixj] = x;
+              }
+            }
+          }
+          __syncthreads();
+        }
+    }
+    auto nidx = [&](int j) { return outer ? j : 4095 - (int)(sortk[j] & 0xfffu); };
+    // -- count children: t (non-empty), e (> 1 key); pu = survivor flag (outer) or t - 1
+    for (int j0 = 0; j0 < V; j0 += 64) {
+      const int j = j0 + lane;
+      const bool valid = j < V;
+      OctNodeS nd{};
+      if (valid) nd = Lc[nidx(j)];
+      const int n = node_n(nd);
+      int t = 0, e = 0;
+      if (valid && n > 1 && n <= kOctLaneKeys && owner(j, n)) {
+        const uint32_t c = lane_divide(nd, keys, false);
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+          const int cq = (c >> (8 * q)) & 255;
+          t += cq > 0;
+          e += cq > 1;
+        }
+      }
+      uint64_t bigm = __ballot(valid && n > kOctLaneKeys);
+      while (bigm) {
+        const int bl = __builtin_ctzll(bigm);
+        bigm &= bigm - 1;
+        if ((j0 + bl) % kOctLvlWaves != w) continue;
+        const OctNodeS nb = Lc[nidx(j0 + bl)];
+        int cnt[4];
+        wave_count(nb, keys, lane, cnt);
+        if (lane == bl) {
+#pragma unroll
+          for (int q = 0; q < 4; q++) {
+            t += cnt[q] > 0;
+            e += cnt[q] > 1;
+          }
+        }
+      }
+      if (valid && owner(j, n)) {
+        pt[j] = (int16_t)t;
+        pe[j] = (int16_t)e;
+        pu[j] = (int16_t)(outer ? (n == 1) : t - 1);
+      }
+    }
+    __syncthreads();
+    int nproc = V;
+    if (!outer) {
+      // processing stops once the list reaches N: first j with m + sum_{i<=j}(t_i - 1) >= N
+      if (w == 0) {
+        int carry = 0, np = V;
+        for (int j0 = 0; j0 < V; j0 += 64) {
+          const int j = j0 + lane;
+          const int v = j < V ? pu[j] : 0;
+          int tot;
+          const int incl = carry + wave_excl_scan(v, lane, &tot) + v;
+          const uint64_t hit = __ballot(j < V && m + incl >= N);
+          if (hit) {
+            np = j0 + __builtin_ctzll(hit) + 1;
+            break;
+          }
+          carry += tot;
+        }
+        if (lane == 0) s_u[3] = np;
+      }
+      for (int i = tid; i < m; i += kOctLvlThreads) processed[i] = 0;
+      __syncthreads();
+      nproc = s_u[3];
+      for (int j = tid; j < nproc; j += kOctLvlThreads) processed[nidx(j)] = 1;
+      __syncthreads();
+      for (int i = tid; i < m; i += kOctLvlThreads) pu[i] = (int16_t)(processed[i] ? 0 : 1);
+      __syncthreads();
+    }
+    // push-order child positions, survivors' order: one array per wave
+    if (w == 0) {
+      const int t = wave_scan_array(pt, nproc, lane);
+      if (lane == 0) s_u[0] = t;
+    } else if (w == 1) {
+      const int t = wave_scan_array(pe, nproc, lane);
+      if (lane == 0) s_u[1] = t;
+    } else if (w == 2) {
+      const int t = wave_scan_array(pu, m, lane);
+      if (lane == 0) s_u[2] = t;
+    }
+    __syncthreads();
+    const int T = s_u[0], E = s_u[1], U = s_u[2];
+    const int newm = T + U;
+    if (newm > NC || E > NC) {
+      if (tid == 0) atomicOr(err, kErrNodeOverflow);
+      break;
+    }
+    // -- divide in place and place children: push order gpos -> list position T-1-gpos
+    auto place = [&](int j, const OctNodeS& nd, uint32_t c4) {
+      int gpos = pt[j], epos = pe[j];
+      const int xm = node_xm(nd), ym = node_ym(nd);
+      const int16_t xs[3] = {nd.x0, (int16_t)xm, nd.x1};
+      const int16_t ys[3] = {nd.y0, (int16_t)ym, nd.y1};
+      int start = node_kbeg(nd);
+#pragma unroll
+      for (int q = 0; q < 4; q++) {
+        const int cq = (int)((c4 >> (8 * q)) & 255u);
+        if (cq > 0) {
+          OctNodeS ch;
+          ch.x0 = xs[q & 1];
+          ch.x1 = xs[(q & 1) + 1];
+          ch.y0 = ys[q >> 1];
+          ch.y1 = ys[(q >> 1) + 1];
+          ch.kn = (uint32_t)start | (uint32_t)cq << 16;
+          const int pos = T - 1 - gpos;
+          Ln[pos] = ch;
+          if (cq > 1) vnext[epos++] = (int16_t)pos;
+          gpos++;
+        }
+        start += cq;
+      }
+    };
+    for (int j0 = 0; j0 < nproc; j0 += 64) {
+      const int j = j0 + lane;
+      const bool valid = j < nproc;
+      OctNodeS nd{};
+      if (valid) nd = Lc[nidx(j)];
+      const int n = node_n(nd);
+      if (valid && n > 1 && n <= kOctLaneKeys && owner(j, n))
+        place(j, nd, lane_divide(nd, keys, true));
+      uint64_t bigm = __ballot(valid && n > kOctLaneKeys);
+      while (bigm) {
+        const int bl = __builtin_ctzll(bigm);
+        bigm &= bigm - 1;
+        if ((j0 + bl) % kOctLvlWaves != w) continue;
+        const OctNodeS nb = Lc[nidx(j0 + bl)];
+        int cnt[4];
+        wave_partition(nb, keys, gscratch, lane, cnt);
+        if (lane == 0) {
+          // counts can exceed 255 here: place() takes 8-bit counts, so place big ones inline
+          int gpos = pt[j0 + bl], epos = pe[j0 + bl];
+          const int xm = node_xm(nb), ym = node_ym(nb);
+          const int16_t xs[3] = {nb.x0, (int16_t)xm, nb.x1};
+          const int16_t ys[3] = {nb.y0, (int16_t)ym, nb.y1};
+          int start = node_kbeg(nb);
+          for (int q = 0; q < 4; q++) {
+            if (cnt[q] > 0) {
+              OctNodeS ch;
+              ch.x0 = xs[q & 1];
+              ch.x1 = xs[(q & 1) + 1];
+              ch.y0 = ys[q >> 1];
+              ch.y1 = ys[(q >> 1) + 1];
+              ch.kn = (uint32_t)start | (uint32_t)cnt[q] << 16;
+              const int pos = T - 1 - gpos;
+              Ln[pos] = ch;
+              if (cnt[q] > 1) vnext[epos++] = (int16_t)pos;
+              gpos++;
+            }
+            start += cnt[q];
+          }
+        }
+      }
+    }
+    for (int i = tid; i < m; i += kOctLvlThreads) {
+      const OctNodeS nd = Lc[i];
+      if (outer ? node_n(nd) == 1 : !processed[i]) Ln[T + pu[i]] = nd;
+    }
+    __syncthreads();
+    for (int i = tid; i < E; i += kOctLvlThreads) sortk[i] = (uint32_t)vnext[i];
+    __syncthreads();
+    const int mprev = m;
+    m = newm;
+    nexp = E;
+    cur ^= 1;
+    if (newm >= N || newm == mprev) break;
+    if (outer && newm + E * 3 > N) outer = false;
+  }
+  // ---- 4. retain the best key of each node (:682-701): strict '>' keeps the first maximum
+  __syncthreads();
+#ifdef OCT_PROFILE
+  oct_t2 = wall_clock64();
+#endif
+  const OctNodeS* Lf = lists + cur * NC;
+  const int mout = min(m, L.out_cap);
+  for (int j = tid; j < mout; j += kOctLvlThreads) {
+    const OctNodeS nd = Lf[j];
+    const int kb = node_kbeg(nd), n = node_n(nd);
+    uint32_t best = keys[kb];
+    for (int k = 1; k < n; k++) {
+      const uint32_t kk = keys[kb + k];
+      if (key_score(kk) > key_score(best)) best = kk;
+    }
+    outk[j] = best;
+  }
+  if (tid == 0) {
+    if (m > L.out_cap) atomicOr(err, kErrNodeOverflow);
+    *outc = mout;
+  }
+#ifdef OCT_PROFILE
+  if (tid == 0 && img < 2 && (level == 0 || level == 7)) {
+    const uint64_t t3 = wall_clock64();
+    printf("octlvl img %d lvl %d K %d gather %d+%d passes %d (%d) retain %d x10ns | %d:%d %d:%d "
+           "%d:%d %d:%d %d:%d\n",
+           img, level, K, (int)(oct_tg - oct_t0), (int)(oct_t1 - oct_tg), (int)(oct_t2 - oct_t1),
+           oct_passes, (int)(t3 - oct_t2), oct_sz[0], (int)(oct_tp[1] - oct_tp[0]), oct_sz[1],
+           (int)(oct_tp[2] - oct_tp[1]), oct_sz[2], (int)(oct_tp[3] - oct_tp[2]), oct_sz[3],
+           (int)((oct_passes > 4 ? oct_tp[4] : oct_t2) - oct_tp[3]), oct_sz[4],
+           (int)(oct_t2 - oct_tp[oct_passes > 4 ? 4 : 3]));
+  }
+#endif
+}
+
+// ---------------------------------------------------------------------------------------
 constexpr int kKpPerWave = 8;
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 
@@ -1746,8 +2197,16 @@ __device__ __forceinline__ int reduce_scatter16(int (&v)[16], int lane) {
 // column's rule (half to even inside the SSE span x < W - W%4, half up in the scalar tail).
 // Border keypoints (the window leaves the image: reflect-101 columns) load bytes one by one.
 // LDS: one 40 x 44 u16 window per wave.
+// OD_PAIRS: a lane task covers two window rows of its 4 columns and stores each column's pair
+// of u16 row sums as one dword (16 dword stores per lane and keypoint instead of 28 u16 ones),
+// over a 46-row (23-dword, odd) column stride: the 10 column quads of a row pair land on 8
+// distinct bank groups instead of 4 (profiles/r3f_ab.log PMC: 5.88 conflict cycles per LDS
+// instruction with u16 stores and a 22-dword stride).
+#ifndef OD_PAIRS
+#define OD_PAIRS 1
+#endif
 #ifndef RT_ROWS
-#define RT_ROWS 44
+#define RT_ROWS (OD_PAIRS ? 46 : 44)
 #endif
 #ifndef RS_PREFETCH
 #define RS_PREFETCH 1
@@ -1924,11 +2383,14 @@ __global__ __launch_bounds__(256) OD_ATTR void orient_desc_kernel(
   // Row-sum tasks: t = lane + 64 i -> window row r = t / 10, column quad gq = t % 10; a task's
   // raw bytes sit at r * pitch + 4 gq past the keypoint's window origin (a lane constant times
   // the level pitch: one v_mad_u32_u24, the origin a scalar base).
-  int trow[7], tcol[7];
+  constexpr int kTaskRows = OD_PAIRS ? 2 : 1;              // window rows per lane task
+  constexpr int kTasks = (44 / kTaskRows - (OD_PAIRS ? 0 : 1)) * 10;  // 22 x 10 or 43 x 10
+  constexpr int kRounds = (kTasks + 63) / 64;
+  int trow[kRounds], tcol[kRounds];
 #pragma unroll
-  for (int i = 0; i < 7; i++) {
+  for (int i = 0; i < kRounds; i++) {
     const int t = lane + 64 * i;
-    trow[i] = t / 10;
+    trow[i] = kTaskRows * (t / 10);
     tcol[i] = 4 * (t - 10 * (t / 10));
   }
   // Per keypoint: its row-summed window into LDS, then its 256 tests from LDS. The window's raw
@@ -1958,19 +2420,26 @@ __global__ __launch_bounds__(256) OD_ATTR void orient_desc_kernel(
     G.org = G.im + (int64_t)(G.ky - 21) * G.pitch + ((G.kx - 21) & ~3);
     return G;
   };
-  auto rs_load = [&](const RsGeo& G, uint4 (&q)[7]) {
+  auto rs_load = [&](const RsGeo& G, uint4 (&q)[kRounds * kTaskRows]) {
     if (!G.fastp) return;
 #pragma unroll
-    for (int i = 0; i < 7; i++) {
-      if (lane + 64 * i < 43 * 10)
-        q[i] = *reinterpret_cast<const uint4*>(
-            G.org + __umul24((uint32_t)trow[i], (uint32_t)G.pitch) + (uint32_t)tcol[i]);
+    for (int i = 0; i < kRounds; i++) {
+      if (lane + 64 * i < kTasks) {
+#pragma unroll
+        for (int h = 0; h < kTaskRows; h++) {
+          // row 43 (the pad of the last pair, weight 0 in every tap) re-reads row 42: the
+          // window's rows stay inside the level
+          const uint32_t row = (uint32_t)min(trow[i] + h, 42);
+          q[kTaskRows * i + h] = *reinterpret_cast<const uint4*>(
+              G.org + __umul24(row, (uint32_t)G.pitch) + (uint32_t)tcol[i]);
+        }
+      }
     }
   };
   uint16_t* rtw = &s_rt[wid][0][0];
   RsGeo gn = rs_geo(0);
 #if RS_PREFETCH
-  uint4 qn[7];
+  uint4 qn[kRounds * kTaskRows];
   rs_load(gn, qn);
 #endif
 #if OD_UNROLL_J
@@ -1980,44 +2449,57 @@ __global__ __launch_bounds__(256) OD_ATTR void orient_desc_kernel(
 #endif
   for (int j = 0; j < kKpPerWave; j++) {
     const RsGeo G = gn;
-    uint4 q[7];
+    uint4 q[kRounds * kTaskRows];
 #if RS_PREFETCH
 #pragma unroll
-    for (int i = 0; i < 7; i++) q[i] = qn[i];
+    for (int i = 0; i < kRounds * kTaskRows; i++) q[i] = qn[i];
 #else
     rs_load(G, q);
 #endif
     const uint32_t sft = (uint32_t)((G.kx - 21) & 3);
 #pragma unroll
-    for (int i = 0; i < 7; i++) {
+    for (int i = 0; i < kRounds; i++) {
       const int t = lane + 64 * i;
-      if (t < 43 * 10) {
+      if (t < kTasks) {
         const int r = trow[i], gq = tcol[i] >> 2;
-        uint32_t u0, u1, u2;
-        if (G.fastp) {
-          u0 = __builtin_amdgcn_alignbyte(q[i].y, q[i].x, sft);
-          u1 = __builtin_amdgcn_alignbyte(q[i].z, q[i].y, sft);
-          u2 = __builtin_amdgcn_alignbyte(q[i].w, q[i].z, sft);
-        } else {  // the window leaves the level: reflect-101 rows and columns, byte loads
-          const uint8_t* row = G.im + (int64_t)reflect101(G.ky - 21 + r, G.h) * G.pitch;
-          const int x0 = G.kx - 18 + 4 * gq;
-          uint32_t wv[3] = {0, 0, 0};
+        uint32_t R[kTaskRows][4];
 #pragma unroll
-          for (int k = 0; k < 10; k++)
-            wv[k >> 2] |= (uint32_t)row[reflect101(x0 - 3 + k, G.w)] << (8 * (k & 3));
-          u0 = wv[0];
-          u1 = wv[1];
-          u2 = wv[2];
+        for (int h = 0; h < kTaskRows; h++) {
+          uint32_t u0, u1, u2;
+          if (G.fastp) {
+            const uint4 v = q[kTaskRows * i + h];
+            u0 = __builtin_amdgcn_alignbyte(v.y, v.x, sft);
+            u1 = __builtin_amdgcn_alignbyte(v.z, v.y, sft);
+            u2 = __builtin_amdgcn_alignbyte(v.w, v.z, sft);
+          } else {  // the window leaves the level: reflect-101 rows and columns, byte loads
+            const int rr = min(r + h, 42);
+            const uint8_t* row = G.im + (int64_t)reflect101(G.ky - 21 + rr, G.h) * G.pitch;
+            const int x0 = G.kx - 18 + 4 * gq;
+            uint32_t wv[3] = {0, 0, 0};
+#pragma unroll
+            for (int k = 0; k < 10; k++)
+              wv[k >> 2] |= (uint32_t)row[reflect101(x0 - 3 + k, G.w)] << (8 * (k & 3));
+            u0 = wv[0];
+            u1 = wv[1];
+            u2 = wv[2];
+          }
+          R[h][0] = __builtin_amdgcn_udot4(u0, KA, __builtin_amdgcn_udot4(u1, KB, 0u, false), false);
+          R[h][1] = __builtin_amdgcn_udot4(u0, C1a, __builtin_amdgcn_udot4(u1, C1b, 0u, false), false);
+          R[h][2] = __builtin_amdgcn_udot4(u0, C2a, __builtin_amdgcn_udot4(u1, C2b,
+                                           __builtin_amdgcn_udot4(u2, C2c, 0u, false), false), false);
+          R[h][3] = __builtin_amdgcn_udot4(u0, C3a, __builtin_amdgcn_udot4(u1, C3b,
+                                           __builtin_amdgcn_udot4(u2, C3c, 0u, false), false), false);
         }
-        uint32_t R[4];
-        R[0] = __builtin_amdgcn_udot4(u0, KA, __builtin_amdgcn_udot4(u1, KB, 0u, false), false);
-        R[1] = __builtin_amdgcn_udot4(u0, C1a, __builtin_amdgcn_udot4(u1, C1b, 0u, false), false);
-        R[2] = __builtin_amdgcn_udot4(u0, C2a, __builtin_amdgcn_udot4(u1, C2b,
-                                      __builtin_amdgcn_udot4(u2, C2c, 0u, false), false), false);
-        R[3] = __builtin_amdgcn_udot4(u0, C3a, __builtin_amdgcn_udot4(u1, C3b,
-                                      __builtin_amdgcn_udot4(u2, C3c, 0u, false), false), false);
+#if OD_PAIRS
+        // rows r, r + 1 of column 4 gq + jx: one dword at u16 index (4 gq + jx) * kRtRows + r
+        uint32_t* rtw32 = reinterpret_cast<uint32_t*>(rtw);
 #pragma unroll
-        for (int jx = 0; jx < 4; jx++) rtw[(4 * gq + jx) * kRtRows + r] = (uint16_t)R[jx];
+        for (int jx = 0; jx < 4; jx++)
+          rtw32[(4 * gq + jx) * (kRtRows / 2) + (r >> 1)] = (R[0][jx] & 0xffffu) | R[1][jx] << 16;
+#else
+#pragma unroll
+        for (int jx = 0; jx < 4; jx++) rtw[(4 * gq + jx) * kRtRows + r] = (uint16_t)R[0][jx];
+#endif
       }
     }
 #if OD_FENCE
@@ -2115,6 +2597,18 @@ __global__ __launch_bounds__(256) OD_ATTR void orient_desc_kernel(
 
 // ---------------------------------------------------------------------------------------
 // Host-side launchers.
+
+// Which octree kernel a launch of n_images uses: the per-level work-groups for small batches
+// (the single-frame call's critical path), one work-group per image otherwise.
+// SLAMGPU_OCT_LVL=0 / 1 forces one of them (A/B and tests).
+static bool octree_per_level(int n_images) {
+  static const int mode = [] {
+    const char* e = std::getenv("SLAMGPU_OCT_LVL");
+    return e ? std::atoi(e) : -1;
+  }();
+  if (mode >= 0) return mode != 0;
+  return n_images <= kOctLvlMaxImages;
+}
 void launch_extract(const ImageBatch& b, const OrbGeomDev& gd, int n_images, hipStream_t st,
                     const ExtractStreams& fx) {
   const OrbGeom& g = *gd.host;
@@ -2156,14 +2650,25 @@ void launch_extract(const ImageBatch& b, const OrbGeomDev& gd, int n_images, hip
   if (split0) fast_level0();
   const bool in_aligned = (((uintptr_t)b.in_l | (uintptr_t)b.in_r | (uintptr_t)b.in_stride |
                            (uintptr_t)b.in_pitch) & 3) == 0;
+  const bool short_strips = n_images <= kPyrShortMaxImages;
   for (int l = 1; l < g.nlevels; l++) {
-    const int tiles = ((g.lv[l].w + 255) >> 8) * ((g.lv[l].h + 4 * kPyrStrip - 1) / (4 * kPyrStrip));
-    if (l > 1 || in_aligned)
-      SLAMGPU_LAUNCH("pyr_down", st, pyr_down_kernel<true>, dim3(tiles, n_images), dim3(256), 0, st,
+    const int strip = short_strips ? kPyrShortStrip : kPyrStrip;
+    const int tiles = ((g.lv[l].w + 255) >> 8) * ((g.lv[l].h + 4 * strip - 1) / (4 * strip));
+    const dim3 grid(tiles, n_images);
+    if (short_strips) {
+      if (l > 1 || in_aligned)
+        SLAMGPU_LAUNCH("pyr_down", st, (pyr_down_kernel<true, kPyrShortStrip>), grid, dim3(256), 0,
+                       st, b, gd.dev, l, gd.rx, gd.ry);
+      else
+        SLAMGPU_LAUNCH("pyr_down", st, (pyr_down_kernel<false, kPyrShortStrip>), grid, dim3(256),
+                       0, st, b, gd.dev, l, gd.rx, gd.ry);
+    } else if (l > 1 || in_aligned) {
+      SLAMGPU_LAUNCH("pyr_down", st, (pyr_down_kernel<true, kPyrStrip>), grid, dim3(256), 0, st,
                      b, gd.dev, l, gd.rx, gd.ry);
-    else
-      SLAMGPU_LAUNCH("pyr_down", st, pyr_down_kernel<false>, dim3(tiles, n_images), dim3(256), 0,
-                     st, b, gd.dev, l, gd.rx, gd.ry);
+    } else {
+      SLAMGPU_LAUNCH("pyr_down", st, (pyr_down_kernel<false, kPyrStrip>), grid, dim3(256), 0, st,
+                     b, gd.dev, l, gd.rx, gd.ry);
+    }
   }
   {
     const dim3 block(64 * kCellWaves);
@@ -2191,9 +2696,15 @@ void launch_extract(const ImageBatch& b, const OrbGeomDev& gd, int n_images, hip
       fast(0, g.cells_per_image, st);
     }
   }
-  SLAMGPU_LAUNCH("octree", st, octree_img_kernel, dim3(n_images), dim3(64 * g.nlevels),
-                 (size_t)g.oct_lds_bytes, st, gd.dev, gd.ws.cell_keys, gd.ws.cell_count,
-                 gd.ws.key_scratch, gd.ws.oct_keys, gd.ws.oct_count, gd.ws.err);
+  if (octree_per_level(n_images))
+    SLAMGPU_LAUNCH("octree", st, octree_lvl_kernel, dim3(g.nlevels, n_images),
+                   dim3(kOctLvlThreads), (size_t)g.oct2_lds_bytes, st, gd.dev, gd.ws.cell_keys,
+                   gd.ws.cell_count, gd.ws.key_scratch, gd.ws.oct_keys, gd.ws.oct_count,
+                   gd.ws.err);
+  else
+    SLAMGPU_LAUNCH("octree", st, octree_img_kernel, dim3(n_images), dim3(64 * g.nlevels),
+                   (size_t)g.oct_lds_bytes, st, gd.dev, gd.ws.cell_keys, gd.ws.cell_count,
+                   gd.ws.key_scratch, gd.ws.oct_keys, gd.ws.oct_count, gd.ws.err);
   SLAMGPU_LAUNCH("octree_global", st, octree_kernel, dim3(g.nlevels, n_images), dim3(kOctThreads), 0, st, gd.dev,
                      gd.ws.cell_keys, gd.ws.cell_count, gd.ws.key_scratch, gd.ws.node_scratch,
                      gd.ws.oct_keys, gd.ws.oct_count, gd.ws.err);

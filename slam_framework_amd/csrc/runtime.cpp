@@ -49,6 +49,7 @@ struct slamgpu_ctx {
   // u_right / depth), filled by slamgpu_frame_stereo before its synchronisation: the downloads
   // that follow it copy host memory instead of issuing synchronous device reads
   uint8_t* h_res = nullptr;
+  uint8_t* d_res = nullptr;  // its device twin: the frame's results packed, then one DMA
   bool res_valid = false;
   // slamgpu_frame_stereo's device work (H2D of the staged pair, the frontend, the mirror copies)
   // as one HIP graph, re-captured when the camera or the distortion changes
@@ -346,6 +347,7 @@ int slamgpu_create(int device, const slamgpu_orb_params* p, int cols, int rows, 
   TRY(dalloc(c, &c->d_blk, (size_t)g.kp_cap));
   TRY(hcheck(c, hipHostMalloc(reinterpret_cast<void**>(&c->h_res), res_mirror_bytes(g.kp_cap),
                               hipHostMallocDefault)));
+  TRY(dalloc(c, &c->d_res, res_mirror_bytes(g.kp_cap)));
 #undef TRY
   *out = c;
   return 0;
@@ -527,23 +529,21 @@ static int enqueue_frame_stereo(slamgpu_ctx* c) {
                              c->stream));
   ImageBatch b{c->d_in, c->d_in + c->in_stride, 2 * c->in_stride, c->in_pitch, c->d_pyr};
   if (int rc = run_frontend(c, b, 1, 2, true, c->stream)) return rc;
-  const ResMirror m = res_mirror(c);
-  const size_t kc = (size_t)c->geom.kp_cap;
-  HIPCHECK(c, hipMemcpyAsync(m.nkps, c->out.nkps, 2 * sizeof(int), hipMemcpyDeviceToHost,
-                             c->stream));
-  HIPCHECK(c, hipMemcpyAsync(m.kps, c->out.kps, 2 * kc * sizeof(KeyPoint), hipMemcpyDeviceToHost,
-                             c->stream));
-  HIPCHECK(c, hipMemcpyAsync(m.desc, c->out.desc, 2 * kc * 32, hipMemcpyDeviceToHost, c->stream));
-  HIPCHECK(c, hipMemcpyAsync(m.u_right, c->sout.u_right, kc * sizeof(float),
+  {
+    TimerScope ts(c);
+    launch_frame_pack(FrameKps{c->out.kps, c->out.desc, c->out.nkps, c->geom.kp_cap, 1},
+                      c->sout.u_right, c->sout.depth, c->ws.err, c->geom.kp_cap, c->d_res,
+                      c->stream);
+  }
+  HIPCHECK(c, hipMemcpyAsync(c->h_res, c->d_res, res_mirror_bytes(c->geom.kp_cap),
                              hipMemcpyDeviceToHost, c->stream));
-  HIPCHECK(c, hipMemcpyAsync(m.depth, c->sout.depth, kc * sizeof(float), hipMemcpyDeviceToHost,
-                             c->stream));
-  HIPCHECK(c, hipMemcpyAsync(m.err, c->ws.err, sizeof(uint32_t), hipMemcpyDeviceToHost,
-                             c->stream));
   return 0;
 }
 
-// SLAMGPU_FRAME_GRAPH=0 issues the frame call's ~25 launches and copies one by one (A/B only).
+// SLAMGPU_FRAME_GRAPH=0 issues the frame call's launches one by one (A/B). With the results
+// packed for one D2H copy the graph is the faster of the two on MI355X: 0.353 vs 0.383 ms per
+// call (profiles/r3g_lat*.log; with six D2H copies as graph nodes it had been the slower one,
+// 0.488 vs 0.463 ms, profiles/r3f_lat*.log).
 static bool frame_graph_enabled() {
   static const bool on = [] {
     const char* e = std::getenv("SLAMGPU_FRAME_GRAPH");

@@ -320,21 +320,23 @@ class Context:
     def sync(self, stream=None):
         self.check(lib().slamgpu_sync(self.h, C.c_void_p(stream or 0)))
 
+    # downloads fill capacity-sized buffers and return views of their first n entries (no
+    # zero-fill, no second copy: the single-frame call pattern times these)
     def keypoints(self, img):
-        kps = np.zeros(self.kp_cap, KP_DTYPE)
-        desc = np.zeros((self.kp_cap, 32), np.uint8)
+        kps = np.empty(self.kp_cap, KP_DTYPE)
+        desc = np.empty((self.kp_cap, 32), np.uint8)
         n = C.c_int()
         self.check(lib().slamgpu_download_keypoints(self.h, img, _ptr(kps), _ptr(desc),
                                                     self.kp_cap, C.byref(n)))
-        return kps[:n.value].copy(), desc[:n.value].copy()
+        return kps[:n.value], desc[:n.value]
 
     def stereo(self, frame):
-        ur = np.zeros(self.kp_cap, np.float32)
-        depth = np.zeros(self.kp_cap, np.float32)
+        ur = np.empty(self.kp_cap, np.float32)
+        depth = np.empty(self.kp_cap, np.float32)
         n = C.c_int()
         self.check(lib().slamgpu_download_stereo(self.h, frame, _ptr(ur), _ptr(depth),
                                                  self.kp_cap, C.byref(n)))
-        return ur[:n.value].copy(), depth[:n.value].copy()
+        return ur[:n.value], depth[:n.value]
 
     def device_results(self):
         v = DeviceView()

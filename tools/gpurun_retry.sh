@@ -4,7 +4,7 @@
 # command -- is returned at once, never retried.
 #   tools/gpurun_retry.sh <gpurun --timeout> '<command>' > log
 T=$1; shift
-for attempt in 1 2 3 4 5 6 7 8; do
+for attempt in $(seq 1 ${ATTEMPTS:-8}); do
   /usr/local/graft/bin/gpurun --timeout "$T" -- "$@"
   rc=$?
   [ $rc -ne 3 ] && exit $rc

@@ -28,7 +28,7 @@ for i in range(30):
     w["stereo"].append(t3 - t2)
 print({k: round(1e3 * float(np.median(v)), 3) for k, v in w.items()})
 names = ["pyr_down", "fast_cells", "octree", "octree_global", "orient_desc",
-         "stereo_rows", "stereo_match", "stereo_median", "grid_build"]
+         "stereo_rows", "stereo_match", "stereo_median", "grid_build", "frame_pack"]
 c.timing_start("*", 4096)
 for i in range(10):
     c.frame_stereo(Ls[i % 4], Rs[i % 4], S.KITTI_CAM)

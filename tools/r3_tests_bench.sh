@@ -35,7 +35,7 @@ if [ "${LAT:-0}" = "1" ]; then  # the single-frame drop-in call: per-kernel trac
   timeout -k 10 120 python3 tools/latency_probe.py > $OUT/lat.log 2>&1
   echo "latency probe rc=$?"; cat $OUT/lat.log
   SLAMGPU_FRAME_GRAPH=0 timeout -k 10 120 python3 tools/latency_probe.py > $OUT/lat_eager.log 2>&1
-  echo "latency probe (eager launches) rc=$?"; head -1 $OUT/lat_eager.log
+  echo "latency probe (eager launches) rc=$?"; grep frame_stereo $OUT/lat_eager.log
   timeout -k 10 120 rocprofv3 --kernel-trace --memory-copy-trace --output-format csv -d $OUT/lat -o run -- \
     python3 tools/latency_probe.py > $OUT/lat_prof.log 2>&1
   echo "latency trace rc=$?"
