@@ -100,11 +100,39 @@ __global__ __launch_bounds__(256) void stereo_rows_kernel(const OrbGeom* __restr
   int* items = ws.row_items + (int64_t)f * ws.row_cap;
   for (int i = tid; i <= nrows; i += 256) cnt[i] = 0;
   __syncthreads();
-  for (int i = tid; i < nr; i += 256) {
-    const KeyPoint kp = kr[i];
-    const float r = 2.0f * g->lv[kp.octave].scale;
-    const int maxr = (int)ceilf(kp.y + r), minr = (int)floorf(kp.y - r);
-    for (int yi = max(minr, 0); yi <= min(maxr, nrows - 1); ++yi) atomicAdd(&cnt[yi], 1);
+  // a thread's keypoints are loaded kChunk at a time before their row updates: one load latency
+  // per chunk instead of one per keypoint (a single frame runs this as one work-group)
+  constexpr int kChunk = 8;
+  auto row_span = [&](int base, int (&lo)[kChunk], int (&hi)[kChunk]) {
+    float ky[kChunk];
+    int ko[kChunk];
+#pragma unroll
+    for (int u = 0; u < kChunk; u++) {
+      const int i = base + 256 * u + tid;
+      ky[u] = 0.0f;
+      ko[u] = -1;
+      if (i < nr) {
+        ky[u] = kr[i].y;
+        ko[u] = kr[i].octave;
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < kChunk; u++) {
+      lo[u] = 0;
+      hi[u] = -1;
+      if (ko[u] >= 0) {
+        const float r = 2.0f * g->lv[ko[u]].scale;
+        lo[u] = max((int)floorf(ky[u] - r), 0);
+        hi[u] = min((int)ceilf(ky[u] + r), nrows - 1);
+      }
+    }
+  };
+  for (int base = 0; base < nr; base += 256 * kChunk) {
+    int lo[kChunk], hi[kChunk];
+    row_span(base, lo, hi);
+#pragma unroll
+    for (int u = 0; u < kChunk; u++)
+      for (int yi = lo[u]; yi <= hi[u]; ++yi) atomicAdd(&cnt[yi], 1);
   }
   __syncthreads();
   const int total = scan256<kMaxRows + 1>(cnt, nrows, wsum);
@@ -114,14 +142,15 @@ __global__ __launch_bounds__(256) void stereo_rows_kernel(const OrbGeom* __restr
     if (total > ws.row_cap) atomicOr(err, kErrRowOverflow);
   }
   __syncthreads();
-  for (int i = tid; i < nr; i += 256) {
-    const KeyPoint kp = kr[i];
-    const float r = 2.0f * g->lv[kp.octave].scale;
-    const int maxr = (int)ceilf(kp.y + r), minr = (int)floorf(kp.y - r);
-    for (int yi = max(minr, 0); yi <= min(maxr, nrows - 1); ++yi) {
-      const int pos = atomicAdd(&cnt[yi], 1);
-      if (pos < ws.row_cap) items[pos] = i;
-    }
+  for (int base = 0; base < nr; base += 256 * kChunk) {
+    int lo[kChunk], hi[kChunk];
+    row_span(base, lo, hi);
+#pragma unroll
+    for (int u = 0; u < kChunk; u++)
+      for (int yi = lo[u]; yi <= hi[u]; ++yi) {
+        const int pos = atomicAdd(&cnt[yi], 1);
+        if (pos < ws.row_cap) items[pos] = base + 256 * u + tid;
+      }
   }
 }
 
@@ -331,9 +360,16 @@ __global__ __launch_bounds__(256) void stereo_median_kernel(const OrbGeom* __res
   const int64_t base = (int64_t)f * g->kp_cap;
   if (tid == 0) n_valid = 0;
   __syncthreads();
-  for (int i = tid; i < nl; i += 256) {
-    const int s = ws.sad[base + i];
-    if (s >= 0) vals[atomicAdd(&n_valid, 1)] = (uint32_t)s;
+  for (int i0 = 0; i0 < nl; i0 += 256 * 4) {  // 4 loads in flight per thread
+    int sv[4];
+#pragma unroll
+    for (int u = 0; u < 4; u++) {
+      const int i = i0 + 256 * u + tid;
+      sv[u] = i < nl ? ws.sad[base + i] : -1;
+    }
+#pragma unroll
+    for (int u = 0; u < 4; u++)
+      if (sv[u] >= 0) vals[atomicAdd(&n_valid, 1)] = (uint32_t)sv[u];
   }
   __syncthreads();
   const int n = n_valid;
@@ -461,19 +497,42 @@ __global__ __launch_bounds__(256) void grid_build_kernel(FrameKps cur, Camera ca
   int* cs = gw.cell_start + (int64_t)f * (kGridCells + 1);
   int* items = gw.cell_items + (int64_t)f * kp_cap;
   for (int i = tid; i <= kGridCells; i += 256) cnt[i] = 0;
+  // cells of a thread's keypoints, kChunk loads in flight at a time
+  constexpr int kChunk = 8;
+  auto cells = [&](int base, int (&c)[kChunk]) {
+    float kx[kChunk], ky[kChunk];
+#pragma unroll
+    for (int u = 0; u < kChunk; u++) {
+      const int i = base + 256 * u + tid;
+      kx[u] = ky[u] = 0.0f;
+      if (i < n) {
+        kx[u] = k[i].x;
+        ky[u] = k[i].y;
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < kChunk; u++)
+      c[u] = base + 256 * u + tid < n ? grid_cell(cam, kx[u], ky[u]) : -1;
+  };
   __syncthreads();
-  for (int i = tid; i < n; i += 256) {
-    const int c = grid_cell(cam, k[i].x, k[i].y);
-    if (c >= 0) atomicAdd(&cnt[c], 1);
+  for (int base = 0; base < n; base += 256 * kChunk) {
+    int c[kChunk];
+    cells(base, c);
+#pragma unroll
+    for (int u = 0; u < kChunk; u++)
+      if (c[u] >= 0) atomicAdd(&cnt[c[u]], 1);
   }
   __syncthreads();
   const int total = scan256<kGridCells + 1>(cnt, kGridCells, wsum);
   for (int i = tid; i < kGridCells; i += 256) cs[i] = cnt[i];
   if (tid == 0) cs[kGridCells] = total;
   __syncthreads();
-  for (int i = tid; i < n; i += 256) {
-    const int c = grid_cell(cam, k[i].x, k[i].y);
-    if (c >= 0) items[atomicAdd(&cnt[c], 1)] = i;
+  for (int base = 0; base < n; base += 256 * kChunk) {
+    int c[kChunk];
+    cells(base, c);
+#pragma unroll
+    for (int u = 0; u < kChunk; u++)
+      if (c[u] >= 0) items[atomicAdd(&cnt[c[u]], 1)] = base + 256 * u + tid;
   }
 }
 

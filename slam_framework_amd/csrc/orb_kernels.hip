@@ -2156,6 +2156,7 @@ __global__ __launch_bounds__(kOctLvlThreads) void octree_lvl_kernel(
 
 // ---------------------------------------------------------------------------------------
 constexpr int kKpPerWave = 8;
+constexpr int kOdSmallMaxImages = 16;  // launches up to this many images: 4 keypoints per wave
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 
 // Sum of the 16 per-lane values v[] over the wave; value i ends up in lanes 4i..4i+3.
@@ -2200,22 +2201,51 @@ __device__ __forceinline__ int reduce_scatter16(int (&v)[16], int lane) {
 // OD_PAIRS: a lane task covers two window rows of its 4 columns and stores each column's pair
 // of u16 row sums as one dword (16 dword stores per lane and keypoint instead of 28 u16 ones),
 // over a 46-row (23-dword, odd) column stride: the 10 column quads of a row pair land on 8
-// distinct bank groups instead of 4 (profiles/r3f_ab.log PMC: 5.88 conflict cycles per LDS
-// instruction with u16 stores and a 22-dword stride).
+// distinct bank groups instead of 4. Measured (profiles/r3h_pmc.txt): LDS instructions -45 %,
+// LDS wait cycles 268 -> 24 per wave, but +13 % VALU (the packing) and 3-5 % slower -- the
+// kernel is bound by VALU issue, not by the LDS -- so off by default.
 #ifndef OD_PAIRS
-#define OD_PAIRS 1
+#define OD_PAIRS 0
 #endif
 #ifndef RT_ROWS
 #define RT_ROWS (OD_PAIRS ? 46 : 44)
+#endif
+// OD_CULL: only the row-sum tasks a rotated pattern sample can read (tools/gen_rs_tasks.py: the
+// pixel of any rotation of pattern point p meets the circle |p|): 368 of 430 single-row tasks
+// (six rounds of 64 lanes instead of seven), 189 of 220 row-pair tasks (three instead of four).
+// Measured slower despite 2.6 % fewer VALU instructions (profiles/r3i_ab.log: 1.13-1.15 vs
+// 1.04 ms; waves live 17.5 % longer), so off.
+// OD_MFMA: the horizontal 7-tap pass of the in-window keypoints (all but the border ones) as a
+// banded integer GEMM on the matrix cores: per keypoint 3 x 3 v_mfma_i32_16x16x32_i8 tiles, rows
+// of the window (A: raw bytes - 128, as int8) times a 32 x 16 band of the Gaussian taps shifted by
+// the window origin's misalignment (B, one of four lane constants); the int32 result + 128 * 257
+// is the exact u16 row sum, written transposed as 4-row u16 runs (one ds_write_b64 per tile) --
+// instead of ~140 VALU instructions and 28 u16 stores per keypoint and lane.
+#ifndef OD_MFMA
+#define OD_MFMA 1
+#endif
+// the keypoint loop unrolled (non-MFMA build) or not; the MFMA build keeps it rolled and asks
+// for 4 waves per SIMD: 126 VGPRs, no AGPRs, no spills (unrolled: 159 + 8 AGPRs, 3 waves)
+#ifndef OD_UNROLL_J
+#define OD_UNROLL_J (OD_MFMA ? 0 : 1)
+#endif
+#if OD_MFMA && !defined(OD_WAVES)
+#define OD_WAVES 4
+#endif
+#ifndef OD_CULL
+#define OD_CULL 0
+#endif
+#include "orient_tasks.inc"
+// OD_PATF: the lane's 8 sample offsets as floats, converted once per wave instead of per
+// keypoint (16 VGPRs instead of 4 packed words)
+#ifndef OD_PATF
+#define OD_PATF 1
 #endif
 #ifndef RS_PREFETCH
 #define RS_PREFETCH 1
 #endif
 #ifndef OD_FENCE
 #define OD_FENCE 0
-#endif
-#ifndef OD_UNROLL_J
-#define OD_UNROLL_J 1
 #endif
 #ifndef PAT_PACKED
 #define PAT_PACKED 1
@@ -2243,7 +2273,7 @@ __device__ __forceinline__ uint32_t rt_tap(const uint16_t* rt, int sy, int sx, u
 __global__ __launch_bounds__(256) OD_ATTR void orient_desc_kernel(
     ImageBatch b, const OrbGeom* __restrict__ g, const uint32_t* __restrict__ oct_keys,
     const int* __restrict__ oct_count, KeyPoint* __restrict__ kps, uint8_t* __restrict__ desc,
-    int* __restrict__ nkps) {
+    int* __restrict__ nkps, int kpw) {
   __shared__ __attribute__((aligned(16))) uint16_t s_rt[4][1][kRtCols * kRtRows];
   int img, bx;
   xcd_image_block(&img, &bx);
@@ -2255,9 +2285,10 @@ __global__ __launch_bounds__(256) OD_ATTR void orient_desc_kernel(
     total += lcount[l];
   }
   if (bx == 0 && threadIdx.x == 0) nkps[img] = total;
-  const int k0 = (bx * 4 + wid) * kKpPerWave;
+  // kpw (<= kKpPerWave) keypoints per wave: fewer for small launches, more waves in flight
+  const int k0 = (bx * 4 + wid) * kpw;
   if (k0 >= total) return;
-  const int nk = min(kKpPerWave, total - k0);
+  const int nk = min(kpw, total - k0);
   int my_level = 0, my_key = 0;
   if (lane < nk) {
     int t = k0 + lane, l = 0;
@@ -2354,6 +2385,16 @@ __global__ __launch_bounds__(256) OD_ATTR void orient_desc_kernel(
 #pragma unroll
   for (int r = 0; r < 4; r++)
     pat[r] = reinterpret_cast<const uint32_t*>(c_pattern)[r * 64 + lane];
+#if OD_PATF
+  float patx[4][2], paty[4][2];
+#pragma unroll
+  for (int r = 0; r < 4; r++)
+#pragma unroll
+    for (int e = 0; e < 2; e++) {
+      patx[r][e] = (float)(int)(int8_t)(pat[r] >> (16 * e));
+      paty[r][e] = (float)(int)(int8_t)(pat[r] >> (16 * e + 8));
+    }
+#endif
 #else
   f32x2 ppx[4][2], ppy[4][2];
 #pragma unroll
@@ -2384,14 +2425,24 @@ __global__ __launch_bounds__(256) OD_ATTR void orient_desc_kernel(
   // raw bytes sit at r * pitch + 4 gq past the keypoint's window origin (a lane constant times
   // the level pitch: one v_mad_u32_u24, the origin a scalar base).
   constexpr int kTaskRows = OD_PAIRS ? 2 : 1;              // window rows per lane task
-  constexpr int kTasks = (44 / kTaskRows - (OD_PAIRS ? 0 : 1)) * 10;  // 22 x 10 or 43 x 10
+  constexpr bool kCull = OD_CULL;
+  constexpr int kTasks = kCull ? 64 * (OD_PAIRS ? kRsTaskRounds : kRsTaskRounds1)
+                               : (44 / kTaskRows - (OD_PAIRS ? 0 : 1)) * 10;  // 22 x 10 / 43 x 10
   constexpr int kRounds = (kTasks + 63) / 64;
-  int trow[kRounds], tcol[kRounds];
+  int trow[kRounds], tcol[kRounds];  // trow < 0: no task (culled table padding)
+  int tofs[kRounds];                   // u16 index of the task's (column 4 gq, row r) in the window
 #pragma unroll
   for (int i = 0; i < kRounds; i++) {
     const int t = lane + 64 * i;
-    trow[i] = kTaskRows * (t / 10);
-    tcol[i] = 4 * (t - 10 * (t / 10));
+    if (kCull) {
+      const int e = OD_PAIRS ? c_rs_tasks[t] : c_rs_tasks1[t];
+      trow[i] = e == 0xffff ? -1 : kTaskRows * (e & 0xff);
+      tcol[i] = 4 * ((e >> 8) & 0xff);
+    } else {
+      trow[i] = t < kTasks ? kTaskRows * (t / 10) : -1;
+      tcol[i] = 4 * (t - 10 * (t / 10));
+    }
+    tofs[i] = tcol[i] * kRtRows + max(trow[i], 0);
   }
   // Per keypoint: its row-summed window into LDS, then its 256 tests from LDS. The window's raw
   // rows (one 16-byte load per lane task, 7 tasks per lane) of keypoint j + 1 are in flight
@@ -2424,7 +2475,7 @@ __global__ __launch_bounds__(256) OD_ATTR void orient_desc_kernel(
     if (!G.fastp) return;
 #pragma unroll
     for (int i = 0; i < kRounds; i++) {
-      if (lane + 64 * i < kTasks) {
+      if (trow[i] >= 0) {
 #pragma unroll
         for (int h = 0; h < kTaskRows; h++) {
           // row 43 (the pad of the last pair, weight 0 in every tap) re-reads row 42: the
@@ -2437,8 +2488,51 @@ __global__ __launch_bounds__(256) OD_ATTR void orient_desc_kernel(
     }
   };
   uint16_t* rtw = &s_rt[wid][0][0];
+#if OD_MFMA
+  static_assert(!OD_PAIRS && RS_PREFETCH, "the MFMA row sums use the u16 layout and prefetch");
+  typedef int v4i_t __attribute__((ext_vector_type(4)));
+  const int mf_n = lane & 15, mf_h = lane >> 4;
+  // B operands: band[k][n] = k_(k - n - s) (0 outside the 7 taps) for window-origin shift s; lane
+  // (n, h) holds band[8 h + jb][n] in byte jb. Kept in the wave's LDS (read back per keypoint by
+  // its shift: one ds_read_b64) rather than in 8 VGPRs.
+  __shared__ uint64_t s_bm[4][4][64];
+#pragma unroll
+  for (int sv = 0; sv < 4; sv++) {
+    uint64_t v = 0;
+#pragma unroll
+    for (int jb = 0; jb < 8; jb++) {
+      const int d = 8 * mf_h + jb - mf_n - sv;
+      const uint32_t gv = (d >= 0 && d <= 6) ? (uint32_t)g->gauss[d] : 0u;
+      v |= (uint64_t)gv << (8 * jb);
+    }
+    s_bm[wid][sv][lane] = v;
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  // A operands of tile (ti, tj): window row 16 ti + n (rows past 42 re-read row 42; never stored)
+  // bytes 16 tj + 8 h .. + 7 from the dword-aligned origin; bytes 48.. are never needed (the
+  // samples read window columns <= 36: bytes <= 36 + 3 + 6), loaded as 0x80 (int8 zero)
+  auto mf_load = [&](const RsGeo& G, uint2 (&a)[9]) {
+    if (!G.fastp) return;
+#pragma unroll
+    for (int ti = 0; ti < 3; ti++) {
+      const uint32_t row = (uint32_t)min(16 * ti + mf_n, 42);
+      const uint8_t* rp = G.org + __umul24(row, (uint32_t)G.pitch) + 8 * mf_h;
+#pragma unroll
+      for (int tj = 0; tj < 3; tj++)
+        a[3 * ti + tj] = (tj == 2 && mf_h >= 2) ? make_uint2(0x80808080u, 0x80808080u)
+                                                 : *reinterpret_cast<const uint2*>(rp + 16 * tj);
+    }
+  };
+  // lane's u16 index of its C rows 4 h .. 4 h + 3 of column n in tile (0, 0)
+  const int mf_st = mf_n * kRtRows + 4 * mf_h;
+#endif
   RsGeo gn = rs_geo(0);
-#if RS_PREFETCH
+#if OD_MFMA
+  uint2 an[9];
+  mf_load(gn, an);
+#elif RS_PREFETCH
   uint4 qn[kRounds * kTaskRows];
   rs_load(gn, qn);
 #endif
@@ -2448,7 +2542,31 @@ __global__ __launch_bounds__(256) OD_ATTR void orient_desc_kernel(
 #pragma unroll 1
 #endif
   for (int j = 0; j < kKpPerWave; j++) {
+    if (j >= nk) break;  // wave-uniform
     const RsGeo G = gn;
+    const uint32_t sft = (uint32_t)((G.kx - 21) & 3);
+#if OD_MFMA
+    uint2 a[9];
+#pragma unroll
+    for (int i = 0; i < 9; i++) a[i] = an[i];
+    if (G.fastp) {  // wave-uniform: every lane takes part in the MFMAs
+      const uint64_t B = s_bm[wid][sft][lane];
+      const v4i_t cinit = {128 * 257, 128 * 257, 128 * 257, 128 * 257};
+#pragma unroll
+      for (int ti = 0; ti < 3; ti++)
+#pragma unroll
+        for (int tj = 0; tj < 3; tj++) {
+          const uint2 v = a[3 * ti + tj];
+          const uint64_t A = (uint64_t)(v.y ^ 0x80808080u) << 32 | (v.x ^ 0x80808080u);
+          const v4i_t c = __builtin_amdgcn_mfma_i32_16x16x32_i8((long)A, (long)B, cinit, 0, 0, 0);
+          // rows >= 44 and columns >= 40 fall outside the window's LDS image
+          if (!(ti == 2 && mf_h == 3) && !(tj == 2 && mf_n >= 8))
+            *reinterpret_cast<uint2*>(rtw + mf_st + 16 * tj * kRtRows + 16 * ti) =
+                make_uint2((uint32_t)c[0] | (uint32_t)c[1] << 16,
+                           (uint32_t)c[2] | (uint32_t)c[3] << 16);
+        }
+    } else
+#else
     uint4 q[kRounds * kTaskRows];
 #if RS_PREFETCH
 #pragma unroll
@@ -2456,22 +2574,24 @@ __global__ __launch_bounds__(256) OD_ATTR void orient_desc_kernel(
 #else
     rs_load(G, q);
 #endif
-    const uint32_t sft = (uint32_t)((G.kx - 21) & 3);
+#endif
 #pragma unroll
     for (int i = 0; i < kRounds; i++) {
-      const int t = lane + 64 * i;
-      if (t < kTasks) {
+      if (trow[i] >= 0) {
         const int r = trow[i], gq = tcol[i] >> 2;
         uint32_t R[kTaskRows][4];
 #pragma unroll
         for (int h = 0; h < kTaskRows; h++) {
           uint32_t u0, u1, u2;
+#if !OD_MFMA
           if (G.fastp) {
             const uint4 v = q[kTaskRows * i + h];
             u0 = __builtin_amdgcn_alignbyte(v.y, v.x, sft);
             u1 = __builtin_amdgcn_alignbyte(v.z, v.y, sft);
             u2 = __builtin_amdgcn_alignbyte(v.w, v.z, sft);
-          } else {  // the window leaves the level: reflect-101 rows and columns, byte loads
+          } else
+#endif
+          {  // the window leaves the level: reflect-101 rows and columns, byte loads
             const int rr = min(r + h, 42);
             const uint8_t* row = G.im + (int64_t)reflect101(G.ky - 21 + rr, G.h) * G.pitch;
             const int x0 = G.kx - 18 + 4 * gq;
@@ -2497,8 +2617,9 @@ __global__ __launch_bounds__(256) OD_ATTR void orient_desc_kernel(
         for (int jx = 0; jx < 4; jx++)
           rtw32[(4 * gq + jx) * (kRtRows / 2) + (r >> 1)] = (R[0][jx] & 0xffffu) | R[1][jx] << 16;
 #else
+        uint16_t* rtt = rtw + tofs[i];
 #pragma unroll
-        for (int jx = 0; jx < 4; jx++) rtw[(4 * gq + jx) * kRtRows + r] = (uint16_t)R[0][jx];
+        for (int jx = 0; jx < 4; jx++) rtt[jx * kRtRows] = (uint16_t)R[0][jx];
 #endif
       }
     }
@@ -2509,9 +2630,11 @@ __global__ __launch_bounds__(256) OD_ATTR void orient_desc_kernel(
 #else
     __asm__ volatile("" ::: "memory");
 #endif
-    if (j + 1 < kKpPerWave) {
+    if (j + 1 < nk) {
       gn = rs_geo(j + 1);
-#if RS_PREFETCH
+#if OD_MFMA
+      mf_load(gn, an);
+#elif RS_PREFETCH
       rs_load(gn, qn);
 #endif
     }
@@ -2522,24 +2645,37 @@ __global__ __launch_bounds__(256) OD_ATTR void orient_desc_kernel(
       const float sj = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(sa), 8 * j));
       const f32x2 ab = {sj, cj}, nab = {cj, -sj};
       const uint32_t* rt32 = reinterpret_cast<const uint32_t*>(&s_rt[wid][0][0]);
+      // a sample's LDS byte offset straight from the float bits b = 0x4B400000 + c of its
+      // rounded window coordinates (cx, cy): the low 24 bits of bx are 0x400000 + cx, and
+      // 0x4B400000 is even, so (cy & ~1) * 2 = (by << 1) & ~3 minus a constant -- the constants
+      // fold into one wave-uniform base (mad_u24, lshl_add, and: 3 VALU instead of 6)
+      const uint8_t* rt8 = reinterpret_cast<const uint8_t*>(&s_rt[0][0][0]);
+      const uint32_t abase = (uint32_t)(wid * (int)sizeof(s_rt[0])) -
+                             (uint32_t)(2 * kRtRows) * 0x400000u - 0x96800000u;
       // the 256 tests; kTail: the window reaches the scalar tail of the row (x >= W - W % 4,
       // rounded half up instead of half to even) -- a wave-uniform case, so two code paths
       auto tests = [&](auto tail_case) {
         constexpr bool kTail = decltype(tail_case)::value;
         const int xt = xvec - kx + 18;  // window columns c >= xt are in the tail
+        const uint32_t xtb = 0x4B400000u + (uint32_t)xt;  // ... as float bits
 #pragma unroll
         for (int r = 0; r < 4; r++) {
           uint32_t v[2];
 #pragma unroll
           for (int e = 0; e < 2; e++) {
+#if OD_PATF
+            const float px = patx[r][e], py = paty[r][e];
+#else
             const float px = (float)(int)(int8_t)(pat[r] >> (16 * e));
             const float py = (float)(int)(int8_t)(pat[r] >> (16 * e + 8));
+#endif
             const f32x2 sp = __builtin_elementwise_fma((f32x2){px, px}, ab, (f32x2){py, py} * nab) + magic;
-            const uint32_t cy = __float_as_uint(sp.x) - 0x4B400000u;  // window row of sy - 3
-            const uint32_t cx = __float_as_uint(sp.y) - 0x4B400000u;  // window column
-            const uint32_t e0 = __umul24(cx, (uint32_t)kRtRows) + cy;
-            const uint32_t* rw = rt32 + (e0 >> 1);
-            const uint32_t sh = cy << 4;  // alignbit takes it mod 32: 16 for an odd start
+            const uint32_t by = __float_as_uint(sp.x);  // 0x4B400000 + window row of sy - 3
+            const uint32_t bx = __float_as_uint(sp.y);  // 0x4B400000 + window column
+            // 2 kRtRows * bx and abase are multiples of 4: one mask after the sum does (by & ~1) * 2
+            const uint32_t off = (__umul24(bx, (uint32_t)(2 * kRtRows)) + abase + (by << 1)) & ~3u;
+            const uint32_t* rw = reinterpret_cast<const uint32_t*>(rt8 + off);
+            const uint32_t sh = by << 4;  // alignbit takes it mod 32: 16 for an odd row
             const uint32_t w0 = rw[0], w1 = rw[1], w2 = rw[2], w3 = rw[3];
             const uint32_t p0 = __builtin_amdgcn_alignbit(w1, w0, sh);
             const uint32_t p1 = __builtin_amdgcn_alignbit(w2, w1, sh);
@@ -2548,7 +2684,7 @@ __global__ __launch_bounds__(256) OD_ATTR void orient_desc_kernel(
             const uint32_t sm = dot2u(p0, K01, dot2u(p1, K23, dot2u(p2, K21, dot2u(p3, K0, 0u))));
             uint32_t o;
             if (kTail) {
-              const bool tail = (int)cx >= xt;
+              const bool tail = bx >= xtb;
               o = (sm + (tail ? 0x8000u : 0x7fffu + ((sm >> 16) & 1u))) >> 16;
             } else {
               o = (sm + 0x7fffu + ((sm >> 16) & 1u)) >> 16;
@@ -2708,10 +2844,11 @@ void launch_extract(const ImageBatch& b, const OrbGeomDev& gd, int n_images, hip
   SLAMGPU_LAUNCH("octree_global", st, octree_kernel, dim3(g.nlevels, n_images), dim3(kOctThreads), 0, st, gd.dev,
                      gd.ws.cell_keys, gd.ws.cell_count, gd.ws.key_scratch, gd.ws.node_scratch,
                      gd.ws.oct_keys, gd.ws.oct_count, gd.ws.err);
+  const int kpw = n_images <= kOdSmallMaxImages ? kKpPerWave / 2 : kKpPerWave;
   SLAMGPU_LAUNCH("orient_desc", st, orient_desc_kernel,
-                 dim3((g.kp_cap + 4 * kKpPerWave - 1) / (4 * kKpPerWave), n_images), dim3(256), 0,
+                 dim3((g.kp_cap + 4 * kpw - 1) / (4 * kpw), n_images), dim3(256), 0,
                  st, b, gd.dev, gd.ws.oct_keys, gd.ws.oct_count, gd.out.kps, gd.out.desc,
-                 gd.out.nkps);
+                 gd.out.nkps, kpw);
 }
 
 }  // namespace slamgpu
