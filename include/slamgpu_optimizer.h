@@ -43,8 +43,10 @@ typedef struct {
   int32_t octave;
 } slamgpu_pose_edge;
 
-/* Largest edge count per frame the pose kernel takes (frames carry <= nfeatures keypoints). */
-#define SLAMGPU_POSE_MAX_EDGES 4096
+/* Largest edge count per frame the pose kernels take (frames carry <= nfeatures keypoints, so
+ * nfeatures up to ~16k). Frames up to 4096 edges run with their edges in LDS; larger ones on an
+ * 8-wave work-group reading them from L2. */
+#define SLAMGPU_POSE_MAX_EDGES 16384
 #define SLAMGPU_MAX_LEVELS 32
 
 /* Replaces: int Optimizer::PoseOptimization(Frame* pFrame)  optimizer.cpp:209-411.

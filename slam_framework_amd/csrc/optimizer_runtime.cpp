@@ -183,7 +183,7 @@ int slamgpu_pose_optimization(const slamgpu_camera* cam, const float* inv_sigma2
   OPT_HIPCHECK(launch_pose_optimization(
       reinterpret_cast<const slamgpu_pose_edge*>(b + off_e), reinterpret_cast<int32_t*>(b), 1, P,
       reinterpret_cast<float*>(b + off_T), reinterpret_cast<uint8_t*>(b + off_o),
-      reinterpret_cast<int32_t*>(b + off_r), nullptr, S.stream));
+      reinterpret_cast<int32_t*>(b + off_r), nullptr, S.stream, n));
   int32_t res = 0;
   OPT_HIPCHECK(hipMemcpyAsync(&res, b + off_r, sizeof(res), hipMemcpyDeviceToHost, S.stream));
   OPT_HIPCHECK(hipMemcpyAsync(Tcw, b + off_T, 16 * sizeof(float), hipMemcpyDeviceToHost, S.stream));

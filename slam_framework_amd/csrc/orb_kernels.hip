@@ -2210,19 +2210,17 @@ __device__ __forceinline__ int reduce_scatter16(int (&v)[16], int lane) {
 #ifndef RT_ROWS
 #define RT_ROWS (OD_PAIRS ? 46 : 44)
 #endif
-// OD_CULL: only the row-sum tasks a rotated pattern sample can read (tools/gen_rs_tasks.py: the
-// pixel of any rotation of pattern point p meets the circle |p|): 368 of 430 single-row tasks
-// (six rounds of 64 lanes instead of seven), 189 of 220 row-pair tasks (three instead of four).
-// Measured slower despite 2.6 % fewer VALU instructions (profiles/r3i_ab.log: 1.13-1.15 vs
-// 1.04 ms; waves live 17.5 % longer), so off.
 // OD_MFMA: the horizontal 7-tap pass of the in-window keypoints (all but the border ones) as a
 // banded integer GEMM on the matrix cores: per keypoint 3 x 3 v_mfma_i32_16x16x32_i8 tiles, rows
 // of the window (A: raw bytes - 128, as int8) times a 32 x 16 band of the Gaussian taps shifted by
 // the window origin's misalignment (B, one of four lane constants); the int32 result + 128 * 257
 // is the exact u16 row sum, written transposed as 4-row u16 runs (one ds_write_b64 per tile) --
 // instead of ~140 VALU instructions and 28 u16 stores per keypoint and lane.
+// Measured 1.36-1.38 ms against 1.03 (profiles/r3j_ab.log; layout verified by
+// tools/mfma_i8_probe.hip, parity green): the VALU count per wave fell only 3 % and waves live
+// 28 % longer (MFMA result latency on the keypoint's critical path), so off.
 #ifndef OD_MFMA
-#define OD_MFMA 1
+#define OD_MFMA 0
 #endif
 // the keypoint loop unrolled (non-MFMA build) or not; the MFMA build keeps it rolled and asks
 // for 4 waves per SIMD: 126 VGPRs, no AGPRs, no spills (unrolled: 159 + 8 AGPRs, 3 waves)
@@ -2231,15 +2229,6 @@ __device__ __forceinline__ int reduce_scatter16(int (&v)[16], int lane) {
 #endif
 #if OD_MFMA && !defined(OD_WAVES)
 #define OD_WAVES 4
-#endif
-#ifndef OD_CULL
-#define OD_CULL 0
-#endif
-#include "orient_tasks.inc"
-// OD_PATF: the lane's 8 sample offsets as floats, converted once per wave instead of per
-// keypoint (16 VGPRs instead of 4 packed words)
-#ifndef OD_PATF
-#define OD_PATF 1
 #endif
 #ifndef RS_PREFETCH
 #define RS_PREFETCH 1
@@ -2270,10 +2259,13 @@ __device__ __forceinline__ uint32_t rt_tap(const uint16_t* rt, int sy, int sx, u
 #else
 #define OD_ATTR
 #endif
+// KPW (<= kKpPerWave) keypoints per wave: 8 for batches, 4 for small launches (more waves in
+// flight for the single-frame call)
+template <int KPW>
 __global__ __launch_bounds__(256) OD_ATTR void orient_desc_kernel(
     ImageBatch b, const OrbGeom* __restrict__ g, const uint32_t* __restrict__ oct_keys,
     const int* __restrict__ oct_count, KeyPoint* __restrict__ kps, uint8_t* __restrict__ desc,
-    int* __restrict__ nkps, int kpw) {
+    int* __restrict__ nkps) {
   __shared__ __attribute__((aligned(16))) uint16_t s_rt[4][1][kRtCols * kRtRows];
   int img, bx;
   xcd_image_block(&img, &bx);
@@ -2285,10 +2277,9 @@ __global__ __launch_bounds__(256) OD_ATTR void orient_desc_kernel(
     total += lcount[l];
   }
   if (bx == 0 && threadIdx.x == 0) nkps[img] = total;
-  // kpw (<= kKpPerWave) keypoints per wave: fewer for small launches, more waves in flight
-  const int k0 = (bx * 4 + wid) * kpw;
+  const int k0 = (bx * 4 + wid) * KPW;
   if (k0 >= total) return;
-  const int nk = min(kpw, total - k0);
+  const int nk = min(KPW, total - k0);
   int my_level = 0, my_key = 0;
   if (lane < nk) {
     int t = k0 + lane, l = 0;
@@ -2385,16 +2376,6 @@ __global__ __launch_bounds__(256) OD_ATTR void orient_desc_kernel(
 #pragma unroll
   for (int r = 0; r < 4; r++)
     pat[r] = reinterpret_cast<const uint32_t*>(c_pattern)[r * 64 + lane];
-#if OD_PATF
-  float patx[4][2], paty[4][2];
-#pragma unroll
-  for (int r = 0; r < 4; r++)
-#pragma unroll
-    for (int e = 0; e < 2; e++) {
-      patx[r][e] = (float)(int)(int8_t)(pat[r] >> (16 * e));
-      paty[r][e] = (float)(int)(int8_t)(pat[r] >> (16 * e + 8));
-    }
-#endif
 #else
   f32x2 ppx[4][2], ppy[4][2];
 #pragma unroll
@@ -2425,24 +2406,14 @@ __global__ __launch_bounds__(256) OD_ATTR void orient_desc_kernel(
   // raw bytes sit at r * pitch + 4 gq past the keypoint's window origin (a lane constant times
   // the level pitch: one v_mad_u32_u24, the origin a scalar base).
   constexpr int kTaskRows = OD_PAIRS ? 2 : 1;              // window rows per lane task
-  constexpr bool kCull = OD_CULL;
-  constexpr int kTasks = kCull ? 64 * (OD_PAIRS ? kRsTaskRounds : kRsTaskRounds1)
-                               : (44 / kTaskRows - (OD_PAIRS ? 0 : 1)) * 10;  // 22 x 10 / 43 x 10
+  constexpr int kTasks = (44 / kTaskRows - (OD_PAIRS ? 0 : 1)) * 10;  // 22 x 10 / 43 x 10
   constexpr int kRounds = (kTasks + 63) / 64;
-  int trow[kRounds], tcol[kRounds];  // trow < 0: no task (culled table padding)
-  int tofs[kRounds];                   // u16 index of the task's (column 4 gq, row r) in the window
+  int trow[kRounds], tcol[kRounds];  // trow < 0: no task (last round's padding)
 #pragma unroll
   for (int i = 0; i < kRounds; i++) {
     const int t = lane + 64 * i;
-    if (kCull) {
-      const int e = OD_PAIRS ? c_rs_tasks[t] : c_rs_tasks1[t];
-      trow[i] = e == 0xffff ? -1 : kTaskRows * (e & 0xff);
-      tcol[i] = 4 * ((e >> 8) & 0xff);
-    } else {
-      trow[i] = t < kTasks ? kTaskRows * (t / 10) : -1;
-      tcol[i] = 4 * (t - 10 * (t / 10));
-    }
-    tofs[i] = tcol[i] * kRtRows + max(trow[i], 0);
+    trow[i] = t < kTasks ? kTaskRows * (t / 10) : -1;
+    tcol[i] = 4 * (t - 10 * (t / 10));
   }
   // Per keypoint: its row-summed window into LDS, then its 256 tests from LDS. The window's raw
   // rows (one 16-byte load per lane task, 7 tasks per lane) of keypoint j + 1 are in flight
@@ -2541,8 +2512,7 @@ __global__ __launch_bounds__(256) OD_ATTR void orient_desc_kernel(
 #else
 #pragma unroll 1
 #endif
-  for (int j = 0; j < kKpPerWave; j++) {
-    if (j >= nk) break;  // wave-uniform
+  for (int j = 0; j < KPW; j++) {
     const RsGeo G = gn;
     const uint32_t sft = (uint32_t)((G.kx - 21) & 3);
 #if OD_MFMA
@@ -2617,9 +2587,8 @@ __global__ __launch_bounds__(256) OD_ATTR void orient_desc_kernel(
         for (int jx = 0; jx < 4; jx++)
           rtw32[(4 * gq + jx) * (kRtRows / 2) + (r >> 1)] = (R[0][jx] & 0xffffu) | R[1][jx] << 16;
 #else
-        uint16_t* rtt = rtw + tofs[i];
 #pragma unroll
-        for (int jx = 0; jx < 4; jx++) rtt[jx * kRtRows] = (uint16_t)R[0][jx];
+        for (int jx = 0; jx < 4; jx++) rtw[(4 * gq + jx) * kRtRows + r] = (uint16_t)R[0][jx];
 #endif
       }
     }
@@ -2630,7 +2599,7 @@ __global__ __launch_bounds__(256) OD_ATTR void orient_desc_kernel(
 #else
     __asm__ volatile("" ::: "memory");
 #endif
-    if (j + 1 < nk) {
+    if (j + 1 < KPW) {
       gn = rs_geo(j + 1);
 #if OD_MFMA
       mf_load(gn, an);
@@ -2645,37 +2614,24 @@ __global__ __launch_bounds__(256) OD_ATTR void orient_desc_kernel(
       const float sj = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(sa), 8 * j));
       const f32x2 ab = {sj, cj}, nab = {cj, -sj};
       const uint32_t* rt32 = reinterpret_cast<const uint32_t*>(&s_rt[wid][0][0]);
-      // a sample's LDS byte offset straight from the float bits b = 0x4B400000 + c of its
-      // rounded window coordinates (cx, cy): the low 24 bits of bx are 0x400000 + cx, and
-      // 0x4B400000 is even, so (cy & ~1) * 2 = (by << 1) & ~3 minus a constant -- the constants
-      // fold into one wave-uniform base (mad_u24, lshl_add, and: 3 VALU instead of 6)
-      const uint8_t* rt8 = reinterpret_cast<const uint8_t*>(&s_rt[0][0][0]);
-      const uint32_t abase = (uint32_t)(wid * (int)sizeof(s_rt[0])) -
-                             (uint32_t)(2 * kRtRows) * 0x400000u - 0x96800000u;
       // the 256 tests; kTail: the window reaches the scalar tail of the row (x >= W - W % 4,
       // rounded half up instead of half to even) -- a wave-uniform case, so two code paths
       auto tests = [&](auto tail_case) {
         constexpr bool kTail = decltype(tail_case)::value;
         const int xt = xvec - kx + 18;  // window columns c >= xt are in the tail
-        const uint32_t xtb = 0x4B400000u + (uint32_t)xt;  // ... as float bits
 #pragma unroll
         for (int r = 0; r < 4; r++) {
           uint32_t v[2];
 #pragma unroll
           for (int e = 0; e < 2; e++) {
-#if OD_PATF
-            const float px = patx[r][e], py = paty[r][e];
-#else
             const float px = (float)(int)(int8_t)(pat[r] >> (16 * e));
             const float py = (float)(int)(int8_t)(pat[r] >> (16 * e + 8));
-#endif
             const f32x2 sp = __builtin_elementwise_fma((f32x2){px, px}, ab, (f32x2){py, py} * nab) + magic;
-            const uint32_t by = __float_as_uint(sp.x);  // 0x4B400000 + window row of sy - 3
-            const uint32_t bx = __float_as_uint(sp.y);  // 0x4B400000 + window column
-            // 2 kRtRows * bx and abase are multiples of 4: one mask after the sum does (by & ~1) * 2
-            const uint32_t off = (__umul24(bx, (uint32_t)(2 * kRtRows)) + abase + (by << 1)) & ~3u;
-            const uint32_t* rw = reinterpret_cast<const uint32_t*>(rt8 + off);
-            const uint32_t sh = by << 4;  // alignbit takes it mod 32: 16 for an odd row
+            const uint32_t cy = __float_as_uint(sp.x) - 0x4B400000u;  // window row of sy - 3
+            const uint32_t cx = __float_as_uint(sp.y) - 0x4B400000u;  // window column
+            const uint32_t e0 = __umul24(cx, (uint32_t)kRtRows) + cy;
+            const uint32_t* rw = rt32 + (e0 >> 1);
+            const uint32_t sh = cy << 4;  // alignbit takes it mod 32: 16 for an odd start
             const uint32_t w0 = rw[0], w1 = rw[1], w2 = rw[2], w3 = rw[3];
             const uint32_t p0 = __builtin_amdgcn_alignbit(w1, w0, sh);
             const uint32_t p1 = __builtin_amdgcn_alignbit(w2, w1, sh);
@@ -2684,7 +2640,7 @@ __global__ __launch_bounds__(256) OD_ATTR void orient_desc_kernel(
             const uint32_t sm = dot2u(p0, K01, dot2u(p1, K23, dot2u(p2, K21, dot2u(p3, K0, 0u))));
             uint32_t o;
             if (kTail) {
-              const bool tail = bx >= xtb;
+              const bool tail = (int)cx >= xt;
               o = (sm + (tail ? 0x8000u : 0x7fffu + ((sm >> 16) & 1u))) >> 16;
             } else {
               o = (sm + 0x7fffu + ((sm >> 16) & 1u)) >> 16;
@@ -2844,11 +2800,17 @@ void launch_extract(const ImageBatch& b, const OrbGeomDev& gd, int n_images, hip
   SLAMGPU_LAUNCH("octree_global", st, octree_kernel, dim3(g.nlevels, n_images), dim3(kOctThreads), 0, st, gd.dev,
                      gd.ws.cell_keys, gd.ws.cell_count, gd.ws.key_scratch, gd.ws.node_scratch,
                      gd.ws.oct_keys, gd.ws.oct_count, gd.ws.err);
-  const int kpw = n_images <= kOdSmallMaxImages ? kKpPerWave / 2 : kKpPerWave;
-  SLAMGPU_LAUNCH("orient_desc", st, orient_desc_kernel,
-                 dim3((g.kp_cap + 4 * kpw - 1) / (4 * kpw), n_images), dim3(256), 0,
-                 st, b, gd.dev, gd.ws.oct_keys, gd.ws.oct_count, gd.out.kps, gd.out.desc,
-                 gd.out.nkps, kpw);
+  if (n_images <= kOdSmallMaxImages) {
+    constexpr int kpw = kKpPerWave / 2;
+    SLAMGPU_LAUNCH("orient_desc", st, orient_desc_kernel<kpw>,
+                   dim3((g.kp_cap + 4 * kpw - 1) / (4 * kpw), n_images), dim3(256), 0, st, b,
+                   gd.dev, gd.ws.oct_keys, gd.ws.oct_count, gd.out.kps, gd.out.desc, gd.out.nkps);
+  } else {
+    SLAMGPU_LAUNCH("orient_desc", st, orient_desc_kernel<kKpPerWave>,
+                   dim3((g.kp_cap + 4 * kKpPerWave - 1) / (4 * kKpPerWave), n_images), dim3(256),
+                   0, st, b, gd.dev, gd.ws.oct_keys, gd.ws.oct_count, gd.out.kps, gd.out.desc,
+                   gd.out.nkps);
+  }
 }
 
 }  // namespace slamgpu

@@ -21,6 +21,6 @@ struct PoseParams {
 hipError_t launch_pose_optimization(const slamgpu_pose_edge* d_edges, const int32_t* d_edge_start,
                                     int n_frames, const PoseParams& P, float* d_Tcw,
                                     uint8_t* d_outlier, int32_t* d_n_inliers,
-                                    int32_t* d_lm_iterations, hipStream_t st);
+                                    int32_t* d_lm_iterations, hipStream_t st, int max_edges = -1);
 
 }  // namespace slamgpu

@@ -47,6 +47,7 @@ using se3::se3_left_update;
 constexpr int kNH = 21;  // upper triangle of the 6x6 H
 // Batches smaller than this run 8 waves per frame (latency); larger ones one wave per frame.
 constexpr int kPoseLatencyFrames = 64;
+constexpr int kPoseLdsEdges = 4096;  // edges of one frame the 1- and 8-wave variants take
 
 // H x = b for the 6x6 H + lambda I, LDLT without pivoting; a zero pivot gives a zero component
 // (Eigen's rule), a negative one fails the solve (LinearSolverDense::solve returns false and
@@ -262,27 +263,30 @@ struct FrameSum {
 #ifndef POSE_LAT_W  // waves per frame of the latency variant
 #define POSE_LAT_W 8
 #endif
-template <int W>
+// kMaxE: the edges one frame may have in this variant (kMaxE / (64 W) slots per thread, <= 64).
+// Frames with fewer than min_edges edges belong to another launch and are left untouched.
+template <int W, int kMaxE>
 __global__ __launch_bounds__(64 * W) void pose_opt_kernel(
     const slamgpu_pose_edge* __restrict__ edges, const int32_t* __restrict__ edge_start,
     PoseParams P, float* __restrict__ Tcw, uint8_t* __restrict__ outlier_out,
-    int32_t* __restrict__ n_inliers, int32_t* __restrict__ lm_iterations) {
+    int32_t* __restrict__ n_inliers, int32_t* __restrict__ lm_iterations, int min_edges) {
 #pragma clang fp contract(fast)  // tolerance-compared FP64 path: let the edge sums fuse
   constexpr int kThreads = 64 * W;
-  constexpr int kEpt = SLAMGPU_POSE_MAX_EDGES / kThreads;
-  static_assert(kEpt <= 64, "slot masks are 64-bit");
+  constexpr int kEpt = kMaxE / kThreads;
+  static_assert(kEpt <= 64 && kEpt * kThreads == kMaxE, "slot masks are 64-bit");
   __shared__ FrameSum<W> fs;
   __shared__ float isig[SLAMGPU_MAX_LEVELS];  // Frame::mvInvLevelSigma2
   // the latency variant (one frame per work-group of W waves) keeps the frame's edges in LDS
   // (4096 x 28 B): the passes then wait on LDS, not on L2, for each edge slot
-  constexpr bool kLdsEdges = W > 1;
-  __shared__ uint32_t s_edges[kLdsEdges ? SLAMGPU_POSE_MAX_EDGES * 7 : 1];
+  constexpr bool kLdsEdges = W > 1 && kMaxE <= kPoseLdsEdges;
+  __shared__ uint32_t s_edges[kLdsEdges ? kMaxE * 7 : 1];
   const int f = blockIdx.x, tid = threadIdx.x;
   const int e0 = edge_start[f];
   const int n = edge_start[f + 1] - e0;
   const slamgpu_pose_edge* E = edges + e0;
   uint8_t* outl_out = outlier_out + e0;
-  if (n > SLAMGPU_POSE_MAX_EDGES || n < 0) {
+  if (n < min_edges) return;  // another launch's frame
+  if (n > kMaxE || n < 0) {
     if (tid == 0) {
       n_inliers[f] = -1;
       if (lm_iterations) lm_iterations[f] = 0;
@@ -545,18 +549,26 @@ __global__ __launch_bounds__(64 * W) void pose_opt_kernel(
 hipError_t launch_pose_optimization(const slamgpu_pose_edge* d_edges, const int32_t* d_edge_start,
                                     int n_frames, const PoseParams& P, float* d_Tcw,
                                     uint8_t* d_outlier, int32_t* d_n_inliers,
-                                    int32_t* d_lm_iterations, hipStream_t st) {
+                                    int32_t* d_lm_iterations, hipStream_t st, int max_edges) {
   if (n_frames <= 0) return hipSuccess;
   if (n_frames < kPoseLatencyFrames) {
     // few frames: POSE_LAT_W waves per frame for latency (the per-frame tracking call)
-    SLAMGPU_LAUNCH("pose_opt", st, pose_opt_kernel<POSE_LAT_W>, dim3(n_frames),
+    SLAMGPU_LAUNCH("pose_opt", st, (pose_opt_kernel<POSE_LAT_W, kPoseLdsEdges>), dim3(n_frames),
                    dim3(64 * POSE_LAT_W), 0, st, d_edges, d_edge_start, P, d_Tcw, d_outlier,
-                   d_n_inliers, d_lm_iterations);
+                   d_n_inliers, d_lm_iterations, 0);
   } else {
     // batches: one wave per frame, many frames resident per CU
-    SLAMGPU_LAUNCH("pose_opt", st, pose_opt_kernel<1>, dim3(n_frames), dim3(64), 0, st, d_edges,
-                   d_edge_start, P, d_Tcw, d_outlier, d_n_inliers, d_lm_iterations);
+    SLAMGPU_LAUNCH("pose_opt", st, (pose_opt_kernel<1, kPoseLdsEdges>), dim3(n_frames), dim3(64),
+                   0, st, d_edges, d_edge_start, P, d_Tcw, d_outlier, d_n_inliers,
+                   d_lm_iterations, 0);
   }
+  // frames past the LDS variants' 4096 edges (the launch above marked them -1): 8 waves, 32
+  // edge slots per thread read from L2, up to SLAMGPU_POSE_MAX_EDGES; max_edges < 0 = unknown
+  // (device batches). 16 waves would cap the registers at 128 and spill.
+  if (max_edges < 0 || max_edges > kPoseLdsEdges)
+    SLAMGPU_LAUNCH("pose_opt", st, (pose_opt_kernel<8, SLAMGPU_POSE_MAX_EDGES>), dim3(n_frames),
+                   dim3(64 * 8), 0, st, d_edges, d_edge_start, P, d_Tcw, d_outlier,
+                   d_n_inliers, d_lm_iterations, kPoseLdsEdges + 1);
   return hipGetLastError();
 }
 

@@ -41,7 +41,7 @@ SIM3_EDGE_DTYPE = np.dtype([("i", "<i4"), ("j", "<i4"), ("pad", "<i4", (2,)), ("
 # slamgpu_pose_edge (include/slamgpu_optimizer.h): one PoseOptimization correspondence.
 POSE_EDGE_DTYPE = np.dtype([("xw", "<f4", (3,)), ("u", "<f4"), ("v", "<f4"), ("ur", "<f4"),
                             ("octave", "<i4")])
-POSE_MAX_EDGES = 4096
+POSE_MAX_EDGES = 16384  # == SLAMGPU_POSE_MAX_EDGES
 # slamgpu_ba_obs (include/slamgpu_optimizer.h): one LocalBundleAdjustment observation.
 BA_OBS_DTYPE = np.dtype([("keyframe", "<i4"), ("u", "<f4"), ("v", "<f4"), ("ur", "<f4"),
                          ("octave", "<i4")])

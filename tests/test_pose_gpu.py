@@ -34,6 +34,8 @@ CASES = [  # (seed, n, stereo_frac, outlier_frac, noise_px)
     (6, 300, 0.6, 0.0, 0.0),
     (7, 9, 0.5, 0.0, 0.5),
     (8, 12, 0.5, 0.2, 0.5),
+    (9, 4097, 0.6, 0.1, 0.7),    # past the LDS variants: the L2-edge kernel
+    (10, 16384, 0.5, 0.1, 0.7),  # SLAMGPU_POSE_MAX_EDGES
 ]
 
 
@@ -81,7 +83,8 @@ def test_pose_optimization_device_batch_matches_oracle(oracle, gpu_lib):
 
     rng = np.random.default_rng(42)
     # >= 64 frames: the batched one-wave-per-frame kernel (the host call covers the 8-wave one)
-    sizes = [2000] * 48 + [0, 2, 9, 10, 500, 4096, 3000, 1] + list(rng.integers(20, 2500, 16))
+    sizes = ([2000] * 48 + [0, 2, 9, 10, 500, 4096, 3000, 1] + list(rng.integers(20, 2500, 16))
+             + [4097, 7000])  # the last two: the L2-edge launch behind the batched one
     probs = [S.pose_problem(100 + f, int(n), stereo_frac=float(rng.uniform(0, 1)),
                             outlier_frac=float(rng.uniform(0, 0.3)))
              for f, n in enumerate(sizes)]
