@@ -66,10 +66,11 @@ def measured_valu(kernel, batch):
         return None, None
     if d.get("batch") != batch:
         return None, None
-    for k, v in d.get("kernels", {}).items():
-        if _symbol_matches(k, kernel):
-            return v.get("sq_insts_valu_per_dispatch"), d.get("valu_issue_peak_per_s")
-    return None, None
+    # several instantiations may match (orient_desc_kernel<4> serves the single-frame call): the
+    # batch launches are the largest
+    vals = [v.get("sq_insts_valu_per_dispatch") or 0 for k, v in d.get("kernels", {}).items()
+            if _symbol_matches(k, kernel)]
+    return (max(vals), d.get("valu_issue_peak_per_s")) if vals else (None, None)
 
 
 def measured_traffic(kernel, batch):
@@ -83,10 +84,9 @@ def measured_traffic(kernel, batch):
         return None, None
     if d.get("batch") != batch:
         return None, None
-    for k, v in d.get("kernels", {}).items():
-        if _symbol_matches(k, kernel):
-            return v.get("hbm_bytes_per_dispatch"), d.get("source")
-    return None, None
+    vals = [v.get("hbm_bytes_per_dispatch") or 0 for k, v in d.get("kernels", {}).items()
+            if _symbol_matches(k, kernel)]  # the batch instantiation: the largest
+    return (max(vals), d.get("source")) if vals else (None, None)
 
 
 def path_bytes_per_frame(level_px, kp_per_image):
@@ -250,9 +250,12 @@ def main():
     # ---- timed region
     launches_per_step = max(1, brk[dominant][1])
     ctx.timing_start(dominant, launches_per_step * args.steps + 16)
+    bench_stream = torch.cuda.current_stream(dev).cuda_stream
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
+    G.trace_marker(1, bench_stream)  # brackets the timed launches in a rocprofv3 kernel trace
+    torch.cuda.synchronize()        # (tools/stats_timed.py); outside the timed interval
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
@@ -262,6 +265,7 @@ def main():
     if world > 1:
         dist.barrier()
     t1 = time.perf_counter()
+    G.trace_marker(2, bench_stream)
     ctx.timing_stop()
     job.sync()
     elapsed = SD.max_over_ranks(t1 - t0, dev)

@@ -266,6 +266,12 @@ int slamgpu_timing_start(slamgpu_ctx* ctx, const char* kernel, int max_launches)
 int slamgpu_timing_stop(slamgpu_ctx* ctx, void* stream);
 int slamgpu_timing_read(slamgpu_ctx* ctx, const char* kernel, double* total_ms, int* launches);
 
+/* Launches one empty kernel, `trace_marker_kernel`, with a 1 x `id` grid on `stream` (NULL =
+ * the default stream): a mark a profiler's kernel trace shows in launch order. bench.py brackets
+ * its timed region with ids 1 and 2 so that tools/stats_timed.py can average exactly the launches
+ * the bench line's roofline times. */
+int slamgpu_trace_marker(int id, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -42,6 +42,9 @@ struct StereoOut {
 // Stereo frame 0 of ext (images 0 / 1) packed in the host mirror's layout (runtime.cpp
 // ResMirror: [nkps x2][err][pad] | kps 2 x kp_cap | desc 2 x kp_cap | u_right kp_cap | depth
 // kp_cap) at dst, valid entries only: one DMA then brings the frame's results to the host.
+// An empty kernel with a 1 x id grid: a mark in a profiler's kernel trace (slamgpu_trace_marker).
+void launch_trace_marker(int id, hipStream_t st);
+
 void launch_frame_pack(const FrameKps& ext, const float* u_right, const float* depth,
                        const uint32_t* err, int kp_cap, uint8_t* dst, hipStream_t st);
 void launch_stereo(const ImageBatch& b, const OrbGeomDev& g, const Camera& cam, int n_frames,

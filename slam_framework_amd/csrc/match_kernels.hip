@@ -465,6 +465,12 @@ void launch_frame_pack(const FrameKps& ext, const float* u_right, const float* d
                  depth, err, kp_cap, dst);
 }
 
+__global__ void trace_marker_kernel() {}
+
+void launch_trace_marker(int id, hipStream_t st) {
+  hipLaunchKernelGGL(trace_marker_kernel, dim3(1, id), dim3(64), 0, st);
+}
+
 void launch_stereo(const ImageBatch& b, const OrbGeomDev& gd, const Camera& cam, int n_frames,
                    const StereoWorkspace& ws, const StereoOut& out, hipStream_t st) {
   const OrbGeom& g = *gd.host;

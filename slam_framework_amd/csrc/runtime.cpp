@@ -856,6 +856,12 @@ int slamgpu_timing_read(slamgpu_ctx* c, const char* kernel, double* total_ms, in
   return 0;
 }
 
+int slamgpu_trace_marker(int id, void* stream) {
+  if (id < 1) return SLAMGPU_EINVAL;
+  launch_trace_marker(id, static_cast<hipStream_t>(stream));
+  return hipGetLastError() == hipSuccess ? 0 : SLAMGPU_EHIP;
+}
+
 int slamgpu_descriptor_distance(const uint8_t* a, const uint8_t* b) {
   int dist = 0;
   for (int i = 0; i < 32; i++) dist += __builtin_popcount((unsigned)(a[i] ^ b[i]));

@@ -58,6 +58,7 @@ EXPORTS = [
     "slamgpu_search_by_projection_mps", "slamgpu_search_by_projection_frame_device",
     "slamgpu_search_by_projection_mps_device", "slamgpu_debug_level_keys",
     "slamgpu_make_vo_queries_device", "slamgpu_timing_start", "slamgpu_timing_stop",
+    "slamgpu_trace_marker",
     "slamgpu_timing_read", "slamgpu_pose_optimization", "slamgpu_pose_optimization_device",
     "slamgpu_optimizer_last_error", "slamgpu_local_bundle_adjustment",
     "slamgpu_local_bundle_adjustment_device", "slamgpu_local_ba_workspace_bytes",
@@ -169,6 +170,8 @@ def lib():
         L.slamgpu_make_vo_queries_device.argtypes = [vp, vp, ip, vp, vp, vp, ip, vp]
         L.slamgpu_timing_start.argtypes = [vp, C.c_char_p, ip]
         L.slamgpu_timing_stop.argtypes = [vp, vp]
+        if hasattr(L, "slamgpu_trace_marker"):  # absent from older A/B builds (tools/abl)
+            L.slamgpu_trace_marker.argtypes = [ip, vp]
         L.slamgpu_timing_read.argtypes = [vp, C.c_char_p, C.POINTER(C.c_double), C.POINTER(ip)]
         L.slamgpu_pose_optimization.argtypes = [C.POINTER(Camera), vp, ip, vp, ip, vp, vp,
                                                 C.POINTER(ip)]
@@ -211,6 +214,14 @@ def lib():
         L.slamgpu_optimizer_last_error.restype = C.c_char_p
         _lib = L
     return _lib
+
+
+def trace_marker(mark_id, stream=None):
+    """slamgpu_trace_marker: an empty kernel with a 1 x mark_id grid on `stream` (a mark in a
+    profiler's kernel trace; bench.py brackets its timed region with ids 1 and 2)."""
+    rc = lib().slamgpu_trace_marker(int(mark_id), C.c_void_p(stream or 0))
+    if rc != 0:
+        raise SlamGpuError(f"slamgpu_trace_marker: error {rc}")
 
 
 def _ptr(a):
