@@ -835,6 +835,20 @@ __device__ void factor_solve_profile(CoopShared& sh, const CoopWs& w, int K, dou
     sh.ok = 1;
     cnt[0] = 0;
   }
+#if FS_PROF  // diagnostic build: thread 0's split of the factorisation into prof[8..13], active
+             // block rows per column: sum in prof[14], max in prof[15]
+  uint64_t fs_t = __builtin_amdgcn_s_memrealtime();
+  auto fs_tick = [&](int slot) {
+    if (w.prof && tid == 0) {
+      const uint64_t t = __builtin_amdgcn_s_memrealtime();
+      w.prof[slot] += 0.01 * (double)(t - fs_t);
+      fs_t = t;
+    }
+  };
+  if (w.prof && tid == 0) w.prof[13] += 1.0;
+#else
+  auto fs_tick = [](int) {};
+#endif
   auto diag_factor = [&](int J) {  // as in factor_solve, on the profile rows
     if (lane != 0) return;
     const int j0 = 6 * J;
@@ -886,6 +900,12 @@ __device__ void factor_solve_profile(CoopShared& sh, const CoopWs& w, int K, dou
     const int* act = lists + (J & 1) * K;
     int* nxt = lists + ((J + 1) & 1) * K;
     const int na = cnt[J & 1], nr = 6 * na;
+#if FS_PROF
+    if (w.prof && tid == 0) {
+      w.prof[14] += (double)na;
+      w.prof[15] = fmax(w.prof[15], (double)na);
+    }
+#endif
     {  // panel rows of the active blocks (forward solve fused)
       double Ljj[15], rdg[6], yj[6];
       int q = 0;
@@ -921,8 +941,10 @@ __device__ void factor_solve_profile(CoopShared& sh, const CoopWs& w, int K, dou
         rhs[i] = r;
       }
     }
+    fs_tick(8);
     if (tid == 0) cnt[(J + 1) & 1] = 0;
     __syncthreads();
+    fs_tick(9);
     const bool next_active = J + 1 < K && pfirst[J + 1] <= J;
     if (wid == 0) {
       if (J + 1 < K) {  // block J + 1: its update by column J (when it is active), then its LDLT
@@ -978,53 +1000,59 @@ __device__ void factor_solve_profile(CoopShared& sh, const CoopWs& w, int K, dou
         }
       }
     }
+    fs_tick(10);
     for (int I = J + 2 + tid; I < K; I += kT)  // A_{J+1}
       if (pfirst[I] <= J + 1) nxt[atomicAdd(&cnt[(J + 1) & 1], 1)] = I;
     if (tid == 0)  // heartbeat for the work-groups waiting at the next grid barrier
       __hip_atomic_fetch_add(&w.ctl[CTL_BEAT], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __syncthreads();
+    fs_tick(11);
   }
-  if (wid == 0) {  // z = D^-1 y; L^T x = z from the last 6x6 block up, over each block's envelope
-    for (int i = lane; i < n; i += 64) rhs[i] /= dg[i];
-    for (int J = K - 1; J >= 0; J--) {
-      const int j0 = 6 * J;
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-      double x[6] = {0, 0, 0, 0, 0, 0};
-      if (lane == 0) {
-        double Lb[15];
+  // z = D^-1 y; L^T x = z from the last 6x6 block up: lane 0 solves the block (x to LDS), then the
+  // whole work-group applies it to the block's envelope (wave 0 alone: 10 ms per solve at 1500
+  // keyframes, profiles/r3n_gba_factor_split.log)
+  double* const xs = sh.rhs;  // 6 doubles (sh.rhs is unused on the profile path)
+  for (int i = tid; i < n; i += kT) rhs[i] /= dg[i];
+  __syncthreads();
+  for (int J = K - 1; J >= 0; J--) {
+    const int j0 = 6 * J;
+    if (tid == 0) {
+      double Lb[15], x[6];
 #pragma unroll
-        for (int c = 1; c < 6; c++)
+      for (int c = 1; c < 6; c++)
 #pragma unroll
-          for (int r = 0; r < c; r++) Lb[c * (c - 1) / 2 + r] = Lp[prow[j0 + c] + j0 + r];
+        for (int r = 0; r < c; r++) Lb[c * (c - 1) / 2 + r] = Lp[prow[j0 + c] + j0 + r];
 #pragma unroll
-        for (int r = 0; r < 6; r++) x[r] = rhs[j0 + r];
+      for (int r = 0; r < 6; r++) x[r] = rhs[j0 + r];
 #pragma unroll
-        for (int c = 5; c >= 0; c--)
+      for (int c = 5; c >= 0; c--)
 #pragma unroll
-          for (int r = 0; r < c; r++) x[r] -= Lb[c * (c - 1) / 2 + r] * x[c];
+        for (int r = 0; r < c; r++) x[r] -= Lb[c * (c - 1) / 2 + r] * x[c];
 #pragma unroll
-        for (int r = 0; r < 6; r++) rhs[j0 + r] = x[r];
-      }
-#pragma unroll
-      for (int c = 0; c < 6; c++) x[c] = rl64(x[c], 0);
-      int64_t rb[6];
-#pragma unroll
-      for (int c = 0; c < 6; c++) rb[c] = prow[j0 + c];
-      for (int i = 6 * pfirst[J] + lane; i < j0; i += 64) {
-        double sx = rhs[i];
-#pragma unroll
-        for (int c = 0; c < 6; c++) sx -= Lp[rb[c] + i] * x[c];
-        rhs[i] = sx;
+      for (int r = 0; r < 6; r++) {
+        rhs[j0 + r] = x[r];
+        xs[r] = x[r];
       }
     }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-    for (int i = lane; i < n; i += 64) w.xp[i] = rhs[i];
+    __syncthreads();
+    double x[6];
+    int64_t rb[6];
+#pragma unroll
+    for (int c = 0; c < 6; c++) {
+      x[c] = xs[c];
+      rb[c] = prow[j0 + c];
+    }
+    for (int i = 6 * pfirst[J] + tid; i < j0; i += kT) {
+      double sx = rhs[i];
+#pragma unroll
+      for (int c = 0; c < 6; c++) sx -= Lp[rb[c] + i] * x[c];
+      rhs[i] = sx;
+    }
+    __syncthreads();
   }
+  for (int i = tid; i < n; i += kT) w.xp[i] = rhs[i];
   __syncthreads();
+  fs_tick(12);
 }
 
 // optimizer.cpp:632-665 between the two optimize() calls: chi2 > threshold or depth <= 0 ->

@@ -490,8 +490,9 @@ int coop_host(const char* what, const slamgpu_camera* cam, const float* inv_sigm
             pr[2], pr[5], pr[6], pr[3], pr[4], pr[7], G, K);
     if (pr[13] > 0)  // FS_PROF diagnostic build of ba_coop.hip
       fprintf(stderr, "[%s] factor split us: panel %.0f bar1 %.0f wave0-diag %.0f bar2 %.0f "
-              "solve %.0f (%.0f factorisations)\n", what, pr[8], pr[9], pr[10], pr[11], pr[12],
-              pr[13]);
+              "solve %.0f (%.0f factorisations; active block rows per column: mean %.1f, "
+              "max %.0f)\n", what, pr[8], pr[9], pr[10], pr[11], pr[12], pr[13],
+              pr[14] / std::max(1.0, pr[13] * (K > 0 ? K : 1)), pr[15]);
   }
   return 0;
 }
