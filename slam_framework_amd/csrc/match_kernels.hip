@@ -24,6 +24,9 @@ namespace slamgpu {
 #ifndef MATCH_XCD
 #define MATCH_XCD 1
 #endif
+#ifndef STEREO_LANES  // lanes per left keypoint in stereo_match (32: two per wave, 16: four)
+#define STEREO_LANES 16
+#endif
 
 constexpr int TH_HIGH = 100, TH_LOW = 50, HISTO_LENGTH = 30;
 constexpr uint64_t kNoKey = ~0ull;
@@ -154,30 +157,34 @@ __global__ __launch_bounds__(256) void stereo_rows_kernel(const OrbGeom* __restr
   }
 }
 
-// One left keypoint per half-wave (32 lanes), two per wave: the kernel is a chain of dependent
-// loads per keypoint (row table -> candidates -> descriptors -> SAD windows), so two independent
-// chains per wave hide twice the latency at the same occupancy.
-__device__ __forceinline__ uint32_t half_min(uint32_t v) {
+// One left keypoint per G lanes (G = 32: two per wave; G = 16: four): the kernel is a chain of
+// dependent loads per keypoint (row table -> candidates -> descriptors -> SAD windows), so several
+// independent chains per wave hide the latency at the same occupancy.
+template <int G>
+__device__ __forceinline__ uint32_t group_min(uint32_t v) {
 #pragma unroll
-  for (int off = 16; off >= 1; off >>= 1) {
+  for (int off = G / 2; off >= 1; off >>= 1) {
     const uint32_t o = __shfl_xor(v, off, 64);
     v = o < v ? o : v;
   }
   return v;
 }
 
+template <int G>
 __global__ __launch_bounds__(256) void stereo_match_kernel(ImageBatch b,
                                                            const OrbGeom* __restrict__ g,
                                                            FrameKps ext, Camera cam, int nrows,
                                                            StereoWorkspace ws, StereoOut out) {
+  constexpr int NPW = 64 / G;  // keypoints per wave
+  constexpr int kRounds = (121 + G - 1) / G;
 #if MATCH_XCD
   int f, bx;
   xcd_image_block(&f, &bx);  // a frame's work-groups share one XCD's L2 (its right keypoints)
 #else
   const int f = blockIdx.y, bx = blockIdx.x;
 #endif
-  const int lane = threadIdx.x & 63, half = lane >> 5, hl = lane & 31;
-  const int iL = (bx * 4 + wave_id()) * 2 + half;
+  const int lane = threadIdx.x & 63, grp = lane / G, hl = lane % G;
+  const int iL = (bx * 4 + wave_id()) * NPW + grp;
   const int il = 2 * f, ir = 2 * f + 1;
   const int nl = ext.n[il * ext.n_stride];
   const int64_t o = (int64_t)f * g->kp_cap + iL;
@@ -210,7 +217,7 @@ __global__ __launch_bounds__(256) void stereo_match_kernel(ImageBatch b,
   const uint8_t* dRb = ext.desc + ir * ext.stride * 32;
   uint32_t best = ((uint32_t)TH_HIGH << 16) | 0xffffu;
   if (ok) {
-    for (int c = c0 + hl; c < c1; c += 32) {
+    for (int c = c0 + hl; c < c1; c += G) {
       const int iR = items[c];
       const KeyPoint kpR = kr[iR];
       if (kpR.octave < levelL - 1 || kpR.octave > levelL + 1) continue;
@@ -222,7 +229,7 @@ __global__ __launch_bounds__(256) void stereo_match_kernel(ImageBatch b,
       }
     }
   }
-  best = half_min(best);
+  best = group_min<G>(best);
   const int bestDist = (int)(best >> 16);
   const int thOrbDist = (TH_HIGH + TH_LOW) / 2;
   ok = ok && bestDist < thOrbDist;
@@ -241,16 +248,16 @@ __global__ __launch_bounds__(256) void stereo_match_kernel(ImageBatch b,
   const int yc = (int)scaledvL, xcl = (int)scaleduL, xcr = (int)scaleduR0;
   // windows the reference would reject with a cv::Mat ROI assertion are treated as no match
   ok = ok && !(yc - w < 0 || yc + w >= LG.h || xcl - w < 0 || xcl + w >= LG.w || xcr - L - w < 0);
-  // SAD of the 11 window offsets: the 121 (offset, row) pairs over the half-wave (four rounds),
+  // SAD of the 11 window offsets: the 121 (offset, row) pairs over the group (kRounds rounds),
   // each lane summing one 11-pixel row; rows are then summed per offset through LDS. The window
   // bytes (left: columns xcl-5..xcl+5, right: xcr-10..xcr+10, rows yc-5..yc+5) are first staged
   // into LDS with dword loads (11 dwords per row: 4 left + 7 right); dwords past a row's last byte
   // are clamped to it (their bytes are never used). Caller images with an odd base or pitch take
   // byte loads instead.
-  __shared__ int s_part[4][2][128];
-  __shared__ uint32_t s_win[4][2][11][11];
-  int* part = s_part[wave_id()][half];
-  uint32_t(*win)[11] = s_win[wave_id()][half];
+  __shared__ int s_part[4][NPW][128];
+  __shared__ uint32_t s_win[4][NPW][11][11];
+  int* part = s_part[wave_id()][grp];
+  uint32_t(*win)[11] = s_win[wave_id()][grp];
   int pl = 0, pr = 0;
   const uint8_t* IL = nullptr;
   const uint8_t* IR = nullptr;
@@ -263,8 +270,8 @@ __global__ __launch_bounds__(256) void stereo_match_kernel(ImageBatch b,
   const int lastw = (LG.w - 1) >> 2;
   if (ok) {
 #pragma unroll
-    for (int rnd = 0; rnd < 4; rnd++) {
-      const int p = hl + 32 * rnd;
+    for (int rnd = 0; rnd < kRounds; rnd++) {
+      const int p = hl + G * rnd;
       if (p < 121) {
         const int r = p / 11, d = p - 11 * r;  // window row, dword slot (0-3 left, 4-10 right)
         const bool left = d < 4;
@@ -289,8 +296,8 @@ __global__ __launch_bounds__(256) void stereo_match_kernel(ImageBatch b,
   const uint8_t* wb = reinterpret_cast<const uint8_t*>(&win[0][0]);  // row r at 44 r
   if (ok) {
 #pragma unroll
-    for (int rnd = 0; rnd < 4; rnd++) {
-      const int p = hl + 32 * rnd;
+    for (int rnd = 0; rnd < kRounds; rnd++) {
+      const int p = hl + G * rnd;
       if (p < 121) {
         const int k = p / 11, yy = p - 11 * k - w;
         const int incR = k - L;
@@ -316,7 +323,7 @@ __global__ __launch_bounds__(256) void stereo_match_kernel(ImageBatch b,
   }
   float vDists[11];
 #pragma unroll
-  for (int k = 0; k < 11; k++) vDists[k] = (float)__shfl(sad, 32 * half + k, 64);
+  for (int k = 0; k < 11; k++) vDists[k] = (float)__shfl(sad, G * grp + k, 64);
   if (!ok || hl != 0) return;
   int bestSad = 0x7fffffff, bestincR = 0;
 #pragma unroll
@@ -478,8 +485,10 @@ void launch_stereo(const ImageBatch& b, const OrbGeomDev& gd, const Camera& cam,
   const int nrows = g.lv[0].h;
   SLAMGPU_LAUNCH("stereo_rows", st, stereo_rows_kernel, dim3(n_frames), dim3(256), 0, st, gd.dev, ext, nrows,
                      ws, gd.ws.err);
-  SLAMGPU_LAUNCH("stereo_match", st, stereo_match_kernel, dim3((g.kp_cap + 7) / 8, n_frames), dim3(256), 0, st,
-                     b, gd.dev, ext, cam, nrows, ws, out);
+  constexpr int kG = STEREO_LANES, kPerBlock = 4 * (64 / kG);
+  SLAMGPU_LAUNCH("stereo_match", st, stereo_match_kernel<kG>,
+                 dim3((g.kp_cap + kPerBlock - 1) / kPerBlock, n_frames), dim3(256), 0, st, b,
+                 gd.dev, ext, cam, nrows, ws, out);
   SLAMGPU_LAUNCH("stereo_median", st, stereo_median_kernel, dim3(n_frames), dim3(256), 0, st, gd.dev, ext, ws,
                      out);
 }
