@@ -289,4 +289,76 @@ void build_cells(const OrbGeom& g, std::vector<CellDesc>* cells) {
   }
 }
 
+void build_pyr_columns(OrbGeom* g, const std::vector<ResizeX>& rx, std::vector<uint32_t>* pc) {
+  pc->clear();
+  for (int l = 1; l < g->nlevels; l++) {
+    LevelGeom& L = g->lv[l];
+    L.pc_base = (int)(pc->size() / 4);
+    for (int x0 = 0; x0 < L.w; x0 += 4) {
+      const int s0 = rx[L.rx_base + x0].sx;  // < 4096 (cols <= 4095)
+      for (int k = 0; k < 4; k++) {
+        const int dx = std::min(x0 + k, L.w - 1);
+        const ResizeX& e = rx[L.rx_base + dx];
+        // the 8-byte window check of compute_geometry bounds sx_k - sx_0 by 6
+        const uint32_t bk = (uint32_t)std::min(e.sx - s0, 6);
+        pc->push_back((uint32_t)e.a0 | (uint32_t)e.a1 << 12 | bk << 24 |
+                      (uint32_t)(dx >= L.xmax) << 27 | (uint32_t)((s0 >> (4 * k)) & 15) << 28);
+      }
+    }
+  }
+}
+
+void build_pyr_bands(const OrbGeom& g, const std::vector<ResizeY>& ry, int nb,
+                     std::vector<PyrBand>* bands, int max_rows[kMaxLevels]) {
+  bands->assign((size_t)nb * kMaxLevels, PyrBand{0, -1, 0, -1});
+  for (int l = 0; l < kMaxLevels; l++) max_rows[l] = 0;
+  const int L = g.nlevels;
+  // Band boundaries: level 1 split evenly; on level l >= 2 a band starts at the first row whose
+  // upper source row (y0) lies at or below the band's start on level l - 1. A band's rows then
+  // never read above its own lower-level rows -- the halo is only at the bottom, about one row
+  // per level (a proportional split of every level would add a halo at the top as well).
+  std::vector<int> bnd((size_t)(nb + 1) * kMaxLevels, 0);
+  auto B = [&](int k, int l) -> int& { return bnd[(size_t)k * kMaxLevels + l]; };
+  for (int k = 0; k <= nb; k++) B(k, 1) = (int)((int64_t)k * g.lv[1].h / nb);
+  for (int l = 2; l < L; l++) {
+    const int h = g.lv[l].h;
+    int d = 0;
+    for (int k = 0; k <= nb; k++) {
+      if (k == nb) { B(k, l) = h; break; }
+      while (d < h && std::min(ry[g.lv[l].ry_base + d].y0, ry[g.lv[l].ry_base + d].y1) < B(k, l - 1))
+        d++;
+      B(k, l) = d;
+    }
+  }
+  for (int k = 0; k < nb; k++) {
+    PyrBand* bt = bands->data() + (size_t)k * kMaxLevels;
+    for (int l = 1; l < L; l++) {
+      bt[l].own_lo = B(k, l);
+      bt[l].own_hi = B(k + 1, l) - 1;
+    }
+    if (L > 1) {
+      bt[L - 1].need_lo = bt[L - 1].own_lo;
+      bt[L - 1].need_hi = bt[L - 1].own_hi;
+    }
+    for (int l = L - 1; l >= 1; l--) {
+      // the level l - 1 rows that level l's need range resizes from (HResize rows y0, y1)
+      int lo = 1 << 30, hi = -1;
+      for (int d = bt[l].need_lo; d <= bt[l].need_hi; d++) {
+        const ResizeY& e = ry[g.lv[l].ry_base + d];
+        lo = std::min(lo, std::min(e.y0, e.y1));
+        hi = std::max(hi, std::max(e.y0, e.y1));
+      }
+      if (l - 1 >= 1 && bt[l - 1].own_lo <= bt[l - 1].own_hi) {
+        lo = std::min(lo, bt[l - 1].own_lo);
+        hi = std::max(hi, bt[l - 1].own_hi);
+      }
+      if (hi < lo) { lo = 0; hi = -1; }
+      bt[l - 1].need_lo = lo;
+      bt[l - 1].need_hi = hi;
+    }
+    for (int l = 0; l < L; l++)
+      max_rows[l] = std::max(max_rows[l], bt[l].need_hi - bt[l].need_lo + 1);
+  }
+}
+
 }  // namespace slamgpu

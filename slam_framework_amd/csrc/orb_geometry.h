@@ -59,6 +59,7 @@ struct LevelGeom {
   // resize tables (level >= 1) in the shared table buffer
   int rx_base, ry_base; // offsets into the x (per dst column) / y (per dst row) tables
   int xmax;             // first dst column that copies S[sx] * 2048 (resize HResizeLinear)
+  int pc_base;          // pyr_band_kernel: first packed 4-column group of this level (>= 1)
   float scale, inv_scale;
   float patch_size;     // (float)(int)(PATCH_SIZE * scale) (:778)
 };
@@ -92,6 +93,12 @@ struct OrbGeom {
 // Resize tables (HResizeLinear / VResizeLinear coefficients, 11-bit fixed point).
 struct ResizeX { int32_t sx; int16_t a0, a1; };
 struct ResizeY { int32_t y0, y1; int16_t b0, b1; };
+
+// Fused pyramid (pyr_band_kernel): band k of level l >= 1 owns (writes) rows [own_lo, own_hi]
+// and computes [need_lo, need_hi] -- its own rows plus the rows its higher-level rows resize
+// from. Level 0 has only the need range (the caller's rows the band reads). Inclusive; an empty
+// range has lo > hi.
+struct PyrBand { int need_lo, need_hi, own_lo, own_hi; };
 
 // One FAST survivor / octree key: x_rel (12 b) | y_rel (11 b) << 12 | score (8 b) << 23,
 // coordinates relative to (minBorderX, minBorderY).

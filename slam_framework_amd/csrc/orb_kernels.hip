@@ -185,6 +185,155 @@ __global__ __launch_bounds__(256) void pyr_down_kernel(ImageBatch b, const OrbGe
 }
 
 // ---------------------------------------------------------------------------------------
+// pyr_band: the whole pyramid (ComputePyramid :1051-1075, each level resized from the one before
+// it) of one row band of one image in one work-group, the intermediate levels held in LDS.
+// Band k owns rows [k*h_l/nb, (k+1)*h_l/nb) of every level l >= 1 and also computes the rows of
+// lower levels its higher-level rows resize from (PyrBand need ranges, build_pyr_bands), so no
+// level is read back from memory: HBM sees the caller's level-0 rows once (plus the few halo rows
+// neighbouring bands share, L2 hits on the same XCD) and every level's rows written once --
+// instead of pyr_down_kernel's one launch per level re-reading level l-1. The per-pixel arithmetic
+// is pyr_down_kernel's (bit-identical output).
+// A work item is one 4-column group x kPyrBandRows dst rows: the source rows' horizontal pass
+// (3 LDS dwords, two alignbytes, v_perm + v_dot2 per column) is computed once per item and row,
+// cached in two slots for the vertical pass.
+// kCopy: how the band's level-0 rows reach LDS. 0: they are one contiguous byte range (row stride
+// = the caller's 16-byte-aligned pitch), copied by global_load_lds_dwordx4 with no VGPR staging;
+// 1: dword copy (4-byte aligned caller images); 2: byte copy. 1 and 2 use rows of stride0 bytes.
+constexpr int kPyrBandThreads = 256;
+#ifndef PYR_BAND_ROWS
+#define PYR_BAND_ROWS 8
+#endif
+constexpr int kPyrBandRows = PYR_BAND_ROWS;
+
+template <int kCopy>
+__global__ __launch_bounds__(kPyrBandThreads) void pyr_band_kernel(
+    ImageBatch b, const OrbGeom* __restrict__ g, const uint4* __restrict__ pcol,
+    const ResizeY* __restrict__ ryt, const PyrBand* __restrict__ bands, int half1, int stride0) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t s_pyr[];
+  int img, band;
+  xcd_image_block(&img, &band);
+  const int tid = threadIdx.x;
+  const PyrBand* bt = bands + band * kMaxLevels;
+  const int n0lo = bt[0].need_lo, n0hi = bt[0].need_hi;
+  if (n0hi < n0lo) return;  // work-group-uniform: a band with no rows at any level
+  const int nlev = g->nlevels;
+  const int pitch = b.in_pitch;
+  const uint8_t* src0 = batch_image(b, img) + (int64_t)n0lo * pitch;
+  const int rows0 = n0hi - n0lo + 1;
+  if constexpr (kCopy == 0) {
+    const int lane = tid & 63, wid = wave_id();
+    const int nbytes = rows0 * pitch;  // a multiple of 16
+    for (int blk = wid; blk * 1024 < nbytes; blk += kPyrBandThreads / 64) {
+      const int off = blk * 1024 + 16 * lane;
+      if (off < nbytes)
+        __builtin_amdgcn_global_load_lds(
+            (const __attribute__((address_space(1))) void*)(src0 + off),
+            (__attribute__((address_space(3))) void*)(s_pyr + blk * 1024), 16, 0, 0);
+    }
+    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): this wave's rows have landed
+  } else {
+    const int w0 = g->lv[0].w;
+    if constexpr (kCopy == 1) {
+      const int nq = (w0 + 3) >> 2;
+      for (int i = tid; i < rows0 * nq; i += kPyrBandThreads) {
+        const int r = i / nq, q = i - r * nq;
+        *reinterpret_cast<uint32_t*>(s_pyr + r * stride0 + 4 * q) =
+            *reinterpret_cast<const uint32_t*>(src0 + (int64_t)r * pitch + 4 * q);
+      }
+    } else {
+      for (int i = tid; i < rows0 * w0; i += kPyrBandThreads) {
+        const int r = i / w0, x = i - r * w0;
+        s_pyr[r * stride0 + x] = src0[(int64_t)r * pitch + x];
+      }
+    }
+  }
+  __syncthreads();
+  uint8_t* const pyr = b.pyr + (int64_t)img * g->pyr_bytes;
+  for (int l = 1; l < nlev; l++) {
+    const PyrBand nd = bt[l];
+    const int sbase = bt[l - 1].need_lo;
+    if (nd.need_hi >= nd.need_lo) {  // work-group-uniform
+      const LevelGeom& D = g->lv[l];
+      const int sw = g->lv[l - 1].w;
+      const uint8_t* sbuf = s_pyr + (((l - 1) & 1) ? half1 : 0);
+      uint8_t* dbuf = s_pyr + ((l & 1) ? half1 : 0);
+      const int ss = l == 1 ? stride0 : ((sw + 15) & ~15);
+      const int ds = (D.w + 15) & ~15;
+      const int ncg = (D.w + 3) >> 2;
+      const int nch = (nd.need_hi - nd.need_lo + kPyrBandRows) / kPyrBandRows;
+      const int qmax = (sw - 1) >> 2;
+      uint8_t* const gdst = pyr + D.offset;
+      const int dpitch = D.pitch, dw = D.w, ryb = D.ry_base, pcb = D.pc_base;
+      for (int it = tid; it < ncg * nch; it += kPyrBandThreads) {
+        const int ch = it / ncg, cg = it - ch * ncg;
+        const int x0 = 4 * cg;
+        const int d0 = nd.need_lo + ch * kPyrBandRows;
+        const int d1 = min(d0 + kPyrBandRows, nd.need_hi + 1);
+        const uint4 pc = pcol[pcb + cg];
+        const uint32_t pw[4] = {pc.x, pc.y, pc.z, pc.w};
+        const int s0 = (int)((pc.x >> 28) | (pc.y >> 28) << 4 | (pc.z >> 28) << 8 |
+                             (pc.w >> 28) << 12);
+        uint32_t sel[4], A[4];
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+          const uint32_t bk = (pw[k] >> 24) & 7u;
+          sel[k] = bk | 0x0c00u | (bk + 1) << 16 | 0x0c000000u;  // bytes bk, bk+1 -> u16 lanes
+          A[k] = ((pw[k] >> 27) & 1u) ? 32768u
+                                      : (16u * (pw[k] & 0xfffu)) | (16u * ((pw[k] >> 12) & 0xfffu)) << 16;
+        }
+        const int q0 = s0 >> 2, sh = s0 & 3;
+        const int qa = min(q0, qmax), qb = min(q0 + 1, qmax), qc = min(q0 + 2, qmax);
+        auto hrow = [&](int sy, uint32_t(&h)[4]) {
+          const uint32_t* rw = reinterpret_cast<const uint32_t*>(sbuf + (sy - sbase) * ss);
+          const uint32_t v0 = rw[qa], v1 = rw[qb], v2 = rw[qc];
+          const uint32_t W0 = __builtin_amdgcn_alignbyte(v1, v0, sh);
+          const uint32_t W1 = __builtin_amdgcn_alignbyte(v2, v1, sh);
+#pragma unroll
+          for (int k = 0; k < 4; k++) h[k] = dot2u(__builtin_amdgcn_perm(W1, W0, sel[k]), A[k], 0u);
+        };
+        int ra = -1, rb = -1;  // source rows held in ha / hb
+        uint32_t ha[4] = {0, 0, 0, 0}, hb[4] = {0, 0, 0, 0};
+        for (int d = d0; d < d1; d++) {
+          const ResizeY e = ryt[ryb + d];
+          if (e.y1 != rb) {
+            if (e.y0 == rb) {
+#pragma unroll
+              for (int k = 0; k < 4; k++) ha[k] = hb[k];
+              ra = rb;
+            }
+            hrow(e.y1, hb);
+            rb = e.y1;
+          }
+          if (e.y0 != rb && e.y0 != ra) {
+            hrow(e.y0, ha);
+            ra = e.y0;
+          }
+          const bool same = e.y0 == rb;
+          const uint32_t b0 = (uint32_t)(uint16_t)e.b0 << 8, b1 = (uint32_t)(uint16_t)e.b1 << 8;
+          uint32_t packed = 0;
+#pragma unroll
+          for (int k = 0; k < 4; k++) {
+            const uint32_t r0 = (same ? hb[k] : ha[k]) & ~0xffu, r1 = hb[k] & ~0xffu;
+            const uint32_t v = (mulhi24(b0, r0) + mulhi24(b1, r1) + 2) >> 2;
+            packed |= (v & 0xffu) << (8 * k);
+          }
+          *reinterpret_cast<uint32_t*>(dbuf + (d - nd.need_lo) * ds + x0) = packed;
+          if (d >= nd.own_lo && d <= nd.own_hi) {
+            uint8_t* drow = gdst + (int64_t)d * dpitch;
+            if (x0 + 4 <= dw) {
+              *reinterpret_cast<uint32_t*>(drow + x0) = packed;  // pitch is a multiple of 64
+            } else {
+              for (int k = 0; x0 + k < dw; k++) drow[x0 + k] = (uint8_t)(packed >> (8 * k));
+            }
+          }
+        }
+      }
+    }
+    __syncthreads();
+  }
+}
+
+// ---------------------------------------------------------------------------------------
 __device__ __forceinline__ int reflect101(int i, int n) {  // cv::BORDER_REFLECT_101, |overshoot| < n
   if (i < 0) i = -i;
   if (i >= n) i = 2 * n - 2 - i;
@@ -2743,7 +2892,42 @@ void launch_extract(const ImageBatch& b, const OrbGeomDev& gd, int n_images, hip
   const bool in_aligned = (((uintptr_t)b.in_l | (uintptr_t)b.in_r | (uintptr_t)b.in_stride |
                            (uintptr_t)b.in_pitch) & 3) == 0;
   const bool short_strips = n_images <= kPyrShortMaxImages;
-  for (int l = 1; l < g.nlevels; l++) {
+  // the fused band kernel (SLAMGPU_PYR_FUSED=0: one pyr_down launch per level, for A/B)
+  static const int fused_mode = [] {
+    const char* e = std::getenv("SLAMGPU_PYR_FUSED");
+    return e ? std::atoi(e) : 1;
+  }();
+  bool fused = false;
+  if (fused_mode && g.nlevels > 1) {
+    const PyrBandSet& bs = *(short_strips ? gd.bands_small : gd.bands_big);
+    auto r16 = [](int v) { return (v + 15) & ~15; };
+    const bool c16 = (((uintptr_t)b.in_l | (uintptr_t)b.in_r | (uintptr_t)b.in_stride |
+                       (uintptr_t)b.in_pitch) & 15) == 0;
+    const int w0r = r16(g.lv[0].w);
+    const int copy = (c16 && b.in_pitch <= 2 * w0r) ? 0 : (in_aligned ? 1 : 2);
+    const int stride0 = copy == 0 ? b.in_pitch : w0r;
+    size_t buf0 = (size_t)bs.max_rows[0] * stride0, buf1 = 0;
+    for (int l = 1; l < g.nlevels; l++) {
+      const size_t s = (size_t)bs.max_rows[l] * r16(g.lv[l].w);
+      if (l & 1) buf1 = std::max(buf1, s); else buf0 = std::max(buf0, s);
+    }
+    const int half1 = (int)((buf0 + 15) & ~(size_t)15);
+    const size_t lds = (size_t)half1 + buf1;
+    if (bs.dev && lds <= 160 * 1024) {
+      const dim3 grid(bs.nb, n_images);
+      if (copy == 0)
+        SLAMGPU_LAUNCH("pyr_down", st, pyr_band_kernel<0>, grid, dim3(kPyrBandThreads), lds, st,
+                       b, gd.dev, gd.pcol, gd.ry, bs.dev, half1, stride0);
+      else if (copy == 1)
+        SLAMGPU_LAUNCH("pyr_down", st, pyr_band_kernel<1>, grid, dim3(kPyrBandThreads), lds, st,
+                       b, gd.dev, gd.pcol, gd.ry, bs.dev, half1, stride0);
+      else
+        SLAMGPU_LAUNCH("pyr_down", st, pyr_band_kernel<2>, grid, dim3(kPyrBandThreads), lds, st,
+                       b, gd.dev, gd.pcol, gd.ry, bs.dev, half1, stride0);
+      fused = true;
+    }
+  }
+  for (int l = 1; l < g.nlevels && !fused; l++) {
     const int strip = short_strips ? kPyrShortStrip : kPyrStrip;
     const int tiles = ((g.lv[l].w + 255) >> 8) * ((g.lv[l].h + 4 * strip - 1) / (4 * strip));
     const dim3 grid(tiles, n_images);
