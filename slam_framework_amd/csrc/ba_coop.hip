@@ -813,6 +813,9 @@ __device__ __forceinline__ void factor_solve(CoopShared& sh, const CoopWs& w, in
   fs_tick(12);
 }
 
+__device__ void profile_back_solve(CoopShared& sh, const CoopWs& w, int K, double* Lp,
+                                   double* rhs, const double* dg);
+
 // The same LDLT for 6K > kCoopLdsN on the block-profile storage (w.prow / w.pfirst): row i holds
 // columns 6 pfirst[i / 6] .. i, and every fill-in stays inside that envelope, so block column J
 // only touches the active block rows A_J = {I > J : pfirst[I] <= J} -- a band of a few dozen
@@ -1008,9 +1011,19 @@ __device__ void factor_solve_profile(CoopShared& sh, const CoopWs& w, int K, dou
     __syncthreads();
     fs_tick(11);
   }
-  // z = D^-1 y; L^T x = z from the last 6x6 block up: lane 0 solves the block (x to LDS), then the
-  // whole work-group applies it to the block's envelope (wave 0 alone: 10 ms per solve at 1500
-  // keyframes, profiles/r3n_gba_factor_split.log)
+  profile_back_solve(sh, w, K, Lp, rhs, dg);
+  fs_tick(12);
+}
+
+// z = D^-1 y; L^T x = z from the last 6x6 block up: lane 0 solves the block (x to LDS), then the
+// whole work-group applies it to the block's envelope (wave 0 alone: 10 ms per solve at 1500
+// keyframes, profiles/r3n_gba_factor_split.log); the solution to w.xp.
+__device__ void profile_back_solve(CoopShared& sh, const CoopWs& w, int K, double* Lp,
+                                   double* rhs, const double* dg) {
+#pragma clang fp contract(fast)  // tolerance-compared FP64 path
+  const int tid = threadIdx.x, n = 6 * K;
+  const int64_t* prow = w.prow;
+  const int32_t* pfirst = w.pfirst;
   double* const xs = sh.rhs;  // 6 doubles (sh.rhs is unused on the profile path)
   for (int i = tid; i < n; i += kT) rhs[i] /= dg[i];
   __syncthreads();
@@ -1052,7 +1065,268 @@ __device__ void factor_solve_profile(CoopShared& sh, const CoopWs& w, int K, dou
   }
   for (int i = tid; i < n; i += kT) w.xp[i] = rhs[i];
   __syncthreads();
-  fs_tick(12);
+}
+
+// ---- the profile LDLT over the whole grid (6K > kCoopLdsN) ---------------------------------
+// Block row I of S (its rows of L, rhs, dg) belongs to work-group I % G for the whole
+// factorisation: its panel rows, its trailing updates and, for its diagonal block, the 6x6 LDLT are
+// all computed there, so L never crosses work-groups and needs no L2 write-back. Per block column
+// J two small hand-offs do, write-through (st_wt / ld_wt, as the reduction partials):
+//   * the owner of block J publishes L_JJ, D_J^-1, y_J and ok (28 doubles) and raises CTL_DFLAG
+//     to J + 1;
+//   * every work-group forms its active panel rows V = A_iJ L_JJ^-T, L_iJ = V D_J^-1 (rhs updated)
+//     and publishes V, then counts itself in at CTL_PCNT.
+// The owner of block J + 1 updates that block from its own V and factors it at once (look-ahead),
+// so column J + 1's hand-off leaves before the other work-groups finish column J; they wait for
+// all of column J's panels, stage the active V rows in LDS and update their own rows. Every element
+// sees the same operations in the same order as in factor_solve_profile (identical results). V and
+// the diagonal hand-off are double-buffered by column parity: a work-group runs at most one column
+// ahead of the slowest (it cannot pass column J + 1's panel count before everyone has finished
+// column J). Active block rows per column <= na_cap (the V rows fit the LDS; host-checked).
+constexpr int kPubStride = 32;  // doubles per published diagonal block (15 + 6 + 6 + ok)
+
+// Thread 0: spin until the word reaches target (relaxed device-scope loads, s_sleep back-off).
+// False once the grid has given up (CTL_ERR), or when nothing moved for ~2^22 sleeps (raised here).
+__device__ bool wait_word(const CoopWs& w, int idx, int32_t target) {
+  uint32_t spins = 0, polls = 0;
+  int32_t seen = -1;
+  for (;;) {
+    const int32_t v = __hip_atomic_load(&w.ctl[idx], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (v >= target) return true;
+    if (v != seen) {
+      seen = v;
+      spins = 0;
+    }
+    if (polls < 256) __builtin_amdgcn_s_sleep(1);
+    else __builtin_amdgcn_s_sleep(8);
+    polls++;
+    if ((++spins & 255u) == 0 && ctl_load(w, CTL_ERR)) return false;
+    if (spins > (1u << 22)) {
+      __hip_atomic_store(&w.ctl[CTL_ERR], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      return false;
+    }
+  }
+}
+
+// factor_profile_grid's LDS in sh.S: two A_J lists + 4 counters + the own-block positions (ints),
+// then (16-byte aligned) the published block, the active V rows and the own L_iJ rows (doubles).
+__device__ __forceinline__ int prof_lists_dw(int K) { return (12 * K + 16 + 15) / 16 * 2; }
+// Active blocks per column whose V rows (36 doubles) and, at most as many, own L_iJ rows fit.
+__device__ __forceinline__ int prof_na_cap(int K) {
+  const int avail = (int)(sizeof(CoopShared::S) / 8) - prof_lists_dw(K) - kPubStride;
+  return avail > 0 ? avail / 72 : 0;
+}
+
+// The 6x6 LDLT of diagonal block J (rows j0.. of the profile, already updated by every column
+// < J), its forward solve y, D^-1: one lane. Returns false on an exact zero pivot.
+__device__ bool diag_block(const CoopWs& w, int J, double* Lp, double* rhs, double* dg,
+                           double* idg) {
+#pragma clang fp contract(fast)  // tolerance-compared FP64 path
+  const int64_t* prow = w.prow;
+  const int j0 = 6 * J;
+  double A[21], y[6];
+#pragma unroll
+  for (int r = 0; r < 6; r++) {
+    y[r] = rhs[j0 + r];
+#pragma unroll
+    for (int k = 0; k <= r; k++) A[r * (r + 1) / 2 + k] = Lp[prow[j0 + r] + j0 + k];
+  }
+  bool good = true;
+#pragma unroll
+  for (int c = 0; c < 6; c++) {
+    const double d = A[c * (c + 3) / 2];
+    good = good && d != 0.0;
+    const double rd = d != 0.0 ? 1.0 / d : 0.0;
+    idg[j0 + c] = rd;
+    double l[6];
+#pragma unroll
+    for (int r = c + 1; r < 6; r++) {
+      l[r] = A[r * (r + 1) / 2 + c] * rd;
+      y[r] -= l[r] * y[c];
+      A[r * (r + 1) / 2 + c] = l[r];
+    }
+#pragma unroll
+    for (int r = c + 1; r < 6; r++) {
+      const double ld = l[r] * d;
+#pragma unroll
+      for (int k = c + 1; k <= r; k++) A[r * (r + 1) / 2 + k] -= ld * l[k];
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < 6; r++) {
+#pragma unroll
+    for (int k = 0; k < r; k++) Lp[prow[j0 + r] + j0 + k] = A[r * (r + 1) / 2 + k];
+    dg[j0 + r] = A[r * (r + 3) / 2];
+    rhs[j0 + r] = y[r];
+  }
+  return good;
+}
+
+// One lane of block J's owner: factor it, publish (L_JJ, D_J^-1, y_J, ok) into slot J & 1, and
+// raise CTL_DFLAG to J + 1 once the hand-off has landed.
+__device__ void diag_publish(const CoopWs& w, int J, double* Lp, double* rhs, double* dg,
+                             double* idg, double* pub) {
+  const bool good = diag_block(w, J, Lp, rhs, dg, idg);
+  const int64_t* prow = w.prow;
+  const int j0 = 6 * J;
+  double* const slot = pub + (J & 1) * kPubStride;
+  int q = 0;
+#pragma unroll
+  for (int c = 1; c < 6; c++)
+#pragma unroll
+    for (int k = 0; k < c; k++) st_wt(slot + q++, Lp[prow[j0 + c] + j0 + k]);
+#pragma unroll
+  for (int c = 0; c < 6; c++) {
+    st_wt(slot + 15 + c, idg[j0 + c]);
+    st_wt(slot + 21 + c, rhs[j0 + c]);
+  }
+  st_wt(slot + 27, good ? 1.0 : 0.0);
+  vm_drain();
+  __hip_atomic_store(&w.ctl[CTL_DFLAG], J + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Every work-group. Returns false (work-group-uniform, the same in every work-group) on a zero
+// pivot or when the grid gave up; CTL_DFLAG / CTL_PCNT must be 0 on entry (zeroed before the grid
+// barrier that precedes it).
+__device__ bool factor_profile_grid(CoopShared& sh, const CoopWs& w, int K, double* Lp,
+                                    double* rhs, double* dg, double* idg, double* Vg0,
+                                    double* Vg1, double* pub) {
+#pragma clang fp contract(fast)  // tolerance-compared FP64 path
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int G = gridDim.x, wg = blockIdx.x;
+  const int64_t* prow = w.prow;
+  const int32_t* pfirst = w.pfirst;
+  // LDS (the unused dense factor storage): A_J lists (two buffers) + counts, the own active
+  // blocks' list positions, column J's published block, the active V rows, the own L_iJ rows
+  int* const lists = reinterpret_cast<int*>(sh.S);
+  int* const cnt = lists + 2 * K;   // [0], [1]: list sizes; [2]: own count; [3]: ok
+  int* const own = cnt + 4;         // [K]
+  double* const pd = sh.S + prof_lists_dw(K);
+  double* const sV = pd + kPubStride;  // [36 * na] V rows of the active blocks, list order
+  // own L_iJ rows: after sV, sized by the caller's cap (6 * 6 per own block, <= na blocks)
+  const int na_cap = prof_na_cap(K);
+  double* const sL = sV + 36 * (size_t)na_cap;
+  if (tid == 0) cnt[0] = 0;
+  __syncthreads();
+  for (int I = 1 + tid; I < K; I += kT)  // A_0
+    if (pfirst[I] <= 0) lists[atomicAdd(&cnt[0], 1)] = I;
+  if (wg == 0 && tid == 0) diag_publish(w, 0, Lp, rhs, dg, idg, pub);
+  __syncthreads();
+  bool ok = true;
+  for (int J = 0; J < K; J++) {
+    const int j0 = 6 * J;
+    const int* act = lists + (J & 1) * K;
+    int* nxt = lists + ((J + 1) & 1) * K;
+    const int na = cnt[J & 1], nr = 6 * na;
+    double* const Vp = (J & 1) ? Vg1 : Vg0;
+    // ---- column J's diagonal block from its owner
+    if (tid == 0) {
+      cnt[2] = 0;
+      cnt[3] = wait_word(w, CTL_DFLAG, J + 1) ? 1 : 0;
+    }
+    __syncthreads();
+    if (!cnt[3]) {
+      ok = false;
+      break;
+    }
+    if (tid < 28) pd[tid] = ld_wt(pub + (J & 1) * kPubStride + tid);
+    for (int t = tid; t < na; t += kT)  // own active blocks (any order)
+      if (act[t] % G == wg) own[atomicAdd(&cnt[2], 1)] = t;
+    __syncthreads();
+    if (pd[27] == 0.0) {  // zero pivot: every work-group stops at this column
+      ok = false;
+      break;
+    }
+    const int no = cnt[2], nro = 6 * no;
+    // ---- panel rows of the own active blocks (forward solve fused); V published, L_iJ kept
+    {
+      double Ljj[15], rdg[6], yj[6];
+#pragma unroll
+      for (int q = 0; q < 15; q++) Ljj[q] = pd[q];
+#pragma unroll
+      for (int c = 0; c < 6; c++) {
+        rdg[c] = pd[15 + c];
+        yj[c] = pd[21 + c];
+      }
+      for (int t = tid; t < nro; t += kT) {
+        const int i = 6 * act[own[t / 6]] + t % 6;
+        const int64_t ro = prow[i] + j0;
+        double v[6];
+        int q = 0;
+#pragma unroll
+        for (int c = 0; c < 6; c++) {
+          double sv = Lp[ro + c];
+#pragma unroll
+          for (int k = 0; k < c; k++) sv -= v[k] * Ljj[q++];
+          v[c] = sv;
+        }
+        double r = rhs[i];
+#pragma unroll
+        for (int c = 0; c < 6; c++) {
+          st_wt(Vp + (size_t)i * 6 + c, v[c]);
+          const double l = v[c] * rdg[c];
+          Lp[ro + c] = l;
+          sL[t * 6 + c] = l;
+          r -= l * yj[c];
+        }
+        rhs[i] = r;
+      }
+    }
+    vm_drain();  // this thread's V hand-off and L / rhs stores have landed
+    __syncthreads();
+    if (tid == 0)
+      __hip_atomic_fetch_add(&w.ctl[CTL_PCNT], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    // ---- look-ahead: block J + 1's owner updates it by column J and publishes its LDLT
+    const bool next_active = J + 1 < K && pfirst[J + 1] <= J;
+    if (J + 1 < K && (J + 1) % G == wg && wid == 0) {
+      if (next_active && lane < 21) {
+        int r = 0;
+        while ((r + 1) * (r + 2) / 2 <= lane) r++;
+        const int c = lane - r * (r + 1) / 2;
+        const int i = j0 + 6 + r, k = j0 + 6 + c;
+        const int64_t ro = prow[i];
+        double sv = Lp[ro + k];
+#pragma unroll
+        for (int m = 0; m < 6; m++) sv -= Lp[ro + j0 + m] * ld_wt(Vp + (size_t)k * 6 + m);
+        Lp[ro + k] = sv;
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+      if (lane == 0) diag_publish(w, J + 1, Lp, rhs, dg, idg, pub);
+    }
+    // ---- every panel of column J, then the trailing update of the own rows outside block J + 1
+    if (tid == 0) cnt[3] = wait_word(w, CTL_PCNT, G * (J + 1)) ? 1 : 0;
+    __syncthreads();
+    if (!cnt[3]) {
+      ok = false;
+      break;
+    }
+    for (int q = tid; q < 36 * na; q += kT) {  // V rows of the active blocks, list order
+      const int t = q / 6, c = q - 6 * t;
+      sV[q] = ld_wt(Vp + (size_t)(6 * act[t / 6] + t % 6) * 6 + c);
+    }
+    __syncthreads();
+    for (int p = tid; p < nro * nr; p += kT) {
+      const int a = p / nr, m = p - a * nr;
+      const int i = 6 * act[own[a / 6]] + a % 6;
+      const int k = 6 * act[m / 6] + m % 6;
+      if (k > i || i < j0 + 12) continue;  // upper part; block J + 1 is its owner's look-ahead
+      const int64_t ro = prow[i];
+      double sv = Lp[ro + k];
+#pragma unroll
+      for (int c = 0; c < 6; c++) sv -= sL[a * 6 + c] * sV[m * 6 + c];
+      Lp[ro + k] = sv;
+    }
+    if (tid == 0) cnt[(J + 1) & 1] = 0;
+    __syncthreads();
+    for (int I = J + 2 + tid; I < K; I += kT)  // A_{J+1}
+      if (pfirst[I] <= J + 1) nxt[atomicAdd(&cnt[(J + 1) & 1], 1)] = I;
+    __syncthreads();
+  }
+  vm_drain();
+  __syncthreads();
+  return ok;
 }
 
 // optimizer.cpp:632-665 between the two optimize() calls: chi2 > threshold or depth <= 0 ->
@@ -1169,6 +1443,10 @@ __global__ __launch_bounds__(kT) void ba_coop_kernel(PoseParams P, CoopProblem p
   double* const Gd = Gv + (size_t)6 * n;
   double* const Gr = Gd + n;
   double* const Gi = Gr + n;
+  double* const Gv2 = Gi + n;            // the grid factorisation's second V buffer
+  double* const Gpub = Gv2 + (size_t)6 * n;  // and its two published diagonal blocks
+  // the profile LDLT over the whole grid when the active V rows fit the LDS (host: na_max)
+  const bool grid_factor = !in_lds && w.mwg && gridDim.x > 1 && w.na_max <= prof_na_cap(K);
   // optional per-phase wall clock of work-group 0 (s_memrealtime: 100 MHz)
   if (tid < 8) sh.pacc[tid] = 0.0;
   if (tid == 0) sh.pt0 = __builtin_amdgcn_s_memrealtime();
@@ -1252,13 +1530,31 @@ __global__ __launch_bounds__(kT) void ba_coop_kernel(PoseParams P, CoopProblem p
       grid_sync(w, stop_flag, false);
       tick(1);
       // ---- work-group 0: factor + solve, keyframe update (backup first) ----
+      if (grid_factor) {  // the profile LDLT over every work-group, then work-group 0 solves
+        if (wg == 0) {
+          build_S_profile(w, K, Gp, Gr);
+          if (tid == 0) {
+            w.ctl[CTL_DFLAG] = 0;
+            w.ctl[CTL_PCNT] = 0;
+          }
+        }
+        tick(5);
+        grid_sync(w, stop_flag, false);
+        const bool fok = factor_profile_grid(sh, w, K, Gp, Gr, Gd, Gi, Gv, Gv2, Gpub);
+        grid_sync(w, stop_flag, false);
+        if (wg == 0) {
+          if (tid == 0) sh.ok = fok ? 1 : 0;
+          if (fok) profile_back_solve(sh, w, K, Gp, Gr, Gd);
+          __syncthreads();
+        }
+      }
       if (wg == 0) {
         if (in_lds) {
           build_S(w, K, lambda, (LdsPtr)sh.S, (LdsPtr)sh.rhs);
           tick(5);
           factor_solve(sh, w, K, (LdsPtr)sh.S, (LdsPtr)sh.rhs, (LdsPtr)sh.dg, (LdsPtr)sh.idg,
                        (LdsPtr)sh.V);
-        } else {
+        } else if (!grid_factor) {
           build_S_profile(w, K, Gp, Gr);
           tick(5);
           factor_solve_profile(sh, w, K, Gp, Gr, Gd, Gi, Gv);
@@ -1479,7 +1775,7 @@ CoopWs coop_layout(void* base, int n_kf, int n_pts, int n_obs, int K, int pairs_
   w.pnnz = pnnz;
   w.bs = reinterpret_cast<double*>(take(8 * (size_t)n + 8));
   w.fac = reinterpret_cast<double*>(
-      take(n > kCoopLdsN ? 8 * ((size_t)pnnz + 9 * (size_t)n) : 8));
+      take(n > kCoopLdsN ? 8 * ((size_t)pnnz + 15 * (size_t)n + 64) : 8));
   w.xp = reinterpret_cast<double*>(take(8 * (size_t)n + 8));
   w.part = reinterpret_cast<double*>(take(8 * 8 * (size_t)(G + 1)));
   w.bar = reinterpret_cast<uint32_t*>(take(64));

@@ -360,6 +360,19 @@ int coop_host(const char* what, const slamgpu_camera* cam, const float* inv_sigm
       if (f >= 0 && mn < pfirst[f]) pfirst[f] = mn;
     }
   }
+  // active block rows of block column J: {I > J : pfirst[I] <= J} (I contributes to J in
+  // [pfirst[I], I - 1]); the grid factorisation stages their V rows in LDS
+  int na_max = 0;
+  {
+    std::vector<int32_t> d((size_t)K + 1, 0);
+    for (int f = 0; f < K; f++)
+      if (pfirst[f] < f) {
+        d[pfirst[f]]++;
+        d[f]--;
+      }
+    int run = 0;
+    for (int j = 0; j < K; j++) na_max = std::max(na_max, run += d[j]);
+  }
   std::vector<int64_t> prow(6 * (size_t)K);
   int64_t pnnz = 0;
   for (int i = 0; i < 6 * K; i++) {
@@ -408,6 +421,14 @@ int coop_host(const char* what, const slamgpu_camera* cam, const float* inv_sigm
   w.pfirst = reinterpret_cast<const int32_t*>(b + o_pf);
   w.prow = reinterpret_cast<const int64_t*>(b + o_prow);
   if (!prof) w.prof = nullptr;
+  w.na_max = na_max;
+  {
+    static const int mwg_env = [] {
+      const char* e = getenv("SLAMGPU_GBA_MWG");
+      return e ? atoi(e) : 1;
+    }();
+    w.mwg = mwg_env;
+  }
   const CoopProblem pb{reinterpret_cast<const slamgpu_ba_obs*>(b + o_obs),
                        reinterpret_cast<const int32_t*>(b + o_ps),
                        reinterpret_cast<const uint8_t*>(b + o_mode),

@@ -137,6 +137,7 @@ int compute_geometry(const OrbParams& p, int cols, int rows, OrbGeom* g,
       const LevelGeom& S = g->lv[l - 1];
       const double inv_scale_x = (double)L.w / S.w, inv_scale_y = (double)L.h / S.h;
       const double scale_x = 1. / inv_scale_x, scale_y = 1. / inv_scale_y;
+      L.rsx = scale_x;
       L.rx_base = (int)rx->size();
       L.xmax = L.w;
       for (int dx = 0; dx < L.w; dx++) {
@@ -289,28 +290,11 @@ void build_cells(const OrbGeom& g, std::vector<CellDesc>* cells) {
   }
 }
 
-void build_pyr_columns(OrbGeom* g, const std::vector<ResizeX>& rx, std::vector<uint32_t>* pc) {
-  pc->clear();
-  for (int l = 1; l < g->nlevels; l++) {
-    LevelGeom& L = g->lv[l];
-    L.pc_base = (int)(pc->size() / 4);
-    for (int x0 = 0; x0 < L.w; x0 += 4) {
-      const int s0 = rx[L.rx_base + x0].sx;  // < 4096 (cols <= 4095)
-      for (int k = 0; k < 4; k++) {
-        const int dx = std::min(x0 + k, L.w - 1);
-        const ResizeX& e = rx[L.rx_base + dx];
-        // the 8-byte window check of compute_geometry bounds sx_k - sx_0 by 6
-        const uint32_t bk = (uint32_t)std::min(e.sx - s0, 6);
-        pc->push_back((uint32_t)e.a0 | (uint32_t)e.a1 << 12 | bk << 24 |
-                      (uint32_t)(dx >= L.xmax) << 27 | (uint32_t)((s0 >> (4 * k)) & 15) << 28);
-      }
-    }
-  }
-}
-
 void build_pyr_bands(const OrbGeom& g, const std::vector<ResizeY>& ry, int nb,
-                     std::vector<PyrBand>* bands, int max_rows[kMaxLevels]) {
-  bands->assign((size_t)nb * kMaxLevels, PyrBand{0, -1, 0, -1});
+                     std::vector<PyrBand>* bands, std::vector<uint32_t>* rows,
+                     int max_rows[kMaxLevels]) {
+  bands->assign((size_t)nb * kMaxLevels, PyrBand{0, -1, 0, -1, 0, 0});
+  rows->clear();
   for (int l = 0; l < kMaxLevels; l++) max_rows[l] = 0;
   const int L = g.nlevels;
   // Band boundaries: level 1 split evenly; on level l >= 2 a band starts at the first row whose
@@ -358,7 +342,41 @@ void build_pyr_bands(const OrbGeom& g, const std::vector<ResizeY>& ry, int nb,
     }
     for (int l = 0; l < L; l++)
       max_rows[l] = std::max(max_rows[l], bt[l].need_hi - bt[l].need_lo + 1);
+    bt[0].rows_off = (int)(rows->size() / 2);
+    for (int l = 1; l < L; l++)
+      for (int d = bt[l].need_lo; d <= bt[l].need_hi; d++) {
+        const ResizeY& e = ry[g.lv[l].ry_base + d];
+        rows->push_back((uint32_t)e.y0 | (uint32_t)e.y1 << 16);
+        rows->push_back((uint32_t)(uint16_t)e.b0 | (uint32_t)(uint16_t)e.b1 << 16);
+      }
+    bt[0].rows_n = (int)(rows->size() / 2) - bt[0].rows_off;
   }
+}
+
+bool check_pyr_bands(const OrbGeom& g, const std::vector<ResizeY>& ry, int nb,
+                     const std::vector<PyrBand>& bands) {
+  const int L = g.nlevels;
+  auto in = [](int v, const PyrBand& r) { return v >= r.need_lo && v <= r.need_hi; };
+  for (int l = 1; l < L; l++) {
+    int next = 0;  // the own ranges, in band order, partition [0, h)
+    for (int k = 0; k < nb; k++) {
+      const PyrBand& r = bands[(size_t)k * kMaxLevels + l];
+      if (r.own_lo > r.own_hi) continue;
+      if (r.own_lo != next || r.own_lo < r.need_lo || r.own_hi > r.need_hi) return false;
+      next = r.own_hi + 1;
+    }
+    if (next != g.lv[l].h) return false;
+  }
+  for (int k = 0; k < nb; k++)  // every computed row's source rows are computed too
+    for (int l = 1; l < L; l++) {
+      const PyrBand& r = bands[(size_t)k * kMaxLevels + l];
+      const PyrBand& s = bands[(size_t)k * kMaxLevels + l - 1];
+      for (int d = r.need_lo; d <= r.need_hi; d++) {
+        const ResizeY& e = ry[g.lv[l].ry_base + d];
+        if (d < 0 || d >= g.lv[l].h || !in(e.y0, s) || !in(e.y1, s)) return false;
+      }
+    }
+  return true;
 }
 
 }  // namespace slamgpu

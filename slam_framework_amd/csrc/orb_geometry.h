@@ -59,7 +59,8 @@ struct LevelGeom {
   // resize tables (level >= 1) in the shared table buffer
   int rx_base, ry_base; // offsets into the x (per dst column) / y (per dst row) tables
   int xmax;             // first dst column that copies S[sx] * 2048 (resize HResizeLinear)
-  int pc_base;          // pyr_band_kernel: first packed 4-column group of this level (>= 1)
+  double rsx;           // resize scale_x = 1 / (w / w_prev) (level >= 1; pyr_band_kernel
+                        // derives the column coefficients from it exactly as the host tables)
   float scale, inv_scale;
   float patch_size;     // (float)(int)(PATCH_SIZE * scale) (:778)
 };
@@ -98,7 +99,9 @@ struct ResizeY { int32_t y0, y1; int16_t b0, b1; };
 // and computes [need_lo, need_hi] -- its own rows plus the rows its higher-level rows resize
 // from. Level 0 has only the need range (the caller's rows the band reads). Inclusive; an empty
 // range has lo > hi.
-struct PyrBand { int need_lo, need_hi, own_lo, own_hi; };
+// rows_off / rows_n (level-0 entry only): the band's packed row-table entries of levels >= 1
+// (y0 | y1 << 16, b0 | b1 << 16 per need row, level by level) in the band row array.
+struct PyrBand { int need_lo, need_hi, own_lo, own_hi, rows_off, rows_n; };
 
 // One FAST survivor / octree key: x_rel (12 b) | y_rel (11 b) << 12 | score (8 b) << 23,
 // coordinates relative to (minBorderX, minBorderY).

@@ -57,6 +57,7 @@ struct ExtractOutput {
 constexpr int kPyrBandsBatch = PYR_BANDS_BATCH, kPyrBandsSmall = PYR_BANDS_SMALL;
 struct PyrBandSet {
   const PyrBand* dev = nullptr;
+  const uint2* rows = nullptr;  // packed row-table entries (PyrBand rows_off / rows_n)
   int nb = 0;
   int max_rows[kMaxLevels] = {};
 };
@@ -66,7 +67,6 @@ struct OrbGeomDev {
   const OrbGeom* dev;
   const ResizeX* rx;
   const ResizeY* ry;
-  const uint4* pcol;            // pyr_band_kernel column table (build_pyr_columns)
   const PyrBandSet* bands_big;  // band partitions for batches / for small launches
   const PyrBandSet* bands_small;
   const CellDesc* cells;   // FAST cell views, cells_per_image entries (build_cells)

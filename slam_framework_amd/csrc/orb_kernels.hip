@@ -187,8 +187,9 @@ __global__ __launch_bounds__(256) void pyr_down_kernel(ImageBatch b, const OrbGe
 // ---------------------------------------------------------------------------------------
 // pyr_band: the whole pyramid (ComputePyramid :1051-1075, each level resized from the one before
 // it) of one row band of one image in one work-group, the intermediate levels held in LDS.
-// Band k owns rows [k*h_l/nb, (k+1)*h_l/nb) of every level l >= 1 and also computes the rows of
-// lower levels its higher-level rows resize from (PyrBand need ranges, build_pyr_bands), so no
+// Band k owns a contiguous run of rows of every level l >= 1 (level 1 split evenly, the higher
+// levels' runs aligned to it) and also computes the rows of lower levels its higher-level rows
+// resize from (PyrBand need ranges, build_pyr_bands), so no
 // level is read back from memory: HBM sees the caller's level-0 rows once (plus the few halo rows
 // neighbouring bands share, L2 hits on the same XCD) and every level's rows written once --
 // instead of pyr_down_kernel's one launch per level re-reading level l-1. The per-pixel arithmetic
@@ -205,21 +206,58 @@ constexpr int kPyrBandThreads = 256;
 #endif
 constexpr int kPyrBandRows = PYR_BAND_ROWS;
 
+// Work-group barrier ordering LDS only: the pending global stores of the level just computed
+// are not waited for (a __syncthreads() would drain them, vmcnt(0), at every level).
+__device__ __forceinline__ void lds_barrier() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+
+// HResizeLinear coefficients of dst column dx, derived as compute_geometry's host table
+// (resize.cpp resizeGeneric_ INTER_LINEAR: the same double / float expression sequence, so the
+// same bits): source column sx, and (a0, a1) x16 packed for v_dot2, or 32768 (S[sx] * 2048) from
+// xmax on.
+__device__ __forceinline__ int pyr_col(double rsx, int sw, int dx, uint32_t* A) {
+  float fx = (float)(((double)dx + 0.5) * rsx - 0.5);
+  int sx = (int)floorf(fx);
+  fx -= (float)sx;
+  if (sx < 0) {
+    fx = 0.f;
+    sx = 0;
+  }
+  bool copy = false;
+  if (sx + 1 >= sw) {
+    copy = true;
+    if (sx >= sw - 1) {
+      fx = 0.f;
+      sx = sw - 1;
+    }
+  }
+  const uint32_t a0 = (uint32_t)(int)rintf((1.f - fx) * 2048.f);
+  const uint32_t a1 = (uint32_t)(int)rintf(fx * 2048.f);
+  *A = copy ? 32768u : (16u * a0) | (16u * a1) << 16;
+  return sx;
+}
+
 template <int kCopy>
 __global__ __launch_bounds__(kPyrBandThreads) void pyr_band_kernel(
-    ImageBatch b, const OrbGeom* __restrict__ g, const uint4* __restrict__ pcol,
-    const ResizeY* __restrict__ ryt, const PyrBand* __restrict__ bands, int half1, int stride0) {
+    ImageBatch b, const OrbGeom* __restrict__ g, const uint2* __restrict__ rowtab,
+    const PyrBand* __restrict__ bands, int half1, int stride0, int ry_off) {
   extern __shared__ __attribute__((aligned(16))) uint8_t s_pyr[];
   int img, band;
   xcd_image_block(&img, &band);
   const int tid = threadIdx.x;
   const PyrBand* bt = bands + band * kMaxLevels;
-  const int n0lo = bt[0].need_lo, n0hi = bt[0].need_hi;
-  if (n0hi < n0lo) return;  // work-group-uniform: a band with no rows at any level
+  const PyrBand b0 = bt[0];
+  if (b0.need_hi < b0.need_lo) return;  // work-group-uniform: a band with no rows at any level
   const int nlev = g->nlevels;
   const int pitch = b.in_pitch;
-  const uint8_t* src0 = batch_image(b, img) + (int64_t)n0lo * pitch;
-  const int rows0 = n0hi - n0lo + 1;
+  const uint8_t* src0 = batch_image(b, img) + (int64_t)b0.need_lo * pitch;
+  const int rows0 = b0.need_hi - b0.need_lo + 1;
+  // the band's packed row-table entries of every level >= 1 into LDS next to the level-0 rows
+  uint2* const s_ry = reinterpret_cast<uint2*>(s_pyr + ry_off);
+  for (int i = tid; i < b0.rows_n; i += kPyrBandThreads) s_ry[i] = rowtab[b0.rows_off + i];
   if constexpr (kCopy == 0) {
     const int lane = tid & 63, wid = wave_id();
     const int nbytes = rows0 * pitch;  // a multiple of 16
@@ -247,39 +285,39 @@ __global__ __launch_bounds__(kPyrBandThreads) void pyr_band_kernel(
       }
     }
   }
-  __syncthreads();
+  __syncthreads();  // the only wait on global loads; the level loop below issues none
   uint8_t* const pyr = b.pyr + (int64_t)img * g->pyr_bytes;
+  int ry_base = 0;  // this level's first entry in s_ry
   for (int l = 1; l < nlev; l++) {
     const PyrBand nd = bt[l];
     const int sbase = bt[l - 1].need_lo;
     if (nd.need_hi >= nd.need_lo) {  // work-group-uniform
       const LevelGeom& D = g->lv[l];
       const int sw = g->lv[l - 1].w;
+      const double rsx = D.rsx;
       const uint8_t* sbuf = s_pyr + (((l - 1) & 1) ? half1 : 0);
       uint8_t* dbuf = s_pyr + ((l & 1) ? half1 : 0);
       const int ss = l == 1 ? stride0 : ((sw + 15) & ~15);
       const int ds = (D.w + 15) & ~15;
       const int ncg = (D.w + 3) >> 2;
-      const int nch = (nd.need_hi - nd.need_lo + kPyrBandRows) / kPyrBandRows;
+      const int items = ncg * ((nd.need_hi - nd.need_lo + kPyrBandRows) / kPyrBandRows);
       const int qmax = (sw - 1) >> 2;
       uint8_t* const gdst = pyr + D.offset;
-      const int dpitch = D.pitch, dw = D.w, ryb = D.ry_base, pcb = D.pc_base;
-      for (int it = tid; it < ncg * nch; it += kPyrBandThreads) {
+      const int dpitch = D.pitch, dw = D.w;
+      const uint2* const ry = s_ry + ry_base - nd.need_lo;  // indexed by dst row
+      for (int it = tid; it < items; it += kPyrBandThreads) {
         const int ch = it / ncg, cg = it - ch * ncg;
         const int x0 = 4 * cg;
         const int d0 = nd.need_lo + ch * kPyrBandRows;
         const int d1 = min(d0 + kPyrBandRows, nd.need_hi + 1);
-        const uint4 pc = pcol[pcb + cg];
-        const uint32_t pw[4] = {pc.x, pc.y, pc.z, pc.w};
-        const int s0 = (int)((pc.x >> 28) | (pc.y >> 28) << 4 | (pc.z >> 28) << 8 |
-                             (pc.w >> 28) << 12);
         uint32_t sel[4], A[4];
+        int s0 = 0;
 #pragma unroll
         for (int k = 0; k < 4; k++) {
-          const uint32_t bk = (pw[k] >> 24) & 7u;
+          const int sx = pyr_col(rsx, sw, min(x0 + k, dw - 1), &A[k]);
+          if (k == 0) s0 = sx;
+          const uint32_t bk = (uint32_t)min(sx - s0, 6);
           sel[k] = bk | 0x0c00u | (bk + 1) << 16 | 0x0c000000u;  // bytes bk, bk+1 -> u16 lanes
-          A[k] = ((pw[k] >> 27) & 1u) ? 32768u
-                                      : (16u * (pw[k] & 0xfffu)) | (16u * ((pw[k] >> 12) & 0xfffu)) << 16;
         }
         const int q0 = s0 >> 2, sh = s0 & 3;
         const int qa = min(q0, qmax), qb = min(q0 + 1, qmax), qc = min(q0 + 2, qmax);
@@ -294,27 +332,29 @@ __global__ __launch_bounds__(kPyrBandThreads) void pyr_band_kernel(
         int ra = -1, rb = -1;  // source rows held in ha / hb
         uint32_t ha[4] = {0, 0, 0, 0}, hb[4] = {0, 0, 0, 0};
         for (int d = d0; d < d1; d++) {
-          const ResizeY e = ryt[ryb + d];
-          if (e.y1 != rb) {
-            if (e.y0 == rb) {
+          const uint2 e = ry[d];
+          const int y0 = (int)(e.x & 0xffffu), y1 = (int)(e.x >> 16);
+          if (y1 != rb) {
+            if (y0 == rb) {
 #pragma unroll
               for (int k = 0; k < 4; k++) ha[k] = hb[k];
               ra = rb;
             }
-            hrow(e.y1, hb);
-            rb = e.y1;
+            hrow(y1, hb);
+            rb = y1;
           }
-          if (e.y0 != rb && e.y0 != ra) {
-            hrow(e.y0, ha);
-            ra = e.y0;
+          if (y0 != rb && y0 != ra) {
+            hrow(y0, ha);
+            ra = y0;
           }
-          const bool same = e.y0 == rb;
-          const uint32_t b0 = (uint32_t)(uint16_t)e.b0 << 8, b1 = (uint32_t)(uint16_t)e.b1 << 8;
+          const bool same = y0 == rb;
+          // (b * (r >> 4)) >> 16 == mulhi24(b << 8, (r >> 4) << 8), as in pyr_down_kernel
+          const uint32_t bb0 = (e.y & 0xffffu) << 8, bb1 = (e.y >> 16) << 8;
           uint32_t packed = 0;
 #pragma unroll
           for (int k = 0; k < 4; k++) {
             const uint32_t r0 = (same ? hb[k] : ha[k]) & ~0xffu, r1 = hb[k] & ~0xffu;
-            const uint32_t v = (mulhi24(b0, r0) + mulhi24(b1, r1) + 2) >> 2;
+            const uint32_t v = (mulhi24(bb0, r0) + mulhi24(bb1, r1) + 2) >> 2;
             packed |= (v & 0xffu) << (8 * k);
           }
           *reinterpret_cast<uint32_t*>(dbuf + (d - nd.need_lo) * ds + x0) = packed;
@@ -328,8 +368,9 @@ __global__ __launch_bounds__(kPyrBandThreads) void pyr_band_kernel(
           }
         }
       }
+      ry_base += nd.need_hi - nd.need_lo + 1;
     }
-    __syncthreads();
+    lds_barrier();
   }
 }
 
@@ -2892,10 +2933,11 @@ void launch_extract(const ImageBatch& b, const OrbGeomDev& gd, int n_images, hip
   const bool in_aligned = (((uintptr_t)b.in_l | (uintptr_t)b.in_r | (uintptr_t)b.in_stride |
                            (uintptr_t)b.in_pitch) & 3) == 0;
   const bool short_strips = n_images <= kPyrShortMaxImages;
-  // the fused band kernel (SLAMGPU_PYR_FUSED=0: one pyr_down launch per level, for A/B)
+  // the fused band kernel is off by default (SLAMGPU_PYR_FUSED=1 selects it, for A/B): measured
+  // slower than the per-level launches (1.24 vs 0.52 ms per step alone)
   static const int fused_mode = [] {
     const char* e = std::getenv("SLAMGPU_PYR_FUSED");
-    return e ? std::atoi(e) : 1;
+    return e ? std::atoi(e) : 0;
   }();
   bool fused = false;
   if (fused_mode && g.nlevels > 1) {
@@ -2912,18 +2954,21 @@ void launch_extract(const ImageBatch& b, const OrbGeomDev& gd, int n_images, hip
       if (l & 1) buf1 = std::max(buf1, s); else buf0 = std::max(buf0, s);
     }
     const int half1 = (int)((buf0 + 15) & ~(size_t)15);
-    const size_t lds = (size_t)half1 + buf1;
-    if (bs.dev && lds <= 160 * 1024) {
+    const int ry_off = (int)(half1 + ((buf1 + 15) & ~(size_t)15));
+    size_t ry_rows = 0;
+    for (int l = 1; l < g.nlevels; l++) ry_rows += bs.max_rows[l];
+    const size_t lds = (size_t)ry_off + 8 * ry_rows;
+    if (bs.dev && bs.rows && lds <= 160 * 1024) {
       const dim3 grid(bs.nb, n_images);
       if (copy == 0)
         SLAMGPU_LAUNCH("pyr_down", st, pyr_band_kernel<0>, grid, dim3(kPyrBandThreads), lds, st,
-                       b, gd.dev, gd.pcol, gd.ry, bs.dev, half1, stride0);
+                       b, gd.dev, bs.rows, bs.dev, half1, stride0, ry_off);
       else if (copy == 1)
         SLAMGPU_LAUNCH("pyr_down", st, pyr_band_kernel<1>, grid, dim3(kPyrBandThreads), lds, st,
-                       b, gd.dev, gd.pcol, gd.ry, bs.dev, half1, stride0);
+                       b, gd.dev, bs.rows, bs.dev, half1, stride0, ry_off);
       else
         SLAMGPU_LAUNCH("pyr_down", st, pyr_band_kernel<2>, grid, dim3(kPyrBandThreads), lds, st,
-                       b, gd.dev, gd.pcol, gd.ry, bs.dev, half1, stride0);
+                       b, gd.dev, bs.rows, bs.dev, half1, stride0, ry_off);
       fused = true;
     }
   }

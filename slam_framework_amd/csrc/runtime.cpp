@@ -41,8 +41,8 @@ struct slamgpu_ctx {
   OrbGeom* d_geom = nullptr;
   ResizeX* d_rx = nullptr;
   ResizeY* d_ry = nullptr;
-  uint32_t* d_pcol = nullptr;
   PyrBand* d_bands[2] = {nullptr, nullptr};
+  uint32_t* d_brows[2] = {nullptr, nullptr};
   PyrBandSet pbands[2];  // fused pyramid: [0] batches, [1] small launches
   CellDesc* d_cells = nullptr;
   // images staged by the host-buffer calls (left at d_in, right at d_in + in_stride)
@@ -99,7 +99,6 @@ struct slamgpu_ctx {
     g.dev = d_geom;
     g.rx = d_rx;
     g.ry = d_ry;
-    g.pcol = reinterpret_cast<const uint4*>(d_pcol);
     g.bands_big = &pbands[0];
     g.bands_small = &pbands[1];
     g.cells = d_cells;
@@ -264,9 +263,8 @@ int slamgpu_create(int device, const slamgpu_orb_params* p, int cols, int rows, 
                        why[std::min(std::max(-gr, 0), 6)]);
   }
   compute_tables(c->params, &c->tables);
-  std::vector<uint32_t> pcol;
-  build_pyr_columns(&c->geom, rx, &pcol);
   std::vector<PyrBand> bands[2];
+  std::vector<uint32_t> brows[2];
   {  // fused pyramid band partitions (SLAMGPU_PYR_NB / SLAMGPU_PYR_NB_SMALL override, A/B)
     const char* e0 = getenv("SLAMGPU_PYR_NB");
     const char* e1 = getenv("SLAMGPU_PYR_NB_SMALL");
@@ -274,7 +272,11 @@ int slamgpu_create(int device, const slamgpu_orb_params* p, int cols, int rows, 
                        std::min(std::max(e1 ? atoi(e1) : kPyrBandsSmall, 1), 1024)};
     for (int i = 0; i < 2; i++) {
       c->pbands[i].nb = nb[i];
-      build_pyr_bands(c->geom, ry, nb[i], &bands[i], c->pbands[i].max_rows);
+      build_pyr_bands(c->geom, ry, nb[i], &bands[i], &brows[i], c->pbands[i].max_rows);
+      if (!check_pyr_bands(c->geom, ry, nb[i], bands[i])) {  // never expected: keep the
+        bands[i].clear();                                    // per-level kernels then
+        c->pbands[i].nb = 0;
+      }
     }
   }
   if (c->geom.kp_cap > 4096) {  // matcher keys carry a 12-bit keypoint index
@@ -330,15 +332,17 @@ int slamgpu_create(int device, const slamgpu_orb_params* p, int cols, int rows, 
   TRY(hcheck(c, hipMemcpy(c->d_geom, &g, sizeof(OrbGeom), hipMemcpyHostToDevice)));
   TRY(hcheck(c, hipMemcpy(c->d_rx, rx.data(), rx.size() * sizeof(ResizeX), hipMemcpyHostToDevice)));
   TRY(hcheck(c, hipMemcpy(c->d_ry, ry.data(), ry.size() * sizeof(ResizeY), hipMemcpyHostToDevice)));
-  TRY(dalloc(c, &c->d_pcol, pcol.size() + 4));
-  if (!pcol.empty())
-    TRY(hcheck(c, hipMemcpy(c->d_pcol, pcol.data(), pcol.size() * sizeof(uint32_t),
-                            hipMemcpyHostToDevice)));
   for (int i = 0; i < 2; i++) {
+    if (c->pbands[i].nb == 0) continue;
     TRY(dalloc(c, &c->d_bands[i], bands[i].size()));
     TRY(hcheck(c, hipMemcpy(c->d_bands[i], bands[i].data(), bands[i].size() * sizeof(PyrBand),
                             hipMemcpyHostToDevice)));
     c->pbands[i].dev = c->d_bands[i];
+    TRY(dalloc(c, &c->d_brows[i], brows[i].size() + 2));
+    if (!brows[i].empty())
+      TRY(hcheck(c, hipMemcpy(c->d_brows[i], brows[i].data(), brows[i].size() * sizeof(uint32_t),
+                              hipMemcpyHostToDevice)));
+    c->pbands[i].rows = reinterpret_cast<const uint2*>(c->d_brows[i]);
   }
   TRY(hcheck(c, hipMemcpy(c->d_cells, cells.data(), cells.size() * sizeof(CellDesc),
                           hipMemcpyHostToDevice)));
