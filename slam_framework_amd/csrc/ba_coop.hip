@@ -1075,7 +1075,8 @@ __device__ void profile_back_solve(CoopShared& sh, const CoopWs& w, int K, doubl
 //   * the owner of block J publishes L_JJ, D_J^-1, y_J and ok (28 doubles) and raises CTL_DFLAG
 //     to J + 1;
 //   * every work-group forms its active panel rows V = A_iJ L_JJ^-T, L_iJ = V D_J^-1 (rhs updated)
-//     and publishes V, then counts itself in at CTL_PCNT.
+//     and publishes V, then raises its own panel flag (one 128-byte line per work-group: no
+//     contended counter) to J + 1.
 // The owner of block J + 1 updates that block from its own V and factors it at once (look-ahead),
 // so column J + 1's hand-off leaves before the other work-groups finish column J; they wait for
 // all of column J's panels, stage the active V rows in LDS and update their own rows. Every element
@@ -1084,6 +1085,41 @@ __device__ void profile_back_solve(CoopShared& sh, const CoopWs& w, int K, doubl
 // ahead of the slowest (it cannot pass column J + 1's panel count before everyone has finished
 // column J). Active block rows per column <= na_cap (the V rows fit the LDS; host-checked).
 constexpr int kPubStride = 32;  // doubles per published diagonal block (15 + 6 + 6 + ok)
+
+// Wave 0: spin until every work-group's flag (pflag[32 g], one 128-byte line each) reaches target;
+// the same give-up rules as wait_word (progress = any flag moving).
+__device__ bool wait_flags(const CoopWs& w, const int32_t* pflag, int32_t target) {
+  const int lane = threadIdx.x & 63, G = gridDim.x;
+  uint32_t spins = 0, polls = 0;
+  int64_t seen = -1;
+  for (;;) {
+    int64_t sum = 0;
+    bool all = true;
+    for (int g0 = 0; g0 < G; g0 += 64) {
+      const int g = g0 + lane;
+      const int32_t v = g < G ? __hip_atomic_load(const_cast<int32_t*>(pflag) + 32 * g,
+                                                  __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                              : target;
+      all = all && __all(v >= target);
+      sum += v;
+    }
+    if (all) return true;
+    sum = __builtin_amdgcn_readfirstlane((int)sum);  // progress proxy (lane 0's partial)
+    if (sum != seen) {
+      seen = sum;
+      spins = 0;
+    }
+    if (polls < 256) __builtin_amdgcn_s_sleep(1);
+    else __builtin_amdgcn_s_sleep(8);
+    polls++;
+    if ((++spins & 255u) == 0 && ctl_load(w, CTL_ERR)) return false;
+    if (spins > (1u << 22)) {
+      if (lane == 0)
+        __hip_atomic_store(&w.ctl[CTL_ERR], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      return false;
+    }
+  }
+}
 
 // Thread 0: spin until the word reaches target (relaxed device-scope loads, s_sleep back-off).
 // False once the grid has given up (CTL_ERR), or when nothing moved for ~2^22 sleeps (raised here).
@@ -1108,13 +1144,13 @@ __device__ bool wait_word(const CoopWs& w, int idx, int32_t target) {
   }
 }
 
-// factor_profile_grid's LDS in sh.S: two A_J lists + 4 counters + the own-block positions (ints),
-// then (16-byte aligned) the published block, the active V rows and the own L_iJ rows (doubles).
-__device__ __forceinline__ int prof_lists_dw(int K) { return (12 * K + 16 + 15) / 16 * 2; }
-// Active blocks per column whose V rows (36 doubles) and, at most as many, own L_iJ rows fit.
+// factor_profile_grid's LDS in sh.S: two A_J lists + 8 counters + the own-block positions + pfirst
+// (ints), then (16-byte aligned) two published blocks, the active V rows and the own L_iJ rows.
+__device__ __forceinline__ int prof_lists_dw(int K) { return (16 * K + 32 + 15) / 16 * 2; }
+// Active blocks per column whose V rows (36 doubles) and, at most as many, own L_iJ and V rows fit.
 __device__ __forceinline__ int prof_na_cap(int K) {
-  const int avail = (int)(sizeof(CoopShared::S) / 8) - prof_lists_dw(K) - kPubStride;
-  return avail > 0 ? avail / 72 : 0;
+  const int avail = (int)(sizeof(CoopShared::S) / 8) - prof_lists_dw(K) - 2 * kPubStride;
+  return avail > 0 ? avail / 108 : 0;
 }
 
 // The 6x6 LDLT of diagonal block J (rows j0.. of the profile, already updated by every column
@@ -1186,11 +1222,11 @@ __device__ void diag_publish(const CoopWs& w, int J, double* Lp, double* rhs, do
 }
 
 // Every work-group. Returns false (work-group-uniform, the same in every work-group) on a zero
-// pivot or when the grid gave up; CTL_DFLAG / CTL_PCNT must be 0 on entry (zeroed before the grid
-// barrier that precedes it).
+// pivot or when the grid gave up; CTL_DFLAG and the panel flags must be 0 on entry (zeroed
+// before the grid barrier that precedes it).
 __device__ bool factor_profile_grid(CoopShared& sh, const CoopWs& w, int K, double* Lp,
                                     double* rhs, double* dg, double* idg, double* Vg0,
-                                    double* Vg1, double* pub) {
+                                    double* Vg1, double* pub, int32_t* pflag) {
 #pragma clang fp contract(fast)  // tolerance-compared FP64 path
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int G = gridDim.x, wg = blockIdx.x;
@@ -1199,37 +1235,61 @@ __device__ bool factor_profile_grid(CoopShared& sh, const CoopWs& w, int K, doub
   // LDS (the unused dense factor storage): A_J lists (two buffers) + counts, the own active
   // blocks' list positions, column J's published block, the active V rows, the own L_iJ rows
   int* const lists = reinterpret_cast<int*>(sh.S);
-  int* const cnt = lists + 2 * K;   // [0], [1]: list sizes; [2]: own count; [3]: ok
-  int* const own = cnt + 4;         // [K]
-  double* const pd = sh.S + prof_lists_dw(K);
-  double* const sV = pd + kPubStride;  // [36 * na] V rows of the active blocks, list order
+  int* const cnt = lists + 2 * K;  // [0], [1]: list sizes; [2]: own count; [3]: ok; [4]: the
+                                   // next column's block already staged
+  int* const own = cnt + 8;        // [K]
+  int* const spf = own + K;        // [K] pfirst
+  double* const pdb = sh.S + prof_lists_dw(K);  // [2][kPubStride] published blocks, by parity
+  double* const sV = pdb + 2 * kPubStride;  // [36 * na] V rows of the active blocks, list order
   // own L_iJ rows: after sV, sized by the caller's cap (6 * 6 per own block, <= na blocks)
   const int na_cap = prof_na_cap(K);
-  double* const sL = sV + 36 * (size_t)na_cap;
-  if (tid == 0) cnt[0] = 0;
+  double* const sL = sV + 36 * (size_t)na_cap;   // [36 * no] own L_iJ rows
+  double* const sVo = sL + 36 * (size_t)na_cap;  // [36 * no] own V rows (the look-ahead's)
+  if (tid == 0) {
+    cnt[0] = 0;
+    cnt[4] = 0;
+  }
+  for (int I = tid; I < K; I += kT) spf[I] = pfirst[I];
   __syncthreads();
   for (int I = 1 + tid; I < K; I += kT)  // A_0
-    if (pfirst[I] <= 0) lists[atomicAdd(&cnt[0], 1)] = I;
+    if (spf[I] <= 0) lists[atomicAdd(&cnt[0], 1)] = I;
   if (wg == 0 && tid == 0) diag_publish(w, 0, Lp, rhs, dg, idg, pub);
   __syncthreads();
   bool ok = true;
+#if FS_PROF  // diagnostic build: thread 0 of work-group 0 splits each column into prof[8..12]
+  const bool gp = w.prof && wg == 0 && tid == 0;
+  uint64_t gt = __builtin_amdgcn_s_memrealtime();
+  double gacc[5] = {0, 0, 0, 0, 0};
+  auto gtick = [&](int slot) {
+    if (gp) {
+      const uint64_t t = __builtin_amdgcn_s_memrealtime();
+      gacc[slot] += 0.01 * (double)(t - gt);
+      gt = t;
+    }
+  };
+#else
+  auto gtick = [](int) {};
+#endif
   for (int J = 0; J < K; J++) {
     const int j0 = 6 * J;
     const int* act = lists + (J & 1) * K;
     int* nxt = lists + ((J + 1) & 1) * K;
     const int na = cnt[J & 1], nr = 6 * na;
     double* const Vp = (J & 1) ? Vg1 : Vg0;
-    // ---- column J's diagonal block from its owner
+    double* const pd = pdb + (J & 1) * kPubStride;
+    // ---- column J's diagonal block from its owner (staged during column J - 1 when it was out)
+    const bool staged = cnt[4] != 0;
+    __syncthreads();
     if (tid == 0) {
       cnt[2] = 0;
-      cnt[3] = wait_word(w, CTL_DFLAG, J + 1) ? 1 : 0;
+      cnt[3] = staged || wait_word(w, CTL_DFLAG, J + 1) ? 1 : 0;
     }
     __syncthreads();
     if (!cnt[3]) {
       ok = false;
       break;
     }
-    if (tid < 28) pd[tid] = ld_wt(pub + (J & 1) * kPubStride + tid);
+    if (!staged && tid < 28) pd[tid] = ld_wt(pub + (J & 1) * kPubStride + tid);
     for (int t = tid; t < na; t += kT)  // own active blocks (any order)
       if (act[t] % G == wg) own[atomicAdd(&cnt[2], 1)] = t;
     __syncthreads();
@@ -1238,6 +1298,7 @@ __device__ bool factor_profile_grid(CoopShared& sh, const CoopWs& w, int K, doub
       break;
     }
     const int no = cnt[2], nro = 6 * no;
+    gtick(0);
     // ---- panel rows of the own active blocks (forward solve fused); V published, L_iJ kept
     {
       double Ljj[15], rdg[6], yj[6];
@@ -1264,6 +1325,7 @@ __device__ bool factor_profile_grid(CoopShared& sh, const CoopWs& w, int K, doub
 #pragma unroll
         for (int c = 0; c < 6; c++) {
           st_wt(Vp + (size_t)i * 6 + c, v[c]);
+          sVo[t * 6 + c] = v[c];
           const double l = v[c] * rdg[c];
           Lp[ro + c] = l;
           sL[t * 6 + c] = l;
@@ -1274,12 +1336,15 @@ __device__ bool factor_profile_grid(CoopShared& sh, const CoopWs& w, int K, doub
     }
     vm_drain();  // this thread's V hand-off and L / rhs stores have landed
     __syncthreads();
-    if (tid == 0)
-      __hip_atomic_fetch_add(&w.ctl[CTL_PCNT], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (tid == 0)  // this work-group's panel of column J is out (its own 128-byte line)
+      __hip_atomic_store(&pflag[32 * wg], J + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    gtick(1);
     // ---- look-ahead: block J + 1's owner updates it by column J and publishes its LDLT
-    const bool next_active = J + 1 < K && pfirst[J + 1] <= J;
+    const bool next_active = J + 1 < K && spf[J + 1] <= J;
     if (J + 1 < K && (J + 1) % G == wg && wid == 0) {
       if (next_active && lane < 21) {
+        int a1 = 0;  // block J + 1 among the own active blocks
+        while (act[own[a1]] != J + 1) a1++;
         int r = 0;
         while ((r + 1) * (r + 2) / 2 <= lane) r++;
         const int c = lane - r * (r + 1) / 2;
@@ -1287,7 +1352,7 @@ __device__ bool factor_profile_grid(CoopShared& sh, const CoopWs& w, int K, doub
         const int64_t ro = prow[i];
         double sv = Lp[ro + k];
 #pragma unroll
-        for (int m = 0; m < 6; m++) sv -= Lp[ro + j0 + m] * ld_wt(Vp + (size_t)k * 6 + m);
+        for (int m = 0; m < 6; m++) sv -= Lp[ro + j0 + m] * sVo[(6 * a1 + c) * 6 + m];
         Lp[ro + k] = sv;
       }
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
@@ -1296,12 +1361,24 @@ __device__ bool factor_profile_grid(CoopShared& sh, const CoopWs& w, int K, doub
       if (lane == 0) diag_publish(w, J + 1, Lp, rhs, dg, idg, pub);
     }
     // ---- every panel of column J, then the trailing update of the own rows outside block J + 1
-    if (tid == 0) cnt[3] = wait_word(w, CTL_PCNT, G * (J + 1)) ? 1 : 0;
+    if (wid == 0) {
+      const bool got = wait_flags(w, pflag, J + 1);
+      if (tid == 0) cnt[3] = got ? 1 : 0;
+    }
+    if (tid == 0) {
+      // column J + 1's block, when already published, staged beside this column's V rows
+      cnt[4] = J + 1 < K && __hip_atomic_load(&w.ctl[CTL_DFLAG], __ATOMIC_RELAXED,
+                                              __HIP_MEMORY_SCOPE_AGENT) >= J + 2;
+    }
     __syncthreads();
     if (!cnt[3]) {
       ok = false;
       break;
     }
+    gtick(2);
+    if (cnt[4] && tid >= kT - 28)
+      pdb[((J + 1) & 1) * kPubStride + tid - (kT - 28)] =
+          ld_wt(pub + ((J + 1) & 1) * kPubStride + tid - (kT - 28));
     for (int q = tid; q < 36 * na; q += kT) {  // V rows of the active blocks, list order
       const int t = q / 6, c = q - 6 * t;
       sV[q] = ld_wt(Vp + (size_t)(6 * act[t / 6] + t % 6) * 6 + c);
@@ -1320,10 +1397,18 @@ __device__ bool factor_profile_grid(CoopShared& sh, const CoopWs& w, int K, doub
     }
     if (tid == 0) cnt[(J + 1) & 1] = 0;
     __syncthreads();
+    gtick(3);
     for (int I = J + 2 + tid; I < K; I += kT)  // A_{J+1}
-      if (pfirst[I] <= J + 1) nxt[atomicAdd(&cnt[(J + 1) & 1], 1)] = I;
+      if (spf[I] <= J + 1) nxt[atomicAdd(&cnt[(J + 1) & 1], 1)] = I;
     __syncthreads();
+    gtick(4);
   }
+#if FS_PROF
+  if (gp) {
+    for (int k = 0; k < 5; k++) w.prof[8 + k] += gacc[k];
+    w.prof[13] -= 1.0;  // negative: the grid factorisation's split
+  }
+#endif
   vm_drain();
   __syncthreads();
   return ok;
@@ -1445,6 +1530,7 @@ __global__ __launch_bounds__(kT) void ba_coop_kernel(PoseParams P, CoopProblem p
   double* const Gi = Gr + n;
   double* const Gv2 = Gi + n;            // the grid factorisation's second V buffer
   double* const Gpub = Gv2 + (size_t)6 * n;  // and its two published diagonal blocks
+  int32_t* const Gflag = reinterpret_cast<int32_t*>(Gpub + 64);  // panel flags, 128 B apart
   // the profile LDLT over the whole grid when the active V rows fit the LDS (host: na_max)
   const bool grid_factor = !in_lds && w.mwg && gridDim.x > 1 && w.na_max <= prof_na_cap(K);
   // optional per-phase wall clock of work-group 0 (s_memrealtime: 100 MHz)
@@ -1533,14 +1619,13 @@ __global__ __launch_bounds__(kT) void ba_coop_kernel(PoseParams P, CoopProblem p
       if (grid_factor) {  // the profile LDLT over every work-group, then work-group 0 solves
         if (wg == 0) {
           build_S_profile(w, K, Gp, Gr);
-          if (tid == 0) {
-            w.ctl[CTL_DFLAG] = 0;
-            w.ctl[CTL_PCNT] = 0;
-          }
+          if (tid == 0) w.ctl[CTL_DFLAG] = 0;
+          for (int g = tid; g < (int)gridDim.x; g += kT)
+            __hip_atomic_store(&Gflag[32 * g], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
         tick(5);
         grid_sync(w, stop_flag, false);
-        const bool fok = factor_profile_grid(sh, w, K, Gp, Gr, Gd, Gi, Gv, Gv2, Gpub);
+        const bool fok = factor_profile_grid(sh, w, K, Gp, Gr, Gd, Gi, Gv, Gv2, Gpub, Gflag);
         grid_sync(w, stop_flag, false);
         if (wg == 0) {
           if (tid == 0) sh.ok = fok ? 1 : 0;
@@ -1775,7 +1860,7 @@ CoopWs coop_layout(void* base, int n_kf, int n_pts, int n_obs, int K, int pairs_
   w.pnnz = pnnz;
   w.bs = reinterpret_cast<double*>(take(8 * (size_t)n + 8));
   w.fac = reinterpret_cast<double*>(
-      take(n > kCoopLdsN ? 8 * ((size_t)pnnz + 15 * (size_t)n + 64) : 8));
+      take(n > kCoopLdsN ? 8 * ((size_t)pnnz + 15 * (size_t)n + 64) + 128 * kMaxGrid : 8));
   w.xp = reinterpret_cast<double*>(take(8 * (size_t)n + 8));
   w.part = reinterpret_cast<double*>(take(8 * 8 * (size_t)(G + 1)));
   w.bar = reinterpret_cast<uint32_t*>(take(64));

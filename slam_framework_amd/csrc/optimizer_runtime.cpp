@@ -509,6 +509,10 @@ int coop_host(const char* what, const slamgpu_camera* cam, const float* inv_sigm
     fprintf(stderr, "[%s] us: lin %.0f barrier %.0f assemble %.0f build_S %.0f factor %.0f "
             "kf_update %.0f points %.0f first-sync %.0f (G %d, K %d)\n", what, pr[0], pr[1],
             pr[2], pr[5], pr[6], pr[3], pr[4], pr[7], G, K);
+    if (pr[13] < 0)  // FS_PROF build, grid factorisation: work-group 0's split per column
+      fprintf(stderr, "[%s] grid factor split us: diag-wait %.0f panel %.0f pcnt-wait %.0f "
+              "trailing %.0f lists %.0f (%.0f factorisations)\n", what, pr[8], pr[9], pr[10],
+              pr[11], pr[12], -pr[13]);
     if (pr[13] > 0)  // FS_PROF diagnostic build of ba_coop.hip
       fprintf(stderr, "[%s] factor split us: panel %.0f bar1 %.0f wave0-diag %.0f bar2 %.0f "
               "solve %.0f (%.0f factorisations; active block rows per column: mean %.1f, "
