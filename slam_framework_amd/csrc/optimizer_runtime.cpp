@@ -422,12 +422,12 @@ int coop_host(const char* what, const slamgpu_camera* cam, const float* inv_sigm
   w.prow = reinterpret_cast<const int64_t*>(b + o_prow);
   if (!prof) w.prof = nullptr;
   w.na_max = na_max;
-  {
-    static const int mwg_env = [] {
-      const char* e = getenv("SLAMGPU_GBA_MWG");
-      return e ? atoi(e) : 1;
-    }();
-    w.mwg = mwg_env;
+  {  // the grid factorisation pays ~12 us of hand-offs per block column: below ~40 keyframes
+     // work-group 0 alone is faster (bench: 30 keyframes 4.6 vs 5.6 ms; 54: 16.1 vs 13.1 ms)
+    const char* e0 = getenv("SLAMGPU_GBA_MWG");  // read per call: tests switch both paths
+    const char* e1 = getenv("SLAMGPU_GBA_MWG_MIN_KF");
+    const int mwg_env = e0 ? atoi(e0) : 1, mwg_min = e1 ? atoi(e1) : 40;
+    w.mwg = mwg_env && K >= mwg_min;
   }
   const CoopProblem pb{reinterpret_cast<const slamgpu_ba_obs*>(b + o_obs),
                        reinterpret_cast<const int32_t*>(b + o_ps),

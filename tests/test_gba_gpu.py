@@ -41,6 +41,24 @@ def test_global_ba_matches_oracle(oracle, gpu_lib, seed, nkf, npt, robust, iters
     assert np.array_equal(kf[0], kf_o[0])  # the fixed keyframe: only the Converter round trip
 
 
+@pytest.mark.parametrize("mwg,min_kf,seed,nkf,npt", [("1", "0", 37, 30, 4000),
+                                                     ("1", "0", 38, 26, 3000),
+                                                     ("0", "40", 39, 60, 6000)])
+def test_global_ba_both_profile_factorisations(oracle, gpu_lib, monkeypatch, mwg, min_kf, seed,
+                                               nkf, npt):
+    """The profile LDLT over the whole grid (factor_profile_grid: block rows owned per
+    work-group, write-through hand-offs) forced below its 40-keyframe default, and work-group 0
+    alone forced above it: both match the oracle."""
+    monkeypatch.setenv("SLAMGPU_GBA_MWG", mwg)
+    monkeypatch.setenv("SLAMGPU_GBA_MWG_MIN_KF", min_kf)
+    P = gba_problem(seed, nkf, npt, spacing=0.8, outlier_frac=0.02)
+    kf_o, pts_o, its_o = oracle.global_ba(CAM, P, 10, True)
+    kf, pts, its = run(gpu_lib, P, 10, True)
+    assert its == its_o
+    assert_close(kf, kf_o, P["kf_Tcw"], "keyframe poses")
+    assert_close(pts, pts_o, P["points"], "points")
+
+
 def test_global_ba_unobserved_point_kept(oracle, gpu_lib):
     """A point without observations is not optimised (optimizer.cpp:149-152)."""
     P = gba_problem(35, 8, 400)
