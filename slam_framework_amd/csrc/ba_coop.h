@@ -78,10 +78,8 @@ struct CoopWs {
 // CTL_BEAT: work-group 0's heartbeat while the others wait at a barrier (bumped per block column
 // of the factorisation); CTL_ARRIVED / CTL_GRID: on a barrier give-up, the arrivals the giving-up
 // waiter last saw and the grid size (missing work-groups vs a slow one).
-// CTL_DFLAG: the grid factorisation's diagonal blocks published so far, zeroed before each
-// factorisation.
 enum { CTL_ERR = 0, CTL_STOPPED = 1, CTL_LM = 2, CTL_POLL = 3, CTL_OK = 4, CTL_BEAT = 5,
-       CTL_ARRIVED = 6, CTL_GRID = 7, CTL_DFLAG = 8 };
+       CTL_ARRIVED = 6, CTL_GRID = 7 };
 
 // One optimize() call of the schedule.
 struct CoopPhase {

@@ -816,6 +816,13 @@ __device__ __forceinline__ void factor_solve(CoopShared& sh, const CoopWs& w, in
 __device__ void profile_back_solve(CoopShared& sh, const CoopWs& w, int K, double* Lp,
                                    double* rhs, const double* dg);
 
+// Work-group barrier ordering LDS only (no vmcnt drain of pending global loads or stores).
+__device__ __forceinline__ void lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+
 // The same LDLT for 6K > kCoopLdsN on the block-profile storage (w.prow / w.pfirst): row i holds
 // columns 6 pfirst[i / 6] .. i, and every fill-in stays inside that envelope, so block column J
 // only touches the active block rows A_J = {I > J : pfirst[I] <= J} -- a band of a few dozen
@@ -1025,6 +1032,77 @@ __device__ void profile_back_solve(CoopShared& sh, const CoopWs& w, int K, doubl
   const int64_t* prow = w.prow;
   const int32_t* pfirst = w.pfirst;
   double* const xs = sh.rhs;  // 6 doubles (sh.rhs is unused on the profile path)
+  // z in LDS when it fits (the unused dense factor storage): the block steps then hand off
+  // through LDS only, and the next block's L values are loaded while this block is solved
+  if (n <= (int)(sizeof(sh.S) / sizeof(double))) {
+    double* const z = sh.S;
+    for (int i = tid; i < n; i += kT) z[i] = rhs[i] / dg[i];
+    double Lb[15], Lr[6];  // thread 0: block J's strict lower L; every thread: its first row
+    auto fetch = [&](int J) {
+      const int j0 = 6 * J;
+      if (tid == 0) {
+#pragma unroll
+        for (int c = 1; c < 6; c++)
+#pragma unroll
+          for (int r = 0; r < c; r++) Lb[c * (c - 1) / 2 + r] = Lp[prow[j0 + c] + j0 + r];
+      }
+      const int i = 6 * pfirst[J] + tid;
+      if (i < j0)
+#pragma unroll
+        for (int c = 0; c < 6; c++) Lr[c] = Lp[prow[j0 + c] + i];
+    };
+    if (K > 0) fetch(K - 1);
+    __syncthreads();
+    for (int J = K - 1; J >= 0; J--) {
+      const int j0 = 6 * J;
+      double Lbc[15], Lrc[6];
+#pragma unroll
+      for (int q = 0; q < 15; q++) Lbc[q] = Lb[q];
+#pragma unroll
+      for (int c = 0; c < 6; c++) Lrc[c] = Lr[c];
+      if (J > 0) fetch(J - 1);  // in flight under this block's solve and update
+      if (tid == 0) {
+        double x[6];
+#pragma unroll
+        for (int r = 0; r < 6; r++) x[r] = z[j0 + r];
+#pragma unroll
+        for (int c = 5; c >= 0; c--)
+#pragma unroll
+          for (int r = 0; r < c; r++) x[r] -= Lbc[c * (c - 1) / 2 + r] * x[c];
+#pragma unroll
+        for (int r = 0; r < 6; r++) {
+          z[j0 + r] = x[r];
+          xs[r] = x[r];
+        }
+      }
+      lds_sync();
+      double x[6];
+#pragma unroll
+      for (int c = 0; c < 6; c++) x[c] = xs[c];
+      const int i0 = 6 * pfirst[J];
+      if (i0 + tid < j0) {
+        double sx = z[i0 + tid];
+#pragma unroll
+        for (int c = 0; c < 6; c++) sx -= Lrc[c] * x[c];
+        z[i0 + tid] = sx;
+      }
+      if (i0 + kT < j0) {
+        int64_t rb[6];
+#pragma unroll
+        for (int c = 0; c < 6; c++) rb[c] = prow[j0 + c];
+        for (int i = i0 + kT + tid; i < j0; i += kT) {
+          double sx = z[i];
+#pragma unroll
+          for (int c = 0; c < 6; c++) sx -= Lp[rb[c] + i] * x[c];
+          z[i] = sx;
+        }
+      }
+      lds_sync();
+    }
+    for (int i = tid; i < n; i += kT) w.xp[i] = z[i];
+    __syncthreads();
+    return;
+  }
   for (int i = tid; i < n; i += kT) rhs[i] /= dg[i];
   __syncthreads();
   for (int J = K - 1; J >= 0; J--) {
@@ -1068,26 +1146,26 @@ __device__ void profile_back_solve(CoopShared& sh, const CoopWs& w, int K, doubl
 }
 
 // ---- the profile LDLT over the whole grid (6K > kCoopLdsN) ---------------------------------
-// Block row I of S (its rows of L, rhs, dg) belongs to work-group I % G for the whole
-// factorisation: its panel rows, its trailing updates and, for its diagonal block, the 6x6 LDLT are
-// all computed there, so L never crosses work-groups and needs no L2 write-back. Per block column
-// J two small hand-offs do, write-through (st_wt / ld_wt, as the reduction partials):
-//   * the owner of block J publishes L_JJ, D_J^-1, y_J and ok (28 doubles) and raises CTL_DFLAG
-//     to J + 1;
-//   * every work-group forms its active panel rows V = A_iJ L_JJ^-T, L_iJ = V D_J^-1 (rhs updated)
-//     and publishes V, then raises its own panel flag (one 128-byte line per work-group: no
-//     contended counter) to J + 1.
-// The owner of block J + 1 updates that block from its own V and factors it at once (look-ahead),
-// so column J + 1's hand-off leaves before the other work-groups finish column J; they wait for
-// all of column J's panels, stage the active V rows in LDS and update their own rows. Every element
-// sees the same operations in the same order as in factor_solve_profile (identical results). V and
-// the diagonal hand-off are double-buffered by column parity: a work-group runs at most one column
-// ahead of the slowest (it cannot pass column J + 1's panel count before everyone has finished
-// column J). Active block rows per column <= na_cap (the V rows fit the LDS; host-checked).
-constexpr int kPubStride = 32;  // doubles per published diagonal block (15 + 6 + 6 + ok)
+// Block row I of S (its rows of L and rhs) belongs to work-group I % G for the whole
+// factorisation: its panel rows and trailing updates are computed there, so L never crosses
+// work-groups and needs no L2 write-back. Per block column J one hand-off does, write-through
+// (st_wt / ld_wt, as the reduction partials): every work-group forms the panel rows of its own
+// active blocks (V = A_iJ L_JJ^-T, L_iJ = V D_J^-1, rhs updated), publishes V and raises its own
+// panel flag (one 128-byte line per work-group: no contended counter) to J + 1; then it stages
+// every active V row in LDS and updates its own rows. The diagonal blocks need no hand-off: every
+// work-group keeps a replica of each active block's diagonal block and rhs slice in LDS (slots
+// from a free ring, filled from S when the block enters the active set) and applies column J's
+// update to all of them from the staged V rows -- the same operands and operation order as the
+// owner's trailing update and panel, so the replicas equal the owner's values bit for bit -- and
+// then factors block J + 1 itself (one lane); the owner also writes that factor to the profile
+// for the backward solve. Every element sees the same operations in the same order as in
+// factor_solve_profile (identical results). V is double-buffered by column parity: a work-group
+// runs at most one column ahead of the slowest (it cannot pass column J + 1's panel flags before
+// every work-group has finished column J). Active block rows per column <= prof_na_cap(K) (their
+// V rows and replicas fit the LDS; host-computed na_max, else work-group 0 factors alone).
 
-// Wave 0: spin until every work-group's flag (pflag[32 g], one 128-byte line each) reaches target;
-// the same give-up rules as wait_word (progress = any flag moving).
+// Wave 0: spin until every work-group's flag (pflag[32 g], one 128-byte line each) reaches target.
+// False once the grid has given up (CTL_ERR), or when no flag moved for ~2^22 sleeps (raised here).
 __device__ bool wait_flags(const CoopWs& w, const int32_t* pflag, int32_t target) {
   const int lane = threadIdx.x & 63, G = gridDim.x;
   uint32_t spins = 0, polls = 0;
@@ -1121,59 +1199,34 @@ __device__ bool wait_flags(const CoopWs& w, const int32_t* pflag, int32_t target
   }
 }
 
-// Thread 0: spin until the word reaches target (relaxed device-scope loads, s_sleep back-off).
-// False once the grid has given up (CTL_ERR), or when nothing moved for ~2^22 sleeps (raised here).
-__device__ bool wait_word(const CoopWs& w, int idx, int32_t target) {
-  uint32_t spins = 0, polls = 0;
-  int32_t seen = -1;
-  for (;;) {
-    const int32_t v = __hip_atomic_load(&w.ctl[idx], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (v >= target) return true;
-    if (v != seen) {
-      seen = v;
-      spins = 0;
-    }
-    if (polls < 256) __builtin_amdgcn_s_sleep(1);
-    else __builtin_amdgcn_s_sleep(8);
-    polls++;
-    if ((++spins & 255u) == 0 && ctl_load(w, CTL_ERR)) return false;
-    if (spins > (1u << 22)) {
-      __hip_atomic_store(&w.ctl[CTL_ERR], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      return false;
-    }
-  }
+// factor_profile_grid's LDS in sh.S: ints -- two A_J lists [2][K], 8 counters, the own blocks'
+// list positions [K], pfirst [K], each block's replica slot [K], the free-slot ring [cap] -- then
+// doubles (16-byte aligned): block J's factor (32), the active V rows [36 cap], the own L_iJ rows
+// [36 cap], the replicas [27 cap] (diagonal block lower 21 + rhs 6).
+constexpr int kRep = 27;
+__device__ __forceinline__ int prof_ints_dw(int K, int cap) {
+  return (4 * (5 * K + 8 + cap + 6 * cap) + 15) / 16 * 2;  // + own rows' prow (low words)
 }
-
-// factor_profile_grid's LDS in sh.S: two A_J lists + 8 counters + the own-block positions + pfirst
-// (ints), then (16-byte aligned) two published blocks, the active V rows and the own L_iJ rows.
-__device__ __forceinline__ int prof_lists_dw(int K) { return (16 * K + 32 + 15) / 16 * 2; }
-// Active blocks per column whose V rows (36 doubles) and, at most as many, own L_iJ and V rows fit.
 __device__ __forceinline__ int prof_na_cap(int K) {
-  const int avail = (int)(sizeof(CoopShared::S) / 8) - prof_lists_dw(K) - 2 * kPubStride;
-  return avail > 0 ? avail / 108 : 0;
+  const int total = (int)(sizeof(CoopShared::S) / 8);
+  int cap = (total - 32 - (5 * K + 8) / 2 - 2) * 2 / (2 * (72 + kRep) + 7);
+  while (cap > 0 && prof_ints_dw(K, cap) + 32 + (72 + kRep) * cap > total) cap--;
+  return cap > 0 ? cap : 0;
 }
 
-// The 6x6 LDLT of diagonal block J (rows j0.. of the profile, already updated by every column
-// < J), its forward solve y, D^-1: one lane. Returns false on an exact zero pivot.
-__device__ bool diag_block(const CoopWs& w, int J, double* Lp, double* rhs, double* dg,
-                           double* idg) {
+// The 6x6 LDLT of a diagonal block (lower triangle A, 21 doubles row-major packed) with the
+// forward solve of its rhs slice y: strict lower L (15, by column c then row r < c, the order the
+// panel reads it), D^-1, D and the solved y in place. False on an exact zero pivot. Same
+// statements as factor_solve_profile's diag_factor.
+__device__ bool diag_ldlt(double (&A)[21], double (&y)[6], double (&rdg)[6]) {
 #pragma clang fp contract(fast)  // tolerance-compared FP64 path
-  const int64_t* prow = w.prow;
-  const int j0 = 6 * J;
-  double A[21], y[6];
-#pragma unroll
-  for (int r = 0; r < 6; r++) {
-    y[r] = rhs[j0 + r];
-#pragma unroll
-    for (int k = 0; k <= r; k++) A[r * (r + 1) / 2 + k] = Lp[prow[j0 + r] + j0 + k];
-  }
   bool good = true;
 #pragma unroll
   for (int c = 0; c < 6; c++) {
     const double d = A[c * (c + 3) / 2];
     good = good && d != 0.0;
     const double rd = d != 0.0 ? 1.0 / d : 0.0;
-    idg[j0 + c] = rd;
+    rdg[c] = rd;
     double l[6];
 #pragma unroll
     for (int r = c + 1; r < 6; r++) {
@@ -1188,72 +1241,100 @@ __device__ bool diag_block(const CoopWs& w, int J, double* Lp, double* rhs, doub
       for (int k = c + 1; k <= r; k++) A[r * (r + 1) / 2 + k] -= ld * l[k];
     }
   }
-#pragma unroll
-  for (int r = 0; r < 6; r++) {
-#pragma unroll
-    for (int k = 0; k < r; k++) Lp[prow[j0 + r] + j0 + k] = A[r * (r + 1) / 2 + k];
-    dg[j0 + r] = A[r * (r + 3) / 2];
-    rhs[j0 + r] = y[r];
-  }
   return good;
 }
 
-// One lane of block J's owner: factor it, publish (L_JJ, D_J^-1, y_J, ok) into slot J & 1, and
-// raise CTL_DFLAG to J + 1 once the hand-off has landed.
-__device__ void diag_publish(const CoopWs& w, int J, double* Lp, double* rhs, double* dg,
-                             double* idg, double* pub) {
-  const bool good = diag_block(w, J, Lp, rhs, dg, idg);
-  const int64_t* prow = w.prow;
-  const int j0 = 6 * J;
-  double* const slot = pub + (J & 1) * kPubStride;
-  int q = 0;
-#pragma unroll
-  for (int c = 1; c < 6; c++)
-#pragma unroll
-    for (int k = 0; k < c; k++) st_wt(slot + q++, Lp[prow[j0 + c] + j0 + k]);
-#pragma unroll
-  for (int c = 0; c < 6; c++) {
-    st_wt(slot + 15 + c, idg[j0 + c]);
-    st_wt(slot + 21 + c, rhs[j0 + c]);
-  }
-  st_wt(slot + 27, good ? 1.0 : 0.0);
-  vm_drain();
-  __hip_atomic_store(&w.ctl[CTL_DFLAG], J + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
 // Every work-group. Returns false (work-group-uniform, the same in every work-group) on a zero
-// pivot or when the grid gave up; CTL_DFLAG and the panel flags must be 0 on entry (zeroed
-// before the grid barrier that precedes it).
+// pivot or when the grid gave up; the panel flags must be 0 on entry (zeroed before the grid
+// barrier that precedes it).
 __device__ bool factor_profile_grid(CoopShared& sh, const CoopWs& w, int K, double* Lp,
                                     double* rhs, double* dg, double* idg, double* Vg0,
-                                    double* Vg1, double* pub, int32_t* pflag) {
+                                    double* Vg1, int32_t* pflag) {
 #pragma clang fp contract(fast)  // tolerance-compared FP64 path
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int tid = threadIdx.x, wid = tid >> 6;
   const int G = gridDim.x, wg = blockIdx.x;
   const int64_t* prow = w.prow;
   const int32_t* pfirst = w.pfirst;
-  // LDS (the unused dense factor storage): A_J lists (two buffers) + counts, the own active
-  // blocks' list positions, column J's published block, the active V rows, the own L_iJ rows
+  const int cap = prof_na_cap(K);
   int* const lists = reinterpret_cast<int*>(sh.S);
-  int* const cnt = lists + 2 * K;  // [0], [1]: list sizes; [2]: own count; [3]: ok; [4]: the
-                                   // next column's block already staged
-  int* const own = cnt + 8;        // [K]
+  int* const cnt = lists + 2 * K;  // [0], [1]: list sizes; [2]: own count; [3]: flags seen;
+                                   // [4]: free-ring pops; [5]: free-ring pushes; [6]: entering
+  int* const own = cnt + 8;        // [K] (the blocks entering A_{J+1} after the own ones)
   int* const spf = own + K;        // [K] pfirst
-  double* const pdb = sh.S + prof_lists_dw(K);  // [2][kPubStride] published blocks, by parity
-  double* const sV = pdb + 2 * kPubStride;  // [36 * na] V rows of the active blocks, list order
-  // own L_iJ rows: after sV, sized by the caller's cap (6 * 6 per own block, <= na blocks)
-  const int na_cap = prof_na_cap(K);
-  double* const sL = sV + 36 * (size_t)na_cap;   // [36 * no] own L_iJ rows
-  double* const sVo = sL + 36 * (size_t)na_cap;  // [36 * no] own V rows (the look-ahead's)
+  int* const slot_of = spf + K;    // [K]
+  int* const ring = slot_of + K;   // [cap]
+  int* const sro = ring + cap;     // [6 cap] prow of the own active rows (32-bit: pnnz < 2^31)
+  double* const pd = sh.S + prof_ints_dw(K, cap);  // L_JJ 15, D_J^-1 6, y_J 6, ok
+  double* const sV = pd + 32;                      // [36 cap] active V rows, list order
+  double* const sL = sV + 36 * (size_t)cap;        // [36 cap] own L_iJ rows
+  double* const rep = sL + 36 * (size_t)cap;       // [kRep cap] replicas
+  double* const nx = sh.V;  // block J + 1's initial diagonal block when it was never active
+  // block I's diagonal block and rhs slice before any update: from S and the reduced rhs (never
+  // written during the factorisation -- the profile copy is: its owner may already be a column
+  // ahead), with build_S_profile's I / 0 for a keyframe left without active edges
+  auto initial = [&](int I, double* A, double* y) {
+    const int i0 = 6 * I;
+    const bool act_kf = kf_active(w, I);
+#pragma unroll
+    for (int r = 0; r < 6; r++) {
+#pragma unroll
+      for (int c = 0; c <= r; c++)
+        A[r * (r + 1) / 2 + c] = (!act_kf && c == r) ? 1.0 : w.S[prow[i0 + r] + i0 + c];
+      y[r] = act_kf ? w.bs[i0 + r] : 0.0;
+    }
+  };
+  // a block entering the active set: a free slot holding its initial diagonal block and rhs
+  auto enter = [&](int I) {
+    const int sl = ring[atomicAdd(&cnt[4], 1) % cap];
+    slot_of[I] = sl;
+    double* R = rep + (size_t)sl * kRep;
+    initial(I, R, R + 21);
+  };
+  // thread 0: factor block J from A / y into pd; its owner also writes the factor to the profile
+  auto factor_block = [&](int J, double (&A)[21], double (&y)[6]) {
+    double rdg[6];
+    const bool good = diag_ldlt(A, y, rdg);
+    int q = 0;
+#pragma unroll
+    for (int c = 1; c < 6; c++)
+#pragma unroll
+      for (int k = 0; k < c; k++) pd[q++] = A[c * (c + 1) / 2 + k];
+#pragma unroll
+    for (int c = 0; c < 6; c++) {
+      pd[15 + c] = rdg[c];
+      pd[21 + c] = y[c];
+    }
+    pd[27] = good ? 1.0 : 0.0;
+    if (J % G == wg) {
+      const int j0 = 6 * J;
+#pragma unroll
+      for (int r = 0; r < 6; r++) {
+#pragma unroll
+        for (int k = 0; k < r; k++) Lp[prow[j0 + r] + j0 + k] = A[r * (r + 1) / 2 + k];
+        dg[j0 + r] = A[r * (r + 3) / 2];
+        idg[j0 + r] = rdg[r];
+        rhs[j0 + r] = y[r];
+      }
+    }
+  };
   if (tid == 0) {
     cnt[0] = 0;
     cnt[4] = 0;
+    cnt[5] = cap;
   }
   for (int I = tid; I < K; I += kT) spf[I] = pfirst[I];
+  for (int q = tid; q < cap; q += kT) ring[q] = q;
   __syncthreads();
   for (int I = 1 + tid; I < K; I += kT)  // A_0
-    if (spf[I] <= 0) lists[atomicAdd(&cnt[0], 1)] = I;
-  if (wg == 0 && tid == 0) diag_publish(w, 0, Lp, rhs, dg, idg, pub);
+    if (spf[I] <= 0) {
+      lists[atomicAdd(&cnt[0], 1)] = I;
+      enter(I);
+    }
+  if (tid == 0 && K > 0) {  // block 0: no update before column 0
+    double A[21], y[6];
+    initial(0, A, y);
+    factor_block(0, A, y);
+  }
   __syncthreads();
   bool ok = true;
 #if FS_PROF  // diagnostic build: thread 0 of work-group 0 splits each column into prof[8..12]
@@ -1276,28 +1357,24 @@ __device__ bool factor_profile_grid(CoopShared& sh, const CoopWs& w, int K, doub
     int* nxt = lists + ((J + 1) & 1) * K;
     const int na = cnt[J & 1], nr = 6 * na;
     double* const Vp = (J & 1) ? Vg1 : Vg0;
-    double* const pd = pdb + (J & 1) * kPubStride;
-    // ---- column J's diagonal block from its owner (staged during column J - 1 when it was out)
-    const bool staged = cnt[4] != 0;
-    __syncthreads();
-    if (tid == 0) {
-      cnt[2] = 0;
-      cnt[3] = staged || wait_word(w, CTL_DFLAG, J + 1) ? 1 : 0;
-    }
-    __syncthreads();
-    if (!cnt[3]) {
-      ok = false;
-      break;
-    }
-    if (!staged && tid < 28) pd[tid] = ld_wt(pub + (J & 1) * kPubStride + tid);
-    for (int t = tid; t < na; t += kT)  // own active blocks (any order)
-      if (act[t] % G == wg) own[atomicAdd(&cnt[2], 1)] = t;
-    __syncthreads();
     if (pd[27] == 0.0) {  // zero pivot: every work-group stops at this column
       ok = false;
       break;
     }
-    const int no = cnt[2], nro = 6 * no;
+    if (tid == 0) {
+      cnt[2] = 0;
+      cnt[6] = 0;
+      cnt[(J + 1) & 1] = 0;  // A_{J+1}'s size (A_{J-1} is no longer read)
+      if (J > 0 && spf[J] < J) {  // block J's replica (read when it was factored) is free now
+        ring[cnt[5] % cap] = slot_of[J];
+        cnt[5]++;
+      }
+    }
+    __syncthreads();
+    for (int t = tid; t < na; t += kT)  // own active blocks (any order)
+      if (act[t] % G == wg) own[atomicAdd(&cnt[2], 1)] = t;
+    __syncthreads();
+    const int nro = 6 * cnt[2];
     gtick(0);
     // ---- panel rows of the own active blocks (forward solve fused); V published, L_iJ kept
     {
@@ -1311,7 +1388,9 @@ __device__ bool factor_profile_grid(CoopShared& sh, const CoopWs& w, int K, doub
       }
       for (int t = tid; t < nro; t += kT) {
         const int i = 6 * act[own[t / 6]] + t % 6;
-        const int64_t ro = prow[i] + j0;
+        const int64_t pr = prow[i];
+        sro[t] = (int)pr;
+        const int64_t ro = pr + j0;
         double v[6];
         int q = 0;
 #pragma unroll
@@ -1325,7 +1404,6 @@ __device__ bool factor_profile_grid(CoopShared& sh, const CoopWs& w, int K, doub
 #pragma unroll
         for (int c = 0; c < 6; c++) {
           st_wt(Vp + (size_t)i * 6 + c, v[c]);
-          sVo[t * 6 + c] = v[c];
           const double l = v[c] * rdg[c];
           Lp[ro + c] = l;
           sL[t * 6 + c] = l;
@@ -1338,37 +1416,22 @@ __device__ bool factor_profile_grid(CoopShared& sh, const CoopWs& w, int K, doub
     __syncthreads();
     if (tid == 0)  // this work-group's panel of column J is out (its own 128-byte line)
       __hip_atomic_store(&pflag[32 * wg], J + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    gtick(1);
-    // ---- look-ahead: block J + 1's owner updates it by column J and publishes its LDLT
-    const bool next_active = J + 1 < K && spf[J + 1] <= J;
-    if (J + 1 < K && (J + 1) % G == wg && wid == 0) {
-      if (next_active && lane < 21) {
-        int a1 = 0;  // block J + 1 among the own active blocks
-        while (act[own[a1]] != J + 1) a1++;
-        int r = 0;
-        while ((r + 1) * (r + 2) / 2 <= lane) r++;
-        const int c = lane - r * (r + 1) / 2;
-        const int i = j0 + 6 + r, k = j0 + 6 + c;
-        const int64_t ro = prow[i];
-        double sv = Lp[ro + k];
-#pragma unroll
-        for (int m = 0; m < 6; m++) sv -= Lp[ro + j0 + m] * sVo[(6 * a1 + c) * 6 + m];
-        Lp[ro + k] = sv;
-      }
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-      if (lane == 0) diag_publish(w, J + 1, Lp, rhs, dg, idg, pub);
+    // while the other panels arrive: the blocks entering A_{J+1} take slots and their initial
+    // diagonal blocks (own[] past the own blocks lists them), and block J + 1's when it was never
+    // active
+    if (wid > 0) {
+      for (int I = J + 2 + tid - 64; I < K; I += kT - 64)
+        if (spf[I] == J + 1) {
+          own[cnt[2] + atomicAdd(&cnt[6], 1)] = I;
+          enter(I);
+        }
+      if (tid == 64 && J + 1 < K && spf[J + 1] > J) initial(J + 1, nx, nx + 21);
     }
-    // ---- every panel of column J, then the trailing update of the own rows outside block J + 1
+    gtick(1);
+    // ---- every panel of column J: the active V rows to LDS
     if (wid == 0) {
       const bool got = wait_flags(w, pflag, J + 1);
       if (tid == 0) cnt[3] = got ? 1 : 0;
-    }
-    if (tid == 0) {
-      // column J + 1's block, when already published, staged beside this column's V rows
-      cnt[4] = J + 1 < K && __hip_atomic_load(&w.ctl[CTL_DFLAG], __ATOMIC_RELAXED,
-                                              __HIP_MEMORY_SCOPE_AGENT) >= J + 2;
     }
     __syncthreads();
     if (!cnt[3]) {
@@ -1376,30 +1439,85 @@ __device__ bool factor_profile_grid(CoopShared& sh, const CoopWs& w, int K, doub
       break;
     }
     gtick(2);
-    if (cnt[4] && tid >= kT - 28)
-      pdb[((J + 1) & 1) * kPubStride + tid - (kT - 28)] =
-          ld_wt(pub + ((J + 1) & 1) * kPubStride + tid - (kT - 28));
-    for (int q = tid; q < 36 * na; q += kT) {  // V rows of the active blocks, list order
+    for (int q = tid; q < 36 * na; q += kT) {
       const int t = q / 6, c = q - 6 * t;
       sV[q] = ld_wt(Vp + (size_t)(6 * act[t / 6] + t % 6) * 6 + c);
     }
     __syncthreads();
+    // ---- trailing update of the own rows, and column J's update of every replica
     for (int p = tid; p < nro * nr; p += kT) {
       const int a = p / nr, m = p - a * nr;
       const int i = 6 * act[own[a / 6]] + a % 6;
       const int k = 6 * act[m / 6] + m % 6;
-      if (k > i || i < j0 + 12) continue;  // upper part; block J + 1 is its owner's look-ahead
-      const int64_t ro = prow[i];
+      if (k > i) continue;
+      const int64_t ro = sro[a];
       double sv = Lp[ro + k];
 #pragma unroll
       for (int c = 0; c < 6; c++) sv -= sL[a * 6 + c] * sV[m * 6 + c];
       Lp[ro + k] = sv;
     }
-    if (tid == 0) cnt[(J + 1) & 1] = 0;
+    {
+      double rdg[6], yj[6];
+#pragma unroll
+      for (int c = 0; c < 6; c++) {
+        rdg[c] = pd[15 + c];
+        yj[c] = pd[21 + c];
+      }
+      for (int q = tid; q < kRep * na; q += kT) {
+        const int t = q / kRep, e = q - kRep * t;
+        double* R = rep + (size_t)slot_of[act[t]] * kRep;
+        if (e < 21) {  // diagonal entry (r, c): -= L(row r) V(row c)^T
+          int r = 0;
+          while ((r + 1) * (r + 2) / 2 <= e) r++;
+          const int c = e - r * (r + 1) / 2;
+          const double* vr = sV + (6 * t + r) * 6;
+          const double* vc = sV + (6 * t + c) * 6;
+          double sv = R[e];
+#pragma unroll
+          for (int m = 0; m < 6; m++) sv -= (vr[m] * rdg[m]) * vc[m];
+          R[e] = sv;
+        } else {  // rhs row r: -= L(row r) y_J
+          const double* vr = sV + (6 * t + e - 21) * 6;
+          double sv = R[e];
+#pragma unroll
+          for (int m = 0; m < 6; m++) {
+            const double l = vr[m] * rdg[m];
+            sv -= l * yj[m];
+          }
+          R[e] = sv;
+        }
+      }
+    }
     __syncthreads();
     gtick(3);
-    for (int I = J + 2 + tid; I < K; I += kT)  // A_{J+1}
-      if (spf[I] <= J + 1) nxt[atomicAdd(&cnt[(J + 1) & 1], 1)] = I;
+    // ---- block J + 1: factor its replica (or the untouched profile when it was never active),
+    // release its slot; then A_{J+1}, slots for the blocks entering it
+    if (J + 1 < K) {
+      const bool was_active = spf[J + 1] <= J;
+      if (tid == 0) {  // (its slot is recycled at the start of column J + 1: the blocks entering
+                       // A_{J+1} below take slots while this lane still reads it)
+        double A[21], y[6];
+        if (was_active) {
+          const double* R = rep + (size_t)slot_of[J + 1] * kRep;
+#pragma unroll
+          for (int e = 0; e < 21; e++) A[e] = R[e];
+#pragma unroll
+          for (int r = 0; r < 6; r++) y[r] = R[21 + r];
+        } else {
+#pragma unroll
+          for (int e = 0; e < 21; e++) A[e] = nx[e];
+#pragma unroll
+          for (int r = 0; r < 6; r++) y[r] = nx[21 + r];
+        }
+        factor_block(J + 1, A, y);
+      }
+      // A_{J+1} = A_J without block J + 1, and the entering blocks
+      const int no = cnt[2], ne = cnt[6];
+      for (int t = tid; t < na + ne; t += kT) {
+        const int I = t < na ? act[t] : own[no + t - na];
+        if (I != J + 1) nxt[atomicAdd(&cnt[(J + 1) & 1], 1)] = I;
+      }
+    }
     __syncthreads();
     gtick(4);
   }
@@ -1529,8 +1647,8 @@ __global__ __launch_bounds__(kT) void ba_coop_kernel(PoseParams P, CoopProblem p
   double* const Gr = Gd + n;
   double* const Gi = Gr + n;
   double* const Gv2 = Gi + n;            // the grid factorisation's second V buffer
-  double* const Gpub = Gv2 + (size_t)6 * n;  // and its two published diagonal blocks
-  int32_t* const Gflag = reinterpret_cast<int32_t*>(Gpub + 64);  // panel flags, 128 B apart
+  // the grid factorisation's panel flags, 128 bytes apart (after 64 spare doubles)
+  int32_t* const Gflag = reinterpret_cast<int32_t*>(Gv2 + (size_t)6 * n + 64);
   // the profile LDLT over the whole grid when the active V rows fit the LDS (host: na_max)
   const bool grid_factor = !in_lds && w.mwg && gridDim.x > 1 && w.na_max <= prof_na_cap(K);
   // optional per-phase wall clock of work-group 0 (s_memrealtime: 100 MHz)
@@ -1619,13 +1737,12 @@ __global__ __launch_bounds__(kT) void ba_coop_kernel(PoseParams P, CoopProblem p
       if (grid_factor) {  // the profile LDLT over every work-group, then work-group 0 solves
         if (wg == 0) {
           build_S_profile(w, K, Gp, Gr);
-          if (tid == 0) w.ctl[CTL_DFLAG] = 0;
           for (int g = tid; g < (int)gridDim.x; g += kT)
             __hip_atomic_store(&Gflag[32 * g], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
         tick(5);
         grid_sync(w, stop_flag, false);
-        const bool fok = factor_profile_grid(sh, w, K, Gp, Gr, Gd, Gi, Gv, Gv2, Gpub, Gflag);
+        const bool fok = factor_profile_grid(sh, w, K, Gp, Gr, Gd, Gi, Gv, Gv2, Gflag);
         grid_sync(w, stop_flag, false);
         if (wg == 0) {
           if (tid == 0) sh.ok = fok ? 1 : 0;

@@ -360,18 +360,24 @@ int coop_host(const char* what, const slamgpu_camera* cam, const float* inv_sigm
       if (f >= 0 && mn < pfirst[f]) pfirst[f] = mn;
     }
   }
-  // active block rows of block column J: {I > J : pfirst[I] <= J} (I contributes to J in
-  // [pfirst[I], I - 1]); the grid factorisation stages their V rows in LDS
+  // active block rows of block column J: A_J = {I > J : pfirst[I] <= J} (I contributes to J in
+  // [pfirst[I], I - 1]); the grid factorisation stages their V rows in LDS and keeps a replica of
+  // each one's diagonal block, plus those of the blocks entering A_{J+1} and one being recycled:
+  // na_max = max_J |A_J| + |{I > J + 1 : pfirst[I] = J + 1}| + 1 slots
   int na_max = 0;
   {
-    std::vector<int32_t> d((size_t)K + 1, 0);
+    std::vector<int32_t> d((size_t)K + 1, 0), enter((size_t)K + 1, 0);
     for (int f = 0; f < K; f++)
       if (pfirst[f] < f) {
         d[pfirst[f]]++;
         d[f]--;
+        if (pfirst[f] >= 1 && f > pfirst[f]) enter[pfirst[f]]++;
       }
     int run = 0;
-    for (int j = 0; j < K; j++) na_max = std::max(na_max, run += d[j]);
+    for (int j = 0; j < K; j++) {
+      run += d[j];
+      na_max = std::max(na_max, run + (j + 1 < K ? enter[j + 1] : 0) + 1);
+    }
   }
   std::vector<int64_t> prow(6 * (size_t)K);
   int64_t pnnz = 0;
