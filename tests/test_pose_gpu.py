@@ -118,8 +118,10 @@ def test_pose_optimization_device_batch_matches_oracle(oracle, gpu_lib):
     # The LM iteration count is no output of the reference. Once a round has converged, rho and
     # the nBad test ((iniChi - currentChi) * 1e3 < iniChi) compare chi2 differences at rounding
     # level, so the tree sums may end a round an iteration earlier or later (a step of ~0);
-    # the bulk of the frames must still follow the oracle's schedule exactly.
-    assert same_its >= 0.75 * B, f"{same_its}/{B} frames ran the oracle's LM iteration count"
+    # the bulk of the frames must still follow the oracle's schedule exactly. Measured on MI355X
+    # (deterministic: seeded problems, fixed reduction trees): 65 of 74 frames (0.88), r3zh.
+    print(f"pose batch: {same_its}/{B} frames ran the oracle's LM iteration count")
+    assert same_its >= 0.85 * B, f"{same_its}/{B} frames ran the oracle's LM iteration count"
 
 
 def test_pose_optimization_device_over_capacity(gpu_lib):
