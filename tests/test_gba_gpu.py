@@ -82,7 +82,7 @@ def test_global_ba_stop_before_start(oracle, gpu_lib):
     assert np.array_equal(kf, kf_o) and np.array_equal(pts, pts_o)
 
 
-@pytest.mark.parametrize("n_kf", [300, 1500])
+@pytest.mark.parametrize("n_kf", [300, 1500, 2000])  # 2000: z past the back-solve LDS
 def test_global_ba_map_scale_loop(oracle, gpu_lib, n_kf):
     """A map-scale global BA after a loop closure (GlobalBundleAdjustemnt passes every keyframe,
     optimizer.cpp:18-31): a closed loop of n_kf keyframes (synthetic.map_problem: ~38 points and
