@@ -1272,27 +1272,29 @@ __device__ bool factor_profile_grid(CoopShared& sh, const CoopWs& w, int K, doub
   // block I's diagonal block and rhs slice before any update: from S and the reduced rhs (never
   // written during the factorisation -- the profile copy is: its owner may already be a column
   // ahead), with build_S_profile's I / 0 for a keyframe left without active edges
-  auto initial = [&](int I, double* A, double* y) {
+  // entry e of that image (e < 21: lower (r, c) of the diagonal block; 21 + r: rhs row r), one
+  // lane per entry (a whole block per lane would hold 27 loads in flight in this register-bound
+  // kernel)
+  auto initial = [&](int I, int e) -> double {
     const int i0 = 6 * I;
     const bool act_kf = kf_active(w, I);
-#pragma unroll
-    for (int r = 0; r < 6; r++) {
-#pragma unroll
-      for (int c = 0; c <= r; c++)
-        A[r * (r + 1) / 2 + c] = (!act_kf && c == r) ? 1.0 : w.S[prow[i0 + r] + i0 + c];
-      y[r] = act_kf ? w.bs[i0 + r] : 0.0;
-    }
+    if (e >= 21) return act_kf ? w.bs[i0 + e - 21] : 0.0;
+    int r = 0;
+    while ((r + 1) * (r + 2) / 2 <= e) r++;
+    const int c = e - r * (r + 1) / 2;
+    return (!act_kf && c == r) ? 1.0 : w.S[prow[i0 + r] + i0 + c];
   };
-  // a block entering the active set: a free slot holding its initial diagonal block and rhs
-  auto enter = [&](int I) {
-    const int sl = ring[atomicAdd(&cnt[4], 1) % cap];
-    slot_of[I] = sl;
-    double* R = rep + (size_t)sl * kRep;
-    initial(I, R, R + 21);
-  };
-  // thread 0: factor block J from A / y into pd; its owner also writes the factor to the profile
-  auto factor_block = [&](int J, double (&A)[21], double (&y)[6]) {
-    double rdg[6];
+  // a block entering the active set takes a free slot (filled by initial())
+  auto take_slot = [&](int I) { slot_of[I] = ring[atomicAdd(&cnt[4], 1) % cap]; };
+  // thread 0: factor block J from its (updated) diagonal block and rhs slice at src (LDS: 21 + 6)
+  // into pd; its owner also writes the factor to the profile. One call site (register pressure:
+  // this kernel holds every phase of the solver)
+  auto factor_block = [&](int J, const double* src) {
+    double A[21], y[6], rdg[6];
+#pragma unroll
+    for (int e = 0; e < 21; e++) A[e] = src[e];
+#pragma unroll
+    for (int r = 0; r < 6; r++) y[r] = src[21 + r];
     const bool good = diag_ldlt(A, y, rdg);
     int q = 0;
 #pragma unroll
@@ -1328,13 +1330,14 @@ __device__ bool factor_profile_grid(CoopShared& sh, const CoopWs& w, int K, doub
   for (int I = 1 + tid; I < K; I += kT)  // A_0
     if (spf[I] <= 0) {
       lists[atomicAdd(&cnt[0], 1)] = I;
-      enter(I);
+      take_slot(I);
     }
-  if (tid == 0 && K > 0) {  // block 0: no update before column 0
-    double A[21], y[6];
-    initial(0, A, y);
-    factor_block(0, A, y);
+  __syncthreads();
+  for (int q = tid; q < kRep * cnt[0]; q += kT) {
+    const int I = lists[q / kRep], e = q % kRep;
+    rep[(size_t)slot_of[I] * kRep + e] = initial(I, e);
   }
+  if (tid < kRep && K > 0) nx[tid] = initial(0, tid);  // block 0: no update before column 0
   __syncthreads();
   bool ok = true;
 #if FS_PROF  // diagnostic build: thread 0 of work-group 0 splits each column into prof[8..12]
@@ -1357,20 +1360,24 @@ __device__ bool factor_profile_grid(CoopShared& sh, const CoopWs& w, int K, doub
     int* nxt = lists + ((J + 1) & 1) * K;
     const int na = cnt[J & 1], nr = 6 * na;
     double* const Vp = (J & 1) ? Vg1 : Vg0;
+    if (tid == 0) {
+      // block J: its replica (it was active in A_{J-1}), or its initial values staged in nx;
+      // then its slot goes back to the ring
+      const bool was_active = J > 0 && spf[J] < J;
+      factor_block(J, was_active ? rep + (size_t)slot_of[J] * kRep : nx);
+      if (was_active) {
+        ring[cnt[5] % cap] = slot_of[J];
+        cnt[5]++;
+      }
+      cnt[2] = 0;
+      cnt[6] = 0;
+      cnt[(J + 1) & 1] = 0;  // A_{J+1}'s size (A_{J-1} is no longer read)
+    }
+    __syncthreads();
     if (pd[27] == 0.0) {  // zero pivot: every work-group stops at this column
       ok = false;
       break;
     }
-    if (tid == 0) {
-      cnt[2] = 0;
-      cnt[6] = 0;
-      cnt[(J + 1) & 1] = 0;  // A_{J+1}'s size (A_{J-1} is no longer read)
-      if (J > 0 && spf[J] < J) {  // block J's replica (read when it was factored) is free now
-        ring[cnt[5] % cap] = slot_of[J];
-        cnt[5]++;
-      }
-    }
-    __syncthreads();
     for (int t = tid; t < na; t += kT)  // own active blocks (any order)
       if (act[t] % G == wg) own[atomicAdd(&cnt[2], 1)] = t;
     __syncthreads();
@@ -1419,13 +1426,26 @@ __device__ bool factor_profile_grid(CoopShared& sh, const CoopWs& w, int K, doub
     // while the other panels arrive: the blocks entering A_{J+1} take slots and their initial
     // diagonal blocks (own[] past the own blocks lists them), and block J + 1's when it was never
     // active
-    if (wid > 0) {
-      for (int I = J + 2 + tid - 64; I < K; I += kT - 64)
-        if (spf[I] == J + 1) {
-          own[cnt[2] + atomicAdd(&cnt[6], 1)] = I;
-          enter(I);
+    if (wid > 0) {  // each wave fills the blocks its lanes found, one entry per lane
+      const int lane = tid & 63;
+      for (int I0 = J + 2 + (wid - 1) * 64; I0 < K; I0 += kT - 64) {
+        const int I = I0 + lane;
+        uint64_t found = __ballot(I < K && spf[I] == J + 1);
+        while (found) {
+          const int b = __ffsll((long long)found) - 1;
+          found &= found - 1;
+          const int Ib = __builtin_amdgcn_readlane(I, b);
+          if (lane == b) {
+            own[cnt[2] + atomicAdd(&cnt[6], 1)] = Ib;
+            take_slot(Ib);
+          }
+          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+          __builtin_amdgcn_wave_barrier();
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+          if (lane < kRep) rep[(size_t)slot_of[Ib] * kRep + lane] = initial(Ib, lane);
         }
-      if (tid == 64 && J + 1 < K && spf[J + 1] > J) initial(J + 1, nx, nx + 21);
+      }
+      if (wid == 1 && J + 1 < K && spf[J + 1] > J && lane < kRep) nx[lane] = initial(J + 1, lane);
     }
     gtick(1);
     // ---- every panel of column J: the active V rows to LDS
@@ -1490,28 +1510,9 @@ __device__ bool factor_profile_grid(CoopShared& sh, const CoopWs& w, int K, doub
     }
     __syncthreads();
     gtick(3);
-    // ---- block J + 1: factor its replica (or the untouched profile when it was never active),
-    // release its slot; then A_{J+1}, slots for the blocks entering it
+    // ---- A_{J+1} = A_J without block J + 1, and the entering blocks (block J + 1 is factored at
+    // the start of the next column)
     if (J + 1 < K) {
-      const bool was_active = spf[J + 1] <= J;
-      if (tid == 0) {  // (its slot is recycled at the start of column J + 1: the blocks entering
-                       // A_{J+1} below take slots while this lane still reads it)
-        double A[21], y[6];
-        if (was_active) {
-          const double* R = rep + (size_t)slot_of[J + 1] * kRep;
-#pragma unroll
-          for (int e = 0; e < 21; e++) A[e] = R[e];
-#pragma unroll
-          for (int r = 0; r < 6; r++) y[r] = R[21 + r];
-        } else {
-#pragma unroll
-          for (int e = 0; e < 21; e++) A[e] = nx[e];
-#pragma unroll
-          for (int r = 0; r < 6; r++) y[r] = nx[21 + r];
-        }
-        factor_block(J + 1, A, y);
-      }
-      // A_{J+1} = A_J without block J + 1, and the entering blocks
       const int no = cnt[2], ne = cnt[6];
       for (int t = tid; t < na + ne; t += kT) {
         const int I = t < na ? act[t] : own[no + t - na];
