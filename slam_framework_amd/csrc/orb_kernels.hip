@@ -2430,6 +2430,16 @@ __device__ __forceinline__ int reduce_scatter16(int (&v)[16], int lane) {
 #define PAT_PACKED 1
 #endif
 constexpr int kRtCols = 40, kRtRows = RT_ROWS;  // u16 per transposed column (even)
+// OD_SHIFTED: a second copy of the row-sum table shifted by one u16 (copy1[i] = copy0[i + 1]), so
+// that a sample whose 7 rows start at an odd u16 reads 4 aligned dwords of copy1 instead of
+// realigning copy0's with 4 v_alignbit: one extra ds_write_b16 per stored row sum (an immediate
+// offset) for 4-5 fewer VALU per sample. Bit-exact, but slower: 1.02 -> 1.11 ms per step at 4
+// waves/SIMD (profiles/r3zs_orient_desc_shifted_ab.log; twice the LDS stores per row sum), so off.
+#ifndef OD_SHIFTED
+#define OD_SHIFTED 0
+#endif
+constexpr int kRtN = kRtCols * kRtRows;  // u16 per copy
+constexpr int kRtCopy1 = kRtN + 2;       // copy1's u16 offset (dword-aligned; copy1[-1] is spare)
 
 __device__ __forceinline__ uint32_t rt_tap(const uint16_t* rt, int sy, int sx, uint32_t K01,
                                            uint32_t K23, uint32_t K21, uint32_t K0) {
@@ -2444,6 +2454,9 @@ __device__ __forceinline__ uint32_t rt_tap(const uint16_t* rt, int sy, int sx, u
   return dot2u(p0, K01, dot2u(p1, K23, dot2u(p2, K21, dot2u(p3, K0, 0u))));
 }
 
+#if OD_SHIFTED && !defined(OD_WAVES)
+#define OD_WAVES 4  // 131 VGPRs unbounded (3 waves/SIMD); 127 at this bound, no spills
+#endif
 #ifdef OD_WAVES
 #define OD_ATTR __attribute__((amdgpu_waves_per_eu(OD_WAVES)))
 #else
@@ -2456,7 +2469,8 @@ __global__ __launch_bounds__(256) OD_ATTR void orient_desc_kernel(
     ImageBatch b, const OrbGeom* __restrict__ g, const uint32_t* __restrict__ oct_keys,
     const int* __restrict__ oct_count, KeyPoint* __restrict__ kps, uint8_t* __restrict__ desc,
     int* __restrict__ nkps) {
-  __shared__ __attribute__((aligned(16))) uint16_t s_rt[4][1][kRtCols * kRtRows];
+  static_assert(!OD_SHIFTED || (!OD_PAIRS && !OD_MFMA), "the shifted copy takes the u16 stores");
+  __shared__ __attribute__((aligned(16))) uint16_t s_rt[4][1][OD_SHIFTED ? kRtCopy1 + kRtN : kRtN];
   int img, bx;
   xcd_image_block(&img, &bx);
   const int lane = threadIdx.x & 63, wid = wave_id();
@@ -2778,7 +2792,10 @@ __global__ __launch_bounds__(256) OD_ATTR void orient_desc_kernel(
           rtw32[(4 * gq + jx) * (kRtRows / 2) + (r >> 1)] = (R[0][jx] & 0xffffu) | R[1][jx] << 16;
 #else
 #pragma unroll
-        for (int jx = 0; jx < 4; jx++) rtw[(4 * gq + jx) * kRtRows + r] = (uint16_t)R[0][jx];
+        for (int jx = 0; jx < 4; jx++) {
+          rtw[(4 * gq + jx) * kRtRows + r] = (uint16_t)R[0][jx];
+          if (OD_SHIFTED) rtw[kRtCopy1 - 1 + (4 * gq + jx) * kRtRows + r] = (uint16_t)R[0][jx];
+        }
 #endif
       }
     }
@@ -2820,6 +2837,11 @@ __global__ __launch_bounds__(256) OD_ATTR void orient_desc_kernel(
             const uint32_t cy = __float_as_uint(sp.x) - 0x4B400000u;  // window row of sy - 3
             const uint32_t cx = __float_as_uint(sp.y) - 0x4B400000u;  // window column
             const uint32_t e0 = __umul24(cx, (uint32_t)kRtRows) + cy;
+#if OD_SHIFTED
+            // an odd start (cy odd: kRtRows is even) reads copy1 at the same dword index
+            const uint32_t* rw = rt32 + (e0 >> 1) + (cy & 1u) * (uint32_t)(kRtCopy1 / 2);
+            const uint32_t p0 = rw[0], p1 = rw[1], p2 = rw[2], p3 = rw[3];  // p3's high u16 x 0
+#else
             const uint32_t* rw = rt32 + (e0 >> 1);
             const uint32_t sh = cy << 4;  // alignbit takes it mod 32: 16 for an odd start
             const uint32_t w0 = rw[0], w1 = rw[1], w2 = rw[2], w3 = rw[3];
@@ -2827,6 +2849,7 @@ __global__ __launch_bounds__(256) OD_ATTR void orient_desc_kernel(
             const uint32_t p1 = __builtin_amdgcn_alignbit(w2, w1, sh);
             const uint32_t p2 = __builtin_amdgcn_alignbit(w3, w2, sh);
             const uint32_t p3 = __builtin_amdgcn_alignbit(0u, w3, sh);
+#endif
             const uint32_t sm = dot2u(p0, K01, dot2u(p1, K23, dot2u(p2, K21, dot2u(p3, K0, 0u))));
             uint32_t o;
             if (kTail) {
