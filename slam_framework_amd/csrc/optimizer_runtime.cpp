@@ -428,11 +428,12 @@ int coop_host(const char* what, const slamgpu_camera* cam, const float* inv_sigm
   w.prow = reinterpret_cast<const int64_t*>(b + o_prow);
   if (!prof) w.prof = nullptr;
   w.na_max = na_max;
-  {  // the grid factorisation pays ~12 us of hand-offs per block column: below ~40 keyframes
-     // work-group 0 alone is faster (bench: 30 keyframes 4.6 vs 5.6 ms; 54: 16.1 vs 13.1 ms)
+  {  // the grid factorisation wherever S takes the profile path (6K > 144): the one-hand-off
+     // version beats work-group 0 alone from there on (30 keyframes 4.5 -> 3.7 ms, 54: 13.1 ->
+     // 8.8 ms); SLAMGPU_GBA_MWG=0 / SLAMGPU_GBA_MWG_MIN_KF select work-group 0 for A/B
     const char* e0 = getenv("SLAMGPU_GBA_MWG");  // read per call: tests switch both paths
     const char* e1 = getenv("SLAMGPU_GBA_MWG_MIN_KF");
-    const int mwg_env = e0 ? atoi(e0) : 1, mwg_min = e1 ? atoi(e1) : 40;
+    const int mwg_env = e0 ? atoi(e0) : 1, mwg_min = e1 ? atoi(e1) : 0;
     w.mwg = mwg_env && K >= mwg_min;
   }
   const CoopProblem pb{reinterpret_cast<const slamgpu_ba_obs*>(b + o_obs),

@@ -43,12 +43,14 @@ def test_global_ba_matches_oracle(oracle, gpu_lib, seed, nkf, npt, robust, iters
 
 @pytest.mark.parametrize("mwg,min_kf,seed,nkf,npt", [("1", "0", 37, 30, 4000),
                                                      ("1", "0", 38, 26, 3000),
-                                                     ("0", "40", 39, 60, 6000)])
+                                                     ("0", "0", 39, 60, 6000),
+                                                     ("1", "40", 40, 30, 4000)])
 def test_global_ba_both_profile_factorisations(oracle, gpu_lib, monkeypatch, mwg, min_kf, seed,
                                                nkf, npt):
     """The profile LDLT over the whole grid (factor_profile_grid: block rows owned per
-    work-group, write-through hand-offs) forced below its 40-keyframe default, and work-group 0
-    alone forced above it: both match the oracle."""
+    work-group, one write-through hand-off per block column, replicated diagonal blocks) and
+    work-group 0 alone (SLAMGPU_GBA_MWG=0, or below SLAMGPU_GBA_MWG_MIN_KF): both match the
+    oracle."""
     monkeypatch.setenv("SLAMGPU_GBA_MWG", mwg)
     monkeypatch.setenv("SLAMGPU_GBA_MWG_MIN_KF", min_kf)
     P = gba_problem(seed, nkf, npt, spacing=0.8, outlier_frac=0.02)
