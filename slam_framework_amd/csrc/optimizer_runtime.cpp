@@ -259,30 +259,37 @@ int slamgpu_local_ba_linearize_device(
 
 namespace {
 
-// Work-groups of the cooperative single-problem solver: 32 (SLAMGPU_BA_WGS overrides), never more
-// than can be resident at once. C5 LocalBA: 2.91 / 2.81 / 2.82 / 2.76 ms at 24 / 32 / 48 / 64;
-// 32 leaves 224 CUs to the tracking front end that shares the device. Computed once per device
-// (the mapping and loop-closing threads may make their first calls at the same time).
 constexpr int kMaxDevices = 64;
 
-int coop_grid(int device) {
+// Work-groups of a coop BA launch over K optimised keyframes, never more than can be resident at
+// once (the device's limits computed once per device: the mapping and loop-closing threads may
+// make their first calls at the same time): 64 (sweep at the round-3 end,
+// profiles/r3zv_ba_grid_sweep.log: C5 2.9 / 3.0 / 3.1 ms at 32 / 64 / 128 work-groups is flat to
+// 64, while a 54-keyframe window 8.7 -> 8.3 ms and GBA-100 15.5 -> 13.5 ms gain; 192 CUs stay free
+// for the tracking front end), and 128 for map-scale systems (K >= 512: GBA-1500 116 -> 110 ms),
+// bounded by the CUs and the kernel's occupancy; SLAMGPU_BA_WGS fixes it.
+int coop_grid(int device, int K) {
   static std::once_flag once[kMaxDevices];
-  static int grid[kMaxDevices];
+  static int grid[kMaxDevices], cap[kMaxDevices];
+  static bool fixed[kMaxDevices];
   if (device < 0 || device >= kMaxDevices) return 1;
   std::call_once(once[device], [device]() {
     hipDeviceProp_t prop{};
-    int g = 32;
+    int c = 256;
     const bool have = hipGetDeviceProperties(&prop, device) == hipSuccess &&
                       prop.multiProcessorCount > 0;
-    if (have) g = std::min(g, prop.multiProcessorCount);
-    if (const char* e = getenv("SLAMGPU_BA_WGS")) g = std::min(256, std::max(1, atoi(e)));
+    if (have) c = std::min(c, prop.multiProcessorCount);
     int per_cu = 0;
     if (have && hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, coop_kernel_ptr(),
                                                              kCoopThreads, 0) == hipSuccess &&
         per_cu > 0)
-      g = std::min(g, per_cu * prop.multiProcessorCount);
-    grid[device] = std::max(1, g);
+      c = std::min(c, per_cu * prop.multiProcessorCount);
+    cap[device] = std::max(1, c);
+    const char* e = getenv("SLAMGPU_BA_WGS");
+    fixed[device] = e != nullptr;
+    grid[device] = std::min(cap[device], e ? std::min(256, std::max(1, atoi(e))) : 64);
   });
+  if (!fixed[device] && K >= 512) return std::min(cap[device], 2 * grid[device]);
   return grid[device];
 }
 
@@ -394,7 +401,7 @@ int coop_host(const char* what, const slamgpu_camera* cam, const float* inv_sigm
   const auto t_host0 = clk::now();
   int dev = 0;
   OPT_HIPCHECK(hipGetDevice(&dev));
-  const int G = coop_grid(dev);
+  const int G = coop_grid(dev, K);
   size_t wsb = 0;
   coop_layout(nullptr, n_kf, n_points, n_obs, K, (int)pairs, G, pnnz, &wsb);
   // inputs and outputs in one region (one DMA each way through a pinned twin), then workspace
