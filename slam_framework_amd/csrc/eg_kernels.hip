@@ -183,6 +183,7 @@ __global__ __launch_bounds__(64) void eg_assemble_kernel(EgGraph G, EgState W) {
 #define EG_EXACT_ROUNDING 1
 #endif
 constexpr int kFacThreads = 1024;
+constexpr int kPanStage = 96;  // extent blocks whose panel is staged in LDS (37.6 KB)
 
 // The LDLT of H + lambda I (profile storage, vertex order) and the solve, by one work-group of
 // 16 waves. Right-looking by 7x7 block column k with a look-ahead: the panel (a thread per row of
@@ -190,7 +191,10 @@ constexpr int kFacThreads = 1024;
 // -> barrier -> waves 1-15 apply the trailing update A_ij -= L_ik D_k L_jk' over the column's
 // extent while wave 0 applies it to the next diagonal block and lane 0 factors that block in
 // registers (pivot reciprocals, in-block forward solve) -> barrier: two barriers per column,
-// the diagonal chain off the critical path. Block (i, j) of an extent row lives at
+// the diagonal chain off the critical path. The panel's blocks also go to LDS (extents of up to
+// kPanStage blocks), so the update and the next diagonal block read L_ik there instead of
+// making another L2 round trip after the barrier; wave 0 loads the next diagonal block before
+// the panel (it is final but for this column's update). Block (i, j) of an extent row lives at
 // ext_base[e] + j (ext_base = off[i] - start[i], precomputed on the host: one dependent load).
 // Then z = D^-1 y and the backward solve by wave 0 alone (lanes 0-6 sum a column's extent, lane 0
 // solves the block; no work-group barriers), and g2o's scale term. EG_EXACT_ROUNDING (default)
@@ -209,6 +213,7 @@ __global__ __launch_bounds__(kFacThreads) void eg_factor_solve_kernel(EgGraph G,
   __shared__ double s_rd[2][7];   // its pivot reciprocals
   __shared__ double s_y[2][7];    // its forward-solved rhs slice
   __shared__ double s_nx[49];     // the next diagonal block after its last update
+  __shared__ double s_pan[kPanStage * 49];  // column k's panel blocks L_ik (extents <= kPanStage)
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, F = G.F;
   double* L = W.L;  // a copy of H (launch_eg_factor_solve)
   double* y = W.y;
@@ -277,6 +282,9 @@ __global__ __launch_bounds__(kFacThreads) void eg_factor_solve_kernel(EgGraph G,
   for (int k = 0; k < F; k++) {
     const int cur = k & 1;
     const int e0 = G.ext_ptr[k], ne = G.ext_ptr[k + 1] - e0;
+    const bool staged = ne <= kPanStage;  // the panel also goes to LDS for the update below
+    double an = 0.0;  // wave 0: the next diagonal block, final but for this column's update
+    if (wid == 0 && lane < 49 && k + 1 < F) an = diag_of(k + 1)[lane];
     for (int q = tid; q < 7 * ne; q += kFacThreads) {  // panel rows
       const int t = q / 7, r = q % 7;
       double* Aik = L + (G.ext_base[e0 + t] + k) * 49 + 7 * r;
@@ -298,6 +306,7 @@ __global__ __launch_bounds__(kFacThreads) void eg_factor_solve_kernel(EgGraph G,
 #pragma unroll
       for (int c = 0; c < 7; c++) {
         Aik[c] = a[c];
+        if (staged) s_pan[q * 7 + c] = a[c];
         sy += a[c] * s_y[cur][c];
       }
       y[7 * G.ext_rows[e0 + t] + r] -= sy;
@@ -307,14 +316,18 @@ __global__ __launch_bounds__(kFacThreads) void eg_factor_solve_kernel(EgGraph G,
     if (wid == 0) {
       if (k + 1 < F) {  // the next diagonal block: its last update, then its factorisation
         if (lane < 49) {
-          const double* An = diag_of(k + 1);
-          double v = An[lane];
+          double v = an;
           if (nxt_in) {
             const int r = lane / 7, c = lane % 7;
-            const double* Ln = L + (G.ext_base[e0] + k) * 49;  // block (k + 1, k)
             double t = 0.0;
+            if (staged) {  // block (k + 1, k): panel block 0
 #pragma unroll
-            for (int m = 0; m < 7; m++) t += Ln[7 * r + m] * s_kk[cur][8 * m] * Ln[7 * c + m];
+              for (int m = 0; m < 7; m++) t += s_pan[7 * r + m] * s_kk[cur][8 * m] * s_pan[7 * c + m];
+            } else {
+              const double* Ln = L + (G.ext_base[e0] + k) * 49;
+#pragma unroll
+              for (int m = 0; m < 7; m++) t += Ln[7 * r + m] * s_kk[cur][8 * m] * Ln[7 * c + m];
+            }
             v -= t;
           }
           s_nx[lane] = v;
@@ -335,11 +348,18 @@ __global__ __launch_bounds__(kFacThreads) void eg_factor_solve_kernel(EgGraph G,
         const int j = G.ext_rows[e0 + tj];
         const int64_t bi = G.ext_base[e0 + ti], bj = G.ext_base[e0 + tj];
         const int r = ent / 7, c = ent % 7;
-        const double* Lik = L + (bi + k) * 49 + 7 * r;
-        const double* Ljk = L + (bj + k) * 49 + 7 * c;
         double t = 0.0;
+        if (staged) {
+          const double* Lik = s_pan + 49 * ti + 7 * r;
+          const double* Ljk = s_pan + 49 * tj + 7 * c;
 #pragma unroll
-        for (int m = 0; m < 7; m++) t += Lik[m] * s_kk[cur][8 * m] * Ljk[m];
+          for (int m = 0; m < 7; m++) t += Lik[m] * s_kk[cur][8 * m] * Ljk[m];
+        } else {
+          const double* Lik = L + (bi + k) * 49 + 7 * r;
+          const double* Ljk = L + (bj + k) * 49 + 7 * c;
+#pragma unroll
+          for (int m = 0; m < 7; m++) t += Lik[m] * s_kk[cur][8 * m] * Ljk[m];
+        }
         L[(bi + j) * 49 + ent] -= t;
       }
     }
