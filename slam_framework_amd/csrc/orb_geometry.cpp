@@ -187,13 +187,14 @@ int compute_geometry(const OrbParams& p, int cols, int rows, OrbGeom* g,
   // score map is indexed by tile column). A row holds the cell view from iniX & ~3 plus the
   // prefilter's spare right-neighbour dword.
   // A tile row starts at iniX & ~15 (16-byte global_load_lds chunks; up to 15 lead bytes).
-  // Tiles are double-buffered and hold whole 1 KiB glds blocks (1024 / stride rows each).
+  // One tile buffer per wave holding exactly the view's rows (the last glds block lane-masked):
+  // LDS, not VGPRs, bounds the kernel's occupancy (double-buffered tiles of whole 1 KiB blocks,
+  // 10.3 KB per wave, were slower than 6.6 KB single: 0.966 -> 0.84 ms per step, round 2).
   g->fast_tile_stride = max_wcell + 6 + 15 + 4 <= 64 ? 64 : 128;
-  g->fast_tile_rows = FAST_EXACT_ROWS ? max_hcell + 6
-                                      : round_up(max_hcell + 6, 1024 / g->fast_tile_stride);
+  g->fast_tile_rows = max_hcell + 6;
   g->fast_score_stride = g->fast_tile_stride;
   g->fast_score_rows = max_hcell + 2;  // detect rows + a zero row above and below
-  g->fast_lds_per_wave = FAST_TILE_BUFS * round_up(g->fast_tile_stride * g->fast_tile_rows, 16) +
+  g->fast_lds_per_wave = round_up(g->fast_tile_stride * g->fast_tile_rows, 16) +
                          round_up(g->fast_score_stride * g->fast_score_rows, 16) +
                          round_up(2 * max_wcell * max_hcell, 16);  // u16 candidate list
   if (max_wcell > 64) return -4;
@@ -288,95 +289,6 @@ void build_cells(const OrbGeom& g, std::vector<CellDesc>* cells) {
       d.vw = (int16_t)(maxX - iniX);
     }
   }
-}
-
-void build_pyr_bands(const OrbGeom& g, const std::vector<ResizeY>& ry, int nb,
-                     std::vector<PyrBand>* bands, std::vector<uint32_t>* rows,
-                     int max_rows[kMaxLevels]) {
-  bands->assign((size_t)nb * kMaxLevels, PyrBand{0, -1, 0, -1, 0, 0});
-  rows->clear();
-  for (int l = 0; l < kMaxLevels; l++) max_rows[l] = 0;
-  const int L = g.nlevels;
-  // Band boundaries: level 1 split evenly; on level l >= 2 a band starts at the first row whose
-  // upper source row (y0) lies at or below the band's start on level l - 1. A band's rows then
-  // never read above its own lower-level rows -- the halo is only at the bottom, about one row
-  // per level (a proportional split of every level would add a halo at the top as well).
-  std::vector<int> bnd((size_t)(nb + 1) * kMaxLevels, 0);
-  auto B = [&](int k, int l) -> int& { return bnd[(size_t)k * kMaxLevels + l]; };
-  for (int k = 0; k <= nb; k++) B(k, 1) = (int)((int64_t)k * g.lv[1].h / nb);
-  for (int l = 2; l < L; l++) {
-    const int h = g.lv[l].h;
-    int d = 0;
-    for (int k = 0; k <= nb; k++) {
-      if (k == nb) { B(k, l) = h; break; }
-      while (d < h && std::min(ry[g.lv[l].ry_base + d].y0, ry[g.lv[l].ry_base + d].y1) < B(k, l - 1))
-        d++;
-      B(k, l) = d;
-    }
-  }
-  for (int k = 0; k < nb; k++) {
-    PyrBand* bt = bands->data() + (size_t)k * kMaxLevels;
-    for (int l = 1; l < L; l++) {
-      bt[l].own_lo = B(k, l);
-      bt[l].own_hi = B(k + 1, l) - 1;
-    }
-    if (L > 1) {
-      bt[L - 1].need_lo = bt[L - 1].own_lo;
-      bt[L - 1].need_hi = bt[L - 1].own_hi;
-    }
-    for (int l = L - 1; l >= 1; l--) {
-      // the level l - 1 rows that level l's need range resizes from (HResize rows y0, y1)
-      int lo = 1 << 30, hi = -1;
-      for (int d = bt[l].need_lo; d <= bt[l].need_hi; d++) {
-        const ResizeY& e = ry[g.lv[l].ry_base + d];
-        lo = std::min(lo, std::min(e.y0, e.y1));
-        hi = std::max(hi, std::max(e.y0, e.y1));
-      }
-      if (l - 1 >= 1 && bt[l - 1].own_lo <= bt[l - 1].own_hi) {
-        lo = std::min(lo, bt[l - 1].own_lo);
-        hi = std::max(hi, bt[l - 1].own_hi);
-      }
-      if (hi < lo) { lo = 0; hi = -1; }
-      bt[l - 1].need_lo = lo;
-      bt[l - 1].need_hi = hi;
-    }
-    for (int l = 0; l < L; l++)
-      max_rows[l] = std::max(max_rows[l], bt[l].need_hi - bt[l].need_lo + 1);
-    bt[0].rows_off = (int)(rows->size() / 2);
-    for (int l = 1; l < L; l++)
-      for (int d = bt[l].need_lo; d <= bt[l].need_hi; d++) {
-        const ResizeY& e = ry[g.lv[l].ry_base + d];
-        rows->push_back((uint32_t)e.y0 | (uint32_t)e.y1 << 16);
-        rows->push_back((uint32_t)(uint16_t)e.b0 | (uint32_t)(uint16_t)e.b1 << 16);
-      }
-    bt[0].rows_n = (int)(rows->size() / 2) - bt[0].rows_off;
-  }
-}
-
-bool check_pyr_bands(const OrbGeom& g, const std::vector<ResizeY>& ry, int nb,
-                     const std::vector<PyrBand>& bands) {
-  const int L = g.nlevels;
-  auto in = [](int v, const PyrBand& r) { return v >= r.need_lo && v <= r.need_hi; };
-  for (int l = 1; l < L; l++) {
-    int next = 0;  // the own ranges, in band order, partition [0, h)
-    for (int k = 0; k < nb; k++) {
-      const PyrBand& r = bands[(size_t)k * kMaxLevels + l];
-      if (r.own_lo > r.own_hi) continue;
-      if (r.own_lo != next || r.own_lo < r.need_lo || r.own_hi > r.need_hi) return false;
-      next = r.own_hi + 1;
-    }
-    if (next != g.lv[l].h) return false;
-  }
-  for (int k = 0; k < nb; k++)  // every computed row's source rows are computed too
-    for (int l = 1; l < L; l++) {
-      const PyrBand& r = bands[(size_t)k * kMaxLevels + l];
-      const PyrBand& s = bands[(size_t)k * kMaxLevels + l - 1];
-      for (int d = r.need_lo; d <= r.need_hi; d++) {
-        const ResizeY& e = ry[g.lv[l].ry_base + d];
-        if (d < 0 || d >= g.lv[l].h || !in(e.y0, s) || !in(e.y1, s)) return false;
-      }
-    }
-  return true;
 }
 
 }  // namespace slamgpu

@@ -8,16 +8,6 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
-// fast_cells tile buffers per wave (2: the next cell's tile streams in while this one is
-// processed; 1: more waves per CU instead -- LDS, not VGPRs, bounds its occupancy: 10.3 KB per
-// wave double-buffered, 6.6 KB single; A/B 0.966 -> 0.84 ms per step) and whether a tile holds
-// exactly the view's rows (the last global_load_lds block lane-masked) or whole 1 KiB blocks.
-#ifndef FAST_TILE_BUFS
-#define FAST_TILE_BUFS 1
-#endif
-#ifndef FAST_EXACT_ROWS
-#define FAST_EXACT_ROWS 1
-#endif
 
 namespace slamgpu {
 
@@ -94,14 +84,6 @@ struct OrbGeom {
 // Resize tables (HResizeLinear / VResizeLinear coefficients, 11-bit fixed point).
 struct ResizeX { int32_t sx; int16_t a0, a1; };
 struct ResizeY { int32_t y0, y1; int16_t b0, b1; };
-
-// Fused pyramid (pyr_band_kernel): band k of level l >= 1 owns (writes) rows [own_lo, own_hi]
-// and computes [need_lo, need_hi] -- its own rows plus the rows its higher-level rows resize
-// from. Level 0 has only the need range (the caller's rows the band reads). Inclusive; an empty
-// range has lo > hi.
-// rows_off / rows_n (level-0 entry only): the band's packed row-table entries of levels >= 1
-// (y0 | y1 << 16, b0 | b1 << 16 per need row, level by level) in the band row array.
-struct PyrBand { int need_lo, need_hi, own_lo, own_hi, rows_off, rows_n; };
 
 // One FAST survivor / octree key: x_rel (12 b) | y_rel (11 b) << 12 | score (8 b) << 23,
 // coordinates relative to (minBorderX, minBorderY).

@@ -46,29 +46,11 @@ struct ExtractOutput {
   int* nkps;               // [img]
 };
 
-// One row-band partition of the fused pyramid kernel: nb bands, device table, and the longest
-// need range per level (host, for the work-group's LDS size).
-#ifndef PYR_BANDS_BATCH
-#define PYR_BANDS_BATCH 32
-#endif
-#ifndef PYR_BANDS_SMALL
-#define PYR_BANDS_SMALL 48
-#endif
-constexpr int kPyrBandsBatch = PYR_BANDS_BATCH, kPyrBandsSmall = PYR_BANDS_SMALL;
-struct PyrBandSet {
-  const PyrBand* dev = nullptr;
-  const uint2* rows = nullptr;  // packed row-table entries (PyrBand rows_off / rows_n)
-  int nb = 0;
-  int max_rows[kMaxLevels] = {};
-};
-
 struct OrbGeomDev {
   const OrbGeom* host;
   const OrbGeom* dev;
   const ResizeX* rx;
   const ResizeY* ry;
-  const PyrBandSet* bands_big;  // band partitions for batches / for small launches
-  const PyrBandSet* bands_small;
   const CellDesc* cells;   // FAST cell views, cells_per_image entries (build_cells)
   ExtractWorkspace ws;
   ExtractOutput out;

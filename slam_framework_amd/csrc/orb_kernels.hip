@@ -185,196 +185,6 @@ __global__ __launch_bounds__(256) void pyr_down_kernel(ImageBatch b, const OrbGe
 }
 
 // ---------------------------------------------------------------------------------------
-// pyr_band: the whole pyramid (ComputePyramid :1051-1075, each level resized from the one before
-// it) of one row band of one image in one work-group, the intermediate levels held in LDS.
-// Band k owns a contiguous run of rows of every level l >= 1 (level 1 split evenly, the higher
-// levels' runs aligned to it) and also computes the rows of lower levels its higher-level rows
-// resize from (PyrBand need ranges, build_pyr_bands), so no
-// level is read back from memory: HBM sees the caller's level-0 rows once (plus the few halo rows
-// neighbouring bands share, L2 hits on the same XCD) and every level's rows written once --
-// instead of pyr_down_kernel's one launch per level re-reading level l-1. The per-pixel arithmetic
-// is pyr_down_kernel's (bit-identical output).
-// A work item is one 4-column group x kPyrBandRows dst rows: the source rows' horizontal pass
-// (3 LDS dwords, two alignbytes, v_perm + v_dot2 per column) is computed once per item and row,
-// cached in two slots for the vertical pass.
-// kCopy: how the band's level-0 rows reach LDS. 0: they are one contiguous byte range (row stride
-// = the caller's 16-byte-aligned pitch), copied by global_load_lds_dwordx4 with no VGPR staging;
-// 1: dword copy (4-byte aligned caller images); 2: byte copy. 1 and 2 use rows of stride0 bytes.
-constexpr int kPyrBandThreads = 256;
-#ifndef PYR_BAND_ROWS
-#define PYR_BAND_ROWS 8
-#endif
-constexpr int kPyrBandRows = PYR_BAND_ROWS;
-
-// Work-group barrier ordering LDS only: the pending global stores of the level just computed
-// are not waited for (a __syncthreads() would drain them, vmcnt(0), at every level).
-__device__ __forceinline__ void lds_barrier() {
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
-  __builtin_amdgcn_s_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
-}
-
-// HResizeLinear coefficients of dst column dx, derived as compute_geometry's host table
-// (resize.cpp resizeGeneric_ INTER_LINEAR: the same double / float expression sequence, so the
-// same bits): source column sx, and (a0, a1) x16 packed for v_dot2, or 32768 (S[sx] * 2048) from
-// xmax on.
-__device__ __forceinline__ int pyr_col(double rsx, int sw, int dx, uint32_t* A) {
-  float fx = (float)(((double)dx + 0.5) * rsx - 0.5);
-  int sx = (int)floorf(fx);
-  fx -= (float)sx;
-  if (sx < 0) {
-    fx = 0.f;
-    sx = 0;
-  }
-  bool copy = false;
-  if (sx + 1 >= sw) {
-    copy = true;
-    if (sx >= sw - 1) {
-      fx = 0.f;
-      sx = sw - 1;
-    }
-  }
-  const uint32_t a0 = (uint32_t)(int)rintf((1.f - fx) * 2048.f);
-  const uint32_t a1 = (uint32_t)(int)rintf(fx * 2048.f);
-  *A = copy ? 32768u : (16u * a0) | (16u * a1) << 16;
-  return sx;
-}
-
-template <int kCopy>
-__global__ __launch_bounds__(kPyrBandThreads) void pyr_band_kernel(
-    ImageBatch b, const OrbGeom* __restrict__ g, const uint2* __restrict__ rowtab,
-    const PyrBand* __restrict__ bands, int half1, int stride0, int ry_off) {
-  extern __shared__ __attribute__((aligned(16))) uint8_t s_pyr[];
-  int img, band;
-  xcd_image_block(&img, &band);
-  const int tid = threadIdx.x;
-  const PyrBand* bt = bands + band * kMaxLevels;
-  const PyrBand b0 = bt[0];
-  if (b0.need_hi < b0.need_lo) return;  // work-group-uniform: a band with no rows at any level
-  const int nlev = g->nlevels;
-  const int pitch = b.in_pitch;
-  const uint8_t* src0 = batch_image(b, img) + (int64_t)b0.need_lo * pitch;
-  const int rows0 = b0.need_hi - b0.need_lo + 1;
-  // the band's packed row-table entries of every level >= 1 into LDS next to the level-0 rows
-  uint2* const s_ry = reinterpret_cast<uint2*>(s_pyr + ry_off);
-  for (int i = tid; i < b0.rows_n; i += kPyrBandThreads) s_ry[i] = rowtab[b0.rows_off + i];
-  if constexpr (kCopy == 0) {
-    const int lane = tid & 63, wid = wave_id();
-    const int nbytes = rows0 * pitch;  // a multiple of 16
-    for (int blk = wid; blk * 1024 < nbytes; blk += kPyrBandThreads / 64) {
-      const int off = blk * 1024 + 16 * lane;
-      if (off < nbytes)
-        __builtin_amdgcn_global_load_lds(
-            (const __attribute__((address_space(1))) void*)(src0 + off),
-            (__attribute__((address_space(3))) void*)(s_pyr + blk * 1024), 16, 0, 0);
-    }
-    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): this wave's rows have landed
-  } else {
-    const int w0 = g->lv[0].w;
-    if constexpr (kCopy == 1) {
-      const int nq = (w0 + 3) >> 2;
-      for (int i = tid; i < rows0 * nq; i += kPyrBandThreads) {
-        const int r = i / nq, q = i - r * nq;
-        *reinterpret_cast<uint32_t*>(s_pyr + r * stride0 + 4 * q) =
-            *reinterpret_cast<const uint32_t*>(src0 + (int64_t)r * pitch + 4 * q);
-      }
-    } else {
-      for (int i = tid; i < rows0 * w0; i += kPyrBandThreads) {
-        const int r = i / w0, x = i - r * w0;
-        s_pyr[r * stride0 + x] = src0[(int64_t)r * pitch + x];
-      }
-    }
-  }
-  __syncthreads();  // the only wait on global loads; the level loop below issues none
-  uint8_t* const pyr = b.pyr + (int64_t)img * g->pyr_bytes;
-  int ry_base = 0;  // this level's first entry in s_ry
-  for (int l = 1; l < nlev; l++) {
-    const PyrBand nd = bt[l];
-    const int sbase = bt[l - 1].need_lo;
-    if (nd.need_hi >= nd.need_lo) {  // work-group-uniform
-      const LevelGeom& D = g->lv[l];
-      const int sw = g->lv[l - 1].w;
-      const double rsx = D.rsx;
-      const uint8_t* sbuf = s_pyr + (((l - 1) & 1) ? half1 : 0);
-      uint8_t* dbuf = s_pyr + ((l & 1) ? half1 : 0);
-      const int ss = l == 1 ? stride0 : ((sw + 15) & ~15);
-      const int ds = (D.w + 15) & ~15;
-      const int ncg = (D.w + 3) >> 2;
-      const int items = ncg * ((nd.need_hi - nd.need_lo + kPyrBandRows) / kPyrBandRows);
-      const int qmax = (sw - 1) >> 2;
-      uint8_t* const gdst = pyr + D.offset;
-      const int dpitch = D.pitch, dw = D.w;
-      const uint2* const ry = s_ry + ry_base - nd.need_lo;  // indexed by dst row
-      for (int it = tid; it < items; it += kPyrBandThreads) {
-        const int ch = it / ncg, cg = it - ch * ncg;
-        const int x0 = 4 * cg;
-        const int d0 = nd.need_lo + ch * kPyrBandRows;
-        const int d1 = min(d0 + kPyrBandRows, nd.need_hi + 1);
-        uint32_t sel[4], A[4];
-        int s0 = 0;
-#pragma unroll
-        for (int k = 0; k < 4; k++) {
-          const int sx = pyr_col(rsx, sw, min(x0 + k, dw - 1), &A[k]);
-          if (k == 0) s0 = sx;
-          const uint32_t bk = (uint32_t)min(sx - s0, 6);
-          sel[k] = bk | 0x0c00u | (bk + 1) << 16 | 0x0c000000u;  // bytes bk, bk+1 -> u16 lanes
-        }
-        const int q0 = s0 >> 2, sh = s0 & 3;
-        const int qa = min(q0, qmax), qb = min(q0 + 1, qmax), qc = min(q0 + 2, qmax);
-        auto hrow = [&](int sy, uint32_t(&h)[4]) {
-          const uint32_t* rw = reinterpret_cast<const uint32_t*>(sbuf + (sy - sbase) * ss);
-          const uint32_t v0 = rw[qa], v1 = rw[qb], v2 = rw[qc];
-          const uint32_t W0 = __builtin_amdgcn_alignbyte(v1, v0, sh);
-          const uint32_t W1 = __builtin_amdgcn_alignbyte(v2, v1, sh);
-#pragma unroll
-          for (int k = 0; k < 4; k++) h[k] = dot2u(__builtin_amdgcn_perm(W1, W0, sel[k]), A[k], 0u);
-        };
-        int ra = -1, rb = -1;  // source rows held in ha / hb
-        uint32_t ha[4] = {0, 0, 0, 0}, hb[4] = {0, 0, 0, 0};
-        for (int d = d0; d < d1; d++) {
-          const uint2 e = ry[d];
-          const int y0 = (int)(e.x & 0xffffu), y1 = (int)(e.x >> 16);
-          if (y1 != rb) {
-            if (y0 == rb) {
-#pragma unroll
-              for (int k = 0; k < 4; k++) ha[k] = hb[k];
-              ra = rb;
-            }
-            hrow(y1, hb);
-            rb = y1;
-          }
-          if (y0 != rb && y0 != ra) {
-            hrow(y0, ha);
-            ra = y0;
-          }
-          const bool same = y0 == rb;
-          // (b * (r >> 4)) >> 16 == mulhi24(b << 8, (r >> 4) << 8), as in pyr_down_kernel
-          const uint32_t bb0 = (e.y & 0xffffu) << 8, bb1 = (e.y >> 16) << 8;
-          uint32_t packed = 0;
-#pragma unroll
-          for (int k = 0; k < 4; k++) {
-            const uint32_t r0 = (same ? hb[k] : ha[k]) & ~0xffu, r1 = hb[k] & ~0xffu;
-            const uint32_t v = (mulhi24(bb0, r0) + mulhi24(bb1, r1) + 2) >> 2;
-            packed |= (v & 0xffu) << (8 * k);
-          }
-          *reinterpret_cast<uint32_t*>(dbuf + (d - nd.need_lo) * ds + x0) = packed;
-          if (d >= nd.own_lo && d <= nd.own_hi) {
-            uint8_t* drow = gdst + (int64_t)d * dpitch;
-            if (x0 + 4 <= dw) {
-              *reinterpret_cast<uint32_t*>(drow + x0) = packed;  // pitch is a multiple of 64
-            } else {
-              for (int k = 0; x0 + k < dw; k++) drow[x0 + k] = (uint8_t)(packed >> (8 * k));
-            }
-          }
-        }
-      }
-      ry_base += nd.need_hi - nd.need_lo + 1;
-    }
-    lds_barrier();
-  }
-}
-
-// ---------------------------------------------------------------------------------------
 __device__ __forceinline__ int reflect101(int i, int n) {  // cv::BORDER_REFLECT_101, |overshoot| < n
   if (i < 0) i = -i;
   if (i >= n) i = 2 * n - 2 - i;
@@ -393,12 +203,6 @@ __device__ __forceinline__ int reflect101(int i, int n) {  // cv::BORDER_REFLECT
 #define FAST_CELL_WAVES 1
 #endif
 constexpr int kCellWaves = FAST_CELL_WAVES;  // waves per work-group
-#ifndef FAST_PRE2
-#define FAST_PRE2 1  // opposite-pair pre-test on (0,8),(4,12) only (0: all four pairs)
-#endif
-#ifndef FAST_MINW
-#define FAST_MINW 1  // A/B: __launch_bounds__ minimum waves per SIMD
-#endif
 
 // max over the 16 contiguous 9-arcs of min(v - ring) ("darker" strength) and of min(ring - v)
 // ("brighter"); p is a FAST-9 corner at threshold t iff the result is > t.
@@ -538,7 +342,7 @@ __device__ __forceinline__ uint4 readlane4(const uint4& x, int j) {
 // while this one is processed. Otherwise dword loads staged through registers (4-byte aligned)
 // or a byte copy.
 template <int TS, bool GLDS>
-__global__ __launch_bounds__(64 * kCellWaves, FAST_MINW) void fast_cells_kernel(ImageBatch b,
+__global__ __launch_bounds__(64 * kCellWaves, 1) void fast_cells_kernel(ImageBatch b,
                                                          const OrbGeom* __restrict__ g,
                                                          const CellDesc* __restrict__ cells,
                                                          uint32_t* __restrict__ cell_keys,
@@ -569,7 +373,7 @@ __global__ __launch_bounds__(64 * kCellWaves, FAST_MINW) void fast_cells_kernel(
   const int min_th = __builtin_amdgcn_readfirstlane(g->min_th);
   const int tile_bytes = (kTileStride * g->fast_tile_rows + 15) & ~15;
   uint8_t* tile0 = s_fast + wid * g->fast_lds_per_wave;
-  uint8_t* sc = tile0 + (GLDS ? FAST_TILE_BUFS : 1) * tile_bytes;
+  uint8_t* sc = tile0 + tile_bytes;
   const int tile_rows = __builtin_amdgcn_readfirstlane(g->fast_tile_rows);
   uint16_t* cand =
       reinterpret_cast<uint16_t*>(sc + ((kScoreStride * g->fast_score_rows + 15) & ~15));
@@ -599,7 +403,7 @@ __global__ __launch_bounds__(64 * kCellWaves, FAST_MINW) void fast_cells_kernel(
     const uint8_t* src = v.base + (int64_t)v.ini_y * v.pitch + v.ax + glc;
 #pragma unroll
     for (int k = 0; k < kGSteps; k++)
-      if (k < n && (!FAST_EXACT_ROWS || k * kGRows + glr < tile_rows))
+      if (k < n && k * kGRows + glr < tile_rows)
         __builtin_amdgcn_global_load_lds(
             (const __attribute__((address_space(1))) void*)(
                 src + (int64_t)min(k * kGRows + glr, v.vh - 1) * v.pitch),
@@ -607,9 +411,7 @@ __global__ __launch_bounds__(64 * kCellWaves, FAST_MINW) void fast_cells_kernel(
     return n;
   };
   CellView nxt = cell_view<kAlign>(b, g, img, in_pitch, readlane4(my_desc, 0));
-  if constexpr (GLDS) {
-    if (FAST_TILE_BUFS == 2 && nxt.vh > 0) issue(nxt, tile0);
-  } else {
+  if constexpr (!GLDS) {
     if (nxt.vh > 0) prefetch(nxt);
   }
 
@@ -617,7 +419,7 @@ __global__ __launch_bounds__(64 * kCellWaves, FAST_MINW) void fast_cells_kernel(
     const CellView v = nxt;
     const int64_t slot = (int64_t)img * ncells + c0 + ci;
     uint8_t* tile = tile0;
-    if constexpr (GLDS && FAST_TILE_BUFS == 1) {
+    if constexpr (GLDS) {
       // one tile buffer: this cell's rows are loaded now (the previous cell's tile reads have
       // all returned), other waves hide the latency
       if (ci + 1 < nc) nxt = cell_view<kAlign>(b, g, img, in_pitch, readlane4(my_desc, ci + 1));
@@ -629,33 +431,6 @@ __global__ __launch_bounds__(64 * kCellWaves, FAST_MINW) void fast_cells_kernel(
       __builtin_amdgcn_wave_barrier();
       issue(v, tile0);
       __builtin_amdgcn_s_waitcnt(0x0F70);
-      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-    } else if constexpr (GLDS) {
-      tile = tile0 + (ci & 1) * tile_bytes;
-      int n_next = 0;
-      if (ci + 1 < nc) {
-        nxt = cell_view<kAlign>(b, g, img, in_pitch, readlane4(my_desc, ci + 1));
-        // the other buffer's last reader was cell ci - 1, whose LDS reads have all returned
-        if (nxt.vh > 0) n_next = issue(nxt, tile0 + ((ci + 1) & 1) * tile_bytes);
-      }
-      if (v.vh == 0) {  // empty cell (:737, :745)
-        if (lane == 0) cell_count[slot] = 0;
-        continue;
-      }
-      // this cell's glds have landed once at most the next cell's n_next are outstanding
-      switch (n_next) {
-        case 0: __builtin_amdgcn_s_waitcnt(0x0F70); break;
-        case 1: __builtin_amdgcn_s_waitcnt(0x0F71); break;
-        case 2: __builtin_amdgcn_s_waitcnt(0x0F72); break;
-        case 3: __builtin_amdgcn_s_waitcnt(0x0F73); break;
-        case 4: __builtin_amdgcn_s_waitcnt(0x0F74); break;
-        case 5: __builtin_amdgcn_s_waitcnt(0x0F75); break;
-        case 6: __builtin_amdgcn_s_waitcnt(0x0F76); break;
-        case 7: __builtin_amdgcn_s_waitcnt(0x0F77); break;
-        case 8: __builtin_amdgcn_s_waitcnt(0x0F78); break;
-        default: __builtin_amdgcn_s_waitcnt(0x0F79); break;
-      }
       __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
       __builtin_amdgcn_wave_barrier();
     } else {
@@ -722,10 +497,6 @@ __global__ __launch_bounds__(64 * kCellWaves, FAST_MINW) void fast_cells_kernel(
             return *reinterpret_cast<const uint32_t*>(row + dy * kTileStride + 4 * dq);
           };
           const uint32_t c = rd(0, 0), cm = rd(0, qm), cp = rd(0, 1);
-#if !FAST_PRE2
-          const uint32_t u2 = rd(2, 0), u2m = rd(2, qm), u2p = rd(2, 1);
-          const uint32_t d2 = rd(-2, 0), d2m = rd(-2, qm), d2p = rd(-2, 1);
-#endif
           const uint32_t p0 = rd(3, 0), p8 = rd(-3, 0);
           // even pixels (bytes 0, 2) and odd pixels (bytes 1, 3) of each ring position as u16
           // pairs; v_perm picks the shifted bytes straight out of two adjacent dwords
@@ -743,25 +514,10 @@ __global__ __launch_bounds__(64 * kCellWaves, FAST_MINW) void fast_cells_kernel(
             const u16x2_t a8 = U(__builtin_amdgcn_perm(p8, p8, s0));      // (0, -3)
             const u16x2_t a4 = U(__builtin_amdgcn_perm(cp, c, s3));       // (+3, 0)
             const u16x2_t a12 = U(__builtin_amdgcn_perm(c, cm, s1));      // (-3, 0)
-#if FAST_PRE2
             const u16x2_t D = __builtin_elementwise_max(__builtin_elementwise_min(a0, a8),
                                                         __builtin_elementwise_min(a4, a12));
             const u16x2_t B = __builtin_elementwise_min(__builtin_elementwise_max(a0, a8),
                                                         __builtin_elementwise_max(a4, a12));
-#else
-            const u16x2_t a2 = U(__builtin_amdgcn_perm(u2p, u2, s2));     // (+2, +2)
-            const u16x2_t a14 = U(__builtin_amdgcn_perm(u2, u2m, s2));    // (-2, +2)
-            const u16x2_t a6 = U(__builtin_amdgcn_perm(d2p, d2, s2));     // (+2, -2)
-            const u16x2_t a10 = U(__builtin_amdgcn_perm(d2, d2m, s2));    // (-2, -2)
-            // FAST_t pre-test on the 4 opposite pairs: darker needs min(pair) < v - t for all
-            // pairs, brighter needs max(pair) > v + t for all pairs
-            const u16x2_t D = __builtin_elementwise_max(
-                __builtin_elementwise_max(__builtin_elementwise_min(a0, a8), __builtin_elementwise_min(a4, a12)),
-                __builtin_elementwise_max(__builtin_elementwise_min(a2, a10), __builtin_elementwise_min(a6, a14)));
-            const u16x2_t B = __builtin_elementwise_min(
-                __builtin_elementwise_min(__builtin_elementwise_max(a0, a8), __builtin_elementwise_max(a4, a12)),
-                __builtin_elementwise_min(__builtin_elementwise_max(a2, a10), __builtin_elementwise_max(a6, a14)));
-#endif
             const u16x2_t lo = __builtin_elementwise_sub_sat(v, tt2), hi = v + tt2;
             any[h] = __builtin_bit_cast(uint32_t, __builtin_elementwise_sub_sat(lo, D)) |
                      __builtin_bit_cast(uint32_t, __builtin_elementwise_sub_sat(B, hi));
@@ -1495,14 +1251,6 @@ __global__ __launch_bounds__(64 * kMaxLevels) void octree_img_kernel(
   }
   __syncthreads();
   if (!active) return;
-#ifdef OCT_LEVEL_MASK  // timing ablation only: skip the levels not in the mask
-  if (!((OCT_LEVEL_MASK >> level) & 1)) return;
-#endif
-#ifdef OCT_PROFILE  // phase timing (timing builds only): wall clock at 100 MHz
-  const uint64_t oct_t0 = wall_clock64();
-  uint64_t oct_t1 = 0, oct_t2 = 0, oct_tp[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  int oct_passes = 0, oct_sz[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-#endif
   int* const outc = oct_count + img * nlev + level;
   uint32_t* const outk = oct_keys + (int64_t)img * g->out_per_image + L.out_base;
   const int nIni = L.n_ini;
@@ -1669,15 +1417,7 @@ __global__ __launch_bounds__(64 * kMaxLevels) void octree_img_kernel(
   const int N = L.budget;
   int cur = 0, nexp = 0;
   bool outer = true;
-#ifdef OCT_PROFILE
-  oct_t1 = wall_clock64();
-#endif
   while (true) {
-#ifdef OCT_PROFILE
-    if (oct_passes < 8) oct_tp[oct_passes] = wall_clock64();
-    if (oct_passes < 8) oct_sz[oct_passes] = (outer ? 1 : -1) * m;
-    oct_passes++;
-#endif
     const OctNodeS* Lc = lists + cur * NC;
     OctNodeS* Ln = lists + (cur ^ 1) * NC;
     const int V = outer ? m : nexp;
@@ -1865,9 +1605,6 @@ __global__ __launch_bounds__(64 * kMaxLevels) void octree_img_kernel(
     if (newm >= N || newm == mprev) break;
     if (outer && newm + E * 3 > N) outer = false;
   }
-#ifdef OCT_PROFILE
-  oct_t2 = wall_clock64();
-#endif
   // ---- 4. retain the best key of each node (:682-701): strict '>' keeps the first maximum
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
   __builtin_amdgcn_wave_barrier();
@@ -1887,17 +1624,6 @@ __global__ __launch_bounds__(64 * kMaxLevels) void octree_img_kernel(
     if (m > L.out_cap) atomicOr(err, kErrNodeOverflow);
     *outc = mout;
   }
-#ifdef OCT_PROFILE
-  if (lane == 0 && img < 2 && (level == 0 || level == 7)) {
-    const uint64_t t3 = wall_clock64();
-    printf("oct img %d lvl %d K %d gather %d passes %d (%d) retain %d x10ns | %d:%d %d:%d %d:%d %d:%d %d:%d\n",
-           img, level, K, (int)(oct_t1 - oct_t0), (int)(oct_t2 - oct_t1), oct_passes,
-           (int)(t3 - oct_t2), oct_sz[0], (int)(oct_tp[1] - oct_tp[0]), oct_sz[1],
-           (int)(oct_tp[2] - oct_tp[1]), oct_sz[2], (int)(oct_tp[3] - oct_tp[2]), oct_sz[3],
-           (int)((oct_passes > 4 ? oct_tp[4] : oct_t2) - oct_tp[3]), oct_sz[4],
-           (int)(oct_t2 - oct_tp[oct_passes > 4 ? 4 : 3]));
-  }
-#endif
 }
 
 // ---------------------------------------------------------------------------------------
@@ -1979,11 +1705,6 @@ __global__ __launch_bounds__(kOctLvlThreads) void octree_lvl_kernel(
     if (tid == 0) *outc = 0;
     return;
   }
-#ifdef OCT_PROFILE  // phase timing (timing builds only): wall clock at 100 MHz
-  const uint64_t oct_t0 = wall_clock64();
-  uint64_t oct_tg = 0, oct_t1 = 0, oct_t2 = 0, oct_tp[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  int oct_passes = 0, oct_sz[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-#endif
   uint32_t* const keys = reinterpret_cast<uint32_t*>(s_lvl);
   uint32_t* const tmp = reinterpret_cast<uint32_t*>(s_lvl + g->oct2_tmp_off);
   int* const cpre = reinterpret_cast<int*>(s_lvl + g->oct2_cpre_off);
@@ -2034,9 +1755,6 @@ __global__ __launch_bounds__(kOctLvlThreads) void octree_lvl_kernel(
       }
   }
   __syncthreads();
-#ifdef OCT_PROFILE
-  oct_tg = wall_clock64();
-#endif
   if (w == 0) {
     int tot;
     const int bb = wave_excl_scan(lane < nIni ? s_bcnt[lane] : 0, lane, &tot);
@@ -2103,15 +1821,7 @@ __global__ __launch_bounds__(kOctLvlThreads) void octree_lvl_kernel(
   auto owner = [&](int j, int n) {
     return (n > kOctLaneKeys ? j : (j >> 6)) % kOctLvlWaves == w;
   };
-#ifdef OCT_PROFILE
-  oct_t1 = wall_clock64();
-#endif
   while (true) {
-#ifdef OCT_PROFILE
-    if (oct_passes < 8) oct_tp[oct_passes] = wall_clock64();
-    if (oct_passes < 8) oct_sz[oct_passes] = (outer ? 1 : -1) * m;
-    oct_passes++;
-#endif
     const OctNodeS* Lc = lists + cur * NC;
     OctNodeS* Ln = lists + (cur ^ 1) * NC;
     const int V = outer ? m : nexp;
@@ -2311,9 +2021,6 @@ __global__ __launch_bounds__(kOctLvlThreads) void octree_lvl_kernel(
   }
   // ---- 4. retain the best key of each node (:682-701): strict '>' keeps the first maximum
   __syncthreads();
-#ifdef OCT_PROFILE
-  oct_t2 = wall_clock64();
-#endif
   const OctNodeS* Lf = lists + cur * NC;
   const int mout = min(m, L.out_cap);
   for (int j = tid; j < mout; j += kOctLvlThreads) {
@@ -2330,18 +2037,6 @@ __global__ __launch_bounds__(kOctLvlThreads) void octree_lvl_kernel(
     if (m > L.out_cap) atomicOr(err, kErrNodeOverflow);
     *outc = mout;
   }
-#ifdef OCT_PROFILE
-  if (tid == 0 && img < 2 && (level == 0 || level == 7)) {
-    const uint64_t t3 = wall_clock64();
-    printf("octlvl img %d lvl %d K %d gather %d+%d passes %d (%d) retain %d x10ns | %d:%d %d:%d "
-           "%d:%d %d:%d %d:%d\n",
-           img, level, K, (int)(oct_tg - oct_t0), (int)(oct_t1 - oct_tg), (int)(oct_t2 - oct_t1),
-           oct_passes, (int)(t3 - oct_t2), oct_sz[0], (int)(oct_tp[1] - oct_tp[0]), oct_sz[1],
-           (int)(oct_tp[2] - oct_tp[1]), oct_sz[2], (int)(oct_tp[3] - oct_tp[2]), oct_sz[3],
-           (int)((oct_passes > 4 ? oct_tp[4] : oct_t2) - oct_tp[3]), oct_sz[4],
-           (int)(oct_t2 - oct_tp[oct_passes > 4 ? 4 : 3]));
-  }
-#endif
 }
 
 // ---------------------------------------------------------------------------------------
@@ -2388,89 +2083,19 @@ __device__ __forceinline__ int reduce_scatter16(int (&v)[16], int lane) {
 // column's rule (half to even inside the SSE span x < W - W%4, half up in the scalar tail).
 // Border keypoints (the window leaves the image: reflect-101 columns) load bytes one by one.
 // LDS: one 40 x 44 u16 window per wave.
-// OD_PAIRS: a lane task covers two window rows of its 4 columns and stores each column's pair
-// of u16 row sums as one dword (16 dword stores per lane and keypoint instead of 28 u16 ones),
-// over a 46-row (23-dword, odd) column stride: the 10 column quads of a row pair land on 8
-// distinct bank groups instead of 4. Measured (profiles/r3h_pmc.txt): LDS instructions -45 %,
-// LDS wait cycles 268 -> 24 per wave, but +13 % VALU (the packing) and 3-5 % slower -- the
-// kernel is bound by VALU issue, not by the LDS -- so off by default.
-#ifndef OD_PAIRS
-#define OD_PAIRS 0
-#endif
-#ifndef RT_ROWS
-#define RT_ROWS (OD_PAIRS ? 46 : 44)
-#endif
-// OD_MFMA: the horizontal 7-tap pass of the in-window keypoints (all but the border ones) as a
-// banded integer GEMM on the matrix cores: per keypoint 3 x 3 v_mfma_i32_16x16x32_i8 tiles, rows
-// of the window (A: raw bytes - 128, as int8) times a 32 x 16 band of the Gaussian taps shifted by
-// the window origin's misalignment (B, one of four lane constants); the int32 result + 128 * 257
-// is the exact u16 row sum, written transposed as 4-row u16 runs (one ds_write_b64 per tile) --
-// instead of ~140 VALU instructions and 28 u16 stores per keypoint and lane.
-// Measured 1.36-1.38 ms against 1.03 (profiles/r3j_ab.log; layout verified by
-// tools/mfma_i8_probe.hip, parity green): the VALU count per wave fell only 3 % and waves live
-// 28 % longer (MFMA result latency on the keypoint's critical path), so off.
-#ifndef OD_MFMA
-#define OD_MFMA 0
-#endif
-// the keypoint loop unrolled (non-MFMA build) or not; the MFMA build keeps it rolled and asks
-// for 4 waves per SIMD: 126 VGPRs, no AGPRs, no spills (unrolled: 159 + 8 AGPRs, 3 waves)
-#ifndef OD_UNROLL_J
-#define OD_UNROLL_J (OD_MFMA ? 0 : 1)
-#endif
-#if OD_MFMA && !defined(OD_WAVES)
-#define OD_WAVES 4
-#endif
-#ifndef RS_PREFETCH
-#define RS_PREFETCH 1
-#endif
-#ifndef OD_FENCE
-#define OD_FENCE 0
-#endif
-#ifndef PAT_PACKED
-#define PAT_PACKED 1
-#endif
-constexpr int kRtCols = 40, kRtRows = RT_ROWS;  // u16 per transposed column (even)
-// OD_SHIFTED: a second copy of the row-sum table shifted by one u16 (copy1[i] = copy0[i + 1]), so
-// that a sample whose 7 rows start at an odd u16 reads 4 aligned dwords of copy1 instead of
-// realigning copy0's with 4 v_alignbit: one extra ds_write_b16 per stored row sum (an immediate
-// offset) for 4-5 fewer VALU per sample. Bit-exact, but slower: 1.02 -> 1.11 ms per step at 4
-// waves/SIMD (profiles/r3zs_orient_desc_shifted_ab.log; twice the LDS stores per row sum), so off.
-#ifndef OD_SHIFTED
-#define OD_SHIFTED 0
-#endif
-constexpr int kRtN = kRtCols * kRtRows;  // u16 per copy
-constexpr int kRtCopy1 = kRtN + 2;       // copy1's u16 offset (dword-aligned; copy1[-1] is spare)
+// Variants measured and rejected in round 3 (dword row pairs, the horizontal pass on MFMA i8, a
+// shifted copy of the table) are in git history before round 4 and in DESIGN.md section 9.
+constexpr int kRtCols = 40, kRtRows = 44;  // u16 per transposed column (even)
+constexpr int kRtN = kRtCols * kRtRows;
 
-__device__ __forceinline__ uint32_t rt_tap(const uint16_t* rt, int sy, int sx, uint32_t K01,
-                                           uint32_t K23, uint32_t K21, uint32_t K0) {
-  const int e0 = (sx + 18) * kRtRows + sy + 18;  // rows sy - 3 .. sy + 3 of column sx
-  const uint32_t* rw = reinterpret_cast<const uint32_t*>(rt) + (e0 >> 1);
-  const uint32_t sh = (uint32_t)(e0 & 1) << 4;
-  const uint32_t w0 = rw[0], w1 = rw[1], w2 = rw[2], w3 = rw[3];
-  const uint32_t p0 = __builtin_amdgcn_alignbit(w1, w0, sh);
-  const uint32_t p1 = __builtin_amdgcn_alignbit(w2, w1, sh);
-  const uint32_t p2 = __builtin_amdgcn_alignbit(w3, w2, sh);
-  const uint32_t p3 = __builtin_amdgcn_alignbit(0u, w3, sh);
-  return dot2u(p0, K01, dot2u(p1, K23, dot2u(p2, K21, dot2u(p3, K0, 0u))));
-}
-
-#if OD_SHIFTED && !defined(OD_WAVES)
-#define OD_WAVES 4  // 131 VGPRs unbounded (3 waves/SIMD); 127 at this bound, no spills
-#endif
-#ifdef OD_WAVES
-#define OD_ATTR __attribute__((amdgpu_waves_per_eu(OD_WAVES)))
-#else
-#define OD_ATTR
-#endif
 // KPW (<= kKpPerWave) keypoints per wave: 8 for batches, 4 for small launches (more waves in
 // flight for the single-frame call)
 template <int KPW>
-__global__ __launch_bounds__(256) OD_ATTR void orient_desc_kernel(
+__global__ __launch_bounds__(256) void orient_desc_kernel(
     ImageBatch b, const OrbGeom* __restrict__ g, const uint32_t* __restrict__ oct_keys,
     const int* __restrict__ oct_count, KeyPoint* __restrict__ kps, uint8_t* __restrict__ desc,
     int* __restrict__ nkps) {
-  static_assert(!OD_SHIFTED || (!OD_PAIRS && !OD_MFMA), "the shifted copy takes the u16 stores");
-  __shared__ __attribute__((aligned(16))) uint16_t s_rt[4][1][OD_SHIFTED ? kRtCopy1 + kRtN : kRtN];
+  __shared__ __attribute__((aligned(16))) uint16_t s_rt[4][1][kRtN];
   int img, bx;
   xcd_image_block(&img, &bx);
   const int lane = threadIdx.x & 63, wid = wave_id();
@@ -2574,25 +2199,11 @@ __global__ __launch_bounds__(256) OD_ATTR void orient_desc_kernel(
   float sa, ca;
   glibc_sincosf(angle * factorPI, &sa, &ca);
   // Phase 3: per 4 keypoints, the row-summed windows (LDS) then the 512 blurred samples each
-#if PAT_PACKED
   // the lane's 4 tests (8 points) as int8 (x0, y0, x1, y1) words: 4 VGPRs instead of 32
   uint32_t pat[4];
 #pragma unroll
   for (int r = 0; r < 4; r++)
     pat[r] = reinterpret_cast<const uint32_t*>(c_pattern)[r * 64 + lane];
-#else
-  f32x2 ppx[4][2], ppy[4][2];
-#pragma unroll
-  for (int r = 0; r < 4; r++) {
-    const int t = r * 64 + lane;
-#pragma unroll
-    for (int e = 0; e < 2; e++) {
-      const float px = (float)c_pattern[4 * t + 2 * e], py = (float)c_pattern[4 * t + 2 * e + 1];
-      ppx[r][e] = (f32x2){px, px};
-      ppy[r][e] = (f32x2){py, py};
-    }
-  }
-#endif
   const uint32_t q0 = g->gauss[0], q1 = g->gauss[1], q2 = g->gauss[2], q3 = g->gauss[3];
   const uint32_t KA = q0 | q1 << 8 | q2 << 16 | q3 << 24, KB = q2 | q1 << 8 | q0 << 16;
   const uint32_t K01 = q0 | q1 << 16, K23 = q2 | q3 << 16, K21 = q2 | q1 << 16, K0 = q0;
@@ -2609,8 +2220,8 @@ __global__ __launch_bounds__(256) OD_ATTR void orient_desc_kernel(
   // Row-sum tasks: t = lane + 64 i -> window row r = t / 10, column quad gq = t % 10; a task's
   // raw bytes sit at r * pitch + 4 gq past the keypoint's window origin (a lane constant times
   // the level pitch: one v_mad_u32_u24, the origin a scalar base).
-  constexpr int kTaskRows = OD_PAIRS ? 2 : 1;              // window rows per lane task
-  constexpr int kTasks = (44 / kTaskRows - (OD_PAIRS ? 0 : 1)) * 10;  // 22 x 10 / 43 x 10
+  constexpr int kTaskRows = 1;              // window rows per lane task
+  constexpr int kTasks = 43 * 10;
   constexpr int kRounds = (kTasks + 63) / 64;
   int trow[kRounds], tcol[kRounds];  // trow < 0: no task (last round's padding)
 #pragma unroll
@@ -2621,7 +2232,7 @@ __global__ __launch_bounds__(256) OD_ATTR void orient_desc_kernel(
   }
   // Per keypoint: its row-summed window into LDS, then its 256 tests from LDS. The window's raw
   // rows (one 16-byte load per lane task, 7 tasks per lane) of keypoint j + 1 are in flight
-  // while keypoint j's tests run (RS_PREFETCH). LDS hand-offs are within the wave (LDS executes
+  // while keypoint j's tests run. LDS hand-offs are within the wave (LDS executes
   // a wave's instructions in order): only compiler ordering is needed between the passes.
   struct RsGeo {
     const uint8_t* im;
@@ -2663,92 +2274,16 @@ __global__ __launch_bounds__(256) OD_ATTR void orient_desc_kernel(
     }
   };
   uint16_t* rtw = &s_rt[wid][0][0];
-#if OD_MFMA
-  static_assert(!OD_PAIRS && RS_PREFETCH, "the MFMA row sums use the u16 layout and prefetch");
-  typedef int v4i_t __attribute__((ext_vector_type(4)));
-  const int mf_n = lane & 15, mf_h = lane >> 4;
-  // B operands: band[k][n] = k_(k - n - s) (0 outside the 7 taps) for window-origin shift s; lane
-  // (n, h) holds band[8 h + jb][n] in byte jb. Kept in the wave's LDS (read back per keypoint by
-  // its shift: one ds_read_b64) rather than in 8 VGPRs.
-  __shared__ uint64_t s_bm[4][4][64];
-#pragma unroll
-  for (int sv = 0; sv < 4; sv++) {
-    uint64_t v = 0;
-#pragma unroll
-    for (int jb = 0; jb < 8; jb++) {
-      const int d = 8 * mf_h + jb - mf_n - sv;
-      const uint32_t gv = (d >= 0 && d <= 6) ? (uint32_t)g->gauss[d] : 0u;
-      v |= (uint64_t)gv << (8 * jb);
-    }
-    s_bm[wid][sv][lane] = v;
-  }
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-  // A operands of tile (ti, tj): window row 16 ti + n (rows past 42 re-read row 42; never stored)
-  // bytes 16 tj + 8 h .. + 7 from the dword-aligned origin; bytes 48.. are never needed (the
-  // samples read window columns <= 36: bytes <= 36 + 3 + 6), loaded as 0x80 (int8 zero)
-  auto mf_load = [&](const RsGeo& G, uint2 (&a)[9]) {
-    if (!G.fastp) return;
-#pragma unroll
-    for (int ti = 0; ti < 3; ti++) {
-      const uint32_t row = (uint32_t)min(16 * ti + mf_n, 42);
-      const uint8_t* rp = G.org + __umul24(row, (uint32_t)G.pitch) + 8 * mf_h;
-#pragma unroll
-      for (int tj = 0; tj < 3; tj++)
-        a[3 * ti + tj] = (tj == 2 && mf_h >= 2) ? make_uint2(0x80808080u, 0x80808080u)
-                                                 : *reinterpret_cast<const uint2*>(rp + 16 * tj);
-    }
-  };
-  // lane's u16 index of its C rows 4 h .. 4 h + 3 of column n in tile (0, 0)
-  const int mf_st = mf_n * kRtRows + 4 * mf_h;
-#endif
   RsGeo gn = rs_geo(0);
-#if OD_MFMA
-  uint2 an[9];
-  mf_load(gn, an);
-#elif RS_PREFETCH
   uint4 qn[kRounds * kTaskRows];
   rs_load(gn, qn);
-#endif
-#if OD_UNROLL_J
 #pragma unroll
-#else
-#pragma unroll 1
-#endif
   for (int j = 0; j < KPW; j++) {
     const RsGeo G = gn;
     const uint32_t sft = (uint32_t)((G.kx - 21) & 3);
-#if OD_MFMA
-    uint2 a[9];
-#pragma unroll
-    for (int i = 0; i < 9; i++) a[i] = an[i];
-    if (G.fastp) {  // wave-uniform: every lane takes part in the MFMAs
-      const uint64_t B = s_bm[wid][sft][lane];
-      const v4i_t cinit = {128 * 257, 128 * 257, 128 * 257, 128 * 257};
-#pragma unroll
-      for (int ti = 0; ti < 3; ti++)
-#pragma unroll
-        for (int tj = 0; tj < 3; tj++) {
-          const uint2 v = a[3 * ti + tj];
-          const uint64_t A = (uint64_t)(v.y ^ 0x80808080u) << 32 | (v.x ^ 0x80808080u);
-          const v4i_t c = __builtin_amdgcn_mfma_i32_16x16x32_i8((long)A, (long)B, cinit, 0, 0, 0);
-          // rows >= 44 and columns >= 40 fall outside the window's LDS image
-          if (!(ti == 2 && mf_h == 3) && !(tj == 2 && mf_n >= 8))
-            *reinterpret_cast<uint2*>(rtw + mf_st + 16 * tj * kRtRows + 16 * ti) =
-                make_uint2((uint32_t)c[0] | (uint32_t)c[1] << 16,
-                           (uint32_t)c[2] | (uint32_t)c[3] << 16);
-        }
-    } else
-#else
     uint4 q[kRounds * kTaskRows];
-#if RS_PREFETCH
 #pragma unroll
     for (int i = 0; i < kRounds * kTaskRows; i++) q[i] = qn[i];
-#else
-    rs_load(G, q);
-#endif
-#endif
 #pragma unroll
     for (int i = 0; i < kRounds; i++) {
       if (trow[i] >= 0) {
@@ -2757,14 +2292,12 @@ __global__ __launch_bounds__(256) OD_ATTR void orient_desc_kernel(
 #pragma unroll
         for (int h = 0; h < kTaskRows; h++) {
           uint32_t u0, u1, u2;
-#if !OD_MFMA
           if (G.fastp) {
             const uint4 v = q[kTaskRows * i + h];
             u0 = __builtin_amdgcn_alignbyte(v.y, v.x, sft);
             u1 = __builtin_amdgcn_alignbyte(v.z, v.y, sft);
             u2 = __builtin_amdgcn_alignbyte(v.w, v.z, sft);
           } else
-#endif
           {  // the window leaves the level: reflect-101 rows and columns, byte loads
             const int rr = min(r + h, 42);
             const uint8_t* row = G.im + (int64_t)reflect101(G.ky - 21 + rr, G.h) * G.pitch;
@@ -2784,35 +2317,16 @@ __global__ __launch_bounds__(256) OD_ATTR void orient_desc_kernel(
           R[h][3] = __builtin_amdgcn_udot4(u0, C3a, __builtin_amdgcn_udot4(u1, C3b,
                                            __builtin_amdgcn_udot4(u2, C3c, 0u, false), false), false);
         }
-#if OD_PAIRS
-        // rows r, r + 1 of column 4 gq + jx: one dword at u16 index (4 gq + jx) * kRtRows + r
-        uint32_t* rtw32 = reinterpret_cast<uint32_t*>(rtw);
-#pragma unroll
-        for (int jx = 0; jx < 4; jx++)
-          rtw32[(4 * gq + jx) * (kRtRows / 2) + (r >> 1)] = (R[0][jx] & 0xffffu) | R[1][jx] << 16;
-#else
 #pragma unroll
         for (int jx = 0; jx < 4; jx++) {
           rtw[(4 * gq + jx) * kRtRows + r] = (uint16_t)R[0][jx];
-          if (OD_SHIFTED) rtw[kRtCopy1 - 1 + (4 * gq + jx) * kRtRows + r] = (uint16_t)R[0][jx];
         }
-#endif
       }
     }
-#if OD_FENCE
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-#else
     __asm__ volatile("" ::: "memory");
-#endif
     if (j + 1 < KPW) {
       gn = rs_geo(j + 1);
-#if OD_MFMA
-      mf_load(gn, an);
-#elif RS_PREFETCH
       rs_load(gn, qn);
-#endif
     }
     {
       const int kx = G.kx;
@@ -2837,11 +2351,6 @@ __global__ __launch_bounds__(256) OD_ATTR void orient_desc_kernel(
             const uint32_t cy = __float_as_uint(sp.x) - 0x4B400000u;  // window row of sy - 3
             const uint32_t cx = __float_as_uint(sp.y) - 0x4B400000u;  // window column
             const uint32_t e0 = __umul24(cx, (uint32_t)kRtRows) + cy;
-#if OD_SHIFTED
-            // an odd start (cy odd: kRtRows is even) reads copy1 at the same dword index
-            const uint32_t* rw = rt32 + (e0 >> 1) + (cy & 1u) * (uint32_t)(kRtCopy1 / 2);
-            const uint32_t p0 = rw[0], p1 = rw[1], p2 = rw[2], p3 = rw[3];  // p3's high u16 x 0
-#else
             const uint32_t* rw = rt32 + (e0 >> 1);
             const uint32_t sh = cy << 4;  // alignbit takes it mod 32: 16 for an odd start
             const uint32_t w0 = rw[0], w1 = rw[1], w2 = rw[2], w3 = rw[3];
@@ -2849,7 +2358,6 @@ __global__ __launch_bounds__(256) OD_ATTR void orient_desc_kernel(
             const uint32_t p1 = __builtin_amdgcn_alignbit(w2, w1, sh);
             const uint32_t p2 = __builtin_amdgcn_alignbit(w3, w2, sh);
             const uint32_t p3 = __builtin_amdgcn_alignbit(0u, w3, sh);
-#endif
             const uint32_t sm = dot2u(p0, K01, dot2u(p1, K23, dot2u(p2, K21, dot2u(p3, K0, 0u))));
             uint32_t o;
             if (kTail) {
@@ -2870,13 +2378,7 @@ __global__ __launch_bounds__(256) OD_ATTR void orient_desc_kernel(
       if (kx + 18 >= xvec) tests(std::true_type{});
       else tests(std::false_type{});
     }
-#if OD_FENCE
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-#else
     __asm__ volatile("" ::: "memory");
-#endif
   }
   const int64_t o = (int64_t)img * g->kp_cap + k0;
   if (lane < 4 * nk)
@@ -2956,46 +2458,7 @@ void launch_extract(const ImageBatch& b, const OrbGeomDev& gd, int n_images, hip
   const bool in_aligned = (((uintptr_t)b.in_l | (uintptr_t)b.in_r | (uintptr_t)b.in_stride |
                            (uintptr_t)b.in_pitch) & 3) == 0;
   const bool short_strips = n_images <= kPyrShortMaxImages;
-  // the fused band kernel is off by default (SLAMGPU_PYR_FUSED=1 selects it, for A/B): measured
-  // slower than the per-level launches (1.24 vs 0.52 ms per step alone)
-  static const int fused_mode = [] {
-    const char* e = std::getenv("SLAMGPU_PYR_FUSED");
-    return e ? std::atoi(e) : 0;
-  }();
-  bool fused = false;
-  if (fused_mode && g.nlevels > 1) {
-    const PyrBandSet& bs = *(short_strips ? gd.bands_small : gd.bands_big);
-    auto r16 = [](int v) { return (v + 15) & ~15; };
-    const bool c16 = (((uintptr_t)b.in_l | (uintptr_t)b.in_r | (uintptr_t)b.in_stride |
-                       (uintptr_t)b.in_pitch) & 15) == 0;
-    const int w0r = r16(g.lv[0].w);
-    const int copy = (c16 && b.in_pitch <= 2 * w0r) ? 0 : (in_aligned ? 1 : 2);
-    const int stride0 = copy == 0 ? b.in_pitch : w0r;
-    size_t buf0 = (size_t)bs.max_rows[0] * stride0, buf1 = 0;
-    for (int l = 1; l < g.nlevels; l++) {
-      const size_t s = (size_t)bs.max_rows[l] * r16(g.lv[l].w);
-      if (l & 1) buf1 = std::max(buf1, s); else buf0 = std::max(buf0, s);
-    }
-    const int half1 = (int)((buf0 + 15) & ~(size_t)15);
-    const int ry_off = (int)(half1 + ((buf1 + 15) & ~(size_t)15));
-    size_t ry_rows = 0;
-    for (int l = 1; l < g.nlevels; l++) ry_rows += bs.max_rows[l];
-    const size_t lds = (size_t)ry_off + 8 * ry_rows;
-    if (bs.dev && bs.rows && lds <= 160 * 1024) {
-      const dim3 grid(bs.nb, n_images);
-      if (copy == 0)
-        SLAMGPU_LAUNCH("pyr_down", st, pyr_band_kernel<0>, grid, dim3(kPyrBandThreads), lds, st,
-                       b, gd.dev, bs.rows, bs.dev, half1, stride0, ry_off);
-      else if (copy == 1)
-        SLAMGPU_LAUNCH("pyr_down", st, pyr_band_kernel<1>, grid, dim3(kPyrBandThreads), lds, st,
-                       b, gd.dev, bs.rows, bs.dev, half1, stride0, ry_off);
-      else
-        SLAMGPU_LAUNCH("pyr_down", st, pyr_band_kernel<2>, grid, dim3(kPyrBandThreads), lds, st,
-                       b, gd.dev, bs.rows, bs.dev, half1, stride0, ry_off);
-      fused = true;
-    }
-  }
-  for (int l = 1; l < g.nlevels && !fused; l++) {
+  for (int l = 1; l < g.nlevels; l++) {
     const int strip = short_strips ? kPyrShortStrip : kPyrStrip;
     const int tiles = ((g.lv[l].w + 255) >> 8) * ((g.lv[l].h + 4 * strip - 1) / (4 * strip));
     const dim3 grid(tiles, n_images);

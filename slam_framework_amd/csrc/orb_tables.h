@@ -30,15 +30,5 @@ int compute_geometry(const OrbParams& p, int cols, int rows, OrbGeom* g,
                      std::vector<ResizeX>* rx, std::vector<ResizeY>* ry);
 // FAST cell views of all levels, in the kernels' per-image cell order (cells_per_image entries).
 void build_cells(const OrbGeom& g, std::vector<CellDesc>* cells);
-// nb row bands of every level (nb * kMaxLevels entries, band-major) and their packed row-table
-// entries (two words per need row); max_rows[l] = the longest need range of level l over the
-// bands (the work-group's LDS is sized from it).
-void build_pyr_bands(const OrbGeom& g, const std::vector<ResizeY>& ry, int nb,
-                     std::vector<PyrBand>* bands, std::vector<uint32_t>* rows,
-                     int max_rows[kMaxLevels]);
-// The invariants pyr_band_kernel relies on: each level's own ranges partition its rows, and every
-// row a band computes resizes from rows the band computes one level down.
-bool check_pyr_bands(const OrbGeom& g, const std::vector<ResizeY>& ry, int nb,
-                     const std::vector<PyrBand>& bands);
 
 }  // namespace slamgpu

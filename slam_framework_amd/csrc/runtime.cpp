@@ -41,9 +41,6 @@ struct slamgpu_ctx {
   OrbGeom* d_geom = nullptr;
   ResizeX* d_rx = nullptr;
   ResizeY* d_ry = nullptr;
-  PyrBand* d_bands[2] = {nullptr, nullptr};
-  uint32_t* d_brows[2] = {nullptr, nullptr};
-  PyrBandSet pbands[2];  // fused pyramid: [0] batches, [1] small launches
   CellDesc* d_cells = nullptr;
   // images staged by the host-buffer calls (left at d_in, right at d_in + in_stride)
   uint8_t* d_in = nullptr;
@@ -99,8 +96,6 @@ struct slamgpu_ctx {
     g.dev = d_geom;
     g.rx = d_rx;
     g.ry = d_ry;
-    g.bands_big = &pbands[0];
-    g.bands_small = &pbands[1];
     g.cells = d_cells;
     g.ws = ws;
     g.out = out;
@@ -263,22 +258,6 @@ int slamgpu_create(int device, const slamgpu_orb_params* p, int cols, int rows, 
                        why[std::min(std::max(-gr, 0), 6)]);
   }
   compute_tables(c->params, &c->tables);
-  std::vector<PyrBand> bands[2];
-  std::vector<uint32_t> brows[2];
-  {  // fused pyramid band partitions (SLAMGPU_PYR_NB / SLAMGPU_PYR_NB_SMALL override, A/B)
-    const char* e0 = getenv("SLAMGPU_PYR_NB");
-    const char* e1 = getenv("SLAMGPU_PYR_NB_SMALL");
-    const int nb[2] = {std::min(std::max(e0 ? atoi(e0) : kPyrBandsBatch, 1), 1024),
-                       std::min(std::max(e1 ? atoi(e1) : kPyrBandsSmall, 1), 1024)};
-    for (int i = 0; i < 2; i++) {
-      c->pbands[i].nb = nb[i];
-      build_pyr_bands(c->geom, ry, nb[i], &bands[i], &brows[i], c->pbands[i].max_rows);
-      if (!check_pyr_bands(c->geom, ry, nb[i], bands[i])) {  // never expected: keep the
-        bands[i].clear();                                    // per-level kernels then
-        c->pbands[i].nb = 0;
-      }
-    }
-  }
   if (c->geom.kp_cap > 4096) {  // matcher keys carry a 12-bit keypoint index
     const int kpc = c->geom.kp_cap;
     delete c;
@@ -332,18 +311,6 @@ int slamgpu_create(int device, const slamgpu_orb_params* p, int cols, int rows, 
   TRY(hcheck(c, hipMemcpy(c->d_geom, &g, sizeof(OrbGeom), hipMemcpyHostToDevice)));
   TRY(hcheck(c, hipMemcpy(c->d_rx, rx.data(), rx.size() * sizeof(ResizeX), hipMemcpyHostToDevice)));
   TRY(hcheck(c, hipMemcpy(c->d_ry, ry.data(), ry.size() * sizeof(ResizeY), hipMemcpyHostToDevice)));
-  for (int i = 0; i < 2; i++) {
-    if (c->pbands[i].nb == 0) continue;
-    TRY(dalloc(c, &c->d_bands[i], bands[i].size()));
-    TRY(hcheck(c, hipMemcpy(c->d_bands[i], bands[i].data(), bands[i].size() * sizeof(PyrBand),
-                            hipMemcpyHostToDevice)));
-    c->pbands[i].dev = c->d_bands[i];
-    TRY(dalloc(c, &c->d_brows[i], brows[i].size() + 2));
-    if (!brows[i].empty())
-      TRY(hcheck(c, hipMemcpy(c->d_brows[i], brows[i].data(), brows[i].size() * sizeof(uint32_t),
-                              hipMemcpyHostToDevice)));
-    c->pbands[i].rows = reinterpret_cast<const uint2*>(c->d_brows[i]);
-  }
   TRY(hcheck(c, hipMemcpy(c->d_cells, cells.data(), cells.size() * sizeof(CellDesc),
                           hipMemcpyHostToDevice)));
   c->in_pitch = (cols + 63) / 64 * 64;

@@ -131,12 +131,15 @@ class FrameGather:
                 dist.gather(host, glist, dst=0)
             else:
                 glist[0].copy_(host)
-        elif self.world > 1:
+        elif self.active:
+            # any initialised process group takes the collective, world 1 included, so the
+            # RCCL gather and the Work.wait() ordering that slot reuse relies on are exercised
+            # by a one-GPU run (tests/test_sharded_gpu.py::test_world1_rccl_gather)
             glist = list(self.recv[s].unbind(0)) if self.rank == 0 else None
             self.work[s] = dist.gather(self.send[s], glist, dst=0, async_op=async_op)
             if not async_op:
                 self.work[s] = None
-        elif self.rank == 0:
+        else:   # no process group: a local copy
             self.recv[s][0].copy_(self.send[s])
         self.k += 1
         return s

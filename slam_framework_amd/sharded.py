@@ -225,7 +225,10 @@ class ShardedFrontend:
         checked = 0
         for j in range(j0, world * F, max(1, (world * F - j0) // 64)):
             g = j + 1
-            a, b = got[j], own[(g % self.D, (g - 1) % self.D)]
+            b = own.get((g % self.D, (g - 1) % self.D))
+            if b is None:   # rank 0 owns fewer frames than the sequence has render pairs
+                continue
+            a = got[j]
             if not frame_results_equal(a, b):
                 raise AssertionError(f"gathered frame {g} differs from rank 0's own result")
             checked += 1

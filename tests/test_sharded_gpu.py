@@ -7,6 +7,8 @@ the object bench.py times (slam_framework_amd.sharded.ShardedFrontend).
   keypoints and descriptors, u_right / depth, the frame-to-frame map-point ids and match count
   (frame.cpp:61-111, tracker.cpp:756-824, orb_matcher.cpp:1312-1453) -- and the bench's own
   gather self-check (ShardedFrontend.check_gather) passes.
+* world 1 over RCCL (a "nccl" process group in a child process): FrameGather's dist.gather
+  branch, five steps over two slots, every gathered frame against the oracle.
 * world 2 (two processes on cuda:0, gloo through host memory, since RCCL needs a GPU per rank):
   the shards + halos gathered to rank 0 reassemble exactly the world-1 job's gathered bytes."""
 import os
@@ -40,19 +42,20 @@ def world1(gpu_lib):
     return job, last, Ls, Rs
 
 
-def test_world1_gather_matches_oracle(oracle, world1):
-    job, last, Ls, Rs = world1
-    got = job.gathered()
-    assert [d["frame"] for d in got] == list(range(1, 9))
+def _check_vs_oracle(oracle, got, gframe, Bs, poses, D, Ls, Rs, parts=None):
+    """Every gathered frame against the oracle: left/right keypoints and descriptors, u_right /
+    depth, and the frame-to-frame search against f - 1 (poses[b] of the batch slot b owning f).
+    The search needs `parts`, the device buffers of a job that ran in this process (its VO
+    queries are checked and searched by the oracle); without them only the extraction and
+    stereo fields are checked."""
     t = oracle.tables()
     g = oracle.grid_geom(COLS, ROWS)
-    _, _, parts = job.groups[last]
     cache = {}
 
     def orc(f):
         if f not in cache:
-            kl, dl, pl = oracle.extract(t, Ls[f % job.D], True)
-            kr, dr, pr = oracle.extract(t, Rs[f % job.D], True)
+            kl, dl, pl = oracle.extract(t, Ls[f % D], True)
+            kr, dr, pr = oracle.extract(t, Rs[f % D], True)
             ur, depth, _ = oracle.stereo(t, kl, dl, kr, dr, pl, pr, CAM[0], CAM[4])
             cache[f] = (kl, dl, kr, dr, ur, depth)
         return cache[f]
@@ -64,11 +67,11 @@ def test_world1_gather_matches_oracle(oracle, world1):
         assert d["kps_right"].tobytes() == kr.tobytes(), f"frame {f} right keypoints"
         assert np.array_equal(d["desc_left"], dl) and np.array_equal(d["desc_right"], dr)
         assert d["u_right"].tobytes() == ur.tobytes() and d["depth"].tobytes() == depth.tobytes()
-        # the frame-to-frame search against f - 1 on the queries the device built (batch slot i
-        # of context si holds global frame f)
+        if parts is None:   # the search is checked against a job of this process instead
+            continue
         # the batch slot that owns frame f (f also appears as the next context's halo slot 0)
-        b = [int(x) for x in np.nonzero(job.gframe == f)[0] if x % job.Bs != 0][0]
-        si, i = divmod(b, job.Bs)
+        b = [int(x) for x in np.nonzero(gframe == f)[0] if x % Bs != 0][0]
+        si, i = divmod(b, Bs)
         pt = parts[si]
         qs, qc = pt["qs"].cpu().numpy(), pt["qc"].cpu().numpy()
         q = pt["q"].cpu().numpy().view(G.F2F_QUERY_DTYPE)[qs[i]:qs[i] + qc[i]]
@@ -84,7 +87,7 @@ def test_world1_gather_matches_oracle(oracle, world1):
         mdesc[idx] = q["desc"]
         nobs = np.zeros(n_last, np.int32)
         nobs[idx] = 1
-        p = job.poses[b]
+        p = poses[b]
         mp_o = np.full(len(kl), -1, np.int32)
         nm_o = oracle.search_frame(t, g, kl, dl, ur, mp_o, pkl, last_mp,
                                    np.zeros(n_last, np.uint8), xyz, mdesc, nobs,
@@ -92,6 +95,14 @@ def test_world1_gather_matches_oracle(oracle, world1):
                                    float(p["baseline"]), CAM, 7.0, 0, 1)
         assert d["nmatches"] == nm_o > 300, f"frame {f}: {d['nmatches']} vs {nm_o}"
         np.testing.assert_array_equal(d["map_point"], mp_o)
+
+
+def test_world1_gather_matches_oracle(oracle, world1):
+    job, last, Ls, Rs = world1
+    got = job.gathered()
+    assert [d["frame"] for d in got] == list(range(1, 9))
+    _, _, parts = job.groups[last]
+    _check_vs_oracle(oracle, got, job.gframe, job.Bs, job.poses, job.D, Ls, Rs, parts)
     info = job.check_gather()
     assert info["identical"] and info["frames_checked_vs_rank0"] == 8
 
@@ -107,21 +118,7 @@ def _free_port():
 def test_world2_shards_reassemble_world1(world1, tmp_path):
     job, _, _, _ = world1
     out = str(tmp_path / "rank0.npz")
-    port = _free_port()
-    script = os.path.join(os.path.dirname(os.path.abspath(__file__)), "sharded_gpu_job.py")
-    procs = []
-    for r in range(2):
-        env = dict(os.environ, RANK=str(r), WORLD_SIZE="2", LOCAL_RANK="0",
-                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-        procs.append(subprocess.Popen([sys.executable, "-u", script, out], env=env))
-    rcs = []
-    for p in procs:
-        try:
-            rcs.append(p.wait(timeout=100))
-        except subprocess.TimeoutExpired:
-            for q in procs:
-                q.kill()
-            raise
+    rcs = _run_ranks(out, 2, "gloo")
     assert rcs == [0, 0], rcs
     w2 = np.load(out)
     assert w2["frames"].tolist() == list(range(1, 9))
@@ -140,3 +137,50 @@ def test_world2_shards_reassemble_world1(world1, tmp_path):
                 assert np.array_equal(w2[k][j].view(np.int32)[:n], ref[j].view(np.int32)[:n]), j
         else:
             assert np.array_equal(w2[k], ref), k
+
+
+def _run_ranks(out, world, backend):
+    port = _free_port()
+    script = os.path.join(os.path.dirname(os.path.abspath(__file__)), "sharded_gpu_job.py")
+    procs = []
+    for r in range(world):
+        env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(world), LOCAL_RANK="0",
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, "-u", script, out, backend], env=env))
+    rcs = []
+    for p in procs:
+        try:
+            rcs.append(p.wait(timeout=100))
+        except subprocess.TimeoutExpired:
+            for q in procs:
+                q.kill()
+            raise
+    return rcs
+
+
+def test_world1_rccl_gather(oracle, world1, tmp_path):
+    """FrameGather's collective branch on RCCL: a world-1 "nccl" process group (created before
+    any other GPU work, TCP store on 127.0.0.1), ShardedFrontend(gather=True, inflight=2) for 5
+    steps over 2 gather slots, so steps 3-5 reuse a slot whose async dist.gather Work was waited
+    on the compute stream. Every frame rank 0 gathered equals the oracle (extraction, stereo) and
+    the world-1 local-copy job, whose frame-to-frame search the oracle checked, byte for byte."""
+    job, _, Ls, Rs = world1
+    out = str(tmp_path / "rccl.npz")
+    assert _run_ranks(out, 1, "nccl") == [0]
+    w = np.load(out)
+    assert int(w["steps"]) == J.NCCL_STEPS and int(w["checked"]) == 8
+    assert w["frames"].tolist() == list(range(1, 9))
+    assert np.array_equal(w["gframe"], job.gframe)
+    recs = [G.unpack_frame_record(r, job.kc) for r in w["frontend"]]
+    mps, nms = w["map_point"].view(np.int32), w["nmatches"].view(np.int32).reshape(-1)
+    got = []
+    for j, d in enumerate(recs):
+        d["map_point"] = mps[j][:len(d["kps_left"])].copy()
+        d["nmatches"] = int(nms[j])
+        d["frame"] = j + 1
+        got.append(d)
+    _check_vs_oracle(oracle, got, job.gframe, job.Bs, job.poses, job.D, Ls, Rs)
+    ref = {d["frame"]: d for d in job.gathered()}
+    from slam_framework_amd.sharded import frame_results_equal
+    for d in got:
+        assert frame_results_equal(d, ref[d["frame"]]), f"frame {d['frame']}"

@@ -1,5 +1,5 @@
 """A/B timing of environment variants of one build:
-    python tools/ab_env.py "SLAMGPU_PYR_FUSED=0" "SLAMGPU_PYR_NB=16" ... [-- bench args]
+    python tools/ab_env.py "SLAMGPU_FORK=0" "SLAMGPU_OCT_LVL=1" ... [-- bench args]
 Each variant is a comma-separated list of NAME=VALUE settings ("-" for none). Runs bench.py once
 per variant, each under its own time limit, and prints the step time, throughput and per-kernel
 ms. Stops at the first failing run."""
