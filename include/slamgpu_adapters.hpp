@@ -368,30 +368,229 @@ inline F2FInput gather_search_by_projection_frame(const FrameView& current, cons
   return in;
 }
 
-// The current frame's claim state before the search: slot[i] = the map point's query position
-// when keypoint i already holds one of the queried map points, else -1; blocked[i] = its map
-// point has observations (:1389-1393 skips such keypoints).
-inline void f2f_current_state(const FrameView& current, const MapPointView* mps,
-                              int32_t* slot, uint8_t* blocked) {
+// The current frame's claim state before either SearchByProjection: slot[i] = -1 (no query has
+// claimed keypoint i yet); blocked[i] = its map point has observations -- both overloads skip
+// such keypoints (:1389-1393, :59-63), including the ones claimed earlier in the same call.
+inline void current_claim_state(const FrameView& current, const MapPointView* mps,
+                                int32_t* slot, uint8_t* blocked) {
   for (int i = 0; i < current.n_kps; ++i) {
     const int m = current.map_points[i];
     slot[i] = -1;
     blocked[i] = m >= 0 && mps[m].n_obs > 0;
   }
 }
+inline void f2f_current_state(const FrameView& current, const MapPointView* mps,
+                              int32_t* slot, uint8_t* blocked) {
+  current_claim_state(current, mps, slot, blocked);
+}
 
-// After the call: the current frame's map point per keypoint -- the queried map point a slot was
-// given (CurrentFrame.SetMapPoint(bestIdx2, pMP), :1414-1415), the previous one elsewhere.
+// After a call: the current frame's map point per keypoint -- the queried map point a slot was
+// given (F.SetMapPoint(bestIdx, pMP): :1414-1415, :99-100), the previous one elsewhere.
 // Returns the number of slots the search assigned.
-inline int apply_search_by_projection_frame(const F2FInput& in, const int32_t* slot,
-                                            int32_t* current_map_points, int n) {
+inline int apply_claims(const std::vector<int32_t>& query_map_point, const int32_t* slot,
+                        int32_t* current_map_points, int n) {
   int assigned = 0;
   for (int i = 0; i < n; ++i)
     if (slot[i] >= 0) {
-      current_map_points[i] = in.query_map_point[slot[i]];
+      current_map_points[i] = query_map_point[slot[i]];
       ++assigned;
     }
   return assigned;
 }
+inline int apply_search_by_projection_frame(const F2FInput& in, const int32_t* slot,
+                                            int32_t* current_map_points, int n) {
+  return apply_claims(in.query_map_point, slot, current_map_points, n);
+}
+
+// The whole call on frame `frame` of the context's last frame / frontend call: gather, claim
+// state, slamgpu_search_by_projection_frame, write-back into current_map_points (the frame's
+// map point indices, in/out). Returns the reference's nmatches; throws on a device error.
+inline int search_by_projection_frame(slamgpu_ctx* ctx, int frame, const FrameView& current,
+                                      const FrameView& last, const MapPointView* mps,
+                                      float baseline, float th, bool mono, bool check_ori,
+                                      int32_t* current_map_points) {
+  const F2FInput in = gather_search_by_projection_frame(current, last, mps, baseline, th, mono,
+                                                        check_ori);
+  std::vector<int32_t> slot(current.n_kps);
+  std::vector<uint8_t> blocked(current.n_kps);
+  current_claim_state(current, mps, slot.data(), blocked.data());
+  int nm = 0;
+  const int rc = slamgpu_search_by_projection_frame(ctx, frame, in.queries.data(),
+                                                    (int)in.queries.size(), &in.pose, slot.data(),
+                                                    blocked.data(), current.n_kps, &nm);
+  if (rc != SLAMGPU_OK) throw std::runtime_error(std::string("slamgpu: ") + slamgpu_last_error(ctx));
+  apply_search_by_projection_frame(in, slot.data(), current_map_points, current.n_kps);
+  return nm;
+}
+
+// ---- OrbMatcher::SearchByProjection(Frame&, const vector<MapPoint*>&, th) (orb_matcher.cpp:13) --
+
+// A map point's tracking fields, MapPoint::track_* as Frame::IsInFrustum (frame.cpp:277-337)
+// left them when Tracker::SearchLocalPoints (tracker.cpp:1176-1227) ran it on the current frame.
+struct TrackView {
+  bool in_view;             // track_is_in_view
+  float proj_x, proj_y;     // track_projected_x / _y
+  float proj_xr;            // track_projected_x_right
+  float view_cos;           // track_view_cos
+  int32_t level;            // track_scale_level
+};
+
+struct MpsInput {
+  std::vector<slamgpu_mps_query> queries;  // one per in-view, not-bad point of vpMapPoints
+  std::vector<int32_t> query_map_point;    // map point index of each query (mp_id = position)
+};
+
+// The queries of :18-26 in vpMapPoints order (a point that is not in view or is bad does nothing
+// in the reference's loop, so it is left out), with the fields the loop reads: the track_*
+// values, NumObservations() > 0 (the claim it makes blocks later points, :59-63) and
+// GetDescriptor(). `track` is indexed like `mps` (the fields live on the MapPoint).
+inline MpsInput gather_search_by_projection_mps(const int32_t* map_points, int n,
+                                                const MapPointView* mps, const TrackView* track) {
+  MpsInput in;
+  for (int i = 0; i < n; ++i) {
+    const int m = map_points[i];
+    const TrackView& t = track[m];
+    if (!t.in_view || mps[m].bad) continue;
+    slamgpu_mps_query q{};
+    q.proj_x = t.proj_x;
+    q.proj_y = t.proj_y;
+    q.proj_xr = t.proj_xr;
+    q.view_cos = t.view_cos;
+    q.level = t.level;
+    q.in_view = 1;
+    q.is_bad = 0;
+    q.mp_id = (int32_t)in.queries.size();
+    q.blocks = mps[m].n_obs > 0;
+    std::memcpy(q.desc, mps[m].desc, 32);
+    in.queries.push_back(q);
+    in.query_map_point.push_back(m);
+  }
+  return in;
+}
+
+inline int apply_search_by_projection_mps(const MpsInput& in, const int32_t* slot,
+                                          int32_t* current_map_points, int n) {
+  return apply_claims(in.query_map_point, slot, current_map_points, n);
+}
+
+// The whole call (SearchLocalPoints' matcher.SearchByProjection(current_frame_,
+// local_map_points_, th) with OrbMatcher(nnratio)): gather, claim state,
+// slamgpu_search_by_projection_mps, write-back. Returns nmatches; throws on a device error.
+inline int search_by_projection_mps(slamgpu_ctx* ctx, int frame, const FrameView& current,
+                                    const MapPointView* mps, const int32_t* map_points, int n,
+                                    const TrackView* track, float nnratio, int th,
+                                    int32_t* current_map_points) {
+  const MpsInput in = gather_search_by_projection_mps(map_points, n, mps, track);
+  std::vector<int32_t> slot(current.n_kps);
+  std::vector<uint8_t> blocked(current.n_kps);
+  current_claim_state(current, mps, slot.data(), blocked.data());
+  int nm = 0;
+  const int rc = slamgpu_search_by_projection_mps(ctx, frame, in.queries.data(),
+                                                  (int)in.queries.size(), nnratio, th,
+                                                  slot.data(), blocked.data(), current.n_kps, &nm);
+  if (rc != SLAMGPU_OK) throw std::runtime_error(std::string("slamgpu: ") + slamgpu_last_error(ctx));
+  apply_search_by_projection_mps(in, slot.data(), current_map_points, current.n_kps);
+  return nm;
+}
+
+// ---- the stereo Frame ctor (frame.cpp:61-111) ----------------------------------------------------
+
+// What the stereo ctor leaves in the Frame: both views' keypoints and descriptors (ExtractORB
+// :86-89), the undistorted left keypoints (:96), StereoCoordRight / StereoDepth
+// (ComputeStereoMatches :97), map points all null and no outliers (:99-100).
+struct StereoFrame {
+  int N = 0;                                     // num_keypoints_ (left view)
+  std::vector<slamgpu_keypoint> keys, keys_right, undist_keys;
+  std::vector<uint8_t> desc, desc_right;         // N x 32, N_right x 32
+  std::vector<float> right_coords, depth;        // N each, -1 = no stereo match
+  std::vector<int32_t> map_points;               // N x -1
+  std::vector<uint8_t> outlier;                  // N x 0
+};
+
+// One device context per tracker holding the current frame (frame 0): Make() runs
+// slamgpu_frame_stereo (extraction of both views + ComputeStereoMatches + undistortion + the
+// grid) and downloads what the Frame keeps; the matchers above then run on the same context
+// (frame 0) against the frame's device-resident grid. The context is created on the first call
+// and again when the image size changes; the distortion is set once per context.
+class StereoFrameCore {
+ public:
+  StereoFrameCore(const slamgpu_orb_params& params, const slamgpu_camera& cam,
+                  const float* dist_coef = nullptr, int n_dist = 0, int device = 0)
+      : params_(params), cam_(cam), dist_(dist_coef, dist_coef + (dist_coef ? n_dist : 0)),
+        device_(device) {}
+  ~StereoFrameCore() { slamgpu_destroy(ctx_); }
+  StereoFrameCore(const StereoFrameCore&) = delete;
+  StereoFrameCore& operator=(const StereoFrameCore&) = delete;
+
+  // frame.cpp:61-111 on two 8-bit images of the same size and row step. An empty left view
+  // leaves N = 0 and the rest empty (:91-94).
+  void Make(const uint8_t* left, const uint8_t* right, int rows, int cols, size_t step,
+            StereoFrame& f) {
+    f = StereoFrame();
+    if (!left || !right || rows <= 0 || cols <= 0) return;
+    ensure(cols, rows);
+    check(slamgpu_frame_stereo(ctx_, left, right, step, &cam_));
+    const int cap = slamgpu_kp_capacity(ctx_);
+    int n = 0, nr = 0, ns = 0, nu = 0;
+    f.keys.resize(cap);
+    f.desc.resize((size_t)cap * 32);
+    check(slamgpu_download_keypoints(ctx_, 0, f.keys.data(), f.desc.data(), cap, &n));
+    f.keys_right.resize(cap);
+    f.desc_right.resize((size_t)cap * 32);
+    check(slamgpu_download_keypoints(ctx_, 1, f.keys_right.data(), f.desc_right.data(), cap, &nr));
+    f.keys.resize(n);
+    f.desc.resize((size_t)n * 32);
+    f.keys_right.resize(nr);
+    f.desc_right.resize((size_t)nr * 32);
+    f.N = n;
+    if (n == 0) return;
+    f.right_coords.resize(n);
+    f.depth.resize(n);
+    check(slamgpu_download_stereo(ctx_, 0, f.right_coords.data(), f.depth.data(), n, &ns));
+    f.undist_keys.resize(n);
+    check(slamgpu_download_undistorted_keypoints(ctx_, 0, f.undist_keys.data(), n, &nu));
+    if (ns != n || nu != n) throw std::logic_error("slamgpu: inconsistent frame downloads");
+    f.map_points.assign(n, -1);
+    f.outlier.assign(n, 0);
+  }
+
+  // A FrameView of `f` (pose Tcw: 4x4 row-major, caller-owned) for the matchers and
+  // PoseOptimization above.
+  static FrameView view(const StereoFrame& f, const float* Tcw) {
+    FrameView v;
+    v.Tcw = Tcw;
+    v.kps = f.keys.data();
+    v.undist_kps = f.undist_keys.data();
+    v.right_coords = f.right_coords.data();
+    v.map_points = f.map_points.data();
+    v.outlier = f.outlier.data();
+    v.n_kps = f.N;
+    return v;
+  }
+
+  slamgpu_ctx* context() { return ctx_; }
+
+ private:
+  void ensure(int cols, int rows) {
+    if (ctx_ && cols == cols_ && rows == rows_) return;
+    slamgpu_destroy(ctx_);
+    ctx_ = nullptr;
+    check(slamgpu_create(device_, &params_, cols, rows, 1, &ctx_));
+    if (!dist_.empty()) check(slamgpu_set_distortion(ctx_, dist_.data(), (int)dist_.size()));
+    cols_ = cols;
+    rows_ = rows;
+  }
+  void check(int rc) const {
+    if (rc != SLAMGPU_OK) throw std::runtime_error(std::string("slamgpu: ") +
+                                                   slamgpu_last_error(ctx_));
+  }
+
+  slamgpu_orb_params params_;
+  slamgpu_camera cam_;
+  std::vector<float> dist_;
+  int device_;
+  slamgpu_ctx* ctx_ = nullptr;
+  int cols_ = 0, rows_ = 0;
+};
 
 }  // namespace slamgpu_adapter

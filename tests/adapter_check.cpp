@@ -1,5 +1,5 @@
 // adapter_check.cpp -- drives include/slamgpu_adapters.hpp (the OpenCV-free graph gathering and
-// write-back of Optimizer / OrbMatcher) on a map read from a file, and writes every record the
+// write-back of Optimizer / both per-frame OrbMatcher::SearchByProjection) on a map read from a file, and writes every record the
 // helpers produce, for tests/test_adapters.py to compare with its own restatement of
 // optimizer.cpp / orb_matcher.cpp. Test infrastructure; CPU only (the one library call,
 // slamgpu_orb_scale_tables, touches no device).
@@ -114,6 +114,19 @@ int main(int argc, char** argv) {
   op.nlevels = r.i32();
   op.ini_th_fast = r.i32();
   op.min_th_fast = r.i32();
+  // Tracker::SearchLocalPoints' local map point list and every map point's track_* fields
+  const int n_local = r.i32();
+  const int32_t* local = r.take<int32_t>(n_local);
+  std::vector<A::TrackView> track(n_mp);
+  for (auto& t : track) {
+    t.in_view = r.i32() != 0;
+    const float* f = r.take<float>(4);
+    t.proj_x = f[0];
+    t.proj_y = f[1];
+    t.proj_xr = f[2];
+    t.view_cos = f[3];
+    t.level = r.i32();
+  }
 
   Writer w;
   // Optimizer::PoseOptimization on the current frame; then an outlier per odd edge
@@ -166,6 +179,17 @@ int main(int argc, char** argv) {
   std::vector<int32_t> after(cur.map_points, cur.map_points + cur.n_kps);
   w.i32(A::apply_search_by_projection_frame(in, slot.data(), after.data(), cur.n_kps));
   w.put(after.data(), after.size());
+  // OrbMatcher::SearchByProjection(current, local map points, th); then a synthetic claim pattern
+  const A::MpsInput mi = A::gather_search_by_projection_mps(local, n_local, mps.data(),
+                                                            track.data());
+  w.i32((int32_t)mi.queries.size());
+  w.put(mi.queries.data(), mi.queries.size());
+  w.put(mi.query_map_point.data(), mi.query_map_point.size());
+  const int nmq = (int)mi.queries.size();
+  for (int i = 0; i < cur.n_kps; ++i) slot[i] = (nmq > 0 && i % 3 == 1) ? (7 * i) % nmq : -1;
+  std::vector<int32_t> after_mps(cur.map_points, cur.map_points + cur.n_kps);
+  w.i32(A::apply_search_by_projection_mps(mi, slot.data(), after_mps.data(), cur.n_kps));
+  w.put(after_mps.data(), after_mps.size());
   // ORBextractor's getters without a device context
   const A::OrbTables t = A::orb_scale_tables(op);
   w.i32(t.rc);

@@ -13,10 +13,18 @@
 //                                   kf_mode[n_kf] u8 (zero-padded to a multiple of 4),
 //                                   n_points i32, points[3 n_points] f32,
 //                                   point_obs_start[n_points + 1] i32, obs[n_obs]
+//         <dir>/stereo.bin          cols, rows, nfeatures i32, camera[5] f32, left, right u8
+//         <dir>/mps.bin             n_mp i32, per map point: bad, n_obs i32, desc[32], in_view
+//                                   i32, proj_x, proj_y, proj_xr, view_cos f32, level i32;
+//                                   n_local i32, local[n_local] i32, nnratio f32, th i32,
+//                                   n i32, the current frame's map points[n] i32
 // writes  <dir>/extract.kps, extract.desc      (n x 28, n x 32 bytes)
 //         <dir>/pose.out            n_inliers i32, Tcw[16] f32, outlier[n] u8
 //         <dir>/lba.out             lm_iterations i32, kf_Tcw[16 n_kf], points[3 n_points],
 //                                   erase[n_obs] u8
+//         <dir>/stereo.out          N, N_right i32, keys[N], desc[N], keys_right, desc_right,
+//                                   right_coords[N], depth[N] f32, undist_keys[N]
+//         <dir>/mps.out             nmatches i32, map points after the call[n] i32
 #include <cstdio>
 #include <cstdlib>
 #include <string>
@@ -84,7 +92,7 @@ int main(int argc, char** argv) {
   }
   const std::string dir = argv[1];
   for (const char* f : {"/extract.kps", "/extract.desc", "/core.kps", "/core.desc", "/core.pyr1",
-                        "/pose.out", "/lba.out"})
+                        "/pose.out", "/lba.out", "/stereo.out", "/mps.out"})
     std::remove((dir + f).c_str());
 
   // ---- ORBextractor::Compute ----
@@ -173,6 +181,66 @@ int main(int argc, char** argv) {
     spit(dir + "/lba.out", kf.data(), kf.size() * 4);
     spit(dir + "/lba.out", pts.data(), pts.size() * 4);
     spit(dir + "/lba.out", erase.data(), no);
+  }
+  // ---- the stereo Frame ctor (slamgpu_adapters.hpp StereoFrameCore over slamgpu_frame_stereo),
+  // then SearchByProjection(F, vpMapPoints, th) on that frame through the adapter's one call ----
+  {
+    const std::vector<char> b = slurp(dir + "/stereo.bin");
+    Reader r{b};
+    const int sc = *r.take<int32_t>(1), sr = *r.take<int32_t>(1), sn = *r.take<int32_t>(1);
+    const slamgpu_camera cam = *r.take<slamgpu_camera>(1);
+    const uint8_t* left = r.take<uint8_t>((size_t)sc * sr);
+    const uint8_t* right = r.take<uint8_t>((size_t)sc * sr);
+    const slamgpu_orb_params sp = {sn, 1.2f, 8, 20, 7};
+    slamgpu_adapter::StereoFrameCore core(sp, cam);
+    slamgpu_adapter::StereoFrame f;
+    core.Make(left, right, sr, sc, (size_t)sc, f);
+    const std::string so = dir + "/stereo.out";
+    const int32_t nn[2] = {f.N, (int32_t)f.keys_right.size()};
+    spit(so, nn, sizeof nn);
+    spit(so, f.keys.data(), sizeof(slamgpu_keypoint) * f.keys.size());
+    spit(so, f.desc.data(), f.desc.size());
+    spit(so, f.keys_right.data(), sizeof(slamgpu_keypoint) * f.keys_right.size());
+    spit(so, f.desc_right.data(), f.desc_right.size());
+    spit(so, f.right_coords.data(), 4 * f.right_coords.size());
+    spit(so, f.depth.data(), 4 * f.depth.size());
+    spit(so, f.undist_keys.data(), sizeof(slamgpu_keypoint) * f.undist_keys.size());
+
+    const std::vector<char> m = slurp(dir + "/mps.bin");
+    Reader q{m};
+    const int n_mp = *q.take<int32_t>(1);
+    std::vector<slamgpu_adapter::MapPointView> mps(n_mp);
+    std::vector<slamgpu_adapter::TrackView> track(n_mp);
+    for (int i = 0; i < n_mp; ++i) {
+      mps[i] = slamgpu_adapter::MapPointView{};
+      mps[i].id = i;
+      mps[i].bad = *q.take<int32_t>(1) != 0;
+      mps[i].n_obs = *q.take<int32_t>(1);
+      mps[i].desc = q.take<uint8_t>(32);
+      track[i].in_view = *q.take<int32_t>(1) != 0;
+      const float* t = q.take<float>(4);
+      track[i].proj_x = t[0];
+      track[i].proj_y = t[1];
+      track[i].proj_xr = t[2];
+      track[i].view_cos = t[3];
+      track[i].level = *q.take<int32_t>(1);
+    }
+    const int n_local = *q.take<int32_t>(1);
+    const int32_t* local = q.take<int32_t>(n_local);
+    const float nnratio = *q.take<float>(1);
+    const int th = *q.take<int32_t>(1);
+    const int nk = *q.take<int32_t>(1);
+    if (nk != f.N) return 4;
+    const int32_t* mp0 = q.take<int32_t>(nk);
+    f.map_points.assign(mp0, mp0 + nk);
+    const float Tcw[16] = {1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1};
+    const slamgpu_adapter::FrameView cv = slamgpu_adapter::StereoFrameCore::view(f, Tcw);
+    std::vector<int32_t> after(f.map_points);
+    const int nm = slamgpu_adapter::search_by_projection_mps(core.context(), 0, cv, mps.data(),
+                                                             local, n_local, track.data(),
+                                                             nnratio, th, after.data());
+    spit(dir + "/mps.out", &nm, 4);
+    spit(dir + "/mps.out", after.data(), 4 * after.size());
   }
   std::printf("capi_check ok: %d keypoints\n", n);
   return 0;

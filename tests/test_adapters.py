@@ -16,7 +16,11 @@ Restated here from the reference, statement by statement:
 * SearchByProjection(Frame, Frame)'s queries (orb_matcher.cpp:1337-1341): last-frame keypoints
   with a map point that are not outliers, in keypoint order; tlc = Rlw * (-Rcw^T tcw) + tlw in
   f32 (:1326-1333); blocked current-frame slots are those whose map point has observations
-  (:1389-1393)."""
+  (:1389-1393).
+* SearchByProjection(Frame, vector<MapPoint*>, th)'s queries (orb_matcher.cpp:18-26): the local
+  map points in list order that are in view (track_is_in_view, set by Frame::IsInFrustum
+  frame.cpp:277-337) and not bad, with their track_* fields; the claims written back as
+  F.SetMapPoint(bestIdx, pMP) (:99-100)."""
 import os
 import subprocess
 
@@ -32,6 +36,9 @@ BA_OBS = np.dtype([("keyframe", "<i4"), ("u", "<f4"), ("v", "<f4"), ("ur", "<f4"
                    ("octave", "<i4")])
 F2F_QUERY = np.dtype([("xyz", "<f4", 3), ("last_angle", "<f4"), ("last_octave", "<i4"),
                       ("mp_id", "<i4"), ("blocks", "<i4"), ("pad", "<i4"), ("desc", "u1", 32)])
+MPS_QUERY = np.dtype([("proj_x", "<f4"), ("proj_y", "<f4"), ("proj_xr", "<f4"), ("view_cos", "<f4"),
+                      ("level", "<i4"), ("in_view", "<i4"), ("is_bad", "<i4"), ("mp_id", "<i4"),
+                      ("blocks", "<i4"), ("pad", "<i4", 3), ("desc", "u1", 32)])
 F2F_POSE = np.dtype([("Rcw", "<f4", 9), ("tcw", "<f4", 3), ("tlc_z", "<f4"), ("baseline", "<f4"),
                      ("th", "<f4"), ("mono", "<i4"), ("check_ori", "<i4"), ("pad", "<i4")])
 
@@ -102,9 +109,15 @@ def make_map(seed):
                          rng.uniform(0, 1241, n)).astype(np.float32)
         return dict(Tcw=_pose(rng), kps=_kps(rng, n), undist=_kps(rng, n), right=right, mp=mp,
                     outlier=(rng.random(n) < 0.2).astype(np.uint8))
+    # Tracker::SearchLocalPoints: local_map_points_ (unique, any order) and the track_* fields
+    # IsInFrustum left on every map point
+    local = rng.permutation(n_mp)[:int(rng.integers(80, 200))].astype(np.int32)
+    track = dict(in_view=(rng.random(n_mp) < 0.6).astype(np.int32),
+                 f=rng.uniform(-5, 1300, (n_mp, 4)).astype(np.float32),
+                 level=rng.integers(0, 8, n_mp).astype(np.int32))
     return dict(kfs=kfs, mps=mps, current=current, cur=frame(), last=frame(),
                 baseline=np.float32(0.537), th=np.float32(7.0), mono=0, check_ori=1,
-                orb=(2000, np.float32(1.2), 8, 20, 7))
+                orb=(2000, np.float32(1.2), 8, 20, 7), local=local, track=track)
 
 
 def write_scenario(S, path):
@@ -151,6 +164,13 @@ def write_scenario(S, path):
     i32(nl)
     i32(ini)
     i32(mn)
+    i32(len(S["local"]))
+    put(S["local"])
+    t = S["track"]
+    for m in range(len(S["mps"])):
+        i32(int(t["in_view"][m]))
+        put(t["f"][m])
+        i32(int(t["level"][m]))
     with open(path, "wb") as fh:
         fh.write(b"".join(out))
 
@@ -292,6 +312,25 @@ def test_adapters_follow_reference_graph_order(adapter_check, tmp_path, seed):
     idx = np.arange(len(exp))
     hit = (idx % 5 == 0) & (nq > 0)
     exp[hit] = qmp[idx[hit] % max(nq, 1)]
+    assert assigned == hit.sum() and np.array_equal(after, exp)
+    # SearchByProjection(Frame, vector<MapPoint*>, th)
+    nmq = o.i32()
+    mq, mqmp = o.take(MPS_QUERY, nmq), o.take(np.int32, nmq)
+    t = S["track"]
+    sel = [int(m) for m in S["local"] if t["in_view"][m] and not mps[m]["bad"]]
+    assert np.array_equal(mqmp, sel) and np.array_equal(mq["mp_id"], np.arange(nmq))
+    for k, name in enumerate(("proj_x", "proj_y", "proj_xr", "view_cos")):
+        assert np.array_equal(mq[name], t["f"][sel, k]), name
+    assert np.array_equal(mq["level"], t["level"][sel])
+    assert (mq["in_view"] == 1).all() and (mq["is_bad"] == 0).all()
+    assert np.array_equal(mq["blocks"], [int(len(mps[m]["obs"]) > 0) for m in sel])
+    assert np.array_equal(mq["desc"], np.array([mps[m]["desc"] for m in sel]).reshape(-1, 32))
+    assert 0 < nmq < len(S["local"])
+    assigned = o.i32()
+    after = o.take(np.int32, len(cur["kps"]))
+    exp = cur["mp"].copy()
+    hit = (idx % 3 == 1) & (nmq > 0)
+    exp[hit] = mqmp[(7 * idx[hit]) % max(nmq, 1)]
     assert assigned == hit.sum() and np.array_equal(after, exp)
     # ORBextractor's tables, host-side, against the oracle's ctor restatement
     assert o.i32() == 0

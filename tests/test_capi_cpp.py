@@ -2,7 +2,11 @@
 to libslamgpu.so -- no Python or ctypes between caller and library): ORBextractor::Compute on the
 committed 320x240 golden fixture (bit-exact), PoseOptimization on a C4-style problem and
 LocalBundleAdjustment on a small graph (oracle tolerance of tests/test_pose_gpu.py /
-tests/test_ba_gpu.py)."""
+tests/test_ba_gpu.py), and the per-frame matcher surface through include/slamgpu_adapters.hpp:
+the stereo Frame ctor (StereoFrameCore over slamgpu_frame_stereo, frame.cpp:61-111) on a
+synthetic KITTI-size pair and SearchByProjection(F, vpMapPoints, th) on that frame
+(search_by_projection_mps: gathering from MapPoint views + track_* fields, the device call, the
+write-back; orb_matcher.cpp:13-103, tracker.cpp:1176-1227), all bit-exact against the oracle."""
 import os
 import subprocess
 
@@ -49,12 +53,73 @@ def _write_inputs(d, img, nfeat, pose, lba):
         f.write(np.ascontiguousarray(P["obs"]).tobytes())
 
 
+def _stereo_inputs(d, oracle, th=3, nnratio=0.8, seed=11):
+    """stereo.bin (frame 1 of a synthetic sequence) and mps.bin: local map points from frame 0's
+    keypoints projected into frame 1 (as tests/test_match_gpu.py::test_mps_matches_oracle), some
+    not in view or bad, plus pre-existing current-frame map points with and without
+    observations. Returns the oracle's expected frame and search results."""
+    t = oracle.tables()
+    L, R = S.sequence(2000, 2)
+    fr = []
+    for i in range(2):
+        kl, dl, pl = oracle.extract(t, L[i], True)
+        kr, dr, pr = oracle.extract(t, R[i], True)
+        ur, depth, _ = oracle.stereo(t, kl, dl, kr, dr, pl, pr, CAM[0], CAM[4])
+        fr.append(dict(kl=kl, dl=dl, kr=kr, dr=dr, ur=ur, depth=depth))
+    rows, cols = L[1].shape
+    with open(os.path.join(d, "stereo.bin"), "wb") as f:
+        f.write(np.array([cols, rows, 2000], np.int32).tobytes())
+        f.write(np.asarray(CAM, np.float32).tobytes())
+        f.write(np.ascontiguousarray(L[1]).tobytes() + np.ascontiguousarray(R[1]).tobytes())
+    rng = np.random.default_rng(seed)
+    src, cur = fr[0], fr[1]
+    m = len(src["kl"])
+    q = np.zeros(m, G.MPS_QUERY_DTYPE)
+    H = S._homography(1)
+    uv = np.stack([src["kl"]["x"], src["kl"]["y"], np.ones(m, np.float32)], 1) @ H.T
+    q["proj_x"] = (uv[:, 0] / uv[:, 2] + rng.normal(0, 0.7, m)).astype(np.float32)
+    q["proj_y"] = (uv[:, 1] / uv[:, 2] + rng.normal(0, 0.7, m)).astype(np.float32)
+    dsp = np.where(src["depth"] > 0, CAM[4] / np.maximum(src["depth"], 1e-3), 30.0)
+    q["proj_xr"] = (q["proj_x"] - dsp).astype(np.float32)
+    q["view_cos"] = rng.choice(np.array([0.9, 0.998, 0.999], np.float32), m)
+    q["level"] = src["kl"]["octave"]
+    q["in_view"] = rng.random(m) < 0.9
+    q["is_bad"] = rng.random(m) < 0.05
+    q["mp_id"] = np.arange(m)
+    q["blocks"] = rng.random(m) < 0.8
+    q["desc"] = src["dl"]
+    n = len(cur["kl"])
+    extra = 64
+    nobs = np.concatenate([q["blocks"].astype(np.int32), rng.integers(0, 2, extra).astype(np.int32)])
+    mp0 = np.full(n, -1, np.int32)
+    pre = rng.choice(n, extra, replace=False)
+    mp0[pre] = m + np.arange(extra)
+    mp_o = mp0.copy()
+    nm_o = oracle.search_mps(t, oracle.grid_geom(S.KITTI_COLS, S.KITTI_ROWS), cur["kl"],
+                             cur["dl"], cur["ur"], mp_o, q, nobs, nnratio, th)
+    with open(os.path.join(d, "mps.bin"), "wb") as f:
+        f.write(np.int32(m + extra).tobytes())
+        for i in range(m + extra):
+            own = i < m
+            f.write(np.array([int(own and q["is_bad"][i]), nobs[i]], np.int32).tobytes())
+            f.write((q["desc"][i] if own else np.zeros(32, np.uint8)).tobytes())
+            f.write(np.int32(int(own and q["in_view"][i])).tobytes())
+            f.write(np.array([q[k][i] if own else 0 for k in ("proj_x", "proj_y", "proj_xr",
+                                                                "view_cos")], np.float32).tobytes())
+            f.write(np.int32(q["level"][i] if own else 0).tobytes())
+        f.write(np.int32(m).tobytes() + np.arange(m, dtype=np.int32).tobytes())
+        f.write(np.float32(nnratio).tobytes() + np.int32(th).tobytes())
+        f.write(np.int32(n).tobytes() + mp0.tobytes())
+    return cur, nm_o, mp_o, mp0
+
+
 @pytest.mark.gpu
 def test_cpp_caller_matches_golden_and_oracle(oracle, gpu_lib, tmp_path):
     z = np.load(os.path.join(HERE, "golden", "orb_small_320x240.npz"))
     edges, T0, _, isig, _ = S.pose_problem(77, 2000)
     P = S.ba_problem(78, n_local=6, n_fixed=2, n_points=400)
     _write_inputs(str(tmp_path), z["image"], 500, (edges, T0, isig), P)
+    cur, nm_o, mp_o, mp0 = _stereo_inputs(str(tmp_path), oracle)
     exe = B.build_capi_check()
     r = subprocess.run([exe, str(tmp_path)], capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stderr
@@ -91,3 +156,23 @@ def test_cpp_caller_matches_golden_and_oracle(oracle, gpu_lib, tmp_path):
     tol = 1e-5 * np.abs(kf_o.astype(np.float64) - P["kf_Tcw"]).max() + 4 * EPS32 * np.maximum(
         np.abs(kf_o), 1)
     assert (np.abs(kf.astype(np.float64) - kf_o) <= tol).all()
+    # the stereo Frame ctor through StereoFrameCore: both views, u_right / depth, undistorted
+    # keypoints (= keypoints without distortion), byte for byte
+    so = np.fromfile(os.path.join(tmp_path, "stereo.out"), np.uint8)
+    N, Nr = so[:8].view(np.int32)
+    assert N == len(cur["kl"]) and Nr == len(cur["kr"])
+    o = 8
+    parts = {}
+    for name, nbytes in (("kl", 28 * N), ("dl", 32 * N), ("kr", 28 * Nr), ("dr", 32 * Nr),
+                         ("ur", 4 * N), ("depth", 4 * N), ("un", 28 * N)):
+        parts[name] = so[o:o + nbytes].tobytes()
+        o += nbytes
+    assert o == len(so)
+    for name in ("kl", "dl", "kr", "dr", "ur", "depth"):
+        assert parts[name] == np.ascontiguousarray(cur[name]).tobytes(), name
+    assert parts["un"] == parts["kl"]
+    # SearchByProjection(F, vpMapPoints, th) through the adapter's one call: the oracle's match
+    # count and map point per keypoint
+    mo = np.fromfile(os.path.join(tmp_path, "mps.out"), np.int32)
+    assert mo[0] == nm_o > 100
+    assert np.array_equal(mo[1:], mp_o)

@@ -34,6 +34,13 @@ OPK(lshl_add, uint32_t, (v << 3) + c1)
 OPK(bfe, uint32_t, __builtin_amdgcn_ubfe(v, c1 & 15, 8))
 OPK(min_u32, uint32_t, (v < c1 ? v : c1) + c2)
 OPK(mul_lo, uint32_t, v * c1)
+OPK(add_xor, uint32_t, (v + c1) ^ c2)                       // 2 instructions
+OPK(lshl_or, uint32_t, (v << 5) | c1)
+OPK(add3, uint32_t, v + c1 + (v >> 3))                     // lshr + add3
+OPK(xor_only, uint32_t, v ^ c1 ^ (v >> 2))                  // lshr + xor3?
+OPK(bfe_add3, uint32_t, v + c1 + __builtin_amdgcn_ubfe(v, 16, 1))
+OPK(cndmask, uint32_t, (v & 1) ? c1 : v + c2)
+OPK(mad_u32_u24, uint32_t, __umul24(v, c1) + v)
 
 __global__ __launch_bounds__(256) void k_pk_fma(float* out, float c1, float c2) {
   f32x2 x[kChains];
@@ -84,6 +91,29 @@ static void run(const char* name, K kern, T c1, T c2, T* out) {
   printf("   (fraction of the 2-cycle wave64 issue peak)\n");
 }
 
+// LDS gather throughput: 8 waves per SIMD, each lane reads random u16 / dword pairs from a 3.5 KB
+// per-wave table (the orient_desc row-sum window)
+template <int MODE>
+__global__ __launch_bounds__(256) void k_lds(uint32_t* out, uint32_t seed, uint32_t c2) {
+  __shared__ uint16_t t[4][1760];
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  for (int i = lane; i < 1760; i += 64) t[w][i] = (uint16_t)(i * 7 + seed);
+  __syncthreads();
+  uint32_t x = lane * 2654435761u + seed, acc = 0;
+  for (int i = 0; i < 512; i++) {
+    x = x * 1664525u + 1013904223u;
+    const uint32_t e = ((x >> 8) & 1023u) + (uint32_t)(lane & 7) * 89u;
+    if (MODE == 0) {  // 7 u16 reads (immediate offsets)
+      const uint16_t* p = &t[w][e];
+      acc += p[0] + p[1] + p[2] + p[3] + p[4] + p[5] + p[6];
+    } else {          // 4 dwords (2 x read2) at the containing dword
+      const uint32_t* p = reinterpret_cast<const uint32_t*>(&t[w][0]) + (e >> 1);
+      acc += p[0] + p[1] + p[2] + p[3];
+    }
+  }
+  out[blockIdx.x * 256 + threadIdx.x] = acc + c2;
+}
+
 int main() {
   void* out = nullptr;
   hipMalloc(&out, 256 * 2048 * 8);
@@ -100,6 +130,15 @@ int main() {
   run("bfe", k_bfe, 3u, 5u, u);
   run("min_u32", k_min_u32, 3000u, 5u, u);
   run("mul_lo", k_mul_lo, 3u, 5u, u);
+  run("add_xor(2)", k_add_xor, 3u, 5u, u);
+  run("lshl_or", k_lshl_or, 3u, 5u, u);
+  run("add3(2)", k_add3, 3u, 5u, u);
+  run("xor3(2)", k_xor_only, 3u, 5u, u);
+  run("bfe_add3(2)", k_bfe_add3, 3u, 5u, u);
+  run("cndmask(3)", k_cndmask, 3u, 5u, u);
+  run("mad_u24_add", k_mad_u32_u24, 3u, 5u, u);
+  run("lds_u16x7", k_lds<0>, 3u, 5u, u);
+  run("lds_2xread2", k_lds<1>, 3u, 5u, u);
   run("pk_fma_f32", k_pk_fma, 0.5f, 0.25f, f);
   run("cvt_f32_i32", k_cvt_f32_i32, 0.5f, 0.25f, f);
   hipFree(out);
