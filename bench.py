@@ -55,6 +55,14 @@ def _symbol_matches(sym, kernel):
     return sym.split("<")[0].replace("_kernel", "") == KERNEL_SYMBOL.get(kernel, kernel)
 
 
+# Sustained VALU issue rate of one MI355X, measured (tools/valu_rates.hip, profiles/r4a_valu_rates.txt):
+# 8 waves per SIMD of independent v_dot4 / v_dot2 / v_alignbit / v_perm / v_bfe / v_pk_fma_f32 /
+# v_cvt / v_add+v_xor chains all issue at 0.44-0.48 of the nominal one-wave64-instruction-per-2-
+# cycles peak (256 CUs x 4 SIMD x 2.4 GHz / 2): one instruction per ~4.2 cycles per SIMD. The
+# integer kernels are priced against this rate (`valu_sustained_frac`) besides the nominal one.
+VALU_SUSTAINED_FRAC_OF_NOMINAL = 0.465
+
+
 def measured_valu(kernel, batch):
     """SQ_INSTS_VALU per dispatch of `kernel` (tools/pmc_valu.sh + tools/valu.py, committed as
     profiles/valu.json) and the chip's VALU issue peak; (None, None) when absent or measured on
@@ -96,7 +104,7 @@ def path_bytes_per_frame(level_px, kp_per_image):
     return 2 * sum(level_px) + 3 * kp_per_image * 60
 
 
-def kernel_bytes(name, n_images, n_frames, kp_per_image, level_px, n_queries):
+def kernel_bytes(name, n_images, n_frames, kp_per_image, level_px, n_queries, fast_cand=None):
     """Algorithmic (compulsory) HBM bytes one step moves through the named kernel (all its
     launches): every input byte the kernel needs read once, every output written once -- the
     per-kernel split of section 8(d)'s per-frame figure, not the bytes the kernel re-reads."""
@@ -112,8 +120,11 @@ def kernel_bytes(name, n_images, n_frames, kp_per_image, level_px, n_queries):
         return n_frames * kp_per_image * (2 * 60 + 121 + 231)
     if name == "search_cand":    # query (64 B) + window candidates' kps/desc (~60 B each, ~8)
         return n_queries * (64 + 8 * 60)
-    if name == "octree":         # FAST candidates read + kept keys written (4 B each)
-        return n_images * 4 * 2 * kp_per_image
+    if name == "octree":         # every FAST survivor of the image read (4 B key; the per-cell
+        # counts ~5 KB per image are left out), the kept keys written (4 B each)
+        if fast_cand is None:
+            return None
+        return n_images * 4 * (fast_cand + kp_per_image)
     return None
 
 
@@ -282,7 +293,10 @@ def main():
         level_px = [ctx.pyramid_level(0, l).size for l in range(8)]
         kp_img = float(nk.mean())
         nqueries = int(nq.sum())
-        dom_bytes = kernel_bytes(dominant, 2 * Bs, Bs, kp_img, level_px, nqueries // NS)
+        # FAST survivors per image (what the octree reads): images 0-3 of the batch, all levels
+        fast_cand = float(np.mean([sum(len(ctx.debug_level_keys(i, l, 0)) for l in range(8))
+                                   for i in range(min(4, 2 * Bs))]))
+        dom_bytes = kernel_bytes(dominant, 2 * Bs, Bs, kp_img, level_px, nqueries // NS, fast_cand)
         avg_launch_s = dom_ms / 1000.0 / max(1, dom_n)
         per_launch_bytes = dom_bytes / max(1, launches_per_step) if dom_bytes else None
         achieved = (per_launch_bytes / avg_launch_s / 1e9) if per_launch_bytes else None
@@ -317,7 +331,11 @@ def main():
             roofline["valu_issue"] = {"wave_instr_per_launch": round(vi), "achieved": rate,
                                       "peak": vpeak, "unit": "wave-instr/s",
                                       "frac": round(rate / vpeak, 4),
-                                      "source": "profiles/valu.json"}
+                                      "sustained_peak": vpeak * VALU_SUSTAINED_FRAC_OF_NOMINAL,
+                                      "sustained_frac": round(
+                                          rate / (vpeak * VALU_SUSTAINED_FRAC_OF_NOMINAL), 4),
+                                      "source": "profiles/valu.json; sustained peak "
+                                                "tools/valu_rates.hip"}
         cpu = None
         if not args.no_cpu_baseline:
             dk, dd = ctx.keypoints(0)   # the left view of the batch's frame 0
@@ -344,7 +362,7 @@ def main():
             avg_s = ms / 1000.0 / nl
             ent = {"ms_per_step": round(ms, 4), "launches_per_step": nl,
                    "avg_launch_us": round(avg_s * 1e6, 2)}
-            kb = kernel_bytes(n, 2 * Bs, Bs, kp_img, level_px, nqueries // NS)
+            kb = kernel_bytes(n, 2 * Bs, Bs, kp_img, level_px, nqueries // NS, fast_cand)
             if kb:
                 ent["algorithmic_bytes_per_launch"] = kb / nl
                 ent["hbm_frac"] = round(kb / nl / avg_s / 1e9 / HBM_PEAK_GBS, 4)
@@ -356,7 +374,11 @@ def main():
             if vi is not None:
                 ent["valu_wave_instr_per_launch"] = round(vi)
                 ent["valu_issue_frac"] = round(vi / avg_s / vpeak, 4)
+                ent["valu_sustained_frac"] = round(
+                    vi / avg_s / (vpeak * VALU_SUSTAINED_FRAC_OF_NOMINAL), 4)
             kernels[n] = ent
+        if "octree" in kernels:
+            kernels["octree"]["fast_candidates_per_image"] = round(fast_cand)
         if "stereo_match" in kernels:
             # HBM moves lines: the windows' distinct 128-B lines (frame 0 of the batch) + the
             # keypoint/descriptor/row-table reads, per launch (tools/stereo_lines.py restates it)

@@ -201,6 +201,14 @@ constexpr int kPanStage = 96;  // extent blocks whose panel is staged in LDS (37
 // keeps the previous kernel's operation order (divisions, no contraction, the same sums), so the
 // results are bit-identical to it; the LM stop test of this ill-conditioned system amplifies
 // last-bit differences into different iteration counts.
+// x of lane l, to every lane (l wave-uniform)
+__device__ __forceinline__ double bcast(double x, int l) {
+  const uint64_t u = __builtin_bit_cast(uint64_t, x);
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)u, l);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(u >> 32), l);
+  return __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
+}
+
 __global__ __launch_bounds__(kFacThreads) void eg_factor_solve_kernel(EgGraph G, EgState W,
                                                                       int64_t n_blocks,
                                                                       double lambda) {
@@ -225,58 +233,57 @@ __global__ __launch_bounds__(kFacThreads) void eg_factor_solve_kernel(EgGraph G,
   if (tid == 0) s_ok = 1;
   __syncthreads();
   auto diag_of = [&](int k) { return L + (G.off[k] + (k - G.start[k])) * 49; };
-  // lane 0: LDLT of diagonal block k from src (lower triangle + diagonal), the forward solve of
-  // y_k; L_kk / D_k to the profile and to s_kk[buf], 1 / D_k to s_rd[buf], y_k to s_y[buf]
+  // lanes 0-6 of a wave, lane r holding row r: LDLT of diagonal block k from src (lower
+  // triangle + diagonal), the forward solve of y_k; L_kk / D_k to the profile and to s_kk[buf],
+  // 1 / D_k to s_rd[buf], y_k to s_y[buf]. Column j: lane j forms the pivot, readlane broadcasts
+  // it and row j, lanes i > j form L_ij. Every entry takes the operations, in the order, of the
+  // serial version (one lane, rows in turn), so the bits are the same with a shorter chain.
   auto diag_factor = [&](int k, const double* src, int buf) {
-    double a[7][7];
+    const int r = lane;
+    double a[7], dm[7];
 #pragma unroll
-    for (int r = 0; r < 7; r++)
-#pragma unroll
-      for (int c = 0; c <= r; c++) a[r][c] = src[7 * r + c];
+    for (int c = 0; c < 7; c++) a[c] = c <= r ? src[7 * r + c] : 0.0;
     bool ok = true;
-    double rd[7];
+    double my_rd = 0.0;
 #pragma unroll
     for (int j = 0; j < 7; j++) {
-      double d = a[j][j];
+      double d = a[j];  // lane j: the pivot
 #pragma unroll
-      for (int m = 0; m < j; m++) d -= a[j][m] * a[j][m] * a[m][m];
-      a[j][j] = d;
+      for (int m = 0; m < j; m++) d -= a[m] * a[m] * dm[m];
+      d = bcast(d, j);
+      dm[j] = d;
       ok = ok && d != 0.0;
-      rd[j] = 1.0 / d;
+      const double rdj = 1.0 / d;
+      if (r == j) my_rd = rdj;
+      double t = a[j];  // lanes i > j: L_ij
 #pragma unroll
-      for (int i = j + 1; i < 7; i++) {
-        double t = a[i][j];
-#pragma unroll
-        for (int m = 0; m < j; m++) t -= a[i][m] * a[j][m] * a[m][m];
+      for (int m = 0; m < j; m++) t -= a[m] * bcast(a[m], j) * dm[m];
 #if EG_EXACT_ROUNDING
-        a[i][j] = t / d;
+      t = t / d;
 #else
-        a[i][j] = t * rd[j];
+      t = t * rdj;
 #endif
-      }
+      a[j] = r > j ? t : (r == j ? d : a[j]);
     }
-    double v[7];
+    double v = y[7 * k + r];
 #pragma unroll
-    for (int r = 0; r < 7; r++) v[r] = y[7 * k + r];
-#pragma unroll
-    for (int r = 1; r < 7; r++)
-#pragma unroll
-      for (int m = 0; m < r; m++) v[r] -= a[r][m] * v[m];
+    for (int m = 0; m < 6; m++) {
+      const double vm = bcast(v, m);
+      if (r > m) v -= a[m] * vm;
+    }
     double* Akk = diag_of(k);
 #pragma unroll
-    for (int r = 0; r < 7; r++) {
-#pragma unroll
-      for (int c = 0; c <= r; c++) {
-        Akk[7 * r + c] = a[r][c];
-        s_kk[buf][7 * r + c] = a[r][c];
+    for (int c = 0; c < 7; c++)
+      if (c <= r) {
+        Akk[7 * r + c] = a[c];
+        s_kk[buf][7 * r + c] = a[c];
       }
-      s_rd[buf][r] = rd[r];
-      s_y[buf][r] = v[r];
-      y[7 * k + r] = v[r];
-    }
-    if (!ok) s_ok = 0;
+    s_rd[buf][r] = my_rd;
+    s_y[buf][r] = v;
+    y[7 * k + r] = v;
+    if (!ok && r == 0) s_ok = 0;
   };
-  if (F > 0 && tid == 0) diag_factor(0, diag_of(0), 0);
+  if (F > 0 && tid < 7) diag_factor(0, diag_of(0), 0);
   __syncthreads();
   // ---- factorisation + forward solve ----
   for (int k = 0; k < F; k++) {
@@ -335,7 +342,7 @@ __global__ __launch_bounds__(kFacThreads) void eg_factor_solve_kernel(EgGraph G,
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-        if (lane == 0) diag_factor(k + 1, s_nx, cur ^ 1);
+        if (lane < 7) diag_factor(k + 1, s_nx, cur ^ 1);
       }
     } else {  // trailing update of the rest of the extent (pair 0 is block (k+1, k+1) if nxt_in)
       const int npairs = ne * (ne + 1) / 2;

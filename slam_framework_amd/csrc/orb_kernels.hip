@@ -2345,7 +2345,7 @@ __global__ __launch_bounds__(256) void orient_desc_kernel(
       // The address comes straight from the rounded coordinates' float bits X = M + cx,
       // Y = M + cy (M = 0x4B400000, low 24 bits 0x400000): 2 (cx kRtRows + cy) =
       // umul24(X, 2 kRtRows) + 2 Y - (2 kRtRows 0x400000 + 2 M), all modulo 2^32.
-      typedef __attribute__((address_space(3))) const volatile uint32_t lds_u32;
+      typedef __attribute__((address_space(3))) const uint32_t lds_u32;
       const uint32_t rt_base =
           (uint32_t)(uintptr_t)(__attribute__((address_space(3))) const uint16_t*)&s_rt[wid][0][0] -
           2u * (uint32_t)kRtRows * 0x400000u - 2u * 0x4B400000u;
@@ -2364,8 +2364,13 @@ __global__ __launch_bounds__(256) void orient_desc_kernel(
             const f32x2 sp = __builtin_elementwise_fma((f32x2){px, px}, ab, (f32x2){py, py} * nab) + magic;
             const uint32_t Y = __float_as_uint(sp.x), X = __float_as_uint(sp.y);
             const uint32_t a = __umul24(X, 2u * kRtRows) + rt_base + (Y << 1);
-            const uint32_t p0 = *(lds_u32*)(uintptr_t)a, p1 = *(lds_u32*)(uintptr_t)(a + 4),
-                           p2 = *(lds_u32*)(uintptr_t)(a + 8), p3 = *(lds_u32*)(uintptr_t)(a + 12);
+            const lds_u32* rw = (const lds_u32*)(uintptr_t)(a & ~3u);
+            const uint32_t sh = Y << 4;  // alignbit takes it mod 32: 16 for an odd start (cy odd)
+            const uint32_t w0 = rw[0], w1 = rw[1], w2 = rw[2], w3 = rw[3];
+            const uint32_t p0 = __builtin_amdgcn_alignbit(w1, w0, sh);
+            const uint32_t p1 = __builtin_amdgcn_alignbit(w2, w1, sh);
+            const uint32_t p2 = __builtin_amdgcn_alignbit(w3, w2, sh);
+            const uint32_t p3 = __builtin_amdgcn_alignbit(0u, w3, sh);
             const uint32_t sm = dot2u(p0, K01, dot2u(p1, K23, dot2u(p2, K21, dot2u(p3, K0, 0u))));
             uint32_t o;
             if (kTail) {
