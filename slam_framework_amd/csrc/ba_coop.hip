@@ -1169,9 +1169,9 @@ __device__ void profile_back_solve(CoopShared& sh, const CoopWs& w, int K, doubl
 __device__ bool wait_flags(const CoopWs& w, const int32_t* pflag, int32_t target) {
   const int lane = threadIdx.x & 63, G = gridDim.x;
   uint32_t spins = 0, polls = 0;
-  int64_t seen = -1;
+  int seen = -1;
   for (;;) {
-    int64_t sum = 0;
+    int sum = 0, cnt = 0;  // this lane's flags: their sum (progress) and how many reached target
     bool all = true;
     for (int g0 = 0; g0 < G; g0 += 64) {
       const int g = g0 + lane;
@@ -1179,10 +1179,18 @@ __device__ bool wait_flags(const CoopWs& w, const int32_t* pflag, int32_t target
                                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
                               : target;
       all = all && __all(v >= target);
-      sum += v;
+      if (g < G) {
+        sum += v;
+        cnt += v >= target ? 1 : 0;
+      }
     }
     if (all) return true;
-    sum = __builtin_amdgcn_readfirstlane((int)sum);  // progress proxy (lane 0's partial)
+    // progress = any flag of the grid moved: the sum over the whole wave, not one lane's part
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) {
+      sum += __shfl_xor(sum, m);
+      cnt += __shfl_xor(cnt, m);
+    }
     if (sum != seen) {
       seen = sum;
       spins = 0;
@@ -1192,8 +1200,11 @@ __device__ bool wait_flags(const CoopWs& w, const int32_t* pflag, int32_t target
     polls++;
     if ((++spins & 255u) == 0 && ctl_load(w, CTL_ERR)) return false;
     if (spins > (1u << 22)) {
-      if (lane == 0)
+      if (lane == 0) {  // what the host reports: the work-groups whose flag had got there
+        __hip_atomic_store(&w.ctl[CTL_ARRIVED], cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&w.ctl[CTL_GRID], G, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __hip_atomic_store(&w.ctl[CTL_ERR], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
       return false;
     }
   }
@@ -2037,8 +2048,9 @@ hipError_t launch_coop_ba(const PoseParams& P, const CoopProblem& pb, const Coop
     // the device holds resident at once, optimizer_runtime.cpp coop_grid) are all dispatched
     // while the first spin at a grid barrier: they only wait for CUs that non-spinning kernels
     // free, and a barrier that still does not fill raises CTL_ERR (bounded spin) rather than
-    // hanging. A plain launch: under rocprofv3 the HIP runtime's cooperative-launch path leaves
-    // the process to crash in its own teardown at exit (r2s/r2t), and costs ~50 us per call.
+    // hanging. A plain launch: the runtime's cooperative launch costs ~50 us per call, and under
+    // rocprofv3 a process that had used it crashed at exit (r2s/r2t; cause not established, so
+    // the cooperative launch is not offered).
     CoopSchedule sch{};
     sch.n_phases = n_phases;
     sch.outlier_pass = outlier_pass ? 1 : 0;
@@ -2049,18 +2061,8 @@ hipError_t launch_coop_ba(const PoseParams& P, const CoopProblem& pb, const Coop
     const int32_t* stop = d_stop;
     void* args[] = {&Pc, &pbc, &wc, &sch, &stop};
     if (g_timer) g_timer->begin("ba_coop", st);
-    // SLAMGPU_BA_COOP_LAUNCH=1: the runtime's cooperative launch instead (residency guaranteed
-    // by the runtime; DESIGN.md section 3 records what the A/B of the two showed)
-    static const bool coop_launch = [] {
-      const char* v = getenv("SLAMGPU_BA_COOP_LAUNCH");
-      return v && v[0] == '1';
-    }();
-    if (coop_launch)
-      e = hipLaunchCooperativeKernel(reinterpret_cast<const void*>(&ba_coop_kernel), dim3(G),
-                                     dim3(kT), args, 0, st);
-    else
-      e = hipLaunchKernel(reinterpret_cast<const void*>(&ba_coop_kernel), dim3(G), dim3(kT), args,
-                          0, st);
+    e = hipLaunchKernel(reinterpret_cast<const void*>(&ba_coop_kernel), dim3(G), dim3(kT), args,
+                        0, st);
     if (g_timer) g_timer->end("ba_coop", st);
     if (e != hipSuccess) return e;
   }

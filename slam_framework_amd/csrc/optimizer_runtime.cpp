@@ -7,6 +7,7 @@
 #include <hip/hip_runtime.h>
 
 #include <chrono>
+#include <condition_variable>
 #include <mutex>
 #include <thread>
 
@@ -268,12 +269,15 @@ constexpr int kMaxDevices = 64;
 // 64, while a 54-keyframe window 8.7 -> 8.3 ms and GBA-100 15.5 -> 13.5 ms gain; 192 CUs stay free
 // for the tracking front end), and 128 for map-scale systems (K >= 512: GBA-1500 116 -> 110 ms),
 // bounded by the CUs and the kernel's occupancy; SLAMGPU_BA_WGS fixes it.
+static int coop_cap[kMaxDevices];  // work-groups of the coop kernel the device keeps resident
+
 int coop_grid(int device, int K) {
   static std::once_flag once[kMaxDevices];
-  static int grid[kMaxDevices], cap[kMaxDevices];
+  static int grid[kMaxDevices];
   static bool fixed[kMaxDevices];
+  int* const cap = coop_cap;
   if (device < 0 || device >= kMaxDevices) return 1;
-  std::call_once(once[device], [device]() {
+  std::call_once(once[device], [device, cap]() {
     hipDeviceProp_t prop{};
     int c = 256;
     const bool have = hipGetDeviceProperties(&prop, device) == hipSuccess &&
@@ -293,15 +297,43 @@ int coop_grid(int device, int K) {
   return grid[device];
 }
 
-// One single-problem solve per device at a time: its G work-groups must all be resident for the
-// grid barriers to complete, so two of them (the LocalMapper's LocalBA and the LoopCloser's global
-// BA, local_mapper.cpp:53, loop_closer.cpp:77) never compete for residency. The front end and
-// PoseOptimization on other streams only delay residency (their work-groups finish and free
-// their CUs); the barrier waits for as long as arrivals keep coming.
-std::mutex& coop_device_mutex(int device) {
-  static std::mutex m[kMaxDevices];
-  return m[device < 0 || device >= kMaxDevices ? 0 : device];
-}
+// The coop solves running on one device hold at most coop_cap work-groups together: each one's G
+// work-groups must all be resident for its grid barriers to complete, so two solves that could
+// not be resident at once would each hold part of the slots and wait forever. Within the budget
+// they run concurrently, as the reference's LocalMapper LocalBA and LoopCloser global BA do
+// (local_mapper.cpp:53, loop_closer.cpp:77): a C5-size LocalBA (64 work-groups) beside a
+// map-scale GBA (128) takes 192 of MI355X's 256 -- it does not wait behind the GBA. A solve that
+// does not fit waits for the running ones to release theirs. The front end and PoseOptimization
+// on other streams only delay residency (their work-groups finish and free their CUs); the
+// barrier waits for as long as arrivals keep coming.
+class CoopSlots {
+ public:
+  CoopSlots(int device, int G) : d_(device < 0 || device >= kMaxDevices ? 0 : device), g_(G) {
+    std::unique_lock<std::mutex> lk(m_[d_]);
+    const int cap = std::max(coop_cap[d_], 1);
+    g_ = std::min(g_, cap);  // (G never exceeds the cap: coop_grid)
+    cv_[d_].wait(lk, [&] { return used_[d_] + g_ <= cap; });
+    used_[d_] += g_;
+  }
+  ~CoopSlots() {
+    {
+      std::lock_guard<std::mutex> lk(m_[d_]);
+      used_[d_] -= g_;
+    }
+    cv_[d_].notify_all();
+  }
+  CoopSlots(const CoopSlots&) = delete;
+  CoopSlots& operator=(const CoopSlots&) = delete;
+
+ private:
+  static std::mutex m_[kMaxDevices];
+  static std::condition_variable cv_[kMaxDevices];
+  static int used_[kMaxDevices];
+  int d_, g_;
+};
+std::mutex CoopSlots::m_[kMaxDevices];
+std::condition_variable CoopSlots::cv_[kMaxDevices];
+int CoopSlots::used_[kMaxDevices];
 
 // One problem (LocalBundleAdjustment after its graph gathering, or the global BundleAdjustment)
 // on the cooperative solver: validate, stage, run the schedule asynchronously while mirroring the
@@ -426,7 +458,7 @@ int coop_host(const char* what, const slamgpu_camera* cam, const float* inv_sigm
   }
   char* b = static_cast<char*>(S.buf);
   char* h = S.pin;
-  std::lock_guard<std::mutex> device_lock(coop_device_mutex(dev));
+  CoopSlots slots(dev, G);  // the device's residency budget for coop solves
   static const bool prof = getenv("SLAMGPU_BA_PROFILE") != nullptr;
   CoopWs w = coop_layout(b + o_ws, n_kf, n_points, n_obs, K, (int)pairs, G, pnnz, nullptr);
   w.free_of_kf = reinterpret_cast<const int32_t*>(b + o_free);

@@ -2217,10 +2217,11 @@ __global__ __launch_bounds__(256) void orient_desc_kernel(
   // even, so round-half-even is unchanged)
   const f32x2 magic = {12582930.0f, 12582930.0f};
   uint32_t dlo = 0, dhi = 0;
-  // Row-sum tasks: t = lane + 64 i -> column quad gq = t / 43, window row r = t % 43, so that
-  // consecutive lanes store consecutive rows of a column (the u16 stores of a wave fill
-  // consecutive dwords: no bank conflicts); a task's raw bytes sit at r * pitch + 4 gq past the
-  // keypoint's window origin (a lane constant times the level pitch, the origin a scalar base).
+  // Row-sum tasks: t = lane + 64 i -> window row r = t / 10, column quad gq = t % 10; a task's
+  // raw bytes sit at r * pitch + 4 gq past the keypoint's window origin (a lane constant times
+  // the level pitch: one v_mad_u32_u24, the origin a scalar base). (Consecutive lanes on
+  // consecutive rows of one column quad would store conflict-free, but each wave load then
+  // touches ~43 rows instead of ~7: orient_desc 1.03 -> 1.50 ms, round 4.)
   constexpr int kTaskRows = 1;              // window rows per lane task
   constexpr int kTasks = 43 * 10;
   constexpr int kRounds = (kTasks + 63) / 64;
@@ -2228,8 +2229,8 @@ __global__ __launch_bounds__(256) void orient_desc_kernel(
 #pragma unroll
   for (int i = 0; i < kRounds; i++) {
     const int t = lane + 64 * i;
-    trow[i] = t < kTasks ? t % 43 : -1;
-    tcol[i] = 4 * (t / 43);
+    trow[i] = t < kTasks ? t / 10 : -1;
+    tcol[i] = 4 * (t % 10);
   }
   // Per keypoint: its row-summed window into LDS, then its 256 tests from LDS. The window's raw
   // rows (one 16-byte load per lane task, 7 tasks per lane) of keypoint j + 1 are in flight

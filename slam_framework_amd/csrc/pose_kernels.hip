@@ -214,18 +214,16 @@ __device__ __forceinline__ void wave_lds_sync() {
 template <int W>
 struct FrameSum {
   double red[2][W][32];  // wave partials, double-buffered: a buffer is rewritten two sums later,
-                         // after a barrier every reader has passed
-  double tot[2][W][32];  // every wave's own copy of the totals, in one of two buffers (the
-                         // linearisation of the current estimate and that of a trial)
+  double tot[W][32];     // after a barrier every reader has passed
   double bc[14];         // the trial step (x, T, ok) from wave 0 to the other waves
   int rb;
 
-  // 32 sums (H, b, chi2) -> tot[buf][wave][0..31]
-  __device__ __forceinline__ const double* sum32(double v[32], int buf) {
+  // 32 sums (H, b, chi2) -> tot[wave][0..31]
+  __device__ __forceinline__ const double* sum32(double v[32]) {
     const int lane = threadIdx.x & 63, w = wave_id();
     const double s = wave_reduce_scatter32(v);
     if (W == 1) {
-      if ((lane & 1) == 0) tot[buf][0][lane >> 1] = s;
+      if ((lane & 1) == 0) tot[0][lane >> 1] = s;
     } else {
       if ((lane & 1) == 0) red[rb][w][lane >> 1] = s;
       __syncthreads();
@@ -233,12 +231,12 @@ struct FrameSum {
         double t = 0.0;
 #pragma unroll
         for (int k = 0; k < W; k++) t += red[rb][k][lane];
-        tot[buf][w][lane] = t;
+        tot[w][lane] = t;
       }
       rb ^= 1;
     }
     wave_lds_sync();
-    return tot[buf][w];
+    return tot[w];
   }
 
   __device__ __forceinline__ double sum1(double v) {
@@ -354,12 +352,12 @@ __global__ __launch_bounds__(64 * W) void pose_opt_kernel(
     }
     double lambda = 0.0;
     int ni = 2, nbad = 0;
-    // computeActiveErrors + activeRobustChi2 + buildSystem at T: error, Huber, Jacobian and the
-    // 21 + 6 + 1 sums of H, b, chi2 of every active edge (lastbad re-set from the errors)
-    auto linearise = [&](const SE3& Tl, double acc[32]) {
+    for (int it = 0; it < 10; it++) {
+      // ---- linearise: computeActiveErrors + activeRobustChi2 + buildSystem at T ----
+      double acc[32];
 #pragma unroll
       for (int i = 0; i < 32; i++) acc[i] = 0.0;
-      const PassPose TP = pass_pose(Tl);
+      const PassPose TP = pass_pose(T);
       // batched variant: a software pipeline, the next slot's edge loads (L2) under this one
       slamgpu_pose_edge en{};
       if (!kLdsEdges && nslots > 0) en = edge(tid);
@@ -410,130 +408,8 @@ __global__ __launch_bounds__(64 * W) void pose_opt_kernel(
           for (int c = a; c < 6; c++, h++) acc[h] += wa0 * J[0][c] + wa1 * J[1][c] + wa2 * J[2][c];
         }
       }
-    };
-    // The trial step (6x6 LDLT + exp(x) * T). W == 1: every lane; otherwise wave 0 alone (its
-    // SIMD undisturbed), then a broadcast through LDS.
-    auto solve_step = [&](const double* H, const double* b, const SE3& from, double x[6],
-                          SE3& to) -> bool {
-      bool ok;
-      if constexpr (W == 1) {
-        ok = ldlt_solve6(H, lambda, b, x);
-        to = se3_left_update(x, from);
-      } else {
-        if (wave_id() == 0) {
-          ok = ldlt_solve6(H, lambda, b, x);
-          to = se3_left_update(x, from);
-          if ((tid & 63) == 0) {
-#pragma unroll
-            for (int j = 0; j < 6; j++) fs.bc[j] = x[j];
-            fs.bc[6] = to.r.x;
-            fs.bc[7] = to.r.y;
-            fs.bc[8] = to.r.z;
-            fs.bc[9] = to.r.w;
-            fs.bc[10] = to.t[0];
-            fs.bc[11] = to.t[1];
-            fs.bc[12] = to.t[2];
-            fs.bc[13] = ok ? 1.0 : 0.0;
-          }
-        }
-        __syncthreads();  // the next write of bc follows a sum's barrier, after every read
-#pragma unroll
-        for (int j = 0; j < 6; j++) x[j] = fs.bc[j];
-        to.r.x = fs.bc[6];
-        to.r.y = fs.bc[7];
-        to.r.z = fs.bc[8];
-        to.r.w = fs.bc[9];
-        to.t[0] = fs.bc[10];
-        to.t[1] = fs.bc[11];
-        to.t[2] = fs.bc[12];
-        ok = fs.bc[13] != 0.0;
-      }
-      return ok;
-    };
-    if constexpr (W > 1) {
-      // The latency variant: a trial evaluates the full linearisation at its estimate, not
-      // only its chi2 -- an accepted trial's estimate is where the next iteration linearises
-      // (same active edges, same robust kernel within a round; g2o recomputes the errors there
-      // and gets the same sums), so that iteration starts from the trial's sums: one edge pass
-      // and one work-group reduction per LM iteration instead of two of each. A trial writes
-      // the other totals buffer, so a rejected one leaves the current linearisation in place.
-      // One pass site: each turn linearises at Tn, either T for a fresh iteration (the first
-      // one, or after an iteration that accepted nothing: g2o recomputes the errors at T) or a
-      // trial estimate, then decides and computes the next step.
-      int lb = 0, it = 0, qmax = 0;
-      bool fresh = true, trial_ok = true;
-      double currentChi = 0.0, iniChi = 0.0, scale = 0.0;
-      const double* S = nullptr;
-      SE3 Tn = T;
-      while (true) {
-        double acc[32];
-        linearise(Tn, acc);
-        ptick(fresh ? 0 : 2);
-        const double* Sp = fs.sum32(acc, fresh ? lb : lb ^ 1);
-        ptick(fresh ? 1 : 3);
-        bool new_iter = fresh;
-        if (fresh) {
-          S = Sp;
-        } else {  // the trial's outcome (optimization_algorithm_levenberg.cpp:116-165)
-          const double tempChi = trial_ok ? Sp[27] : DBL_MAX;
-          const double rho = (currentChi - tempChi) / scale;
-          qmax++;
-          const bool accept = rho > 0 && isfinite(tempChi);
-          if (accept) {
-            double alpha = 1. - pow(2 * rho - 1, 3.0);
-            alpha = fmin(alpha, 2. / 3.);
-            lambda *= fmax(1. / 3., alpha);
-            ni = 2;
-            currentChi = tempChi;
-            T = Tn;
-            lb ^= 1;
-            S = Sp;
-          } else {
-            lambda *= ni;
-            ni *= 2;  // T stays: the edges keep the errors of the rejected estimate
-          }
-          if (accept || !(rho < 0 && qmax < 10)) {  // the iteration ends
-            lm_total++;
-            if (qmax == 10 || rho == 0) break;
-            if ((iniChi - currentChi) * 1e3 < iniChi) nbad++;
-            else nbad = 0;
-            if (nbad >= 3 || ++it == 10) break;
-            if (!accept) {  // the next iteration recomputes the errors at T
-              fresh = true;
-              Tn = T;
-              continue;
-            }
-            new_iter = true;
-          }
-        }
-        fresh = false;
-        if (new_iter) {
-          currentChi = S[27];
-          iniChi = currentChi;
-          qmax = 0;
-          if (it == 0) {  // computeLambdaInit: tau * max |H_jj|, tau = 1e-5
-            double maxd = 0.0;
-#pragma unroll
-            for (int j = 0; j < 6; j++) maxd = fmax(fabs(S[j * 6 - (j * (j - 1)) / 2]), maxd);
-            lambda = 1e-5 * maxd;
-            ni = 2;
-            nbad = 0;
-          }
-        }
-        double x[6] = {0, 0, 0, 0, 0, 0};
-        trial_ok = solve_step(S, S + kNH, T, x, Tn);
-        ptick(5);
-        scale = 0.0;
-#pragma unroll
-        for (int j = 0; j < 6; j++) scale += x[j] * (lambda * x[j] + S[kNH + j]);
-        scale += 1e-3;
-      }
-    } else {
-    for (int it = 0; it < 10; it++) {
-      double acc[32];
-      linearise(T, acc);
       ptick(0);
-      const double* S = fs.sum32(acc, 0);
+      const double* S = fs.sum32(acc);
       ptick(1);
       const double* H = S;
       const double* b = S + kNH;
@@ -551,7 +427,39 @@ __global__ __launch_bounds__(64 * W) void pose_opt_kernel(
       int qmax = 0;
       do {
         const SE3 backup = T;
-        const bool ok = solve_step(H, b, backup, x, T);
+        bool ok;
+        if constexpr (W == 1) {
+          ok = ldlt_solve6(H, lambda, b, x);
+          T = se3_left_update(x, backup);
+        } else {  // wave 0 alone (its SIMD undisturbed), then a broadcast through LDS
+          if (wave_id() == 0) {
+            ok = ldlt_solve6(H, lambda, b, x);
+            T = se3_left_update(x, backup);
+            if ((tid & 63) == 0) {
+#pragma unroll
+              for (int j = 0; j < 6; j++) fs.bc[j] = x[j];
+              fs.bc[6] = T.r.x;
+              fs.bc[7] = T.r.y;
+              fs.bc[8] = T.r.z;
+              fs.bc[9] = T.r.w;
+              fs.bc[10] = T.t[0];
+              fs.bc[11] = T.t[1];
+              fs.bc[12] = T.t[2];
+              fs.bc[13] = ok ? 1.0 : 0.0;
+            }
+          }
+          __syncthreads();  // the next write of bc follows sum1's barrier, after every read
+#pragma unroll
+          for (int j = 0; j < 6; j++) x[j] = fs.bc[j];
+          T.r.x = fs.bc[6];
+          T.r.y = fs.bc[7];
+          T.r.z = fs.bc[8];
+          T.r.w = fs.bc[9];
+          T.t[0] = fs.bc[10];
+          T.t[1] = fs.bc[11];
+          T.t[2] = fs.bc[12];
+          ok = fs.bc[13] != 0.0;
+        }
         ptick(5);
         // ---- trial: computeActiveErrors + activeRobustChi2 at the new estimate ----
         double part = 0.0;
@@ -595,7 +503,6 @@ __global__ __launch_bounds__(64 * W) void pose_opt_kernel(
       if ((iniChi - currentChi) * 1e3 < iniChi) nbad++;
       else nbad = 0;
       if (nbad >= 3) break;
-    }
     }
     // ---- classify (optimizer.cpp:352-401): inactive edges get their error at the final T ----
     double bad = 0.0;

@@ -98,3 +98,43 @@ def test_global_ba_map_scale_loop(oracle, gpu_lib, n_kf):
     assert its == its_o
     assert_close(kf, kf_o, P["kf_Tcw"], f"{n_kf}-keyframe loop poses")
     assert_close(pts, pts_o, P["points"], f"{n_kf}-keyframe loop points")
+
+
+def test_local_ba_runs_beside_a_global_ba(oracle, gpu_lib):
+    """The LocalMapper's LocalBundleAdjustment and the LoopCloser's global BA run on their own
+    threads in the reference (local_mapper.cpp:53, loop_closer.cpp:77). Their coop solves share
+    the device's residency budget (64 + 128 of 256 work-groups) instead of a lock, so a C5
+    LocalBA started while a 1500-keyframe global BA is running finishes before it, and both match
+    the oracle."""
+    import threading
+    import time
+    G = gpu_lib
+    PM = S.map_problem(1540, 1500)
+    P5 = S.c5_problem(11)
+    kf_m, pts_m, its_m = oracle.global_ba(CAM, PM, 10, True)
+    kf_5, pts_5, er_5, its_5 = oracle.local_ba(CAM, P5)
+    out, errors, t_end = {}, [], {}
+
+    def gba():
+        try:
+            out["gba"] = run(G, PM, 10, True)
+            t_end["gba"] = time.perf_counter()
+        except Exception as e:  # reported by the main thread
+            errors.append(e)
+
+    th = threading.Thread(target=gba)
+    th.start()
+    time.sleep(0.02)  # the global BA is on the device first
+    from test_ba_gpu import run_host
+    r5 = run_host(G, P5)
+    t_end["lba"] = time.perf_counter()
+    th.join(timeout=60)
+    assert not errors, errors
+    assert t_end["lba"] < t_end["gba"], "the LocalBA waited for the global BA"
+    kf, pts, er, its = r5
+    assert its == its_5 and np.array_equal(er, er_5)
+    assert_close(kf, kf_5, P5["kf_Tcw"], "LocalBA poses beside a global BA")
+    kf, pts, its = out["gba"]
+    assert its == its_m
+    assert_close(kf, kf_m, PM["kf_Tcw"], "global BA poses beside a LocalBA")
+    assert_close(pts, pts_m, PM["points"], "global BA points beside a LocalBA")

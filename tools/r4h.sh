@@ -1,0 +1,13 @@
+set -o pipefail
+O=gpurun_out/r4h; mkdir -p $O
+SLAMGPU_LIB=$(realpath tools/abl/libslamgpu_poseprof.so) timeout -k 10 200 python tools/pose_lat_ab.py tools/abl/libslamgpu_poseprof.so > $O/poseprof.log 2>&1
+SLAMGPU_LIB=$(realpath tools/abl/libslamgpu_poseprof.so) timeout -k 10 200 python -c "
+import sys; sys.path.insert(0,'.')
+import numpy as np
+from slam_framework_amd import slamgpu as G, synthetic as S
+p = S.c4_problem(7)
+for _ in range(3):
+    r = G.Optimizer.PoseOptimization(p[0], p[1].copy(), S.KITTI_CAM, p[3])
+print('done')
+" > $O/poseprof_host.log 2>&1
+exit 0
