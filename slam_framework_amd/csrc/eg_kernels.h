@@ -35,6 +35,8 @@ struct EgGraph {
   const int32_t* ext_ptr;      // [F + 1]
   const int32_t* ext_rows;
   const int64_t* ext_base;     // per extent entry: off[row] - start[row] (block (row, j) at + j)
+  int n_ext;                   // extent entries (ext_ptr[F]; host copy, sizes the staged variant)
+  int64_t n_blocks;            // blocks of the profile
 };
 
 // Mutable device state of one call.

@@ -209,6 +209,11 @@ __device__ __forceinline__ double bcast(double x, int l) {
   return __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
 }
 
+// kMeta: the factorisation's structure -- ext_ptr, ext_rows, ext_base and each column's
+// diagonal block index -- is staged in LDS at the start (dynamic LDS, 4 B per entry), so the
+// per-column chain of dependent structure loads (ext_ptr -> ext_base -> the block) reads LDS
+// instead of L2. The host takes this variant whenever the structure fits (eg_meta_bytes).
+template <bool kMeta>
 __global__ __launch_bounds__(kFacThreads) void eg_factor_solve_kernel(EgGraph G, EgState W,
                                                                       int64_t n_blocks,
                                                                       double lambda) {
@@ -222,17 +227,38 @@ __global__ __launch_bounds__(kFacThreads) void eg_factor_solve_kernel(EgGraph G,
   __shared__ double s_y[2][7];    // its forward-solved rhs slice
   __shared__ double s_nx[49];     // the next diagonal block after its last update
   __shared__ double s_pan[kPanStage * 49];  // column k's panel blocks L_ik (extents <= kPanStage)
+  extern __shared__ int32_t s_meta[];  // kMeta: ext_ptr [F + 1], diag block [F], rows, bases
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, F = G.F;
   double* L = W.L;  // a copy of H (launch_eg_factor_solve)
   double* y = W.y;
+  const int n_ext = kMeta ? G.ext_ptr[F] : 0;
+  int32_t* const m_ep = s_meta;
+  int32_t* const m_db = s_meta + F + 1;
+  int32_t* const m_er = m_db + F;
+  int32_t* const m_eb = m_er + n_ext;
+  if constexpr (kMeta) {
+    for (int q = tid; q <= F; q += kFacThreads) m_ep[q] = G.ext_ptr[q];
+    for (int q = tid; q < F; q += kFacThreads) m_db[q] = (int32_t)(G.off[q] + (q - G.start[q]));
+    for (int q = tid; q < n_ext; q += kFacThreads) {
+      m_er[q] = G.ext_rows[q];
+      m_eb[q] = (int32_t)G.ext_base[q];
+    }
+  }
+  auto EP = [&](int k) -> int { return kMeta ? m_ep[k] : G.ext_ptr[k]; };
+  auto ER = [&](int e) -> int { return kMeta ? m_er[e] : G.ext_rows[e]; };
+  auto EB = [&](int e) -> int64_t { return kMeta ? (int64_t)m_eb[e] : G.ext_base[e]; };
+  auto DB = [&](int k) -> int64_t {
+    return kMeta ? (int64_t)m_db[k] : G.off[k] + (k - G.start[k]);
+  };
+  __syncthreads();
   for (int q = tid; q < 7 * F; q += kFacThreads) {
     const int v = q / 7, r = q % 7;
-    L[(G.off[v] + (v - G.start[v])) * 49 + 8 * r] += lambda;  // setLambda: H + lambda I
+    L[DB(v) * 49 + 8 * r] += lambda;  // setLambda: H + lambda I
     y[q] = W.b[q];
   }
   if (tid == 0) s_ok = 1;
   __syncthreads();
-  auto diag_of = [&](int k) { return L + (G.off[k] + (k - G.start[k])) * 49; };
+  auto diag_of = [&](int k) { return L + DB(k) * 49; };
   // lanes 0-6 of a wave, lane r holding row r: LDLT of diagonal block k from src (lower
   // triangle + diagonal), the forward solve of y_k; L_kk / D_k to the profile and to s_kk[buf],
   // 1 / D_k to s_rd[buf], y_k to s_y[buf]. Column j: lane j forms the pivot, readlane broadcasts
@@ -288,13 +314,13 @@ __global__ __launch_bounds__(kFacThreads) void eg_factor_solve_kernel(EgGraph G,
   // ---- factorisation + forward solve ----
   for (int k = 0; k < F; k++) {
     const int cur = k & 1;
-    const int e0 = G.ext_ptr[k], ne = G.ext_ptr[k + 1] - e0;
+    const int e0 = EP(k), ne = EP(k + 1) - e0;
     const bool staged = ne <= kPanStage;  // the panel also goes to LDS for the update below
     double an = 0.0;  // wave 0: the next diagonal block, final but for this column's update
     if (wid == 0 && lane < 49 && k + 1 < F) an = diag_of(k + 1)[lane];
     for (int q = tid; q < 7 * ne; q += kFacThreads) {  // panel rows
       const int t = q / 7, r = q % 7;
-      double* Aik = L + (G.ext_base[e0 + t] + k) * 49 + 7 * r;
+      double* Aik = L + (EB(e0 + t) + k) * 49 + 7 * r;
       double a[7];
 #pragma unroll
       for (int c = 0; c < 7; c++) a[c] = Aik[c];
@@ -316,10 +342,10 @@ __global__ __launch_bounds__(kFacThreads) void eg_factor_solve_kernel(EgGraph G,
         if (staged) s_pan[q * 7 + c] = a[c];
         sy += a[c] * s_y[cur][c];
       }
-      y[7 * G.ext_rows[e0 + t] + r] -= sy;
+      y[7 * ER(e0 + t) + r] -= sy;
     }
     __syncthreads();
-    const bool nxt_in = k + 1 < F && ne > 0 && G.ext_rows[e0] == k + 1;
+    const bool nxt_in = k + 1 < F && ne > 0 && ER(e0) == k + 1;
     if (wid == 0) {
       if (k + 1 < F) {  // the next diagonal block: its last update, then its factorisation
         if (lane < 49) {
@@ -331,7 +357,7 @@ __global__ __launch_bounds__(kFacThreads) void eg_factor_solve_kernel(EgGraph G,
 #pragma unroll
               for (int m = 0; m < 7; m++) t += s_pan[7 * r + m] * s_kk[cur][8 * m] * s_pan[7 * c + m];
             } else {
-              const double* Ln = L + (G.ext_base[e0] + k) * 49;
+              const double* Ln = L + (EB(e0) + k) * 49;
 #pragma unroll
               for (int m = 0; m < 7; m++) t += Ln[7 * r + m] * s_kk[cur][8 * m] * Ln[7 * c + m];
             }
@@ -352,8 +378,8 @@ __global__ __launch_bounds__(kFacThreads) void eg_factor_solve_kernel(EgGraph G,
         while ((ti + 1) * (ti + 2) / 2 <= pair) ti++;
         while (ti * (ti + 1) / 2 > pair) ti--;
         const int tj = pair - ti * (ti + 1) / 2;
-        const int j = G.ext_rows[e0 + tj];
-        const int64_t bi = G.ext_base[e0 + ti], bj = G.ext_base[e0 + tj];
+        const int j = ER(e0 + tj);
+        const int64_t bi = EB(e0 + ti), bj = EB(e0 + tj);
         const int r = ent / 7, c = ent % 7;
         double t = 0.0;
         if (staged) {
@@ -377,12 +403,12 @@ __global__ __launch_bounds__(kFacThreads) void eg_factor_solve_kernel(EgGraph G,
   __syncthreads();
   if (wid == 0) {
     for (int k = F - 1; k >= 0; k--) {
-      const int e0 = G.ext_ptr[k], ne = G.ext_ptr[k + 1] - e0;
+      const int e0 = EP(k), ne = EP(k + 1) - e0;
       if (lane < 7) {  // y_k -= sum over the later rows i of L_ik' x_i (lane c: component c)
         double acc = 0.0;
         for (int t = 0; t < ne; t++) {
-          const double* Lik = L + (G.ext_base[e0 + t] + k) * 49;
-          const double* xi = y + 7 * G.ext_rows[e0 + t];
+          const double* Lik = L + (EB(e0 + t) + k) * 49;
+          const double* xi = y + 7 * ER(e0 + t);
 #pragma unroll
           for (int r = 0; r < 7; r++) acc += Lik[7 * r + lane] * xi[r];
         }
@@ -513,13 +539,26 @@ hipError_t launch_eg_assemble(const EgGraph& G, const EgState& W, int64_t n_bloc
   return hipGetLastError();
 }
 
+// Dynamic LDS of the staged-structure factorisation, 0 when it does not fit beside the static
+// arrays (s_pan and the rest, ~45 KB) or a block index exceeds 31 bits.
+static size_t eg_meta_bytes(const EgGraph& G) {
+  if (G.n_ext < 0 || G.n_blocks > INT32_MAX) return 0;
+  const size_t b = 4 * (2 * (size_t)G.F + 1 + 2 * (size_t)G.n_ext);
+  return b <= 100 * 1024 ? b : 0;
+}
+
 hipError_t launch_eg_factor_solve(const EgGraph& G, const EgState& W, int64_t n_blocks,
                                   double lambda, hipStream_t st) {
   hipError_t e = hipMemcpyAsync(W.L, W.H, (size_t)n_blocks * 49 * sizeof(double),
                                 hipMemcpyDeviceToDevice, st);
   if (e != hipSuccess) return e;
-  SLAMGPU_LAUNCH("eg_factor_solve", st, eg_factor_solve_kernel, dim3(1), dim3(kFacThreads), 0, st,
-                 G, W, n_blocks, lambda);
+  const size_t meta = eg_meta_bytes(G);
+  if (meta > 0)
+    SLAMGPU_LAUNCH("eg_factor_solve", st, eg_factor_solve_kernel<true>, dim3(1), dim3(kFacThreads),
+                   meta, st, G, W, n_blocks, lambda);
+  else
+    SLAMGPU_LAUNCH("eg_factor_solve", st, eg_factor_solve_kernel<false>, dim3(1), dim3(kFacThreads),
+                   0, st, G, W, n_blocks, lambda);
   return hipGetLastError();
 }
 

@@ -804,6 +804,8 @@ int slamgpu_optimize_essential_graph(int n_kf, double* Scw, const uint8_t* fixed
   G.ext_ptr = reinterpret_cast<const int32_t*>(d + o_ep);
   G.ext_rows = reinterpret_cast<const int32_t*>(d + o_er);
   G.ext_base = reinterpret_cast<const int64_t*>(d + o_eb);
+  G.n_ext = (int)ext_rows.size();
+  G.n_blocks = n_blocks;
   EgState W;
   W.S = reinterpret_cast<double*>(d + o_S);
   W.S_trial = reinterpret_cast<double*>(d + o_S2);

@@ -58,10 +58,12 @@ struct OrbGeomDev {
 
 // Optional side streams of the extraction (all null: everything on `st`):
 //   side0: FAST of level 0 (reads only the caller's images) beside the pyramid, joined before
-//          the octree;
+//          the octree; after the extraction, the left views' undistortion + grid beside the
+//          stereo matching (fork1 / join1, runtime.cpp run_frontend).
 struct ExtractStreams {
   hipStream_t side0 = nullptr;
   hipEvent_t fork0 = nullptr, join0 = nullptr;
+  hipEvent_t fork1 = nullptr, join1 = nullptr;
 };
 void launch_extract(const ImageBatch& b, const OrbGeomDev& g, int n_images, hipStream_t st,
                     const ExtractStreams& fx = ExtractStreams());

@@ -748,13 +748,13 @@ __device__ void divide_wave(const OctNode& nd, uint32_t* const keys[2], OctNode 
   }
 }
 
-__global__ __launch_bounds__(kOctThreads) void octree_kernel(
-    const OrbGeom* __restrict__ g, const uint32_t* __restrict__ cell_keys,
-    const int* __restrict__ cell_count, uint32_t* __restrict__ key_scratch,
-    OctNode* __restrict__ node_scratch, uint32_t* __restrict__ oct_keys,
-    int* __restrict__ oct_count, uint32_t* __restrict__ err) {
-  __shared__ OctShared S;
-  const int level = blockIdx.x, img = blockIdx.y;
+// The global-memory DistributeOctTree of one (level, image) by a 256-thread work-group, for the
+// levels the LDS kernels cannot hold (their oct_count entry is -1). S: LDS scratch.
+__device__ __forceinline__ void octree_global(
+    OctShared& S, int level, int img, const OrbGeom* __restrict__ g,
+    const uint32_t* __restrict__ cell_keys, const int* __restrict__ cell_count,
+    uint32_t* __restrict__ key_scratch, OctNode* __restrict__ node_scratch,
+    uint32_t* __restrict__ oct_keys, int* __restrict__ oct_count, uint32_t* __restrict__ err) {
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const LevelGeom& L = g->lv[level];
   const int N = L.budget;
@@ -1081,6 +1081,16 @@ __global__ __launch_bounds__(kOctThreads) void octree_kernel(
     if (m > L.out_cap) atomicOr(err, kErrNodeOverflow);
     *outc = mout;
   }
+}
+
+__global__ __launch_bounds__(kOctThreads) void octree_kernel(
+    const OrbGeom* __restrict__ g, const uint32_t* __restrict__ cell_keys,
+    const int* __restrict__ cell_count, uint32_t* __restrict__ key_scratch,
+    OctNode* __restrict__ node_scratch, uint32_t* __restrict__ oct_keys,
+    int* __restrict__ oct_count, uint32_t* __restrict__ err) {
+  __shared__ OctShared S;
+  octree_global(S, blockIdx.x, blockIdx.y, g, cell_keys, cell_count, key_scratch, node_scratch,
+                oct_keys, oct_count, err);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -1676,7 +1686,8 @@ __device__ void lvl_block_scan(int* a, int n, int* red) {
 __global__ __launch_bounds__(kOctLvlThreads) void octree_lvl_kernel(
     const OrbGeom* __restrict__ g, const uint32_t* __restrict__ cell_keys,
     const int* __restrict__ cell_count, uint32_t* __restrict__ key_scratch,
-    uint32_t* __restrict__ oct_keys, int* __restrict__ oct_count, uint32_t* __restrict__ err) {
+    OctNode* __restrict__ node_scratch, uint32_t* __restrict__ oct_keys,
+    int* __restrict__ oct_count, uint32_t* __restrict__ err) {
   extern __shared__ __attribute__((aligned(16))) uint8_t s_lvl[];
   __shared__ int s_red[kOctLvlWaves];
   __shared__ int s_bc[kOctLvlWaves][16];  // per-wave bucket counts of one placement round
@@ -1691,7 +1702,9 @@ __global__ __launch_bounds__(kOctLvlThreads) void octree_lvl_kernel(
   const int64_t cbase = (int64_t)img * g->cells_per_image + L.cell_base;
   int* const outc = oct_count + img * nlev + level;
   uint32_t* const outk = oct_keys + (int64_t)img * g->out_per_image + L.out_base;
-  // ---- 1. candidate count; levels that do not fit fall back to octree_kernel
+  // ---- 1. candidate count; a level that does not fit is done here by the global-memory
+  // algorithm (octree_global, its scratch on this work-group's LDS; the host checked it fits),
+  // so the small launches need no octree_kernel launch after this one
   int K = 0;
   for (int c = tid; c < ncell; c += kOctLvlThreads) K += cell_count[cbase + c];
   K = lvl_block_sum(K, s_red);
@@ -1699,6 +1712,10 @@ __global__ __launch_bounds__(kOctLvlThreads) void octree_lvl_kernel(
   const int NC = L.oct_nc;
   if (K > g->oct2_kcap || nIni > 16 || ncell + 1 > g->oct2_ccap || NC > g->oct2_nc) {
     if (tid == 0) *outc = -1;
+    __syncthreads();
+    static_assert(kOctLvlThreads == kOctThreads, "octree_global runs on this work-group");
+    octree_global(*reinterpret_cast<OctShared*>(s_lvl), level, img, g, cell_keys, cell_count,
+                  key_scratch, node_scratch, oct_keys, oct_count, err);
     return;
   }
   if (K == 0) {
@@ -2523,18 +2540,24 @@ void launch_extract(const ImageBatch& b, const OrbGeomDev& gd, int n_images, hip
       fast(0, g.cells_per_image, st);
     }
   }
-  if (octree_per_level(n_images))
+  // the per-level kernel redoes its oversized levels itself (its LDS sized for the global
+  // algorithm's scratch too): no octree_kernel launch after it -- the single-frame call's chain
+  // is one dependent launch shorter; after the per-image kernel octree_kernel does them
+  const bool lvl = octree_per_level(n_images);
+  if (lvl)
     SLAMGPU_LAUNCH("octree", st, octree_lvl_kernel, dim3(g.nlevels, n_images),
-                   dim3(kOctLvlThreads), (size_t)g.oct2_lds_bytes, st, gd.dev, gd.ws.cell_keys,
-                   gd.ws.cell_count, gd.ws.key_scratch, gd.ws.oct_keys, gd.ws.oct_count,
-                   gd.ws.err);
+                   dim3(kOctLvlThreads), std::max((size_t)g.oct2_lds_bytes, sizeof(OctShared)),
+                   st, gd.dev, gd.ws.cell_keys, gd.ws.cell_count, gd.ws.key_scratch,
+                   gd.ws.node_scratch, gd.ws.oct_keys, gd.ws.oct_count, gd.ws.err);
   else
     SLAMGPU_LAUNCH("octree", st, octree_img_kernel, dim3(n_images), dim3(64 * g.nlevels),
                    (size_t)g.oct_lds_bytes, st, gd.dev, gd.ws.cell_keys, gd.ws.cell_count,
                    gd.ws.key_scratch, gd.ws.oct_keys, gd.ws.oct_count, gd.ws.err);
-  SLAMGPU_LAUNCH("octree_global", st, octree_kernel, dim3(g.nlevels, n_images), dim3(kOctThreads), 0, st, gd.dev,
-                     gd.ws.cell_keys, gd.ws.cell_count, gd.ws.key_scratch, gd.ws.node_scratch,
-                     gd.ws.oct_keys, gd.ws.oct_count, gd.ws.err);
+  if (!lvl)
+    SLAMGPU_LAUNCH("octree_global", st, octree_kernel, dim3(g.nlevels, n_images),
+                   dim3(kOctThreads), 0, st, gd.dev, gd.ws.cell_keys, gd.ws.cell_count,
+                   gd.ws.key_scratch, gd.ws.node_scratch, gd.ws.oct_keys, gd.ws.oct_count,
+                   gd.ws.err);
   if (n_images <= kOdSmallMaxImages) {
     constexpr int kpw = kKpPerWave / 2;
     SLAMGPU_LAUNCH("orient_desc", st, orient_desc_kernel<kpw>,

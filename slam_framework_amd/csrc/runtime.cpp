@@ -296,7 +296,9 @@ int slamgpu_create(int device, const slamgpu_orb_params* p, int cols, int rows, 
     if (mode >= 1)
       TRY(hipStreamCreateWithFlags(&fx.side0, hipStreamNonBlocking) == hipSuccess &&
                   hipEventCreateWithFlags(&fx.fork0, hipEventDisableTiming) == hipSuccess &&
-                  hipEventCreateWithFlags(&fx.join0, hipEventDisableTiming) == hipSuccess
+                  hipEventCreateWithFlags(&fx.join0, hipEventDisableTiming) == hipSuccess &&
+                  hipEventCreateWithFlags(&fx.fork1, hipEventDisableTiming) == hipSuccess &&
+                  hipEventCreateWithFlags(&fx.join1, hipEventDisableTiming) == hipSuccess
               ? 0
               : fail(c, SLAMGPU_EHIP, "side stream / events"));
   }
@@ -365,7 +367,7 @@ void slamgpu_destroy(slamgpu_ctx* c) {
   if (c->h_res) (void)hipHostFree(c->h_res);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   if (c->fx.side0) (void)hipStreamDestroy(c->fx.side0);
-  for (hipEvent_t e : {c->fx.fork0, c->fx.join0})
+  for (hipEvent_t e : {c->fx.fork0, c->fx.join0, c->fx.fork1, c->fx.join1})
     if (e) (void)hipEventDestroy(e);
   delete c;
 }
@@ -418,12 +420,26 @@ static int run_frontend(slamgpu_ctx* c, const ImageBatch& b, int n_frames, int n
   OrbGeomDev g = c->gd();
   launch_extract(b, g, n_images, st, c->fx);
   if (stereo) {
-    launch_stereo(b, g, c->cam, n_frames, c->sws, c->sout, st);
-    if (c->dist_on)  // Frame ctor: UndistortKeyPoints after ComputeStereoMatches (frame.cpp:96)
+    // UndistortKeyPoints + AssignFeaturesToGrid read only the left views' keypoints (frame.cpp:
+    // 96, 110; stereo matching reads the distorted ones): on the side stream beside
+    // ComputeStereoMatches, joined after it -- two fewer launches on the call's critical path
+    const ExtractStreams& fx = c->fx;
+    const bool fork = fx.side0 && fx.fork1 && fx.join1;
+    hipStream_t gs = fork ? fx.side0 : st;
+    if (fork) {
+      HIPCHECK(c, hipEventRecord(fx.fork1, st));
+      HIPCHECK(c, hipStreamWaitEvent(gs, fx.fork1, 0));
+    }
+    if (c->dist_on)
       launch_undistort(FrameKps{c->out.kps, c->out.desc, c->out.nkps, 2 * (int64_t)c->geom.kp_cap, 2},
                        c->kps_un, 2 * (int64_t)c->geom.kp_cap, c->cam, c->dist, n_frames,
-                       c->geom.kp_cap, st);
-    launch_grid(left_views(c), c->cam, n_frames, c->geom.kp_cap, c->gws, st);
+                       c->geom.kp_cap, gs);
+    launch_grid(left_views(c), c->cam, n_frames, c->geom.kp_cap, c->gws, gs);
+    launch_stereo(b, g, c->cam, n_frames, c->sws, c->sout, st);
+    if (fork) {
+      HIPCHECK(c, hipEventRecord(fx.join1, gs));
+      HIPCHECK(c, hipStreamWaitEvent(st, fx.join1, 0));
+    }
   }
   HIPCHECK(c, hipGetLastError());
   return 0;
