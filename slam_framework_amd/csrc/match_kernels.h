@@ -46,9 +46,12 @@ struct StereoOut {
 void launch_trace_marker(int id, hipStream_t st);
 
 void launch_frame_pack(const FrameKps& ext, const float* u_right, const float* depth,
-                       const uint32_t* err, int kp_cap, uint8_t* dst, hipStream_t st);
+                       const uint32_t* err, int kp_cap, uint8_t* dst, hipStream_t st,
+                       int parts = 3);
+// pack: the single-frame call's packed record (frame 0's u_right / depth go there too), or null
 void launch_stereo(const ImageBatch& b, const OrbGeomDev& g, const Camera& cam, int n_frames,
-                   const StereoWorkspace& ws, const StereoOut& out, hipStream_t st);
+                   const StereoWorkspace& ws, const StereoOut& out, hipStream_t st,
+                   uint8_t* pack = nullptr);
 
 // Frame::UndistortKeyPoints of n_sets keypoint sets (set f: src.kps + f * src.stride, count
 // src.n[f * src.n_stride]) into dst + f * dst_stride.

@@ -355,9 +355,14 @@ __global__ __launch_bounds__(256) void stereo_match_kernel(ImageBatch b,
 // Median SAD filter (:564-576): drop matches whose SAD >= 2.1 * median. The median (element
 // n / 2 of the ascending sort, :564-566) is found by an MSB-first radix select over the SADs
 // (four 8-bit digit histograms) instead of sorting them.
+// pack (the single-frame call, frame 0 only): the frame's final u_right / depth also go to the
+// packed host-mirror record (frame_pack_kernel's layout), and the device error word to its
+// header slot 8 -- no frame_pack launch after this one on the call's critical path.
 __global__ __launch_bounds__(256) void stereo_median_kernel(const OrbGeom* __restrict__ g,
                                                             FrameKps ext, StereoWorkspace ws,
-                                                            StereoOut out) {
+                                                            StereoOut out,
+                                                            uint8_t* __restrict__ pack,
+                                                            const uint32_t* __restrict__ err) {
   constexpr int kCap = 4096;
   __shared__ uint32_t vals[kCap];
   __shared__ int hist[256];
@@ -380,10 +385,10 @@ __global__ __launch_bounds__(256) void stereo_median_kernel(const OrbGeom* __res
   }
   __syncthreads();
   const int n = n_valid;
-  if (n == 0) return;  // the reference indexes an empty vector here (UB); we skip the filter
+  // n == 0: the reference indexes an empty vector here (UB); we skip the filter
   uint32_t prefix = 0, mask = 0;
   int k = n / 2;  // rank of the median among the values matching prefix under mask
-  for (int shift = 24; shift >= 0; shift -= 8) {
+  for (int shift = 24; shift >= 0 && n > 0; shift -= 8) {
     hist[tid] = 0;
     __syncthreads();
     for (int i = tid; i < n; i += 256) {
@@ -423,32 +428,50 @@ __global__ __launch_bounds__(256) void stereo_median_kernel(const OrbGeom* __res
   }
   const float median = (float)(int)prefix;
   const float thDist = (1.5f * 1.4f) * median;
-  for (int i = tid; i < nl; i += 256) {
-    const int s = ws.sad[base + i];
-    if (s >= 0 && !((float)s < thDist)) {
+  const size_t kc = (size_t)g->kp_cap;
+  float* const pur = pack && f == 0
+                         ? reinterpret_cast<float*>(pack + 16 + 2 * kc * sizeof(KeyPoint) + 2 * kc * 32)
+                         : nullptr;
+  const int nall = pur ? min(max(ext.n[0], 0), (int)kc) : nl;
+  for (int i = tid; i < nall; i += 256) {
+    const int s = i < nl ? ws.sad[base + i] : -1;
+    if (n > 0 && s >= 0 && !((float)s < thDist)) {
       out.u_right[base + i] = -1.0f;
       out.depth[base + i] = -1.0f;
       ws.sad[base + i] = -1;
+      if (pur) pur[i] = pur[kc + i] = -1.0f;
+    } else if (pur) {
+      pur[i] = out.u_right[base + i];
+      pur[kc + i] = out.depth[base + i];
     }
   }
+  __syncthreads();  // every error bit this stream's kernels raise is in err by now
+  if (pur && tid == 0) reinterpret_cast<uint32_t*>(pack)[2] = *err;
 }
 
 // ---------------------------------------------------------------------------------------
 // Frame results -> the host mirror's layout (see match_kernels.h), copied as dwords.
+// parts: bit 0 -- the counts, both views' keypoints and descriptors, the error word to header
+// slot 12; bit 1 -- u_right / depth, the error word to slot 8 (stereo_median_kernel does this part
+// itself in the single-frame call). The host ORs the two error slots.
 __global__ __launch_bounds__(256) void frame_pack_kernel(FrameKps ext,
                                                          const float* __restrict__ u_right,
                                                          const float* __restrict__ depth,
                                                          const uint32_t* __restrict__ err,
-                                                         int kp_cap, uint8_t* __restrict__ dst) {
+                                                         int kp_cap, uint8_t* __restrict__ dst,
+                                                         int parts) {
   const int gid = blockIdx.x * blockDim.x + threadIdx.x, gsz = gridDim.x * blockDim.x;
   const int c0 = ext.n[0], c1 = ext.n[ext.n_stride];
   const int n0 = min(max(c0, 0), kp_cap), n1 = min(max(c1, 0), kp_cap);
   const size_t kc = (size_t)kp_cap;
   if (gid == 0) {
     int* h = reinterpret_cast<int*>(dst);
-    h[0] = c0;
-    h[1] = c1;
-    h[2] = (int)*err;
+    if (parts & 1) {
+      h[0] = c0;
+      h[1] = c1;
+      h[3] = (int)*err;
+    }
+    if (parts & 2) h[2] = (int)*err;
   }
   auto copy = [&](const void* src, size_t dst_off, int words) {
     const uint32_t* s = reinterpret_cast<const uint32_t*>(src);
@@ -457,19 +480,23 @@ __global__ __launch_bounds__(256) void frame_pack_kernel(FrameKps ext,
   };
   const size_t kps_off = 16, desc_off = kps_off + 2 * kc * sizeof(KeyPoint);
   const size_t ur_off = desc_off + 2 * kc * 32, dp_off = ur_off + kc * sizeof(float);
-  copy(ext.kps, kps_off, 7 * n0);
-  copy(ext.kps + ext.stride, kps_off + kc * sizeof(KeyPoint), 7 * n1);
-  copy(ext.desc, desc_off, 8 * n0);
-  copy(ext.desc + 32 * ext.stride, desc_off + 32 * kc, 8 * n1);
-  copy(u_right, ur_off, n0);
-  copy(depth, dp_off, n0);
+  if (parts & 1) {
+    copy(ext.kps, kps_off, 7 * n0);
+    copy(ext.kps + ext.stride, kps_off + kc * sizeof(KeyPoint), 7 * n1);
+    copy(ext.desc, desc_off, 8 * n0);
+    copy(ext.desc + 32 * ext.stride, desc_off + 32 * kc, 8 * n1);
+  }
+  if (parts & 2) {
+    copy(u_right, ur_off, n0);
+    copy(depth, dp_off, n0);
+  }
 }
 
 void launch_frame_pack(const FrameKps& ext, const float* u_right, const float* depth,
-                       const uint32_t* err, int kp_cap, uint8_t* dst, hipStream_t st) {
+                       const uint32_t* err, int kp_cap, uint8_t* dst, hipStream_t st, int parts) {
   static_assert(sizeof(KeyPoint) == 28, "keypoint layout");
   SLAMGPU_LAUNCH("frame_pack", st, frame_pack_kernel, dim3(32), dim3(256), 0, st, ext, u_right,
-                 depth, err, kp_cap, dst);
+                 depth, err, kp_cap, dst, parts);
 }
 
 __global__ void trace_marker_kernel() {}
@@ -479,7 +506,8 @@ void launch_trace_marker(int id, hipStream_t st) {
 }
 
 void launch_stereo(const ImageBatch& b, const OrbGeomDev& gd, const Camera& cam, int n_frames,
-                   const StereoWorkspace& ws, const StereoOut& out, hipStream_t st) {
+                   const StereoWorkspace& ws, const StereoOut& out, hipStream_t st,
+                   uint8_t* pack) {
   const OrbGeom& g = *gd.host;
   FrameKps ext{gd.out.kps, gd.out.desc, gd.out.nkps, g.kp_cap, 1};
   const int nrows = g.lv[0].h;
@@ -489,8 +517,8 @@ void launch_stereo(const ImageBatch& b, const OrbGeomDev& gd, const Camera& cam,
   SLAMGPU_LAUNCH("stereo_match", st, stereo_match_kernel<kG>,
                  dim3((g.kp_cap + kPerBlock - 1) / kPerBlock, n_frames), dim3(256), 0, st, b,
                  gd.dev, ext, cam, nrows, ws, out);
-  SLAMGPU_LAUNCH("stereo_median", st, stereo_median_kernel, dim3(n_frames), dim3(256), 0, st, gd.dev, ext, ws,
-                     out);
+  SLAMGPU_LAUNCH("stereo_median", st, stereo_median_kernel, dim3(n_frames), dim3(256), 0, st,
+                 gd.dev, ext, ws, out, pack, gd.ws.err);
 }
 
 // ---------------------------------------------------------------------------------------

@@ -199,7 +199,7 @@ static FrameKps left_views(const slamgpu_ctx* c) {
 // keypoints and descriptors at kp_cap each, then frame 0's u_right and depth.
 struct ResMirror {
   int* nkps;
-  uint32_t* err;  // the device error word, copied behind the results
+  uint32_t* err;  // [2]: the device error word, copied by the two packing kernels
   KeyPoint* kps;
   uint8_t* desc;
   float* u_right;
@@ -410,8 +410,11 @@ int slamgpu_orb_scale_tables(const slamgpu_orb_params* p, float* scale, float* i
   return 0;
 }
 
+// pack (the single-frame call): the frame's results are also packed into this record for one
+// D2H copy -- keypoints and descriptors on the side stream beside stereo matching, u_right /
+// depth by stereo_median_kernel.
 static int run_frontend(slamgpu_ctx* c, const ImageBatch& b, int n_frames, int n_images,
-                        bool stereo, hipStream_t st) {
+                        bool stereo, hipStream_t st, uint8_t* pack = nullptr) {
   TimerScope ts(c);
   c->res_valid = false;
   c->batch = b;
@@ -435,7 +438,10 @@ static int run_frontend(slamgpu_ctx* c, const ImageBatch& b, int n_frames, int n
                        c->kps_un, 2 * (int64_t)c->geom.kp_cap, c->cam, c->dist, n_frames,
                        c->geom.kp_cap, gs);
     launch_grid(left_views(c), c->cam, n_frames, c->geom.kp_cap, c->gws, gs);
-    launch_stereo(b, g, c->cam, n_frames, c->sws, c->sout, st);
+    if (pack)
+      launch_frame_pack(FrameKps{c->out.kps, c->out.desc, c->out.nkps, c->geom.kp_cap, 1},
+                        c->sout.u_right, c->sout.depth, c->ws.err, c->geom.kp_cap, pack, gs, 1);
+    launch_stereo(b, g, c->cam, n_frames, c->sws, c->sout, st, pack);
     if (fork) {
       HIPCHECK(c, hipEventRecord(fx.join1, gs));
       HIPCHECK(c, hipStreamWaitEvent(st, fx.join1, 0));
@@ -544,13 +550,7 @@ static int enqueue_frame_stereo(slamgpu_ctx* c) {
   HIPCHECK(c, hipMemcpyAsync(c->d_in, c->h_in, 2 * (size_t)c->in_stride, hipMemcpyHostToDevice,
                              c->stream));
   ImageBatch b{c->d_in, c->d_in + c->in_stride, 2 * c->in_stride, c->in_pitch, c->d_pyr};
-  if (int rc = run_frontend(c, b, 1, 2, true, c->stream)) return rc;
-  {
-    TimerScope ts(c);
-    launch_frame_pack(FrameKps{c->out.kps, c->out.desc, c->out.nkps, c->geom.kp_cap, 1},
-                      c->sout.u_right, c->sout.depth, c->ws.err, c->geom.kp_cap, c->d_res,
-                      c->stream);
-  }
+  if (int rc = run_frontend(c, b, 1, 2, true, c->stream, c->d_res)) return rc;
   HIPCHECK(c, hipMemcpyAsync(c->h_res, c->d_res, res_mirror_bytes(c->geom.kp_cap),
                              hipMemcpyDeviceToHost, c->stream));
   return 0;
@@ -625,8 +625,8 @@ int slamgpu_frame_stereo(slamgpu_ctx* c, const uint8_t* left, const uint8_t* rig
   if (rc) return rc;
   HIPCHECK(c, hipStreamSynchronize(c->stream));
   const ResMirror m = res_mirror(c);
-  if (*m.err) {
-    const uint32_t e = *m.err;
+  if (m.err[0] | m.err[1]) {  // the error word as the two packing kernels saw it
+    const uint32_t e = m.err[0] | m.err[1];
     (void)hipMemset(c->ws.err, 0, sizeof(uint32_t));
     return fail(c, SLAMGPU_EDEVICE, "device capacity overflow (bits 0x%x)", e);
   }
