@@ -193,27 +193,6 @@ __global__ __launch_bounds__(256) void pyr_down_kernel(ImageBatch b, const OrbGe
   pyr_strip<kAligned, kStrip>(b, g, level, img, tx, (ty * 4 + wave_id()) * kStrip, rxt, ryt);
 }
 
-// Small launches (the single-frame call): levels lo .. nlevels - 1 of one image per work-group of
-// 16 waves, level after level, the strips of a level spread over the waves -- one launch instead
-// of nlevels - lo dependent ones (each costs ~10 us of dispatch gap on the call's critical path).
-// A level's rows go to global memory and the work-group barrier orders them before the next
-// level's reads (the work-group's own stores, through its CU's caches).
-constexpr int kPyrChainWaves = 16;
-__global__ __launch_bounds__(64 * kPyrChainWaves) void pyr_chain_kernel(
-    ImageBatch b, const OrbGeom* __restrict__ g, int lo, const ResizeX* __restrict__ rxt,
-    const ResizeY* __restrict__ ryt) {
-  const int img = blockIdx.x, wid = wave_id();
-  for (int l = lo; l < g->nlevels; l++) {
-    const LevelGeom& D = g->lv[l];
-    const int tiles_x = (D.w + 255) >> 8;
-    const int units = tiles_x * ((D.h + kPyrShortStrip - 1) / kPyrShortStrip);
-    for (int u = wid; u < units; u += kPyrChainWaves)
-      pyr_strip<true, kPyrShortStrip>(b, g, l, img, u % tiles_x, (u / tiles_x) * kPyrShortStrip,
-                                      rxt, ryt);
-    __syncthreads();
-  }
-}
-
 // ---------------------------------------------------------------------------------------
 __device__ __forceinline__ int reflect101(int i, int n) {  // cv::BORDER_REFLECT_101, |overshoot| < n
   if (i < 0) i = -i;
@@ -2525,14 +2504,7 @@ void launch_extract(const ImageBatch& b, const OrbGeomDev& gd, int n_images, hip
   const bool in_aligned = (((uintptr_t)b.in_l | (uintptr_t)b.in_r | (uintptr_t)b.in_stride |
                            (uintptr_t)b.in_pitch) & 3) == 0;
   const bool short_strips = n_images <= kPyrShortMaxImages;
-  // small launches: level 1 over the whole chip, then levels 2 .. nlevels - 1 chained per image
-  // in one launch (pyr_chain_kernel); SLAMGPU_PYR_CHAIN=0 keeps the per-level launches (A/B)
-  static const bool chain_on = [] {
-    const char* e = std::getenv("SLAMGPU_PYR_CHAIN");
-    return !(e && e[0] == '0');
-  }();
-  const int l_end = (short_strips && chain_on && g.nlevels > 2) ? 2 : g.nlevels;
-  for (int l = 1; l < l_end; l++) {
+  for (int l = 1; l < g.nlevels; l++) {
     const int strip = short_strips ? kPyrShortStrip : kPyrStrip;
     const int tiles = ((g.lv[l].w + 255) >> 8) * ((g.lv[l].h + 4 * strip - 1) / (4 * strip));
     const dim3 grid(tiles, n_images);
@@ -2551,9 +2523,6 @@ void launch_extract(const ImageBatch& b, const OrbGeomDev& gd, int n_images, hip
                      b, gd.dev, l, gd.rx, gd.ry);
     }
   }
-  if (l_end < g.nlevels)
-    SLAMGPU_LAUNCH("pyr_down", st, pyr_chain_kernel, dim3(n_images), dim3(64 * kPyrChainWaves), 0,
-                   st, b, gd.dev, l_end, gd.rx, gd.ry);
   {
     const dim3 block(64 * kCellWaves);
     const size_t lds = (size_t)kCellWaves * g.fast_lds_per_wave;

@@ -327,6 +327,7 @@ __global__ __launch_bounds__(64 * W) void pose_opt_kernel(
 #if POSE_PROF  // diagnostic build: thread 0's per-phase wall time (printf at the end)
   double pp[6] = {0, 0, 0, 0, 0, 0};
   uint64_t pt = __builtin_amdgcn_s_memrealtime();
+  const uint64_t pc0 = clock64(), pw0 = pt;
   auto ptick = [&](int k) {
     const uint64_t t = __builtin_amdgcn_s_memrealtime();
     pp[k] += 0.01 * (double)(t - pt);
@@ -523,10 +524,11 @@ __global__ __launch_bounds__(64 * W) void pose_opt_kernel(
     if (n < 10) break;
   }
 #if POSE_PROF
+  const uint64_t pc1 = clock64(), pw1 = __builtin_amdgcn_s_memrealtime();
   if (tid == 0 && f == 0)
     printf("[pose W=%d] us: lin %.1f sum32 %.1f solve+update %.1f trial %.1f sum1 %.1f "
-           "classify %.1f, %d LM iterations\n", W, pp[0], pp[1], pp[5], pp[2], pp[3], pp[4],
-           lm_total);
+           "classify %.1f, %d LM iterations; shader clock %.0f MHz\n", W, pp[0], pp[1], pp[5],
+           pp[2], pp[3], pp[4], lm_total, 100.0 * (double)(pc1 - pc0) / (double)(pw1 - pw0));
 #endif
   // ---- write back: Frame::SetPose(Converter::toCvMat(SE3quat_recov)), mvbOutlier ----
   for (int j = 0; j < nslots; j++) outl_out[tid + j * kThreads] = (outl >> j) & 1;
