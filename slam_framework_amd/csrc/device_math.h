@@ -203,6 +203,35 @@ __device__ __forceinline__ T wave_sum(T v) {
   return v;
 }
 
+// The value of the partner lane in a butterfly whose level M (32, 16, ..., 1) pairs lanes that
+// differ in bit log2(M) and agree above it: lane ^ 32 and lane ^ 16 through the gfx950 permlane
+// swaps, lane ^ 15, ^ 7, ^ 3 (row mirror, half-row mirror, quad reverse) and ^ 1 through DPP --
+// no LDS round trip (ds_bpermute). Each level is an xor with a constant, so levels 32 .. 1
+// together reach all 64 lanes, and a butterfly that adds own + partner leaves every lane of a
+// group with the same bits (IEEE addition commutes).
+__device__ __forceinline__ uint32_t lane_partner_u32(uint32_t v, int M) {
+  const int lane = __lane_id();
+  switch (M) {
+    case 32: {  // lanes 32-63 of the first operand <-> lanes 0-31 of the second
+      const auto r = __builtin_amdgcn_permlane32_swap(v, v, false, false);
+      return (lane & 32) ? r[0] : r[1];
+    }
+    case 16: {  // odd rows of the first operand <-> even rows of the second
+      const auto r = __builtin_amdgcn_permlane16_swap(v, v, false, false);
+      return (lane & 16) ? r[0] : r[1];
+    }
+    case 8: return __builtin_amdgcn_update_dpp(0u, v, 0x140, 0xf, 0xf, false);  // row_mirror
+    case 4: return __builtin_amdgcn_update_dpp(0u, v, 0x141, 0xf, 0xf, false);  // row_half_mirror
+    case 2: return __builtin_amdgcn_update_dpp(0u, v, 0x1b, 0xf, 0xf, false);   // quad [3,2,1,0]
+    default: return __builtin_amdgcn_update_dpp(0u, v, 0xb1, 0xf, 0xf, false);  // quad [1,0,3,2]
+  }
+}
+__device__ __forceinline__ double lane_partner(double v, int M) {
+  const uint64_t b = __builtin_bit_cast(uint64_t, v);
+  const uint64_t lo = lane_partner_u32((uint32_t)b, M), hi = lane_partner_u32((uint32_t)(b >> 32), M);
+  return __builtin_bit_cast(double, hi << 32 | lo);
+}
+
 // Number of set bits of `mask` strictly below this lane.
 __device__ __forceinline__ int lanes_below(uint64_t mask) {
   return __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32),

@@ -18,9 +18,13 @@
 //                    H (upper triangle), b and the robust chi2 in one sweep (computeActiveErrors,
 //                    activeRobustChi2 and buildSystem all evaluate at the same estimate);
 //   trial pass     : error, chi2 and robust chi2 at exp(dx) * T.
-// The sums are reductions (reduce-scatter across the wave, wave partials through LDS), after
-// which every lane of every wave holds bitwise-identical totals and runs the LM control (6x6
-// LDLT, exp, lambda update) itself with uniform branches: no broadcast, no single-lane section.
+// The sums are reductions (reduce-scatter across the wave through permlane / DPP exchanges, wave
+// partials through LDS), after which every lane of every wave holds bitwise-identical totals.
+// A one-wave frame runs the LM control (6x6 LDLT, exp, lambda update) in every lane with uniform
+// branches; the latency variant lets wave 0 alone solve and broadcasts the step through LDS (all
+// eight waves solving measured 0.527 ms per frame against 0.452, profiles/r4i_pose_*). The
+// latency variant's solve is a dependent chain of ~800 FP64 instructions (~5 us per LM trial):
+// one reciprocal per pivot, the exp map's Taylor coefficients for small steps, contraction.
 //
 // FP64 throughout, with the reference's f32 quirks: f32 inputs and outputs (Converter), float
 // inverse depth in the stereo projection (types_six_dof_expmap.cpp:299-306), f32 Huber deltas and
@@ -42,7 +46,6 @@ using se3::SE3;
 using se3::normalize_rotation;
 using se3::quat_from_R;
 using se3::quat_to_R;
-using se3::se3_left_update;
 
 constexpr int kNH = 21;  // upper triangle of the 6x6 H
 // Batches smaller than this run 8 waves per frame (latency); larger ones one wave per frame.
@@ -51,22 +54,26 @@ constexpr int kPoseLdsEdges = 4096;  // edges of one frame the 1- and 8-wave var
 
 // H x = b for the 6x6 H + lambda I, LDLT without pivoting; a zero pivot gives a zero component
 // (Eigen's rule), a negative one fails the solve (LinearSolverDense::solve returns false and
-// g2o applies the previous x).
+// g2o applies the previous x). One reciprocal per pivot, and the unscaled column entries
+// (L_ik d_k) kept for the later columns' sums: six divisions on the wave's dependent chain, not
+// twenty-seven.
 __device__ bool ldlt_solve6(const double H[kNH], double lambda, const double b[6], double x[6]) {
-  double L[6][6], d[6];
+#pragma clang fp contract(fast)  // tolerance-compared: the column sums fuse
+  double L[6][6], D[6][6], id[6];  // D[i][k] = L[i][k] d[k]
 #pragma unroll
   for (int j = 0; j < 6; j++) {
     double dj = H[j * 6 - (j * (j - 1)) / 2] + lambda;  // H(j, j) in the packed upper triangle
 #pragma unroll
-    for (int k = 0; k < j; k++) dj -= L[j][k] * L[j][k] * d[k];
-    d[j] = dj;
+    for (int k = 0; k < j; k++) dj -= L[j][k] * D[j][k];
     if (dj < 0) return false;
+    id[j] = dj > DBL_MIN ? 1.0 / dj : 0.0;
 #pragma unroll
     for (int i = j + 1; i < 6; i++) {
       double s = H[j * 6 - (j * (j - 1)) / 2 + (i - j)];  // H(j, i) = H(i, j)
 #pragma unroll
-      for (int k = 0; k < j; k++) s -= L[i][k] * L[j][k] * d[k];
-      L[i][j] = dj > DBL_MIN ? s / dj : 0.0;
+      for (int k = 0; k < j; k++) s -= L[i][k] * D[j][k];
+      D[i][j] = s;
+      L[i][j] = s * id[j];
     }
   }
   double y[6];
@@ -78,7 +85,7 @@ __device__ bool ldlt_solve6(const double H[kNH], double lambda, const double b[6
     y[i] = s;
   }
 #pragma unroll
-  for (int i = 0; i < 6; i++) y[i] = fabs(d[i]) > DBL_MIN ? y[i] / d[i] : 0.0;
+  for (int i = 0; i < 6; i++) y[i] *= id[i];
 #pragma unroll
   for (int i = 5; i >= 0; i--) {
     double s = y[i];
@@ -89,6 +96,83 @@ __device__ bool ldlt_solve6(const double H[kNH], double lambda, const double b[6
   return true;
 }
 
+// exp(dx) * T as se3::se3_left_update (SE3Quat::exp, se3quat.h:223-257), shortened for the
+// wave's dependent chain: for 1e-5 <= theta < 1e-2 (LM steps of a tracked frame) the
+// coefficients sin t / t, (1 - cos t) / t^2, (t - sin t) / t^3 come from their Taylor series
+// (truncation below 1e-20 relative) instead of sincos and three divisions; the two
+// normalisations take one reciprocal square root each. g2o's theta < 1e-5 branch (R = V = I + O
+// + O^2) is kept as it is.
+__device__ __forceinline__ void pose_normalize(Quat& q) {
+  if (q.w < 0) {
+    q.x = -q.x;
+    q.y = -q.y;
+    q.z = -q.z;
+    q.w = -q.w;
+  }
+  const double in = 1.0 / sqrt(q.x * q.x + q.y * q.y + q.z * q.z + q.w * q.w);
+  q.x *= in;
+  q.y *= in;
+  q.z *= in;
+  q.w *= in;
+}
+__device__ __forceinline__ SE3 pose_left_update(const double u[6], const SE3& T) {
+#pragma clang fp contract(fast)
+  const double w0 = u[0], w1 = u[1], w2 = u[2];
+  const double t2 = w0 * w0 + w1 * w1 + w2 * w2;
+  const double th = sqrt(t2);
+  const double O[9] = {0, -w2, w1, w2, 0, -w0, -w1, w0, 0};
+  double O2[9];
+#pragma unroll
+  for (int i = 0; i < 3; i++)
+#pragma unroll
+    for (int j = 0; j < 3; j++)
+      O2[3 * i + j] = O[3 * i] * O[j] + O[3 * i + 1] * O[3 + j] + O[3 * i + 2] * O[6 + j];
+  double a = 1.0, b = 1.0, c = 1.0;
+  if (!(th < 0.00001)) {
+    if (th < 0.01) {
+      // Horner in t^2 with constant reciprocals (multiplications, not divisions)
+      constexpr double k6 = 1.0 / 6, k12 = 1.0 / 12, k20 = 1.0 / 20, k30 = 1.0 / 30;
+      constexpr double k42 = 1.0 / 42, k56 = 1.0 / 56, k72 = 1.0 / 72, k90 = 1.0 / 90;
+      constexpr double k110 = 1.0 / 110;
+      a = 1.0 - t2 * k6 * (1.0 - t2 * k20 * (1.0 - t2 * k42 * (1.0 - t2 * k72)));
+      b = 0.5 * (1.0 - t2 * k12 * (1.0 - t2 * k30 * (1.0 - t2 * k56 * (1.0 - t2 * k90))));
+      c = k6 * (1.0 - t2 * k20 * (1.0 - t2 * k42 * (1.0 - t2 * k72 * (1.0 - t2 * k110))));
+    } else {
+      double s, co;
+      sincos(th, &s, &co);
+      const double it = 1.0 / th;
+      a = s * it;
+      b = (1 - co) * it * it;
+      c = (th - s) * it * it * it;
+    }
+  }
+  double R[9], V[9];
+#pragma unroll
+  for (int i = 0; i < 9; i++) {
+    const double I = (i % 4 == 0) ? 1.0 : 0.0;
+    R[i] = I + a * O[i] + b * O2[i];
+    V[i] = I + b * O[i] + c * O2[i];
+  }
+  SE3 E;
+#pragma unroll
+  for (int i = 0; i < 3; i++) E.t[i] = V[3 * i] * u[3] + V[3 * i + 1] * u[4] + V[3 * i + 2] * u[5];
+  E.r = quat_from_R(R);
+  pose_normalize(E.r);
+  SE3 out;  // E * T
+  double rt[3];
+  se3::quat_rotate(E.r, T.t, rt);
+#pragma unroll
+  for (int i = 0; i < 3; i++) out.t[i] = E.t[i] + rt[i];
+  const Quat& p = E.r;
+  const Quat& q = T.r;
+  out.r.w = p.w * q.w - p.x * q.x - p.y * q.y - p.z * q.z;
+  out.r.x = p.w * q.x + p.x * q.w + p.y * q.z - p.z * q.y;
+  out.r.y = p.w * q.y + p.y * q.w + p.z * q.x - p.x * q.z;
+  out.r.z = p.w * q.z + p.z * q.w + p.x * q.y - p.y * q.x;
+  pose_normalize(out.r);
+  return out;
+}
+
 // RobustKernelHuber::robustify (robust_kernel_impl.cpp:78-91): rho(e) and rho'(e). The sqrt and
 // division run only for lanes past the kernel's corner (a skipped branch for inlier waves).
 __device__ __forceinline__ double huber_rho0(double e, double delta) {
@@ -96,6 +180,12 @@ __device__ __forceinline__ double huber_rho0(double e, double delta) {
   const double d2 = delta * delta;
   if (e > d2) r = 2 * sqrt(e) * delta - d2;
   return r;
+}
+// huber_rho0 without the branch (the latency variant's paired trial pass)
+__device__ __forceinline__ double huber_rho0_sel(double e, double delta) {
+  const double d2 = delta * delta;
+  const double r = 2 * sqrt(e) * delta - d2;
+  return e > d2 ? r : e;
 }
 __device__ __forceinline__ void huber_rho01(double e, double delta, double& r0, double& r1) {
   r0 = e;
@@ -174,7 +264,8 @@ __device__ __forceinline__ double eval_edge(const slamgpu_pose_edge& E, const Po
 
 // ---- reductions -------------------------------------------------------------------------------
 // Sum 32 per-lane doubles over the wave: after 5 halving exchanges lane l holds the sum of value
-// l >> 1 over 32 lanes; the last exchange (xor 1) completes it over all 64.
+// l >> 1 over 32 lanes; the last exchange completes it over all 64. The exchanges are
+// lane_partner's permlane / DPP levels (pairs differ in bit log2(m)), not LDS permutes.
 __device__ __forceinline__ double wave_reduce_scatter32(double v[32]) {
   const int lane = threadIdx.x & 63;
 #pragma unroll
@@ -189,17 +280,17 @@ __device__ __forceinline__ double wave_reduce_scatter32(double v[32]) {
       const uint64_t hi = __builtin_bit_cast(uint64_t, v[i + h]);
       const double send = __builtin_bit_cast(double, (lo & up) | (hi & ~up));
       const double keep = __builtin_bit_cast(double, (hi & up) | (lo & ~up));
-      v[i] = keep + __shfl_xor(send, m);
+      v[i] = keep + lane_partner(send, m);
     }
   }
-  return v[0] + __shfl_xor(v[0], 1);
+  return v[0] + lane_partner(v[0], 1);
 }
 
-// xor butterfly: every lane ends with the same bits (each level adds a + b on one side and b + a
-// on the other, and IEEE addition commutes).
+// butterfly: every lane ends with the same bits (each level adds a + b on one side and b + a on
+// the other, and IEEE addition commutes).
 __device__ __forceinline__ double wave_sum(double v) {
 #pragma unroll
-  for (int m = 32; m >= 1; m >>= 1) v += __shfl_xor(v, m);
+  for (int m = 32; m >= 1; m >>= 1) v += lane_partner(v, m);
   return v;
 }
 
@@ -253,6 +344,49 @@ struct FrameSum {
   }
 };
 
+// One edge's share of the linearisation (computeError + linearizeOplus + buildSystem): the
+// robust chi2, b -= rho' J' Omega e and H += J' (rho' Omega) J into acc (H upper triangle, b,
+// chi2).
+__device__ __forceinline__ void lin_accumulate(const EdgeEval& ev, double wgt, double r0,
+                                               const PoseParams& P, double (&acc)[32]) {
+#pragma clang fp contract(fast)
+  acc[27] += r0;
+  // Jacobian of the error wrt [omega, upsilon] (types_six_dof_expmap.cpp:266-288, 311-364)
+  const double iz = ev.iz, iz2 = iz * iz, x = ev.x, y = ev.y;
+  const double fx = P.fx, fy = P.fy, bf = P.bf;
+  double J[3][6];
+  J[0][0] = x * y * iz2 * fx;
+  J[0][1] = -(1 + (x * x * iz2)) * fx;
+  J[0][2] = y * iz * fx;
+  J[0][3] = -iz * fx;
+  J[0][4] = 0;
+  J[0][5] = x * iz2 * fx;
+  J[1][0] = (1 + y * y * iz2) * fy;
+  J[1][1] = -x * y * iz2 * fy;
+  J[1][2] = -x * iz * fy;
+  J[1][3] = 0;
+  J[1][4] = -iz * fy;
+  J[1][5] = y * iz2 * fy;
+  const double sm = ev.stereo ? 1.0 : 0.0;  // the third row only for stereo edges
+  J[2][0] = sm * (J[0][0] - bf * y * iz2);
+  J[2][1] = sm * (J[0][1] + bf * x * iz2);
+  J[2][2] = sm * J[0][2];
+  J[2][3] = sm * J[0][3];
+  J[2][4] = 0;
+  J[2][5] = sm * (J[0][5] - bf * iz2);
+  // b -= rho' J' Omega e ; H += J' (rho' Omega) J  (base_unary_edge.hpp:43-71)
+  const double wi = wgt * ev.info;
+  int h = 0;
+#pragma unroll
+  for (int a = 0; a < 6; a++) {
+    const double ja0 = J[0][a] * ev.info, ja1 = J[1][a] * ev.info, ja2 = J[2][a] * ev.info;
+    acc[kNH + a] -= wgt * (ja0 * ev.e[0] + ja1 * ev.e[1] + ja2 * ev.e[2]);
+    const double wa0 = J[0][a] * wi, wa1 = J[1][a] * wi, wa2 = J[2][a] * wi;
+#pragma unroll
+    for (int c = a; c < 6; c++, h++) acc[h] += wa0 * J[0][c] + wa1 * J[1][c] + wa2 * J[2][c];
+  }
+}
+
 // Optimizer::PoseOptimization for frame blockIdx.x with W waves. Edge k is slot k / (64 W) of
 // thread k % (64 W); per slot a thread keeps two bits: the edge is an outlier (level 1,
 // inactive), and the f32 test chi2 > threshold of the edge's last computed chi2 -- the only use
@@ -279,6 +413,7 @@ __global__ __launch_bounds__(64 * W) void pose_opt_kernel(
   // the latency variant (one frame per work-group of W waves) keeps the frame's edges in LDS
   // (4096 x 28 B): the passes then wait on LDS, not on L2, for each edge slot
   constexpr bool kLdsEdges = W > 1 && kMaxE <= kPoseLdsEdges;
+  constexpr bool kPairSlots = kLdsEdges;  // the latency variant pairs its trial slots
   __shared__ uint32_t s_edges[kLdsEdges ? kMaxE * 7 : 1];
   const int f = blockIdx.x, tid = threadIdx.x;
   const int e0 = edge_start[f];
@@ -373,41 +508,7 @@ __global__ __launch_bounds__(64 * W) void pose_opt_kernel(
         const double delta = ev.stereo ? delta_stereo : delta_mono;
         double wgt = 1.0, r0 = c2;
         if (robust) huber_rho01(c2, delta, r0, wgt);
-        acc[27] += r0;
-        // Jacobian of the error wrt [omega, upsilon] (types_six_dof_expmap.cpp:266-288, 311-364)
-        const double iz = ev.iz, iz2 = iz * iz, x = ev.x, y = ev.y;
-        const double fx = P.fx, fy = P.fy, bf = P.bf;
-        double J[3][6];
-        J[0][0] = x * y * iz2 * fx;
-        J[0][1] = -(1 + (x * x * iz2)) * fx;
-        J[0][2] = y * iz * fx;
-        J[0][3] = -iz * fx;
-        J[0][4] = 0;
-        J[0][5] = x * iz2 * fx;
-        J[1][0] = (1 + y * y * iz2) * fy;
-        J[1][1] = -x * y * iz2 * fy;
-        J[1][2] = -x * iz * fy;
-        J[1][3] = 0;
-        J[1][4] = -iz * fy;
-        J[1][5] = y * iz2 * fy;
-        const double sm = ev.stereo ? 1.0 : 0.0;  // the third row only for stereo edges
-        J[2][0] = sm * (J[0][0] - bf * y * iz2);
-        J[2][1] = sm * (J[0][1] + bf * x * iz2);
-        J[2][2] = sm * J[0][2];
-        J[2][3] = sm * J[0][3];
-        J[2][4] = 0;
-        J[2][5] = sm * (J[0][5] - bf * iz2);
-        // b -= rho' J' Omega e ; H += J' (rho' Omega) J  (base_unary_edge.hpp:43-71)
-        const double wi = wgt * ev.info;
-        int h = 0;
-#pragma unroll
-        for (int a = 0; a < 6; a++) {
-          const double ja0 = J[0][a] * ev.info, ja1 = J[1][a] * ev.info, ja2 = J[2][a] * ev.info;
-          acc[kNH + a] -= wgt * (ja0 * ev.e[0] + ja1 * ev.e[1] + ja2 * ev.e[2]);
-          const double wa0 = J[0][a] * wi, wa1 = J[1][a] * wi, wa2 = J[2][a] * wi;
-#pragma unroll
-          for (int c = a; c < 6; c++, h++) acc[h] += wa0 * J[0][c] + wa1 * J[1][c] + wa2 * J[2][c];
-        }
+        lin_accumulate(ev, wgt, r0, P, acc);
       }
       ptick(0);
       const double* S = fs.sum32(acc);
@@ -431,11 +532,11 @@ __global__ __launch_bounds__(64 * W) void pose_opt_kernel(
         bool ok;
         if constexpr (W == 1) {
           ok = ldlt_solve6(H, lambda, b, x);
-          T = se3_left_update(x, backup);
+          T = pose_left_update(x, backup);
         } else {  // wave 0 alone (its SIMD undisturbed), then a broadcast through LDS
           if (wave_id() == 0) {
             ok = ldlt_solve6(H, lambda, b, x);
-            T = se3_left_update(x, backup);
+            T = pose_left_update(x, backup);
             if ((tid & 63) == 0) {
 #pragma unroll
               for (int j = 0; j < 6; j++) fs.bc[j] = x[j];
@@ -465,17 +566,40 @@ __global__ __launch_bounds__(64 * W) void pose_opt_kernel(
         // ---- trial: computeActiveErrors + activeRobustChi2 at the new estimate ----
         double part = 0.0;
         const PassPose TP = pass_pose(T);
-        slamgpu_pose_edge en{};
-        if (!kLdsEdges && nslots > 0) en = edge(tid);
-        for (int j = 0; j < nslots; j++) {
-          const slamgpu_pose_edge ec = kLdsEdges ? edge(tid + j * kThreads) : en;
-          if (!kLdsEdges && j + 1 < nslots) en = edge(tid + (j + 1) * kThreads);
-          if ((outl >> j) & 1) continue;
-          EdgeEval ev;
-          const double c2 = eval_edge(ec, P, isig, TP, ev);
-          const uint64_t bit = 1ull << j;
-          lastbad = ((float)c2 > (ev.stereo ? 7.815f : 5.991f)) ? (lastbad | bit) : (lastbad & ~bit);
-          part += robust ? huber_rho0(c2, ev.stereo ? delta_stereo : delta_mono) : c2;
+        if constexpr (kPairSlots) {
+          // two slots per step, branch-free (an outlier's error is computed and discarded by
+          // selects), so the two edges' dependent chains interleave; same order of additions
+          for (int j = 0; j < nslots; j += 2) {
+            const bool has1 = j + 1 < nslots;
+            const slamgpu_pose_edge e0 = edge(tid + j * kThreads);
+            const slamgpu_pose_edge e1 = edge(has1 ? tid + (j + 1) * kThreads : tid + j * kThreads);
+            EdgeEval v0, v1;
+            const double c0 = eval_edge(e0, P, isig, TP, v0);
+            const double c1 = eval_edge(e1, P, isig, TP, v1);
+            const bool a0 = !((outl >> j) & 1), a1 = has1 && !((outl >> (j + 1)) & 1);
+            const uint64_t b0 = 1ull << j, b1 = has1 ? 1ull << (j + 1) : 0ull;
+            if (a0)
+              lastbad = ((float)c0 > (v0.stereo ? 7.815f : 5.991f)) ? (lastbad | b0) : (lastbad & ~b0);
+            if (a1)
+              lastbad = ((float)c1 > (v1.stereo ? 7.815f : 5.991f)) ? (lastbad | b1) : (lastbad & ~b1);
+            const double r0 = robust ? huber_rho0_sel(c0, v0.stereo ? delta_stereo : delta_mono) : c0;
+            const double r1 = robust ? huber_rho0_sel(c1, v1.stereo ? delta_stereo : delta_mono) : c1;
+            part += a0 ? r0 : 0.0;
+            part += a1 ? r1 : 0.0;
+          }
+        } else {
+          slamgpu_pose_edge en{};
+          if (!kLdsEdges && nslots > 0) en = edge(tid);
+          for (int j = 0; j < nslots; j++) {
+            const slamgpu_pose_edge ec = kLdsEdges ? edge(tid + j * kThreads) : en;
+            if (!kLdsEdges && j + 1 < nslots) en = edge(tid + (j + 1) * kThreads);
+            if ((outl >> j) & 1) continue;
+            EdgeEval ev;
+            const double c2 = eval_edge(ec, P, isig, TP, ev);
+            const uint64_t bit = 1ull << j;
+            lastbad = ((float)c2 > (ev.stereo ? 7.815f : 5.991f)) ? (lastbad | bit) : (lastbad & ~bit);
+            part += robust ? huber_rho0(c2, ev.stereo ? delta_stereo : delta_mono) : c2;
+          }
         }
         ptick(2);
         double tempChi = fs.sum1(part);
