@@ -246,16 +246,18 @@ int compute_geometry(const OrbParams& p, int cols, int rows, OrbGeom* g,
     }
     g->oct_lds_bytes = off + 4 * kcap;
   }
-  {  // octree_lvl_kernel LDS (80 KB: two work-groups per CU)
-    constexpr int kLdsBudget = 80 * 1024, kNodeBytes = 12, kWorkBytesPerNode = 4 + 4 * 2 + 1;
+  {  // octree_lvl_kernel LDS (one work-group per CU: the small launches have <= 128 of them)
+    // per node: sort key, pt / pe / pu / vnext, processed + candidate flags, the two scan
+    // prefixes, the first child's push index (+16 B alignment)
+    constexpr int kLdsBudget = 144 * 1024, kNodeBytes = 12, kWorkBytesPerNode = 4 + 4 * 2 + 2 + 16 + 2;
     int nc = 64, ccap = 0;
     for (int l = 0; l < p.nlevels; l++) {
       nc = std::max(nc, g->lv[l].oct_nc);
       ccap = std::max(ccap, g->lv[l].ncols * g->lv[l].nrows + 1);
     }
     ccap = round_up(ccap, 4);
-    const int fixed = ccap * 4 + 2 * nc * kNodeBytes + round_up(nc * kWorkBytesPerNode, 16);
-    const int kcap = std::min((kLdsBudget - fixed) / 8 / 4 * 4, 65535);
+    const int fixed = ccap * 4 + 2 * nc * kNodeBytes + round_up(nc * kWorkBytesPerNode + 16, 16);
+    const int kcap = std::min((kLdsBudget - fixed) / 8 / 4 * 4, 8192);
     if (kcap < 1024) return -7;
     g->oct2_kcap = kcap;
     g->oct2_ccap = ccap;
@@ -264,7 +266,7 @@ int compute_geometry(const OrbParams& p, int cols, int rows, OrbGeom* g,
     g->oct2_cpre_off = 8 * kcap;
     g->oct2_list_off = g->oct2_cpre_off + 4 * ccap;
     g->oct2_work_off = g->oct2_list_off + 2 * nc * kNodeBytes;
-    g->oct2_lds_bytes = g->oct2_work_off + round_up(nc * kWorkBytesPerNode, 16);
+    g->oct2_lds_bytes = g->oct2_work_off + round_up(nc * kWorkBytesPerNode + 16, 16);
   }
   g->out_per_image = out_off;
   g->kp_cap = out_off;

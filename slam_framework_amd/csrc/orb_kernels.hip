@@ -651,12 +651,13 @@ struct OctShared {
   int a[kOctCap];
   int b[kOctCap];
   int c[kOctCap];
-  int wsum[kOctWaves];
+  int wsum[16];  // per-wave totals (up to 16 waves)
   int bucket[64 + 1];
   int m, seq_next, mode, nexp, finish, ktotal, total;
 };
 
-// Block-wide exclusive scan of v (one value per thread); returns prefix, *total gets the sum.
+// Block-wide exclusive scan of v (one value per thread of kThr); returns prefix, *total the sum.
+template <int kThr>
 __device__ __forceinline__ int block_scan(int v, int* wsum, int* total) {
   const int lane = threadIdx.x & 63, wid = wave_id();
   int x = v;
@@ -669,7 +670,7 @@ __device__ __forceinline__ int block_scan(int v, int* wsum, int* total) {
   __syncthreads();
   int pre = 0, tot = 0;
 #pragma unroll
-  for (int w = 0; w < kOctWaves; w++) {
+  for (int w = 0; w < kThr / 64; w++) {
     const int s = wsum[w];
     pre += (w < wid) ? s : 0;
     tot += s;
@@ -679,9 +680,10 @@ __device__ __forceinline__ int block_scan(int v, int* wsum, int* total) {
   return pre + x - v;
 }
 
-// Exclusive scan of arr[0..n) in place (n <= kOctCap); returns the total.
+// Exclusive scan of arr[0..n) in place (n <= kOctCap) by kThr threads; returns the total.
+template <int kThr>
 __device__ int block_scan_array(int* arr, int n, int* wsum) {
-  constexpr int per = kOctCap / kOctThreads;
+  constexpr int per = kOctCap / kThr;
   const int base = threadIdx.x * per;
   int loc[per];
   int s = 0;
@@ -691,7 +693,7 @@ __device__ int block_scan_array(int* arr, int n, int* wsum) {
     s += loc[i];
   }
   int total;
-  int pre = block_scan(s, wsum, &total);
+  int pre = block_scan<kThr>(s, wsum, &total);
 #pragma unroll
   for (int i = 0; i < per; i++) {
     if (base + i < n) arr[base + i] = pre;
@@ -759,6 +761,7 @@ __device__ void divide_wave(const OctNode& nd, uint32_t* const keys[2], OctNode 
 
 // The global-memory DistributeOctTree of one (level, image) by a 256-thread work-group, for the
 // levels the LDS kernels cannot hold (their oct_count entry is -1). S: LDS scratch.
+template <int kThr>
 __device__ __forceinline__ void octree_global(
     OctShared& S, int level, int img, const OrbGeom* __restrict__ g,
     const uint32_t* __restrict__ cell_keys, const int* __restrict__ cell_count,
@@ -782,12 +785,12 @@ __device__ __forceinline__ void octree_global(
   // ---- 1. gather FAST candidates in cell row-major order into keys[0]
   for (int c0 = 0; c0 < ncell; c0 += kOctCap) {
     const int n = min(kOctCap, ncell - c0);
-    for (int i = tid; i < n; i += kOctThreads) S.a[i] = cell_count[cbase + c0 + i];
+    for (int i = tid; i < n; i += kThr) S.a[i] = cell_count[cbase + c0 + i];
     __syncthreads();
     if (tid == 0) S.total = 0;
-    const int tot = block_scan_array(S.a, n, S.wsum);
+    const int tot = block_scan_array<kThr>(S.a, n, S.wsum);
     const int base = (c0 == 0) ? 0 : S.ktotal;
-    for (int i = wid; i < n; i += kOctWaves) {
+    for (int i = wid; i < n; i += (kThr / 64)) {
       const int cnt = cell_count[cbase + c0 + i];
       const int off = base + S.a[i];
       const uint32_t* src = cell_keys + (cbase + c0 + i) * g->cell_cap;
@@ -889,7 +892,7 @@ __device__ __forceinline__ void octree_global(
     OctNode* const Ln = lists[cur ^ 1];
     if (S.mode == 0) {
       // outer pass: divide every node with > 1 key, in list order
-      for (int j = wid; j < m; j += kOctWaves) {
+      for (int j = wid; j < m; j += (kThr / 64)) {
         const OctNode nd = Lc[j];
         int t = 0, e = 0;
         if (nd.n > 1) {
@@ -909,14 +912,14 @@ __device__ __forceinline__ void octree_global(
         }
       }
       __syncthreads();
-      const int T = block_scan_array(S.a, m, S.wsum);
-      const int U = block_scan_array(S.b, m, S.wsum);
-      const int E = block_scan_array(S.c, m, S.wsum);
+      const int T = block_scan_array<kThr>(S.a, m, S.wsum);
+      const int U = block_scan_array<kThr>(S.b, m, S.wsum);
+      const int E = block_scan_array<kThr>(S.c, m, S.wsum);
       const int newm = T + U;
       const int seq0 = S.seq_next;
       const bool ovf = newm > min(2 * L.node_cap, kOctCap) || E > kOctCap;
       if (!ovf) {
-        for (int j = tid; j < m; j += kOctThreads) {
+        for (int j = tid; j < m; j += kThr) {
           const OctNode nd = Lc[j];
           if (nd.n > 1) {
             int gpos = S.a[j], epos = S.c[j];
@@ -955,7 +958,7 @@ __device__ __forceinline__ void octree_global(
       const int V = S.nexp;
       int P2 = 1;
       while (P2 < V) P2 <<= 1;
-      for (int i = tid; i < P2; i += kOctThreads) {
+      for (int i = tid; i < P2; i += kThr) {
         uint64_t key = 0;  // pads sort to the end (descending)
         if (i < V) {
           const int pos = (int)S.sortk[i];
@@ -968,7 +971,7 @@ __device__ __forceinline__ void octree_global(
       // bitonic sort, descending by (n, seq): reference processes sort() ascending from the end
       for (int k = 2; k <= P2; k <<= 1) {
         for (int jj = k >> 1; jj > 0; jj >>= 1) {
-          for (int i = tid; i < P2; i += kOctThreads) {
+          for (int i = tid; i < P2; i += kThr) {
             const int ixj = i ^ jj;
             if (ixj > i) {
               const uint64_t x = S.sortk[i], y = S.sortk[ixj];
@@ -983,7 +986,7 @@ __device__ __forceinline__ void octree_global(
         }
       }
       // speculative division of every vPrev node in processing order
-      for (int j = wid; j < V; j += kOctWaves) {
+      for (int j = wid; j < V; j += (kThr / 64)) {
         const int pos = (int)(S.sortk[j] & 0xfff);
         const OctNode nd = Lc[pos];
         OctNode ch[4];
@@ -1002,43 +1005,43 @@ __device__ __forceinline__ void octree_global(
       }
       __syncthreads();
       // cut: first j with m + sum_{i<=j}(t_i - 1) >= N
-      for (int i = tid; i < V; i += kOctThreads) S.b[i] = S.a[i] - 1;
+      for (int i = tid; i < V; i += kThr) S.b[i] = S.a[i] - 1;
       __syncthreads();
-      block_scan_array(S.b, V, S.wsum);  // exclusive prefix of (t - 1)
+      block_scan_array<kThr>(S.b, V, S.wsum);  // exclusive prefix of (t - 1)
       if (tid == 0) S.total = V - 1;
       __syncthreads();
-      for (int j = tid; j < V; j += kOctThreads)
+      for (int j = tid; j < V; j += kThr)
         if (m + S.b[j] + (S.a[j] - 1) >= N) atomicMin(&S.total, j);
       __syncthreads();
       const int J = S.total;  // last processed index
       const int nproc = J + 1;
-      for (int i = tid; i < V; i += kOctThreads)
+      for (int i = tid; i < V; i += kThr)
         if (i >= nproc) {
           S.a[i] = 0;
           S.c[i] = 0;
         }
       __syncthreads();
-      const int T = block_scan_array(S.a, V, S.wsum);  // push-order child positions
-      const int E = block_scan_array(S.c, V, S.wsum);
+      const int T = block_scan_array<kThr>(S.a, V, S.wsum);  // push-order child positions
+      const int E = block_scan_array<kThr>(S.c, V, S.wsum);
       // survivors: old list minus processed nodes
-      for (int i = tid; i < m; i += kOctThreads) S.b[i] = 1;
+      for (int i = tid; i < m; i += kThr) S.b[i] = 1;
       __syncthreads();
-      for (int j = tid; j < nproc; j += kOctThreads) S.b[(int)(S.sortk[j] & 0xfff)] = 0;
+      for (int j = tid; j < nproc; j += kThr) S.b[(int)(S.sortk[j] & 0xfff)] = 0;
       __syncthreads();
-      const int U = block_scan_array(S.b, m, S.wsum);
+      const int U = block_scan_array<kThr>(S.b, m, S.wsum);
       // block_scan_array overwrote the flags with prefixes; recover flags from processed set
       const int newm = T + U;
       const int seq0 = S.seq_next;
       const bool ovf = newm > min(2 * L.node_cap, kOctCap) || E > kOctCap;
       __shared__ uint8_t processed[kOctCap];
-      for (int i = tid; i < m; i += kOctThreads) processed[i] = 0;
+      for (int i = tid; i < m; i += kThr) processed[i] = 0;
       __syncthreads();
-      for (int j = tid; j < nproc; j += kOctThreads) processed[(int)(S.sortk[j] & 0xfff)] = 1;
+      for (int j = tid; j < nproc; j += kThr) processed[(int)(S.sortk[j] & 0xfff)] = 1;
       __syncthreads();
       // new vSize goes to a temporary (S.c keeps E prefixes): reuse child area tail? keep in LDS
       __shared__ int vnext[kOctCap];
       if (!ovf) {
-        for (int j = tid; j < nproc; j += kOctThreads) {
+        for (int j = tid; j < nproc; j += kThr) {
           int gpos = S.a[j], epos = S.c[j];
           for (int q = 0; q < 4; q++) {
             OctNode ch = child[4 * j + q];
@@ -1050,11 +1053,11 @@ __device__ __forceinline__ void octree_global(
             gpos++;
           }
         }
-        for (int i = tid; i < m; i += kOctThreads)
+        for (int i = tid; i < m; i += kThr)
           if (!processed[i]) Ln[T + S.b[i]] = Lc[i];
       }
       __syncthreads();
-      for (int i = tid; i < E; i += kOctThreads) S.sortk[i] = (uint64_t)vnext[i];
+      for (int i = tid; i < E; i += kThr) S.sortk[i] = (uint64_t)vnext[i];
       __syncthreads();
       if (tid == 0) {
         if (ovf) {
@@ -1076,7 +1079,7 @@ __device__ __forceinline__ void octree_global(
   const int m = S.m;
   const OctNode* Lf = lists[cur];
   const int mout = min(m, L.out_cap);
-  for (int j = tid; j < mout; j += kOctThreads) {
+  for (int j = tid; j < mout; j += kThr) {
     const OctNode nd = Lf[j];
     const uint32_t* ks = keys[nd.buf] + nd.kbeg;
     uint32_t best = ks[0];
@@ -1098,8 +1101,8 @@ __global__ __launch_bounds__(kOctThreads) void octree_kernel(
     OctNode* __restrict__ node_scratch, uint32_t* __restrict__ oct_keys,
     int* __restrict__ oct_count, uint32_t* __restrict__ err) {
   __shared__ OctShared S;
-  octree_global(S, blockIdx.x, blockIdx.y, g, cell_keys, cell_count, key_scratch, node_scratch,
-                oct_keys, oct_count, err);
+  octree_global<kOctThreads>(S, blockIdx.x, blockIdx.y, g, cell_keys, cell_count, key_scratch,
+                             node_scratch, oct_keys, oct_count, err);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -1652,7 +1655,11 @@ __global__ __launch_bounds__(64 * kMaxLevels) void octree_img_kernel(
 // 120 us, profiles/r3f_lat_octprof.log); here the gather's loads, the vPrev sort, the per-node
 // divides and the big nodes' partitions are spread over the waves. Same list semantics and
 // output bytes; a level that does not fit its LDS falls back to octree_kernel as before.
-constexpr int kOctLvlWaves = 4, kOctLvlThreads = 64 * kOctLvlWaves;
+constexpr int kOctLvlWaves = 8, kOctLvlThreads = 64 * kOctLvlWaves;
+constexpr int kOctKpt = 16;  // key positions per thread of the passes: levels up to 8192 keys
+#ifndef OCT_PROF
+#define OCT_PROF 0
+#endif
 #ifndef OCT_LVL_MAX_IMAGES
 #define OCT_LVL_MAX_IMAGES 16
 #endif
@@ -1703,6 +1710,7 @@ __global__ __launch_bounds__(kOctLvlThreads) void octree_lvl_kernel(
   __shared__ int s_brun[16];              // next free slot of each initial bucket
   __shared__ int s_bcnt[16];              // keys per initial bucket
   __shared__ int s_u[4];                  // T, E, U of a pass; nproc
+  __shared__ int s_scan[kOctLvlWaves][2];  // per-wave totals of the key scan
   const int level = blockIdx.x, img = blockIdx.y;
   const int tid = threadIdx.x, lane = tid & 63, w = wave_id();
   const int nlev = g->nlevels;
@@ -1710,6 +1718,19 @@ __global__ __launch_bounds__(kOctLvlThreads) void octree_lvl_kernel(
   const int ncell = L.ncols * L.nrows;
   const int64_t cbase = (int64_t)img * g->cells_per_image + L.cell_base;
   int* const outc = oct_count + img * nlev + level;
+#if OCT_PROF  // diagnostic build: per-phase wall time of (image 0, levels 0 and 7), printf at the end
+  uint64_t op_t = __builtin_amdgcn_s_memrealtime();
+  const uint64_t op_t0 = op_t;
+  uint32_t op_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  int op_pass = 0;
+  auto otick = [&](int k) {
+    const uint64_t t = __builtin_amdgcn_s_memrealtime();
+    op_acc[k] += (uint32_t)(t - op_t);
+    op_t = t;
+  };
+#else
+  auto otick = [](int) {};
+#endif
   uint32_t* const outk = oct_keys + (int64_t)img * g->out_per_image + L.out_base;
   // ---- 1. candidate count; a level that does not fit is done here by the global-memory
   // algorithm (octree_global, its scratch on this work-group's LDS; the host checked it fits),
@@ -1719,12 +1740,12 @@ __global__ __launch_bounds__(kOctLvlThreads) void octree_lvl_kernel(
   K = lvl_block_sum(K, s_red);
   const int nIni = L.n_ini;
   const int NC = L.oct_nc;
-  if (K > g->oct2_kcap || nIni > 16 || ncell + 1 > g->oct2_ccap || NC > g->oct2_nc) {
+  if (K > g->oct2_kcap || K > kOctKpt * kOctLvlThreads || nIni > 16 ||
+      ncell + 1 > g->oct2_ccap || NC > g->oct2_nc) {
     if (tid == 0) *outc = -1;
     __syncthreads();
-    static_assert(kOctLvlThreads == kOctThreads, "octree_global runs on this work-group");
-    octree_global(*reinterpret_cast<OctShared*>(s_lvl), level, img, g, cell_keys, cell_count,
-                  key_scratch, node_scratch, oct_keys, oct_count, err);
+    octree_global<kOctLvlThreads>(*reinterpret_cast<OctShared*>(s_lvl), level, img, g, cell_keys,
+                                  cell_count, key_scratch, node_scratch, oct_keys, oct_count, err);
     return;
   }
   if (K == 0) {
@@ -1741,7 +1762,11 @@ __global__ __launch_bounds__(kOctLvlThreads) void octree_lvl_kernel(
   int16_t* const pu = pe + NC;
   int16_t* const vnext = pu + NC;
   uint8_t* const processed = reinterpret_cast<uint8_t*>(vnext + NC);
-  uint32_t* const gscratch = key_scratch + img * g->keys_per_image + L.key_base;
+  uint8_t* const cand = processed + NC;  // the inner passes' candidates (vPrev), by list index
+  uint2* const nst = reinterpret_cast<uint2*>(
+      (reinterpret_cast<uintptr_t>(cand + NC) + 15) & ~static_cast<uintptr_t>(15));
+  uint2* const nen = nst + NC;                         // prefix at / past a node's keys
+  int16_t* const cb = reinterpret_cast<int16_t*>(nen + NC);  // first child's push index, or -1
 
   // ---- 2. gather in cell row-major order (a key slot finds its cell by binary search over the
   // cell prefix), then a stable placement into the initial nodes' buckets (:484-526)
@@ -1839,14 +1864,38 @@ __global__ __launch_bounds__(kOctLvlThreads) void octree_lvl_kernel(
   int m = s_u[0];
   __syncthreads();
 
-  // ---- 3. passes (as octree_img_kernel; node j of a pass belongs to wave (j / 64) % W when it
-  // is divided by one lane, to wave j % W when a whole wave divides it)
+  // ---- 3. passes: the list semantics of octree_img_kernel, divided key-parallel. Thread t owns
+  // the key positions [t * kpt, (t + 1) * kpt) for the whole level: their keys, the node covering
+  // each position and the position's exclusive prefix of quadrant one-hots (four 16-bit counters
+  // in two words) stay in registers. A pass: one block scan of the one-hots over the candidate
+  // nodes' keys -> every node's quadrant counts are the prefix difference across its segment
+  // (recorded by the segment's first and last owners) -> the node list's counts, scans and
+  // children as before -> each key moves to kbeg + (keys of lower quadrants) + (its rank in its
+  // quadrant = its prefix minus the segment's), each position learns its new covering node.
+  // No serial per-node loops over keys, and the same stable partition.
+  otick(0);
   const int N = L.budget;
   int cur = 0, nexp = 0;
   bool outer = true;
-  auto owner = [&](int j, int n) {
-    return (n > kOctLaneKeys ? j : (j >> 6)) % kOctLvlWaves == w;
-  };
+  int Kn = 0;  // keys in the initial nodes (keys past the last bucket are dropped)
+  for (int i = 0; i < m; i++) Kn += node_n(lists[i]);
+  const int kpt = (Kn + kOctLvlThreads - 1) / kOctLvlThreads;  // <= kOctKpt (checked above)
+  const int kb0 = tid * kpt;
+  uint32_t kr[kOctKpt];
+  int nd[kOctKpt];
+  uint32_t plo[kOctKpt], phi[kOctKpt];
+  uint64_t qbits = 0;  // 2 bits per position: its key's quadrant in this pass
+#pragma unroll
+  for (int i = 0; i < kOctKpt; i++) {
+    nd[i] = 0;
+    if (i < kpt && kb0 + i < Kn) {
+      const int k = kb0 + i;
+      kr[i] = keys[k];
+      int c = 0;  // initial nodes are in key order: the last one starting at or before k
+      for (int q = 1; q < m; q++) c += node_kbeg(lists[q]) <= k;
+      nd[i] = c;
+    }
+  }
   while (true) {
     const OctNodeS* Lc = lists + cur * NC;
     OctNodeS* Ln = lists + (cur ^ 1) * NC;
@@ -1862,64 +1911,150 @@ __global__ __launch_bounds__(kOctLvlThreads) void octree_lvl_kernel(
         }
         sortk[i] = key;
       }
+      for (int i = tid; i < m; i += kOctLvlThreads) cand[i] = 0;
       __syncthreads();
-      for (int k = 2; k <= P2; k <<= 1)
-        for (int jj = k >> 1; jj > 0; jj >>= 1) {
-          for (int i = tid; i < P2; i += kOctLvlThreads) {
-            const int ixj = i ^ jj;
-            if (ixj > i) {
-              const uint32_t x = sortk[i], y = sortk[ixj];
-              const bool desc = (i & k) == 0;
-              if (desc ? (x < y) : (x > y)) {
-                sortk[i] = y;
-                sortk[ixj] = x;
+      for (int i = tid; i < V; i += kOctLvlThreads) cand[4095 - (int)(sortk[i] & 0xfffu)] = 1;
+      __syncthreads();
+      if (V <= 2 * kOctLvlThreads) {
+        // rank sort (the keys are distinct): an element's place is the number of larger keys,
+        // counted over the whole set with broadcast reads -- two barriers instead of the
+        // bitonic network's log^2 steps
+        uint32_t mine[2];
+        int rk[2] = {0, 0};
+#pragma unroll
+        for (int r = 0; r < 2; r++) {
+          const int i = tid + r * kOctLvlThreads;
+          mine[r] = i < V ? sortk[i] : 0u;
+        }
+        const uint4* s4 = reinterpret_cast<const uint4*>(sortk);
+        for (int j4 = 0; j4 < P2 / 4; j4++) {  // pads (0) count for nobody
+          const uint4 o = s4[j4];
+#pragma unroll
+          for (int r = 0; r < 2; r++)
+            rk[r] += (int)(o.x > mine[r]) + (int)(o.y > mine[r]) + (int)(o.z > mine[r]) +
+                     (int)(o.w > mine[r]);
+        }
+        __syncthreads();
+#pragma unroll
+        for (int r = 0; r < 2; r++)
+          if (tid + r * kOctLvlThreads < V) sortk[rk[r]] = mine[r];
+        __syncthreads();
+      } else {
+        for (int k = 2; k <= P2; k <<= 1)
+          for (int jj = k >> 1; jj > 0; jj >>= 1) {
+            for (int i = tid; i < P2; i += kOctLvlThreads) {
+              const int ixj = i ^ jj;
+              if (ixj > i) {
+                const uint32_t x = sortk[i], y = sortk[ixj];
+                const bool desc = (i & k) == 0;
+                if (desc ? (x < y) : (x > y)) {
+                  sortk[i] = y;
+                  sortk[ixj] = x;
+                }
               }
             }
+            __syncthreads();
           }
-          __syncthreads();
-        }
+      }
     }
+    otick(1);
+#if OCT_PROF
+    op_pass++;
+#endif
     auto nidx = [&](int j) { return outer ? j : 4095 - (int)(sortk[j] & 0xfffu); };
-    // -- count children: t (non-empty), e (> 1 key); pu = survivor flag (outer) or t - 1
-    for (int j0 = 0; j0 < V; j0 += 64) {
-      const int j = j0 + lane;
-      const bool valid = j < V;
-      OctNodeS nd{};
-      if (valid) nd = Lc[nidx(j)];
-      const int n = node_n(nd);
-      int t = 0, e = 0;
-      if (valid && n > 1 && n <= kOctLaneKeys && owner(j, n)) {
-        const uint32_t c = lane_divide(nd, keys, false);
+    auto is_cand = [&](int i, const OctNodeS& nn) { return outer ? node_n(nn) > 1 : cand[i] != 0; };
+    // -- the key scan: quadrant one-hots of the candidates' keys, exclusive prefix per position
+    uint32_t slo = 0, shi = 0;
+    qbits = 0;
 #pragma unroll
-        for (int q = 0; q < 4; q++) {
-          const int cq = (c >> (8 * q)) & 255;
-          t += cq > 0;
-          e += cq > 1;
-        }
-      }
-      uint64_t bigm = __ballot(valid && n > kOctLaneKeys);
-      while (bigm) {
-        const int bl = __builtin_ctzll(bigm);
-        bigm &= bigm - 1;
-        if ((j0 + bl) % kOctLvlWaves != w) continue;
-        const OctNodeS nb = Lc[nidx(j0 + bl)];
-        int cnt[4];
-        wave_count(nb, keys, lane, cnt);
-        if (lane == bl) {
-#pragma unroll
-          for (int q = 0; q < 4; q++) {
-            t += cnt[q] > 0;
-            e += cnt[q] > 1;
+    for (int i = 0; i < kOctKpt; i++) {
+      if (i < kpt) {
+        uint32_t olo = 0, ohi = 0;
+        if (kb0 + i < Kn) {
+          const OctNodeS nn = Lc[nd[i]];
+          if (is_cand(nd[i], nn)) {
+            const uint32_t q = (uint32_t)quadrant(kr[i], node_xm(nn), node_ym(nn));
+            qbits |= (uint64_t)q << (2 * i);
+            const uint32_t oh = 1u << (16 * (q & 1));
+            olo = q < 2 ? oh : 0u;
+            ohi = q < 2 ? 0u : oh;
           }
         }
+        plo[i] = slo;
+        phi[i] = shi;
+        slo += olo;
+        shi += ohi;
       }
-      if (valid && owner(j, n)) {
-        pt[j] = (int16_t)t;
-        pe[j] = (int16_t)e;
-        pu[j] = (int16_t)(outer ? (n == 1) : t - 1);
+    }
+    {
+      int tl, th;
+      const int el = wave_excl_scan((int)slo, lane, &tl);
+      const int eh = wave_excl_scan((int)shi, lane, &th);
+      if (lane == 0) {
+        s_scan[w][0] = tl;
+        s_scan[w][1] = th;
+      }
+      __syncthreads();
+      uint32_t blo = (uint32_t)el, bhi = (uint32_t)eh;
+      for (int k = 0; k < w; k++) {
+        blo += (uint32_t)s_scan[k][0];
+        bhi += (uint32_t)s_scan[k][1];
+      }
+#pragma unroll
+      for (int i = 0; i < kOctKpt; i++) {
+        if (i < kpt) {
+          plo[i] += blo;
+          phi[i] += bhi;
+        }
+      }
+    }
+    // segment boundaries: the prefix at a candidate node's first key and past its last
+#pragma unroll
+    for (int i = 0; i < kOctKpt; i++) {
+      if (i < kpt && kb0 + i < Kn) {
+        const int k = kb0 + i;
+        const OctNodeS nn = Lc[nd[i]];
+        if (is_cand(nd[i], nn)) {
+          if (k == node_kbeg(nn)) nst[nd[i]] = make_uint2(plo[i], phi[i]);
+          if (k == node_kbeg(nn) + node_n(nn) - 1) {
+            const uint32_t q = (uint32_t)(qbits >> (2 * i)) & 3u;
+            const uint32_t oh = 1u << (16 * (q & 1));
+            nen[nd[i]] = make_uint2(plo[i] + (q < 2 ? oh : 0u), phi[i] + (q < 2 ? 0u : oh));
+          }
+        }
       }
     }
     __syncthreads();
+    auto counts = [&](int i, int c[4]) {
+      const uint2 a0 = nst[i], a1 = nen[i];
+      const uint32_t dl = a1.x - a0.x, dh = a1.y - a0.y;
+      c[0] = (int)(dl & 0xffffu);
+      c[1] = (int)(dl >> 16);
+      c[2] = (int)(dh & 0xffffu);
+      c[3] = (int)(dh >> 16);
+    };
+    // -- count children: t (non-empty), e (> 1 key); pu = survivor flag (outer) or t - 1
+    for (int j = tid; j < V; j += kOctLvlThreads) {
+      const int i = nidx(j);
+      const OctNodeS nn = Lc[i];
+      const int n = node_n(nn);
+      int t = 0, e = 0;
+      if (n > 1) {
+        int c[4];
+        counts(i, c);
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+          t += c[q] > 0;
+          e += c[q] > 1;
+        }
+      }
+      pt[j] = (int16_t)t;
+      pe[j] = (int16_t)e;
+      pu[j] = (int16_t)(outer ? (n == 1) : t - 1);
+    }
+    for (int i = tid; i < m; i += kOctLvlThreads) cb[i] = -1;
+    __syncthreads();
+    otick(2);
     int nproc = V;
     if (!outer) {
       // processing stops once the list reaches N: first j with m + sum_{i<=j}(t_i - 1) >= N
@@ -1959,85 +2094,91 @@ __global__ __launch_bounds__(kOctLvlThreads) void octree_lvl_kernel(
       if (lane == 0) s_u[2] = t;
     }
     __syncthreads();
+    otick(3);
     const int T = s_u[0], E = s_u[1], U = s_u[2];
     const int newm = T + U;
     if (newm > NC || E > NC) {
       if (tid == 0) atomicOr(err, kErrNodeOverflow);
       break;
     }
-    // -- divide in place and place children: push order gpos -> list position T-1-gpos
-    auto place = [&](int j, const OctNodeS& nd, uint32_t c4) {
+    // -- children at their final list positions: push order gpos -> list position T-1-gpos
+    for (int j = tid; j < nproc; j += kOctLvlThreads) {
+      const int i = nidx(j);
+      const OctNodeS nn = Lc[i];
+      if (node_n(nn) <= 1) continue;
+      int c[4];
+      counts(i, c);
       int gpos = pt[j], epos = pe[j];
-      const int xm = node_xm(nd), ym = node_ym(nd);
-      const int16_t xs[3] = {nd.x0, (int16_t)xm, nd.x1};
-      const int16_t ys[3] = {nd.y0, (int16_t)ym, nd.y1};
-      int start = node_kbeg(nd);
+      cb[i] = (int16_t)gpos;
+      const int xm = node_xm(nn), ym = node_ym(nn);
+      const int16_t xs[3] = {nn.x0, (int16_t)xm, nn.x1};
+      const int16_t ys[3] = {nn.y0, (int16_t)ym, nn.y1};
+      int start = node_kbeg(nn);
 #pragma unroll
       for (int q = 0; q < 4; q++) {
-        const int cq = (int)((c4 >> (8 * q)) & 255u);
-        if (cq > 0) {
+        if (c[q] > 0) {
           OctNodeS ch;
           ch.x0 = xs[q & 1];
           ch.x1 = xs[(q & 1) + 1];
           ch.y0 = ys[q >> 1];
           ch.y1 = ys[(q >> 1) + 1];
-          ch.kn = (uint32_t)start | (uint32_t)cq << 16;
+          ch.kn = (uint32_t)start | (uint32_t)c[q] << 16;
           const int pos = T - 1 - gpos;
           Ln[pos] = ch;
-          if (cq > 1) vnext[epos++] = (int16_t)pos;
+          if (c[q] > 1) vnext[epos++] = (int16_t)pos;
           gpos++;
         }
-        start += cq;
+        start += c[q];
       }
-    };
-    for (int j0 = 0; j0 < nproc; j0 += 64) {
-      const int j = j0 + lane;
-      const bool valid = j < nproc;
-      OctNodeS nd{};
-      if (valid) nd = Lc[nidx(j)];
-      const int n = node_n(nd);
-      if (valid && n > 1 && n <= kOctLaneKeys && owner(j, n))
-        place(j, nd, lane_divide(nd, keys, true));
-      uint64_t bigm = __ballot(valid && n > kOctLaneKeys);
-      while (bigm) {
-        const int bl = __builtin_ctzll(bigm);
-        bigm &= bigm - 1;
-        if ((j0 + bl) % kOctLvlWaves != w) continue;
-        const OctNodeS nb = Lc[nidx(j0 + bl)];
-        int cnt[4];
-        wave_partition(nb, keys, gscratch, lane, cnt);
-        if (lane == 0) {
-          // counts can exceed 255 here: place() takes 8-bit counts, so place big ones inline
-          int gpos = pt[j0 + bl], epos = pe[j0 + bl];
-          const int xm = node_xm(nb), ym = node_ym(nb);
-          const int16_t xs[3] = {nb.x0, (int16_t)xm, nb.x1};
-          const int16_t ys[3] = {nb.y0, (int16_t)ym, nb.y1};
-          int start = node_kbeg(nb);
-          for (int q = 0; q < 4; q++) {
-            if (cnt[q] > 0) {
-              OctNodeS ch;
-              ch.x0 = xs[q & 1];
-              ch.x1 = xs[(q & 1) + 1];
-              ch.y0 = ys[q >> 1];
-              ch.y1 = ys[(q >> 1) + 1];
-              ch.kn = (uint32_t)start | (uint32_t)cnt[q] << 16;
-              const int pos = T - 1 - gpos;
-              Ln[pos] = ch;
-              if (cnt[q] > 1) vnext[epos++] = (int16_t)pos;
-              gpos++;
-            }
-            start += cnt[q];
+    }
+    otick(4);
+    for (int i = tid; i < m; i += kOctLvlThreads) {
+      const OctNodeS nn = Lc[i];
+      if (outer ? node_n(nn) == 1 : !processed[i]) Ln[T + pu[i]] = nn;
+    }
+    __syncthreads();
+    // -- keys to their quadrant's range; each position's covering node in the new list
+#pragma unroll
+    for (int i = 0; i < kOctKpt; i++) {
+      if (i < kpt && kb0 + i < Kn) {
+        const int k = kb0 + i;
+        const int o = nd[i];
+        const int base = cb[o];
+        if (base >= 0) {
+          const OctNodeS nn = Lc[o];
+          int c[4];
+          counts(o, c);
+          const uint2 s0 = nst[o];
+          const uint32_t q = (uint32_t)(qbits >> (2 * i)) & 3u;
+          const uint32_t dl = plo[i] - s0.x, dh = phi[i] - s0.y;
+          const int rank = (int)(((q < 2 ? dl : dh) >> (16 * (q & 1))) & 0xffffu);
+          int off = 0;
+#pragma unroll
+          for (int qq = 0; qq < 4; qq++) off += (uint32_t)qq < q ? c[qq] : 0;
+          const int kb = node_kbeg(nn);
+          keys[kb + off + rank] = kr[i];
+          // the child whose range holds position k: ranges in quadrant order from kb
+          const int r = k - kb;
+          int cum = 0, nz = 0, child = 0;
+#pragma unroll
+          for (int qq = 0; qq < 4; qq++) {
+            if (c[qq] > 0 && r >= cum) child = nz;
+            nz += c[qq] > 0;
+            cum += c[qq];
           }
+          nd[i] = T - 1 - (base + child);
+        } else {
+          nd[i] = T + pu[o];
         }
       }
     }
-    for (int i = tid; i < m; i += kOctLvlThreads) {
-      const OctNodeS nd = Lc[i];
-      if (outer ? node_n(nd) == 1 : !processed[i]) Ln[T + pu[i]] = nd;
-    }
     __syncthreads();
+#pragma unroll
+    for (int i = 0; i < kOctKpt; i++)
+      if (i < kpt && kb0 + i < Kn) kr[i] = keys[kb0 + i];
     for (int i = tid; i < E; i += kOctLvlThreads) sortk[i] = (uint32_t)vnext[i];
     __syncthreads();
+    otick(5);
     const int mprev = m;
     m = newm;
     nexp = E;
@@ -2063,6 +2204,15 @@ __global__ __launch_bounds__(kOctLvlThreads) void octree_lvl_kernel(
     if (m > L.out_cap) atomicOr(err, kErrNodeOverflow);
     *outc = mout;
   }
+#if OCT_PROF
+  otick(6);
+  if (tid == 0 && img == 0 && (level == 0 || level == nlev - 1))
+    printf("[octlvl L%d] K %d m %d passes %d | us: gather %.1f sort %.1f count %.1f nproc+scan %.1f "
+           "place %.1f survivors %.1f retain %.1f | total %.1f\n", level, K, m, op_pass,
+           0.01 * op_acc[0], 0.01 * op_acc[1], 0.01 * op_acc[2], 0.01 * op_acc[3],
+           0.01 * op_acc[4], 0.01 * op_acc[5], 0.01 * op_acc[6],
+           0.01 * (double)(__builtin_amdgcn_s_memrealtime() - op_t0));
+#endif
 }
 
 // ---------------------------------------------------------------------------------------
