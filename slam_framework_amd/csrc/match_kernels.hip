@@ -48,10 +48,10 @@ __device__ __forceinline__ const uint8_t* level_img(const ImageBatch& b, const O
   return b.pyr + (int64_t)img * g->pyr_bytes + g->lv[level].offset;
 }
 
-// 256-thread exclusive scan of arr[0..n) in place; returns the total.
-template <int CAP>
+// NT-thread exclusive scan of arr[0..n) in place; returns the total. wsum: NT / 64 ints.
+template <int CAP, int NT = 256>
 __device__ int scan256(int* arr, int n, int* wsum) {
-  constexpr int per = (CAP + 255) / 256;
+  constexpr int per = (CAP + NT - 1) / NT;
   const int lane = threadIdx.x & 63, wid = wave_id();
   const int base = threadIdx.x * per;
   int loc[per];
@@ -71,7 +71,7 @@ __device__ int scan256(int* arr, int n, int* wsum) {
   __syncthreads();
   int pre = 0, tot = 0;
 #pragma unroll
-  for (int w = 0; w < 4; w++) {
+  for (int w = 0; w < NT / 64; w++) {
     pre += (w < wid) ? wsum[w] : 0;
     tot += wsum[w];
   }
@@ -85,33 +85,42 @@ __device__ int scan256(int* arr, int n, int* wsum) {
   return tot;
 }
 
+__device__ __forceinline__ uint32_t wave_or(uint32_t v) {
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) v |= __shfl_xor(v, off, 64);
+  return v;
+}
+
 // ---------------------------------------------------------------------------------------
 // Stereo (frame.cpp:406-577). Frame f: left = image 2f, right = image 2f+1.
 constexpr int kMaxRows = 2048;
 
-__global__ __launch_bounds__(256) void stereo_rows_kernel(const OrbGeom* __restrict__ g,
-                                                          FrameKps ext, int nrows,
-                                                          StereoWorkspace ws,
-                                                          uint32_t* __restrict__ err) {
+// NT threads per frame: 256 for batches, 1024 for the single-frame call (its one work-group is
+// the whole launch: a quarter of the serial LDS-atomic loops per thread).
+template <int NT>
+__global__ __launch_bounds__(NT) void stereo_rows_kernel(const OrbGeom* __restrict__ g,
+                                                         FrameKps ext, int nrows,
+                                                         StereoWorkspace ws,
+                                                         uint32_t* __restrict__ err) {
   __shared__ int cnt[kMaxRows + 1];
-  __shared__ int wsum[4];
+  __shared__ int wsum[NT / 64];
   const int f = blockIdx.x, tid = threadIdx.x;
   const int ir = 2 * f + 1;
   const KeyPoint* kr = ext.kps + ir * ext.stride;
   const int nr = ext.n[ir * ext.n_stride];
   int* rs = ws.row_start + (int64_t)f * (nrows + 1);
   int* items = ws.row_items + (int64_t)f * ws.row_cap;
-  for (int i = tid; i <= nrows; i += 256) cnt[i] = 0;
+  for (int i = tid; i <= nrows; i += NT) cnt[i] = 0;
   __syncthreads();
   // a thread's keypoints are loaded kChunk at a time before their row updates: one load latency
   // per chunk instead of one per keypoint (a single frame runs this as one work-group)
-  constexpr int kChunk = 8;
+  constexpr int kChunk = 2048 / NT;
   auto row_span = [&](int base, int (&lo)[kChunk], int (&hi)[kChunk]) {
     float ky[kChunk];
     int ko[kChunk];
 #pragma unroll
     for (int u = 0; u < kChunk; u++) {
-      const int i = base + 256 * u + tid;
+      const int i = base + NT * u + tid;
       ky[u] = 0.0f;
       ko[u] = -1;
       if (i < nr) {
@@ -130,7 +139,7 @@ __global__ __launch_bounds__(256) void stereo_rows_kernel(const OrbGeom* __restr
       }
     }
   };
-  for (int base = 0; base < nr; base += 256 * kChunk) {
+  for (int base = 0; base < nr; base += NT * kChunk) {
     int lo[kChunk], hi[kChunk];
     row_span(base, lo, hi);
 #pragma unroll
@@ -138,21 +147,21 @@ __global__ __launch_bounds__(256) void stereo_rows_kernel(const OrbGeom* __restr
       for (int yi = lo[u]; yi <= hi[u]; ++yi) atomicAdd(&cnt[yi], 1);
   }
   __syncthreads();
-  const int total = scan256<kMaxRows + 1>(cnt, nrows, wsum);
-  for (int i = tid; i < nrows; i += 256) rs[i] = cnt[i];
+  const int total = scan256<kMaxRows + 1, NT>(cnt, nrows, wsum);
+  for (int i = tid; i < nrows; i += NT) rs[i] = cnt[i];
   if (tid == 0) {
     rs[nrows] = total;
     if (total > ws.row_cap) atomicOr(err, kErrRowOverflow);
   }
   __syncthreads();
-  for (int base = 0; base < nr; base += 256 * kChunk) {
+  for (int base = 0; base < nr; base += NT * kChunk) {
     int lo[kChunk], hi[kChunk];
     row_span(base, lo, hi);
 #pragma unroll
     for (int u = 0; u < kChunk; u++)
       for (int yi = lo[u]; yi <= hi[u]; ++yi) {
         const int pos = atomicAdd(&cnt[yi], 1);
-        if (pos < ws.row_cap) items[pos] = base + 256 * u + tid;
+        if (pos < ws.row_cap) items[pos] = base + NT * u + tid;
       }
   }
 }
@@ -358,40 +367,55 @@ __global__ __launch_bounds__(256) void stereo_match_kernel(ImageBatch b,
 // pack (the single-frame call, frame 0 only): the frame's final u_right / depth also go to the
 // packed host-mirror record (frame_pack_kernel's layout), and the device error word to its
 // header slot 8 -- no frame_pack launch after this one on the call's critical path.
-__global__ __launch_bounds__(256) void stereo_median_kernel(const OrbGeom* __restrict__ g,
-                                                            FrameKps ext, StereoWorkspace ws,
-                                                            StereoOut out,
-                                                            uint8_t* __restrict__ pack,
-                                                            const uint32_t* __restrict__ err) {
+// NT threads per frame (1024 for the single-frame call). The digit rounds start at the highest
+// non-zero byte of the OR of all SADs (SADs are below 121 * 510 < 2^16: two rounds, not four).
+template <int NT>
+__global__ __launch_bounds__(NT) void stereo_median_kernel(const OrbGeom* __restrict__ g,
+                                                           FrameKps ext, StereoWorkspace ws,
+                                                           StereoOut out,
+                                                           uint8_t* __restrict__ pack,
+                                                           const uint32_t* __restrict__ err) {
   constexpr int kCap = 4096;
   __shared__ uint32_t vals[kCap];
   __shared__ int hist[256];
   __shared__ int n_valid, s_digit, s_rank;
+  __shared__ uint32_t s_or;
   const int f = blockIdx.x, tid = threadIdx.x, lane = tid & 63;
   const int nl = min(ext.n[2 * f * ext.n_stride], kCap);
   const int64_t base = (int64_t)f * g->kp_cap;
-  if (tid == 0) n_valid = 0;
+  if (tid == 0) {
+    n_valid = 0;
+    s_or = 0;
+  }
   __syncthreads();
-  for (int i0 = 0; i0 < nl; i0 += 256 * 4) {  // 4 loads in flight per thread
+  uint32_t vor = 0;
+  for (int i0 = 0; i0 < nl; i0 += NT * 4) {  // 4 loads in flight per thread
     int sv[4];
 #pragma unroll
     for (int u = 0; u < 4; u++) {
-      const int i = i0 + 256 * u + tid;
+      const int i = i0 + NT * u + tid;
       sv[u] = i < nl ? ws.sad[base + i] : -1;
     }
 #pragma unroll
     for (int u = 0; u < 4; u++)
-      if (sv[u] >= 0) vals[atomicAdd(&n_valid, 1)] = (uint32_t)sv[u];
+      if (sv[u] >= 0) {
+        vals[atomicAdd(&n_valid, 1)] = (uint32_t)sv[u];
+        vor |= (uint32_t)sv[u];
+      }
   }
+  vor = wave_or(vor);
+  if (lane == 0 && vor) atomicOr(&s_or, vor);
   __syncthreads();
   const int n = n_valid;
+  const uint32_t all_or = s_or;
   // n == 0: the reference indexes an empty vector here (UB); we skip the filter
   uint32_t prefix = 0, mask = 0;
   int k = n / 2;  // rank of the median among the values matching prefix under mask
-  for (int shift = 24; shift >= 0 && n > 0; shift -= 8) {
-    hist[tid] = 0;
+  const int top = all_or >> 24 ? 24 : all_or >> 16 ? 16 : all_or >> 8 ? 8 : 0;
+  for (int shift = top; shift >= 0 && n > 0; shift -= 8) {
+    if (tid < 256) hist[tid] = 0;
     __syncthreads();
-    for (int i = tid; i < n; i += 256) {
+    for (int i = tid; i < n; i += NT) {
       const uint32_t v = vals[i];
       if ((v & mask) == prefix) atomicAdd(&hist[(v >> shift) & 255u], 1);
     }
@@ -433,7 +457,7 @@ __global__ __launch_bounds__(256) void stereo_median_kernel(const OrbGeom* __res
                          ? reinterpret_cast<float*>(pack + 16 + 2 * kc * sizeof(KeyPoint) + 2 * kc * 32)
                          : nullptr;
   const int nall = pur ? min(max(ext.n[0], 0), (int)kc) : nl;
-  for (int i = tid; i < nall; i += 256) {
+  for (int i = tid; i < nall; i += NT) {
     const int s = i < nl ? ws.sad[base + i] : -1;
     if (n > 0 && s >= 0 && !((float)s < thDist)) {
       out.u_right[base + i] = -1.0f;
@@ -511,14 +535,22 @@ void launch_stereo(const ImageBatch& b, const OrbGeomDev& gd, const Camera& cam,
   const OrbGeom& g = *gd.host;
   FrameKps ext{gd.out.kps, gd.out.desc, gd.out.nkps, g.kp_cap, 1};
   const int nrows = g.lv[0].h;
-  SLAMGPU_LAUNCH("stereo_rows", st, stereo_rows_kernel, dim3(n_frames), dim3(256), 0, st, gd.dev, ext, nrows,
-                     ws, gd.ws.err);
+  if (n_frames <= 8)
+    SLAMGPU_LAUNCH("stereo_rows", st, stereo_rows_kernel<1024>, dim3(n_frames), dim3(1024), 0, st,
+                   gd.dev, ext, nrows, ws, gd.ws.err);
+  else
+    SLAMGPU_LAUNCH("stereo_rows", st, stereo_rows_kernel<256>, dim3(n_frames), dim3(256), 0, st,
+                   gd.dev, ext, nrows, ws, gd.ws.err);
   constexpr int kG = STEREO_LANES, kPerBlock = 4 * (64 / kG);
   SLAMGPU_LAUNCH("stereo_match", st, stereo_match_kernel<kG>,
                  dim3((g.kp_cap + kPerBlock - 1) / kPerBlock, n_frames), dim3(256), 0, st, b,
                  gd.dev, ext, cam, nrows, ws, out);
-  SLAMGPU_LAUNCH("stereo_median", st, stereo_median_kernel, dim3(n_frames), dim3(256), 0, st,
-                 gd.dev, ext, ws, out, pack, gd.ws.err);
+  if (n_frames <= 8)
+    SLAMGPU_LAUNCH("stereo_median", st, stereo_median_kernel<1024>, dim3(n_frames), dim3(1024), 0,
+                   st, gd.dev, ext, ws, out, pack, gd.ws.err);
+  else
+    SLAMGPU_LAUNCH("stereo_median", st, stereo_median_kernel<256>, dim3(n_frames), dim3(256), 0,
+                   st, gd.dev, ext, ws, out, pack, gd.ws.err);
 }
 
 // ---------------------------------------------------------------------------------------
