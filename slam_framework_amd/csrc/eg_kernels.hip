@@ -184,6 +184,7 @@ __global__ __launch_bounds__(64) void eg_assemble_kernel(EgGraph G, EgState W) {
 #endif
 constexpr int kFacThreads = 1024;
 constexpr int kPanStage = 96;  // extent blocks whose panel is staged in LDS (37.6 KB)
+constexpr int kXr = 64;        // columns of x the backward solve keeps in its LDS ring
 
 // The LDLT of H + lambda I (profile storage, vertex order) and the solve, by one work-group of
 // 16 waves. Right-looking by 7x7 block column k with a look-ahead: the panel (a thread per row of
@@ -209,6 +210,14 @@ __device__ __forceinline__ double bcast(double x, int l) {
   return __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
 }
 
+// x of lane l - 1 (DPP wave_shr:1; lane 0 gets 0)
+__device__ __forceinline__ double bcast_dpp_shr1(double x) {
+  const uint64_t u = __builtin_bit_cast(uint64_t, x);
+  const uint32_t lo = __builtin_amdgcn_update_dpp(0u, (uint32_t)u, 0x138, 0xf, 0xf, false);
+  const uint32_t hi = __builtin_amdgcn_update_dpp(0u, (uint32_t)(u >> 32), 0x138, 0xf, 0xf, false);
+  return __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
+}
+
 // kMeta: the factorisation's structure -- ext_ptr, ext_rows, ext_base and each column's
 // diagonal block index -- is staged in LDS at the start (dynamic LDS, 4 B per entry), so the
 // per-column chain of dependent structure loads (ext_ptr -> ext_base -> the block) reads LDS
@@ -227,6 +236,7 @@ __global__ __launch_bounds__(kFacThreads) void eg_factor_solve_kernel(EgGraph G,
   __shared__ double s_y[2][7];    // its forward-solved rhs slice
   __shared__ double s_nx[49];     // the next diagonal block after its last update
   __shared__ double s_pan[kPanStage * 49];  // column k's panel blocks L_ik (extents <= kPanStage)
+  __shared__ double s_xr[kXr * 7];          // the backward solve's x of the last kXr columns
   extern __shared__ int32_t s_meta[];  // kMeta: ext_ptr [F + 1], diag block [F], rows, bases
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, F = G.F;
   double* L = W.L;  // a copy of H (launch_eg_factor_solve)
@@ -402,34 +412,110 @@ __global__ __launch_bounds__(kFacThreads) void eg_factor_solve_kernel(EgGraph G,
   for (int q = tid; q < 7 * F; q += kFacThreads) y[q] /= diag_of(q / 7)[8 * (q % 7)];
   __syncthreads();
   if (wid == 0) {
+    // Lane l = 9 c + t (c < 7, t < 9): component c of extent block t (blocks in groups of 9).
+    // Each lane forms its block's seven products L_ik(r, c) x_i(r) at once; the sum over the
+    // extent keeps the serial order (block by block, r = 0..6 within a block) as a chain handed
+    // from lane t - 1 to lane t (DPP wave shift), so the bits are those of the one-lane loop.
+    // The column's L blocks are loaded one column ahead; x of the last kXr columns is read from
+    // an LDS ring, older x (loop rows) from y in memory. Then lanes 0-6 solve the diagonal block
+    // (lane r holds x_k(r); each subtraction in the serial order).
+    const int c = lane / 9, t = lane - 9 * c;
+    const bool lane_ok = c < 7;
+    // block g0 + t of column k's extent: its L column c, and x of its row when that row is
+    // older than the ring (written by this wave kXr+ columns ago; ordered by the wavefront-scope
+    // release / acquire closing every column -- AMDGPU memory model, no wait needed)
+    auto load_blk = [&](int k, int g0, double (&lv)[7], double (&xv)[7]) {
+      const int e0 = EP(k), ne = EP(k + 1) - e0;
+      if (lane_ok && g0 + t < ne) {
+        const double* Lik = L + (EB(e0 + g0 + t) + k) * 49 + c;
+#pragma unroll
+        for (int r = 0; r < 7; r++) lv[r] = Lik[7 * r];
+        const int i = ER(e0 + g0 + t);
+        if (i - k > kXr)
+#pragma unroll
+          for (int r = 0; r < 7; r++) xv[r] = y[7 * i + r];
+      }
+    };
+    auto load_diag = [&](int k, double (&dv)[7]) {  // lane r < 7: Lkk(m, r) for m = 0..6
+      if (lane < 7) {
+        const double* Lkk = diag_of(k);
+#pragma unroll
+        for (int m = 0; m < 7; m++) dv[m] = Lkk[7 * m + lane];
+      }
+    };
+    double lnext[7], dnext[7], xnext[7];
+#pragma unroll
+    for (int r = 0; r < 7; r++) lnext[r] = dnext[r] = xnext[r] = 0.0;
+    if (F > 0) {
+      load_blk(F - 1, 0, lnext, xnext);
+      load_diag(F - 1, dnext);
+    }
     for (int k = F - 1; k >= 0; k--) {
       const int e0 = EP(k), ne = EP(k + 1) - e0;
-      if (lane < 7) {  // y_k -= sum over the later rows i of L_ik' x_i (lane c: component c)
-        double acc = 0.0;
-        for (int t = 0; t < ne; t++) {
-          const double* Lik = L + (EB(e0 + t) + k) * 49;
-          const double* xi = y + 7 * ER(e0 + t);
+      double lcur[7], dcur[7], xcur[7];
 #pragma unroll
-          for (int r = 0; r < 7; r++) acc += Lik[7 * r + lane] * xi[r];
+      for (int r = 0; r < 7; r++) {
+        lcur[r] = lnext[r];
+        dcur[r] = dnext[r];
+        xcur[r] = xnext[r];
+      }
+      if (k > 0) {  // the next column's blocks, in flight under this one
+        load_blk(k - 1, 0, lnext, xnext);
+        load_diag(k - 1, dnext);
+      }
+      double acc = 0.0;
+      for (int g0 = 0; g0 < ne; g0 += 9) {
+        if (g0 > 0) load_blk(k, g0, lcur, xcur);
+        const int tt = g0 + t;
+        const bool has = lane_ok && tt < ne;
+        const int i = has ? ER(e0 + tt) : k;
+        const bool far = has && i - k > kXr;
+        double pr[7];
+#pragma unroll
+        for (int r = 0; r < 7; r++) {
+          const double xi = !has ? 0.0 : far ? xcur[r] : s_xr[(i % kXr) * 7 + r];
+          pr[r] = lcur[r] * xi;
         }
-        y[7 * k + lane] -= acc;
+        const int steps = min(9, ne - g0);
+        double carry = acc;  // lane 9 c + 8 of the previous group: its total, to lane 9 c
+        if (g0 > 0) carry = __shfl(acc, lane + 8, 64);
+#pragma unroll
+        for (int st2 = 0; st2 < 9; st2++) {  // branch-free: lane t keeps step t's sum
+          if (st2 < steps) {
+            const double prev = bcast_dpp_shr1(acc);
+            double v = st2 == 0 ? carry : prev;
+#pragma unroll
+            for (int r = 0; r < 7; r++) v += pr[r];
+            acc = t == st2 ? v : acc;
+          }
+        }
       }
-      __builtin_amdgcn_s_waitcnt(0);  // the stores land before lane 0 reads them
-      __builtin_amdgcn_wave_barrier();
-      if (lane == 0) {
-        const double* Lkk = diag_of(k);
-        double v[7];
-#pragma unroll
-        for (int r = 0; r < 7; r++) v[r] = y[7 * k + r];
-#pragma unroll
-        for (int r = 5; r >= 0; r--)
-#pragma unroll
-          for (int m = r + 1; m < 7; m++) v[r] -= Lkk[7 * m + r] * v[m];
-#pragma unroll
-        for (int r = 0; r < 6; r++) y[7 * k + r] = v[r];
+      // component c's sum sits in lane 9 c + (ne - 1) % 9; lanes 0-6 take it
+      const double tot = __shfl(acc, 9 * min(lane, 6) + (ne > 0 ? (ne - 1) % 9 : 0), 64);
+      double v = 0.0;
+      if (lane < 7) {
+        v = y[7 * k + lane];
+        if (ne > 0) v -= tot;
       }
-      __builtin_amdgcn_s_waitcnt(0);
+      // the diagonal block: x(r) -= Lkk(m, r) x(m) for m = r + 1 .. 6, r = 5 .. 0
+      // (lane m - 1 finishes once x(m) is final: all of its subtractions m' = m .. 6 then, in
+      // increasing m'; branch-free, the other lanes' copies discarded)
+      double xm[7];
+#pragma unroll
+      for (int m = 6; m >= 1; m--) {
+        xm[m] = bcast(v, m);
+        double w = v;
+#pragma unroll
+        for (int mm = m; mm < 7; mm++) w -= dcur[mm] * xm[mm];
+        v = lane == m - 1 ? w : v;
+      }
+      if (lane < 7) {
+        s_xr[(k % kXr) * 7 + lane] = v;
+        y[7 * k + lane] = v;
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     }
   }
   __syncthreads();

@@ -1,9 +1,9 @@
 #!/bin/bash
-# Round-3 evidence on the current tree: the GPU parity suite, smoke(), a default bench line and a
+# Round evidence on the current tree: the GPU parity suite, smoke(), a default bench line and a
 # rocprofv3 kernel trace (stats) of the same bench command.
-#   TAG=r3zb tools/r3_final.sh
+#   TAG=r4x tools/round_final.sh
 export TMPDIR=/tmp
-TAG=${TAG:-r3final}
+TAG=${TAG:-final}
 OUT=gpurun_out/$TAG
 mkdir -p $OUT
 timeout -k 10 400 python3 -u -m pytest tests -m gpu -v --timeout 200 --timeout-method thread \
@@ -21,4 +21,4 @@ if [ "${STATS:-1}" = "1" ]; then
     python3 bench.py > $OUT/stats_bench.json 2> $OUT/stats.log || { echo "rocprof rc=$?"; exit 1; }
   echo "rocprof ok"
 fi
-echo "r3_final done"
+echo "round_final done"
