@@ -12,6 +12,7 @@
 namespace slamgpu {
 
 constexpr int kMaxLevels = 12;
+constexpr int kPyrMaxBands = 32;
 constexpr int kEdgeThreshold = 19;
 constexpr int kMinBorder = kEdgeThreshold - 3;  // minBorderX/Y (:712)
 constexpr int kPatchSize = 31;
@@ -72,13 +73,20 @@ struct OrbGeom {
   int oct_kcap;          // keys of all levels of one image that fit in that LDS
   // octree_lvl_kernel (one work-group per level): one layout for every level
   // [keys u32 x oct2_kcap][gather staging u32 x oct2_kcap][cell prefix int x oct2_ccap]
-  // [two node lists x oct2_nc][sort keys u32, pt / pe / pu / vnext i16, processed u8 x oct2_nc]
+  // [two node lists x oct2_nc][sort keys u32, pt / pe / pu / vnext i16, processed + candidate
+  // u8, two scan prefixes (uint2), first-child index i16 x oct2_nc]
   int oct2_lds_bytes, oct2_kcap, oct2_ccap, oct2_nc;
   int oct2_tmp_off, oct2_cpre_off, oct2_list_off, oct2_work_off;
   int out_per_image;     // sum of out_cap
   int kp_cap;            // max keypoints per image after Compute (== out_per_image)
   int umax[16];
   LevelGeom lv[kMaxLevels];
+  // pyr_band_kernel (small launches: levels 2 .. nlevels - 1 in one launch): band s computes
+  // rows [pyr_band[s][l][0], pyr_band[s][l][1]) of level l -- its share of the level plus every
+  // source row its own next level needs (so a band reads only rows it wrote itself)
+  int pyr_bands;
+  int pyr_band_lds;  // bytes of one of its two LDS row buffers (the largest band level)
+  int16_t pyr_band[kPyrMaxBands][kMaxLevels][2];
 };
 
 // Resize tables (HResizeLinear / VResizeLinear coefficients, 11-bit fixed point).

@@ -70,17 +70,20 @@ constexpr int kPyrShortStrip = PYR_SHORT_STRIP, kPyrShortMaxImages = 16;
 // more waves per SIMD hide the strip's chain of row loads.
 // kStrip: output rows per wave -- kPyrStrip for batches; small launches (a single frame) take
 // short strips so that more waves share a level and each walks a shorter chain of row loads.
-// One wave: output rows [dy0, dy0 + kStrip) x columns [256 tx, 256 tx + 256) of `level`.
+// One wave: output rows [dy0, dy0 + min(kStrip, nlim)) x columns [256 tx, 256 tx + 256) of
+// `level`. A strip fetches every source row its rows need, so strips compose in any partition.
 template <bool kAligned, int kStrip>
 __device__ __forceinline__ void pyr_strip(const ImageBatch& b, const OrbGeom* __restrict__ g,
                                           int level, int img, int tx, int dy0,
                                           const ResizeX* __restrict__ rxt,
-                                          const ResizeY* __restrict__ ryt) {
+                                          const ResizeY* __restrict__ ryt, int nlim = kStrip,
+                                          const uint8_t* src_rows = nullptr, int src_row0 = 0,
+                                          uint8_t* copy_rows = nullptr, int copy_row0 = 0) {
   const int lane = threadIdx.x & 63;
   const LevelGeom& D = g->lv[level];
   const LevelGeom& S = g->lv[level - 1];
-  if (dy0 >= D.h) return;
-  const int nrows = min(kStrip, D.h - dy0);
+  if (dy0 >= D.h || nlim <= 0) return;
+  const int nrows = min(min(kStrip, D.h - dy0), nlim);
   // the strip's row table, one entry per lane (read back with readlane)
   int ry_y0 = 0, ry_y1 = 0, ry_b = 0;
   if (lane < nrows) {
@@ -108,10 +111,15 @@ __device__ __forceinline__ void pyr_strip(const ImageBatch& b, const OrbGeom* __
   const int q0 = s0 >> 2, sh = s0 & 3, qmax = (S.w - 1) >> 2;
   int spitch;
   const uint8_t* src = level_ptr(b, g, img, level - 1, &spitch);
+  int srow0 = 0;  // row of src's first row (rows staged elsewhere, e.g. LDS, start later)
+  if (src_rows) {
+    src = src_rows;
+    srow0 = src_row0;
+  }
   const bool aligned = kAligned;
   const int qa = min(q0, qmax), qb = min(q0 + 1, qmax), qc = min(q0 + 2, qmax);
   auto fetch = [&](int sy, uint32_t (&wv)[3]) {
-    const uint8_t* row = src + (int64_t)min(sy, sy_hi) * spitch;  // wave-uniform
+    const uint8_t* row = src + (int64_t)(min(sy, sy_hi) - srow0) * spitch;  // wave-uniform
     if (aligned) {  // clamped dwords stay inside the row; bytes past sx+1 carry zero weight
       const uint32_t* rw = reinterpret_cast<const uint32_t*>(row);
       wv[0] = rw[(uint32_t)qa];
@@ -166,8 +174,15 @@ __device__ __forceinline__ void pyr_strip(const ImageBatch& b, const OrbGeom* __
           uint8_t* drow = dst + (int64_t)(dy0 + nd) * D.pitch;
           if (x0 + 4 <= D.w) {
             *reinterpret_cast<uint32_t*>(drow + x0) = packed;  // pitch is a multiple of 64
+            if (copy_rows)
+              *reinterpret_cast<uint32_t*>(copy_rows + (dy0 + nd - copy_row0) * D.pitch + x0) =
+                  packed;
           } else {
             for (int k = 0; x0 + k < D.w; k++) drow[x0 + k] = (uint8_t)(packed >> (8 * k));
+            if (copy_rows) {
+              uint8_t* crow = copy_rows + (dy0 + nd - copy_row0) * D.pitch;
+              for (int k = 0; x0 + k < D.w; k++) crow[x0 + k] = (uint8_t)(packed >> (8 * k));
+            }
           }
           nd++;
         }
@@ -191,6 +206,37 @@ __global__ __launch_bounds__(256) void pyr_down_kernel(ImageBatch b, const OrbGe
   const int tiles_x = (g->lv[level].w + 255) >> 8;
   const int tx = bx % tiles_x, ty = bx / tiles_x;
   pyr_strip<kAligned, kStrip>(b, g, level, img, tx, (ty * 4 + wave_id()) * kStrip, rxt, ryt);
+}
+
+// Small launches (the single-frame call): levels 2 .. nlevels - 1 in one launch of row bands
+// (g->pyr_band, geometry): band s computes its rows of each level -- its share plus the source
+// rows its next level needs, so it reads only rows it wrote itself (halo rows are computed by
+// two bands with the same bytes) -- its 16 waves spread over the level's (tile, strip) tasks,
+// a work-group barrier between levels. One launch instead of nlevels - 2 dependent ones (~5 us
+// each on the call's critical path), with the levels' work still spread over many CUs.
+// The band's rows of each level also go to LDS (two buffers of g->pyr_band_lds bytes, rows at
+// the level's pitch), where the next level reads them: one global round trip (level 1) per band.
+constexpr int kPyrBandWaves = 16;
+__global__ __launch_bounds__(64 * kPyrBandWaves) void pyr_band_kernel(
+    ImageBatch b, const OrbGeom* __restrict__ g, const ResizeX* __restrict__ rxt,
+    const ResizeY* __restrict__ ryt) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t s_band[];
+  const int band = blockIdx.x, img = blockIdx.y, wid = wave_id();
+  const int half = g->pyr_band_lds;
+  for (int l = 2; l < g->nlevels; l++) {
+    const int r0 = g->pyr_band[band][l][0], r1 = g->pyr_band[band][l][1];
+    const int tiles = (g->lv[l].w + 255) >> 8;
+    const int chunks = (r1 - r0 + kPyrShortStrip - 1) / kPyrShortStrip;
+    uint8_t* out = s_band + (l & 1) * half;
+    const uint8_t* in = l > 2 ? s_band + ((l - 1) & 1) * half : nullptr;
+    const int in_row0 = l > 2 ? g->pyr_band[band][l - 1][0] : 0;
+    for (int t = wid; t < tiles * chunks; t += kPyrBandWaves) {
+      const int tx = t % tiles, dy0 = r0 + (t / tiles) * kPyrShortStrip;
+      pyr_strip<true, kPyrShortStrip>(b, g, l, img, tx, dy0, rxt, ryt, r1 - dy0, in, in_row0, out,
+                                      r0);
+    }
+    __syncthreads();  // this level's rows (LDS) before the next level reads them
+  }
 }
 
 // ---------------------------------------------------------------------------------------
@@ -2621,7 +2667,10 @@ void launch_extract(const ImageBatch& b, const OrbGeomDev& gd, int n_images, hip
                       reinterpret_cast<uintptr_t>(b.pyr) | (uintptr_t)g.pyr_bytes) & 15) == 0;
   // FAST of level 0 reads only the caller's images: with a second side stream it runs beside
   // the pyramid (whose small levels leave the chip mostly idle)
-  const bool split0 = fx.side0 && fx.fork0 && fx.join0 && g.nlevels > 1;
+  // (batches only: in the single-frame call the join's cross-queue dependency costs more than
+  // the overlap saves -- 0.296 -> 0.276 ms per call without it, profiles/r4w_lat_ab.log)
+  const bool split0 = fx.side0 && fx.fork0 && fx.join0 && g.nlevels > 1 &&
+                      n_images > kPyrShortMaxImages;
   if (split0) {
     (void)hipEventRecord(fx.fork0, st);
     (void)hipStreamWaitEvent(fx.side0, fx.fork0, 0);
@@ -2654,7 +2703,9 @@ void launch_extract(const ImageBatch& b, const OrbGeomDev& gd, int n_images, hip
   const bool in_aligned = (((uintptr_t)b.in_l | (uintptr_t)b.in_r | (uintptr_t)b.in_stride |
                            (uintptr_t)b.in_pitch) & 3) == 0;
   const bool short_strips = n_images <= kPyrShortMaxImages;
-  for (int l = 1; l < g.nlevels; l++) {
+  // small launches: level 1 over the chip, then levels 2+ in one launch of row bands
+  const int l_end = (short_strips && g.pyr_bands > 0) ? 2 : g.nlevels;
+  for (int l = 1; l < l_end; l++) {
     const int strip = short_strips ? kPyrShortStrip : kPyrStrip;
     const int tiles = ((g.lv[l].w + 255) >> 8) * ((g.lv[l].h + 4 * strip - 1) / (4 * strip));
     const dim3 grid(tiles, n_images);
@@ -2673,6 +2724,10 @@ void launch_extract(const ImageBatch& b, const OrbGeomDev& gd, int n_images, hip
                      b, gd.dev, l, gd.rx, gd.ry);
     }
   }
+  if (l_end < g.nlevels)
+    SLAMGPU_LAUNCH("pyr_down", st, pyr_band_kernel, dim3(g.pyr_bands, n_images),
+                   dim3(64 * kPyrBandWaves), 2 * (size_t)g.pyr_band_lds, st, b, gd.dev, gd.rx,
+                   gd.ry);
   {
     const dim3 block(64 * kCellWaves);
     const size_t lds = (size_t)kCellWaves * g.fast_lds_per_wave;

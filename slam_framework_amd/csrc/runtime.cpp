@@ -427,7 +427,8 @@ static int run_frontend(slamgpu_ctx* c, const ImageBatch& b, int n_frames, int n
     // 96, 110; stereo matching reads the distorted ones): on the side stream beside
     // ComputeStereoMatches, joined after it -- two fewer launches on the call's critical path
     const ExtractStreams& fx = c->fx;
-    const bool fork = fx.side0 && fx.fork1 && fx.join1;
+    // (batches only, as launch_extract's level-0 FAST fork: a small launch's join costs more)
+    const bool fork = fx.side0 && fx.fork1 && fx.join1 && n_frames > 8;
     hipStream_t gs = fork ? fx.side0 : st;
     if (fork) {
       HIPCHECK(c, hipEventRecord(fx.fork1, st));
