@@ -51,7 +51,7 @@ void launch_frame_pack(const FrameKps& ext, const float* u_right, const float* d
 // pack: the single-frame call's packed record (frame 0's u_right / depth go there too), or null
 void launch_stereo(const ImageBatch& b, const OrbGeomDev& g, const Camera& cam, int n_frames,
                    const StereoWorkspace& ws, const StereoOut& out, hipStream_t st,
-                   uint8_t* pack = nullptr);
+                   uint8_t* pack = nullptr, bool rows_done = false);
 
 // Frame::UndistortKeyPoints of n_sets keypoint sets (set f: src.kps + f * src.stride, count
 // src.n[f * src.n_stride]) into dst + f * dst_stride.
@@ -122,6 +122,12 @@ struct MatchIO {
 
 void launch_grid(const FrameKps& cur, const Camera& cam, int n_frames, int kp_cap,
                  const GridWorkspace& gw, hipStream_t st);
+// One frame (the single-frame call): the stereo row tables, the left view's grid and the packing
+// of counts / keypoints / descriptors into `pack`, as three work-groups of one launch; then
+// launch_stereo(..., rows_done = true).
+void launch_frame_aux(const OrbGeomDev& g, const FrameKps& left, const Camera& cam,
+                      const GridWorkspace& gw, const StereoWorkspace& ws, uint8_t* pack,
+                      hipStream_t st);
 
 void launch_search_frame(const FrameKps& cur, const float* u_right, int64_t ur_stride,
                          const Camera& cam, const OrbGeomDev& g, const F2FQuery* queries,

@@ -98,13 +98,13 @@ constexpr int kMaxRows = 2048;
 // NT threads per frame: 256 for batches, 1024 for the single-frame call (its one work-group is
 // the whole launch: a quarter of the serial LDS-atomic loops per thread).
 template <int NT>
-__global__ __launch_bounds__(NT) void stereo_rows_kernel(const OrbGeom* __restrict__ g,
-                                                         FrameKps ext, int nrows,
-                                                         StereoWorkspace ws,
-                                                         uint32_t* __restrict__ err) {
+__device__ __forceinline__ void stereo_rows_body(int f, const OrbGeom* __restrict__ g,
+                                                 const FrameKps& ext, int nrows,
+                                                 const StereoWorkspace& ws,
+                                                 uint32_t* __restrict__ err) {
   __shared__ int cnt[kMaxRows + 1];
   __shared__ int wsum[NT / 64];
-  const int f = blockIdx.x, tid = threadIdx.x;
+  const int tid = threadIdx.x;
   const int ir = 2 * f + 1;
   const KeyPoint* kr = ext.kps + ir * ext.stride;
   const int nr = ext.n[ir * ext.n_stride];
@@ -164,6 +164,14 @@ __global__ __launch_bounds__(NT) void stereo_rows_kernel(const OrbGeom* __restri
         if (pos < ws.row_cap) items[pos] = base + NT * u + tid;
       }
   }
+}
+
+template <int NT>
+__global__ __launch_bounds__(NT) void stereo_rows_kernel(const OrbGeom* __restrict__ g,
+                                                         FrameKps ext, int nrows,
+                                                         StereoWorkspace ws,
+                                                         uint32_t* __restrict__ err) {
+  stereo_rows_body<NT>(blockIdx.x, g, ext, nrows, ws, err);
 }
 
 // One left keypoint per G lanes (G = 32: two per wave; G = 16: four): the kernel is a chain of
@@ -478,13 +486,12 @@ __global__ __launch_bounds__(NT) void stereo_median_kernel(const OrbGeom* __rest
 // parts: bit 0 -- the counts, both views' keypoints and descriptors, the error word to header
 // slot 12; bit 1 -- u_right / depth, the error word to slot 8 (stereo_median_kernel does this part
 // itself in the single-frame call). The host ORs the two error slots.
-__global__ __launch_bounds__(256) void frame_pack_kernel(FrameKps ext,
-                                                         const float* __restrict__ u_right,
-                                                         const float* __restrict__ depth,
-                                                         const uint32_t* __restrict__ err,
-                                                         int kp_cap, uint8_t* __restrict__ dst,
-                                                         int parts) {
-  const int gid = blockIdx.x * blockDim.x + threadIdx.x, gsz = gridDim.x * blockDim.x;
+__device__ __forceinline__ void frame_pack_body(const FrameKps& ext,
+                                                const float* __restrict__ u_right,
+                                                const float* __restrict__ depth,
+                                                const uint32_t* __restrict__ err, int kp_cap,
+                                                uint8_t* __restrict__ dst, int parts, int gid,
+                                                int gsz) {
   const int c0 = ext.n[0], c1 = ext.n[ext.n_stride];
   const int n0 = min(max(c0, 0), kp_cap), n1 = min(max(c1, 0), kp_cap);
   const size_t kc = (size_t)kp_cap;
@@ -515,6 +522,15 @@ __global__ __launch_bounds__(256) void frame_pack_kernel(FrameKps ext,
     copy(depth, dp_off, n0);
   }
 }
+__global__ __launch_bounds__(256) void frame_pack_kernel(FrameKps ext,
+                                                         const float* __restrict__ u_right,
+                                                         const float* __restrict__ depth,
+                                                         const uint32_t* __restrict__ err,
+                                                         int kp_cap, uint8_t* __restrict__ dst,
+                                                         int parts) {
+  frame_pack_body(ext, u_right, depth, err, kp_cap, dst, parts,
+                  blockIdx.x * blockDim.x + threadIdx.x, gridDim.x * blockDim.x);
+}
 
 void launch_frame_pack(const FrameKps& ext, const float* u_right, const float* depth,
                        const uint32_t* err, int kp_cap, uint8_t* dst, hipStream_t st, int parts) {
@@ -531,11 +547,12 @@ void launch_trace_marker(int id, hipStream_t st) {
 
 void launch_stereo(const ImageBatch& b, const OrbGeomDev& gd, const Camera& cam, int n_frames,
                    const StereoWorkspace& ws, const StereoOut& out, hipStream_t st,
-                   uint8_t* pack) {
+                   uint8_t* pack, bool rows_done) {
   const OrbGeom& g = *gd.host;
   FrameKps ext{gd.out.kps, gd.out.desc, gd.out.nkps, g.kp_cap, 1};
   const int nrows = g.lv[0].h;
-  if (n_frames <= 8)
+  if (rows_done) {  // frame_aux_kernel built them
+  } else if (n_frames <= 8)
     SLAMGPU_LAUNCH("stereo_rows", st, stereo_rows_kernel<1024>, dim3(n_frames), dim3(1024), 0, st,
                    gd.dev, ext, nrows, ws, gd.ws.err);
   else
@@ -562,23 +579,24 @@ __device__ __forceinline__ int grid_cell(const Camera& cam, float x, float y) {
   return px * kGridRows + py;
 }
 
-__global__ __launch_bounds__(256) void grid_build_kernel(FrameKps cur, Camera cam, int kp_cap,
-                                                         GridWorkspace gw) {
+template <int NT>
+__device__ __forceinline__ void grid_build_body(int f, const FrameKps& cur, const Camera& cam,
+                                                int kp_cap, const GridWorkspace& gw) {
   __shared__ int cnt[kGridCells + 1];
-  __shared__ int wsum[4];
-  const int f = blockIdx.x, tid = threadIdx.x;
+  __shared__ int wsum[NT / 64];
+  const int tid = threadIdx.x;
   const KeyPoint* k = cur.kps + f * cur.stride;
   const int n = cur.n[f * cur.n_stride];
   int* cs = gw.cell_start + (int64_t)f * (kGridCells + 1);
   int* items = gw.cell_items + (int64_t)f * kp_cap;
-  for (int i = tid; i <= kGridCells; i += 256) cnt[i] = 0;
+  for (int i = tid; i <= kGridCells; i += NT) cnt[i] = 0;
   // cells of a thread's keypoints, kChunk loads in flight at a time
-  constexpr int kChunk = 8;
+  constexpr int kChunk = 2048 / NT;
   auto cells = [&](int base, int (&c)[kChunk]) {
     float kx[kChunk], ky[kChunk];
 #pragma unroll
     for (int u = 0; u < kChunk; u++) {
-      const int i = base + 256 * u + tid;
+      const int i = base + NT * u + tid;
       kx[u] = ky[u] = 0.0f;
       if (i < n) {
         kx[u] = k[i].x;
@@ -587,10 +605,10 @@ __global__ __launch_bounds__(256) void grid_build_kernel(FrameKps cur, Camera ca
     }
 #pragma unroll
     for (int u = 0; u < kChunk; u++)
-      c[u] = base + 256 * u + tid < n ? grid_cell(cam, kx[u], ky[u]) : -1;
+      c[u] = base + NT * u + tid < n ? grid_cell(cam, kx[u], ky[u]) : -1;
   };
   __syncthreads();
-  for (int base = 0; base < n; base += 256 * kChunk) {
+  for (int base = 0; base < n; base += NT * kChunk) {
     int c[kChunk];
     cells(base, c);
 #pragma unroll
@@ -598,22 +616,53 @@ __global__ __launch_bounds__(256) void grid_build_kernel(FrameKps cur, Camera ca
       if (c[u] >= 0) atomicAdd(&cnt[c[u]], 1);
   }
   __syncthreads();
-  const int total = scan256<kGridCells + 1>(cnt, kGridCells, wsum);
-  for (int i = tid; i < kGridCells; i += 256) cs[i] = cnt[i];
+  const int total = scan256<kGridCells + 1, NT>(cnt, kGridCells, wsum);
+  for (int i = tid; i < kGridCells; i += NT) cs[i] = cnt[i];
   if (tid == 0) cs[kGridCells] = total;
   __syncthreads();
-  for (int base = 0; base < n; base += 256 * kChunk) {
+  for (int base = 0; base < n; base += NT * kChunk) {
     int c[kChunk];
     cells(base, c);
 #pragma unroll
     for (int u = 0; u < kChunk; u++)
-      if (c[u] >= 0) items[atomicAdd(&cnt[c[u]], 1)] = base + 256 * u + tid;
+      if (c[u] >= 0) items[atomicAdd(&cnt[c[u]], 1)] = base + NT * u + tid;
   }
+}
+__global__ __launch_bounds__(256) void grid_build_kernel(FrameKps cur, Camera cam, int kp_cap,
+                                                         GridWorkspace gw) {
+  grid_build_body<256>(blockIdx.x, cur, cam, kp_cap, gw);
 }
 
 void launch_grid(const FrameKps& cur, const Camera& cam, int n_frames, int kp_cap,
                  const GridWorkspace& gw, hipStream_t st) {
-  SLAMGPU_LAUNCH("grid_build", st, grid_build_kernel, dim3(n_frames), dim3(256), 0, st, cur, cam, kp_cap, gw);
+  SLAMGPU_LAUNCH("grid_build", st, grid_build_kernel, dim3(n_frames), dim3(256), 0, st, cur, cam,
+                 kp_cap, gw);
+}
+
+// The single-frame call's three independent steps after the descriptors, as three work-groups
+// of one launch (side by side on three CUs): blockIdx.y 0 the stereo row tables, 1 the left
+// view's grid, 2 the counts / keypoints / descriptors packed into the host mirror.
+__global__ __launch_bounds__(1024) void frame_aux_kernel(const OrbGeom* __restrict__ g,
+                                                         FrameKps ext, int nrows,
+                                                         StereoWorkspace ws, uint32_t* err,
+                                                         FrameKps left, Camera cam, int kp_cap,
+                                                         GridWorkspace gw, uint8_t* pack) {
+  switch (blockIdx.y) {
+    case 0: stereo_rows_body<1024>(0, g, ext, nrows, ws, err); break;
+    case 1: grid_build_body<1024>(0, left, cam, kp_cap, gw); break;
+    default:
+      frame_pack_body(ext, nullptr, nullptr, err, kp_cap, pack, 1, threadIdx.x, 1024);
+      break;
+  }
+}
+
+void launch_frame_aux(const OrbGeomDev& gd, const FrameKps& left, const Camera& cam,
+                      const GridWorkspace& gw, const StereoWorkspace& ws, uint8_t* pack,
+                      hipStream_t st) {
+  const OrbGeom& g = *gd.host;
+  FrameKps ext{gd.out.kps, gd.out.desc, gd.out.nkps, g.kp_cap, 1};
+  SLAMGPU_LAUNCH("frame_aux", st, frame_aux_kernel, dim3(1, 3), dim3(1024), 0, st, gd.dev, ext,
+                 g.lv[0].h, ws, gd.ws.err, left, cam, g.kp_cap, gw, pack);
 }
 
 // ---------------------------------------------------------------------------------------

@@ -438,11 +438,18 @@ static int run_frontend(slamgpu_ctx* c, const ImageBatch& b, int n_frames, int n
       launch_undistort(FrameKps{c->out.kps, c->out.desc, c->out.nkps, 2 * (int64_t)c->geom.kp_cap, 2},
                        c->kps_un, 2 * (int64_t)c->geom.kp_cap, c->cam, c->dist, n_frames,
                        c->geom.kp_cap, gs);
-    launch_grid(left_views(c), c->cam, n_frames, c->geom.kp_cap, c->gws, gs);
-    if (pack)
-      launch_frame_pack(FrameKps{c->out.kps, c->out.desc, c->out.nkps, c->geom.kp_cap, 1},
-                        c->sout.u_right, c->sout.depth, c->ws.err, c->geom.kp_cap, pack, gs, 1);
-    launch_stereo(b, g, c->cam, n_frames, c->sws, c->sout, st, pack);
+    // one frame with a host mirror (the single-frame call): row tables, grid and packing as
+    // three work-groups of one launch, side by side
+    const bool aux = pack && n_frames == 1 && !fork;
+    if (aux) {
+      launch_frame_aux(g, left_views(c), c->cam, c->gws, c->sws, pack, st);
+    } else {
+      launch_grid(left_views(c), c->cam, n_frames, c->geom.kp_cap, c->gws, gs);
+      if (pack)
+        launch_frame_pack(FrameKps{c->out.kps, c->out.desc, c->out.nkps, c->geom.kp_cap, 1},
+                          c->sout.u_right, c->sout.depth, c->ws.err, c->geom.kp_cap, pack, gs, 1);
+    }
+    launch_stereo(b, g, c->cam, n_frames, c->sws, c->sout, st, pack, aux);
     if (fork) {
       HIPCHECK(c, hipEventRecord(fx.join1, gs));
       HIPCHECK(c, hipStreamWaitEvent(st, fx.join1, 0));
@@ -471,6 +478,30 @@ static int stage_images(slamgpu_ctx* c, const uint8_t* const* imgs, int n, size_
   stage_host(c, imgs, n, step);
   HIPCHECK(c, hipMemcpyAsync(c->d_in, c->h_in, (size_t)n * c->in_stride, hipMemcpyHostToDevice,
                              c->stream));
+  return 0;
+}
+// The same, pipelined for the single-frame call: each image in two row halves, a half's DMA
+// issued as soon as its rows are packed, so the host's packing of the next half runs under it
+// (the packing is the larger part: ~933 KB of row copies against ~23 us of DMA).
+static int stage_images_pipelined(slamgpu_ctx* c, const uint8_t* const* imgs, int n,
+                                  size_t step) {
+  const int cols = c->geom.cols, rows = c->geom.rows, pitch = c->in_pitch;
+  for (int i = 0; i < n; i++) {
+    uint8_t* dst = c->h_in + i * c->in_stride;
+    for (int part = 0; part < 2; part++) {
+      const int y0 = part ? rows / 2 : 0, y1 = part ? rows : rows / 2;
+      if (step == (size_t)pitch) {
+        std::memcpy(dst + (int64_t)y0 * pitch, imgs[i] + (int64_t)y0 * pitch,
+                    (size_t)(y1 - y0 - 1) * pitch + cols);
+      } else {
+        for (int y = y0; y < y1; y++)
+          std::memcpy(dst + (int64_t)y * pitch, imgs[i] + y * step, cols);
+      }
+      const size_t off = (size_t)i * c->in_stride + (size_t)y0 * pitch;
+      HIPCHECK(c, hipMemcpyAsync(c->d_in + off, c->h_in + off, (size_t)(y1 - y0) * pitch,
+                                 hipMemcpyHostToDevice, c->stream));
+    }
+  }
   return 0;
 }
 
@@ -547,9 +578,8 @@ int slamgpu_debug_level_keys(slamgpu_ctx* c, int img, int level, int stage, uint
 
 // The device half of slamgpu_frame_stereo on c->stream: the staged pair's DMA, the frontend,
 // then the frame's results and the device error word into the pinned mirror.
+// (the images are already on their way: stage_images_pipelined, before this)
 static int enqueue_frame_stereo(slamgpu_ctx* c) {
-  HIPCHECK(c, hipMemcpyAsync(c->d_in, c->h_in, 2 * (size_t)c->in_stride, hipMemcpyHostToDevice,
-                             c->stream));
   ImageBatch b{c->d_in, c->d_in + c->in_stride, 2 * c->in_stride, c->in_pitch, c->d_pyr};
   if (int rc = run_frontend(c, b, 1, 2, true, c->stream, c->d_res)) return rc;
   HIPCHECK(c, hipMemcpyAsync(c->h_res, c->d_res, res_mirror_bytes(c->geom.kp_cap),
@@ -619,7 +649,7 @@ int slamgpu_frame_stereo(slamgpu_ctx* c, const uint8_t* left, const uint8_t* rig
   HIPCHECK(c, hipSetDevice(c->device));
   set_camera(c, cam);
   const uint8_t* imgs[2] = {left, right};
-  stage_host(c, imgs, 2, step);
+  if (int r = stage_images_pipelined(c, imgs, 2, step)) return r;
   // kernel timing records events around each launch: those calls stay eager
   const int rc = frame_graph_enabled() && !c->timer.on ? launch_frame_graph(c)
                                                        : enqueue_frame_stereo(c);
