@@ -170,12 +170,12 @@ int compute_geometry(const OrbParams& p, int cols, int rows, OrbGeom* g,
     }
   }
   g->cells_per_image = cell_base;
-  {  // pyr_band_kernel's row bands, top-down from the last level to level 1
+  {  // pyr_band_kernel's row bands, top-down from the last level
     const int nb = p.nlevels > 2 ? std::min(std::max(g->lv[2].h / 12, 1), kPyrMaxBands) : 0;
     g->pyr_bands = nb;
     std::memset(g->pyr_band, 0, sizeof(g->pyr_band));
     for (int s = 0; s < nb; s++) {
-      for (int l = p.nlevels - 1; l >= 1; l--) {
+      for (int l = p.nlevels - 1; l >= 2; l--) {
         const int h = g->lv[l].h;
         int lo = (int)((int64_t)s * h / nb), hi = (int)((int64_t)(s + 1) * h / nb);
         if (l + 1 < p.nlevels) {
@@ -192,7 +192,7 @@ int compute_geometry(const OrbParams& p, int cols, int rows, OrbGeom* g,
     }
     int lds = 0;
     for (int s = 0; s < nb; s++)
-      for (int l = 1; l < p.nlevels; l++)
+      for (int l = 2; l < p.nlevels; l++)
         lds = std::max(lds, (g->pyr_band[s][l][1] - g->pyr_band[s][l][0]) * g->lv[l].pitch);
     g->pyr_band_lds = (lds + 15) & ~15;
     if (2 * g->pyr_band_lds > 64 * 1024) g->pyr_bands = 0;  // per-level launches instead

@@ -81,8 +81,8 @@ struct OrbGeom {
   int kp_cap;            // max keypoints per image after Compute (== out_per_image)
   int umax[16];
   LevelGeom lv[kMaxLevels];
-  // pyr_band_kernel (levels 1 or 2 .. nlevels - 1 in one launch): band s computes rows
-  // [pyr_band[s][l][0], pyr_band[s][l][1]) of level l -- its share of the level plus every
+  // pyr_band_kernel (small launches: levels 2 .. nlevels - 1 in one launch): band s computes
+  // rows [pyr_band[s][l][0], pyr_band[s][l][1]) of level l -- its share of the level plus every
   // source row its own next level needs (so a band reads only rows it wrote itself)
   int pyr_bands;
   int pyr_band_lds;  // bytes of one of its two LDS row buffers (the largest band level)

@@ -208,37 +208,32 @@ __global__ __launch_bounds__(256) void pyr_down_kernel(ImageBatch b, const OrbGe
   pyr_strip<kAligned, kStrip>(b, g, level, img, tx, (ty * 4 + wave_id()) * kStrip, rxt, ryt);
 }
 
-// Levels lo .. nlevels - 1 in one launch of row bands (g->pyr_band, geometry): band s computes
-// its rows of each level -- its share plus the source rows its next level needs, so it reads
-// only rows it wrote itself (halo rows are computed by two bands with the same bytes) -- its 16
-// waves spread over the level's (tile, strip) tasks, a work-group barrier between levels. The
-// band's rows also go to LDS (two buffers of g->pyr_band_lds bytes, rows at the level's pitch),
-// where its next level reads them: level lo reads its source from memory, the rest never does.
-// lo = 2 for the single-frame call (level 1 runs over the whole chip first), 1 for batches (the
-// caller's images are read once; levels 1-6 are not read back from HBM).
+// Small launches (the single-frame call): levels 2 .. nlevels - 1 in one launch of row bands
+// (g->pyr_band, geometry): band s computes its rows of each level -- its share plus the source
+// rows its next level needs, so it reads only rows it wrote itself (halo rows are computed by
+// two bands with the same bytes) -- its 16 waves spread over the level's (tile, strip) tasks,
+// a work-group barrier between levels. One launch instead of nlevels - 2 dependent ones (~5 us
+// each on the call's critical path), with the levels' work still spread over many CUs.
+// The band's rows of each level also go to LDS (two buffers of g->pyr_band_lds bytes, rows at
+// the level's pitch), where the next level reads them: one global round trip (level 1) per band.
 constexpr int kPyrBandWaves = 16;
-template <bool kAligned1>
 __global__ __launch_bounds__(64 * kPyrBandWaves) void pyr_band_kernel(
     ImageBatch b, const OrbGeom* __restrict__ g, const ResizeX* __restrict__ rxt,
-    const ResizeY* __restrict__ ryt, int lo) {
+    const ResizeY* __restrict__ ryt) {
   extern __shared__ __attribute__((aligned(16))) uint8_t s_band[];
   const int band = blockIdx.x, img = blockIdx.y, wid = wave_id();
   const int half = g->pyr_band_lds;
-  for (int l = lo; l < g->nlevels; l++) {
+  for (int l = 2; l < g->nlevels; l++) {
     const int r0 = g->pyr_band[band][l][0], r1 = g->pyr_band[band][l][1];
     const int tiles = (g->lv[l].w + 255) >> 8;
     const int chunks = (r1 - r0 + kPyrShortStrip - 1) / kPyrShortStrip;
     uint8_t* out = s_band + (l & 1) * half;
-    const uint8_t* in = l > lo ? s_band + ((l - 1) & 1) * half : nullptr;
-    const int in_row0 = l > lo ? g->pyr_band[band][l - 1][0] : 0;
+    const uint8_t* in = l > 2 ? s_band + ((l - 1) & 1) * half : nullptr;
+    const int in_row0 = l > 2 ? g->pyr_band[band][l - 1][0] : 0;
     for (int t = wid; t < tiles * chunks; t += kPyrBandWaves) {
       const int tx = t % tiles, dy0 = r0 + (t / tiles) * kPyrShortStrip;
-      if (l == 1)
-        pyr_strip<kAligned1, kPyrShortStrip>(b, g, l, img, tx, dy0, rxt, ryt, r1 - dy0, in,
-                                             in_row0, out, r0);
-      else
-        pyr_strip<true, kPyrShortStrip>(b, g, l, img, tx, dy0, rxt, ryt, r1 - dy0, in, in_row0,
-                                        out, r0);
+      pyr_strip<true, kPyrShortStrip>(b, g, l, img, tx, dy0, rxt, ryt, r1 - dy0, in, in_row0, out,
+                                      r0);
     }
     __syncthreads();  // this level's rows (LDS) before the next level reads them
   }
@@ -2708,14 +2703,8 @@ void launch_extract(const ImageBatch& b, const OrbGeomDev& gd, int n_images, hip
   const bool in_aligned = (((uintptr_t)b.in_l | (uintptr_t)b.in_r | (uintptr_t)b.in_stride |
                            (uintptr_t)b.in_pitch) & 3) == 0;
   const bool short_strips = n_images <= kPyrShortMaxImages;
-  // small launches: level 1 over the chip, then levels 2+ in one launch of row bands; batches:
-  // per-level launches (SLAMGPU_PYR_BANDS=1: levels 1+ in one launch of row bands, A/B)
-  static const bool bands_batch = [] {
-    const char* e = std::getenv("SLAMGPU_PYR_BANDS");
-    return e && e[0] == '1';
-  }();
-  const bool band_all = !short_strips && bands_batch && g.pyr_bands > 0;
-  const int l_end = band_all ? 1 : (short_strips && g.pyr_bands > 0) ? 2 : g.nlevels;
+  // small launches: level 1 over the chip, then levels 2+ in one launch of row bands
+  const int l_end = (short_strips && g.pyr_bands > 0) ? 2 : g.nlevels;
   for (int l = 1; l < l_end; l++) {
     const int strip = short_strips ? kPyrShortStrip : kPyrStrip;
     const int tiles = ((g.lv[l].w + 255) >> 8) * ((g.lv[l].h + 4 * strip - 1) / (4 * strip));
@@ -2735,16 +2724,10 @@ void launch_extract(const ImageBatch& b, const OrbGeomDev& gd, int n_images, hip
                      b, gd.dev, l, gd.rx, gd.ry);
     }
   }
-  if (l_end < g.nlevels) {
-    const size_t lds = 2 * (size_t)g.pyr_band_lds;
-    const dim3 grid(g.pyr_bands, n_images), block(64 * kPyrBandWaves);
-    if (l_end > 1 || in_aligned)
-      SLAMGPU_LAUNCH("pyr_down", st, pyr_band_kernel<true>, grid, block, lds, st, b, gd.dev, gd.rx,
-                     gd.ry, l_end);
-    else
-      SLAMGPU_LAUNCH("pyr_down", st, pyr_band_kernel<false>, grid, block, lds, st, b, gd.dev,
-                     gd.rx, gd.ry, l_end);
-  }
+  if (l_end < g.nlevels)
+    SLAMGPU_LAUNCH("pyr_down", st, pyr_band_kernel, dim3(g.pyr_bands, n_images),
+                   dim3(64 * kPyrBandWaves), 2 * (size_t)g.pyr_band_lds, st, b, gd.dev, gd.rx,
+                   gd.ry);
   {
     const dim3 block(64 * kCellWaves);
     const size_t lds = (size_t)kCellWaves * g.fast_lds_per_wave;
