@@ -289,8 +289,10 @@ __global__ __launch_bounds__(kFacThreads) void eg_factor_solve_kernel(EgGraph G,
       d = bcast(d, j);
       dm[j] = d;
       ok = ok && d != 0.0;
+#if !EG_EXACT_ROUNDING  // the pivot reciprocals serve the tolerance-compared path only
       const double rdj = 1.0 / d;
       if (r == j) my_rd = rdj;
+#endif
       double t = a[j];  // lanes i > j: L_ij
 #pragma unroll
       for (int m = 0; m < j; m++) t -= a[m] * bcast(a[m], j) * dm[m];
