@@ -52,6 +52,25 @@ constexpr int kNH = 21;  // upper triangle of the 6x6 H
 constexpr int kPoseLatencyFrames = 64;
 constexpr int kPoseLdsEdges = 4096;  // edges of one frame the 1- and 8-wave variants take
 
+// Tolerance-compared path: 1 / x and 1 / sqrt(x) from the hardware estimates (v_rcp_f64,
+// v_rsq_f64) and two Newton steps -- within an ulp or two -- instead of the IEEE division and
+// square-root expansions, for the solve's and the update's dependent chain (x > 0, finite).
+__device__ __forceinline__ double rcp_nr(double x) {
+  double y = __builtin_amdgcn_rcp(x);
+  double e = __builtin_fma(-x, y, 1.0);
+  y = __builtin_fma(y, e, y);
+  e = __builtin_fma(-x, y, 1.0);
+  return __builtin_fma(y, e, y);
+}
+__device__ __forceinline__ double rsq_nr(double x) {
+  double y = __builtin_amdgcn_rsq(x);
+  const double h = 0.5 * x;
+  double r = __builtin_fma(-h * y, y, 0.5);  // y <- y (1.5 - x y^2 / 2), twice
+  y = __builtin_fma(y, r, y);
+  r = __builtin_fma(-h * y, y, 0.5);
+  return __builtin_fma(y, r, y);
+}
+
 // H x = b for the 6x6 H + lambda I, LDLT without pivoting; a zero pivot gives a zero component
 // (Eigen's rule), a negative one fails the solve (LinearSolverDense::solve returns false and
 // g2o applies the previous x). One reciprocal per pivot, and the unscaled column entries
@@ -66,7 +85,7 @@ __device__ bool ldlt_solve6(const double H[kNH], double lambda, const double b[6
 #pragma unroll
     for (int k = 0; k < j; k++) dj -= L[j][k] * D[j][k];
     if (dj < 0) return false;
-    id[j] = dj > DBL_MIN ? 1.0 / dj : 0.0;
+    id[j] = dj > DBL_MIN ? rcp_nr(dj) : 0.0;
 #pragma unroll
     for (int i = j + 1; i < 6; i++) {
       double s = H[j * 6 - (j * (j - 1)) / 2 + (i - j)];  // H(j, i) = H(i, j)
@@ -109,7 +128,7 @@ __device__ __forceinline__ void pose_normalize(Quat& q) {
     q.z = -q.z;
     q.w = -q.w;
   }
-  const double in = 1.0 / sqrt(q.x * q.x + q.y * q.y + q.z * q.z + q.w * q.w);
+  const double in = rsq_nr(q.x * q.x + q.y * q.y + q.z * q.z + q.w * q.w);
   q.x *= in;
   q.y *= in;
   q.z *= in;
@@ -118,8 +137,7 @@ __device__ __forceinline__ void pose_normalize(Quat& q) {
 __device__ __forceinline__ SE3 pose_left_update(const double u[6], const SE3& T) {
 #pragma clang fp contract(fast)
   const double w0 = u[0], w1 = u[1], w2 = u[2];
-  const double t2 = w0 * w0 + w1 * w1 + w2 * w2;
-  const double th = sqrt(t2);
+  const double t2 = w0 * w0 + w1 * w1 + w2 * w2;  // theta^2: the branches test it, not theta
   const double O[9] = {0, -w2, w1, w2, 0, -w0, -w1, w0, 0};
   double O2[9];
 #pragma unroll
@@ -128,8 +146,8 @@ __device__ __forceinline__ SE3 pose_left_update(const double u[6], const SE3& T)
     for (int j = 0; j < 3; j++)
       O2[3 * i + j] = O[3 * i] * O[j] + O[3 * i + 1] * O[3 + j] + O[3 * i + 2] * O[6 + j];
   double a = 1.0, b = 1.0, c = 1.0;
-  if (!(th < 0.00001)) {
-    if (th < 0.01) {
+  if (!(t2 < 1e-10)) {
+    if (t2 < 1e-4) {
       // Horner in t^2 with constant reciprocals (multiplications, not divisions)
       constexpr double k6 = 1.0 / 6, k12 = 1.0 / 12, k20 = 1.0 / 20, k30 = 1.0 / 30;
       constexpr double k42 = 1.0 / 42, k56 = 1.0 / 56, k72 = 1.0 / 72, k90 = 1.0 / 90;
@@ -138,9 +156,10 @@ __device__ __forceinline__ SE3 pose_left_update(const double u[6], const SE3& T)
       b = 0.5 * (1.0 - t2 * k12 * (1.0 - t2 * k30 * (1.0 - t2 * k56 * (1.0 - t2 * k90))));
       c = k6 * (1.0 - t2 * k20 * (1.0 - t2 * k42 * (1.0 - t2 * k72 * (1.0 - t2 * k110))));
     } else {
+      const double th = sqrt(t2);
       double s, co;
       sincos(th, &s, &co);
-      const double it = 1.0 / th;
+      const double it = rcp_nr(th);
       a = s * it;
       b = (1 - co) * it * it;
       c = (th - s) * it * it * it;
@@ -156,7 +175,16 @@ __device__ __forceinline__ SE3 pose_left_update(const double u[6], const SE3& T)
   SE3 E;
 #pragma unroll
   for (int i = 0; i < 3; i++) E.t[i] = V[3 * i] * u[3] + V[3 * i + 1] * u[4] + V[3 * i + 2] * u[5];
-  E.r = quat_from_R(R);
+  const double tr = R[0] + R[4] + R[8];
+  if (tr > 0.0) {  // quat_from_R's first branch (a tracked frame's step), sqrt and 0.5 / t by rsq
+    const double sq = tr + 1.0, rq = rsq_nr(sq), h = 0.5 * rq;
+    E.r.w = 0.5 * (sq * rq);
+    E.r.x = (R[7] - R[5]) * h;
+    E.r.y = (R[2] - R[6]) * h;
+    E.r.z = (R[3] - R[1]) * h;
+  } else {
+    E.r = quat_from_R(R);
+  }
   pose_normalize(E.r);
   SE3 out;  // E * T
   double rt[3];
@@ -611,7 +639,8 @@ __global__ __launch_bounds__(64 * W) void pose_opt_kernel(
         scale += 1e-3;
         rho = (currentChi - tempChi) / scale;
         if (rho > 0 && isfinite(tempChi)) {
-          double alpha = 1. - pow(2 * rho - 1, 3.0);
+          const double rm = 2 * rho - 1;
+          double alpha = 1. - rm * rm * rm;  // pow(2 rho - 1, 3)
           alpha = fmin(alpha, 2. / 3.);
           lambda *= fmax(1. / 3., alpha);
           ni = 2;
