@@ -294,10 +294,33 @@ __device__ __forceinline__ double eval_edge(const slamgpu_pose_edge& E, const Po
 // Sum 32 per-lane doubles over the wave: after 5 halving exchanges lane l holds the sum of value
 // l >> 1 over 32 lanes; the last exchange completes it over all 64. The exchanges are
 // lane_partner's permlane / DPP levels (pairs differ in bit log2(m)), not LDS permutes.
+// Levels 32 and 16 exchange two registers' halves in one permlane swap per dword (no selects):
+// after it the first holds (own, partner) of element i where the lane keeps i, the second the
+// other order, and their sum is the same keep + partner (IEEE addition commutes).
+template <int M>
+__device__ __forceinline__ void swap_halves(double& a, double& b) {
+  const uint64_t ua = __builtin_bit_cast(uint64_t, a), ub = __builtin_bit_cast(uint64_t, b);
+  const auto lo = M == 32 ? __builtin_amdgcn_permlane32_swap((uint32_t)ua, (uint32_t)ub, false, false)
+                          : __builtin_amdgcn_permlane16_swap((uint32_t)ua, (uint32_t)ub, false, false);
+  const auto hi = M == 32 ? __builtin_amdgcn_permlane32_swap((uint32_t)(ua >> 32), (uint32_t)(ub >> 32), false, false)
+                          : __builtin_amdgcn_permlane16_swap((uint32_t)(ua >> 32), (uint32_t)(ub >> 32), false, false);
+  a = __builtin_bit_cast(double, (uint64_t)hi[0] << 32 | lo[0]);
+  b = __builtin_bit_cast(double, (uint64_t)hi[1] << 32 | lo[1]);
+}
 __device__ __forceinline__ double wave_reduce_scatter32(double v[32]) {
   const int lane = threadIdx.x & 63;
 #pragma unroll
-  for (int h = 16, m = 32; h >= 1; h >>= 1, m >>= 1) {
+  for (int i = 0; i < 16; i++) {
+    swap_halves<32>(v[i], v[i + 16]);
+    v[i] = v[i] + v[i + 16];
+  }
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    swap_halves<16>(v[i], v[i + 8]);
+    v[i] = v[i] + v[i + 8];
+  }
+#pragma unroll
+  for (int h = 4, m = 8; h >= 1; h >>= 1, m >>= 1) {
     // The upper lane of each pair keeps the upper half. Both candidates are read first and the
     // choice is made on the values (v_cndmask), never on their addresses (which would move v
     // to scratch).
