@@ -55,74 +55,82 @@ __device__ __forceinline__ Sim3 oplus_axis(const Sim3& S, int d, double h, int f
   return sim3::sim3_mul(sim3::sim3_exp(u), S);
 }
 
-__global__ __launch_bounds__(256) void eg_linearize_kernel(EgGraph G, EgState W) {
-  const int k = blockIdx.x * blockDim.x + threadIdx.x;
-  if (k >= G.n_edges) return;
+// The linearisation in two launches, so an edge's 14 numeric-Jacobian columns (two error
+// evaluations each: Sim3 exp, products, log) run on 14 threads instead of in turn on one --
+// the one-thread-per-edge kernel kept a few hundred threads busy for ~20 serial evaluations.
+// Same operations per value, so the same bits.
+// eg_jac_kernel: thread (edge k, q): q < 14 the Jacobian column q (vertex q / 7, axis q % 7)
+// by central differences (BaseBinaryEdge::linearizeOplus, delta 1e-9); q == 14 the error and
+// chi2 at the estimate.
+constexpr int kEgJacThreads = 15;
+__global__ __launch_bounds__(256) void eg_jac_kernel(EgGraph G, EgState W) {
+  const int64_t gt = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (gt >= (int64_t)G.n_edges * kEgJacThreads) return;
+  const int k = (int)(gt / kEgJacThreads), q = (int)(gt % kEgJacThreads);
   const slamgpu_sim3_edge ed = G.edges[k];
-  const int fi = G.fidx[ed.i], fj = G.fidx[ed.j];
   const Sim3 Si = sim3::sim3_load(W.S + 8 * ed.i), Sj = sim3::sim3_load(W.S + 8 * ed.j);
   const Sim3 M = sim3::sim3_load(ed.Sji);
-  double e[7];
-  W.chi2[k] = edge_error(M, Si, Sj, e);
+  if (q == 14) {
+    double e[7];
+    W.chi2[k] = edge_error(M, Si, Sj, e);
 #pragma unroll
-  for (int r = 0; r < 7; r++) W.err[7 * k + r] = e[r];
-  double* c = W.contrib + (int64_t)k * kEgContrib;
-  // Jacobian columns (Ji, Jj row-major 7x7) into the edge's Jacobian slots, then the products
-  double* Jk = W.J + (int64_t)k * 98;
-  const double delta = 1e-9, scalar = 1.0 / (2 * delta);
-  for (int which = 0; which < 2; which++) {
-    if ((which ? fj : fi) < 0) continue;
-    double* J = Jk + 49 * which;
-#pragma unroll 1
-    for (int d = 0; d < 7; d++) {
-      double ep[7], em[7];
-      if (which == 0) {
-        edge_error(M, oplus_axis(Si, d, delta, G.fix_scale), Sj, ep);
-        edge_error(M, oplus_axis(Si, d, -delta, G.fix_scale), Sj, em);
-      } else {
-        edge_error(M, Si, oplus_axis(Sj, d, delta, G.fix_scale), ep);
-        edge_error(M, Si, oplus_axis(Sj, d, -delta, G.fix_scale), em);
-      }
-#pragma unroll
-      for (int r = 0; r < 7; r++) J[7 * r + d] = scalar * (ep[r] - em[r]);
-    }
+    for (int r = 0; r < 7; r++) W.err[7 * k + r] = e[r];
+    return;
   }
-  // b += J' omega_r (omega_r = -e), H += J' J (base_binary_edge.hpp:55-121, Omega = I)
-  const double* Ja = Jk;
-  const double* Jb = Jk + 49;
+  const int which = q / 7, d = q % 7;
+  if ((which ? G.fidx[ed.j] : G.fidx[ed.i]) < 0) return;  // a fixed vertex has no block
+  const double delta = 1e-9, scalar = 1.0 / (2 * delta);
+  double ep[7], em[7];
+  if (which == 0) {
+    edge_error(M, oplus_axis(Si, d, delta, G.fix_scale), Sj, ep);
+    edge_error(M, oplus_axis(Si, d, -delta, G.fix_scale), Sj, em);
+  } else {
+    edge_error(M, Si, oplus_axis(Sj, d, delta, G.fix_scale), ep);
+    edge_error(M, Si, oplus_axis(Sj, d, -delta, G.fix_scale), em);
+  }
+  double* J = W.J + (int64_t)k * 98 + 49 * which;
+#pragma unroll
+  for (int r = 0; r < 7; r++) J[7 * r + d] = scalar * (ep[r] - em[r]);
+}
+
+// eg_products_kernel: thread (edge k, row a): b += J' omega_r (omega_r = -e), H += J' J
+// (base_binary_edge.hpp:55-121, Omega = I) -- row a of each product, sums over q in order.
+__global__ __launch_bounds__(256) void eg_products_kernel(EgGraph G, EgState W) {
+  const int64_t gt = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (gt >= (int64_t)G.n_edges * 7) return;
+  const int k = (int)(gt / 7), a = (int)(gt % 7);
+  const slamgpu_sim3_edge ed = G.edges[k];
+  const int fi = G.fidx[ed.i], fj = G.fidx[ed.j];
+  double e[7];
+#pragma unroll
+  for (int r = 0; r < 7; r++) e[r] = W.err[7 * k + r];
+  double* c = W.contrib + (int64_t)k * kEgContrib;
+  const double* Ja = W.J + (int64_t)k * 98;
+  const double* Jb = Ja + 49;
   if (fi >= 0) {
-#pragma unroll 1
-    for (int a = 0; a < 7; a++) {
-      double s = 0.0;
-      for (int q = 0; q < 7; q++) s += Ja[7 * q + a] * -e[q];
-      c[147 + a] = s;
+    double s = 0.0;
+    for (int q = 0; q < 7; q++) s += Ja[7 * q + a] * -e[q];
+    c[147 + a] = s;
+    for (int cc = 0; cc < 7; cc++) {
+      double h = 0.0;
+      for (int q = 0; q < 7; q++) h += Ja[7 * q + a] * Ja[7 * q + cc];
+      c[7 * a + cc] = h;
+    }
+    if (fj >= 0)
       for (int cc = 0; cc < 7; cc++) {
         double h = 0.0;
-        for (int q = 0; q < 7; q++) h += Ja[7 * q + a] * Ja[7 * q + cc];
-        c[7 * a + cc] = h;
+        for (int q = 0; q < 7; q++) h += Ja[7 * q + a] * Jb[7 * q + cc];
+        c[98 + 7 * a + cc] = h;
       }
-    }
-    if (fj >= 0) {
-#pragma unroll 1
-      for (int a = 0; a < 7; a++)
-        for (int cc = 0; cc < 7; cc++) {
-          double h = 0.0;
-          for (int q = 0; q < 7; q++) h += Ja[7 * q + a] * Jb[7 * q + cc];
-          c[98 + 7 * a + cc] = h;
-        }
-    }
   }
   if (fj >= 0) {
-#pragma unroll 1
-    for (int a = 0; a < 7; a++) {
-      double s = 0.0;
-      for (int q = 0; q < 7; q++) s += Jb[7 * q + a] * -e[q];
-      c[154 + a] = s;
-      for (int cc = 0; cc < 7; cc++) {
-        double h = 0.0;
-        for (int q = 0; q < 7; q++) h += Jb[7 * q + a] * Jb[7 * q + cc];
-        c[49 + 7 * a + cc] = h;
-      }
+    double s = 0.0;
+    for (int q = 0; q < 7; q++) s += Jb[7 * q + a] * -e[q];
+    c[154 + a] = s;
+    for (int cc = 0; cc < 7; cc++) {
+      double h = 0.0;
+      for (int q = 0; q < 7; q++) h += Jb[7 * q + a] * Jb[7 * q + cc];
+      c[49 + 7 * a + cc] = h;
     }
   }
 }
@@ -601,7 +609,9 @@ int blocks_of(int n, int t) { return (n + t - 1) / t; }
 
 hipError_t launch_eg_linearize(const EgGraph& G, const EgState& W, hipStream_t st) {
   if (G.n_edges <= 0) return hipSuccess;
-  SLAMGPU_LAUNCH("eg_linearize", st, eg_linearize_kernel, dim3(blocks_of(G.n_edges, 256)),
+  SLAMGPU_LAUNCH("eg_jac", st, eg_jac_kernel,
+                 dim3(blocks_of(G.n_edges * kEgJacThreads, 256)), dim3(256), 0, st, G, W);
+  SLAMGPU_LAUNCH("eg_products", st, eg_products_kernel, dim3(blocks_of(G.n_edges * 7, 256)),
                  dim3(256), 0, st, G, W);
   return hipGetLastError();
 }
