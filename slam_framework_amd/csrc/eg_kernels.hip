@@ -434,13 +434,14 @@ __global__ __launch_bounds__(kFacThreads) void eg_factor_solve_kernel(EgGraph G,
     // block g0 + t of column k's extent: its L column c, and x of its row when that row is
     // older than the ring (written by this wave kXr+ columns ago; ordered by the wavefront-scope
     // release / acquire closing every column -- AMDGPU memory model, no wait needed)
-    auto load_blk = [&](int k, int g0, double (&lv)[7], double (&xv)[7]) {
+    auto load_blk = [&](int k, int g0, double (&lv)[7], double (&xv)[7], int& iv) {
       const int e0 = EP(k), ne = EP(k + 1) - e0;
       if (lane_ok && g0 + t < ne) {
         const double* Lik = L + (EB(e0 + g0 + t) + k) * 49 + c;
 #pragma unroll
         for (int r = 0; r < 7; r++) lv[r] = Lik[7 * r];
         const int i = ER(e0 + g0 + t);
+        iv = i;
         if (i - k > kXr)
 #pragma unroll
           for (int r = 0; r < 7; r++) xv[r] = y[7 * i + r];
@@ -453,32 +454,37 @@ __global__ __launch_bounds__(kFacThreads) void eg_factor_solve_kernel(EgGraph G,
         for (int m = 0; m < 7; m++) dv[m] = Lkk[7 * m + lane];
       }
     };
-    double lnext[7], dnext[7], xnext[7];
+    double lnext[7], dnext[7], xnext[7], znext = 0.0;
+    int inext = 0;  // the lane's extent row (its block's row i)
 #pragma unroll
     for (int r = 0; r < 7; r++) lnext[r] = dnext[r] = xnext[r] = 0.0;
     if (F > 0) {
-      load_blk(F - 1, 0, lnext, xnext);
+      load_blk(F - 1, 0, lnext, xnext, inext);
       load_diag(F - 1, dnext);
+      if (lane < 7) znext = y[7 * (F - 1) + lane];
     }
     for (int k = F - 1; k >= 0; k--) {
       const int e0 = EP(k), ne = EP(k + 1) - e0;
       double lcur[7], dcur[7], xcur[7];
+      const double zcur = znext;  // z_k (lanes 0-6): y below column k is not yet overwritten
+      int icur = inext;
 #pragma unroll
       for (int r = 0; r < 7; r++) {
         lcur[r] = lnext[r];
         dcur[r] = dnext[r];
         xcur[r] = xnext[r];
       }
-      if (k > 0) {  // the next column's blocks, in flight under this one
-        load_blk(k - 1, 0, lnext, xnext);
+      if (k > 0) {  // the next column's blocks and z, in flight under this one
+        load_blk(k - 1, 0, lnext, xnext, inext);
         load_diag(k - 1, dnext);
+        if (lane < 7) znext = y[7 * (k - 1) + lane];
       }
       double acc = 0.0;
       for (int g0 = 0; g0 < ne; g0 += 9) {
-        if (g0 > 0) load_blk(k, g0, lcur, xcur);
+        if (g0 > 0) load_blk(k, g0, lcur, xcur, icur);
         const int tt = g0 + t;
         const bool has = lane_ok && tt < ne;
-        const int i = has ? ER(e0 + tt) : k;
+        const int i = has ? icur : k;
         const bool far = has && i - k > kXr;
         double pr[7];
 #pragma unroll
@@ -504,7 +510,7 @@ __global__ __launch_bounds__(kFacThreads) void eg_factor_solve_kernel(EgGraph G,
       const double tot = __shfl(acc, 9 * min(lane, 6) + (ne > 0 ? (ne - 1) % 9 : 0), 64);
       double v = 0.0;
       if (lane < 7) {
-        v = y[7 * k + lane];
+        v = zcur;
         if (ne > 0) v -= tot;
       }
       // the diagonal block: x(r) -= Lkk(m, r) x(m) for m = r + 1 .. 6, r = 5 .. 0
