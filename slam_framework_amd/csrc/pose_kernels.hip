@@ -79,12 +79,13 @@ __device__ __forceinline__ double rsq_nr(double x) {
 __device__ bool ldlt_solve6(const double H[kNH], double lambda, const double b[6], double x[6]) {
 #pragma clang fp contract(fast)  // tolerance-compared: the column sums fuse
   double L[6][6], D[6][6], id[6];  // D[i][k] = L[i][k] d[k]
+  bool neg = false;  // a negative pivot fails the solve; tested once, after the straight-line code
 #pragma unroll
   for (int j = 0; j < 6; j++) {
     double dj = H[j * 6 - (j * (j - 1)) / 2] + lambda;  // H(j, j) in the packed upper triangle
 #pragma unroll
     for (int k = 0; k < j; k++) dj -= L[j][k] * D[j][k];
-    if (dj < 0) return false;
+    neg = neg || dj < 0;
     id[j] = dj > DBL_MIN ? rcp_nr(dj) : 0.0;
 #pragma unroll
     for (int i = j + 1; i < 6; i++) {
@@ -95,6 +96,7 @@ __device__ bool ldlt_solve6(const double H[kNH], double lambda, const double b[6
       L[i][j] = s * id[j];
     }
   }
+  if (neg) return false;
   double y[6];
 #pragma unroll
   for (int i = 0; i < 6; i++) {
