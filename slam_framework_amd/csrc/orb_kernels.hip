@@ -259,107 +259,102 @@ __device__ __forceinline__ int reflect101(int i, int n) {  // cv::BORDER_REFLECT
 #endif
 constexpr int kCellWaves = FAST_CELL_WAVES;  // waves per work-group
 
-// max over the 16 contiguous 9-arcs of min(v - ring) ("darker" strength) and of min(ring - v)
-// ("brighter"); p is a FAST-9 corner at threshold t iff the result is > t.
-__device__ __forceinline__ int fast_s(const uint8_t* t, int o, const int kTileStride) {
-  const int v = t[o];
-  int d[16];
-  d[0] = v - t[o + 3 * kTileStride];
-  d[1] = v - t[o + 1 + 3 * kTileStride];
-  d[2] = v - t[o + 2 + 2 * kTileStride];
-  d[3] = v - t[o + 3 + 1 * kTileStride];
-  d[4] = v - t[o + 3];
-  d[5] = v - t[o + 3 - 1 * kTileStride];
-  d[6] = v - t[o + 2 - 2 * kTileStride];
-  d[7] = v - t[o + 1 - 3 * kTileStride];
-  d[8] = v - t[o - 3 * kTileStride];
-  d[9] = v - t[o - 1 - 3 * kTileStride];
-  d[10] = v - t[o - 2 - 2 * kTileStride];
-  d[11] = v - t[o - 3 - 1 * kTileStride];
-  d[12] = v - t[o - 3];
-  d[13] = v - t[o - 3 + 1 * kTileStride];
-  d[14] = v - t[o - 2 + 2 * kTileStride];
-  d[15] = v - t[o - 1 + 3 * kTileStride];
-  int mn2[16], mx2[16];
-#pragma unroll
-  for (int k = 0; k < 16; k++) {
-    mn2[k] = min(d[k], d[(k + 1) & 15]);
-    mx2[k] = max(d[k], d[(k + 1) & 15]);
-  }
-  int mn4[16], mx4[16];
-#pragma unroll
-  for (int k = 0; k < 16; k++) {
-    mn4[k] = min(mn2[k], mn2[(k + 2) & 15]);
-    mx4[k] = max(mx2[k], mx2[(k + 2) & 15]);
-  }
-  int sd = -1024, sb = 1024;
-#pragma unroll
-  for (int k = 0; k < 16; k++) {
-    sd = max(sd, min(min(mn4[k], mn4[(k + 4) & 15]), d[(k + 8) & 15]));
-    sb = min(sb, max(max(mx4[k], mx4[(k + 4) & 15]), d[(k + 8) & 15]));
-  }
-  return max(sd, -sb);
+// ---- byte-parallel comparisons (r5). v_lerp_u8 adds two bytes and a rounding bit per byte and
+// halves, with no carry between bytes: lerp(x, ~y, r) = floor((x - y + 255 + r) / 2) encodes
+// x - y in [-255, 255] as a byte, and a second lerp against a constant C sets bit 7 of a byte
+// exactly when that byte is >= 256 - C. So "x - y >= t + 1" is bit 7 of two lerps for four
+// pixels at once (t + r even makes the halving exact: r = t & 1, K = 128 + (t + r) / 2):
+//   bright_a  (a - v >= t + 1) = bit 7 of lerp(lerp(a, ~v, r), 256 - K, 0)
+//   !dark_a   (v - a <= t)     = bit 7 of lerp(lerp(~v, a, 1 - r), K, 0)
+// (lerp(~v, a, 1 - r) = 255 - lerp(v, ~a, r), so the dark test needs no ~a.)
+__device__ __forceinline__ uint32_t lerp_u8(uint32_t a, uint32_t b, uint32_t r) {
+  return __builtin_amdgcn_lerp(a, b, r);
 }
 
-// fast_s on int16 pairs: x_k = (v - p_k, p_k - v), so one min/max network yields both the dark
-// arc minimum (low half) and minus the bright arc maximum (high half): s = max(lo, hi).
-typedef short i16x2 __attribute__((ext_vector_type(2)));
+struct FastTh {        // one pass's threshold constants (wave-uniform)
+  int th;              // clamped to [0, 255] as cv::FAST does
+  uint32_t r, rn;      // rounding bytes r and 1 - r
+  uint32_t cb, cd;     // second-level constants 256 - K and K
+};
+__device__ __forceinline__ FastTh fast_th(int th) {
+  FastTh f;
+  f.th = min(max(th, 0), 255);
+  const int r = f.th & 1, K = 128 + ((f.th + r) >> 1);  // K = 256 at t = 255: no corner
+  f.r = (uint32_t)r * 0x01010101u;
+  f.rn = (uint32_t)(r ^ 1) * 0x01010101u;
+  f.cb = (uint32_t)(256 - K) * 0x01010101u;
+  f.cd = (uint32_t)min(K, 255) * 0x01010101u;
+  return f;
+}
+
+// The FAST pre-test of 4 pixels (one tile dword c, its row neighbours cm / cp and the dwords 3
+// rows below / above): a pixel can be a corner only if both opposite ring pairs (0, 8) and
+// (4, 12) hold a pixel darker than v - t (or both a pixel brighter than v + t) -- every 9-arc of
+// the ring contains one pixel of each pair. Bit 7 of each byte = that pixel survives.
+__device__ __forceinline__ uint32_t fast_pretest4(uint32_t c, uint32_t cm, uint32_t cp,
+                                                  uint32_t p0, uint32_t p8, const FastTh& f) {
+  const uint32_t a4 = __builtin_amdgcn_alignbyte(cp, c, 3);   // (x + 3, y)
+  const uint32_t a12 = __builtin_amdgcn_alignbyte(c, cm, 1);  // (x - 3, y)
+  const uint32_t nv = ~c;
+  auto B = [&](uint32_t a) { return lerp_u8(lerp_u8(a, nv, f.r), f.cb, 0u); };
+  auto G = [&](uint32_t a) { return lerp_u8(lerp_u8(nv, a, f.rn), f.cd, 0u); };
+  const uint32_t bright = (B(p0) | B(p8)) & (B(a4) | B(a12));
+  const uint32_t ndark = (G(p0) & G(p8)) | (G(a4) & G(a12));
+  return bright | ~ndark;  // bit 7 of each byte (other bits: don't care)
+}
+
+// Exact FAST-9 strength s of one pixel (see above) on the 16 ring differences as f16 pairs
+// x = (v - p, p - v): as f16 bit patterns the bytes v and p are the denormals v 2^-24 and
+// p 2^-24, so one v_pk_add_f16 (negation per half, the byte broadcast by op_sel_hi) forms both
+// differences exactly, and v_pk_minimum3 / v_pk_maximum3 evaluate the min-over-9-arcs /
+// max-over-arcs network three operands at a time (16 + 16 + 8 instructions for both signs).
+// A non-negative result's bit pattern is the integer s; a negative one (sign bit) means s < 0.
+__device__ __forceinline__ uint32_t pk_minimum3(uint32_t a, uint32_t b, uint32_t c) {
+  uint32_t d;
+  asm("v_pk_minimum3_f16 %0, %1, %2, %3" : "=v"(d) : "v"(a), "v"(b), "v"(c));
+  return d;
+}
+__device__ __forceinline__ uint32_t pk_maximum3(uint32_t a, uint32_t b, uint32_t c) {
+  uint32_t d;
+  asm("v_pk_maximum3_f16 %0, %1, %2, %3" : "=v"(d) : "v"(a), "v"(b), "v"(c));
+  return d;
+}
 template <int ts>
-__device__ __forceinline__ int fast_s_pk(const uint8_t* t, int o) {
-  const int v = t[o];
-  const i16x2 v2 = {(short)v, (short)-v}, np = {-1, 1};
-  // ring offsets relative to the top-left of the 7x7 window (immediates, all >= 0)
+__device__ __forceinline__ int fast_score(const uint8_t* w) {  // w: top-left of the 7x7 window
   constexpr int offs[16] = {3 + 6 * ts, 4 + 6 * ts, 5 + 5 * ts, 6 + 4 * ts, 6 + 3 * ts, 6 + 2 * ts,
                             5 + ts,     4,          3,          2,          1 + ts,     2 * ts,
                             3 * ts,     4 * ts,     1 + 5 * ts, 2 + 6 * ts};
-  const uint8_t* w = t + o - 3 - 3 * ts;
-  i16x2 x[16];
+  const uint32_t v = w[3 + 3 * ts];
+  uint32_t x[16];
 #pragma unroll
   for (int k = 0; k < 16; k++) {
     const uint32_t p = w[offs[k]];
-    x[k] = __builtin_bit_cast(i16x2, p * 0x10001u) * np + v2;
+    asm("v_pk_add_f16 %0, %1, %2 op_sel_hi:[0,0] neg_lo:[1,0] neg_hi:[0,1]"
+        : "=v"(x[k]) : "v"(p), "v"(v));
   }
-  i16x2 m2[16], m4[16];
+  uint32_t m3[16], m9[16];
 #pragma unroll
-  for (int k = 0; k < 16; k++) m2[k] = __builtin_elementwise_min(x[k], x[(k + 1) & 15]);
+  for (int k = 0; k < 16; k++) m3[k] = pk_minimum3(x[k], x[(k + 1) & 15], x[(k + 2) & 15]);
 #pragma unroll
-  for (int k = 0; k < 16; k++) m4[k] = __builtin_elementwise_min(m2[k], m2[(k + 2) & 15]);
-  i16x2 best = {-32768, -32768};
-#pragma unroll
-  for (int k = 0; k < 16; k++) {
-    const i16x2 arc = __builtin_elementwise_min(__builtin_elementwise_min(m4[k], m4[(k + 4) & 15]),
-                                                x[(k + 8) & 15]);
-    best = __builtin_elementwise_max(best, arc);
-  }
-  return max((int)best.x, (int)best.y);
+  for (int k = 0; k < 16; k++) m9[k] = pk_minimum3(m3[k], m3[(k + 3) & 15], m3[(k + 6) & 15]);
+  const uint32_t u0 = pk_maximum3(pk_maximum3(m9[0], m9[1], m9[2]), pk_maximum3(m9[3], m9[4], m9[5]),
+                                  pk_maximum3(m9[6], m9[7], m9[8]));
+  const uint32_t u1 = pk_maximum3(pk_maximum3(m9[9], m9[10], m9[11]),
+                                  pk_maximum3(m9[12], m9[13], m9[14]), m9[15]);
+  const uint32_t best = pk_maximum3(u0, u1, u1);
+  return max(max((int)(int16_t)(best & 0xffffu), (int)(int16_t)(best >> 16)), 0);
 }
 
-// Exact necessary condition for a corner at threshold t: every 9-arc of the 16-ring contains
-// one pixel of each opposite pair (0,8), (4,12), (2,10), (6,14) -- FAST_t's own pre-test.
-__device__ __forceinline__ bool fast_maybe(const uint8_t* t, int o, int th,
-                                           const int kTileStride) {
-  const int v = t[o];
-  const int lo = v - th, hi = v + th;
-  const int p0 = t[o + 3 * kTileStride], p8 = t[o - 3 * kTileStride];
-  const int p4 = t[o + 3], p12 = t[o - 3];
-  const int p2 = t[o + 2 + 2 * kTileStride], p10 = t[o - 2 - 2 * kTileStride];
-  const int p6 = t[o + 2 - 2 * kTileStride], p14 = t[o - 2 + 2 * kTileStride];
-  const bool dark = (p0 < lo || p8 < lo) && (p4 < lo || p12 < lo) && (p2 < lo || p10 < lo) &&
-                    (p6 < lo || p14 < lo);
-  const bool bright = (p0 > hi || p8 > hi) && (p4 > hi || p12 > hi) && (p2 > hi || p10 > hi) &&
-                      (p6 > hi || p14 > hi);
-  return dark || bright;
-}
-
-// bit 7 of every byte: the per-pixel flag format of the prefilter masks
-constexpr uint32_t kH = 0x80808080u;
-
-// A wave runs kCellsPerWave consecutive cells of one image: the next cell's tile is loaded
-// into registers while the current one is processed from LDS.
+// A wave runs kCellsPerWave consecutive cells of one image.
 #ifndef FAST_CELLS_PER_WAVE
 #define FAST_CELLS_PER_WAVE 4
 #endif
 constexpr int kCellsPerWave = FAST_CELLS_PER_WAVE;
+
+// ceil(4096 / n) for n = 1..32 (the pre-test's lane -> (row, dword) split by a multiply)
+__constant__ int16_t c_inv4096[33] = {
+    0,   4096, 2048, 1366, 1024, 820, 683, 586, 512, 456, 410, 373, 342, 316, 293, 274, 256,
+    241, 228,  216,  205,  196,  187, 179, 171, 164, 158, 152, 147, 142, 137, 133, 128};
 
 struct CellView {
   int level, ini_x, ini_y, vw, vh, pitch, ax, off, nd;
@@ -393,9 +388,8 @@ __device__ __forceinline__ uint4 readlane4(const uint4& x, int j) {
 
 // GLDS: every cell view of the launch is 16-byte aligned (pyramid levels, and a caller image
 // with 16-byte base/pitch/stride): tiles go HBM -> LDS by global_load_lds_dwordx4 (no VGPRs, one
-// instruction per 1 KiB = 1024/TS tile rows), double-buffered so the next cell's tile streams in
-// while this one is processed. Otherwise dword loads staged through registers (4-byte aligned)
-// or a byte copy.
+// instruction per 1 KiB = 1024/TS tile rows). Otherwise dword loads staged through registers
+// (4-byte aligned) or a byte copy.
 template <int TS, bool GLDS>
 __global__ __launch_bounds__(64 * kCellWaves, 1) void fast_cells_kernel(ImageBatch b,
                                                          const OrbGeom* __restrict__ g,
@@ -424,8 +418,8 @@ __global__ __launch_bounds__(64 * kCellWaves, 1) void fast_cells_kernel(ImageBat
   // configuration scalars read once (the stores below would otherwise make the compiler reload
   // them inside the NMS loop, each behind a scalar-load wait)
   const int cell_cap = __builtin_amdgcn_readfirstlane(g->cell_cap);
-  const int ini_th = __builtin_amdgcn_readfirstlane(g->ini_th);
-  const int min_th = __builtin_amdgcn_readfirstlane(g->min_th);
+  const FastTh th_ini = fast_th(__builtin_amdgcn_readfirstlane(g->ini_th));
+  const FastTh th_min = fast_th(__builtin_amdgcn_readfirstlane(g->min_th));
   const int tile_bytes = (kTileStride * g->fast_tile_rows + 15) & ~15;
   uint8_t* tile0 = s_fast + wid * g->fast_lds_per_wave;
   uint8_t* sc = tile0 + tile_bytes;
@@ -452,18 +446,18 @@ __global__ __launch_bounds__(64 * kCellWaves, 1) void fast_cells_kernel(ImageBat
   // glds: tile row r of the view = image row ini_y + min(r, vh - 1) (rows past the view repeat
   // its last row; they are never read), 16-byte chunk lane % kGLpr of [ax, ax + TS). The view
   // ends >= 16 rows above the level's last row, so the TS-byte row reads stay in the image.
+  // The row offsets are 32-bit lane offsets from one scalar base (saddr form).
   const int glr = lane / kGLpr, glc = 16 * (lane % kGLpr);
-  auto issue = [&](const CellView& v, uint8_t* buf) -> int {
-    const int n = (v.vh + kGRows - 1) / kGRows;  // wave-uniform
-    const uint8_t* src = v.base + (int64_t)v.ini_y * v.pitch + v.ax + glc;
+  auto issue = [&](const CellView& v, uint8_t* buf) {
+    const uint8_t* src = v.base + (int64_t)v.ini_y * v.pitch + v.ax;  // wave-uniform
+    const int n = (v.vh + kGRows - 1) / kGRows;
 #pragma unroll
     for (int k = 0; k < kGSteps; k++)
       if (k < n && k * kGRows + glr < tile_rows)
         __builtin_amdgcn_global_load_lds(
             (const __attribute__((address_space(1))) void*)(
-                src + (int64_t)min(k * kGRows + glr, v.vh - 1) * v.pitch),
+                src + (uint32_t)(min(k * kGRows + glr, v.vh - 1) * v.pitch + glc)),
             (__attribute__((address_space(3))) void*)(buf + 1024 * k), 16, 0, 0);
-    return n;
   };
   CellView nxt = cell_view<kAlign>(b, g, img, in_pitch, readlane4(my_desc, 0));
   if constexpr (!GLDS) {
@@ -524,71 +518,41 @@ __global__ __launch_bounds__(64 * kCellWaves, 1) void fast_cells_kernel(ImageBat
     // sc1 = row 0. Until then the pass keeps its prefilter records in the same bytes.
     uint8_t* sc1 = sc + kScoreStride;
     uint32_t* const recs = reinterpret_cast<uint32_t*>(sc);
-    // ---- one FAST pass at threshold th: prefilter every detect pixel (4 pixels, one tile dword,
+    // ---- one FAST pass at threshold th: pre-test every detect pixel (4 pixels, one tile dword,
     // per lane), exact score of the survivors into the score map, NMS at th, survivors out in
     // row-major order.
     // Detect pixel (rr, col): tile row rr + 3, tile column col in [off + 3, off + 3 + dw).
+    // Lane -> (row lr of a step, dword Q): rows_per rows of nq dwords per step.
     const int q_lo = (off + 3) >> 2, q_hi = (off + 2 + dw) >> 2;
     const int nq = q_hi - q_lo + 1;
-    // lane / nq by a reciprocal (exact for lane < 64, nq < 64): no integer division
-    const int inv_nq = (int)ceilf(4096.0f / (float)nq);
+    const int inv_nq = c_inv4096[nq];  // lane / nq = (lane * inv_nq) >> 12 (exact for lane < 64)
     const int rows_per = (64 * inv_nq) >> 12;
     const int lr = (lane * inv_nq) >> 12, Q = q_lo + (lane - lr * nq);
     const int blo = max(0, off + 3 - 4 * Q), bhi = min(4, off + 3 + dw - 4 * Q);
-    const uint32_t vmask =
-        (uint32_t)(((1ull << (8 * bhi)) - 1) & ~((1ull << (8 * blo)) - 1)) & kH;
-    const int qm = max(Q - 1, 0) - Q;  // dword step left (clamped at the tile edge)
+    const uint32_t vmask = lr < rows_per
+        ? (uint32_t)(0x80808080ull >> (32 - 8 * bhi)) & (uint32_t)(0x80808080ull << (8 * blo))
+        : 0u;
+    const uint8_t* trow = tile + (lr + 3) * kTileStride + 4 * Q;  // this lane's dword, step 0
     uint32_t* out = cell_keys + slot * cell_cap;
-    auto fast_pass = [&](int th) -> int {
-      // prefilter: a lane with any surviving pixel appends one record (its tile dword's pixel
-      // index | 4-bit survivor mask << 16); records come out in row-major order (row, dword)
+    auto fast_pass = [&](const FastTh& f) -> int {
+      if (f.th >= 255) return 0;  // FAST at 255: no pixel differs by more
+      // pre-test: a lane with any surviving pixel appends one record -- its survivor flags (bit
+      // 7 of each byte) | lane | step << 8 -- so records come out in row-major order
       int nrec = 0;
-      for (int r0 = 0; r0 < dh; r0 += rows_per) {
-        const int rr = r0 + lr;
-        uint32_t m = 0;
-        if (lr < rows_per && rr < dh) {
-          const uint8_t* row = tile + (rr + 3) * kTileStride + 4 * Q;
-          auto rd = [&](int dy, int dq) {
-            return *reinterpret_cast<const uint32_t*>(row + dy * kTileStride + 4 * dq);
-          };
-          const uint32_t c = rd(0, 0), cm = rd(0, qm), cp = rd(0, 1);
-          const uint32_t p0 = rd(3, 0), p8 = rd(-3, 0);
-          // even pixels (bytes 0, 2) and odd pixels (bytes 1, 3) of each ring position as u16
-          // pairs; v_perm picks the shifted bytes straight out of two adjacent dwords
-          typedef unsigned short u16x2_t __attribute__((ext_vector_type(2)));
-          auto U = [](uint32_t x) { return __builtin_bit_cast(u16x2_t, x); };
-          const u16x2_t tt2 = U((uint32_t)th * 0x10001u);
-          uint32_t any[2];
-#pragma unroll
-          for (int h = 0; h < 2; h++) {
-            const uint32_t sh = h ? 0x00010001u : 0u;  // odd pixels: data selectors + 1
-            const uint32_t s0 = 0x0c020c00u + sh, s1 = 0x0c030c01u + sh, s2 = 0x0c040c02u + sh,
-                           s3 = 0x0c050c03u + sh;
-            const u16x2_t v = U(__builtin_amdgcn_perm(c, c, s0));
-            const u16x2_t a0 = U(__builtin_amdgcn_perm(p0, p0, s0));      // (0, +3)
-            const u16x2_t a8 = U(__builtin_amdgcn_perm(p8, p8, s0));      // (0, -3)
-            const u16x2_t a4 = U(__builtin_amdgcn_perm(cp, c, s3));       // (+3, 0)
-            const u16x2_t a12 = U(__builtin_amdgcn_perm(c, cm, s1));      // (-3, 0)
-            const u16x2_t D = __builtin_elementwise_max(__builtin_elementwise_min(a0, a8),
-                                                        __builtin_elementwise_min(a4, a12));
-            const u16x2_t B = __builtin_elementwise_min(__builtin_elementwise_max(a0, a8),
-                                                        __builtin_elementwise_max(a4, a12));
-            const u16x2_t lo = __builtin_elementwise_sub_sat(v, tt2), hi = v + tt2;
-            any[h] = __builtin_bit_cast(uint32_t, __builtin_elementwise_sub_sat(lo, D)) |
-                     __builtin_bit_cast(uint32_t, __builtin_elementwise_sub_sat(B, hi));
-          }
-          // non-zero u16 lane -> bit 7 of that pixel's byte
-          m = ((((any[0] + 0x7fff7fffu) & 0x80008000u) >> 8) | ((any[1] + 0x7fff7fffu) & 0x80008000u)) &
-              vmask;
-        }
+      auto step = [&](int it, int r0, auto tail_case) {
+        constexpr bool kTail = decltype(tail_case)::value;
+        const uint8_t* row = trow + r0 * kTileStride;
+        auto rd = [&](int o) { return *reinterpret_cast<const uint32_t*>(row + o); };
+        uint32_t m = fast_pretest4(rd(0), rd(-4), rd(4), rd(3 * kTileStride),
+                                   rd(-3 * kTileStride), f) & vmask;
+        if (kTail && r0 + lr >= dh) m = 0;
         const uint64_t act = __ballot(m != 0);
-        if (m) {  // bits 7, 15, 23, 31 -> bits 16..19
-          const uint32_t bits = ((m >> 7) & 1u) | ((m >> 14) & 2u) | ((m >> 21) & 4u) |
-                                ((m >> 28) & 8u);
-          recs[nrec + lanes_below(act)] = (uint32_t)(rr * kScoreStride + 4 * Q) | bits << 16;
-        }
+        if (m) recs[nrec + lanes_below(act)] = m | (uint32_t)lane | (uint32_t)it << 8;
         nrec += __popcll(act);
-      }
+      };
+      int it = 0, r0 = 0;
+      for (; r0 + rows_per <= dh; r0 += rows_per, it++) step(it, r0, std::false_type{});
+      if (r0 < dh) step(it, r0, std::true_type{});
       __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
       __builtin_amdgcn_wave_barrier();
       // records -> one candidate per surviving pixel, row-major (exclusive prefix of the
@@ -597,13 +561,17 @@ __global__ __launch_bounds__(64 * kCellWaves, 1) void fast_cells_kernel(ImageBat
       for (int i0 = 0; i0 < nrec; i0 += 64) {
         const int i = i0 + lane;
         const uint32_t rec = i < nrec ? recs[i] : 0u;
-        const int cnt = __popc(rec >> 16);
+        const uint32_t fl = rec & 0x80808080u;
+        const int cnt = __popc(fl);
         const uint64_t b0 = __ballot(cnt & 1), b1 = __ballot(cnt & 2), b2 = __ballot(cnt & 4);
         int pos = ncand + lanes_below(b0) + 2 * lanes_below(b1) + 4 * lanes_below(b2);
-        const uint32_t pix0 = rec & 0xffffu;
+        const int ln = (int)(rec & 63u), rit = (int)((rec >> 8) & 127u);
+        const int lr2 = (ln * inv_nq) >> 12;
+        const uint32_t pix0 =
+            (uint32_t)((rit * rows_per + lr2) * kScoreStride + 4 * (q_lo + ln - lr2 * nq));
 #pragma unroll
         for (int bb = 0; bb < 4; bb++)
-          if (rec & (0x10000u << bb)) cand[pos++] = (uint16_t)(pix0 + bb);
+          if (fl & (0x80u << (8 * bb))) cand[pos++] = (uint16_t)(pix0 + bb);
         ncand += __popcll(b0) + 2 * __popcll(b1) + 4 * __popcll(b2);
       }
       __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
@@ -613,12 +581,10 @@ __global__ __launch_bounds__(64 * kCellWaves, 1) void fast_cells_kernel(ImageBat
         *reinterpret_cast<uint32_t*>(sc1 + rz * kScoreStride + 4 * pld) = 0;
       __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
       __builtin_amdgcn_wave_barrier();
-      // exact FAST score of the survivors
+      // exact FAST score of the survivors (window top-left: tile (r, cc - 3) = tile + pix - 3)
       for (int i = lane; i < ncand; i += 64) {
         const int pix = cand[i];
-        const int r = pix / kScoreStride, cc = pix - r * kScoreStride;
-        const int sv = fast_s_pk<TS>(tile, (r + 3) * kTileStride + cc);
-        sc1[pix] = (uint8_t)(sv < 0 ? 0 : sv);
+        sc1[pix] = (uint8_t)fast_score<TS>(tile + pix - 3);
       }
       __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
       __builtin_amdgcn_wave_barrier();
@@ -627,6 +593,7 @@ __global__ __launch_bounds__(64 * kCellWaves, 1) void fast_cells_kernel(ImageBat
       //   s > th  &&  s >= 2  &&  Q < max(s, th + 1),
       // and a neighbour this pass did not score has s <= th < s_p (the pre-test is necessary),
       // so it cannot change the test.
+      const int th = f.th;
       int count = 0;
       for (int i0 = 0; i0 < ncand; i0 += 64) {
         const int i = i0 + lane;
@@ -660,11 +627,11 @@ __global__ __launch_bounds__(64 * kCellWaves, 1) void fast_cells_kernel(ImageBat
     };
     // FAST at iniTh; the reference re-runs the whole cell at minTh when the iniTh output (after
     // NMS) is empty (:753-757)
-    int count = fast_pass(ini_th);
+    int count = fast_pass(th_ini);
     if (count == 0) {
       __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
       __builtin_amdgcn_wave_barrier();
-      count = fast_pass(min_th);
+      count = fast_pass(th_min);
     }
     if (lane == 0) {
       if (count > cell_cap) {
@@ -675,7 +642,6 @@ __global__ __launch_bounds__(64 * kCellWaves, 1) void fast_cells_kernel(ImageBat
     }
   }
 }
-
 // ---------------------------------------------------------------------------------------
 // octree: DistributeOctTree (:480-704), one 256-thread workgroup per (image, level).
 // The std::list is kept as an array in list order and rebuilt every pass; node keys are
