@@ -21,6 +21,8 @@
 #include <vector>
 
 #include "slamgpu.h"
+#include "slamgpu_bow.h"
+#include "slamgpu_kfmatch.h"
 #include "slamgpu_optimizer.h"
 
 namespace slamgpu_adapter {
@@ -592,5 +594,390 @@ class StereoFrameCore {
   slamgpu_ctx* ctx_ = nullptr;
   int cols_ = 0, rows_ = 0;
 };
+
+
+// =================================================================================================
+// The keyframe-rate surfaces: SearchByBoW, SearchForTriangulation, Fuse,
+// OptimizeSim3 and the global BundleAdjustment, gathered from the same views, called, written back.
+
+// DBoW2::FeatureVector (std::map<NodeId, std::vector<unsigned>>) as arrays: node ids ascending,
+// each node's feature indices in insertion order.
+struct FeatureVecView {
+  const uint32_t* nodes = nullptr;
+  const int32_t* node_start = nullptr;  // [n_nodes + 1]
+  const uint32_t* node_feats = nullptr;
+  int n_nodes = 0;
+};
+
+// What the keyframe-rate matchers read of a KeyFrame beyond KeyFrameView: its descriptors
+// (KeyFrame::descriptors), feature_vec, and GetCameraCenter() (the stored Ow).
+struct KeyFrameFeatures {
+  const uint8_t* desc = nullptr;
+  FeatureVecView fv;
+  const float* Ow = nullptr;
+};
+
+inline void throw_if(int rc, const char* (*msg)(void)) {
+  if (rc != SLAMGPU_OK) throw std::runtime_error(std::string("slamgpu: ") + msg());
+}
+
+inline slamgpu_bow_set bow_set(const uint8_t* desc, const slamgpu_keypoint* kps, const uint8_t* valid,
+                               int n, const FeatureVecView& fv) {
+  slamgpu_bow_set b;
+  b.desc = desc;
+  b.kps = kps;
+  b.valid = valid;
+  b.nodes = fv.nodes;
+  b.node_start = fv.node_start;
+  b.node_feats = fv.node_feats;
+  b.n = n;
+  b.n_nodes = fv.n_nodes;
+  return b;
+}
+
+// A keyframe's features whose map point exists and is not bad (the `if(!pMP) continue; if
+// (pMP->isBad()) continue;` of both SearchByBoW overloads).
+inline std::vector<uint8_t> good_map_point_mask(const KeyFrameView& kf, const MapPointView* mps) {
+  std::vector<uint8_t> v(kf.n_kps);
+  for (int i = 0; i < kf.n_kps; ++i) v[i] = kf.map_points[i] >= 0 && !mps[kf.map_points[i]].bad;
+  return v;
+}
+
+// ---- OrbMatcher::SearchByBoW(KeyFrame* pKF, Frame& F, vector<MapPoint*>&) (orb_matcher.cpp:
+// 133-262): Tracker::TrackReferenceKeyFrame (tracker.cpp:666, OrbMatcher(0.7, true)) and the
+// relocalisation (:860, 0.75). map_point_matches[j] = the keyframe map point matched to frame
+// keypoint j, or -1 (the vpMapPointMatches the caller then gives to Frame::SetMapPoints).
+inline int search_by_bow(const KeyFrameView& kf, const KeyFrameFeatures& kff,
+                         const MapPointView* mps, const slamgpu_keypoint* f_keys,
+                         const uint8_t* f_desc, int f_n, const FeatureVecView& f_fv,
+                         float nnratio, bool check_ori, std::vector<int32_t>& map_point_matches) {
+  const std::vector<uint8_t> valid = good_map_point_mask(kf, mps);
+  const slamgpu_bow_set a = bow_set(kff.desc, kf.undist_kps, valid.data(), kf.n_kps, kff.fv);
+  const slamgpu_bow_set b = bow_set(f_desc, f_keys, nullptr, f_n, f_fv);
+  std::vector<int32_t> match(kf.n_kps > 0 ? kf.n_kps : 1);
+  int nm = 0;
+  throw_if(slamgpu_search_by_bow(&a, &b, 0, nnratio, check_ori ? 1 : 0, match.data(), &nm),
+           slamgpu_bow_last_error);
+  map_point_matches.assign(f_n, -1);
+  for (int i = 0; i < kf.n_kps; ++i)
+    if (match[i] >= 0) map_point_matches[match[i]] = kf.map_points[i];
+  return nm;
+}
+
+// ---- OrbMatcher::SearchByBoW(KeyFrame* pKF1, KeyFrame* pKF2, vector<MapPoint*>& vpMatches12)
+// (orb_matcher.cpp:499-632): LoopCloser::ComputeSim3 (loop_closer.cpp:327, OrbMatcher(0.75,
+// true)). matches12[i] = pKF2's map point matched to pKF1 feature i, or -1.
+inline int search_by_bow(const KeyFrameView& kf1, const KeyFrameFeatures& f1,
+                         const KeyFrameView& kf2, const KeyFrameFeatures& f2,
+                         const MapPointView* mps, float nnratio, bool check_ori,
+                         std::vector<int32_t>& matches12) {
+  const std::vector<uint8_t> v1 = good_map_point_mask(kf1, mps), v2 = good_map_point_mask(kf2, mps);
+  const slamgpu_bow_set a = bow_set(f1.desc, kf1.undist_kps, v1.data(), kf1.n_kps, f1.fv);
+  const slamgpu_bow_set b = bow_set(f2.desc, kf2.undist_kps, v2.data(), kf2.n_kps, f2.fv);
+  std::vector<int32_t> match(kf1.n_kps > 0 ? kf1.n_kps : 1);
+  int nm = 0;
+  throw_if(slamgpu_search_by_bow(&a, &b, 1, nnratio, check_ori ? 1 : 0, match.data(), &nm),
+           slamgpu_bow_last_error);
+  matches12.assign(kf1.n_kps, -1);
+  for (int i = 0; i < kf1.n_kps; ++i)
+    if (match[i] >= 0) matches12[i] = kf2.map_points[match[i]];
+  return nm;
+}
+
+// The matchers' record of one keyframe (pose split as KeyFrame::GetRotation / GetTranslation
+// return it; has_mp[i] = GetMapPoint(i) != NULL, bad or not, as SearchForTriangulation tests it).
+struct KfRecord {
+  slamgpu_kf kf;
+  std::vector<uint8_t> has_mp;
+};
+inline KfRecord kf_record(const KeyFrameView& v, const KeyFrameFeatures& f) {
+  KfRecord r;
+  r.has_mp.resize(v.n_kps > 0 ? v.n_kps : 1);
+  for (int i = 0; i < v.n_kps; ++i) r.has_mp[i] = v.map_points[i] >= 0;
+  slamgpu_kf& k = r.kf;
+  std::memset(&k, 0, sizeof(k));
+  k.kps = v.undist_kps;
+  k.desc = f.desc;
+  k.u_right = v.right_coords;
+  k.has_mp = r.has_mp.data();
+  k.nodes = f.fv.nodes;
+  k.node_start = f.fv.node_start;
+  k.node_feats = f.fv.node_feats;
+  k.n = v.n_kps;
+  k.n_nodes = f.fv.n_nodes;
+  for (int r0 = 0; r0 < 3; ++r0) {
+    for (int c = 0; c < 3; ++c) k.Rcw[3 * r0 + c] = v.Tcw[4 * r0 + c];
+    k.tcw[r0] = v.Tcw[4 * r0 + 3];
+    k.Ow[r0] = f.Ow[r0];
+  }
+  return r;
+}
+
+// ---- OrbMatcher::SearchForTriangulation (orb_matcher.cpp:634-802) as LocalMapper::
+// CreateNewMapPoints calls it (local_mapper.cpp:312, OrbMatcher(0.6, false), only_stereo =
+// false): F12 from LocalMapper::ComputeFundamentalMatrix; cam / lv = pKF2's calibration and
+// level tables. Returns vMatchedPairs: (pKF1 index, pKF2 index), ascending pKF1 index.
+inline std::vector<std::pair<int, int>> search_for_triangulation(
+    const KeyFrameView& kf1, const KeyFrameFeatures& f1, const KeyFrameView& kf2,
+    const KeyFrameFeatures& f2, const float F12[9], const slamgpu_camera& cam,
+    const slamgpu_levels& lv, bool only_stereo, bool check_ori) {
+  const KfRecord r1 = kf_record(kf1, f1), r2 = kf_record(kf2, f2);
+  std::vector<int32_t> match(kf1.n_kps > 0 ? kf1.n_kps : 1);
+  int nm = 0;
+  throw_if(slamgpu_search_for_triangulation(&r1.kf, &r2.kf, F12, &cam, &lv, only_stereo ? 1 : 0,
+                                            check_ori ? 1 : 0, match.data(), &nm),
+           slamgpu_kfmatch_last_error);
+  std::vector<std::pair<int, int>> pairs;
+  for (int i = 0; i < kf1.n_kps; ++i)
+    if (match[i] >= 0) pairs.emplace_back(i, match[i]);
+  return pairs;
+}
+
+// ---- OrbMatcher::Fuse(KeyFrame* pKF, const vector<MapPoint*>& vpMapPoints, float th)
+// (orb_matcher.cpp:804-954), LocalMapper::SearchInNeighbors (local_mapper.cpp:521, 540).
+// What Fuse reads of a map point beyond MapPointView: GetNormal(), min_dist_ / max_dist_ and
+// NumObservations() (the stereo-weighted count AddObservation keeps, map_point.cpp:114-125).
+struct MapPointGeometry {
+  float normal[3];
+  float min_dist, max_dist;
+  int32_t num_observations;
+};
+
+// The object-graph changes of one Fuse call, in the reference's order, for the caller to apply
+// to its MapPoints / KeyFrame:
+//   kReplaceByKf:  point->Replace(other)   (other = the keyframe's map point, more observations)
+//   kReplaceKf:    other->Replace(point)
+//   kAdd:          point->AddObservation(pKF, keypoint); pKF->AddMapPoint(point, keypoint)
+//   kNone:         the keyframe's map point at keypoint is bad: nothing (still counted as fused)
+struct FuseAction {
+  enum Kind : int32_t { kNone = 0, kReplaceByKf = 1, kReplaceKf = 2, kAdd = 3 };
+  int32_t kind, point, other, keypoint;
+};
+struct FuseResult {
+  int nfused = 0;
+  std::vector<FuseAction> actions;
+};
+
+// The reference checks isBad() and IsInKeyFrame(pKF) of each offered point when the loop reaches
+// it, after the Replace / AddObservation calls of earlier points (:821-828). The device search
+// of a point does not depend on those calls (it reads the keyframe's keypoints, not its map
+// points), so the candidates are searched once with the skip state at the start, and the walk
+// below replays the loop on a model of the state those calls change: bad flags, the keyframe's
+// slots, each touched point's keyframes and observation count (Replace, map_point.cpp:190-226:
+// the survivor takes the other's observations in keyframes it is not in and the other's slot
+// there; where both were, the keyframe drops the replaced point's slot).
+inline FuseResult fuse(int kf_index, const KeyFrameView* kfs, const KeyFrameFeatures& kff,
+                       const MapPointView* mps, const MapPointGeometry* geom, int n_mp,
+                       const int32_t* points, int n_points, float th, const slamgpu_camera& cam,
+                       const slamgpu_levels& lv, const slamgpu_kf_grid& grid) {
+  const KeyFrameView& kf = kfs[kf_index];
+  auto in_kf0 = [&](int m) {
+    for (int o = 0; o < mps[m].n_obs; ++o)
+      if (mps[m].obs[o].keyframe == kf_index) return true;
+    return false;
+  };
+  std::vector<slamgpu_fuse_point> pts(n_points > 0 ? n_points : 1);
+  for (int i = 0; i < n_points; ++i) {
+    slamgpu_fuse_point& q = pts[i];
+    std::memset(&q, 0, sizeof(q));
+    const int m = points[i];
+    q.skip = m < 0 || mps[m].bad || in_kf0(m);
+    if (m < 0) continue;
+    std::memcpy(q.xyz, mps[m].xyz, sizeof(q.xyz));
+    std::memcpy(q.normal, geom[m].normal, sizeof(q.normal));
+    q.min_dist = geom[m].min_dist;
+    q.max_dist = geom[m].max_dist;
+    std::memcpy(q.desc, mps[m].desc, 32);
+  }
+  const KfRecord rec = kf_record(kf, kff);
+  std::vector<int32_t> best(n_points > 0 ? n_points : 1), dist(n_points > 0 ? n_points : 1);
+  int nf = 0;
+  throw_if(slamgpu_fuse(&rec.kf, pts.data(), n_points, th, &cam, &lv, &grid, best.data(),
+                        dist.data(), &nf),
+           slamgpu_kfmatch_last_error);
+  // the model: touched points' keyframe -> keypoint maps, counts and bad flags
+  std::vector<uint8_t> bad(n_mp);
+  std::vector<int32_t> nobs(n_mp);
+  std::vector<std::vector<ObsRef>> obs(n_mp);
+  std::vector<uint8_t> loaded(n_mp, 0);
+  for (int m = 0; m < n_mp; ++m) {
+    bad[m] = mps[m].bad;
+    nobs[m] = geom[m].num_observations;
+  }
+  auto load = [&](int m) -> std::vector<ObsRef>& {
+    if (!loaded[m]) {
+      obs[m].assign(mps[m].obs, mps[m].obs + mps[m].n_obs);
+      loaded[m] = 1;
+    }
+    return obs[m];
+  };
+  std::vector<int32_t> slot(kf.map_points, kf.map_points + kf.n_kps);  // pKF->GetMapPoint(i)
+  auto find = [](const std::vector<ObsRef>& o, int k) {
+    for (size_t j = 0; j < o.size(); ++j)
+      if (o[j].keyframe == k) return (int)j;
+    return -1;
+  };
+  auto weight = [&](int k, int idx) { return kfs[k].right_coords[idx] >= 0 ? 2 : 1; };
+  // this->Replace(point): map_point.cpp:190-226, on the model
+  auto replace = [&](int victim, int survivor) {
+    if (victim == survivor) return;
+    bad[victim] = 1;
+    std::vector<ObsRef>& vo = load(victim);
+    std::vector<ObsRef>& so = load(survivor);
+    for (const ObsRef& r : vo) {
+      if (find(so, r.keyframe) < 0) {  // ReplaceMapPointMatch + AddObservation
+        if (r.keyframe == kf_index) slot[r.keypoint] = survivor;
+        so.push_back(r);
+        nobs[survivor] += weight(r.keyframe, r.keypoint);
+      } else if (r.keyframe == kf_index) {  // EraseMapPointMatch
+        slot[r.keypoint] = -1;
+      }
+    }
+    vo.clear();
+  };
+  FuseResult res;
+  for (int i = 0; i < n_points; ++i) {
+    const int m = points[i];
+    if (m < 0 || bad[m] || find(load(m), kf_index) >= 0) continue;  // :821-828
+    if (best[i] < 0) continue;                                       // bestDist > TH_LOW
+    const int j = best[i], cur = slot[j];
+    FuseAction a{FuseAction::kNone, m, cur, j};
+    if (cur >= 0) {
+      if (!bad[cur]) {
+        if (nobs[cur] > nobs[m]) {
+          a.kind = FuseAction::kReplaceByKf;
+          replace(m, cur);
+        } else {
+          a.kind = FuseAction::kReplaceKf;
+          replace(cur, m);
+        }
+      }
+    } else {
+      a.kind = FuseAction::kAdd;
+      load(m).push_back(ObsRef{kf_index, j});
+      nobs[m] += weight(kf_index, j);
+      slot[j] = m;
+    }
+    res.actions.push_back(a);
+    res.nfused++;
+  }
+  return res;
+}
+
+// ---- Optimizer::OptimizeSim3 (optimizer.cpp:962-1152), LoopCloser::ComputeSim3
+// (loop_closer.cpp:393): the correspondences of :1020-1096 -- match i kept when both map points
+// exist, are not bad and pKF2 observes the second (GetIndexInKeyFrame(pKF2) >= 0) -- with the
+// points in their keyframes' camera frames as the f32 cv::Mat expression R*X + t forms them
+// (one gemm: float dot, then (float)((double)dot + (double)t)).
+struct Sim3Problem {
+  std::vector<slamgpu_sim3_match> matches;
+  std::vector<int32_t> match_index;  // i of each correspondence
+};
+inline float cv_gemm_row(const float* T, int r, const float* x) {
+  const float dot = T[4 * r] * x[0] + T[4 * r + 1] * x[1] + T[4 * r + 2] * x[2];
+  return (float)((double)dot + (double)T[4 * r + 3]);
+}
+inline Sim3Problem gather_optimize_sim3(int kf1_index, int kf2_index, const KeyFrameView* kfs,
+                                        const MapPointView* mps, const int32_t* matches1, int n) {
+  const KeyFrameView& kf1 = kfs[kf1_index];
+  const KeyFrameView& kf2 = kfs[kf2_index];
+  Sim3Problem p;
+  for (int i = 0; i < n; ++i) {
+    const int m2 = matches1[i];
+    if (m2 < 0) continue;
+    const int m1 = kf1.map_points[i];
+    if (m1 < 0) continue;
+    int i2 = -1;
+    for (int o = 0; o < mps[m2].n_obs; ++o)
+      if (mps[m2].obs[o].keyframe == kf2_index) i2 = mps[m2].obs[o].keypoint;
+    if (mps[m1].bad || mps[m2].bad || i2 < 0) continue;
+    slamgpu_sim3_match c;
+    for (int r = 0; r < 3; ++r) {
+      c.x1c[r] = cv_gemm_row(kf1.Tcw, r, mps[m1].xyz);
+      c.x2c[r] = cv_gemm_row(kf2.Tcw, r, mps[m2].xyz);
+    }
+    c.u1 = kf1.undist_kps[i].x;
+    c.v1 = kf1.undist_kps[i].y;
+    c.u2 = kf2.undist_kps[i2].x;
+    c.v2 = kf2.undist_kps[i2].y;
+    c.octave1 = kf1.undist_kps[i].octave;
+    c.octave2 = kf2.undist_kps[i2].octave;
+    p.matches.push_back(c);
+    p.match_index.push_back(i);
+  }
+  return p;
+}
+// The whole call: matches1 (vpMatches1: pKF2's map point per pKF1 feature, -1 none) is updated
+// as the reference nulls its outliers (:1103-1106, :1135-1140; also on the early return); S12
+// (qx, qy, qz, qw, tx, ty, tz, s) is updated unless the reference returns early. Returns nIn.
+inline int optimize_sim3(int kf1_index, int kf2_index, const KeyFrameView* kfs,
+                         const MapPointView* mps, int32_t* matches1, int n, const float K1[4],
+                         const float K2[4], const float* inv_sigma2_1, const float* inv_sigma2_2,
+                         int nlevels, double S12[8], float th2, bool fix_scale) {
+  const Sim3Problem p = gather_optimize_sim3(kf1_index, kf2_index, kfs, mps, matches1, n);
+  std::vector<uint8_t> inl(p.matches.size() + 1, 1);
+  int n_in = 0;
+  throw_if(slamgpu_optimize_sim3(K1, K2, inv_sigma2_1, inv_sigma2_2, nlevels, p.matches.data(),
+                                 (int)p.matches.size(), th2, fix_scale ? 1 : 0, S12, inl.data(),
+                                 &n_in),
+           slamgpu_optimizer_last_error);
+  for (size_t c = 0; c < p.matches.size(); ++c)
+    if (!inl[c]) matches1[p.match_index[c]] = -1;
+  return n_in;
+}
+
+// ---- Optimizer::BundleAdjustment (optimizer.cpp:33-207), GlobalBundleAdjustemnt (:18-31) ----
+// Vertices: every keyframe that is not bad (fixed when Id() == 0), every map point that is not
+// bad with its observations in GetObservations() order, skipping bad keyframes. A point left
+// with no edge is still a vertex here and stays where it is (the device leaves points without
+// observations out of the system, as :149-152 does).
+inline LocalBaGraph gather_global_bundle_adjustment(const KeyFrameView* kfs, int n_kf,
+                                                    const MapPointView* mps, int n_mp) {
+  LocalBaGraph g;
+  std::vector<int32_t> vertex_of(n_kf, -1);
+  for (int k = 0; k < n_kf; ++k) {
+    if (kfs[k].bad) continue;
+    vertex_of[k] = (int32_t)g.keyframe.size();
+    g.keyframe.push_back(k);
+    g.kf_Tcw.insert(g.kf_Tcw.end(), kfs[k].Tcw, kfs[k].Tcw + 16);
+    g.kf_mode.push_back(kfs[k].id == 0 ? SLAMGPU_KF_LOCAL_FIXED : SLAMGPU_KF_LOCAL);
+  }
+  g.n_local = (int)g.keyframe.size();
+  g.point_obs_start.push_back(0);
+  for (int m = 0; m < n_mp; ++m) {
+    if (mps[m].bad) continue;
+    g.map_point.push_back(m);
+    g.points.insert(g.points.end(), mps[m].xyz, mps[m].xyz + 3);
+    for (int o = 0; o < mps[m].n_obs; ++o) {
+      const ObsRef r = mps[m].obs[o];
+      if (kfs[r.keyframe].bad) continue;
+      const slamgpu_keypoint& kp = kfs[r.keyframe].undist_kps[r.keypoint];
+      slamgpu_ba_obs e;
+      e.keyframe = vertex_of[r.keyframe];
+      e.u = kp.x;
+      e.v = kp.y;
+      e.ur = kfs[r.keyframe].right_coords[r.keypoint];
+      e.octave = kp.octave;
+      g.obs.push_back(e);
+      g.obs_ref.push_back(r);
+    }
+    g.point_obs_start.push_back((int32_t)g.obs.size());
+  }
+  return g;
+}
+// The whole call: gather, solve (optimised keyframe poses and point positions written into the
+// graph: the caller stores them as the reference's :170-206 does), LM iterations run.
+inline int global_bundle_adjustment(LocalBaGraph& g, const slamgpu_camera& cam,
+                                    const float* inv_sigma2, int nlevels, int n_iterations,
+                                    bool robust, const volatile bool* stop_flag) {
+  int its = 0;
+  throw_if(slamgpu_global_bundle_adjustment(&cam, inv_sigma2, nlevels, g.kf_Tcw.data(),
+                                            g.kf_mode.data(), (int)g.keyframe.size(),
+                                            g.points.data(), (int)g.map_point.size(),
+                                            g.point_obs_start.data(), g.obs.data(), n_iterations,
+                                            robust ? 1 : 0, stop_flag, &its),
+           slamgpu_optimizer_last_error);
+  return its;
+}
 
 }  // namespace slamgpu_adapter

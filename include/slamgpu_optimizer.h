@@ -262,6 +262,11 @@ int slamgpu_optimize_essential_graph(int n_kf, double* Scw, const uint8_t* fixed
 
 const char* slamgpu_optimizer_last_error(void);
 
+/* Diagnostic: the work-groups the cooperative BA solves running on `device` hold right now (the
+ * residency budget shared by slamgpu_local_bundle_adjustment / slamgpu_global_bundle_adjustment
+ * calls on concurrent threads, as the reference's LocalMapper and LoopCloser run them). */
+int slamgpu_coop_slots_in_use(int device);
+
 #ifdef __cplusplus
 }
 #endif

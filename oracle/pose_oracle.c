@@ -128,9 +128,17 @@ static void compute_active_errors(problem* P, const se3* T) {
     if (P->active[k]) P->chi2[k] = edge_error(&P->E[k], T, P->cam, &P->err[3 * k]);
 }
 
+// Diagnostic only (tools/pose_schedule.py): 1 sums the chi2 and the normal equations over the
+// edges in reverse order -- a different rounding of the same sums -- to measure how often the LM
+// schedule (iteration count) depends on the summation order alone. 0 (default): g2o's order.
+static int g_sum_reverse = 0;
+void oc_pose_set_sum_reverse(int on) { g_sum_reverse = on; }
+#define EDGE_LOOP(k, n) for (int k##_ = 0, k = g_sum_reverse ? (n) - 1 : 0; k##_ < (n); \
+                             k##_++, k = g_sum_reverse ? (n) - 1 - k##_ : k##_)
+
 static double active_robust_chi2(const problem* P) {
   double chi = 0.0;
-  for (int k = 0; k < P->n; k++) {
+  EDGE_LOOP(k, P->n) {
     if (!P->active[k]) continue;
     if (P->robust[k]) {
       double rho[3];
@@ -146,7 +154,7 @@ static double active_robust_chi2(const problem* P) {
 static void build_system(const problem* P, const se3* T, double H[36], double b[6]) {
   memset(H, 0, 36 * sizeof(double));
   memset(b, 0, 6 * sizeof(double));
-  for (int k = 0; k < P->n; k++) {
+  EDGE_LOOP(k, P->n) {
     if (!P->active[k]) continue;
     const edge* E = &P->E[k];
     double J[18];

@@ -70,17 +70,22 @@ def build(force: bool = False, verbose: bool = False) -> str:
 ROOT = os.path.dirname(PKG)
 CAPI_SRC = os.path.join(ROOT, "tests", "capi_check.cpp")
 CAPI_BIN = os.path.join(ROOT, "tests", "capi_check")
+CAPI_KF_SRC = os.path.join(ROOT, "tests", "capi_kf_check.cpp")
+CAPI_KF_BIN = os.path.join(ROOT, "tests", "capi_kf_check")
 
 
 def build_capi_check() -> str:
-    """g++ build of tests/capi_check.cpp against include/*.h, linked to libslamgpu.so: the C++
-    caller side of the drop-in boundary, with no HIP or Python in between."""
-    if os.path.exists(CAPI_BIN) and os.path.getmtime(CAPI_BIN) >= max(
-            os.path.getmtime(CAPI_SRC), os.path.getmtime(LIB)):
-        return CAPI_BIN
-    subprocess.run(["g++", "-O2", "-std=c++17", "-Wall", "-I", os.path.join(ROOT, "include"),
-                    CAPI_SRC, "-L", PKG, "-lslamgpu",
-                    "-Wl,-rpath,$ORIGIN/../slam_framework_amd", "-o", CAPI_BIN], check=True)
+    """g++ builds of tests/capi_check.cpp and tests/capi_kf_check.cpp against include/*.h*,
+    linked to libslamgpu.so: the C++ caller side of the drop-in boundary, with no HIP or Python
+    in between."""
+    headers = glob.glob(os.path.join(ROOT, "include", "*.h*"))
+    for src, exe in ((CAPI_SRC, CAPI_BIN), (CAPI_KF_SRC, CAPI_KF_BIN)):
+        if os.path.exists(exe) and os.path.getmtime(exe) >= max(
+                os.path.getmtime(d) for d in [src, LIB] + headers):
+            continue
+        subprocess.run(["g++", "-O2", "-std=c++17", "-Wall", "-I", os.path.join(ROOT, "include"),
+                        src, "-L", PKG, "-lslamgpu",
+                        "-Wl,-rpath,$ORIGIN/../slam_framework_amd", "-o", exe], check=True)
     return CAPI_BIN
 
 

@@ -312,20 +312,46 @@ __global__ __launch_bounds__(256) void stereo_match_kernel(ImageBatch b,
   __builtin_amdgcn_wave_barrier();
   const uint8_t* wb = reinterpret_cast<const uint8_t*>(&win[0][0]);  // row r at 44 r
   if (ok) {
+    // A task (offset k, window row yr) sums |(IL - cl) - (IR - cr)| over 11 pixels as v_sad_u16
+    // on u16 pairs: (IL + 512) - (IR + 512 + cl - cr); v_perm builds each pair with the +512 bias
+    // bytes taken from a constant operand, and a 12th pair element is made equal on both sides.
+    const uint32_t* ww = &win[0][0];
+    const int oL = xcl - w - al, oR0 = xcr - L - w - ar;  // byte offsets of the rows (0..3)
+    const int cl = wb[44 * w + (xcl - al)];
+    constexpr uint32_t kBias = 0x02020202u;  // bias bytes: 0x0202 = 514 per u16 half
 #pragma unroll
     for (int rnd = 0; rnd < kRounds; rnd++) {
       const int p = hl + G * rnd;
       if (p < 121) {
-        const int k = p / 11, yy = p - 11 * k - w;
-        const int incR = k - L;
-        const int cl = wb[44 * w + (xcl - al)];
-        const int cr = wb[44 * w + 16 + (xcr + incR - ar)];
-        const uint8_t* rl = wb + 44 * (yy + w) + (xcl - w - al);
-        const uint8_t* rr = wb + 44 * (yy + w) + 16 + (xcr + incR - w - ar);
-        int acc = 0;
+        const int k = p / 11, yr = p - 11 * k;  // offset k - L, window row yr - w
+        const int cr = wb[44 * w + 16 + (xcr + k - L - ar)];
+        const uint32_t* rowL = ww + 11 * yr;
+        const int oR = oR0 + k;  // 0..13: the right row's bytes oR .. oR + 10 (of 28)
+        const uint32_t* rowR = rowL + 4 + (oR >> 2);
+        const uint32_t l0 = rowL[0], l1 = rowL[1], l2 = rowL[2], l3 = rowL[3];
+        const uint32_t r0 = rowR[0], r1 = rowR[1], r2 = rowR[2], r3 = rowR[3];
+        const uint32_t a[3] = {__builtin_amdgcn_alignbyte(l1, l0, oL),
+                               __builtin_amdgcn_alignbyte(l2, l1, oL),
+                               __builtin_amdgcn_alignbyte(l3, l2, oL)};
+        const uint32_t bsh = (uint32_t)(oR & 3);
+        const uint32_t bb[3] = {__builtin_amdgcn_alignbyte(r1, r0, bsh),
+                                __builtin_amdgcn_alignbyte(r2, r1, bsh),
+                                __builtin_amdgcn_alignbyte(r3, r2, bsh)};
+        // cl - cr added to each u16 half (v_pk_add_u16 wraps per half; every sum lies in
+        // [257, 1022]): the last pair's high half stays the bias on both sides
+        typedef unsigned short u16x2_t __attribute__((ext_vector_type(2)));
+        const unsigned short d = (unsigned short)(cl - cr);
+        const u16x2_t dd = {d, d}, dlast = {d, 0};
+        uint32_t acc = 0;
 #pragma unroll
-        for (int xx = 0; xx < 2 * w + 1; xx++) acc += abs((rl[xx] - cl) - (rr[xx] - cr));
-        part[p] = acc;
+        for (int j = 0; j < 6; j++) {
+          const uint32_t sel = j == 5 ? 0x04040402u : (j & 1) ? 0x04030402u : 0x05010400u;
+          const uint32_t A = __builtin_amdgcn_perm(kBias, a[j >> 1], sel);
+          const u16x2_t B = __builtin_bit_cast(u16x2_t, __builtin_amdgcn_perm(kBias, bb[j >> 1], sel)) +
+                            (j == 5 ? dlast : dd);
+          acc = __builtin_amdgcn_sad_u16(A, __builtin_bit_cast(uint32_t, B), acc);
+        }
+        part[p] = (int)acc;
       }
     }
   }
@@ -708,15 +734,70 @@ struct FrameView {
   const uint8_t* blocked;
 };
 
-__device__ int scan_query(const ScanCtx& c, const Camera& cam, const FrameView& F,
-                          const uint32_t* claimed, uint64_t* top, int lane) {
+// Wave reductions over the lanes by the permlane / DPP butterfly of lane_partner_u32 (no LDS
+// round trips; every lane ends with the result). Keys are compared as unsigned integers.
+__device__ __forceinline__ uint32_t wave_min_key(uint32_t v) {
+#pragma unroll
+  for (int M = 32; M >= 1; M >>= 1) v = min(v, lane_partner_u32(v, M));
+  return v;
+}
+__device__ __forceinline__ uint64_t wave_min_key(uint64_t v) {
+#pragma unroll
+  for (int M = 32; M >= 1; M >>= 1) {
+    const uint64_t o = (uint64_t)lane_partner_u32((uint32_t)(v >> 32), M) << 32 |
+                       lane_partner_u32((uint32_t)v, M);
+    v = o < v ? o : v;
+  }
+  return v;
+}
+__device__ __forceinline__ int wave_sum_bfly(int v) {
+#pragma unroll
+  for (int M = 32; M >= 1; M >>= 1) v += (int)lane_partner_u32((uint32_t)v, M);
+  return v;
+}
+// Inclusive prefix sum over the 64 lanes: DPP row shifts within each row of 16 lanes, then the
+// row totals carried by row_bcast:15 / row_bcast:31.
+__device__ __forceinline__ int wave_incl_scan(int v) {
+  v += __builtin_amdgcn_update_dpp(0, v, 0x111, 0xf, 0xf, true);  // row_shr:1
+  v += __builtin_amdgcn_update_dpp(0, v, 0x112, 0xf, 0xf, true);  // row_shr:2
+  v += __builtin_amdgcn_update_dpp(0, v, 0x114, 0xf, 0xf, true);  // row_shr:4
+  v += __builtin_amdgcn_update_dpp(0, v, 0x118, 0xf, 0xf, true);  // row_shr:8
+  v += __builtin_amdgcn_update_dpp(0, v, 0x142, 0xa, 0xf, false);  // row_bcast:15 -> rows 1, 3
+  v += __builtin_amdgcn_update_dpp(0, v, 0x143, 0xc, 0xf, false);  // row_bcast:31 -> rows 2, 3
+  return v;
+}
+
+// The scan's candidate key, ordered as (distance, cell, index): 32 bits -- dist (<= 256) << 23 |
+// cell (< 4096) << 11 | index (< 2048) -- when the frame's keypoint capacity allows, else the 64-bit
+// form the resolution pass reads (dist << 32 | cell << 12 | index).
+template <typename K>
+__device__ __forceinline__ K scan_key(int dist, int cell, int i) {
+  if constexpr (sizeof(K) == 4)
+    return (uint32_t)dist << 23 | (uint32_t)cell << 11 | (uint32_t)i;
+  else
+    return ((uint64_t)dist << 32) | ((uint64_t)cell << 12) | (uint64_t)i;
+}
+template <typename K>
+__device__ __forceinline__ uint64_t key64(K k) {
+  if constexpr (sizeof(K) == 4)
+    return k == ~0u ? kNoKey
+                    : ((uint64_t)(k >> 23) << 32) | ((uint64_t)((k >> 11) & 0xfffu) << 12) |
+                          (uint64_t)(k & 0x7ffu);
+  else
+    return k;
+}
+
+template <typename K>
+__device__ int scan_query_k(const ScanCtx& c, const Camera& cam, const FrameView& F,
+                            const uint32_t* claimed, uint64_t* top, int lane) {
   const int nMinCellX = max(0, (int)floorf((c.x - cam.min_x - c.r) / cam.cell_w));
   const int nMaxCellX = min(kGridCols - 1, (int)ceilf((c.x - cam.min_x + c.r) / cam.cell_w));
   const int nMinCellY = max(0, (int)floorf((c.y - cam.min_y - c.r) / cam.cell_h));
   const int nMaxCellY = min(kGridRows - 1, (int)ceilf((c.y - cam.min_y + c.r) / cam.cell_h));
-  uint64_t t[kTopK];
+  constexpr K kNone = (K)~(K)0;
+  K t[kTopK];
 #pragma unroll
-  for (int k = 0; k < kTopK; k++) t[k] = kNoKey;
+  for (int k = 0; k < kTopK; k++) t[k] = kNone;
   int cnt = 0;
   if (!(nMaxCellX < 0 || nMinCellX >= kGridCols || nMaxCellY < 0 || nMinCellY >= kGridRows)) {
     const bool bCheckLevels = (c.min_level > 0) || (c.max_level >= 0);
@@ -736,14 +817,9 @@ __device__ int scan_query(const ScanCtx& c, const Camera& cam, const FrameView& 
         q0 = F.cell_start[cell];
         nq = F.cell_start[cell + 1] - q0;
       }
-      int incl = nq;  // inclusive prefix sum over the lanes
-#pragma unroll
-      for (int off = 1; off < 64; off <<= 1) {
-        const int y = __shfl_up(incl, off, 64);
-        if (lane >= off) incl += y;
-      }
+      const int incl = wave_incl_scan(nq);
       const int excl = incl - nq;
-      const int npairs = __shfl(incl, 63, 64);
+      const int npairs = __builtin_amdgcn_readlane(incl, 63);
       // every lane takes part in the shuffles (a shuffle reads 0 from an inactive lane)
       for (int k0 = 0; k0 < npairs; k0 += 64) {
         const int k = k0 + lane;
@@ -771,14 +847,14 @@ __device__ int scan_query(const ScanCtx& c, const Camera& cam, const FrameView& 
         if (ur > 0 && fabsf(c.ur - ur) > c.gate) continue;
         const int dist = hamming32(c.desc, F.desc + i * 32);
         if (dist > c.max_dist) continue;
-        const uint64_t key = ((uint64_t)dist << 32) | ((uint64_t)pcell << 12) | (uint64_t)i;
+        const K key = scan_key<K>(dist, pcell, i);
         cnt++;
         if (key < t[kTopK - 1]) {
           t[kTopK - 1] = key;
 #pragma unroll
           for (int k2 = kTopK - 1; k2 > 0; k2--)
             if (t[k2] < t[k2 - 1]) {
-              const uint64_t s2 = t[k2];
+              const K s2 = t[k2];
               t[k2] = t[k2 - 1];
               t[k2 - 1] = s2;
             }
@@ -789,15 +865,24 @@ __device__ int scan_query(const ScanCtx& c, const Camera& cam, const FrameView& 
   // merge the per-lane sorted lists: kTopK rounds of wave minimum
 #pragma unroll
   for (int k = 0; k < kTopK; k++) {
-    const uint64_t m = wave_min(t[0]);
-    if (t[0] == m && m != kNoKey) {
+    const K m = wave_min_key(t[0]);
+    if (t[0] == m && m != kNone) {
 #pragma unroll
       for (int j = 0; j < kTopK - 1; j++) t[j] = t[j + 1];
-      t[kTopK - 1] = kNoKey;
+      t[kTopK - 1] = kNone;
     }
-    top[k] = m;
+    top[k] = key64<K>(m);
   }
-  return wave_sum(cnt);
+  return wave_sum_bfly(cnt);
+}
+
+// 32-bit keys whenever the frame's keypoint indices fit 11 bits (kp_cap <= 2048: nfeatures up to
+// ~2000 with the per-level slack), the 64-bit form otherwise.
+__device__ __forceinline__ int scan_query(const ScanCtx& c, const Camera& cam, const FrameView& F,
+                                          const uint32_t* claimed, uint64_t* top, int lane,
+                                          int kp_cap) {
+  if (kp_cap <= 2048) return scan_query_k<uint32_t>(c, cam, F, claimed, top, lane);
+  return scan_query_k<uint64_t>(c, cam, F, claimed, top, lane);
 }
 
 __device__ __forceinline__ int key_idx(uint64_t k) { return (int)(k & 0xfff); }
@@ -895,7 +980,7 @@ __global__ __launch_bounds__(256) void search_cand_kernel(
   uint64_t top[kTopK];
   int n = 0;
   if (ok) {
-    n = scan_query(c, cam, F, nullptr, top, lane);
+    n = scan_query(c, cam, F, nullptr, top, lane, g->kp_cap);
   } else {
 #pragma unroll
     for (int k = 0; k < kTopK; k++) top[k] = kNoKey;
@@ -1081,7 +1166,7 @@ __global__ __launch_bounds__(64) void search_resolve_kernel(
         if constexpr (kF2F) okc = f2f_ctx(queries[qr], poses[f], cam, g, &c);
         else okc = mps_ctx(queries[qr], th, g, &c);
         uint64_t top[kTopK];
-        if (okc) scan_query(c, cam, F, claimed, top, lane);
+        if (okc) scan_query(c, cam, F, claimed, top, lane, g->kp_cap);
         const uint64_t t1 = __shfl(okc ? top[0] : kNoKey, 0, 64);
         const uint64_t t2 = __shfl(okc ? top[1] : kNoKey, 0, 64);
         commit(lane == r, t1, t2);

@@ -308,19 +308,38 @@ int coop_grid(int device, int K) {
 // barrier waits for as long as arrivals keep coming.
 class CoopSlots {
  public:
-  CoopSlots(int device, int G) : d_(device < 0 || device >= kMaxDevices ? 0 : device), g_(G) {
+  // stop: the LocalMapper's abort flag (LocalBundleAdjustment only): while the solve waits for
+  // slots it is polled every millisecond, and a raised flag ends the wait without slots -- the
+  // caller then returns as the reference does when the flag is set before optimising
+  // (optimizer.cpp:616-618).
+  CoopSlots(int device, int G, const volatile bool* stop = nullptr)
+      : d_(device < 0 || device >= kMaxDevices ? 0 : device), g_(G) {
     std::unique_lock<std::mutex> lk(m_[d_]);
     const int cap = std::max(coop_cap[d_], 1);
     g_ = std::min(g_, cap);  // (G never exceeds the cap: coop_grid)
-    cv_[d_].wait(lk, [&] { return used_[d_] + g_ <= cap; });
+    while (used_[d_] + g_ > cap) {
+      if (stop && *stop) {
+        g_ = 0;
+        stopped_ = true;
+        return;
+      }
+      cv_[d_].wait_for(lk, std::chrono::milliseconds(1));
+    }
     used_[d_] += g_;
   }
   ~CoopSlots() {
+    if (stopped_) return;
     {
       std::lock_guard<std::mutex> lk(m_[d_]);
       used_[d_] -= g_;
     }
     cv_[d_].notify_all();
+  }
+  bool stopped() const { return stopped_; }
+  static int in_use(int device) {
+    if (device < 0 || device >= kMaxDevices) return 0;
+    std::lock_guard<std::mutex> lk(m_[device]);
+    return used_[device];
   }
   CoopSlots(const CoopSlots&) = delete;
   CoopSlots& operator=(const CoopSlots&) = delete;
@@ -330,6 +349,7 @@ class CoopSlots {
   static std::condition_variable cv_[kMaxDevices];
   static int used_[kMaxDevices];
   int d_, g_;
+  bool stopped_ = false;
 };
 std::mutex CoopSlots::m_[kMaxDevices];
 std::condition_variable CoopSlots::cv_[kMaxDevices];
@@ -458,7 +478,11 @@ int coop_host(const char* what, const slamgpu_camera* cam, const float* inv_sigm
   }
   char* b = static_cast<char*>(S.buf);
   char* h = S.pin;
-  CoopSlots slots(dev, G);  // the device's residency budget for coop solves
+  CoopSlots slots(dev, G, local ? stop_flag : nullptr);  // the device's coop residency budget
+  if (slots.stopped()) {  // the LocalMapper aborted while the solve waited for slots
+    for (int e = 0; e < n_obs; e++) erase[e] = 0;
+    return 0;
+  }
   static const bool prof = getenv("SLAMGPU_BA_PROFILE") != nullptr;
   CoopWs w = coop_layout(b + o_ws, n_kf, n_points, n_obs, K, (int)pairs, G, pnnz, nullptr);
   w.free_of_kf = reinterpret_cast<const int32_t*>(b + o_free);
@@ -584,6 +608,8 @@ int slamgpu_local_bundle_adjustment(const slamgpu_camera* cam, const float* inv_
   return coop_host("local BA", cam, inv_sigma2, nlevels, kf_Tcw, kf_mode, n_kf, points, n_points,
                    point_obs_start, obs, stop_flag, erase, ph, 2, true, lm_iterations);
 }
+
+int slamgpu_coop_slots_in_use(int device) { return CoopSlots::in_use(device); }
 
 int slamgpu_global_bundle_adjustment(const slamgpu_camera* cam, const float* inv_sigma2,
                                      int nlevels, float* kf_Tcw, const uint8_t* kf_mode, int n_kf,

@@ -136,11 +136,46 @@ __device__ __forceinline__ void pyr_strip(const ImageBatch& b, const OrbGeom* __
     }
   };
   uint8_t* dst = b.pyr + (int64_t)img * g->pyr_bytes + D.offset;
+  const int dpitch = __builtin_amdgcn_readfirstlane(D.pitch), dw = __builtin_amdgcn_readfirstlane(D.w);
   uint32_t cur[kPyrChunk][3], nxt[kPyrChunk][3];
 #pragma unroll
   for (int j = 0; j < kPyrChunk; j++) fetch(sy_lo + j, cur[j]);
+  // hp / hc: the previous / current source row's horizontal results, already in the vertical
+  // pass's operand form (r >> 4) << 8 = (16 r) & ~0xff (once per source row, not per output row)
   uint32_t hp[4] = {0, 0, 0, 0}, hc[4] = {0, 0, 0, 0};
   int nd = 0;  // next strip row to emit
+  // one output row from source rows (r0, r1): v = ((b0*(r0>>4))>>16) + ((b1*(r1>>4))>>16) + 2)
+  // >> 2 (<= 255 for any coefficient rounding), packed by two u16 pairs, one
+  // v_pk_lshrrev_b16 each and one v_perm
+  auto emit = [&](const uint32_t (&r0)[4], const uint32_t (&r1)[4], uint32_t b0, uint32_t b1) {
+    uint32_t t[4];
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      // v_mul_hi_u32_u24 as such: the operands are < 2^24 by construction (the C helper's masks
+      // would be re-applied to the carried row, whose known bits the loop phi loses)
+      uint32_t m0, m1;
+      asm("v_mul_hi_u32_u24 %0, %1, %2" : "=v"(m0) : "s"(b0), "v"(r0[k]));
+      asm("v_mul_hi_u32_u24 %0, %1, %2" : "=v"(m1) : "s"(b1), "v"(r1[k]));
+      t[k] = m0 + m1 + 2u;
+    }
+    typedef unsigned short u16x2_t __attribute__((ext_vector_type(2)));
+    const u16x2_t two = {2, 2};
+    const uint32_t p01 = __builtin_bit_cast(uint32_t, __builtin_bit_cast(u16x2_t, t[0] | t[1] << 16) >> two);
+    const uint32_t p23 = __builtin_bit_cast(uint32_t, __builtin_bit_cast(u16x2_t, t[2] | t[3] << 16) >> two);
+    const uint32_t packed = __builtin_amdgcn_perm(p23, p01, 0x06040200u);
+    uint8_t* drow = dst + (int64_t)(dy0 + nd) * dpitch;
+    if (x0 + 4 <= dw) {
+      *reinterpret_cast<uint32_t*>(drow + x0) = packed;  // pitch is a multiple of 64
+      if (copy_rows)
+        *reinterpret_cast<uint32_t*>(copy_rows + (dy0 + nd - copy_row0) * dpitch + x0) = packed;
+    } else {
+      for (int k = 0; x0 + k < dw; k++) drow[x0 + k] = (uint8_t)(packed >> (8 * k));
+      if (copy_rows) {
+        uint8_t* crow = copy_rows + (dy0 + nd - copy_row0) * dpitch;
+        for (int k = 0; x0 + k < dw; k++) crow[x0 + k] = (uint8_t)(packed >> (8 * k));
+      }
+    }
+  };
   for (int c0 = sy_lo; c0 <= sy_hi; c0 += kPyrChunk) {
     if (c0 + kPyrChunk <= sy_hi) {
 #pragma unroll
@@ -155,35 +190,17 @@ __device__ __forceinline__ void pyr_strip(const ImageBatch& b, const OrbGeom* __
 #pragma unroll
         for (int k = 0; k < 4; k++) {
           hp[k] = hc[k];
-          hc[k] = dot2u(__builtin_amdgcn_perm(W1, W0, sel[k]), A[k], 0u);
+          hc[k] = dot2u(__builtin_amdgcn_perm(W1, W0, sel[k]), A[k], 0u) & 0xffff00u;  // 16 r < 2^23
         }
         // emit the strip rows whose lower source row is sy (rows are in y1 order)
         while (nd < nrows && __builtin_amdgcn_readlane(ry_y1, nd) == sy) {
-          const bool same = __builtin_amdgcn_readlane(ry_y0, nd) == sy;
           const uint32_t bb = (uint32_t)__builtin_amdgcn_readlane(ry_b, nd);
-          // (b * (r >> 4)) >> 16 == mulhi24(b << 8, (r >> 4) << 8), and (r >> 4) << 8 is
-          // (16 r) & ~0xff with 16 r from the scaled dot product (all operands < 2^24)
+          // (b * (r >> 4)) >> 16 == mulhi24(b << 8, (r >> 4) << 8) (all operands < 2^24)
           const uint32_t b0 = (bb & 0xffffu) << 8, b1 = (bb >> 16) << 8;
-          uint32_t packed = 0;
-#pragma unroll
-          for (int k = 0; k < 4; k++) {
-            const uint32_t r0 = (same ? hc[k] : hp[k]) & ~0xffu, r1 = hc[k] & ~0xffu;
-            const uint32_t v = (mulhi24(b0, r0) + mulhi24(b1, r1) + 2) >> 2;
-            packed |= (v & 0xffu) << (8 * k);
-          }
-          uint8_t* drow = dst + (int64_t)(dy0 + nd) * D.pitch;
-          if (x0 + 4 <= D.w) {
-            *reinterpret_cast<uint32_t*>(drow + x0) = packed;  // pitch is a multiple of 64
-            if (copy_rows)
-              *reinterpret_cast<uint32_t*>(copy_rows + (dy0 + nd - copy_row0) * D.pitch + x0) =
-                  packed;
-          } else {
-            for (int k = 0; x0 + k < D.w; k++) drow[x0 + k] = (uint8_t)(packed >> (8 * k));
-            if (copy_rows) {
-              uint8_t* crow = copy_rows + (dy0 + nd - copy_row0) * D.pitch;
-              for (int k = 0; x0 + k < D.w; k++) crow[x0 + k] = (uint8_t)(packed >> (8 * k));
-            }
-          }
+          if (__builtin_amdgcn_readlane(ry_y0, nd) == sy)  // both source rows are row sy
+            emit(hc, hc, b0, b1);
+          else
+            emit(hp, hc, b0, b1);
           nd++;
         }
       }
@@ -1107,14 +1124,37 @@ __device__ __forceinline__ void octree_global(
   }
 }
 
+// The fallback after octree_img_kernel: a small grid scans the (image, level) results for the
+// levels octree_img left at -1 (every thread checks one entry per sweep, one ballot per wave)
+// and redoes only those, one at a time per work-group. A batch whose levels all fit costs one
+// load per thread -- not a work-group (and its 41 KB of LDS) per (level, image) queued behind
+// the other stream's kernels on the batch's critical path (0.1-0.5 ms in the round-4 traces).
+constexpr int kOctFbMaxGroups = 64;
 __global__ __launch_bounds__(kOctThreads) void octree_kernel(
-    const OrbGeom* __restrict__ g, const uint32_t* __restrict__ cell_keys,
+    const OrbGeom* __restrict__ g, int n_images, const uint32_t* __restrict__ cell_keys,
     const int* __restrict__ cell_count, uint32_t* __restrict__ key_scratch,
     OctNode* __restrict__ node_scratch, uint32_t* __restrict__ oct_keys,
     int* __restrict__ oct_count, uint32_t* __restrict__ err) {
   __shared__ OctShared S;
-  octree_global<kOctThreads>(S, blockIdx.x, blockIdx.y, g, cell_keys, cell_count, key_scratch,
-                             node_scratch, oct_keys, oct_count, err);
+  __shared__ int s_todo[kOctThreads];
+  __shared__ int s_ntodo;
+  const int tid = threadIdx.x, nlev = g->nlevels;
+  const int total = n_images * nlev;  // entry e = img * nlevels + level (oct_count's layout)
+  for (int e0 = blockIdx.x * kOctThreads; e0 < total; e0 += gridDim.x * kOctThreads) {
+    if (tid == 0) s_ntodo = 0;
+    __syncthreads();
+    const int e = e0 + tid;
+    if (e < total && oct_count[e] == -1) s_todo[atomicAdd(&s_ntodo, 1)] = e;
+    __syncthreads();
+    const int nt = s_ntodo;
+    for (int i = 0; i < nt; i++) {  // octree_global re-initialises everything it uses in S
+      const int ei = s_todo[i];
+      octree_global<kOctThreads>(S, ei % nlev, ei / nlev, g, cell_keys, cell_count, key_scratch,
+                                 node_scratch, oct_keys, oct_count, err);
+      __syncthreads();
+    }
+    __syncthreads();  // every thread has read s_ntodo before the next sweep resets it
+  }
 }
 
 // ---------------------------------------------------------------------------------------
@@ -2552,7 +2592,9 @@ __global__ __launch_bounds__(256) void orient_desc_kernel(
             const float py = (float)(int)(int8_t)(pat[r] >> (16 * e + 8));
             const f32x2 sp = __builtin_elementwise_fma((f32x2){px, px}, ab, (f32x2){py, py} * nab) + magic;
             const uint32_t Y = __float_as_uint(sp.x), X = __float_as_uint(sp.y);
-            const uint32_t a = __umul24(X, 2u * kRtRows) + rt_base + (Y << 1);
+            uint32_t t;  // X * 2 kRtRows + rt_base in one v_mad_u32_u24 (X's low 24 bits)
+            asm("v_mad_u32_u24 %0, %1, %2, %3" : "=v"(t) : "v"(X), "v"(2u * kRtRows), "s"(rt_base));
+            const uint32_t a = (Y << 1) + t;
             const lds_u32* rw = (const lds_u32*)(uintptr_t)(a & ~3u);
             const uint32_t sh = Y << 4;  // alignbit takes it mod 32: 16 for an odd start (cy odd)
             const uint32_t w0 = rw[0], w1 = rw[1], w2 = rw[2], w3 = rw[3];
@@ -2733,11 +2775,13 @@ void launch_extract(const ImageBatch& b, const OrbGeomDev& gd, int n_images, hip
     SLAMGPU_LAUNCH("octree", st, octree_img_kernel, dim3(n_images), dim3(64 * g.nlevels),
                    (size_t)g.oct_lds_bytes, st, gd.dev, gd.ws.cell_keys, gd.ws.cell_count,
                    gd.ws.key_scratch, gd.ws.oct_keys, gd.ws.oct_count, gd.ws.err);
-  if (!lvl)
-    SLAMGPU_LAUNCH("octree_global", st, octree_kernel, dim3(g.nlevels, n_images),
-                   dim3(kOctThreads), 0, st, gd.dev, gd.ws.cell_keys, gd.ws.cell_count,
-                   gd.ws.key_scratch, gd.ws.node_scratch, gd.ws.oct_keys, gd.ws.oct_count,
-                   gd.ws.err);
+  if (!lvl) {
+    const int groups = std::min((g.nlevels * n_images + kOctThreads - 1) / kOctThreads,
+                                kOctFbMaxGroups);
+    SLAMGPU_LAUNCH("octree_global", st, octree_kernel, dim3(groups), dim3(kOctThreads), 0, st,
+                   gd.dev, n_images, gd.ws.cell_keys, gd.ws.cell_count, gd.ws.key_scratch,
+                   gd.ws.node_scratch, gd.ws.oct_keys, gd.ws.oct_count, gd.ws.err);
+  }
   if (n_images <= kOdSmallMaxImages) {
     constexpr int kpw = kKpPerWave / 2;
     SLAMGPU_LAUNCH("orient_desc", st, orient_desc_kernel<kpw>,

@@ -60,7 +60,7 @@ EXPORTS = [
     "slamgpu_make_vo_queries_device", "slamgpu_timing_start", "slamgpu_timing_stop",
     "slamgpu_trace_marker",
     "slamgpu_timing_read", "slamgpu_pose_optimization", "slamgpu_pose_optimization_device",
-    "slamgpu_optimizer_last_error", "slamgpu_local_bundle_adjustment",
+    "slamgpu_optimizer_last_error", "slamgpu_coop_slots_in_use", "slamgpu_local_bundle_adjustment",
     "slamgpu_local_bundle_adjustment_device", "slamgpu_local_ba_workspace_bytes",
     "slamgpu_global_bundle_adjustment", "slamgpu_optimize_sim3", "slamgpu_optimize_sim3_device",
     "slamgpu_optimize_essential_graph",
@@ -212,6 +212,8 @@ def lib():
                                              C.POINTER(ip)]
         L.slamgpu_optimizer_last_error.argtypes = []
         L.slamgpu_optimizer_last_error.restype = C.c_char_p
+        L.slamgpu_coop_slots_in_use.argtypes = [C.c_int]
+        L.slamgpu_coop_slots_in_use.restype = C.c_int
         _lib = L
     return _lib
 

@@ -12,18 +12,11 @@ import numpy as np
 import pytest
 
 from slam_framework_amd import synthetic as S
+from tolerance import assert_close
 
 pytestmark = pytest.mark.gpu
 CAM = S.KITTI_CAM
 EPS32 = np.finfo(np.float32).eps
-
-
-def assert_close(A, A_ref, A0, what):
-    A, A_ref, A0 = (np.asarray(a, np.float64) for a in (A, A_ref, A0))
-    delta = np.abs(A_ref - A0).max()
-    tol = 1e-5 * delta + 4 * EPS32 * np.maximum(np.abs(A_ref), 1.0)
-    err = np.abs(A - A_ref)
-    assert (err <= tol).all(), f"{what}: max err {err.max():.3g} (delta {delta:.3g})"
 
 
 def run_host(G, P, stop=False):

@@ -13,6 +13,8 @@ import subprocess
 import numpy as np
 import pytest
 
+from tolerance import assert_close
+
 from slam_framework_amd import build as B
 from slam_framework_amd import slamgpu as G
 from slam_framework_amd import synthetic as S
@@ -143,8 +145,7 @@ def test_cpp_caller_matches_golden_and_oracle(oracle, gpu_lib, tmp_path):
     outl = out[68:68 + len(edges)].astype(bool)
     r_o, T_o, out_o, _ = oracle.pose_optimization(CAM, isig, edges, T0)
     assert n_inl == r_o and np.array_equal(outl, out_o)
-    tol = 1e-5 * np.abs(T_o.astype(np.float64) - T0).max() + 4 * EPS32 * np.maximum(np.abs(T_o), 1)
-    assert (np.abs(T.astype(np.float64) - T_o) <= tol).all()
+    assert_close(T, T_o, T0, "PoseOptimization from C++")
     # LocalBundleAdjustment: the oracle's erase list, poses within the tolerance
     lo = np.fromfile(os.path.join(tmp_path, "lba.out"), np.uint8)
     nk, npt, no = len(P["kf_mode"]), len(P["points"]), len(P["obs"])
@@ -153,9 +154,7 @@ def test_cpp_caller_matches_golden_and_oracle(oracle, gpu_lib, tmp_path):
     er = lo[4 + 64 * nk + 12 * npt:4 + 64 * nk + 12 * npt + no].astype(bool)
     kf_o, _, er_o, its_o = oracle.local_ba(CAM, P)
     assert its > 0 and np.array_equal(er, er_o)
-    tol = 1e-5 * np.abs(kf_o.astype(np.float64) - P["kf_Tcw"]).max() + 4 * EPS32 * np.maximum(
-        np.abs(kf_o), 1)
-    assert (np.abs(kf.astype(np.float64) - kf_o) <= tol).all()
+    assert_close(kf, kf_o, P["kf_Tcw"], "LocalBundleAdjustment from C++")
     # the stereo Frame ctor through StereoFrameCore: both views, u_right / depth, undistorted
     # keypoints (= keypoints without distortion), byte for byte
     so = np.fromfile(os.path.join(tmp_path, "stereo.out"), np.uint8)

@@ -1,0 +1,313 @@
+"""The keyframe-rate surfaces from a C++ caller: tests/capi_kf_check.cpp
+reads a map of KeyFrame / MapPoint views, runs the compiled adapter cores of
+include/slamgpu_adapters.hpp (gathering, device call through the C ABI, write-back) and writes
+their results; this test restates each gathering in Python from the same map (the reference's
+loops: orb_matcher.cpp:133-262, 499-632, 634-802, 804-954; optimizer.cpp:18-207, 962-1152) and
+compares with the oracle (oracle/, the CPU restatement; parity against the reference itself is
+unpinned): SearchByBoW both overloads, SearchForTriangulation and the Fuse
+candidates bit-exact, Fuse's Replace / AddObservation walk action for action, OptimizeSim3's inlier
+count / outliers exactly and S12 to the BA tolerance, the global BA to the BA tolerance."""
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+import kf_scenario as KS
+from tolerance import assert_close
+from slam_framework_amd import build as B
+from slam_framework_amd import synthetic as S
+
+pytestmark = pytest.mark.gpu
+CAM = KS.CAM
+N_KF = 3
+
+
+def _project(T, X):
+    Xc = T[:3, :3].astype(np.float64) @ X + T[:3, 3]
+    return CAM[0] * Xc[0] / Xc[2] + CAM[2], CAM[1] * Xc[1] / Xc[2] + CAM[3], Xc[2]
+
+
+def make_map(oracle):
+    """Three keyframes (frames 0, 1, 1 of a synthetic sequence at three poses, id 0 = the fixed
+    one), map points unprojected from keyframe 0's stereo depths and seen by the others where a
+    keypoint lies within 1.5 px of their projection; a few points and keyframe slots bad."""
+    kfs, _ = KS.keyframes(oracle)
+    feats = [kfs[0], kfs[1], kfs[1]]
+    Ts = [KS.pose(0), KS.pose(1, (-0.4, 0.02, 0.1)), KS.pose(1, (-0.2, 0.0, 0.3))]
+    rng = np.random.default_rng(5)
+    K = []
+    for k, (f, T) in enumerate(zip(feats, Ts)):
+        n = len(f["desc"])
+        K.append(dict(id=k, bad=0, Tcw=T.astype(np.float32), Ow=KS.center(T),
+                      kps=np.ascontiguousarray(f["kps"]), ur=f["ur"].astype(np.float32),
+                      mp=np.full(n, -1, np.int32), desc=f["desc"],
+                      fv=tuple(np.asarray(a) for a in f["fv"])))
+    fx, fy, cx, cy, bf = CAM
+    sc = KS.levels_arrays()[0]
+    M = []
+    k0 = K[0]
+    for i in np.nonzero(feats[0]["depth"] > 0)[0]:
+        z = float(feats[0]["depth"][i])
+        kp = k0["kps"][i]
+        Xc = np.array([(kp["x"] - cx) * z / fx, (kp["y"] - cy) * z / fy, z])
+        R, t = Ts[0][:3, :3].astype(np.float64), Ts[0][:3, 3].astype(np.float64)
+        Xw = R.T @ (Xc - t)
+        Ow = k0["Ow"].astype(np.float64)
+        d = float(np.linalg.norm(Xw - Ow))
+        m = len(M)
+        M.append(dict(id=1000 + m, bad=0, xyz=Xw.astype(np.float32), desc=k0["desc"][i],
+                      obs=[(0, int(i))], normal=((Xw - Ow) / d).astype(np.float32),
+                      min_dist=np.float32(d * sc[kp["octave"]] / sc[-1]),
+                      max_dist=np.float32(d * sc[kp["octave"]])))
+        k0["mp"][i] = m
+        for k in (1, 2):
+            u, v, zc = _project(Ts[k], Xw)
+            if zc <= 0:
+                continue
+            kk = K[k]["kps"]
+            d2 = (kk["x"] - u) ** 2 + (kk["y"] - v) ** 2
+            j = int(np.argmin(d2))
+            if d2[j] < 2.25 and K[k]["mp"][j] < 0 and rng.random() < 0.7:
+                K[k]["mp"][j] = m
+                M[m]["obs"].append((k, j))
+    for m in rng.choice(len(M), len(M) // 20, replace=False):
+        M[m]["bad"] = 1
+    for P in M:
+        P["nobs"] = sum(2 if K[k]["ur"][j] >= 0 else 1 for k, j in P["obs"])
+    return K, M, Ts
+
+
+def write_map(path, K, M):
+    with open(path, "wb") as f:
+        w = lambda a, t: f.write(np.ascontiguousarray(a, t).tobytes())  # noqa: E731
+        w([len(K), len(M)], np.int32)
+        for k in K:
+            w([k["id"]], np.int64)
+            w([k["bad"]], np.int32)
+            w(k["Tcw"].reshape(-1), np.float32)
+            w(k["Ow"], np.float32)
+            w([len(k["desc"])], np.int32)
+            f.write(np.ascontiguousarray(k["kps"]).tobytes())
+            w(k["ur"], np.float32)
+            w(k["mp"], np.int32)
+            w(k["desc"], np.uint8)
+            nodes, start, feats = k["fv"]
+            w([len(nodes)], np.int32)
+            w(nodes, np.uint32)
+            w(start, np.int32)
+            w(feats, np.uint32)
+        for p in M:
+            w([p["id"]], np.int64)
+            w([p["bad"]], np.int32)
+            w(p["xyz"], np.float32)
+            w(p["desc"], np.uint8)
+            w([len(p["obs"])], np.int32)
+            w(np.array(p["obs"], np.int32).reshape(-1), np.int32)
+            w(p["normal"], np.float32)
+            w([p["min_dist"], p["max_dist"]], np.float32)
+            w([p["nobs"]], np.int32)
+
+
+def fuse_walk(K, M, kf, points, best):
+    """The reference's walk over Fuse's candidates (orb_matcher.cpp:821-951) with Replace
+    (map_point.cpp:190-226) and AddObservation (:114-125) on a copy of the map: the actions in
+    order (kind 1 = point->Replace(kf's point), 2 = kf's point->Replace(point), 3 = add, 0 = the
+    kf's point is bad) and nFused."""
+    bad = [P["bad"] for P in M]
+    obs = [dict(P["obs"]) for P in M]   # keyframe -> keypoint (one per keyframe)
+    nobs = [P["nobs"] for P in M]
+    slot = K[kf]["mp"].copy()
+    wgt = lambda k, j: 2 if K[k]["ur"][j] >= 0 else 1  # noqa: E731
+
+    def replace(victim, surv):
+        if victim == surv:
+            return
+        bad[victim] = 1
+        for k, j in list(obs[victim].items()):
+            if k not in obs[surv]:
+                if k == kf:
+                    slot[j] = surv
+                obs[surv][k] = j
+                nobs[surv] += wgt(k, j)
+            elif k == kf:
+                slot[j] = -1
+        obs[victim] = {}
+
+    actions, nf = [], 0
+    for i, m in enumerate(points):
+        if m < 0 or bad[m] or kf in obs[m] or best[i] < 0:
+            continue
+        j = int(best[i])
+        cur = int(slot[j])
+        kind = 0
+        if cur >= 0:
+            if not bad[cur]:
+                if nobs[cur] > nobs[m]:
+                    kind = 1
+                    replace(m, cur)
+                else:
+                    kind = 2
+                    replace(cur, m)
+        else:
+            kind = 3
+            obs[m][kf] = j
+            nobs[m] += wgt(kf, j)
+            slot[j] = m
+        actions.append((kind, m, cur, j))
+        nf += 1
+    return nf, actions
+
+
+def gemm_row(T, r, x):  # OpenCV small f32 gemm R*X + t: float dot, added in double
+    d = np.float32(np.float32(np.float32(T[r, 0] * x[0]) + np.float32(T[r, 1] * x[1]))
+                   + np.float32(T[r, 2] * x[2]))
+    return np.float32(np.float64(d) + np.float64(T[r, 3]))
+
+
+def test_keyframe_surfaces_from_cpp(oracle, gpu_lib, tmp_path):
+    from slam_framework_amd import kfmatch
+    from slam_framework_amd.slamgpu import SIM3_MATCH_DTYPE, BA_OBS_DTYPE
+    B.build_capi_check()
+    K, M, Ts = make_map(oracle)
+    write_map(tmp_path / "map.bin", K, M)
+    lv = kfmatch.levels()
+    grid = kfmatch.kf_grid(1241, 376)
+    sc, s2, isig, lsf = KS.levels_arrays()
+    F12 = KS.fundamental(Ts[0], Ts[1])
+    fuse_pts = np.array([m for m in K[0]["mp"] if m >= 0][::-1] + [-1], np.int32)
+    # ---- expected results, restated from the map -----------------------------------------------
+    valid = [np.array([m >= 0 and not M[m]["bad"] for m in k["mp"]], np.uint8) for k in K]
+    nm1, ma1 = oracle.search_by_bow(K[0]["desc"], K[0]["kps"], valid[0], K[0]["fv"],
+                                    K[1]["desc"], K[1]["kps"], None, K[1]["fv"], 0, 0.7, True)
+    exp_bow1 = np.full(len(K[1]["desc"]), -1, np.int32)
+    for i in np.nonzero(ma1 >= 0)[0]:
+        exp_bow1[ma1[i]] = K[0]["mp"][i]
+    nm2, ma2 = oracle.search_by_bow(K[0]["desc"], K[0]["kps"], valid[0], K[0]["fv"],
+                                    K[1]["desc"], K[1]["kps"], valid[1], K[1]["fv"], 1, 0.75, True)
+    exp_bow2 = np.where(ma2 >= 0, K[1]["mp"][np.maximum(ma2, 0)], -1).astype(np.int32)
+    m12_in = exp_bow2.copy()
+    tk = lambda k: dict(kps=k["kps"], desc=k["desc"], ur=k["ur"],  # noqa: E731
+                        mp=(k["mp"] >= 0).astype(np.uint8), fv=k["fv"])
+    T2w = np.concatenate([Ts[1][:3, :3].reshape(-1), Ts[1][:3, 3]]).astype(np.float32)
+    nmt, mt = oracle.search_for_triangulation(tk(K[0]), tk(K[1]), K[0]["Ow"], T2w, CAM[:4], sc,
+                                              s2, F12, False, True)
+    pts = np.zeros(len(fuse_pts), kfmatch.FUSE_POINT_DTYPE)
+    for i, m in enumerate(fuse_pts):
+        if m < 0:
+            pts[i]["skip"] = 1
+            continue
+        P = M[m]
+        pts[i]["xyz"], pts[i]["normal"], pts[i]["desc"] = P["xyz"], P["normal"], P["desc"]
+        pts[i]["min_dist"], pts[i]["max_dist"] = P["min_dist"], P["max_dist"]
+        pts[i]["skip"] = int(P["bad"] or any(k == 1 for k, _ in P["obs"]))
+    grid_o = oracle.grid_geom(1241, 376)
+    _, bi, _ = oracle.fuse(K[1]["kps"], K[1]["desc"], K[1]["ur"], grid_o,
+                           Ts[1][:3, :3].reshape(-1), Ts[1][:3, 3], K[1]["Ow"], CAM, sc, isig,
+                           float(lv.log_scale_factor), pts, 3.0)
+    nf_o, act_o = fuse_walk(K, M, 1, fuse_pts, bi)
+    # OptimizeSim3 (loop_closer.cpp:393 after SearchByBoW): matches1 = the KF-KF matches
+    sm = []
+    for i, m2 in enumerate(m12_in):
+        m1 = K[0]["mp"][i]
+        if m2 < 0 or m1 < 0 or M[m1]["bad"] or M[m2]["bad"]:
+            continue
+        i2 = dict(M[m2]["obs"]).get(1, -1)
+        if i2 < 0:
+            continue
+        x1 = [gemm_row(Ts[0], r, M[m1]["xyz"]) for r in range(3)]
+        x2 = [gemm_row(Ts[1], r, M[m2]["xyz"]) for r in range(3)]
+        k1, k2 = K[0]["kps"][i], K[1]["kps"][i2]
+        sm.append((x1, x2, k1["x"], k1["y"], k2["x"], k2["y"], k1["octave"], k2["octave"], i))
+    matches = np.zeros(len(sm), SIM3_MATCH_DTYPE)
+    for c, e in enumerate(sm):
+        matches[c] = e[:8]
+    T12 = Ts[0].astype(np.float64) @ np.linalg.inv(Ts[1].astype(np.float64))
+    from scipy.spatial.transform import Rotation
+    q = Rotation.from_matrix(T12[:3, :3]).as_quat()  # x, y, z, w
+    S12_0 = np.array([*q, *T12[:3, 3], 1.0])
+    K4 = np.array(CAM[:4], np.float32)
+    n_in_o, S12_o, inl_o, _ = oracle.optimize_sim3(K4, K4, isig, isig, matches, S12_0, 10.0, True)
+    exp_m12 = m12_in.copy()
+    for c, e in enumerate(sm):
+        if not inl_o[c]:
+            exp_m12[e[8]] = -1
+    # global BA: every keyframe, every good map point, observations in order
+    kfm = np.array([1 if k["id"] == 0 else 0 for k in K], np.uint8)
+    gp, gobs, gstart = [], [], [0]
+    for m, P in enumerate(M):
+        if P["bad"]:
+            continue
+        gp.append(m)
+        for k, j in P["obs"]:
+            kp = K[k]["kps"][j]
+            gobs.append((k, kp["x"], kp["y"], K[k]["ur"][j], kp["octave"]))
+        gstart.append(len(gobs))
+    prob = dict(kf_Tcw=np.stack([k["Tcw"] for k in K]), kf_mode=kfm,
+                points=np.stack([M[m]["xyz"] for m in gp]), point_obs_start=np.array(gstart),
+                obs=np.array(gobs, BA_OBS_DTYPE), inv_sigma2=isig)
+    kf_g_o, pts_g_o, its_g_o = oracle.global_ba(CAM, prob, 10, True)
+    # ---- the C++ caller --------------------------------------------------------------------------
+    with open(tmp_path / "calls.bin", "wb") as f:
+        w = lambda a, t: f.write(np.ascontiguousarray(a, t).tobytes())  # noqa: E731
+        w(CAM, np.float32)
+        f.write(bytes(lv))
+        f.write(bytes(grid))
+        w([len(isig)], np.int32)
+        w(isig, np.float32)
+        w([0, 1], np.int32), w([0.7], np.float32), w([1], np.int32)
+        w([0, 1], np.int32), w([0.75], np.float32), w([1], np.int32)
+        w([0, 1], np.int32), w(F12.reshape(-1), np.float32), w([0, 1], np.int32)
+        w([1], np.int32), w([3.0], np.float32), w([len(fuse_pts)], np.int32), w(fuse_pts, np.int32)
+        w([0, 1, len(m12_in)], np.int32), w(m12_in, np.int32), w(K4, np.float32), w(K4, np.float32)
+        w([10.0], np.float32), w([1], np.int32), w(S12_0, np.float64)
+        w([10, 1], np.int32)
+    r = subprocess.run([B.CAPI_KF_BIN, str(tmp_path)], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
+    out = np.fromfile(tmp_path / "kf.out", np.uint8)
+    o = [0]
+
+    def take(dtype, n):
+        a = out[o[0]:o[0] + np.dtype(dtype).itemsize * n].view(dtype)
+        o[0] += np.dtype(dtype).itemsize * n
+        return a
+
+    # SearchByBoW(KF, Frame), SearchByBoW(KF, KF)
+    assert take(np.int32, 1)[0] == nm1 and nm1 > 20
+    np.testing.assert_array_equal(take(np.int32, len(K[1]["desc"])), exp_bow1)
+    assert take(np.int32, 1)[0] == nm2 and nm2 > 10
+    np.testing.assert_array_equal(take(np.int32, len(K[0]["desc"])), exp_bow2)
+    # SearchForTriangulation: vMatchedPairs in ascending pKF1 order
+    npairs = take(np.int32, 1)[0]
+    pairs = take(np.int32, 2 * npairs).reshape(-1, 2)
+    exp_pairs = np.stack([np.nonzero(mt >= 0)[0], mt[mt >= 0]], 1)
+    assert npairs == nmt and nmt > 20
+    np.testing.assert_array_equal(pairs, exp_pairs)
+    # Fuse: nFused and the walk, action for action
+    nf, na = take(np.int32, 2)
+    acts = take(np.int32, 4 * na).reshape(-1, 4)
+    assert nf == nf_o and nf_o > 20
+    np.testing.assert_array_equal(acts, np.array(act_o, np.int32).reshape(-1, 4))
+    kinds = {a[0] for a in act_o}
+    assert 3 in kinds and kinds & {1, 2}, "the map exercises Replace and AddObservation"
+    # OptimizeSim3
+    n_in = take(np.int32, 1)[0]
+    S12 = take(np.float64, 8)
+    m12 = take(np.int32, len(m12_in))
+    assert n_in == n_in_o and len(sm) > 20
+    np.testing.assert_array_equal(m12, exp_m12)
+    assert_close(S12, S12_o, S12_0, "OptimizeSim3 S12")
+    # global BA: the gathered graph, then the solve
+    its = take(np.int32, 1)[0]
+    nk = take(np.int32, 1)[0]
+    assert list(take(np.int32, nk)) == list(range(N_KF))
+    kf_g = take(np.float32, 16 * nk).reshape(nk, 4, 4)
+    npt = take(np.int32, 1)[0]
+    assert list(take(np.int32, npt)) == gp
+    pts_g = take(np.float32, 3 * npt).reshape(-1, 3)
+    nob = take(np.int32, 1)[0]
+    np.testing.assert_array_equal(take(np.uint8, nob * BA_OBS_DTYPE.itemsize).view(BA_OBS_DTYPE),
+                                  prob["obs"])
+    assert its == its_g_o
+    assert_close(kf_g, kf_g_o, prob["kf_Tcw"], "global BA poses")
+    assert_close(pts_g, pts_g_o, prob["points"], "global BA points")

@@ -122,14 +122,26 @@ def test_local_ba_runs_beside_a_global_ba(oracle, gpu_lib):
         except Exception as e:  # reported by the main thread
             errors.append(e)
 
+    L = G.lib()
+    assert L.slamgpu_coop_slots_in_use(0) == 0
     th = threading.Thread(target=gba)
+    t0 = time.perf_counter()
     th.start()
-    time.sleep(0.02)  # the global BA is on the device first
+    # the LocalBA starts once the global BA holds its residency slots (past its host staging, its
+    # kernel launched or about to be): the two solves then overlap on the device
+    while L.slamgpu_coop_slots_in_use(0) == 0 and th.is_alive():
+        time.sleep(0.0005)
+    held = L.slamgpu_coop_slots_in_use(0)
+    t_lba0 = time.perf_counter()
     from test_ba_gpu import run_host
     r5 = run_host(G, P5)
     t_end["lba"] = time.perf_counter()
     th.join(timeout=60)
     assert not errors, errors
+    print(f"global BA holds {held} slots; LocalBA started {1e3 * (t_lba0 - t0):.1f} ms after it, "
+          f"ran {1e3 * (t_end['lba'] - t_lba0):.1f} ms; the global BA ended at "
+          f"{1e3 * (t_end['gba'] - t0):.1f} ms")
+    assert held >= 64, "the global BA's slots were not observed before the LocalBA started"
     assert t_end["lba"] < t_end["gba"], "the LocalBA waited for the global BA"
     kf, pts, er, its = r5
     assert its == its_5 and np.array_equal(er, er_5)

@@ -12,6 +12,7 @@
 #   pmc=GROUPFILE   one --pmc pass with the counters listed in GROUPFILE (tools/pmc_groups/)
 #   ab=LIB,LIB,...  tools/ab.py A/B of library builds (bench --steps 10), run twice
 #   py=SCRIPT[:ARGS] python3 SCRIPT ARGS (ARGS ':'-separated)
+#   pmclibs=LIB,... one --pmc pass per library build (counters: $PMC_COUNTERS), tools/pmc_libs.sh
 #   rates           tools/valu_rates (VALU issue-rate probe; build it first)
 set -o pipefail
 export TMPDIR=/tmp
@@ -26,7 +27,8 @@ for s in "$@"; do
       timeout -k 10 500 python3 -u -m pytest ${paths:-tests} -m gpu -v --timeout 200 \
         --timeout-method thread > $O/gpu_tests.log 2>&1
       rc=$?; tail -3 $O/gpu_tests.log; grep -E "FAILED|ERROR" $O/gpu_tests.log | head -20
-      [ $rc -ne 0 ] && { echo "stop: pytest rc=$rc"; exit $rc; } ;;
+      # test failures (rc 1) are reported and the call goes on; a crash, abort or timeout stops it
+      [ $rc -gt 1 ] && { echo "stop: pytest rc=$rc"; exit $rc; } ;;
     smoke)
       timeout -k 10 300 python3 -u -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 \
         || { echo "smoke rc=$?"; tail -5 $O/smoke.log; exit 1; }
@@ -66,6 +68,11 @@ for s in "$@"; do
       timeout -k 10 600 python3 -u $script ${args//:/ } > $O/$(basename $script .py).log 2>&1 \
         || { echo "py $script rc=$?"; tail -20 $O/$(basename $script .py).log; exit 1; }
       tail -20 $O/$(basename $script .py).log ;;
+    pmclibs=*)
+      spec=${s#pmclibs=}; libs=${spec//,/ }
+      bash tools/pmc_libs.sh $O/pmclibs "${PMC_COUNTERS:-SQ_INSTS_VALU SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_LDS SQ_INSTS_SALU}" $libs \
+        > $O/pmclibs.log 2>&1 || { echo "pmclibs rc=$?"; tail $O/pmclibs.log; exit 1; }
+      cat $O/pmclibs.log ;;
     rates)
       timeout -k 10 120 ./tools/valu_rates > $O/valu_rates.txt 2>&1 || { echo "rates rc=$?"; exit 1; }
       cat $O/valu_rates.txt ;;

@@ -42,6 +42,11 @@ OPK(bitop3, "v_bitop3_b32 %0, %0, %1, %2 bitop3:0xc8")
 OPK(bfe_u32, "v_bfe_u32 %0, %0, 8, 8")
 OPK(min_u32, "v_min_u32 %0, %0, %1")
 OPK(cndmask, "v_cndmask_b32 %0, %0, %1, vcc")
+OPK(cndmask_s, "v_cndmask_b32_e64 %0, %0, %1, s[4:5]")
+OPK(and_b32, "v_and_b32 %0, %0, %1")
+OPK(lshrrev, "v_lshrrev_b32 %0, 3, %0")
+OPK(sub_u32, "v_sub_u32 %0, %0, %1")
+OPK(mul_f32, "v_mul_f32 %0, %0, %1")
 OPK(udot4, "v_dot4_u32_u8 %0, %0, %1, %2")
 OPK(udot2, "v_dot2_u32_u16 %0, %0, %1, %2")
 OPK(alignbit, "v_alignbit_b32 %0, %0, %1, %2")
@@ -93,7 +98,8 @@ int main() {
   uint32_t* u = (uint32_t*)out;
 #define R(NAME) run(#NAME, k_##NAME, u)
   R(add_u32); R(xor_b32); R(mul_lo_u32); R(mul_u32_u24); R(mad_u32_u24); R(lshl_add); R(add3);
-  R(bitop3); R(bfe_u32); R(min_u32); R(cndmask); R(udot4); R(udot2); R(alignbit); R(alignbyte);
+  R(bitop3); R(bfe_u32); R(min_u32); R(cndmask); R(cndmask_s); R(and_b32); R(lshrrev); R(sub_u32);
+  R(mul_f32); R(udot4); R(udot2); R(alignbit); R(alignbyte);
   R(perm); R(lerp_u8); R(sad_u8); R(pk_add_u16); R(pk_min_i16); R(pk_mad_i16); R(pk_add_f16);
   R(pk_min_f16); R(pk_minimum3_f16); R(pk_maximum3_f16); R(max3_u32); R(add_f32); R(fma_f32);
   R(cvt_f32_u32); R(mul_hi_u24);
