@@ -24,6 +24,8 @@
 // computes the same factorisation up to rounding.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+#include <atomic>
 #include <cfloat>
 #include <cmath>
 
@@ -643,12 +645,37 @@ hipError_t launch_eg_assemble(const EgGraph& G, const EgState& W, int64_t n_bloc
   return hipGetLastError();
 }
 
+// Dynamic LDS the staged variant may take on the current device: the per-work-group limit less
+// the kernel's static arrays (s_pan and the rest, ~45 KB), at most 100 KB (the gfx950 choice);
+// queried once per device.
+static size_t eg_meta_limit() {
+  static std::atomic<int64_t> cache[64] = {};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 0;
+  int64_t v = cache[dev].load(std::memory_order_relaxed);
+  if (v == 0) {
+    int max_lds = 0;
+    hipFuncAttributes a{};
+    if (hipDeviceGetAttribute(&max_lds, hipDeviceAttributeMaxSharedMemoryPerBlock, dev) !=
+            hipSuccess ||
+        hipFuncGetAttributes(&a, reinterpret_cast<const void*>(&eg_factor_solve_kernel<true>)) !=
+            hipSuccess) {
+      (void)hipGetLastError();
+      return 0;
+    }
+    v = std::min<int64_t>(100 * 1024, (int64_t)max_lds - (int64_t)a.sharedSizeBytes);
+    v = std::max<int64_t>(v, -1);  // -1: nothing fits (cached as such)
+    cache[dev].store(v, std::memory_order_relaxed);
+  }
+  return v > 0 ? (size_t)v : 0;
+}
+
 // Dynamic LDS of the staged-structure factorisation, 0 when it does not fit beside the static
-// arrays (s_pan and the rest, ~45 KB) or a block index exceeds 31 bits.
+// arrays on this device or a block index exceeds 31 bits (then the global-memory variant runs).
 static size_t eg_meta_bytes(const EgGraph& G) {
   if (G.n_ext < 0 || G.n_blocks > INT32_MAX) return 0;
   const size_t b = 4 * (2 * (size_t)G.F + 1 + 2 * (size_t)G.n_ext);
-  return b <= 100 * 1024 ? b : 0;
+  return b <= eg_meta_limit() ? b : 0;
 }
 
 hipError_t launch_eg_factor_solve(const EgGraph& G, const EgState& W, int64_t n_blocks,

@@ -21,9 +21,6 @@
 
 namespace slamgpu {
 
-#ifndef MATCH_XCD
-#define MATCH_XCD 1
-#endif
 #ifndef STEREO_LANES  // lanes per left keypoint in stereo_match (32: two per wave, 16: four)
 #define STEREO_LANES 16
 #endif
@@ -194,12 +191,8 @@ __global__ __launch_bounds__(256) void stereo_match_kernel(ImageBatch b,
                                                            StereoWorkspace ws, StereoOut out) {
   constexpr int NPW = 64 / G;  // keypoints per wave
   constexpr int kRounds = (121 + G - 1) / G;
-#if MATCH_XCD
   int f, bx;
   xcd_image_block(&f, &bx);  // a frame's work-groups share one XCD's L2 (its right keypoints)
-#else
-  const int f = blockIdx.y, bx = blockIdx.x;
-#endif
   const int lane = threadIdx.x & 63, grp = lane / G, hl = lane % G;
   const int iL = (bx * 4 + wave_id()) * NPW + grp;
   const int il = 2 * f, ir = 2 * f + 1;
@@ -953,12 +946,8 @@ __global__ __launch_bounds__(256) void search_cand_kernel(
     FrameKps cur, const float* __restrict__ u_right, int64_t ur_stride, Camera cam,
     const OrbGeom* __restrict__ g, const Q* __restrict__ queries, const F2FPose* __restrict__ poses,
     int th, GridWorkspace gw, MatchWorkspace mw, MatchIO io) {
-#if MATCH_XCD
   int f, bx;
   xcd_image_block(&f, &bx);  // a frame's work-groups share one XCD's L2 (its grid and keypoints)
-#else
-  const int f = blockIdx.y, bx = blockIdx.x;
-#endif
   const int lane = threadIdx.x & 63;
   const int qi = bx * 4 + wave_id();
   if (qi >= io.q_count[f]) return;

@@ -77,7 +77,8 @@ static void gauss_kernel_int(int k[7]) {
 static inline int round_up(int v, int a) { return (v + a - 1) / a * a; }
 
 int compute_geometry(const OrbParams& p, int cols, int rows, OrbGeom* g,
-                     std::vector<ResizeX>* rx, std::vector<ResizeY>* ry) {
+                     std::vector<ResizeX>* rx, std::vector<ResizeY>* ry, int oct_img_lds,
+                     int oct_lvl_lds) {
   if (p.nlevels < 1 || p.nlevels > kMaxLevels || cols < 64 || rows < 64 || cols > 4095 ||
       rows > 2047 || p.nfeatures < 1)
     return -1;
@@ -251,7 +252,9 @@ int compute_geometry(const OrbParams& p, int cols, int rows, OrbGeom* g,
   g->keys_per_image = key_off;
   g->nodes_per_image = node_off;
   {  // octree_img_kernel LDS: [keys u32 x kcap][per level: 2 node lists][per level: arrays]
-    constexpr int kLdsBudget = 156 * 1024, kNodeBytes = 12, kWorkBytesPerNode = 4 + 4 * 2 + 1;
+    // gfx950: 156 KB of the 160 KB; a device with less LDS per work-group gets its own limit
+    const int kLdsBudget = std::min(156 * 1024, oct_img_lds);
+    constexpr int kNodeBytes = 12, kWorkBytesPerNode = 4 + 4 * 2 + 1;
     int off = 0;
     for (int l = 0; l < p.nlevels; l++) {
       LevelGeom& L = g->lv[l];
@@ -276,7 +279,8 @@ int compute_geometry(const OrbParams& p, int cols, int rows, OrbGeom* g,
   {  // octree_lvl_kernel LDS (one work-group per CU: the small launches have <= 128 of them)
     // per node: sort key, pt / pe / pu / vnext, processed + candidate flags, the two scan
     // prefixes, the first child's push index (+16 B alignment)
-    constexpr int kLdsBudget = 144 * 1024, kNodeBytes = 12, kWorkBytesPerNode = 4 + 4 * 2 + 2 + 16 + 2;
+    const int kLdsBudget = std::min(144 * 1024, oct_lvl_lds);
+    constexpr int kNodeBytes = 12, kWorkBytesPerNode = 4 + 4 * 2 + 2 + 16 + 2;
     int nc = 64, ccap = 0;
     for (int l = 0; l < p.nlevels; l++) {
       nc = std::max(nc, g->lv[l].oct_nc);

@@ -68,4 +68,9 @@ struct ExtractStreams {
 void launch_extract(const ImageBatch& b, const OrbGeomDev& g, int n_images, hipStream_t st,
                     const ExtractStreams& fx = ExtractStreams());
 
+// Dynamic LDS the octree kernels may take on `device`: the device's per-work-group limit less
+// each kernel's static LDS (octree_img_kernel, octree_lvl_kernel); compute_geometry sizes their
+// key capacities within these.
+hipError_t octree_lds_limits(int device, int* img_bytes, int* lvl_bytes);
+
 }  // namespace slamgpu

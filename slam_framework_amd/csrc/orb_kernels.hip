@@ -1709,9 +1709,6 @@ __global__ __launch_bounds__(64 * kMaxLevels) void octree_img_kernel(
 // output bytes; a level that does not fit its LDS falls back to octree_kernel as before.
 constexpr int kOctLvlWaves = 8, kOctLvlThreads = 64 * kOctLvlWaves;
 constexpr int kOctKpt = 16;  // key positions per thread of the passes: levels up to 8192 keys
-#ifndef OCT_PROF
-#define OCT_PROF 0
-#endif
 #ifndef OCT_LVL_MAX_IMAGES
 #define OCT_LVL_MAX_IMAGES 16
 #endif
@@ -1770,19 +1767,7 @@ __global__ __launch_bounds__(kOctLvlThreads) void octree_lvl_kernel(
   const int ncell = L.ncols * L.nrows;
   const int64_t cbase = (int64_t)img * g->cells_per_image + L.cell_base;
   int* const outc = oct_count + img * nlev + level;
-#if OCT_PROF  // diagnostic build: per-phase wall time of (image 0, levels 0 and 7), printf at the end
-  uint64_t op_t = __builtin_amdgcn_s_memrealtime();
-  const uint64_t op_t0 = op_t;
-  uint32_t op_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  int op_pass = 0;
-  auto otick = [&](int k) {
-    const uint64_t t = __builtin_amdgcn_s_memrealtime();
-    op_acc[k] += (uint32_t)(t - op_t);
-    op_t = t;
-  };
-#else
   auto otick = [](int) {};
-#endif
   uint32_t* const outk = oct_keys + (int64_t)img * g->out_per_image + L.out_base;
   // ---- 1. candidate count; a level that does not fit is done here by the global-memory
   // algorithm (octree_global, its scratch on this work-group's LDS; the host checked it fits),
@@ -2010,9 +1995,6 @@ __global__ __launch_bounds__(kOctLvlThreads) void octree_lvl_kernel(
       }
     }
     otick(1);
-#if OCT_PROF
-    op_pass++;
-#endif
     auto nidx = [&](int j) { return outer ? j : 4095 - (int)(sortk[j] & 0xfffu); };
     auto is_cand = [&](int i, const OctNodeS& nn) { return outer ? node_n(nn) > 1 : cand[i] != 0; };
     // -- the key scan: quadrant one-hots of the candidates' keys, exclusive prefix per position
@@ -2256,15 +2238,6 @@ __global__ __launch_bounds__(kOctLvlThreads) void octree_lvl_kernel(
     if (m > L.out_cap) atomicOr(err, kErrNodeOverflow);
     *outc = mout;
   }
-#if OCT_PROF
-  otick(6);
-  if (tid == 0 && img == 0 && (level == 0 || level == nlev - 1))
-    printf("[octlvl L%d] K %d m %d passes %d | us: gather %.1f sort %.1f count %.1f nproc+scan %.1f "
-           "place %.1f survivors %.1f retain %.1f | total %.1f\n", level, K, m, op_pass,
-           0.01 * op_acc[0], 0.01 * op_acc[1], 0.01 * op_acc[2], 0.01 * op_acc[3],
-           0.01 * op_acc[4], 0.01 * op_acc[5], 0.01 * op_acc[6],
-           0.01 * (double)(__builtin_amdgcn_s_memrealtime() - op_t0));
-#endif
 }
 
 // ---------------------------------------------------------------------------------------
@@ -2372,17 +2345,15 @@ __global__ __launch_bounds__(256) void orient_desc_kernel(
     klev[j] = __builtin_amdgcn_readlane(my_level, jj);
   }
   const int in_pitch = __builtin_amdgcn_readfirstlane(b.in_pitch);
-  // Phases 1-2: the IC_Angle patches (raw level, registers), PH12_SPLIT keypoints at a time,
+  // Phases 1-2: the IC_Angle patches (raw level, registers), kPh12Split keypoints at a time,
   // then their moments (lane 8j ends up with keypoint j's)
-#ifndef PH12_SPLIT
-#define PH12_SPLIT 4
-#endif
+  constexpr int kPh12Split = 4;
   int mv[16];
 #pragma unroll
-  for (int j0 = 0; j0 < kKpPerWave; j0 += PH12_SPLIT) {
-    uint32_t raw[PH12_SPLIT][5];
+  for (int j0 = 0; j0 < kKpPerWave; j0 += kPh12Split) {
+    uint32_t raw[kPh12Split][5];
 #pragma unroll
-    for (int jj = 0; jj < PH12_SPLIT; jj++) {
+    for (int jj = 0; jj < kPh12Split; jj++) {
       const int j = j0 + jj;
 #pragma unroll
       for (int k = 0; k < 5; k++) raw[jj][k] = 0;
@@ -2405,7 +2376,7 @@ __global__ __launch_bounds__(256) void orient_desc_kernel(
       }
     }
 #pragma unroll
-    for (int jj = 0; jj < PH12_SPLIT; jj++) {
+    for (int jj = 0; jj < kPh12Split; jj++) {
       const int j = j0 + jj;
       const int a = (key_x(kkey[j]) + kMinBorder - 15) & 3;
       uint32_t s = 0, t = 0;
@@ -2418,7 +2389,7 @@ __global__ __launch_bounds__(256) void orient_desc_kernel(
       mv[2 * j] = (int)t - 20 * (int)s;
       mv[2 * j + 1] = hv * (int)s;
     }
-    if (PH12_SPLIT < kKpPerWave) __asm__ volatile("" ::: "memory");
+    if (kPh12Split < kKpPerWave) __asm__ volatile("" ::: "memory");
   }
   int mom = reduce_scatter16(mv, lane);
   const int m01 = __builtin_amdgcn_mov_dpp(mom, 0x104, 0xf, 0xf, false);  // row_shl:4
@@ -2564,16 +2535,16 @@ __global__ __launch_bounds__(256) void orient_desc_kernel(
       const float cj = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(ca), 8 * j));
       const float sj = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(sa), 8 * j));
       const f32x2 ab = {sj, cj}, nab = {cj, -sj};
-      // A sample's 7 row sums are u16 (cx, cy .. cy + 6) of the table: three dword reads at the
-      // sample's u16 address (2-byte aligned: DS reads of 32 bits run unaligned at full rate,
-      // MI355X_MICROARCH / cdna_hip_programming G17) give the u16 pairs (R0, R1), (R2, R3),
-      // (R4, R5) for v_dot2 as they are, and a fourth gives (R6, R7) -- R7 meets K0's zero high
-      // half (the table's spare rows and columns keep the read inside the window). The reads are
-      // volatile so that the compiler cannot merge them into a b96 read, which misaligned
-      // replays at 64 cycles.
+      // A sample's 7 row sums are u16 (cx, cy .. cy + 6) of the table: four aligned dword reads
+      // at (a & ~3) cover them, and v_alignbit by 16 (cy odd) or 0 (cy even) shifts the pairs into
+      // (R0, R1), (R2, R3), (R4, R5), (R6, R7) for v_dot2 -- R7 meets K0's zero high half (the
+      // table's spare rows and columns keep the reads inside the window). The parity of the u16
+      // address is cy's parity only because a column holds an even number of u16 (kRtRows even,
+      // asserted below); alignbit takes the shift Y << 4 mod 32.
       // The address comes straight from the rounded coordinates' float bits X = M + cx,
       // Y = M + cy (M = 0x4B400000, low 24 bits 0x400000): 2 (cx kRtRows + cy) =
       // umul24(X, 2 kRtRows) + 2 Y - (2 kRtRows 0x400000 + 2 M), all modulo 2^32.
+      static_assert((kRtRows & 1) == 0, "the u16 address parity must equal cy's parity");
       typedef __attribute__((address_space(3))) const uint32_t lds_u32;
       const uint32_t rt_base =
           (uint32_t)(uintptr_t)(__attribute__((address_space(3))) const uint16_t*)&s_rt[wid][0][0] -
@@ -2793,6 +2764,22 @@ void launch_extract(const ImageBatch& b, const OrbGeomDev& gd, int n_images, hip
                    0, st, b, gd.dev, gd.ws.oct_keys, gd.ws.oct_count, gd.out.kps, gd.out.desc,
                    gd.out.nkps);
   }
+}
+
+hipError_t octree_lds_limits(int device, int* img_bytes, int* lvl_bytes) {
+  int max_lds = 0;
+  hipError_t e = hipDeviceGetAttribute(&max_lds, hipDeviceAttributeMaxSharedMemoryPerBlock, device);
+  if (e != hipSuccess) return e;
+  hipFuncAttributes a{};
+  if ((e = hipFuncGetAttributes(&a, reinterpret_cast<const void*>(&octree_img_kernel))) != hipSuccess)
+    return e;
+  *img_bytes = max_lds - (int)a.sharedSizeBytes;
+  if ((e = hipFuncGetAttributes(&a, reinterpret_cast<const void*>(&octree_lvl_kernel))) != hipSuccess)
+    return e;
+  // the per-level kernel's dynamic LDS is at least the global algorithm's OctShared
+  *lvl_bytes = max_lds - (int)a.sharedSizeBytes;
+  if (*lvl_bytes < (int)sizeof(OctShared)) *lvl_bytes = 0;
+  return hipSuccess;
 }
 
 }  // namespace slamgpu

@@ -26,8 +26,11 @@ struct OrbTables {
 
 void compute_tables(const OrbParams& p, OrbTables* t);
 // Returns 0 on success, <0 if the configuration is outside what the kernels support.
+// oct_img_lds / oct_lvl_lds: the dynamic LDS the octree kernels may take on the device
+// (octree_lds_limits); the key capacities are sized within min(these, the gfx950 budgets).
 int compute_geometry(const OrbParams& p, int cols, int rows, OrbGeom* g,
-                     std::vector<ResizeX>* rx, std::vector<ResizeY>* ry);
+                     std::vector<ResizeX>* rx, std::vector<ResizeY>* ry,
+                     int oct_img_lds = 1 << 30, int oct_lvl_lds = 1 << 30);
 // FAST cell views of all levels, in the kernels' per-image cell order (cells_per_image entries).
 void build_cells(const OrbGeom& g, std::vector<CellDesc>* cells);
 

@@ -244,7 +244,16 @@ int slamgpu_create(int device, const slamgpu_orb_params* p, int cols, int rows, 
                         std::min(std::max(p->min_th_fast, 0), 255)};
   std::vector<ResizeX> rx;
   std::vector<ResizeY> ry;
-  if (int gr = compute_geometry(c->params, cols, rows, &c->geom, &rx, &ry)) {
+  // the octree kernels' LDS limits on this device (without a usable device: the gfx950 budgets;
+  // hipSetDevice below then reports the failure)
+  int oct_img_lds = 1 << 30, oct_lvl_lds = 1 << 30;
+  if (hipSetDevice(device) != hipSuccess ||
+      octree_lds_limits(device, &oct_img_lds, &oct_lvl_lds) != hipSuccess) {
+    oct_img_lds = oct_lvl_lds = 1 << 30;
+    (void)hipGetLastError();
+  }
+  if (int gr = compute_geometry(c->params, cols, rows, &c->geom, &rx, &ry, oct_img_lds,
+                                oct_lvl_lds)) {
     static const char* why[] = {
         "", "bad parameters",
         "image too small: a pyramid level is under 2*19+8 pixels (the reference's FAST cell grid "

@@ -212,8 +212,9 @@ def lib():
                                              C.POINTER(ip)]
         L.slamgpu_optimizer_last_error.argtypes = []
         L.slamgpu_optimizer_last_error.restype = C.c_char_p
-        L.slamgpu_coop_slots_in_use.argtypes = [C.c_int]
-        L.slamgpu_coop_slots_in_use.restype = C.c_int
+        if hasattr(L, "slamgpu_coop_slots_in_use"):  # diagnostic (absent from older A/B builds)
+            L.slamgpu_coop_slots_in_use.argtypes = [C.c_int]
+            L.slamgpu_coop_slots_in_use.restype = C.c_int
         _lib = L
     return _lib
 

@@ -29,12 +29,15 @@ def _project(T, X):
 
 
 def make_map(oracle):
-    """Three keyframes (frames 0, 1, 1 of a synthetic sequence at three poses, id 0 = the fixed
-    one), map points unprojected from keyframe 0's stereo depths and seen by the others where a
-    keypoint lies within 1.5 px of their projection; a few points and keyframe slots bad."""
+    """Three keyframes (frames 0, 1, 1 of a synthetic sequence, id 0 = the fixed one), map points
+    unprojected from keyframe 0's stereo depths and seen by the others where a keypoint lies
+    within 1.5 px of their projection by the frame's true camera (the sequence rotates about the
+    camera centre); keyframes 1 and 2 store that pose moved by a few cm, so that F12 has a
+    baseline and the global BA has something to correct; a few points and keyframe slots bad."""
     kfs, _ = KS.keyframes(oracle)
     feats = [kfs[0], kfs[1], kfs[1]]
-    Ts = [KS.pose(0), KS.pose(1, (-0.4, 0.02, 0.1)), KS.pose(1, (-0.2, 0.0, 0.3))]
+    Ts = [KS.pose(0), KS.pose(1, (-0.02, 0.002, 0.01)), KS.pose(1, (-0.01, 0.0, 0.03))]
+    T_true = [KS.pose(0), KS.pose(1), KS.pose(1)]
     rng = np.random.default_rng(5)
     K = []
     for k, (f, T) in enumerate(zip(feats, Ts)):
@@ -62,7 +65,7 @@ def make_map(oracle):
                       max_dist=np.float32(d * sc[kp["octave"]])))
         k0["mp"][i] = m
         for k in (1, 2):
-            u, v, zc = _project(Ts[k], Xw)
+            u, v, zc = _project(T_true[k], Xw)
             if zc <= 0:
                 continue
             kk = K[k]["kps"]
