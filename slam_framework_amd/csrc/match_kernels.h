@@ -9,7 +9,10 @@ namespace slamgpu {
 
 constexpr int kGridCols = 64, kGridRows = 48;  // Frame::grid_cols / grid_rows (frame.h:104-105)
 constexpr int kGridCells = kGridCols * kGridRows;
-constexpr int kTopK = 4;                       // candidates kept per query for claim resolution
+// candidates kept per query for claim resolution: 6 (r5) -- a query whose kept candidates are all
+// claimed by earlier queries is rescanned alone on the resolve chain (4: 0.153 ms/step of
+// search_resolve, 6: 0.095, 8: 0.062 against search_cand 0.19 / 0.215 / 0.23)
+constexpr int kTopK = 6;
 
 struct Camera {
   float fx, fy, cx, cy, bf;

@@ -227,16 +227,46 @@ __global__ __launch_bounds__(256) void stereo_match_kernel(ImageBatch b,
   const uint8_t* dRb = ext.desc + ir * ext.stride * 32;
   uint32_t best = ((uint32_t)TH_HIGH << 16) | 0xffffu;
   if (ok) {
-    for (int c = c0 + hl; c < c1; c += G) {
-      const int iR = items[c];
-      const KeyPoint kpR = kr[iR];
-      if (kpR.octave < levelL - 1 || kpR.octave > levelL + 1) continue;
-      const float uR = kpR.x;
-      if (uR >= minU && uR <= maxU) {
-        const int dist = hamming32(dL, dRb + iR * 32);
-        const uint32_t key = ((uint32_t)dist << 16) | (uint32_t)iR;
-        if (dist < TH_HIGH && key < best) best = key;
+    // kCandU candidates per lane at a time, each stage's loads all in flight before the next
+    // stage needs them: row items -> (octave, x) -> descriptors -> distances (the loop was a
+    // chain of three dependent loads per candidate)
+    constexpr int kCandU = 2;  // 2 and 4 measured equal (0.35 ms/step), 2 holds fewer VGPRs
+    const uint4* dLq = reinterpret_cast<const uint4*>(dL);
+    const uint4 l0 = dLq[0], l1 = dLq[1];
+    for (int cb = c0 + hl; cb < c1; cb += G * kCandU) {
+      int iR[kCandU];
+#pragma unroll
+      for (int u = 0; u < kCandU; u++) {
+        const int c = cb + G * u;
+        iR[u] = c < c1 ? items[c] : -1;
       }
+      bool pass[kCandU];
+#pragma unroll
+      for (int u = 0; u < kCandU; u++) {
+        pass[u] = false;
+        if (iR[u] >= 0) {
+          const int oct = kr[iR[u]].octave;
+          const float uR = kr[iR[u]].x;
+          pass[u] = oct >= levelL - 1 && oct <= levelL + 1 && uR >= minU && uR <= maxU;
+        }
+      }
+      uint4 r0[kCandU], r1[kCandU];
+#pragma unroll
+      for (int u = 0; u < kCandU; u++)
+        if (pass[u]) {
+          const uint4* dr = reinterpret_cast<const uint4*>(dRb + iR[u] * 32);
+          r0[u] = dr[0];
+          r1[u] = dr[1];
+        }
+#pragma unroll
+      for (int u = 0; u < kCandU; u++)
+        if (pass[u]) {
+          const int dist = __popc(l0.x ^ r0[u].x) + __popc(l0.y ^ r0[u].y) + __popc(l0.z ^ r0[u].z) +
+                           __popc(l0.w ^ r0[u].w) + __popc(l1.x ^ r1[u].x) + __popc(l1.y ^ r1[u].y) +
+                           __popc(l1.z ^ r1[u].z) + __popc(l1.w ^ r1[u].w);
+          const uint32_t key = ((uint32_t)dist << 16) | (uint32_t)iR[u];
+          if (dist < TH_HIGH && key < best) best = key;
+        }
     }
   }
   best = group_min<G>(best);
@@ -984,7 +1014,13 @@ __global__ __launch_bounds__(256) void search_cand_kernel(
   if (lane == 0) mw.ncand[q] = ok ? n : 0;
 }
 
-// Sequential, in-query-order claim resolution: one wave per frame.
+// Sequential, in-query-order claim resolution: one wave per frame. The kernel is a chain of
+// latency (a frame's queries in order), so everything it can take off that chain is: the
+// keypoint fields it needs are staged with all loads in flight, the next 64 queries' candidates
+// are loaded while the current ones resolve, a candidate's "claimed" state is read once per
+// round (claims change only when a round commits), and the rotation-histogram bookkeeping of the
+// first kResolveLdsQ queries stays in LDS (a frame's later queries, if any, use the workspace).
+constexpr int kResolveLdsQ = 4096;
 template <typename Q>
 __global__ __launch_bounds__(64) void search_resolve_kernel(
     FrameKps cur, const float* __restrict__ u_right, int64_t ur_stride, Camera cam,
@@ -993,13 +1029,16 @@ __global__ __launch_bounds__(64) void search_resolve_kernel(
   constexpr bool kF2F = sizeof(Q) == sizeof(F2FQuery);
   __shared__ uint32_t claimed[128];  // kp_cap <= 4096
   __shared__ int hist[HISTO_LENGTH];
+  __shared__ float s_kang[kF2F ? 4096 : 1];
+  __shared__ int8_t s_koct[kF2F ? 1 : 4096];
+  __shared__ int owner[4096];
+  __shared__ int8_t s_bin[kF2F ? kResolveLdsQ : 1];     // rotation bin of query qi (-1 none)
+  __shared__ int16_t s_best[kF2F ? kResolveLdsQ : 1];   // its matched keypoint
   const int f = blockIdx.x;
   const int lane = threadIdx.x;
   const int n = cur.n[f * cur.n_stride];
   for (int i = lane; i < 128; i += 64) claimed[i] = 0;
   if (lane < HISTO_LENGTH) hist[lane] = 0;
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
   FrameView F;
   F.kps = cur.kps + f * cur.stride;
   F.desc = cur.desc + f * cur.stride * 32;
@@ -1022,42 +1061,97 @@ __global__ __launch_bounds__(64) void search_resolve_kernel(
   // rounds suffice. A lane whose kept top-K is exhausted while more candidates exist is rescanned
   // alone, at its place in the order. For non-blocking duplicates the last writer of mp[idx]
   // wins, as in the sequential loop.
-  __shared__ float s_kang[4096];
-  __shared__ int8_t s_koct[4096];
-  __shared__ int owner[4096];
-  for (int i = lane; i < n; i += 64) {
-    const KeyPoint kp = F.kps[i];
-    s_kang[i] = kp.angle;
-    s_koct[i] = (int8_t)kp.octave;
-    owner[i] = INT_MAX;
+  // keypoint fields (F2F: the angle, only with the rotation check; local map: the octave),
+  // four loads in flight per lane
+  for (int i0 = 0; i0 < n; i0 += 256) {
+    float ang[4];
+    int oct[4];
+#pragma unroll
+    for (int u = 0; u < 4; u++) {
+      const int i = i0 + 64 * u + lane;
+      ang[u] = 0.f;
+      oct[u] = 0;
+      if (i < n) {
+        if constexpr (kF2F) {
+          if (check_ori) ang[u] = F.kps[i].angle;
+        } else {
+          oct[u] = F.kps[i].octave;
+        }
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < 4; u++) {
+      const int i = i0 + 64 * u + lane;
+      if (i < n) {
+        if constexpr (kF2F) s_kang[i] = ang[u];
+        else s_koct[i] = (int8_t)oct[u];
+        owner[i] = INT_MAX;
+      }
+    }
   }
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
   __builtin_amdgcn_wave_barrier();
   const int need = kF2F ? 1 : 2;
   auto is_claimed = [&](int idx) { return (claimed[idx >> 5] >> (idx & 31)) & 1u; };
+  // one lane's query of a chunk: its kept candidates, candidate count, map point word, angle
+  struct QIn {
+    uint64_t key[kTopK];
+    int nc, mpw;
+    float qang;
+  };
+  auto load_chunk = [&](int c0, QIn& in) {
+    const int qi = c0 + lane;
+    if (qi < qn) {
+      const int q = q0 + qi;
+#pragma unroll
+      for (int k = 0; k < kTopK; k++) in.key[k] = mw.topk[(int64_t)q * kTopK + k];
+      in.nc = mw.ncand[q];
+      const Q& qq = queries[q];
+      in.mpw = (qq.mp_id & 0x7fffffff) | (qq.blocks ? (int)0x80000000u : 0);
+      in.qang = 0.f;
+      if constexpr (kF2F) in.qang = qq.last_angle;
+    } else {
+#pragma unroll
+      for (int k = 0; k < kTopK; k++) in.key[k] = kNoKey;
+      in.nc = 0;
+      in.mpw = 0;
+      in.qang = 0.f;
+    }
+  };
+  auto set_bin = [&](int qi, int bin, int idx) {
+    if (qi < kResolveLdsQ) {
+      s_bin[qi] = (int8_t)bin;
+      s_best[qi] = (int16_t)idx;
+    } else {
+      mw.rot_bin[q0 + qi] = bin;
+      mw.best_idx[q0 + qi] = idx;
+    }
+  };
+  QIn nx;
+  load_chunk(0, nx);
   for (int c0 = 0; c0 < qn; c0 += 64) {
     const int qi = c0 + lane;
     const bool valid = qi < qn;
     const int q = q0 + qi;
-    uint64_t key[kTopK];
-    int nc = 0, mpw = 0;
-    float qang = 0.f;
-    if (valid) {
-#pragma unroll
-      for (int k = 0; k < kTopK; k++) key[k] = mw.topk[(int64_t)q * kTopK + k];
-      nc = mw.ncand[q];
-      const Q& qq = queries[q];
-      mpw = (qq.mp_id & 0x7fffffff) | (qq.blocks ? (int)0x80000000u : 0);
-      if constexpr (kF2F) qang = qq.last_angle;
-      mw.rot_bin[q] = -1;
-    } else {
-#pragma unroll
-      for (int k = 0; k < kTopK; k++) key[k] = kNoKey;
+    const QIn in = nx;
+    if (c0 + 64 < qn) load_chunk(c0 + 64, nx);  // in flight while this chunk resolves
+    const uint64_t* key = in.key;
+    const int nc = in.nc, mpw = in.mpw;
+    const float qang = in.qang;
+    if constexpr (kF2F) {
+      if (valid) set_bin(qi, -1, 0);
     }
     const bool qblocks = mpw < 0;
     int start = 0;
     while (start < 64 && c0 + start < qn) {
       const bool act = valid && lane >= start && nc > 0;
+      // the kept candidates still unclaimed (claims change only at the commits below)
+      uint32_t live = 0;
+      if (act) {
+#pragma unroll
+        for (int k = 0; k < kTopK; k++)
+          if (key[k] != kNoKey && !is_claimed(key_idx(key[k]))) live |= 1u << k;
+      }
       // -- fixed point of the choices of lanes >= start
       uint64_t b1 = kNoKey, b2 = kNoKey;
       int navail = 0, mine = -1, prev = -2;
@@ -1065,16 +1159,13 @@ __global__ __launch_bounds__(64) void search_resolve_kernel(
         b1 = kNoKey;
         b2 = kNoKey;
         navail = 0;
-        if (act) {
 #pragma unroll
-          for (int k = 0; k < kTopK; k++) {
-            if (key[k] == kNoKey) continue;
-            const int idx = key_idx(key[k]);
-            if (is_claimed(idx) || owner[idx] < lane) continue;
-            if (navail == 0) b1 = key[k];
-            else if (navail == 1) b2 = key[k];
-            navail++;
-          }
+        for (int k = 0; k < kTopK; k++) {
+          if (!((live >> k) & 1u)) continue;
+          if (owner[key_idx(key[k])] < lane) continue;
+          if (navail == 0) b1 = key[k];
+          else if (navail == 1) b2 = key[k];
+          navail++;
         }
         // accepted blocking choice -> owner (the lowest such lane wins the keypoint)
         bool acc = b1 != kNoKey && key_dist(b1) <= TH_HIGH;
@@ -1135,8 +1226,7 @@ __global__ __launch_bounds__(64) void search_resolve_kernel(
             const float factor = 1.0f / HISTO_LENGTH;
             int bin = (int)roundf(rot * factor);
             if (bin == HISTO_LENGTH) bin = 0;
-            mw.rot_bin[q] = bin;
-            mw.best_idx[q] = idx;
+            set_bin(qi, bin, idx);
             atomicAdd(&hist[bin], 1);
           }
         }
@@ -1162,6 +1252,7 @@ __global__ __launch_bounds__(64) void search_resolve_kernel(
       }
       start = r + 1;
     }
+    (void)q;
   }
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
   __builtin_amdgcn_wave_barrier();
@@ -1191,9 +1282,10 @@ __global__ __launch_bounds__(64) void search_resolve_kernel(
       // SetMapPoint(rotHist[i][j], nullptr) for every entry of a rejected bin (:1441-1450)
       int removed = 0;
       for (int qi = lane; qi < qn; qi += 64) {
-        const int bin = mw.rot_bin[q0 + qi];
+        const bool in_lds = qi < kResolveLdsQ;
+        const int bin = in_lds ? (int)s_bin[qi] : mw.rot_bin[q0 + qi];
         if (bin >= 0 && bin != ind1 && bin != ind2 && bin != ind3) {
-          const int idx = mw.best_idx[q0 + qi];
+          const int idx = in_lds ? (int)s_best[qi] : mw.best_idx[q0 + qi];
           mp[idx] = -1;
           blk[idx] = 0;
           removed++;
