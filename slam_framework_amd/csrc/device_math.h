@@ -110,6 +110,21 @@ __device__ __forceinline__ float cv_fast_atan2(float y, float x) {
   return a;
 }
 
+// A wave-uniform pointer as such (its value read from the first active lane into SGPRs).
+template <typename T>
+__device__ __forceinline__ T* uniform_ptr(T* p) {
+  const uint64_t v = (uint64_t)(uintptr_t)p;
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
+  return (T*)(uintptr_t)(((uint64_t)hi << 32) | lo);
+}
+
+// A raw buffer descriptor over `bytes` bytes at the wave-uniform address p: loads through it take
+// a 32-bit lane offset (+ a scalar one) instead of a 64-bit address computed per lane.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t buf_rsrc(const void* p, int bytes = 0x7ffffff0) {
+  return __builtin_amdgcn_make_buffer_rsrc((void*)uniform_ptr(p), 0, bytes, 0x00020000);
+}
+
 __device__ __forceinline__ int cv_round(float v) { return (int)rintf(v); }
 __device__ __forceinline__ int max3(int a, int b, int c) { return max(max(a, b), c); }
 // high 32 bits of a 24 x 24-bit product (v_mul_hi_u32_u24); a, b < 2^24

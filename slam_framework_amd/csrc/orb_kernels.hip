@@ -118,9 +118,22 @@ __device__ __forceinline__ void pyr_strip(const ImageBatch& b, const OrbGeom* __
   }
   const bool aligned = kAligned;
   const int qa = min(q0, qmax), qb = min(q0 + 1, qmax), qc = min(q0 + 2, qmax);
+  // Source rows in global memory (pyr_down) are read through a buffer descriptor of the source
+  // level: the row offset is a scalar, the lane's dword offsets are constants, so a row costs
+  // three buffer loads and no address arithmetic (a flat load needs a 64-bit add per lane each).
+  spitch = __builtin_amdgcn_readfirstlane(spitch);
+  const bool gsrc = src_rows == nullptr;
+  const __amdgpu_buffer_rsrc_t srsrc = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)uniform_ptr(src), 0, __builtin_amdgcn_readfirstlane(spitch * S.h), 0x00020000);
+  const int oa = 4 * qa, ob = 4 * qb, oc = 4 * qc;
   auto fetch = [&](int sy, uint32_t (&wv)[3]) {
-    const uint8_t* row = src + (int64_t)(min(sy, sy_hi) - srow0) * spitch;  // wave-uniform
-    if (aligned) {  // clamped dwords stay inside the row; bytes past sx+1 carry zero weight
+    const int roff = __builtin_amdgcn_readfirstlane((min(sy, sy_hi) - srow0) * spitch);
+    const uint8_t* row = src + roff;  // wave-uniform
+    if (aligned && gsrc) {  // clamped dwords stay inside the row; bytes past sx+1: zero weight
+      wv[0] = __builtin_amdgcn_raw_buffer_load_b32(srsrc, oa, roff, 0);
+      wv[1] = __builtin_amdgcn_raw_buffer_load_b32(srsrc, ob, roff, 0);
+      wv[2] = __builtin_amdgcn_raw_buffer_load_b32(srsrc, oc, roff, 0);
+    } else if (aligned) {  // rows staged in LDS by pyr_band_kernel
       const uint32_t* rw = reinterpret_cast<const uint32_t*>(row);
       wv[0] = rw[(uint32_t)qa];
       wv[1] = rw[(uint32_t)qb];
@@ -137,6 +150,8 @@ __device__ __forceinline__ void pyr_strip(const ImageBatch& b, const OrbGeom* __
   };
   uint8_t* dst = b.pyr + (int64_t)img * g->pyr_bytes + D.offset;
   const int dpitch = __builtin_amdgcn_readfirstlane(D.pitch), dw = __builtin_amdgcn_readfirstlane(D.w);
+  const __amdgpu_buffer_rsrc_t drsrc = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)uniform_ptr(dst), 0, __builtin_amdgcn_readfirstlane(dpitch * D.h), 0x00020000);
   uint32_t cur[kPyrChunk][3], nxt[kPyrChunk][3];
 #pragma unroll
   for (int j = 0; j < kPyrChunk; j++) fetch(sy_lo + j, cur[j]);
@@ -163,9 +178,10 @@ __device__ __forceinline__ void pyr_strip(const ImageBatch& b, const OrbGeom* __
     const uint32_t p01 = __builtin_bit_cast(uint32_t, __builtin_bit_cast(u16x2_t, t[0] | t[1] << 16) >> two);
     const uint32_t p23 = __builtin_bit_cast(uint32_t, __builtin_bit_cast(u16x2_t, t[2] | t[3] << 16) >> two);
     const uint32_t packed = __builtin_amdgcn_perm(p23, p01, 0x06040200u);
-    uint8_t* drow = dst + (int64_t)(dy0 + nd) * dpitch;
-    if (x0 + 4 <= dw) {
-      *reinterpret_cast<uint32_t*>(drow + x0) = packed;  // pitch is a multiple of 64
+    const int doff = __builtin_amdgcn_readfirstlane((dy0 + nd) * dpitch);
+    uint8_t* drow = dst + doff;
+    if (x0 + 4 <= dw) {  // pitch is a multiple of 64
+      __builtin_amdgcn_raw_buffer_store_b32(packed, drsrc, x0, doff, 0);
       if (copy_rows)
         *reinterpret_cast<uint32_t*>(copy_rows + (dy0 + nd - copy_row0) * dpitch + x0) = packed;
     } else {
@@ -2364,11 +2380,15 @@ __global__ __launch_bounds__(256) void orient_desc_kernel(
       const uint8_t* im = level == 0 ? batch_image(b, img)
                                      : b.pyr + (int64_t)img * g->pyr_bytes + L.offset;
       const uint8_t* rbase = im + (int64_t)(y - 15) * pitch + ((x - 15) & ~3);
-      const uint8_t* rp = rbase + (__umul24(hr, pitch) + 16 * hh);
+      const uint32_t loff = __umul24(hr, pitch) + 16 * hh;
+      const uint8_t* rp = rbase + loff;
       if (hr < 31) {
         if ((((uintptr_t)im | (uintptr_t)pitch) & 3) == 0) {
+          // buffer loads off the patch's (wave-uniform) base: no 64-bit address per lane
+          const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+              (void*)uniform_ptr(rbase), 0, 31 * pitch + 32, 0x00020000);
 #pragma unroll
-          for (int k = 0; k < 5; k++) raw[jj][k] = reinterpret_cast<const uint32_t*>(rp)[k];
+          for (int k = 0; k < 5; k++) raw[jj][k] = __builtin_amdgcn_raw_buffer_load_b32(rs, loff + 4 * k, 0, 0);
         } else {
 #pragma unroll
           for (int k = 0; k < 20; k++) raw[jj][k >> 2] |= (uint32_t)rp[k] << (8 * (k & 3));
@@ -2458,8 +2478,13 @@ __global__ __launch_bounds__(256) void orient_desc_kernel(
     G.org = G.im + (int64_t)(G.ky - 21) * G.pitch + ((G.kx - 21) & ~3);
     return G;
   };
+  // the window rows by buffer loads off the window origin (wave-uniform): a 32-bit lane offset
+  // per row task, no 64-bit address arithmetic
   auto rs_load = [&](const RsGeo& G, uint4 (&q)[kRounds * kTaskRows]) {
     if (!G.fastp) return;
+    typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)uniform_ptr(G.org), 0, 43 * G.pitch, 0x00020000);
 #pragma unroll
     for (int i = 0; i < kRounds; i++) {
       if (trow[i] >= 0) {
@@ -2468,8 +2493,9 @@ __global__ __launch_bounds__(256) void orient_desc_kernel(
           // row 43 (the pad of the last pair, weight 0 in every tap) re-reads row 42: the
           // window's rows stay inside the level
           const uint32_t row = (uint32_t)min(trow[i] + h, 42);
-          q[kTaskRows * i + h] = *reinterpret_cast<const uint4*>(
-              G.org + __umul24(row, (uint32_t)G.pitch) + (uint32_t)tcol[i]);
+          const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(
+              rs, __umul24(row, (uint32_t)G.pitch) + (uint32_t)tcol[i], 0, 0);
+          q[kTaskRows * i + h] = make_uint4(v.x, v.y, v.z, v.w);
         }
       }
     }
