@@ -56,7 +56,7 @@ __device__ __forceinline__ uint32_t dot2u(uint32_t a, uint32_t b, uint32_t c) {
 #define PYR_STRIP 16
 #endif
 #ifndef PYR_CHUNK
-#define PYR_CHUNK 4
+#define PYR_CHUNK 2
 #endif
 constexpr int kPyrStrip = PYR_STRIP;  // output rows per wave
 constexpr int kPyrChunk = PYR_CHUNK;  // source rows fetched per batch
@@ -459,6 +459,10 @@ __global__ __launch_bounds__(64 * kCellWaves, 1) void fast_cells_kernel(ImageBat
   const int tile_rows = __builtin_amdgcn_readfirstlane(g->fast_tile_rows);
   uint16_t* cand =
       reinterpret_cast<uint16_t*>(sc + ((kScoreStride * g->fast_score_rows + 15) & ~15));
+  {  // the score map starts zero; each FAST pass leaves it zero again
+    const int zb = (kScoreStride * g->fast_score_rows + 15) & ~15;
+    for (int o = 4 * lane; o < zb; o += 256) *reinterpret_cast<uint32_t*>(sc + o) = 0u;
+  }
 
   // ---- tile prefetch: aligned dwords covering [ini_x & ~3, ini_x + vw) x [ini_y, ini_y + vh)
   // into registers, lane = (row within a step, dword): each element is a scalar row base plus a
@@ -483,14 +487,14 @@ __global__ __launch_bounds__(64 * kCellWaves, 1) void fast_cells_kernel(ImageBat
   const int glr = lane / kGLpr, glc = 16 * (lane % kGLpr);
   auto issue = [&](const CellView& v, uint8_t* buf) {
     const uint8_t* src = v.base + (int64_t)v.ini_y * v.pitch + v.ax;  // wave-uniform
+    const __amdgpu_buffer_rsrc_t rs = buf_rsrc(src);  // 32-bit lane offsets, no 64-bit adds
     const int n = (v.vh + kGRows - 1) / kGRows;
 #pragma unroll
     for (int k = 0; k < kGSteps; k++)
       if (k < n && k * kGRows + glr < tile_rows)
-        __builtin_amdgcn_global_load_lds(
-            (const __attribute__((address_space(1))) void*)(
-                src + (uint32_t)(min(k * kGRows + glr, v.vh - 1) * v.pitch + glc)),
-            (__attribute__((address_space(3))) void*)(buf + 1024 * k), 16, 0, 0);
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(
+            rs, (__attribute__((address_space(3))) void*)(buf + 1024 * k), 16,
+            (uint32_t)(min(k * kGRows + glr, v.vh - 1) * v.pitch + glc), 0, 0, 0);
   };
   CellView nxt = cell_view<kAlign>(b, g, img, in_pitch, readlane4(my_desc, 0));
   if constexpr (!GLDS) {
@@ -609,9 +613,9 @@ __global__ __launch_bounds__(64 * kCellWaves, 1) void fast_cells_kernel(ImageBat
       }
       __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
       __builtin_amdgcn_wave_barrier();
-#pragma unroll 4
-      for (int rz = plr - 1; rz <= dh; rz += kRps)
-        *reinterpret_cast<uint32_t*>(sc1 + rz * kScoreStride + 4 * pld) = 0;
+      // the map is zero but for the records just read (it is zeroed once per wave and every
+      // pass clears what it wrote): clear them
+      for (int i = lane; i < nrec; i += 64) recs[i] = 0u;
       __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
       __builtin_amdgcn_wave_barrier();
       // exact FAST score of the survivors (window top-left: tile (r, cc - 3) = tile + pix - 3)
@@ -656,6 +660,9 @@ __global__ __launch_bounds__(64 * kCellWaves, 1) void fast_cells_kernel(ImageBat
         }
         count += __popcll(mk);
       }
+      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      for (int i = lane; i < ncand; i += 64) sc1[cand[i]] = 0;  // the map back to zero
       return count;
     };
     // FAST at iniTh; the reference re-runs the whole cell at minTh when the iniTh output (after
