@@ -885,11 +885,15 @@ __device__ int scan_query_k(const ScanCtx& c, const Camera& cam, const FrameView
       }
     }
   }
-  // merge the per-lane sorted lists: kTopK rounds of wave minimum
+  // merge the per-lane sorted lists: up to kTopK rounds of wave minimum, ending early once the
+  // wave has no candidate left (most queries keep fewer than kTopK)
+#pragma unroll
+  for (int k = 0; k < kTopK; k++) top[k] = kNoKey;
 #pragma unroll
   for (int k = 0; k < kTopK; k++) {
     const K m = wave_min_key(t[0]);
-    if (t[0] == m && m != kNone) {
+    if (m == kNone) break;  // wave-uniform
+    if (t[0] == m) {
 #pragma unroll
       for (int j = 0; j < kTopK - 1; j++) t[j] = t[j + 1];
       t[kTopK - 1] = kNone;
