@@ -122,7 +122,7 @@ int compute_geometry(const OrbParams& p, int cols, int rows, OrbGeom* g,
     L.wcell = (int)std::ceil(width / L.ncols);
     L.hcell = (int)std::ceil(height / L.nrows);
     L.cell_base = cell_base;
-    cell_base += L.ncols * L.nrows;
+    cell_base += round_up(L.ncols * L.nrows, kCellGroup);  // padding cells are empty (vh 0)
     max_wcell = std::max(max_wcell, L.wcell);
     max_hcell = std::max(max_hcell, L.hcell);
     // octree (:484-486)

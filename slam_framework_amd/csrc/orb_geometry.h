@@ -12,6 +12,14 @@
 namespace slamgpu {
 
 constexpr int kMaxLevels = 12;
+// fast_cells writes the FAST survivors of each aligned group of kCellGroup cells (a wave's cells)
+// (FAST_CELLS_PER_WAVE: the cells one fast_cells wave runs)
+// contiguously from the group's first slot; every level's cell range is padded to a multiple of
+// kCellGroup with empty cells, so groups never straddle levels or launches.
+#ifndef FAST_CELLS_PER_WAVE
+#define FAST_CELLS_PER_WAVE 8
+#endif
+constexpr int kCellGroup = FAST_CELLS_PER_WAVE;
 constexpr int kPyrMaxBands = 32;
 constexpr int kEdgeThreshold = 19;
 constexpr int kMinBorder = kEdgeThreshold - 3;  // minBorderX/Y (:712)

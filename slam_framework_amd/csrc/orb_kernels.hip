@@ -379,10 +379,8 @@ __device__ __forceinline__ int fast_score(const uint8_t* w) {  // w: top-left of
 }
 
 // A wave runs kCellsPerWave consecutive cells of one image.
-#ifndef FAST_CELLS_PER_WAVE
-#define FAST_CELLS_PER_WAVE 4
-#endif
-constexpr int kCellsPerWave = FAST_CELLS_PER_WAVE;
+constexpr int kCellsPerWave = FAST_CELLS_PER_WAVE;  // orb_geometry.h (4: 0.687 ms, 8: 0.670)
+static_assert(kCellsPerWave == kCellGroup, "a wave's cells are one key group (orb_geometry.h)");
 
 // ceil(4096 / n) for n = 1..32 (the pre-test's lane -> (row, dword) split by a multiply)
 __constant__ int16_t c_inv4096[33] = {
@@ -501,6 +499,10 @@ __global__ __launch_bounds__(64 * kCellWaves, 1) void fast_cells_kernel(ImageBat
     if (nxt.vh > 0) prefetch(nxt);
   }
 
+  // the group's keys, contiguous from its first cell's slot (kCellGroup == kCellsPerWave and
+  // c0 is group-aligned: launch boundaries are level boundaries, padded to kCellGroup)
+  uint32_t* const grp_keys = cell_keys + ((int64_t)img * ncells + c0) * cell_cap;
+  int gfill = 0;
   for (int ci = 0; ci < nc; ci++) {
     const CellView v = nxt;
     const int64_t slot = (int64_t)img * ncells + c0 + ci;
@@ -570,7 +572,7 @@ __global__ __launch_bounds__(64 * kCellWaves, 1) void fast_cells_kernel(ImageBat
         ? (uint32_t)(0x80808080ull >> (32 - 8 * bhi)) & (uint32_t)(0x80808080ull << (8 * blo))
         : 0u;
     const uint8_t* trow = tile + (lr + 3) * kTileStride + 4 * Q;  // this lane's dword, step 0
-    uint32_t* out = cell_keys + slot * cell_cap;
+    uint32_t* out = grp_keys + gfill;  // this cell's survivors follow the group's earlier cells
     auto fast_pass = [&](const FastTh& f) -> int {
       if (f.th >= 255) return 0;  // FAST at 255: no pixel differs by more
       // pre-test: a lane with any surviving pixel appends one record -- its survivor flags (bit
@@ -673,13 +675,12 @@ __global__ __launch_bounds__(64 * kCellWaves, 1) void fast_cells_kernel(ImageBat
       __builtin_amdgcn_wave_barrier();
       count = fast_pass(th_min);
     }
-    if (lane == 0) {
-      if (count > cell_cap) {
-        atomicOr(err, kErrCellOverflow);
-        count = cell_cap;
-      }
-      cell_count[slot] = count;
+    if (count > cell_cap) {
+      if (lane == 0) atomicOr(err, kErrCellOverflow);
+      count = cell_cap;
     }
+    if (lane == 0) cell_count[slot] = count;
+    gfill += count;
   }
 }
 // ---------------------------------------------------------------------------------------
@@ -845,7 +846,8 @@ __device__ __forceinline__ void octree_global(
     for (int i = wid; i < n; i += (kThr / 64)) {
       const int cnt = cell_count[cbase + c0 + i];
       const int off = base + S.a[i];
-      const uint32_t* src = cell_keys + (cbase + c0 + i) * g->cell_cap;
+      const int gi = i & ~(kCellGroup - 1);  // the cell's key group (c0 is group-aligned)
+      const uint32_t* src = cell_keys + (cbase + c0 + gi) * g->cell_cap + (S.a[i] - S.a[gi]);
       for (int k = lane; k < cnt; k += 64)
         if (off + k < L.key_cap) keys[0][off + k] = src[k];
     }
@@ -1421,7 +1423,8 @@ __global__ __launch_bounds__(64 * kMaxLevels) void octree_img_kernel(
           if (cpre[mid] <= s) lo = mid;
           else hi = mid;
         }
-        kr[r] = cell_keys[(cbase + lo) * g->cell_cap + (s - cpre[lo])];
+        const int gs = lo & ~(kCellGroup - 1);  // key group of cell lo: contiguous from gs
+        kr[r] = cell_keys[(cbase + gs) * g->cell_cap + (s - cpre[gs])];
       }
     }
 #pragma unroll
@@ -1470,11 +1473,12 @@ __global__ __launch_bounds__(64 * kMaxLevels) void octree_img_kernel(
             const int pv = __shfl(cex, cand & 63, 64);
             if (cand < 64 && pv <= r) lo = cand;
           }
-          const int base = __shfl(cex, lo, 64);
+          const int gs = lo & ~(kCellGroup - 1);  // key group of cell lo (c0 is group-aligned)
+          const int base = __shfl(cex, gs, 64);
           int b = -1;
           uint32_t k = 0;
           if (r < ctot) {
-            k = cell_keys[(cbase + c0 + lo) * g->cell_cap + (r - base)];
+            k = cell_keys[(cbase + c0 + gs) * g->cell_cap + (r - base)];
             b = (int)((float)key_x(k) / hX);
             if (b >= nIni) b = -1;
           }
@@ -1854,7 +1858,8 @@ __global__ __launch_bounds__(kOctLvlThreads) void octree_lvl_kernel(
           if (cpre[mid] <= s) lo = mid;
           else hi = mid;
         }
-        kr[r] = cell_keys[(cbase + lo) * g->cell_cap + (s - cpre[lo])];
+        const int gs = lo & ~(kCellGroup - 1);  // key group of cell lo: contiguous from gs
+        kr[r] = cell_keys[(cbase + gs) * g->cell_cap + (s - cpre[gs])];
       }
     }
 #pragma unroll

@@ -222,6 +222,8 @@ static ResMirror res_mirror(const slamgpu_ctx* c) {
   return m;
 }
 
+static int round_up_cells(int n) { return (n + kCellGroup - 1) / kCellGroup * kCellGroup; }
+
 static int check_device_err(slamgpu_ctx* c) {
   uint32_t e = 0;
   HIPCHECK(c, hipMemcpy(&e, c->ws.err, sizeof(e), hipMemcpyDeviceToHost));
@@ -563,12 +565,17 @@ int slamgpu_debug_level_keys(slamgpu_ctx* c, int img, int level, int stage, uint
     const int64_t cb = (int64_t)img * g.cells_per_image + L.cell_base;
     HIPCHECK(c, hipMemcpy(cnt.data(), c->ws.cell_count + cb, sizeof(int) * ncell,
                           hipMemcpyDeviceToHost));
-    std::vector<uint32_t> cell(g.cell_cap);
+    // the level's key slots at once; a cell's keys follow its group's earlier cells
+    // (kCellGroup, fast_cells_kernel)
+    std::vector<uint32_t> keys((size_t)round_up_cells(ncell) * g.cell_cap);
+    HIPCHECK(c, hipMemcpy(keys.data(), c->ws.cell_keys + cb * g.cell_cap,
+                          sizeof(uint32_t) * keys.size(), hipMemcpyDeviceToHost));
+    int gfill = 0;
     for (int i = 0; i < ncell; i++) {
-      if (!cnt[i]) continue;
-      HIPCHECK(c, hipMemcpy(cell.data(), c->ws.cell_keys + (cb + i) * g.cell_cap,
-                            sizeof(uint32_t) * cnt[i], hipMemcpyDeviceToHost));
-      out.insert(out.end(), cell.begin(), cell.begin() + cnt[i]);
+      if (i % kCellGroup == 0) gfill = 0;
+      const uint32_t* src = keys.data() + (size_t)(i - i % kCellGroup) * g.cell_cap + gfill;
+      out.insert(out.end(), src, src + cnt[i]);
+      gfill += cnt[i];
     }
   } else {
     int n = 0;
