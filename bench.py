@@ -55,12 +55,14 @@ def _symbol_matches(sym, kernel):
     return sym.split("<")[0].replace("_kernel", "") == KERNEL_SYMBOL.get(kernel, kernel)
 
 
-# Sustained VALU issue rate of one MI355X, measured (tools/valu_rates.hip, profiles/r4a_valu_rates.txt):
-# 8 waves per SIMD of independent v_dot4 / v_dot2 / v_alignbit / v_perm / v_bfe / v_pk_fma_f32 /
-# v_cvt / v_add+v_xor chains all issue at 0.44-0.48 of the nominal one-wave64-instruction-per-2-
-# cycles peak (256 CUs x 4 SIMD x 2.4 GHz / 2): one instruction per ~4.2 cycles per SIMD. The
-# integer kernels are priced against this rate (`valu_sustained_frac`) besides the nominal one.
-VALU_SUSTAINED_FRAC_OF_NOMINAL = 0.465
+# Sustained VALU issue rate of one MI355X, measured (tools/valu_rates.hip, profiles/r5d_valu_rates.txt):
+# at 8 waves per SIMD, chains of v_dot4 / v_dot2 / v_alignbit / v_perm / v_lerp_u8 / v_bfe /
+# v_pk_* / v_cvt issue at 0.44-0.48 of the nominal one-wave64-instruction-per-2-cycles peak
+# (256 CUs x 4 SIMD x 2.4 GHz / 2), v_add / v_xor / v_bitop3 / f32 add, mul, fma at 0.70-0.83.
+# The sustained peak is the fastest class (0.83 of nominal), so `valu_sustained_frac` is a lower
+# bound of a kernel's issue utilisation whatever its instruction mix (round 4 priced against
+# the integer class alone, and kernels rich in adds read above 1).
+VALU_SUSTAINED_FRAC_OF_NOMINAL = 0.83
 
 
 def measured_valu(kernel, batch):
