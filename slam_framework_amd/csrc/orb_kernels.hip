@@ -2314,7 +2314,12 @@ __device__ __forceinline__ int reduce_scatter16(int (&v)[16], int lane) {
 // LDS: one 40 x 44 u16 window per wave.
 // Variants measured and rejected in round 3 (dword row pairs, the horizontal pass on MFMA i8, a
 // shifted copy of the table) are in git history before round 4 and in DESIGN.md section 9.
-constexpr int kRtCols = 40, kRtRows = 44;  // u16 per transposed column (even)
+// u16 per transposed column (even, see the sample reads). 50 rather than the 43 + 1 the window
+// needs: a row-sum store instruction writes rows r .. r + 6 of the 10 column quads, and a
+// column-quad stride of 2 * 50 = 100 dwords (4 mod 32 banks) leaves only quads 8 and 9 sharing
+// banks with 0 and 1 (2-way), where 44 (24 mod 32) put three quads on one bank: LDS conflict
+// cycles per launch 2.64e8 -> 2.04e8 (profiles/r5zc_pmc_rt_rows.txt)
+constexpr int kRtCols = 40, kRtRows = 50;
 constexpr int kRtN = kRtCols * kRtRows;
 
 // KPW (<= kKpPerWave) keypoints per wave: 8 for batches, 4 for small launches (more waves in
