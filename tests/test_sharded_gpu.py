@@ -184,3 +184,26 @@ def test_world1_rccl_gather(oracle, world1, tmp_path):
     from slam_framework_amd.sharded import frame_results_equal
     for d in got:
         assert frame_results_equal(d, ref[d["frame"]]), f"frame {d['frame']}"
+
+
+def test_bench_shape_gather_matches_oracle(oracle, gpu_lib):
+    """configs[2] at the bench's own shape: one context of 256 frames (255 owned), two batches in
+    flight, three steps with the gather on (what bench.py times with SLAMGPU_BENCH_GATHER=1 or at
+    world > 1): the bench's self-check holds for 64 frames spread over the batch, and frames at the
+    start, middle and end of it equal the oracle (extraction, stereo, frame-to-frame search)."""
+    import torch
+    from slam_framework_amd.sharded import ShardedFrontend
+    dev = torch.device("cuda", 0)
+    Ls, Rs = S.layered_sequence(J.SEED, 16)
+    with torch.cuda.stream(torch.cuda.Stream(device=dev)):
+        job = ShardedFrontend(Ls, Rs, CAM, 256, dev, streams=1, inflight=2, gather=True)
+        last = [job.step() for _ in range(3)][-1]
+        job.sync()
+    got = job.gathered()
+    assert [d["frame"] for d in got] == list(range(1, 256))
+    info = job.check_gather()
+    assert info["identical"] and info["frames_checked_vs_rank0"] >= 15
+    _, _, parts = job.groups[last]
+    # (frames g with g % 16 == 0 pair the sequence's last render with its first: few matches)
+    pick = [got[i] for i in (0, 1, 126, 200, 254)]
+    _check_vs_oracle(oracle, pick, job.gframe, job.Bs, job.poses, job.D, Ls, Rs, parts)
