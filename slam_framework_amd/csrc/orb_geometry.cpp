@@ -267,14 +267,16 @@ int compute_geometry(const OrbParams& p, int cols, int rows, OrbGeom* g,
       L.oct_work_off = off;
       off += round_up(L.oct_nc * kWorkBytesPerNode, 16);
     }
+    // every level's node lists live in LDS at once: a large nfeatures (the monocular
+    // initialiser's 2 * nFeatures extractor, tracker.cpp:84-89) leaves no room for keys, and
+    // such a geometry runs every batch through octree_lvl_kernel (oct_kcap 0)
     const int kcap = std::min((kLdsBudget - off) / 4, 65535);
-    if (kcap < 1024) return -6;
-    g->oct_kcap = kcap;
+    g->oct_kcap = kcap >= 1024 ? kcap : 0;
     for (int l = 0; l < p.nlevels; l++) {  // keys go first
-      g->lv[l].oct_list_off += 4 * kcap;
-      g->lv[l].oct_work_off += 4 * kcap;
+      g->lv[l].oct_list_off += 4 * g->oct_kcap;
+      g->lv[l].oct_work_off += 4 * g->oct_kcap;
     }
-    g->oct_lds_bytes = off + 4 * kcap;
+    g->oct_lds_bytes = g->oct_kcap ? off + 4 * g->oct_kcap : 0;
   }
   {  // octree_lvl_kernel LDS (one work-group per CU: the small launches have <= 128 of them)
     // per node: sort key, pt / pe / pu / vnext, processed + candidate flags, the two scan

@@ -78,7 +78,7 @@ struct OrbGeom {
   int64_t keys_per_image;
   int64_t nodes_per_image;
   int oct_lds_bytes;     // octree_img_kernel dynamic LDS (keys + per-level lists and arrays)
-  int oct_kcap;          // keys of all levels of one image that fit in that LDS
+  int oct_kcap;          // keys of all levels of one image that fit in that LDS (0: no room)
   // octree_lvl_kernel (one work-group per level): one layout for every level
   // [keys u32 x oct2_kcap][gather staging u32 x oct2_kcap][cell prefix int x oct2_ccap]
   // [two node lists x oct2_nc][sort keys u32, pt / pe / pu / vnext i16, processed + candidate

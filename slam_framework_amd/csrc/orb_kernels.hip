@@ -2779,7 +2779,7 @@ void launch_extract(const ImageBatch& b, const OrbGeomDev& gd, int n_images, hip
   // the per-level kernel redoes its oversized levels itself (its LDS sized for the global
   // algorithm's scratch too): no octree_kernel launch after it -- the single-frame call's chain
   // is one dependent launch shorter; after the per-image kernel octree_kernel does them
-  const bool lvl = octree_per_level(n_images);
+  const bool lvl = g.oct_kcap == 0 || octree_per_level(n_images);
   if (lvl)
     SLAMGPU_LAUNCH("octree", st, octree_lvl_kernel, dim3(g.nlevels, n_images),
                    dim3(kOctLvlThreads), std::max((size_t)g.oct2_lds_bytes, sizeof(OctShared)),

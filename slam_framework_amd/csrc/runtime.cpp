@@ -262,11 +262,12 @@ int slamgpu_create(int device, const slamgpu_orb_params* p, int cols, int rows, 
         "would be empty, orb_extractor.cpp:712-733)",
         "a pyramid level yields no initial octree node (orb_extractor.cpp:484-486)",
         "FAST cell wider than 64 pixels", "resize span exceeds the pyr_down window",
-        "unsupported Gaussian kernel or octree LDS budget"};
+        "unsupported Gaussian kernel",
+        "a level's octree nodes overflow octree_lvl_kernel's LDS budget"};
     delete c;
     return create_fail(SLAMGPU_EINVAL, "slamgpu_create(%dx%d, nlevels %d, scale %g): %s", cols,
                        rows, p->nlevels, (double)p->scale_factor,
-                       why[std::min(std::max(-gr, 0), 6)]);
+                       why[std::min(std::max(-gr, 0), 7)]);
   }
   compute_tables(c->params, &c->tables);
   if (c->geom.kp_cap > 4096) {  // matcher keys carry a 12-bit keypoint index

@@ -49,3 +49,40 @@ def test_stages_match_oracle(oracle, gpu_lib, seed):
         octo = oracle.distribute_octree(t, pyr, l, cand)
         np.testing.assert_array_equal(ctx.debug_level_keys(0, l, 1), oracle.pack_keys(octo),
                                       err_msg=f"octree level {l}")
+
+
+def test_init_extractor_double_features(oracle, gpu_lib):
+    """The monocular initialiser's extractor takes 2 * nFeatures (tracker.cpp:84-89): 4000 on the
+    KITTI config. Every level's octree node lists then overflow the per-image octree kernel's LDS,
+    so every batch size runs octree_lvl_kernel (octree_global for a level whose keys do not fit).
+    One extract call and an 18-image batch (above OCT_LVL_MAX_IMAGES, where a 2000-feature
+    context would take the per-image kernel; one uniform-noise frame) must match the oracle."""
+    import torch
+    nf = 4000
+    t = oracle.tables(nfeatures=nf, scale_factor=1.2, nlevels=8, ini_th=20, min_th=7)
+    ctx = gpu_lib.Context(S.KITTI_COLS, S.KITTI_ROWS, nf, 1.2, 8, 20, 7, max_frames=9)
+    assert ctx.kp_cap <= 4096
+    img = S.image(1004)
+    kr, dr = oracle.extract(t, img)[:2]
+    kg, dg = ctx.extract(img)
+    assert len(kr) > 3000
+    _compare_kps(kg, kr)
+    np.testing.assert_array_equal(dg, dr)
+
+    cols, rows, pitch, B = S.KITTI_COLS, S.KITTI_ROWS, 1280, 9
+    L = np.zeros((B, rows, pitch), np.uint8)
+    R = np.zeros((B, rows, pitch), np.uint8)
+    for f in range(B):
+        L[f, :, :cols], R[f, :, :cols] = S.stereo_pair(2000 + f)
+    L[4, :, :cols] = np.random.default_rng(5).integers(0, 256, (rows, cols), dtype=np.uint8)
+    dev = torch.device("cuda", 0)
+    d_l, d_r = torch.from_numpy(L).to(dev), torch.from_numpy(R).to(dev)
+    torch.cuda.synchronize()
+    ctx.frontend_device(d_l, d_r, rows * pitch, pitch, B, S.KITTI_CAM)
+    ctx.sync()
+    for f, side in ((0, 0), (4, 0), (4, 1), (8, 1)):
+        src = (L if side == 0 else R)[f, :, :cols]
+        kr, dr = oracle.extract(t, np.ascontiguousarray(src))[:2]
+        kg, dg = ctx.keypoints(2 * f + side)
+        _compare_kps(kg, kr)
+        np.testing.assert_array_equal(dg, dr)
