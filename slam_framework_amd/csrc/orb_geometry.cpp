@@ -171,6 +171,36 @@ int compute_geometry(const OrbParams& p, int cols, int rows, OrbGeom* g,
     }
   }
   g->cells_per_image = cell_base;
+  // pyr_ring_kernel's row segments: lane k of a 256-column tile reads source dwords q0 .. q0 + 2
+  // (clamped to the row's last dword) of columns 4k .. 4k + 3; the segment starts at the tile's
+  // first dword rounded down to 16 bytes
+  int ring_slots = 0;
+  bool ring_ok = true;
+  for (int l = 1; l < p.nlevels; l++) {
+    LevelGeom& L = g->lv[l];
+    const LevelGeom& S = g->lv[l - 1];
+    const int qmax = (S.w - 1) >> 2;
+    auto q0 = [&](int x) { return std::min((*rx)[L.rx_base + std::min(x, L.w - 1)].sx >> 2, qmax); };
+    int span = 0;
+    for (int x0 = 0; x0 < L.w; x0 += 256) {
+      const int lo = (4 * q0(x0)) & ~15;
+      int hi = 0;
+      for (int k = 0; k < 64; k++) hi = std::max(hi, 4 * std::min(q0(x0 + 4 * k) + 2, qmax) + 4);
+      span = std::max(span, hi - lo);
+    }
+    int nsrc = 0;
+    for (int dy0 = 0; dy0 < L.h; dy0 += PYR_RING_STRIP) {
+      const int dy1 = std::min(dy0 + PYR_RING_STRIP, L.h) - 1;
+      nsrc = std::max(nsrc, (*ry)[L.ry_base + dy1].y1 - (*ry)[L.ry_base + dy0].y0 + 1);
+    }
+    L.pyr_lpr = (span + 15) / 16;
+    L.pyr_rpi = L.pyr_lpr <= 64 ? 64 / L.pyr_lpr : 0;
+    L.pyr_inv_rpi = L.pyr_rpi ? (65536 + L.pyr_rpi - 1) / L.pyr_rpi : 0;
+    L.pyr_slots = L.pyr_rpi ? (nsrc + L.pyr_rpi - 1) / L.pyr_rpi : 0;
+    ring_ok = ring_ok && L.pyr_rpi > 0;
+    ring_slots = std::max(ring_slots, L.pyr_slots);
+  }
+  g->pyr_ring_slots = ring_ok ? ring_slots : 0;
   {  // pyr_band_kernel's row bands, top-down from the last level
     const int nb = p.nlevels > 2 ? std::min(std::max(g->lv[2].h / 12, 1), kPyrMaxBands) : 0;
     g->pyr_bands = nb;

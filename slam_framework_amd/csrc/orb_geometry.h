@@ -33,6 +33,13 @@ struct CellDesc {
 };
 static_assert(sizeof(CellDesc) == 16, "CellDesc is one dwordx4");
 
+#ifndef PYR_STRIP
+#define PYR_STRIP 16  // pyr_down output rows per wave (batches)
+#endif
+#ifndef PYR_RING_STRIP
+#define PYR_RING_STRIP 16  // pyr_ring_kernel output rows per wave (batches)
+#endif
+
 struct LevelGeom {
   int w, h;             // level image size
   int pitch;            // row pitch of this level in the pyramid buffers (level >= 1)
@@ -58,6 +65,10 @@ struct LevelGeom {
   // resize tables (level >= 1) in the shared table buffer
   int rx_base, ry_base; // offsets into the x (per dst column) / y (per dst row) tables
   int xmax;             // first dst column that copies S[sx] * 2048 (resize HResizeLinear)
+  // pyr_ring_kernel (level >= 1): a strip's source rows staged in LDS by 16-byte buffer-to-LDS
+  // loads, pyr_rpi rows of pyr_lpr chunks per 1 KiB slot (0: the row segment needs > 1 KiB);
+  // pyr_slots slots hold the largest strip's rows; pyr_inv_rpi = ceil(2^16 / pyr_rpi)
+  int pyr_lpr, pyr_rpi, pyr_inv_rpi, pyr_slots;
   double rsx;           // resize scale_x = 1 / (w / w_prev) (level >= 1; pyr_band_kernel
                         // derives the column coefficients from it exactly as the host tables)
   float scale, inv_scale;
@@ -93,6 +104,7 @@ struct OrbGeom {
   // rows [pyr_band[s][l][0], pyr_band[s][l][1]) of level l -- its share of the level plus every
   // source row its own next level needs (so a band reads only rows it wrote itself)
   int pyr_bands;
+  int pyr_ring_slots;  // pyr_ring_kernel: 1 KiB LDS slots per wave (max over levels; 0: unusable)
   int pyr_band_lds;  // bytes of one of its two LDS row buffers (the largest band level)
   int16_t pyr_band[kPyrMaxBands][kMaxLevels][2];
 };

@@ -52,13 +52,11 @@ __device__ __forceinline__ uint32_t dot2u(uint32_t a, uint32_t b, uint32_t c) {
                                 false);
 }
 
-#ifndef PYR_STRIP
-#define PYR_STRIP 16
-#endif
 #ifndef PYR_CHUNK
 #define PYR_CHUNK 2
 #endif
 constexpr int kPyrStrip = PYR_STRIP;  // output rows per wave
+constexpr int kPyrRingStrip = PYR_RING_STRIP;
 constexpr int kPyrChunk = PYR_CHUNK;  // source rows fetched per batch
 #ifndef PYR_SHORT_STRIP
 #define PYR_SHORT_STRIP 4
@@ -72,13 +70,17 @@ constexpr int kPyrShortStrip = PYR_SHORT_STRIP, kPyrShortMaxImages = 16;
 // short strips so that more waves share a level and each walks a shorter chain of row loads.
 // One wave: output rows [dy0, dy0 + min(kStrip, nlim)) x columns [256 tx, 256 tx + 256) of
 // `level`. A strip fetches every source row its rows need, so strips compose in any partition.
-template <bool kAligned, int kStrip>
+// kRing (pyr_ring_kernel): every source row of the strip is first staged in the wave's LDS
+// slots (`ring`, D.pyr_slots KiB) by 16-byte buffer-to-LDS loads issued at once -- a strip's
+// whole input in flight with no VGPRs held -- and the rows are then read from LDS.
+template <bool kAligned, int kStrip, bool kRing = false>
 __device__ __forceinline__ void pyr_strip(const ImageBatch& b, const OrbGeom* __restrict__ g,
                                           int level, int img, int tx, int dy0,
                                           const ResizeX* __restrict__ rxt,
                                           const ResizeY* __restrict__ ryt, int nlim = kStrip,
                                           const uint8_t* src_rows = nullptr, int src_row0 = 0,
-                                          uint8_t* copy_rows = nullptr, int copy_row0 = 0) {
+                                          uint8_t* copy_rows = nullptr, int copy_row0 = 0,
+                                          uint8_t* ring = nullptr) {
   const int lane = threadIdx.x & 63;
   const LevelGeom& D = g->lv[level];
   const LevelGeom& S = g->lv[level - 1];
@@ -126,10 +128,37 @@ __device__ __forceinline__ void pyr_strip(const ImageBatch& b, const OrbGeom* __
   const __amdgpu_buffer_rsrc_t srsrc = __builtin_amdgcn_make_buffer_rsrc(
       (void*)uniform_ptr(src), 0, __builtin_amdgcn_readfirstlane(spitch * S.h), 0x00020000);
   const int oa = 4 * qa, ob = 4 * qb, oc = 4 * qc;
+  // kRing: the strip's rows [sy_lo, sy_hi], row r in slot r / rpi at (r % rpi) * lpr * 16; each
+  // row's bytes from seg0 (lane 0's first dword, rounded down to 16 bytes) on
+  const int lpr = kRing ? D.pyr_lpr : 1, rpi = kRing ? D.pyr_rpi : 1;
+  const int inv_rpi = kRing ? D.pyr_inv_rpi : 0;
+  const int seg0 = kRing ? __builtin_amdgcn_readfirstlane(oa) & ~15 : 0;
+  const int ra = (oa - seg0) >> 2, rb_ = (ob - seg0) >> 2, rc = (oc - seg0) >> 2;
+  if constexpr (kRing) {
+    const int rl = lane / lpr, cl = lane - rl * lpr;  // this lane's row in a slot and chunk
+    const int nsrc = sy_hi - sy_lo + 1;
+    for (int k = 0; k * rpi < nsrc; k++) {
+      // lanes past the slot's rows repeat its last row into the slot's unused tail
+      const int r = min(k * rpi + min(rl, rpi - 1), nsrc - 1);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(
+          srsrc, (__attribute__((address_space(3))) void*)(ring + 1024 * k), 16,
+          (uint32_t)((sy_lo + r) * spitch + seg0 + 16 * cl), 0, 0, 0);
+    }
+    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): the rows have landed
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+  }
   auto fetch = [&](int sy, uint32_t (&wv)[3]) {
     const int roff = __builtin_amdgcn_readfirstlane((min(sy, sy_hi) - srow0) * spitch);
     const uint8_t* row = src + roff;  // wave-uniform
-    if (aligned && gsrc) {  // clamped dwords stay inside the row; bytes past sx+1: zero weight
+    if constexpr (kRing) {
+      const int r = min(sy, sy_hi) - sy_lo, slot = (r * inv_rpi) >> 16;  // r < 64: exact
+      const uint32_t* rw = reinterpret_cast<const uint32_t*>(
+          ring + 1024 * slot + (r - slot * rpi) * lpr * 16);
+      wv[0] = rw[(uint32_t)ra];
+      wv[1] = rw[(uint32_t)rb_];
+      wv[2] = rw[(uint32_t)rc];
+    } else if (aligned && gsrc) {  // clamped dwords stay inside the row; bytes past sx+1: zero weight
       wv[0] = __builtin_amdgcn_raw_buffer_load_b32(srsrc, oa, roff, 0);
       wv[1] = __builtin_amdgcn_raw_buffer_load_b32(srsrc, ob, roff, 0);
       wv[2] = __builtin_amdgcn_raw_buffer_load_b32(srsrc, oc, roff, 0);
@@ -239,6 +268,22 @@ __global__ __launch_bounds__(256) void pyr_down_kernel(ImageBatch b, const OrbGe
   const int tiles_x = (g->lv[level].w + 255) >> 8;
   const int tx = bx % tiles_x, ty = bx / tiles_x;
   pyr_strip<kAligned, kStrip>(b, g, level, img, tx, (ty * 4 + wave_id()) * kStrip, rxt, ryt);
+}
+
+// pyr_down with each wave's source rows staged in LDS (pyr_strip kRing): g->pyr_ring_slots KiB
+// of dynamic LDS per wave
+__global__ __launch_bounds__(256) void pyr_ring_kernel(ImageBatch b, const OrbGeom* __restrict__ g,
+                                                       int level,
+                                                       const ResizeX* __restrict__ rxt,
+                                                       const ResizeY* __restrict__ ryt) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t s_ring[];
+  int img, bx;
+  xcd_image_block(&img, &bx);
+  const int tiles_x = (g->lv[level].w + 255) >> 8;
+  const int tx = bx % tiles_x, ty = bx / tiles_x;
+  uint8_t* ring = s_ring + 1024 * g->pyr_ring_slots * wave_id();
+  pyr_strip<true, kPyrRingStrip, true>(b, g, level, img, tx, (ty * 4 + wave_id()) * kPyrRingStrip,
+                                       rxt, ryt, kPyrRingStrip, nullptr, 0, nullptr, 0, ring);
 }
 
 // Small launches (the single-frame call): levels 2 .. nlevels - 1 in one launch of row bands
@@ -2725,10 +2770,18 @@ void launch_extract(const ImageBatch& b, const OrbGeomDev& gd, int n_images, hip
   const bool in_aligned = (((uintptr_t)b.in_l | (uintptr_t)b.in_r | (uintptr_t)b.in_stride |
                            (uintptr_t)b.in_pitch) & 3) == 0;
   const bool short_strips = n_images <= kPyrShortMaxImages;
+  // batches: the LDS-staged strips (16-byte buffer-to-LDS loads need 16-byte aligned rows)
+  static const int ring_mode = [] {
+    const char* e = std::getenv("SLAMGPU_PYR_RING");
+    return e ? std::atoi(e) : 0xfe;
+  }();
+  // SLAMGPU_PYR_RING: bit l selects the LDS-staged kernel for level l (A/B)
+  const bool ring_ok = glds && g.pyr_ring_slots > 0 && g.pyr_ring_slots <= 8;
   // small launches: level 1 over the chip, then levels 2+ in one launch of row bands
   const int l_end = (short_strips && g.pyr_bands > 0) ? 2 : g.nlevels;
   for (int l = 1; l < l_end; l++) {
-    const int strip = short_strips ? kPyrShortStrip : kPyrStrip;
+    const bool ring = ring_ok && !short_strips && ((ring_mode >> l) & 1);
+    const int strip = short_strips ? kPyrShortStrip : ring ? kPyrRingStrip : kPyrStrip;
     const int tiles = ((g.lv[l].w + 255) >> 8) * ((g.lv[l].h + 4 * strip - 1) / (4 * strip));
     const dim3 grid(tiles, n_images);
     if (short_strips) {
@@ -2738,6 +2791,9 @@ void launch_extract(const ImageBatch& b, const OrbGeomDev& gd, int n_images, hip
       else
         SLAMGPU_LAUNCH("pyr_down", st, (pyr_down_kernel<false, kPyrShortStrip>), grid, dim3(256),
                        0, st, b, gd.dev, l, gd.rx, gd.ry);
+    } else if (ring) {
+      SLAMGPU_LAUNCH("pyr_down", st, pyr_ring_kernel, grid, dim3(256),
+                     (size_t)4096 * g.pyr_ring_slots, st, b, gd.dev, l, gd.rx, gd.ry);
     } else if (l > 1 || in_aligned) {
       SLAMGPU_LAUNCH("pyr_down", st, (pyr_down_kernel<true, kPyrStrip>), grid, dim3(256), 0, st,
                      b, gd.dev, l, gd.rx, gd.ry);
