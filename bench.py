@@ -47,12 +47,14 @@ VALU_FILE = os.path.join(ROOT, "profiles", "valu.json")
 
 
 # bench.py's timing names -> kernel symbols where they differ (the octree timing is the per-image
-# kernel; octree_kernel is its global-memory fallback)
-KERNEL_SYMBOL = {"octree": "octree_img", "octree_global": "octree"}
+# kernel; octree_kernel is its global-memory fallback; the batches' pyramid levels run
+# pyr_ring_kernel, the single-frame call pyr_down_kernel)
+KERNEL_SYMBOL = {"octree": ("octree_img",), "octree_global": ("octree",),
+                 "pyr_down": ("pyr_down", "pyr_ring")}
 
 
 def _symbol_matches(sym, kernel):
-    return sym.split("<")[0].replace("_kernel", "") == KERNEL_SYMBOL.get(kernel, kernel)
+    return sym.split("<")[0].replace("_kernel", "") in KERNEL_SYMBOL.get(kernel, (kernel,))
 
 
 # Sustained VALU issue rate of one MI355X, measured (tools/valu_rates.hip, profiles/r5d_valu_rates.txt):

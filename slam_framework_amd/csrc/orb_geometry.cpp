@@ -172,8 +172,8 @@ int compute_geometry(const OrbParams& p, int cols, int rows, OrbGeom* g,
   }
   g->cells_per_image = cell_base;
   // pyr_ring_kernel's row segments: lane k of a 256-column tile reads source dwords q0 .. q0 + 2
-  // (clamped to the row's last dword) of columns 4k .. 4k + 3; the segment starts at the tile's
-  // first dword rounded down to 16 bytes
+  // of columns 4k .. 4k + 3 (unclamped: bytes past the row's end have zero weight); the segment
+  // starts at the tile's first dword rounded down to 16 bytes
   int ring_slots = 0;
   bool ring_ok = true;
   for (int l = 1; l < p.nlevels; l++) {
@@ -185,7 +185,7 @@ int compute_geometry(const OrbParams& p, int cols, int rows, OrbGeom* g,
     for (int x0 = 0; x0 < L.w; x0 += 256) {
       const int lo = (4 * q0(x0)) & ~15;
       int hi = 0;
-      for (int k = 0; k < 64; k++) hi = std::max(hi, 4 * std::min(q0(x0 + 4 * k) + 2, qmax) + 4);
+      for (int k = 0; k < 64; k++) hi = std::max(hi, 4 * (q0(x0 + 4 * k) + 2) + 4);
       span = std::max(span, hi - lo);
     }
     int nsrc = 0;
@@ -196,6 +196,7 @@ int compute_geometry(const OrbParams& p, int cols, int rows, OrbGeom* g,
     L.pyr_lpr = (span + 15) / 16;
     L.pyr_rpi = L.pyr_lpr <= 64 ? 64 / L.pyr_lpr : 0;
     L.pyr_inv_rpi = L.pyr_rpi ? (65536 + L.pyr_rpi - 1) / L.pyr_rpi : 0;
+    L.pyr_inv_lpr = (65536 + L.pyr_lpr - 1) / L.pyr_lpr;
     L.pyr_slots = L.pyr_rpi ? (nsrc + L.pyr_rpi - 1) / L.pyr_rpi : 0;
     ring_ok = ring_ok && L.pyr_rpi > 0;
     ring_slots = std::max(ring_slots, L.pyr_slots);

@@ -67,8 +67,9 @@ struct LevelGeom {
   int xmax;             // first dst column that copies S[sx] * 2048 (resize HResizeLinear)
   // pyr_ring_kernel (level >= 1): a strip's source rows staged in LDS by 16-byte buffer-to-LDS
   // loads, pyr_rpi rows of pyr_lpr chunks per 1 KiB slot (0: the row segment needs > 1 KiB);
-  // pyr_slots slots hold the largest strip's rows; pyr_inv_rpi = ceil(2^16 / pyr_rpi)
-  int pyr_lpr, pyr_rpi, pyr_inv_rpi, pyr_slots;
+  // pyr_slots slots hold the largest strip's rows; pyr_inv_rpi = ceil(2^16 / pyr_rpi),
+  // pyr_inv_lpr = ceil(2^16 / pyr_lpr) (quotients of values < 64 by a multiply)
+  int pyr_lpr, pyr_rpi, pyr_inv_rpi, pyr_inv_lpr, pyr_slots;
   double rsx;           // resize scale_x = 1 / (w / w_prev) (level >= 1; pyr_band_kernel
                         // derives the column coefficients from it exactly as the host tables)
   float scale, inv_scale;

@@ -133,9 +133,11 @@ __device__ __forceinline__ void pyr_strip(const ImageBatch& b, const OrbGeom* __
   const int lpr = kRing ? D.pyr_lpr : 1, rpi = kRing ? D.pyr_rpi : 1;
   const int inv_rpi = kRing ? D.pyr_inv_rpi : 0;
   const int seg0 = kRing ? __builtin_amdgcn_readfirstlane(oa) & ~15 : 0;
-  const int ra = (oa - seg0) >> 2, rb_ = (ob - seg0) >> 2, rc = (oc - seg0) >> 2;
+  // the lane's first dword in a staged row; it reads that dword and the next two unclamped (a
+  // byte past the row's end has zero weight, as behind the clamped reads' repeated dword)
+  const int ra = (oa - seg0) >> 2;
   if constexpr (kRing) {
-    const int rl = lane / lpr, cl = lane - rl * lpr;  // this lane's row in a slot and chunk
+    const int rl = (lane * D.pyr_inv_lpr) >> 16, cl = lane - rl * lpr;  // row in a slot, chunk
     const int nsrc = sy_hi - sy_lo + 1;
     for (int k = 0; k * rpi < nsrc; k++) {
       // lanes past the slot's rows repeat its last row into the slot's unused tail
@@ -155,9 +157,10 @@ __device__ __forceinline__ void pyr_strip(const ImageBatch& b, const OrbGeom* __
       const int r = min(sy, sy_hi) - sy_lo, slot = (r * inv_rpi) >> 16;  // r < 64: exact
       const uint32_t* rw = reinterpret_cast<const uint32_t*>(
           ring + 1024 * slot + (r - slot * rpi) * lpr * 16);
-      wv[0] = rw[(uint32_t)ra];
-      wv[1] = rw[(uint32_t)rb_];
-      wv[2] = rw[(uint32_t)rc];
+      const uint32_t* rl_ = rw + (uint32_t)ra;
+      wv[0] = rl_[0];
+      wv[1] = rl_[1];
+      wv[2] = rl_[2];
     } else if (aligned && gsrc) {  // clamped dwords stay inside the row; bytes past sx+1: zero weight
       wv[0] = __builtin_amdgcn_raw_buffer_load_b32(srsrc, oa, roff, 0);
       wv[1] = __builtin_amdgcn_raw_buffer_load_b32(srsrc, ob, roff, 0);
