@@ -31,7 +31,7 @@ struct FrameKps {
 
 struct StereoWorkspace {
   int* row_start;      // [frame][rows + 1]
-  int* row_items;      // [frame][row_cap]
+  uint2* row_items;    // [frame][row_cap]: (right keypoint | octave << 16, its x as float bits)
   int row_cap;
   int* sad;            // [frame][kp_cap] SAD score of accepted matches (-1 otherwise)
 };

@@ -106,12 +106,15 @@ __device__ __forceinline__ void stereo_rows_body(int f, const OrbGeom* __restric
   const KeyPoint* kr = ext.kps + ir * ext.stride;
   const int nr = ext.n[ir * ext.n_stride];
   int* rs = ws.row_start + (int64_t)f * (nrows + 1);
-  int* items = ws.row_items + (int64_t)f * ws.row_cap;
+  uint2* items = ws.row_items + (int64_t)f * ws.row_cap;
   for (int i = tid; i <= nrows; i += NT) cnt[i] = 0;
   __syncthreads();
   // a thread's keypoints are loaded kChunk at a time before their row updates: one load latency
   // per chunk instead of one per keypoint (a single frame runs this as one work-group)
   constexpr int kChunk = 2048 / NT;
+  // the row items carry the candidate's octave and x, the matcher's first filter (one load per
+  // candidate instead of the item and then its keypoint)
+  uint2 kit[kChunk];
   auto row_span = [&](int base, int (&lo)[kChunk], int (&hi)[kChunk]) {
     float ky[kChunk];
     int ko[kChunk];
@@ -123,6 +126,7 @@ __device__ __forceinline__ void stereo_rows_body(int f, const OrbGeom* __restric
       if (i < nr) {
         ky[u] = kr[i].y;
         ko[u] = kr[i].octave;
+        kit[u] = make_uint2((uint32_t)i | (uint32_t)ko[u] << 16, __float_as_uint(kr[i].x));
       }
     }
 #pragma unroll
@@ -158,7 +162,7 @@ __device__ __forceinline__ void stereo_rows_body(int f, const OrbGeom* __restric
     for (int u = 0; u < kChunk; u++)
       for (int yi = lo[u]; yi <= hi[u]; ++yi) {
         const int pos = atomicAdd(&cnt[yi], 1);
-        if (pos < ws.row_cap) items[pos] = base + NT * u + tid;
+        if (pos < ws.row_cap) items[pos] = kit[u];
       }
   }
 }
@@ -206,13 +210,12 @@ __global__ __launch_bounds__(256) void stereo_match_kernel(ImageBatch b,
   }
   KeyPoint kpL{};
   if (ok) kpL = ext.kps[il * ext.stride + iL];
-  const KeyPoint* kr = ext.kps + ir * ext.stride;
   const int levelL = kpL.octave;
   const float vL = kpL.y, uL = kpL.x;
   const int row = (int)vL;
   ok = ok && row >= 0 && row < nrows;
   const int* rs = ws.row_start + (int64_t)f * (nrows + 1);
-  const int* items = ws.row_items + (int64_t)f * ws.row_cap;
+  const uint2* items = ws.row_items + (int64_t)f * ws.row_cap;
   int c0 = 0, c1 = 0;
   if (ok) {
     c0 = rs[row];
@@ -226,6 +229,7 @@ __global__ __launch_bounds__(256) void stereo_match_kernel(ImageBatch b,
   const uint8_t* dL = ext.desc + (il * ext.stride + (ok ? iL : 0)) * 32;
   const uint8_t* dRb = ext.desc + ir * ext.stride * 32;
   uint32_t best = ((uint32_t)TH_HIGH << 16) | 0xffffu;
+  float bestU = 0.0f;  // x of this lane's best candidate
   if (ok) {
     // kCandU candidates per lane at a time, each stage's loads all in flight before the next
     // stage needs them: row items -> (octave, x) -> descriptors -> distances (the loop was a
@@ -235,20 +239,17 @@ __global__ __launch_bounds__(256) void stereo_match_kernel(ImageBatch b,
     const uint4 l0 = dLq[0], l1 = dLq[1];
     for (int cb = c0 + hl; cb < c1; cb += G * kCandU) {
       int iR[kCandU];
-#pragma unroll
-      for (int u = 0; u < kCandU; u++) {
-        const int c = cb + G * u;
-        iR[u] = c < c1 ? items[c] : -1;
-      }
+      float uR[kCandU];
       bool pass[kCandU];
 #pragma unroll
       for (int u = 0; u < kCandU; u++) {
-        pass[u] = false;
-        if (iR[u] >= 0) {
-          const int oct = kr[iR[u]].octave;
-          const float uR = kr[iR[u]].x;
-          pass[u] = oct >= levelL - 1 && oct <= levelL + 1 && uR >= minU && uR <= maxU;
-        }
+        const int c = cb + G * u;
+        const uint2 it = c < c1 ? items[c] : make_uint2(0xffffffffu, 0u);
+        iR[u] = (int)(it.x & 0xffffu);
+        const int oct = (int)(it.x >> 16);
+        uR[u] = __uint_as_float(it.y);
+        pass[u] = c < c1 && oct >= levelL - 1 && oct <= levelL + 1 && uR[u] >= minU &&
+                  uR[u] <= maxU;
       }
       uint4 r0[kCandU], r1[kCandU];
 #pragma unroll
@@ -265,17 +266,24 @@ __global__ __launch_bounds__(256) void stereo_match_kernel(ImageBatch b,
                            __popc(l0.w ^ r0[u].w) + __popc(l1.x ^ r1[u].x) + __popc(l1.y ^ r1[u].y) +
                            __popc(l1.z ^ r1[u].z) + __popc(l1.w ^ r1[u].w);
           const uint32_t key = ((uint32_t)dist << 16) | (uint32_t)iR[u];
-          if (dist < TH_HIGH && key < best) best = key;
+          if (dist < TH_HIGH && key < best) {
+            best = key;
+            bestU = uR[u];
+          }
         }
     }
   }
+  const uint32_t mine = best;
   best = group_min<G>(best);
+  // the x of the group's best candidate from the lane that found it (keys are unique)
+  const uint64_t gmask = (G == 64 ? ~0ull : ((1ull << G) - 1ull)) << (G * grp);
+  const uint64_t hit = __ballot(mine == best) & gmask;
+  const float uRbest = __shfl(bestU, hit ? __builtin_ctzll(hit) : lane, 64);
   const int bestDist = (int)(best >> 16);
   const int thOrbDist = (TH_HIGH + TH_LOW) / 2;
   ok = ok && bestDist < thOrbDist;
   // sliding-window SAD at the left keypoint's level (:481-531)
-  const int bestIdxR = ok ? (int)(best & 0xffff) : 0;
-  const float uR0 = ok ? kr[bestIdxR].x : 0.f;
+  const float uR0 = ok ? uRbest : 0.f;
   const float scaleFactor = g->lv[levelL].inv_scale;
   const float scaleduL = roundf(kpL.x * scaleFactor);
   const float scaledvL = roundf(kpL.y * scaleFactor);
