@@ -65,7 +65,7 @@ void launch_undistort(const FrameKps& src, KeyPoint* dst, int64_t dst_stride, co
 // Per-frame keypoint grid (AssignFeaturesToGrid), CSR over the 64x48 cells.
 struct GridWorkspace {
   int* cell_start;     // [frame][kGridCells + 1]
-  int* cell_items;     // [frame][kp_cap] keypoint indices
+  uint4* cell_items;   // [frame][kp_cap]: (keypoint index | octave << 16, x, y as float bits, 0)
   int* cell_fill;      // [frame][kGridCells] scratch
 };
 

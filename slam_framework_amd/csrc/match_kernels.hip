@@ -645,19 +645,23 @@ __device__ __forceinline__ void grid_build_body(int f, const FrameKps& cur, cons
   const KeyPoint* k = cur.kps + f * cur.stride;
   const int n = cur.n[f * cur.n_stride];
   int* cs = gw.cell_start + (int64_t)f * (kGridCells + 1);
-  int* items = gw.cell_items + (int64_t)f * kp_cap;
+  uint4* items = gw.cell_items + (int64_t)f * kp_cap;
   for (int i = tid; i <= kGridCells; i += NT) cnt[i] = 0;
-  // cells of a thread's keypoints, kChunk loads in flight at a time
+  // cells of a thread's keypoints, kChunk loads in flight at a time; the items carry the fields
+  // the projection searches filter on first (one load per candidate instead of two)
   constexpr int kChunk = 2048 / NT;
+  float kx[kChunk], ky[kChunk];
+  int ko[kChunk];
   auto cells = [&](int base, int (&c)[kChunk]) {
-    float kx[kChunk], ky[kChunk];
 #pragma unroll
     for (int u = 0; u < kChunk; u++) {
       const int i = base + NT * u + tid;
       kx[u] = ky[u] = 0.0f;
+      ko[u] = 0;
       if (i < n) {
         kx[u] = k[i].x;
         ky[u] = k[i].y;
+        ko[u] = k[i].octave;
       }
     }
 #pragma unroll
@@ -682,7 +686,10 @@ __device__ __forceinline__ void grid_build_body(int f, const FrameKps& cur, cons
     cells(base, c);
 #pragma unroll
     for (int u = 0; u < kChunk; u++)
-      if (c[u] >= 0) items[atomicAdd(&cnt[c[u]], 1)] = base + NT * u + tid;
+      if (c[u] >= 0)
+        items[atomicAdd(&cnt[c[u]], 1)] =
+            make_uint4((uint32_t)(base + NT * u + tid) | (uint32_t)ko[u] << 16,
+                       __float_as_uint(kx[u]), __float_as_uint(ky[u]), 0u);
   }
 }
 __global__ __launch_bounds__(256) void grid_build_kernel(FrameKps cur, Camera cam, int kp_cap,
@@ -761,7 +768,7 @@ struct FrameView {
   const uint8_t* desc;
   const float* u_right;
   const int* cell_start;
-  const int* cell_items;
+  const uint4* cell_items;
   const uint8_t* blocked;
 };
 
@@ -864,19 +871,21 @@ __device__ int scan_query_k(const ScanCtx& c, const Camera& cam, const FrameView
         const int p = __shfl(q0, lo, 64) + (k - __shfl(excl, lo, 64));
         const int pcell = __shfl(cell, lo, 64);
         if (k >= npairs) continue;
-        const int i = F.cell_items[p];
-        const KeyPoint kp = F.kps[i];
+        const uint4 it = F.cell_items[p];
+        const int i = (int)(it.x & 0xffffu), octave = (int)(it.x >> 16);
         if (bCheckLevels) {
-          if (kp.octave < c.min_level) continue;
-          if (c.max_level >= 0 && kp.octave > c.max_level) continue;
+          if (octave < c.min_level) continue;
+          if (c.max_level >= 0 && octave > c.max_level) continue;
         }
-        const float distx = kp.x - c.x, disty = kp.y - c.y;
+        const float distx = __uint_as_float(it.y) - c.x, disty = __uint_as_float(it.z) - c.y;
         if (!(fabsf(distx) < c.r && fabsf(disty) < c.r)) continue;
-        if (F.blocked[i]) continue;
-        if (claimed && (claimed[i >> 5] >> (i & 31)) & 1u) continue;
+        // the remaining filters' loads all in flight together (the filters commute)
+        const bool blk = F.blocked[i] != 0;
         const float ur = F.u_right[i];
-        if (ur > 0 && fabsf(c.ur - ur) > c.gate) continue;
         const int dist = hamming32(c.desc, F.desc + i * 32);
+        if (blk) continue;
+        if (claimed && (claimed[i >> 5] >> (i & 31)) & 1u) continue;
+        if (ur > 0 && fabsf(c.ur - ur) > c.gate) continue;
         if (dist > c.max_dist) continue;
         const K key = scan_key<K>(dist, pcell, i);
         cnt++;
