@@ -234,7 +234,10 @@ __global__ __launch_bounds__(256) void stereo_match_kernel(ImageBatch b,
     // kCandU candidates per lane at a time, each stage's loads all in flight before the next
     // stage needs them: row items -> (octave, x) -> descriptors -> distances (the loop was a
     // chain of three dependent loads per candidate)
-    constexpr int kCandU = 2;  // 2 and 4 measured equal (0.35 ms/step), 2 holds fewer VGPRs
+    // 2 and 4 measured equal (0.35 ms/step), 2 holds fewer VGPRs; with the packed row items
+    // (two loads per candidate) 2 is still best, as are 16 lanes per keypoint (8 / 32 lanes and
+    // 4 candidates: 0.29-0.36 ms against 0.28, profiles/r6d_stereo_lanes_ab.log)
+    constexpr int kCandU = 2;
     const uint4* dLq = reinterpret_cast<const uint4*>(dL);
     const uint4 l0 = dLq[0], l1 = dLq[1];
     for (int cb = c0 + hl; cb < c1; cb += G * kCandU) {
