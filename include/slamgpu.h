@@ -62,7 +62,10 @@ typedef struct {
 /* ---- lifecycle ---------------------------------------------------------------------------- */
 /* Replaces: ORBextractor::ORBextractor (orb_extractor.cpp:351-411) for images of cols x rows,
  * batched up to max_frames stereo pairs (2 * max_frames images). Returns 0 and *out, or a
- * negative code with *out = NULL (nothing to destroy; the reason: slamgpu_last_error(NULL)). */
+ * negative code with *out = NULL (nothing to destroy; the reason: slamgpu_last_error(NULL)).
+ * Limits: at most 4096 keypoints per image (slamgpu_kp_capacity ~ nfeatures + 3 * nlevels: on
+ * 1241 x 376 nfeatures up to ~4070, which covers the monocular initialiser's 2 * nFeatures
+ * extractor of tracker.cpp:84-89) and <= 1024 octree nodes per level. */
 int slamgpu_create(int device, const slamgpu_orb_params* params, int cols, int rows,
                    int max_frames, slamgpu_ctx** out);
 void slamgpu_destroy(slamgpu_ctx* ctx);
