@@ -86,3 +86,33 @@ def test_init_extractor_double_features(oracle, gpu_lib):
         kg, dg = ctx.keypoints(2 * f + side)
         _compare_kps(kg, kr)
         np.testing.assert_array_equal(dg, dr)
+
+
+@pytest.mark.parametrize("cols,rows,nf", [(752, 480, 1200), (640, 480, 1000), (1226, 370, 2000)])
+def test_batch_extract_other_sizes(oracle, gpu_lib, cols, rows, nf):
+    """The batch path's LDS-staged pyramid (pyr_ring_kernel: per-level row segments and slots
+    from the geometry), FAST and octree at the EuRoC / TUM / KITTI-03 image sizes: a 9-frame
+    (18-image) device batch, four images checked against the oracle."""
+    import torch
+    t = oracle.tables(nfeatures=nf, scale_factor=1.2, nlevels=8, ini_th=20, min_th=7)
+    B, pitch = 9, (cols + 63) // 64 * 64
+    ctx = gpu_lib.Context(cols, rows, nf, 1.2, 8, 20, 7, max_frames=B)
+    L = np.zeros((B, rows, pitch), np.uint8)
+    R = np.zeros((B, rows, pitch), np.uint8)
+    for f in range(B):
+        L[f, :, :cols], R[f, :, :cols] = S.stereo_pair(3000 + f, cols, rows)
+    dev = torch.device("cuda", 0)
+    d_l, d_r = torch.from_numpy(L).to(dev), torch.from_numpy(R).to(dev)
+    torch.cuda.synchronize()
+    cam = (0.8 * cols, 0.8 * cols, cols / 2, rows / 2, 0.4 * cols)
+    ctx.frontend_device(d_l, d_r, rows * pitch, pitch, B, cam)
+    ctx.sync()
+    for f, side in ((0, 0), (3, 1), (7, 0), (8, 1)):
+        src = np.ascontiguousarray((L if side == 0 else R)[f, :, :cols])
+        kr, dr, pyr = oracle.extract(t, src, with_pyramid=True)
+        for l in range(1, 8):
+            np.testing.assert_array_equal(ctx.pyramid_level(2 * f + side, l), pyr.level(l),
+                                          err_msg=f"image {2 * f + side} level {l}")
+        kg, dg = ctx.keypoints(2 * f + side)
+        _compare_kps(kg, kr)
+        np.testing.assert_array_equal(dg, dr)
