@@ -808,6 +808,44 @@ __device__ __forceinline__ int wave_incl_scan(int v) {
   return v;
 }
 
+// The same over groups of G lanes (G = 16: a DPP row; 64: the wave); a butterfly level M < 16
+// stays inside a row (lane_partner_u32)
+template <int G>
+__device__ __forceinline__ int group_incl_scan(int v) {
+  static_assert(G == 16 || G == 64, "groups are DPP rows or the wave");
+  if constexpr (G == 64) {
+    return wave_incl_scan(v);
+  } else {
+    v += __builtin_amdgcn_update_dpp(0, v, 0x111, 0xf, 0xf, true);  // row_shr:1
+    v += __builtin_amdgcn_update_dpp(0, v, 0x112, 0xf, 0xf, true);  // row_shr:2
+    v += __builtin_amdgcn_update_dpp(0, v, 0x114, 0xf, 0xf, true);  // row_shr:4
+    v += __builtin_amdgcn_update_dpp(0, v, 0x118, 0xf, 0xf, true);  // row_shr:8
+    return v;
+  }
+}
+template <int G>
+__device__ __forceinline__ uint32_t group_min_key(uint32_t v) {
+#pragma unroll
+  for (int M = G / 2; M >= 1; M >>= 1) v = min(v, lane_partner_u32(v, M));
+  return v;
+}
+template <int G>
+__device__ __forceinline__ uint64_t group_min_key(uint64_t v) {
+#pragma unroll
+  for (int M = G / 2; M >= 1; M >>= 1) {
+    const uint64_t o = (uint64_t)lane_partner_u32((uint32_t)(v >> 32), M) << 32 |
+                       lane_partner_u32((uint32_t)v, M);
+    v = o < v ? o : v;
+  }
+  return v;
+}
+template <int G>
+__device__ __forceinline__ int group_sum(int v) {
+#pragma unroll
+  for (int M = G / 2; M >= 1; M >>= 1) v += (int)lane_partner_u32((uint32_t)v, M);
+  return v;
+}
+
 // The scan's candidate key, ordered as (distance, cell, index): 32 bits -- dist (<= 256) << 23 |
 // cell (< 4096) << 11 | index (< 2048) -- when the frame's keypoint capacity allows, else the 64-bit
 // form the resolution pass reads (dist << 32 | cell << 12 | index).
@@ -828,9 +866,12 @@ __device__ __forceinline__ uint64_t key64(K k) {
     return k;
 }
 
-template <typename K>
+// G lanes per query (the group of `lane`): 64 for the resolution pass's rescans, 16 for
+// search_cand (a window holds a handful of keypoints: four queries per wave keep the lanes busy)
+template <typename K, int G = 64>
 __device__ int scan_query_k(const ScanCtx& c, const Camera& cam, const FrameView& F,
                             const uint32_t* claimed, uint64_t* top, int lane) {
+  const int gl = lane & (G - 1), gb = lane & ~(G - 1);
   const int nMinCellX = max(0, (int)floorf((c.x - cam.min_x - c.r) / cam.cell_w));
   const int nMaxCellX = min(kGridCols - 1, (int)ceilf((c.x - cam.min_x + c.r) / cam.cell_w));
   const int nMinCellY = max(0, (int)floorf((c.y - cam.min_y - c.r) / cam.cell_h));
@@ -849,8 +890,8 @@ __device__ int scan_query_k(const ScanCtx& c, const Camera& cam, const FrameView
     // lanes of empty or absent cells idle. Cells 64 at a time: per-lane keypoint counts, their
     // wave prefix sum, then lane k takes pair k (its cell found by a binary search over the
     // prefix sums). The kept candidates are an order-free minimum, so any order gives the same.
-    for (int cb = 0; cb < total; cb += 64) {
-      const int ci = cb + lane;
+    for (int cb = 0; cb < total; cb += G) {
+      const int ci = cb + gl;
       int cell = 0, q0 = 0, nq = 0;
       if (ci < total) {
         const int ix = nMinCellX + ci / ny, iy = nMinCellY + ci % ny;
@@ -858,21 +899,22 @@ __device__ int scan_query_k(const ScanCtx& c, const Camera& cam, const FrameView
         q0 = F.cell_start[cell];
         nq = F.cell_start[cell + 1] - q0;
       }
-      const int incl = wave_incl_scan(nq);
+      const int incl = group_incl_scan<G>(nq);
       const int excl = incl - nq;
-      const int npairs = __builtin_amdgcn_readlane(incl, 63);
-      // every lane takes part in the shuffles (a shuffle reads 0 from an inactive lane)
-      for (int k0 = 0; k0 < npairs; k0 += 64) {
-        const int k = k0 + lane;
-        int lo = 0;  // the last lane whose exclusive offset is <= k
+      const int npairs = G == 64 ? __builtin_amdgcn_readlane(incl, 63) : __shfl(incl, gb + G - 1, 64);
+      // every lane of the group takes part in the shuffles (a shuffle reads 0 from an inactive
+      // lane); groups run their own trip counts, their shuffles stay inside the group
+      for (int k0 = 0; k0 < npairs; k0 += G) {
+        const int k = k0 + gl;
+        int lo = 0;  // the group's last lane whose exclusive offset is <= k
 #pragma unroll
-        for (int step = 32; step >= 1; step >>= 1) {
+        for (int step = G / 2; step >= 1; step >>= 1) {
           const int cand = lo + step;
-          const int ec = __shfl(excl, cand & 63, 64);
-          if (cand < 64 && ec <= k) lo = cand;
+          const int ec = __shfl(excl, gb + (cand & (G - 1)), 64);
+          if (cand < G && ec <= k) lo = cand;
         }
-        const int p = __shfl(q0, lo, 64) + (k - __shfl(excl, lo, 64));
-        const int pcell = __shfl(cell, lo, 64);
+        const int p = __shfl(q0, gb + lo, 64) + (k - __shfl(excl, gb + lo, 64));
+        const int pcell = __shfl(cell, gb + lo, 64);
         if (k >= npairs) continue;
         const uint4 it = F.cell_items[p];
         const int i = (int)(it.x & 0xffffu), octave = (int)(it.x >> 16);
@@ -911,25 +953,32 @@ __device__ int scan_query_k(const ScanCtx& c, const Camera& cam, const FrameView
   for (int k = 0; k < kTopK; k++) top[k] = kNoKey;
 #pragma unroll
   for (int k = 0; k < kTopK; k++) {
-    const K m = wave_min_key(t[0]);
-    if (m == kNone) break;  // wave-uniform
-    if (t[0] == m) {
-#pragma unroll
-      for (int j = 0; j < kTopK - 1; j++) t[j] = t[j + 1];
-      t[kTopK - 1] = kNone;
+    const K m = G == 64 ? wave_min_key(t[0]) : group_min_key<G>(t[0]);
+    if (G == 64) {
+      if (m == kNone) break;  // wave-uniform
+    } else if (__ballot(m != kNone) == 0) {
+      break;  // no group has a candidate left
     }
-    top[k] = key64<K>(m);
+    if (m != kNone) {
+      if (t[0] == m) {
+#pragma unroll
+        for (int j = 0; j < kTopK - 1; j++) t[j] = t[j + 1];
+        t[kTopK - 1] = kNone;
+      }
+      top[k] = key64<K>(m);
+    }
   }
-  return wave_sum_bfly(cnt);
+  return G == 64 ? wave_sum_bfly(cnt) : group_sum<G>(cnt);
 }
 
 // 32-bit keys whenever the frame's keypoint indices fit 11 bits (kp_cap <= 2048: nfeatures up to
 // ~2000 with the per-level slack), the 64-bit form otherwise.
+template <int G = 64>
 __device__ __forceinline__ int scan_query(const ScanCtx& c, const Camera& cam, const FrameView& F,
                                           const uint32_t* claimed, uint64_t* top, int lane,
                                           int kp_cap) {
-  if (kp_cap <= 2048) return scan_query_k<uint32_t>(c, cam, F, claimed, top, lane);
-  return scan_query_k<uint64_t>(c, cam, F, claimed, top, lane);
+  if (kp_cap <= 2048) return scan_query_k<uint32_t, G>(c, cam, F, claimed, top, lane);
+  return scan_query_k<uint64_t, G>(c, cam, F, claimed, top, lane);
 }
 
 __device__ __forceinline__ int key_idx(uint64_t k) { return (int)(k & 0xfff); }
@@ -995,6 +1044,10 @@ __device__ bool mps_ctx(const MpsQuery& q, int th, const OrbGeom* g, ScanCtx* c)
   return true;
 }
 
+#ifndef SEARCH_LANES
+#define SEARCH_LANES 16
+#endif
+constexpr int kSearchG = SEARCH_LANES;  // lanes per query in search_cand (16 or 64)
 template <typename Q>
 __global__ __launch_bounds__(256) void search_cand_kernel(
     FrameKps cur, const float* __restrict__ u_right, int64_t ur_stride, Camera cam,
@@ -1002,10 +1055,13 @@ __global__ __launch_bounds__(256) void search_cand_kernel(
     int th, GridWorkspace gw, MatchWorkspace mw, MatchIO io) {
   int f, bx;
   xcd_image_block(&f, &bx);  // a frame's work-groups share one XCD's L2 (its grid and keypoints)
-  const int lane = threadIdx.x & 63;
-  const int qi = bx * 4 + wave_id();
-  if (qi >= io.q_count[f]) return;
-  const int q = io.q_start[f] + qi;
+  // kSearchG lanes per query: 64 / kSearchG queries per wave
+  const int lane = threadIdx.x & 63, gl = lane & (kSearchG - 1);
+  const int qi = (bx * 4 + wave_id()) * (64 / kSearchG) + lane / kSearchG;
+  const int qcount = io.q_count[f];
+  if (__builtin_amdgcn_readfirstlane((bx * 4 + wave_id()) * (64 / kSearchG)) >= qcount) return;
+  const bool live = qi < qcount;  // the wave's last groups may have no query
+  const int q = io.q_start[f] + (live ? qi : 0);
   FrameView F;
   F.kps = cur.kps + f * cur.stride;
   F.desc = cur.desc + f * cur.stride * 32;
@@ -1020,22 +1076,21 @@ __global__ __launch_bounds__(256) void search_cand_kernel(
   } else {
     ok = mps_ctx(queries[q], th, g, &c);
   }
-  uint64_t top[kTopK];
-  int n = 0;
-  if (ok) {
-    n = scan_query(c, cam, F, nullptr, top, lane, g->kp_cap);
-  } else {
-#pragma unroll
-    for (int k = 0; k < kTopK; k++) top[k] = kNoKey;
+  ok = ok && live;
+  if (!ok) {  // a window left of the grid: the group scans nothing but takes part in the merge
+    c.x = c.y = -1e30f;
+    c.r = 0.0f;
   }
-  if (lane < kTopK) {
+  uint64_t top[kTopK];
+  const int n = scan_query<kSearchG>(c, cam, F, nullptr, top, lane, g->kp_cap);
+  if (live && gl < kTopK) {
     uint64_t v = top[0];
 #pragma unroll
     for (int k = 1; k < kTopK; k++)
-      if (lane == k) v = top[k];
-    mw.topk[(int64_t)q * kTopK + lane] = v;
+      if (gl == k) v = top[k];
+    mw.topk[(int64_t)q * kTopK + gl] = ok ? v : kNoKey;
   }
-  if (lane == 0) mw.ncand[q] = ok ? n : 0;
+  if (live && gl == 0) mw.ncand[q] = ok ? n : 0;
 }
 
 // Sequential, in-query-order claim resolution: one wave per frame. The kernel is a chain of
@@ -1327,7 +1382,8 @@ void launch_search_frame(const FrameKps& cur, const float* u_right, int64_t ur_s
                          const F2FPose* poses, int n_frames, int max_q, const GridWorkspace& gw,
                          const MatchWorkspace& mw, const MatchIO& io, hipStream_t st) {
   if (max_q > 0)
-    SLAMGPU_LAUNCH("search_cand", st, search_cand_kernel<F2FQuery>, dim3((max_q + 3) / 4, n_frames), dim3(256),
+    SLAMGPU_LAUNCH("search_cand", st, search_cand_kernel<F2FQuery>,
+                   dim3((max_q + 4 * (64 / kSearchG) - 1) / (4 * (64 / kSearchG)), n_frames), dim3(256),
                        0, st, cur, u_right, ur_stride, cam, g.dev, queries, poses, 0, gw, mw, io);
   SLAMGPU_LAUNCH("search_resolve", st, search_resolve_kernel<F2FQuery>, dim3(n_frames), dim3(64), 0, st, cur,
                      u_right, ur_stride, cam, g.dev, queries, poses, 0, 0.0f, gw, mw, io);
@@ -1338,7 +1394,8 @@ void launch_search_mps(const FrameKps& cur, const float* u_right, int64_t ur_str
                        float nnratio, int th, int n_frames, int max_q, const GridWorkspace& gw,
                        const MatchWorkspace& mw, const MatchIO& io, hipStream_t st) {
   if (max_q > 0)
-    SLAMGPU_LAUNCH("search_cand", st, search_cand_kernel<MpsQuery>, dim3((max_q + 3) / 4, n_frames), dim3(256),
+    SLAMGPU_LAUNCH("search_cand", st, search_cand_kernel<MpsQuery>,
+                   dim3((max_q + 4 * (64 / kSearchG) - 1) / (4 * (64 / kSearchG)), n_frames), dim3(256),
                        0, st, cur, u_right, ur_stride, cam, g.dev, queries,
                        (const F2FPose*)nullptr, th, gw, mw, io);
   SLAMGPU_LAUNCH("search_resolve", st, search_resolve_kernel<MpsQuery>, dim3(n_frames), dim3(64), 0, st, cur,
