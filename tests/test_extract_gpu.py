@@ -116,3 +116,33 @@ def test_batch_extract_other_sizes(oracle, gpu_lib, cols, rows, nf):
         kg, dg = ctx.keypoints(2 * f + side)
         _compare_kps(kg, kr)
         np.testing.assert_array_equal(dg, dr)
+
+
+@pytest.mark.parametrize("pitch_pad,params", [(1, (2000, 1.2, 8, 20, 7)),
+                                              (0, (500, 1.5, 4, 30, 10)),
+                                              (0, (1500, 1.3, 6, 12, 5))])
+def test_batch_extract_pitch_and_parameters(oracle, gpu_lib, pitch_pad, params):
+    """Batches off the LDS-staged paths (a caller pitch that is not a multiple of 16: the
+    register-staged pyramid, FAST and window loads) and with other scale factors / level counts
+    (the ring's row segments grow with the scale factor): 9 frames, four images vs the oracle."""
+    import torch
+    nf, sf, nl, ini, mn = params
+    cols, rows, B = S.KITTI_COLS, S.KITTI_ROWS, 9
+    pitch = 1280 + pitch_pad
+    t = oracle.tables(nfeatures=nf, scale_factor=sf, nlevels=nl, ini_th=ini, min_th=mn)
+    ctx = gpu_lib.Context(cols, rows, nf, sf, nl, ini, mn, max_frames=B)
+    L = np.zeros((B, rows, pitch), np.uint8)
+    R = np.zeros((B, rows, pitch), np.uint8)
+    for f in range(B):
+        L[f, :, :cols], R[f, :, :cols] = S.stereo_pair(4000 + f)
+    dev = torch.device("cuda", 0)
+    d_l, d_r = torch.from_numpy(L).to(dev), torch.from_numpy(R).to(dev)
+    torch.cuda.synchronize()
+    ctx.frontend_device(d_l, d_r, rows * pitch, pitch, B, S.KITTI_CAM)
+    ctx.sync()
+    for f, side in ((0, 0), (2, 1), (6, 0), (8, 1)):
+        src = np.ascontiguousarray((L if side == 0 else R)[f, :, :cols])
+        kr, dr = oracle.extract(t, src)[:2]
+        kg, dg = ctx.keypoints(2 * f + side)
+        _compare_kps(kg, kr)
+        np.testing.assert_array_equal(dg, dr)
