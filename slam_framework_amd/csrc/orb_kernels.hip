@@ -2776,7 +2776,7 @@ void launch_extract(const ImageBatch& b, const OrbGeomDev& gd, int n_images, hip
   // batches: the LDS-staged strips (16-byte buffer-to-LDS loads need 16-byte aligned rows)
   static const int ring_mode = [] {
     const char* e = std::getenv("SLAMGPU_PYR_RING");
-    return e ? std::atoi(e) : 0xfe;
+    return e ? std::atoi(e) : 0x7ffffffe;  // every level >= 1
   }();
   // SLAMGPU_PYR_RING: bit l selects the LDS-staged kernel for level l (A/B)
   const bool ring_ok = glds && g.pyr_ring_slots > 0 && g.pyr_ring_slots <= 8;
