@@ -120,7 +120,8 @@ def test_batch_extract_other_sizes(oracle, gpu_lib, cols, rows, nf):
 
 @pytest.mark.parametrize("pitch_pad,params", [(1, (2000, 1.2, 8, 20, 7)),
                                               (0, (500, 1.5, 4, 30, 10)),
-                                              (0, (1500, 1.3, 6, 12, 5))])
+                                              (0, (1500, 1.3, 6, 12, 5)),
+                                              (0, (2000, 1.2, 10, 20, 7))])
 def test_batch_extract_pitch_and_parameters(oracle, gpu_lib, pitch_pad, params):
     """Batches off the LDS-staged paths (a caller pitch that is not a multiple of 16: the
     register-staged pyramid, FAST and window loads) and with other scale factors / level counts
