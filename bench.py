@@ -191,6 +191,11 @@ def main():
                     help="skip the ComputeBoW / SearchByBoW measurement")
     ap.add_argument("--no-latency", action="store_true",
                     help="skip the single-frame drop-in latency and the PCIe-inclusive rate")
+    ap.add_argument("--dist-backend", choices=("nccl", "gloo"),
+                    default=os.environ.get("SLAMGPU_BENCH_BACKEND", "nccl"),
+                    help="process-group backend for N > 1: nccl (RCCL, one GPU per rank; the "
+                         "driver's runs) or gloo (the gather staged through host memory; ranks "
+                         "may share a GPU -- exercises the N-rank path on a one-GPU box)")
     args = ap.parse_args()
 
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
@@ -203,13 +208,19 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         sys.exit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}")
+    gloo = world > 1 and args.dist_backend == "gloo"
+    if gloo:  # ranks share the visible GPUs round-robin (torch.cuda.device_count() makes no HIP call)
+        local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     # One explicit stream for torch ops and library launches alike: a null stream handle would
     # put the library's kernels on the context's own (non-blocking) stream, unordered with torch.
     torch.cuda.set_stream(torch.cuda.Stream(device=dev))
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if gloo:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=dev)
         world = dist.get_world_size()
         # the CPU baseline and the optimizer / BoW legs are N=1 measurements
         args.no_cpu_baseline = args.no_optimizer = args.no_bow = args.no_latency = True
@@ -229,7 +240,7 @@ def main():
     # runs the pack + gather path at world 1 too, as a local copy)
     gather = world > 1 or os.environ.get("SLAMGPU_BENCH_GATHER") == "1"
     job = ShardedFrontend(Ls, Rs, cam, B, dev, streams=args.streams, inflight=args.inflight,
-                          rank=rank, world=world, gather=gather)
+                          rank=rank, world=world, gather=gather, host_gather=gloo)
     NS, Bs, INF = job.NS, job.Bs, job.INF
     host_l, host_r, poses = job.host_l, job.host_r, job.poses
     ctxs, parts = job.contexts, job.parts
@@ -403,8 +414,10 @@ def main():
                        "nfeatures": 2000,
                        "nlevels": 8, "scale_factor": 1.2, "fast_th": [20, 7],
                        "parallelism": f"frame-sharded x{world}" + (
-                           ", contiguous shards + 1 halo frame, RCCL gather to rank 0"
-                           if world > 1 else "")},
+                           ", contiguous shards + 1 halo frame, " + (
+                               "gloo gather through host memory to rank 0" if gloo else
+                               "RCCL gather to rank 0") if world > 1 else ""),
+                       "dist_backend": (args.dist_backend if world > 1 else None)},
             "gather": gather_info,
             "roofline": roofline,
             "path_roofline": path_roof,

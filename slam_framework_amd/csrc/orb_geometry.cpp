@@ -237,6 +237,38 @@ int compute_geometry(const OrbParams& p, int cols, int rows, OrbGeom* g,
       sum += g->gauss[i];
     }
     if (sum > 257) return -6;
+    // the MFMA band is signed int8
+    for (int i = 0; i < 7; i++)
+      if (g->gauss[i] > 127) return -6;
+  }
+  for (int lane = 0; lane < 64; lane++) {  // orient_desc's per-lane constants (orb_geometry.h)
+    const int n = lane & 15, gq = lane >> 4;
+    for (int tj = 0; tj < 3; tj++)
+      for (int w = 0; w < 4; w++) {
+        uint32_t v = 0;
+        for (int bb = 0; bb < 4; bb++) {
+          const int t = 16 * gq + 4 * w + bb - 16 * tj - n;
+          if (t >= 0 && t <= 6) v |= (uint32_t)g->gauss[t] << (8 * bb);
+        }
+        g->od_band[tj][lane][w] = v;
+      }
+    const int ick = lane & 3;
+    for (int q = 0; q < 2; q++) {
+      const int r = 16 * q + (lane >> 2), vv = r - 15;
+      const int hd = r < 31 ? g->umax[vv < 0 ? -vv : vv] : -1;
+      for (int jj = 0; jj < 2; jj++) {
+        uint32_t wt = 0, one = 0;
+        for (int bb = 0; bb < 4; bb++) {
+          const int u = 8 * ick + 4 * jj + bb - 15;
+          if (u >= -hd && u <= hd) {
+            wt |= (uint32_t)(u + 20) << (8 * bb);
+            one |= 1u << (8 * bb);
+          }
+        }
+        g->od_ic[lane][2 * q + jj] = wt;
+        g->od_ic[lane][4 + 2 * q + jj] = one;
+      }
+    }
   }
   // strict 8-neighbour NMS keeps at most one pixel per 2x2 block of the detect area
   g->cell_cap = ((max_wcell + 1) / 2) * ((max_hcell + 1) / 2);

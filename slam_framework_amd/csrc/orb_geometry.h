@@ -108,6 +108,13 @@ struct OrbGeom {
   int pyr_ring_slots;  // pyr_ring_kernel: 1 KiB LDS slots per wave (max over levels; 0: unusable)
   int pyr_band_lds;  // bytes of one of its two LDS row buffers (the largest band level)
   int16_t pyr_band[kPyrMaxBands][kMaxLevels][2];
+  // orient_desc per-lane constants (host-built from gauss / umax, read once per wave):
+  // od_band[tj][lane]: the v_mfma_i32_16x16x64_i8 B operand of tile column tj -- byte b of lane
+  // (n = lane & 15, g = lane >> 4) is gauss[16 g + b - 16 tj - n] inside the 7 taps, else 0;
+  // od_ic[lane]: the IC_Angle circle weights of the lane's two patch slots, {wt[0][0..1],
+  // wt[1][0..1], one[0][0..1], one[1][0..1]} (see orient_desc_kernel)
+  uint32_t od_band[3][64][4];
+  uint32_t od_ic[64][8];
 };
 
 // Resize tables (HResizeLinear / VResizeLinear coefficients, 11-bit fixed point).

@@ -12,6 +12,7 @@
 #include <stdint.h>
 
 #include <type_traits>
+#include <utility>
 #include <cstdlib>
 
 #include "device_math.h"
@@ -2317,6 +2318,16 @@ __global__ __launch_bounds__(kOctLvlThreads) void octree_lvl_kernel(
 }
 
 // ---------------------------------------------------------------------------------------
+// compile-time loops (lane selects and writelane lanes as immediates)
+template <class F, int... J>
+__device__ __forceinline__ void static_for_impl(F&& f, std::integer_sequence<int, J...>) {
+  (f(std::integral_constant<int, J>{}), ...);
+}
+template <int N, class F>
+__device__ __forceinline__ void static_for(F&& f) {
+  static_for_impl(f, std::make_integer_sequence<int, N>{});
+}
+
 constexpr int kKpPerWave = 8;
 constexpr int kOdSmallMaxImages = 16;  // launches up to this many images: 4 keypoints per wave
 typedef float f32x2 __attribute__((ext_vector_type(2)));
@@ -2352,32 +2363,48 @@ __device__ __forceinline__ int reduce_scatter16(int (&v)[16], int lane) {
 // computeOrbDescriptor (:49-88) on the level blurred by cv::GaussianBlur(7x7, sigma 2) (:1029-1030),
 // with the blur folded in: no blurred pyramid is written or read back. The blur is separable
 // with exact integer sums: a pixel is round(sum_i k_i R_i / 2^16), R_i = the row
-// sums sum_j k_j I(y+i-3, x+j-3) <= 255 * 257 (u16). Per keypoint a wave forms the row sums of
-// the 43 x 37 window the samples' columns need (rows y-21..y+21, columns x-18..x+18: 430 lane
-// tasks of 4 columns, one dwordx4 load of the raw row + 2 v_dot4_u32_u8 per column, stored
-// TRANSPOSED as u16 in LDS), then each of the 512 samples takes its 7 vertical row sums as 4
-// dwords of its column (v_alignbit for an odd start) and 4 v_dot2_u32_u16, and rounds with the
-// column's rule (half to even inside the SSE span x < W - W%4, half up in the scalar tail).
-// Border keypoints (the window leaves the image: reflect-101 columns) load bytes one by one.
-// LDS: one 40 x 44 u16 window per wave.
-// Variants measured and rejected in round 3 (dword row pairs, the horizontal pass on MFMA i8, a
-// shifted copy of the table) are in git history before round 4 and in DESIGN.md section 9.
-// u16 per transposed column (even, see the sample reads). 50 rather than the 43 + 1 the window
-// needs: a row-sum store instruction writes rows r .. r + 6 of the 10 column quads, and a
-// column-quad stride of 2 * 50 = 100 dwords (4 mod 32 banks) leaves only quads 8 and 9 sharing
-// banks with 0 and 1 (2-way), where 44 (24 mod 32) put three quads on one bank: LDS conflict
-// cycles per launch 2.64e8 -> 2.04e8 (profiles/r5zc_pmc_rt_rows.txt)
-constexpr int kRtCols = 40, kRtRows = 50;
-constexpr int kRtN = kRtCols * kRtRows;
+// sums sum_j k_j I(y+i-3, x+j-3) <= 255 * 257 (u16).
+// Per keypoint the row sums of its window (rows y-21..y+21, the columns the rotated samples can
+// reach) come from the matrix cores: a banded int8 GEMM per 16 x 16 tile of the window
+// (v_mfma_i32_16x16x32_i8: A = the window's bytes - 128 as int8, B = the 7 taps, accumulator
+// initialised to 128 * 257, so the i32 result IS the u16 row sum), 3 x 3 tiles per keypoint. The
+// A rows are mapped so that a lane's 12 accumulator elements are 12 consecutive window rows of one
+// column; it pairs them as dwords W[e] = R[e] | R[e + 1] << 16 (the overlapping-pair table, one
+// v_perm each, the row after its last from the next lane group by ds_bpermute) and stores them with
+// three ds_write_b128. A sample's 7 vertical taps are then the dwords e, e+2, e+4, e+6 of its
+// column: two ds_read2_b32 and four v_dot2_u32_u16, no realignment. It rounds with the column's
+// rule (half to even inside the SSE span x < W - W%4, half up in the scalar tail).
+// Border keypoints (the window leaves the image: reflect-101 rows and columns) gather the A bytes
+// one by one; the GEMM and the table are the same.
+// Round 3-5 variants (VALU row sums stored as transposed u16 with a v_alignbit per tap pair, an
+// MFMA row-sum variant without the pair table or the pipelined loads, dword row pairs, a shifted
+// copy of the table) are in git history and DESIGN.md sections 9-11.
+// The pair table per wave: kWCols columns (window column c = image column x - 18 - s + c, s the
+// window origin's misalignment) x kWs dwords (rows 0..43; 44 = 12 mod 32 banks, so the eight
+// lanes of a ds_write_b128 group write 32 distinct banks).
+constexpr int kWCols = 40, kWs = 44;
+constexpr int kWN = kWCols * kWs;
+// The window staging area per wave: 48 rows x 64 bytes from the dword-aligned origin, filled by
+// buffer-to-LDS loads in row order (four lanes per row: each load instruction's quarter-waves
+// fetch four rows as whole lines) and read back in the MFMA's A layout (16 rows per quarter-wave,
+// which as direct loads made every quarter-wave touch 16 lines). Within a row the four 16-byte
+// chunks sit in the order chunk ^ swz(row), a table found by search that makes the A reads
+// (ds_read_b128, 16-lane groups) bank-conflict free for the three tile rows.
+constexpr int kWinRows = 48, kWinBytes = kWinRows * 64;
+__device__ __forceinline__ int win_swz(int r) {
+  const uint32_t t = r < 16 ? 0x330dbacdu : r < 32 ? 0x3a652155u : 0x159bb6u;
+  return (int)((t >> (2 * (r & 15))) & 3u);
+}
 
 // KPW (<= kKpPerWave) keypoints per wave: 8 for batches, 4 for small launches (more waves in
 // flight for the single-frame call)
 template <int KPW>
-__global__ __launch_bounds__(256) void orient_desc_kernel(
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void orient_desc_kernel(
     ImageBatch b, const OrbGeom* __restrict__ g, const uint32_t* __restrict__ oct_keys,
     const int* __restrict__ oct_count, KeyPoint* __restrict__ kps, uint8_t* __restrict__ desc,
     int* __restrict__ nkps) {
-  __shared__ __attribute__((aligned(16))) uint16_t s_rt[4][1][kRtN];
+  __shared__ __attribute__((aligned(16))) uint32_t s_w[4][kWN + 4];  // + a 16-byte front pad
+  __shared__ __attribute__((aligned(16))) uint8_t s_win[4][kWinBytes];
   int img, bx;
   xcd_image_block(&img, &bx);
   const int lane = threadIdx.x & 63, wid = wave_id();
@@ -2401,21 +2428,20 @@ __global__ __launch_bounds__(256) void orient_desc_kernel(
     my_level = l;
     my_key = (int)oct_keys[(int64_t)img * g->out_per_image + g->lv[l].out_base + t];
   }
-  const int hr = lane >> 1, hh = lane & 1, hv = hr - 15;
-  const int hd = hr < 31 ? g->umax[hv < 0 ? -hv : hv] : -1;
-  uint32_t wt[4], one[4];
-#pragma unroll
-  for (int k = 0; k < 4; k++) {
-    wt[k] = 0;
-    one[k] = 0;
-#pragma unroll
-    for (int bb = 0; bb < 4; bb++) {
-      const int u = 16 * hh + 4 * k + bb - 15;
-      if (u >= -hd && u <= hd) {
-        wt[k] |= (uint32_t)(u + 20) << (8 * bb);
-        one[k] |= 1u << (8 * bb);
-      }
-    }
+  // IC_Angle lane roles: two slots of 16 patch rows, four lanes per row. Lane (row r, k) loads 12
+  // bytes at 8 k from the row's dword-aligned start (x - 15) & ~3 -- one 16-row x 36-byte block
+  // per load instruction, so the patch's rows are fetched as whole lines (a 2-lanes-per-row map
+  // with 5 dword loads touched every row 5 times: the texture data path, not the VALU, bound the
+  // kernel) -- and realigns them into its two patch dwords 2 k, 2 k + 1 (columns 8 k .. 8 k + 7 of
+  // x - 15 .. x + 15) with v_alignbyte; wt / one: the circle's u + 20 weights and 0/1 masks.
+  const int ick = lane & 3;
+  const int icv[2] = {(lane >> 2) - 15, (lane >> 2) + 1};
+  uint32_t wt[2][2], one[2][2];
+  {
+    const uint4* t = reinterpret_cast<const uint4*>(g->od_ic[lane]);
+    const uint4 w = t[0], o = t[1];
+    wt[0][0] = w.x; wt[0][1] = w.y; wt[1][0] = w.z; wt[1][1] = w.w;
+    one[0][0] = o.x; one[0][1] = o.y; one[1][0] = o.z; one[1][1] = o.w;
   }
   uint32_t kkey[kKpPerWave];
   int klev[kKpPerWave];
@@ -2428,16 +2454,15 @@ __global__ __launch_bounds__(256) void orient_desc_kernel(
   const int in_pitch = __builtin_amdgcn_readfirstlane(b.in_pitch);
   // Phases 1-2: the IC_Angle patches (raw level, registers), kPh12Split keypoints at a time,
   // then their moments (lane 8j ends up with keypoint j's)
+  typedef unsigned int u32x3 __attribute__((ext_vector_type(3)));
   constexpr int kPh12Split = 4;
   int mv[16];
 #pragma unroll
   for (int j0 = 0; j0 < kKpPerWave; j0 += kPh12Split) {
-    uint32_t raw[kPh12Split][5];
+    u32x3 raw[kPh12Split][2];
 #pragma unroll
     for (int jj = 0; jj < kPh12Split; jj++) {
       const int j = j0 + jj;
-#pragma unroll
-      for (int k = 0; k < 5; k++) raw[jj][k] = 0;
       const int level = klev[j];
       const int x = key_x(kkey[j]) + kMinBorder, y = key_y(kkey[j]) + kMinBorder;
       const LevelGeom& L = g->lv[level];
@@ -2445,18 +2470,26 @@ __global__ __launch_bounds__(256) void orient_desc_kernel(
       const uint8_t* im = level == 0 ? batch_image(b, img)
                                      : b.pyr + (int64_t)img * g->pyr_bytes + L.offset;
       const uint8_t* rbase = im + (int64_t)(y - 15) * pitch + ((x - 15) & ~3);
-      const uint32_t loff = __umul24(hr, pitch) + 16 * hh;
-      const uint8_t* rp = rbase + loff;
-      if (hr < 31) {
-        if ((((uintptr_t)im | (uintptr_t)pitch) & 3) == 0) {
-          // buffer loads off the patch's (wave-uniform) base: no 64-bit address per lane
-          const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-              (void*)uniform_ptr(rbase), 0, 31 * pitch + 32, 0x00020000);
+      if ((((uintptr_t)im | (uintptr_t)pitch) & 3) == 0) {
+        // buffer loads off the patch's (wave-uniform) base: no 64-bit address per lane; row 31
+        // (the second slot's last four lanes) lies past the 31-row range and reads zeros
+        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+            (void*)uniform_ptr(rbase), 0, 30 * pitch + 36, 0x00020000);
 #pragma unroll
-          for (int k = 0; k < 5; k++) raw[jj][k] = __builtin_amdgcn_raw_buffer_load_b32(rs, loff + 4 * k, 0, 0);
-        } else {
+        for (int q = 0; q < 2; q++)
+          raw[jj][q] = __builtin_amdgcn_raw_buffer_load_b96(
+              rs, __umul24((uint32_t)(16 * q + (lane >> 2)), (uint32_t)pitch) + 8u * ick, 0, 0);
+      } else {
 #pragma unroll
-          for (int k = 0; k < 20; k++) raw[jj][k >> 2] |= (uint32_t)rp[k] << (8 * (k & 3));
+        for (int q = 0; q < 2; q++) {
+          const int r = 16 * q + (lane >> 2);
+          uint32_t w3[3] = {0, 0, 0};
+          if (r < 31) {
+            const uint8_t* rp = rbase + (int64_t)r * pitch + 8 * ick;
+#pragma unroll
+            for (int k = 0; k < 12; k++) w3[k >> 2] |= (uint32_t)rp[k] << (8 * (k & 3));
+          }
+          raw[jj][q] = (u32x3){w3[0], w3[1], w3[2]};
         }
       }
     }
@@ -2464,15 +2497,18 @@ __global__ __launch_bounds__(256) void orient_desc_kernel(
     for (int jj = 0; jj < kPh12Split; jj++) {
       const int j = j0 + jj;
       const int a = (key_x(kkey[j]) + kMinBorder - 15) & 3;
-      uint32_t s = 0, t = 0;
+      int m10 = 0, m01 = 0;
 #pragma unroll
-      for (int k = 0; k < 4; k++) {
-        const uint32_t e = __builtin_amdgcn_alignbyte(raw[jj][k + 1], raw[jj][k], a);
-        s = __builtin_amdgcn_udot4(e, one[k], s, false);
-        t = __builtin_amdgcn_udot4(e, wt[k], t, false);
+      for (int q = 0; q < 2; q++) {
+        const uint32_t e0 = __builtin_amdgcn_alignbyte(raw[jj][q].y, raw[jj][q].x, a);
+        const uint32_t e1 = __builtin_amdgcn_alignbyte(raw[jj][q].z, raw[jj][q].y, a);
+        const uint32_t s = __builtin_amdgcn_udot4(e1, one[q][1], __builtin_amdgcn_udot4(e0, one[q][0], 0u, false), false);
+        const uint32_t t = __builtin_amdgcn_udot4(e1, wt[q][1], __builtin_amdgcn_udot4(e0, wt[q][0], 0u, false), false);
+        m10 += (int)t - 20 * (int)s;
+        m01 += icv[q] * (int)s;
       }
-      mv[2 * j] = (int)t - 20 * (int)s;
-      mv[2 * j + 1] = hv * (int)s;
+      mv[2 * j] = m10;
+      mv[2 * j + 1] = m01;
     }
     if (kPh12Split < kKpPerWave) __asm__ volatile("" ::: "memory");
   }
@@ -2482,216 +2518,341 @@ __global__ __launch_bounds__(256) void orient_desc_kernel(
   const float factorPI = (float)(3.14159265358979323846 / 180.0);
   float sa, ca;
   glibc_sincosf(angle * factorPI, &sa, &ca);
-  // Phase 3: per 4 keypoints, the row-summed windows (LDS) then the 512 blurred samples each
+  // Phase 3: per keypoint, the pair table (LDS) then the 512 blurred samples
   // the lane's 4 tests (8 points) as int8 (x0, y0, x1, y1) words: 4 VGPRs instead of 32
-  uint32_t pat[4];
+  // as float pairs (x, y): 16 VGPRs; the packed products broadcast x or y by op_sel
+  f32x2 pf[8];
 #pragma unroll
-  for (int r = 0; r < 4; r++)
-    pat[r] = reinterpret_cast<const uint32_t*>(c_pattern)[r * 64 + lane];
+  for (int r = 0; r < 4; r++) {
+    const uint32_t pw = reinterpret_cast<const uint32_t*>(c_pattern)[r * 64 + lane];
+#pragma unroll
+    for (int e = 0; e < 2; e++)
+      pf[2 * r + e] = (f32x2){(float)(int)(int8_t)(pw >> (16 * e)),
+                              (float)(int)(int8_t)(pw >> (16 * e + 8))};
+  }
   const uint32_t q0 = g->gauss[0], q1 = g->gauss[1], q2 = g->gauss[2], q3 = g->gauss[3];
-  const uint32_t KA = q0 | q1 << 8 | q2 << 16 | q3 << 24, KB = q2 | q1 << 8 | q0 << 16;
   const uint32_t K01 = q0 | q1 << 16, K23 = q2 | q3 << 16, K21 = q2 | q1 << 16, K0 = q0;
-  // the horizontal taps of the four columns of a row task straight from the three dwords
-  // u0..u2 holding bytes x-3 .. x+8 (no per-column realignment): column jx weights byte jx+m by
-  // k_m (k symmetric: k4 = k2, k5 = k1, k6 = k0)
-  const uint32_t C1a = q0 << 8 | q1 << 16 | q2 << 24, C1b = q3 | q2 << 8 | q1 << 16 | q0 << 24;
-  const uint32_t C2a = q0 << 16 | q1 << 24, C2b = q2 | q3 << 8 | q2 << 16 | q1 << 24, C2c = q0;
-  const uint32_t C3a = q0 << 24, C3b = q1 | q2 << 8 | q3 << 16 | q2 << 24, C3c = q1 | q0 << 8;
   // magic + 18: a rounded sample coordinate comes out as its window index (round(x) + 18; 18 is
   // even, so round-half-even is unchanged)
   const f32x2 magic = {12582930.0f, 12582930.0f};
   uint32_t dlo = 0, dhi = 0;
-  // Row-sum tasks: t = lane + 64 i -> window row r = t / 10, column quad gq = t % 10; a task's
-  // raw bytes sit at r * pitch + 4 gq past the keypoint's window origin (a lane constant times
-  // the level pitch: one v_mad_u32_u24, the origin a scalar base). (Consecutive lanes on
-  // consecutive rows of one column quad would store conflict-free, but each wave load then
-  // touches ~43 rows instead of ~7: orient_desc 1.03 -> 1.50 ms, round 4.)
-  constexpr int kTaskRows = 1;              // window rows per lane task
-  constexpr int kTasks = 43 * 10;
-  constexpr int kRounds = (kTasks + 63) / 64;
-  int trow[kRounds], tcol[kRounds];  // trow < 0: no task (last round's padding)
+  // MFMA lane roles (v_mfma_i32_16x16x64_i8): lane l holds row / column l & 15 of A / B and 16
+  // bytes of K (lane group g = l >> 4), C[4 g + i][l & 15] in element i (tools/mfma_i8_probe.hip
+  // checks the 16x16x32 form's map; only "A and B bytes b of lane group g share one K index" is
+  // relied on here, and the parity tests pin it). A lane's 16 K bytes are window bytes 16 g ..
+  // 16 g + 15 of its row (from the dword-aligned origin xa = (x - 21) & ~3): one 16-byte load, the
+  // row's four lanes one 64-byte block. Output column 16 tj + n is the row sum of bytes
+  // 16 tj + n .. + 6, so B is the band shifted by 16 tj: one operand per tile column.
+  typedef int v4i __attribute__((ext_vector_type(4)));
+  const int mf_n = lane & 15, mf_g = lane >> 4;
+  v4i bm[3];
 #pragma unroll
-  for (int i = 0; i < kRounds; i++) {
-    const int t = lane + 64 * i;
-    trow[i] = t < kTasks ? t / 10 : -1;
-    tcol[i] = 4 * (t % 10);
+  for (int tj = 0; tj < 3; tj++) {
+    const uint4 t = reinterpret_cast<const uint4*>(g->od_band[tj])[lane];
+    bm[tj] = (v4i){(int)t.x, (int)t.y, (int)t.z, (int)t.w};
   }
-  // Per keypoint: its row-summed window into LDS, then its 256 tests from LDS. The window's raw
-  // rows (one 16-byte load per lane task, 7 tasks per lane) of keypoint j + 1 are in flight
-  // while keypoint j's tests run. LDS hand-offs are within the wave (LDS executes
-  // a wave's instructions in order): only compiler ordering is needed between the passes.
+  // A rows: tile row ti's row m is window row 12 (m >> 2) + 4 ti + (m & 3), so lane (n, g) ends up
+  // with window rows 12 g .. 12 g + 11 of column n. Rows past 42 repeat row 42 (they only feed the
+  // table's zero-weight pad): the loads stay inside the window's 43 rows.
+  uint32_t arow[3];
+#pragma unroll
+  for (int ti = 0; ti < 3; ti++)
+    arow[ti] = (uint32_t)min(12 * (mf_n >> 2) + 4 * ti + (mf_n & 3), 42);
   struct RsGeo {
-    const uint8_t* im;
-    const uint8_t* org;  // window origin (kx - 21 rounded down to a dword, ky - 21), fast path
-    int pitch, w, h, kx, ky;
-    bool fastp;          // the whole window is inside the level: dword loads, no reflection
+    const uint8_t* org;  // window origin (xa, y - 21)
+    int pitch, w, h, kx, ky, level;
+    bool fastp;          // the whole window is inside the level: buffer loads, no reflection
   };
+  // every keypoint's window geometry computed once, lane j for keypoint j (vector loads of its
+  // level's geometry), then read back per keypoint by five v_readlane: the per-keypoint scalar
+  // chain (level table loads, 64-bit pointer arithmetic, the window tests) was ~60 SALU
+  // instructions per keypoint on the wave's issue stream
+  uint32_t gv_org_lo, gv_org_hi, gv_pitch, gv_wh, gv_k;
+  {
+    const LevelGeom& L = g->lv[my_level];
+    const int kx = key_x((uint32_t)my_key) + kMinBorder, ky = key_y((uint32_t)my_key) + kMinBorder;
+    const int w = L.w, h = L.h;
+    const int pitch = my_level == 0 ? in_pitch : L.pitch;
+    const uint8_t* im = my_level == 0 ? batch_image(b, img)
+                                      : b.pyr + (int64_t)img * g->pyr_bytes + L.offset;
+    const bool fastp = kx >= 21 && kx <= w - 31 && ky >= 21 && ky + 21 < h &&
+                       ((((uintptr_t)im | (uintptr_t)pitch) & 3) == 0);
+    const uintptr_t org = (uintptr_t)(im + (int64_t)(ky - 21) * pitch + ((kx - 21) & ~3));
+    gv_org_lo = (uint32_t)org;
+    gv_org_hi = (uint32_t)(org >> 32);
+    gv_pitch = (uint32_t)pitch;
+    gv_wh = (uint32_t)w | (uint32_t)h << 16;
+    gv_k = (uint32_t)kx | (uint32_t)ky << 12 | (uint32_t)my_level << 24 | (fastp ? 1u << 31 : 0u);
+  }
   auto rs_geo = [&](int j) {
     RsGeo G;
     const int jj = min(j, nk - 1);
-    const int level = __builtin_amdgcn_readlane(my_level, jj);
-    const uint32_t key = (uint32_t)__builtin_amdgcn_readlane(my_key, jj);
-    const LevelGeom& L = g->lv[level];
-    G.kx = key_x(key) + kMinBorder;
-    G.ky = key_y(key) + kMinBorder;
-    G.w = L.w;
-    G.h = L.h;
-    G.pitch = level == 0 ? in_pitch : L.pitch;
-    G.im = level == 0 ? batch_image(b, img) : b.pyr + (int64_t)img * g->pyr_bytes + L.offset;
-    G.fastp = G.kx >= 21 && G.kx <= G.w - 31 && G.ky >= 21 && G.ky + 21 < G.h &&
-              ((((uintptr_t)G.im | (uintptr_t)G.pitch) & 3) == 0);
-    G.org = G.im + (int64_t)(G.ky - 21) * G.pitch + ((G.kx - 21) & ~3);
+    const uintptr_t org = (uintptr_t)(uint32_t)__builtin_amdgcn_readlane(gv_org_lo, jj) |
+                          (uintptr_t)(uint32_t)__builtin_amdgcn_readlane(gv_org_hi, jj) << 32;
+    G.org = reinterpret_cast<const uint8_t*>(org);
+    G.pitch = __builtin_amdgcn_readlane(gv_pitch, jj);
+    const uint32_t wh = (uint32_t)__builtin_amdgcn_readlane(gv_wh, jj);
+    const uint32_t k = (uint32_t)__builtin_amdgcn_readlane(gv_k, jj);
+    G.w = (int)(wh & 0xffffu);
+    G.h = (int)(wh >> 16);
+    G.kx = (int)(k & 0xfffu);
+    G.ky = (int)((k >> 12) & 0xfffu);
+    G.level = (int)((k >> 24) & 0xfu);
+    G.fastp = (k >> 31) != 0;
     return G;
   };
-  // the window rows by buffer loads off the window origin (wave-uniform): a 32-bit lane offset
-  // per row task, no 64-bit address arithmetic
-  auto rs_load = [&](const RsGeo& G, uint4 (&q)[kRounds * kTaskRows]) {
-    if (!G.fastp) return;
-    typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-        (void*)uniform_ptr(G.org), 0, 43 * G.pitch, 0x00020000);
+  // The window of a keypoint into the wave's staging area: slot 64 i + lane (16 bytes) holds row
+  // 16 i + (lane >> 2) (rows past 42 repeat row 42), chunk (lane & 3) ^ swz(row). Fast path: three
+  // buffer-to-LDS loads off the (wave-uniform) window origin, bounded by the window's 43 rows
+  // (pitch >= 64: every load is inside them; bytes past x + 24 only feed output columns past the
+  // table's 40). Border windows (reflect-101 rows and columns) gather bytes into the same slots.
+  uint8_t* win = &s_win[wid][0];
+  uint32_t dma_row[3], dma_off[3], a_lds[3];
 #pragma unroll
-    for (int i = 0; i < kRounds; i++) {
-      if (trow[i] >= 0) {
+  for (int i = 0; i < 3; i++) {
+    const int r = 16 * i + (lane >> 2);
+    dma_row[i] = (uint32_t)min(r, 42);
+    dma_off[i] = 16u * (uint32_t)((lane & 3) ^ win_swz(r));
+    // the A read of tile row i: row arow[i], chunk g
+    a_lds[i] = 16u * (4u * arow[i] + (uint32_t)(mf_g ^ win_swz((int)arow[i])));
+  }
+  typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+  auto win_fill = [&](const RsGeo& G) {
+    if (G.fastp) {
+      const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+          (void*)uniform_ptr(G.org), 0, 43 * G.pitch, 0x00020000);
 #pragma unroll
-        for (int h = 0; h < kTaskRows; h++) {
-          // row 43 (the pad of the last pair, weight 0 in every tap) re-reads row 42: the
-          // window's rows stay inside the level
-          const uint32_t row = (uint32_t)min(trow[i] + h, 42);
-          const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(
-              rs, __umul24(row, (uint32_t)G.pitch) + (uint32_t)tcol[i], 0, 0);
-          q[kTaskRows * i + h] = make_uint4(v.x, v.y, v.z, v.w);
+      for (int i = 0; i < 3; i++)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(
+            rs, (__attribute__((address_space(3))) void*)(win + 1024 * i), 16,
+            __umul24(dma_row[i], (uint32_t)G.pitch) + dma_off[i], 0, 0, 0);
+    } else {
+      // a dword whose 4 columns are inside the level is one aligned load; only the dwords that
+      // straddle or leave an edge gather bytes (divergent, few lanes)
+      const int xa = (G.kx - 21) & ~3;
+      const uint8_t* im = G.level == 0 ? batch_image(b, img)
+                                       : b.pyr + (int64_t)img * g->pyr_bytes + g->lv[G.level].offset;
+      const bool al = (((uintptr_t)im | (uintptr_t)G.pitch) & 3) == 0;
+#pragma unroll
+      for (int i = 0; i < 3; i++) {
+        const uint8_t* row =
+            im + (int64_t)reflect101(G.ky - 21 + (int)dma_row[i], G.h) * G.pitch;
+        uint32_t wv[4];
+#pragma unroll
+        for (int d = 0; d < 4; d++) {
+          const int c = xa + (int)dma_off[i] + 4 * d;
+          if (al && c >= 0 && c + 3 < G.w) {
+            wv[d] = *reinterpret_cast<const uint32_t*>(row + c);
+          } else {
+            uint32_t v = 0;
+#pragma unroll
+            for (int k = 0; k < 4; k++) v |= (uint32_t)row[reflect101(c + k, G.w)] << (8 * k);
+            wv[d] = v;
+          }
         }
+        reinterpret_cast<uint4*>(win + 1024 * i)[lane] = make_uint4(wv[0], wv[1], wv[2], wv[3]);
       }
     }
   };
-  uint16_t* rtw = &s_rt[wid][0][0];
-  RsGeo gn = rs_geo(0);
-  uint4 qn[kRounds * kTaskRows];
-  rs_load(gn, qn);
-#pragma unroll
-  for (int j = 0; j < KPW; j++) {
-    const RsGeo G = gn;
+  typedef __attribute__((address_space(3))) const uint32_t lds_u32;
+  uint32_t* tw = &s_w[wid][4];
+  // the lane's first table dword of tile column 0: column n, row 12 g
+  uint32_t* tw_lane = tw + mf_n * kWs + 12 * mf_g;
+  // Software pipeline over the wave's keypoints: iteration j issues keypoint j's MFMAs, stores
+  // keypoint j's table, issues the next keypoint's window loads, finishes keypoint j - 1's tests
+  // from the table reads it issued last iteration (their latency covered by this iteration's
+  // MFMAs and stores), then issues keypoint j's sample reads. The table is single-buffered: a
+  // wave's LDS operations execute in order, so j's stores cannot overtake j - 1's reads.
+  const uint32_t rt_lds = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) const uint32_t*)tw -
+                          4u * (uint32_t)kWs * 0x400000u - 4u * 0x4B400000u;
+  uint32_t wr[8][4];         // the pending keypoint's sample reads
+  bool tail_p = false;       // ... whether its window reaches the row's scalar tail
+  uint32_t xt_p = 0;         // ... and that tail's first column bits
+  f32x2 ab_p = {0.f, 0.f}, nab_p = {0.f, 0.f};  // ... and its rotation (the tail case recomputes X)
+  // the lane's 8 samples of keypoint j: addresses, then all 16 reads in flight
+  auto issue_reads = [&](int j, const RsGeo& G) {
     const uint32_t sft = (uint32_t)((G.kx - 21) & 3);
-    uint4 q[kRounds * kTaskRows];
+    const float cj = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(ca), 8 * j));
+    const float sj = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(sa), 8 * j));
+    const f32x2 ab = {sj, cj}, nab = {cj, -sj};
+    // A sample (cx, cy) reads column c = cx + 18 + s, dwords cy + 18 + {0, 2, 4, 6}: the pairs
+    // (R0, R1), (R2, R3), (R4, R5), (R6, R7) of its 7 taps for v_dot2 -- R7 meets K0's zero high
+    // half. The byte address comes straight from the rounded coordinates' float bits
+    // X = M + 18 + cx, Y = M + 18 + cy (M = 0x4B400000, low 24 bits 0x400000):
+    // 4 (c kWs + cy + 18) = umul24(X, 4 kWs) + 4 Y + 4 kWs s - 4 kWs 0x400000 - 4 M, mod 2^32.
+    const uint32_t rt_base = rt_lds + 4u * (uint32_t)kWs * sft;
 #pragma unroll
-    for (int i = 0; i < kRounds * kTaskRows; i++) q[i] = qn[i];
+    for (int k = 0; k < 8; k++) {
+      // sp = fma({px, px}, ab, {py, py} * nab) + magic, x and y broadcast from the pair
+      f32x2 pq, sp;
+      asm("v_pk_mul_f32 %0, %1, %2 op_sel:[1,0] op_sel_hi:[1,1]"
+          : "=v"(pq) : "v"(pf[k]), "s"(nab));
+      asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[0,0,0] op_sel_hi:[0,1,1]"
+          : "=v"(sp) : "v"(pf[k]), "s"(ab), "v"(pq));
+      sp = sp + magic;
+      const uint32_t Y = __float_as_uint(sp.x), X = __float_as_uint(sp.y);
+      uint32_t t;  // X * 4 kWs + rt_base in one v_mad_u32_u24 (X's low 24 bits)
+      asm("v_mad_u32_u24 %0, %1, %2, %3" : "=v"(t) : "v"(X), "v"(4u * kWs), "s"(rt_base));
+      const lds_u32* rw = (const lds_u32*)(uintptr_t)((Y << 2) + t);
+      wr[k][0] = rw[0];
+      wr[k][1] = rw[2];
+      wr[k][2] = rw[4];
+      wr[k][3] = rw[6];
+    }
+    // kTail: the window reaches the scalar tail of the row (x >= W - W % 4, rounded half up
+    // instead of half to even) -- a wave-uniform case
+    const int xvec = G.w - (G.w & 3);
+    tail_p = G.kx + 18 >= xvec;
+    xt_p = (uint32_t)(xvec - G.kx + 18) + 0x4B400000u;  // X >= this: tail
+    ab_p = ab;
+    nab_p = nab;
+  };
+  // keypoint j's 256 tests from the pending reads: descriptor dwords of lanes 4 j .. 4 j + 3
+  auto finish = [&](auto jc) {
+    constexpr int j = decltype(jc)::value;
+    auto run = [&](auto tail_case) {
+      constexpr bool kTail = decltype(tail_case)::value;
+      // the 8 samples' sums level by level: consecutive v_dot2 are independent (a dependent one
+      // needs wait states)
+      uint32_t smv[8];
 #pragma unroll
-    for (int i = 0; i < kRounds; i++) {
-      if (trow[i] >= 0) {
-        const int r = trow[i], gq = tcol[i] >> 2;
-        uint32_t R[kTaskRows][4];
+      for (int k = 0; k < 8; k++) smv[k] = dot2u(wr[k][3], K0, 0u);
 #pragma unroll
-        for (int h = 0; h < kTaskRows; h++) {
-          uint32_t u0, u1, u2;
-          if (G.fastp) {
-            const uint4 v = q[kTaskRows * i + h];
-            u0 = __builtin_amdgcn_alignbyte(v.y, v.x, sft);
-            u1 = __builtin_amdgcn_alignbyte(v.z, v.y, sft);
-            u2 = __builtin_amdgcn_alignbyte(v.w, v.z, sft);
-          } else
-          {  // the window leaves the level: reflect-101 rows and columns, byte loads
-            const int rr = min(r + h, 42);
-            const uint8_t* row = G.im + (int64_t)reflect101(G.ky - 21 + rr, G.h) * G.pitch;
-            const int x0 = G.kx - 18 + 4 * gq;
-            uint32_t wv[3] = {0, 0, 0};
+      for (int k = 0; k < 8; k++) smv[k] = dot2u(wr[k][2], K21, smv[k]);
 #pragma unroll
-            for (int k = 0; k < 10; k++)
-              wv[k >> 2] |= (uint32_t)row[reflect101(x0 - 3 + k, G.w)] << (8 * (k & 3));
-            u0 = wv[0];
-            u1 = wv[1];
-            u2 = wv[2];
+      for (int k = 0; k < 8; k++) smv[k] = dot2u(wr[k][1], K23, smv[k]);
+#pragma unroll
+      for (int k = 0; k < 8; k++) smv[k] = dot2u(wr[k][0], K01, smv[k]);
+      uint64_t words[4];
+      static_for<4>([&](auto rc) {
+        constexpr int r = decltype(rc)::value;
+        uint32_t v[2];
+#pragma unroll
+        for (int e = 0; e < 2; e++) {
+          const int k = 2 * r + e;
+          const uint32_t sm = smv[k];
+          uint32_t o;
+          if (kTail) {
+            f32x2 pq, sp;  // the sample's column bits again (rare case: no VGPRs held for it)
+            asm("v_pk_mul_f32 %0, %1, %2 op_sel:[1,0] op_sel_hi:[1,1]"
+                : "=v"(pq) : "v"(pf[k]), "s"(nab_p));
+            asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[0,0,0] op_sel_hi:[0,1,1]"
+                : "=v"(sp) : "v"(pf[k]), "s"(ab_p), "v"(pq));
+            sp = sp + magic;
+            const bool tail = __float_as_uint(sp.y) >= xt_p;
+            o = (sm + (tail ? 0x8000u : 0x7fffu + ((sm >> 16) & 1u))) >> 16;
+          } else {
+            o = (sm + 0x7fffu + ((sm >> 16) & 1u)) >> 16;
           }
-          R[h][0] = __builtin_amdgcn_udot4(u0, KA, __builtin_amdgcn_udot4(u1, KB, 0u, false), false);
-          R[h][1] = __builtin_amdgcn_udot4(u0, C1a, __builtin_amdgcn_udot4(u1, C1b, 0u, false), false);
-          R[h][2] = __builtin_amdgcn_udot4(u0, C2a, __builtin_amdgcn_udot4(u1, C2b,
-                                           __builtin_amdgcn_udot4(u2, C2c, 0u, false), false), false);
-          R[h][3] = __builtin_amdgcn_udot4(u0, C3a, __builtin_amdgcn_udot4(u1, C3b,
-                                           __builtin_amdgcn_udot4(u2, C3c, 0u, false), false), false);
+          v[e] = o > 255u ? 255u : o;
         }
+        words[r] = __ballot(v[0] < v[1]);
+      });
+      // descriptor dword pairs of lanes 4 j .. 4 j + 3 (v_writelane: no per-lane select; the
+      // lane selects are inline constants, j and r being compile-time). A v_writelane that reads
+      // an SGPR a VALU compare has just written needs wait states (measured: without them bit
+      // 7 of ~12 % of the descriptor bytes came out wrong), so the four ballots come first and
+      // one s_nop covers them all.
+      uint32_t lo = dlo, hi = dhi;  // (local copies: the asm operands of a nested lambda)
+      asm volatile("s_nop 4\n\t"
+                   "v_writelane_b32 %0, %2, %10\n\tv_writelane_b32 %1, %3, %10\n\t"
+                   "v_writelane_b32 %0, %4, %11\n\tv_writelane_b32 %1, %5, %11\n\t"
+                   "v_writelane_b32 %0, %6, %12\n\tv_writelane_b32 %1, %7, %12\n\t"
+                   "v_writelane_b32 %0, %8, %13\n\tv_writelane_b32 %1, %9, %13"
+                   : "+v"(lo), "+v"(hi)
+                   : "s"((uint32_t)words[0]), "s"((uint32_t)(words[0] >> 32)),
+                     "s"((uint32_t)words[1]), "s"((uint32_t)(words[1] >> 32)),
+                     "s"((uint32_t)words[2]), "s"((uint32_t)(words[2] >> 32)),
+                     "s"((uint32_t)words[3]), "s"((uint32_t)(words[3] >> 32)),
+                     "i"(4 * j), "i"(4 * j + 1), "i"(4 * j + 2), "i"(4 * j + 3));
+      dlo = lo;
+      dhi = hi;
+    };
+    if (tail_p) run(std::true_type{});
+    else run(std::false_type{});
+  };
+  RsGeo gn = rs_geo(0);
+  win_fill(gn);
+  static_for<KPW>([&](auto jc) {
+    constexpr int j = decltype(jc)::value;
+    const RsGeo G = gn;
+    // the window has landed (buffer-to-LDS loads count in vmcnt; border windows were stored by
+    // this wave's own ds_writes, which its LDS reads follow in order): the A operands
+    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    u32x4 axn[3];
 #pragma unroll
-        for (int jx = 0; jx < 4; jx++) {
-          rtw[(4 * gq + jx) * kRtRows + r] = (uint16_t)R[0][jx];
-        }
+    for (int ti = 0; ti < 3; ti++) axn[ti] = *reinterpret_cast<const u32x4*>(win + a_lds[ti]);
+    // keypoint j - 1's tests (their table reads were issued last iteration; this VALU covers the
+    // A reads' latency, and the sample reads' registers are free again before the MFMA results
+    // need theirs)
+    if constexpr (j > 0) finish(std::integral_constant<int, j - 1>{});
+    // the row sums: 9 MFMAs (A bytes - 128 as int8: x ^ 0x80)
+    v4i acc[3][3];
+    {
+      const v4i cinit = {128 * 257, 128 * 257, 128 * 257, 128 * 257};
+#pragma unroll
+      for (int ti = 0; ti < 3; ti++) {
+        const u32x4 x = axn[ti] ^ 0x80808080u;
+        const v4i av = {(int)x.x, (int)x.y, (int)x.z, (int)x.w};
+#pragma unroll
+        for (int tj = 0; tj < 3; tj++)
+          acc[ti][tj] = __builtin_amdgcn_mfma_i32_16x16x64_i8(av, bm[tj], cinit, 0, 0, 0);
       }
     }
-    __asm__ volatile("" ::: "memory");
     if (j + 1 < KPW) {
+      // the next keypoint's window: its loads overwrite the staging area this keypoint's A reads
+      // came from, so they wait for those (the MFMAs above consumed them)
       gn = rs_geo(j + 1);
-      rs_load(gn, qn);
+      __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
+      win_fill(gn);
     }
-    {
-      const int kx = G.kx;
-      const int w = G.w, xvec = w - (w & 3);
-      const float cj = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(ca), 8 * j));
-      const float sj = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(sa), 8 * j));
-      const f32x2 ab = {sj, cj}, nab = {cj, -sj};
-      // A sample's 7 row sums are u16 (cx, cy .. cy + 6) of the table: four aligned dword reads
-      // at (a & ~3) cover them, and v_alignbit by 16 (cy odd) or 0 (cy even) shifts the pairs into
-      // (R0, R1), (R2, R3), (R4, R5), (R6, R7) for v_dot2 -- R7 meets K0's zero high half (the
-      // table's spare rows and columns keep the reads inside the window). The parity of the u16
-      // address is cy's parity only because a column holds an even number of u16 (kRtRows even,
-      // asserted below); alignbit takes the shift Y << 4 mod 32.
-      // The address comes straight from the rounded coordinates' float bits X = M + cx,
-      // Y = M + cy (M = 0x4B400000, low 24 bits 0x400000): 2 (cx kRtRows + cy) =
-      // umul24(X, 2 kRtRows) + 2 Y - (2 kRtRows 0x400000 + 2 M), all modulo 2^32.
-      static_assert((kRtRows & 1) == 0, "the u16 address parity must equal cy's parity");
-      typedef __attribute__((address_space(3))) const uint32_t lds_u32;
-      const uint32_t rt_base =
-          (uint32_t)(uintptr_t)(__attribute__((address_space(3))) const uint16_t*)&s_rt[wid][0][0] -
-          2u * (uint32_t)kRtRows * 0x400000u - 2u * 0x4B400000u;
-      // the 256 tests; kTail: the window reaches the scalar tail of the row (x >= W - W % 4,
-      // rounded half up instead of half to even) -- a wave-uniform case, so two code paths
-      auto tests = [&](auto tail_case) {
-        constexpr bool kTail = decltype(tail_case)::value;
-        const uint32_t xt_bits = (uint32_t)(xvec - kx + 18) + 0x4B400000u;  // X >= this: tail
+    // the pair table: lane (n, g) writes W[12 g .. 12 g + 11] of column 16 tj + n. W[12 g + 11]'s
+    // high half is R[12 g + 12], which the next lane group holds: that lane writes it (a u16
+    // store after the b128 stores), so no lane waits for another's data; lane group 0's u16 lands
+    // in the previous column's row 43 (never read) or, for column 0, the table's front pad.
+    // Stores are grouped by predicate (columns past 39 and rows past 43 are outside the table):
+    // one exec change per group instead of one per store.
+    uint32_t wv[3][12];
 #pragma unroll
-        for (int r = 0; r < 4; r++) {
-          uint32_t v[2];
+    for (int tj = 0; tj < 3; tj++) {
 #pragma unroll
-          for (int e = 0; e < 2; e++) {
-            const float px = (float)(int)(int8_t)(pat[r] >> (16 * e));
-            const float py = (float)(int)(int8_t)(pat[r] >> (16 * e + 8));
-            const f32x2 sp = __builtin_elementwise_fma((f32x2){px, px}, ab, (f32x2){py, py} * nab) + magic;
-            const uint32_t Y = __float_as_uint(sp.x), X = __float_as_uint(sp.y);
-            uint32_t t;  // X * 2 kRtRows + rt_base in one v_mad_u32_u24 (X's low 24 bits)
-            asm("v_mad_u32_u24 %0, %1, %2, %3" : "=v"(t) : "v"(X), "v"(2u * kRtRows), "s"(rt_base));
-            const uint32_t a = (Y << 1) + t;
-            const lds_u32* rw = (const lds_u32*)(uintptr_t)(a & ~3u);
-            const uint32_t sh = Y << 4;  // alignbit takes it mod 32: 16 for an odd start (cy odd)
-            const uint32_t w0 = rw[0], w1 = rw[1], w2 = rw[2], w3 = rw[3];
-            const uint32_t p0 = __builtin_amdgcn_alignbit(w1, w0, sh);
-            const uint32_t p1 = __builtin_amdgcn_alignbit(w2, w1, sh);
-            const uint32_t p2 = __builtin_amdgcn_alignbit(w3, w2, sh);
-            const uint32_t p3 = __builtin_amdgcn_alignbit(0u, w3, sh);
-            const uint32_t sm = dot2u(p0, K01, dot2u(p1, K23, dot2u(p2, K21, dot2u(p3, K0, 0u))));
-            uint32_t o;
-            if (kTail) {
-              const bool tail = X >= xt_bits;
-              o = (sm + (tail ? 0x8000u : 0x7fffu + ((sm >> 16) & 1u))) >> 16;
-            } else {
-              o = (sm + 0x7fffu + ((sm >> 16) & 1u)) >> 16;
-            }
-            v[e] = o > 255u ? 255u : o;
-          }
-          const uint64_t word = __ballot(v[0] < v[1]);
-          // descriptor dword pair of lane 4 j + r (v_writelane: no per-lane select)
-          uint32_t lo = dlo, hi = dhi;
-          const int sel = 4 * j + r;
-          // (the lane select in M0: gfx9's constant bus takes one SGPR besides M0)
-          asm("s_mov_b32 m0, %2\n\tv_writelane_b32 %0, %1, m0"
-              : "+v"(lo) : "s"((uint32_t)word), "s"(sel) : "m0");
-          asm("s_mov_b32 m0, %2\n\tv_writelane_b32 %0, %1, m0"
-              : "+v"(hi) : "s"((uint32_t)(word >> 32)), "s"(sel) : "m0");
-          dlo = lo;
-          dhi = hi;
-        }
-      };
-      if (kx + 18 >= xvec) tests(std::true_type{});
-      else tests(std::false_type{});
+      for (int i = 0; i < 11; i++)
+        wv[tj][i] = __builtin_amdgcn_perm((uint32_t)acc[(i + 1) >> 2][tj][(i + 1) & 3],
+                                          (uint32_t)acc[i >> 2][tj][i & 3], 0x05040100u);
+      wv[tj][11] = (uint32_t)acc[2][tj][3];
+    }
+    auto st = [&](int tj, int q) {
+      reinterpret_cast<uint4*>(tw_lane + 16 * tj * kWs)[q] =
+          make_uint4(wv[tj][4 * q], wv[tj][4 * q + 1], wv[tj][4 * q + 2], wv[tj][4 * q + 3]);
+    };
+    auto st16 = [&](int tj) {
+      reinterpret_cast<uint16_t*>(tw_lane + 16 * tj * kWs - 1)[1] = (uint16_t)acc[0][tj][0];
+    };
+    // (a u16 store must follow the b128 store of the lane group below it, which writes the
+    // whole dword with a zero high half)
+    st(0, 0);
+    st(0, 1);
+    st(1, 0);
+    st(1, 1);
+    if (mf_g < 3) {
+      st(0, 2);
+      st(1, 2);
+    }
+    st16(0);
+    st16(1);
+    if (mf_n < 8) {
+      st(2, 0);
+      st(2, 1);
+      if (mf_g < 3) st(2, 2);
+      st16(2);
     }
     __asm__ volatile("" ::: "memory");
-  }
+    issue_reads(j, G);
+    __asm__ volatile("" ::: "memory");
+  });
+  finish(std::integral_constant<int, KPW - 1>{});
   const int64_t o = (int64_t)img * g->kp_cap + k0;
   if (lane < 4 * nk)
     reinterpret_cast<uint64_t*>(desc + o * 32)[lane] = ((uint64_t)dhi << 32) | dlo;

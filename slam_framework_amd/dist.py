@@ -26,17 +26,25 @@ def shard(n_units: int, rank: int, world: int):
     return lo, lo + q + (1 if rank < r else 0)
 
 
+def collective_device(device=None):
+    """Where a small collective's tensor lives: the process group's device for RCCL ("nccl"),
+    host memory for gloo (the CPU backend; bench.py --dist-backend gloo, the CPU tests)."""
+    if dist.is_available() and dist.is_initialized() and dist.get_backend() == "gloo":
+        return torch.device("cpu")
+    return device
+
+
 def max_over_ranks(x: float, device=None) -> float:
     if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
         return float(x)
-    t = torch.tensor([float(x)], dtype=torch.float64, device=device)
+    t = torch.tensor([float(x)], dtype=torch.float64, device=collective_device(device))
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
 
 
 def gather_summary(values, device=None):
     """All ranks' small int64 summaries, stacked [world, len(values)] (on every rank)."""
-    t = torch.tensor(list(values), dtype=torch.int64, device=device)
+    t = torch.tensor(list(values), dtype=torch.int64, device=collective_device(device))
     if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
         return t[None].cpu()
     out = [torch.empty_like(t) for _ in range(dist.get_world_size())]

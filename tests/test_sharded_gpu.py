@@ -207,3 +207,29 @@ def test_bench_shape_gather_matches_oracle(oracle, gpu_lib):
     # (frames g with g % 16 == 0 pair the sequence's last render with its first: few matches)
     pick = [got[i] for i in (0, 1, 126, 200, 254)]
     _check_vs_oracle(oracle, pick, job.gframe, job.Bs, job.poses, job.D, Ls, Rs, parts)
+
+
+def test_bench_two_ranks_gloo():
+    """`bench.py --gpus 2` end to end on one GPU: spawn_ranks starts two rank
+    processes before any GPU call, each runs the timed job on its shard with the gather staged
+    through host memory (gloo), max_over_ranks / gather_summary run over the group, and rank 0
+    prints ONE JSON line whose n_gpus / parallelism describe the 2-rank job and whose gather check
+    found the other rank's frames identical to its own. Only the RCCL transport itself is left to
+    the driver's multi-GPU runs."""
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    cmd = [sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--dist-backend", "gloo",
+           "--steps", "2", "--warmup", "1", "--batch", "32", "--no-cpu-baseline",
+           "--no-optimizer", "--no-bow", "--no-latency"]
+    p = subprocess.run(cmd, capture_output=True, text=True, timeout=150,
+                       env=dict(os.environ, PYTHONUNBUFFERED="1"))
+    assert p.returncode == 0, p.stderr[-3000:]
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, p.stdout[-2000:]
+    d = __import__("json").loads(lines[0])
+    assert d["n_gpus"] == 2 and d["scaling"] == "weak"
+    assert d["config"]["dist_backend"] == "gloo" and "x2" in d["config"]["parallelism"]
+    assert d["config"]["frames_per_gpu_per_step"] == 31
+    g = d["gather"]
+    assert g["identical"] is True and g["frames_checked_vs_rank0"] > 0, g
+    assert len(d["per_rank_matches_per_step"]) == 2 and min(d["per_rank_matches_per_step"]) > 0
+    assert d["value"] > 0 and d["roofline"]["avg_launch_us"] > 0
