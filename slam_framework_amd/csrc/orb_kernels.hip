@@ -2328,8 +2328,9 @@ __device__ __forceinline__ void static_for(F&& f) {
   static_for_impl(f, std::make_integer_sequence<int, N>{});
 }
 
-constexpr int kKpPerWave = 8;
-constexpr int kOdSmallMaxImages = 16;  // launches up to this many images: 4 keypoints per wave
+constexpr int kKpPerWave = 16;        // batches: keypoints per wave (two halves of 8)
+constexpr int kKpPerWaveSmall = 4;    // launches up to kOdSmallMaxImages images
+constexpr int kOdSmallMaxImages = 16;
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 
 // Sum of the 16 per-lane values v[] over the wave; value i ends up in lanes 4i..4i+3.
@@ -2383,7 +2384,14 @@ __device__ __forceinline__ int reduce_scatter16(int (&v)[16], int lane) {
 // window origin's misalignment) x kWs dwords (rows 0..43; 44 = 12 mod 32 banks, so the eight
 // lanes of a ds_write_b128 group write 32 distinct banks).
 constexpr int kWCols = 40, kWs = 44;
-constexpr int kWN = kWCols * kWs;
+// OD_U16: the plain u16 row-sum table instead (column stride kUs u16: 52 = 26 dwords, so the
+// 16 lanes of a ds_write_b64 group hit 16 distinct bank pairs), half the bytes stored per
+// keypoint, samples realigned by v_alignbit as before round 6
+#ifndef OD_U16
+#define OD_U16 1
+#endif
+constexpr int kUs = 52;
+constexpr int kWN = OD_U16 ? kWCols * kUs / 2 : kWCols * kWs;
 // The window staging area per wave: 48 rows x 64 bytes from the dword-aligned origin, filled by
 // buffer-to-LDS loads in row order (four lanes per row: each load instruction's quarter-waves
 // fetch four rows as whole lines) and read back in the MFMA's A layout (16 rows per quarter-wave,
@@ -2443,34 +2451,57 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void o
     wt[0][0] = w.x; wt[0][1] = w.y; wt[1][0] = w.z; wt[1][1] = w.w;
     one[0][0] = o.x; one[0][1] = o.y; one[1][0] = o.z; one[1][1] = o.w;
   }
-  uint32_t kkey[kKpPerWave];
-  int klev[kKpPerWave];
-#pragma unroll
-  for (int j = 0; j < kKpPerWave; j++) {
-    const int jj = min(j, nk - 1);
-    kkey[j] = (uint32_t)__builtin_amdgcn_readlane(my_key, jj);
-    klev[j] = __builtin_amdgcn_readlane(my_level, jj);
-  }
   const int in_pitch = __builtin_amdgcn_readfirstlane(b.in_pitch);
+  // every keypoint's window geometry computed once, lane j for keypoint j (vector loads of its
+  // level's geometry), then read back per keypoint by v_readlane: the per-keypoint scalar chain
+  // (level table loads, 64-bit pointer arithmetic, the window tests) was ~60 SALU instructions
+  // per keypoint on the wave's issue stream. gv_k: x | y << 12 | level << 24 | aligned << 28 |
+  // fastp << 31 (aligned: level base and pitch dword-aligned; fastp: aligned and the whole
+  // 43 x 46 window inside the level)
+  uint32_t gv_org_lo, gv_org_hi, gv_pitch, gv_wh, gv_k;
+  {
+    const LevelGeom& L = g->lv[my_level];
+    const int kx = key_x((uint32_t)my_key) + kMinBorder, ky = key_y((uint32_t)my_key) + kMinBorder;
+    const int w = L.w, h = L.h;
+    const int pitch = my_level == 0 ? in_pitch : L.pitch;
+    const uint8_t* im = my_level == 0 ? batch_image(b, img)
+                                      : b.pyr + (int64_t)img * g->pyr_bytes + L.offset;
+    const bool al = ((((uintptr_t)im | (uintptr_t)pitch) & 3) == 0);
+    const bool fastp = al && kx >= 21 && kx <= w - 31 && ky >= 21 && ky + 21 < h;
+    const uintptr_t org = (uintptr_t)(im + (int64_t)(ky - 21) * pitch + ((kx - 21) & ~3));
+    gv_org_lo = (uint32_t)org;
+    gv_org_hi = (uint32_t)(org >> 32);
+    gv_pitch = (uint32_t)pitch;
+    gv_wh = (uint32_t)w | (uint32_t)h << 16;
+    gv_k = (uint32_t)kx | (uint32_t)ky << 12 | (uint32_t)my_level << 24 | (al ? 1u << 28 : 0u) |
+           (fastp ? 1u << 31 : 0u);
+  }
   // Phases 1-2: the IC_Angle patches (raw level, registers), kPh12Split keypoints at a time,
-  // then their moments (lane 8j ends up with keypoint j's)
+  // then their moments. The patch base is the window origin + 6 rows + ((x - 15) & ~3) -
+  // ((x - 21) & ~3) (4 or 8) bytes: no level lookup per keypoint.
   typedef unsigned int u32x3 __attribute__((ext_vector_type(3)));
   constexpr int kPh12Split = 4;
+  constexpr int KIC = KPW > 8 ? 16 : 8;  // keypoints whose angles the wave computes
+  int mom[2];
+#pragma unroll
+  for (int g8 = 0; g8 < KIC / 8; g8++) {  // eight keypoints' moments, then their reduction
   int mv[16];
 #pragma unroll
-  for (int j0 = 0; j0 < kKpPerWave; j0 += kPh12Split) {
+  for (int j0 = 8 * g8; j0 < 8 * g8 + 8; j0 += kPh12Split) {
     u32x3 raw[kPh12Split][2];
+    int ash[kPh12Split];
 #pragma unroll
     for (int jj = 0; jj < kPh12Split; jj++) {
-      const int j = j0 + jj;
-      const int level = klev[j];
-      const int x = key_x(kkey[j]) + kMinBorder, y = key_y(kkey[j]) + kMinBorder;
-      const LevelGeom& L = g->lv[level];
-      const int pitch = level == 0 ? in_pitch : L.pitch;
-      const uint8_t* im = level == 0 ? batch_image(b, img)
-                                     : b.pyr + (int64_t)img * g->pyr_bytes + L.offset;
-      const uint8_t* rbase = im + (int64_t)(y - 15) * pitch + ((x - 15) & ~3);
-      if ((((uintptr_t)im | (uintptr_t)pitch) & 3) == 0) {
+      const int j = min(j0 + jj, nk - 1);
+      const uint32_t k = (uint32_t)__builtin_amdgcn_readlane(gv_k, j);
+      const int x = (int)(k & 0xfffu);
+      const int pitch = __builtin_amdgcn_readlane(gv_pitch, j);
+      const uintptr_t org = (uintptr_t)(uint32_t)__builtin_amdgcn_readlane(gv_org_lo, j) |
+                            (uintptr_t)(uint32_t)__builtin_amdgcn_readlane(gv_org_hi, j) << 32;
+      const uint8_t* rbase = reinterpret_cast<const uint8_t*>(org) + 6 * pitch +
+                             (((x - 15) & ~3) - ((x - 21) & ~3));
+      ash[jj] = (x - 15) & 3;
+      if ((k >> 28) & 1u) {
         // buffer loads off the patch's (wave-uniform) base: no 64-bit address per lane; row 31
         // (the second slot's last four lanes) lies past the 31-row range and reads zeros
         const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
@@ -2487,7 +2518,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void o
           if (r < 31) {
             const uint8_t* rp = rbase + (int64_t)r * pitch + 8 * ick;
 #pragma unroll
-            for (int k = 0; k < 12; k++) w3[k >> 2] |= (uint32_t)rp[k] << (8 * (k & 3));
+            for (int kk = 0; kk < 12; kk++) w3[kk >> 2] |= (uint32_t)rp[kk] << (8 * (kk & 3));
           }
           raw[jj][q] = (u32x3){w3[0], w3[1], w3[2]};
         }
@@ -2496,7 +2527,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void o
 #pragma unroll
     for (int jj = 0; jj < kPh12Split; jj++) {
       const int j = j0 + jj;
-      const int a = (key_x(kkey[j]) + kMinBorder - 15) & 3;
+      const int a = ash[jj];
       int m10 = 0, m01 = 0;
 #pragma unroll
       for (int q = 0; q < 2; q++) {
@@ -2507,14 +2538,30 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void o
         m10 += (int)t - 20 * (int)s;
         m01 += icv[q] * (int)s;
       }
-      mv[2 * j] = m10;
-      mv[2 * j + 1] = m01;
+      mv[2 * (j & 7)] = m10;
+      mv[2 * (j & 7) + 1] = m01;
     }
-    if (kPh12Split < kKpPerWave) __asm__ volatile("" ::: "memory");
+    __asm__ volatile("" ::: "memory");
   }
-  int mom = reduce_scatter16(mv, lane);
-  const int m01 = __builtin_amdgcn_mov_dpp(mom, 0x104, 0xf, 0xf, false);  // row_shl:4
-  const float angle = cv_fast_atan2((float)m01, (float)mom);
+  mom[g8] = reduce_scatter16(mv, lane);  // keypoint j: m10 at lanes 8 j.., m01 at 8 j + 4..
+  }
+  // the moments reduced over the wave: keypoint j's at lane 8 (j & 7) + 4 (j >> 3) (a DPP row
+  // shift merges the second group of 8 into the lanes the first leaves free)
+  int m10v, m01v;
+  {
+    const int mom0 = mom[0];
+    m10v = mom0;
+    m01v = __builtin_amdgcn_mov_dpp(mom0, 0x104, 0xf, 0xf, false);  // row_shl:4
+    if constexpr (KIC > 8) {
+      const int mom1 = mom[1];
+      const int m10h = __builtin_amdgcn_mov_dpp(mom1, 0x114, 0xf, 0xf, false);  // row_shr:4
+      const bool up = lane & 4;
+      m10v = up ? m10h : m10v;
+      m01v = up ? mom1 : m01v;
+    }
+  }
+  auto angle_lane = [](int j) { return 8 * (j & 7) + 4 * (j >> 3); };
+  const float angle = cv_fast_atan2((float)m01v, (float)m10v);
   const float factorPI = (float)(3.14159265358979323846 / 180.0);
   float sa, ca;
   glibc_sincosf(angle * factorPI, &sa, &ca);
@@ -2563,27 +2610,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void o
     int pitch, w, h, kx, ky, level;
     bool fastp;          // the whole window is inside the level: buffer loads, no reflection
   };
-  // every keypoint's window geometry computed once, lane j for keypoint j (vector loads of its
-  // level's geometry), then read back per keypoint by five v_readlane: the per-keypoint scalar
-  // chain (level table loads, 64-bit pointer arithmetic, the window tests) was ~60 SALU
-  // instructions per keypoint on the wave's issue stream
-  uint32_t gv_org_lo, gv_org_hi, gv_pitch, gv_wh, gv_k;
-  {
-    const LevelGeom& L = g->lv[my_level];
-    const int kx = key_x((uint32_t)my_key) + kMinBorder, ky = key_y((uint32_t)my_key) + kMinBorder;
-    const int w = L.w, h = L.h;
-    const int pitch = my_level == 0 ? in_pitch : L.pitch;
-    const uint8_t* im = my_level == 0 ? batch_image(b, img)
-                                      : b.pyr + (int64_t)img * g->pyr_bytes + L.offset;
-    const bool fastp = kx >= 21 && kx <= w - 31 && ky >= 21 && ky + 21 < h &&
-                       ((((uintptr_t)im | (uintptr_t)pitch) & 3) == 0);
-    const uintptr_t org = (uintptr_t)(im + (int64_t)(ky - 21) * pitch + ((kx - 21) & ~3));
-    gv_org_lo = (uint32_t)org;
-    gv_org_hi = (uint32_t)(org >> 32);
-    gv_pitch = (uint32_t)pitch;
-    gv_wh = (uint32_t)w | (uint32_t)h << 16;
-    gv_k = (uint32_t)kx | (uint32_t)ky << 12 | (uint32_t)my_level << 24 | (fastp ? 1u << 31 : 0u);
-  }
   auto rs_geo = [&](int j) {
     RsGeo G;
     const int jj = min(j, nk - 1);
@@ -2657,47 +2683,83 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void o
   typedef __attribute__((address_space(3))) const uint32_t lds_u32;
   uint32_t* tw = &s_w[wid][4];
   // the lane's first table dword of tile column 0: column n, row 12 g
+#if OD_U16
+  uint32_t* tw_lane = tw + mf_n * (kUs / 2) + 6 * mf_g;  // u16 row 12 g of column n
+#else
   uint32_t* tw_lane = tw + mf_n * kWs + 12 * mf_g;
+#endif
   // Software pipeline over the wave's keypoints: iteration j issues keypoint j's MFMAs, stores
   // keypoint j's table, issues the next keypoint's window loads, finishes keypoint j - 1's tests
   // from the table reads it issued last iteration (their latency covered by this iteration's
   // MFMAs and stores), then issues keypoint j's sample reads. The table is single-buffered: a
   // wave's LDS operations execute in order, so j's stores cannot overtake j - 1's reads.
+#if OD_U16
+  // byte address of u16 (c, r) = tw + 2 kUs c + 2 r, c = cx + 18 + s, r = cy + 18:
+  // umul24(X, 2 kUs) + 2 Y + 2 kUs s - 2 kUs 0x400000 - 2 M
+  const uint32_t rt_lds = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) const uint32_t*)tw -
+                          2u * (uint32_t)kUs * 0x400000u - 2u * 0x4B400000u;
+  constexpr uint32_t kColBytes = 2u * kUs;
+#else
   const uint32_t rt_lds = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) const uint32_t*)tw -
                           4u * (uint32_t)kWs * 0x400000u - 4u * 0x4B400000u;
+  constexpr uint32_t kColBytes = 4u * kWs;
+#endif
   uint32_t wr[8][4];         // the pending keypoint's sample reads
+#if OD_U16
+  uint32_t wsh[8];           // ... and their realignment shifts (u16 table)
+#endif
   bool tail_p = false;       // ... whether its window reaches the row's scalar tail
   uint32_t xt_p = 0;         // ... and that tail's first column bits
   f32x2 ab_p = {0.f, 0.f}, nab_p = {0.f, 0.f};  // ... and its rotation (the tail case recomputes X)
   // the lane's 8 samples of keypoint j: addresses, then all 16 reads in flight
-  auto issue_reads = [&](int j, const RsGeo& G) {
+  auto issue_reads = [&](int alane, const RsGeo& G) {
     const uint32_t sft = (uint32_t)((G.kx - 21) & 3);
-    const float cj = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(ca), 8 * j));
-    const float sj = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(sa), 8 * j));
+    const float cj = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(ca), alane));
+    const float sj = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(sa), alane));
     const f32x2 ab = {sj, cj}, nab = {cj, -sj};
     // A sample (cx, cy) reads column c = cx + 18 + s, dwords cy + 18 + {0, 2, 4, 6}: the pairs
     // (R0, R1), (R2, R3), (R4, R5), (R6, R7) of its 7 taps for v_dot2 -- R7 meets K0's zero high
     // half. The byte address comes straight from the rounded coordinates' float bits
     // X = M + 18 + cx, Y = M + 18 + cy (M = 0x4B400000, low 24 bits 0x400000):
     // 4 (c kWs + cy + 18) = umul24(X, 4 kWs) + 4 Y + 4 kWs s - 4 kWs 0x400000 - 4 M, mod 2^32.
-    const uint32_t rt_base = rt_lds + 4u * (uint32_t)kWs * sft;
+    const uint32_t rt_base = rt_lds + kColBytes * sft;
+    // stage by stage over the 8 samples: a dependent packed-f32 / VALU pair needs a wait state,
+    // a sample-at-a-time chain issued one s_nop per step
+    // sp = fma({px, px}, ab, {py, py} * nab) + magic, x and y broadcast from the pair
+    f32x2 sp[8];
+#pragma unroll
+    for (int k = 0; k < 8; k++)
+      asm("v_pk_mul_f32 %0, %1, %2 op_sel:[1,0] op_sel_hi:[1,1]" : "=v"(sp[k]) : "v"(pf[k]), "s"(nab));
+#pragma unroll
+    for (int k = 0; k < 8; k++)
+      asm("v_pk_fma_f32 %0, %1, %2, %0 op_sel:[0,0,0] op_sel_hi:[0,1,1]"
+          : "+v"(sp[k]) : "v"(pf[k]), "s"(ab));
+#pragma unroll
+    for (int k = 0; k < 8; k++) sp[k] = sp[k] + magic;
+    uint32_t ta[8];
+#pragma unroll
+    for (int k = 0; k < 8; k++)  // X * 4 kWs + rt_base in one v_mad_u32_u24 (X's low 24 bits)
+      asm("v_mad_u32_u24 %0, %1, %2, %3"
+          : "=v"(ta[k]) : "v"(__float_as_uint(sp[k].y)), "v"(kColBytes), "s"(rt_base));
 #pragma unroll
     for (int k = 0; k < 8; k++) {
-      // sp = fma({px, px}, ab, {py, py} * nab) + magic, x and y broadcast from the pair
-      f32x2 pq, sp;
-      asm("v_pk_mul_f32 %0, %1, %2 op_sel:[1,0] op_sel_hi:[1,1]"
-          : "=v"(pq) : "v"(pf[k]), "s"(nab));
-      asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[0,0,0] op_sel_hi:[0,1,1]"
-          : "=v"(sp) : "v"(pf[k]), "s"(ab), "v"(pq));
-      sp = sp + magic;
-      const uint32_t Y = __float_as_uint(sp.x), X = __float_as_uint(sp.y);
-      uint32_t t;  // X * 4 kWs + rt_base in one v_mad_u32_u24 (X's low 24 bits)
-      asm("v_mad_u32_u24 %0, %1, %2, %3" : "=v"(t) : "v"(X), "v"(4u * kWs), "s"(rt_base));
-      const lds_u32* rw = (const lds_u32*)(uintptr_t)((Y << 2) + t);
+#if OD_U16
+      // 4 aligned dwords from the dword holding row cy: u16 rows cy .. cy + 7 (+ one before
+      // when cy is odd); the realignment shift (16 for odd cy) rides along in wsh
+      const uint32_t a = (__float_as_uint(sp[k].x) << 1) + ta[k];
+      const lds_u32* rw = (const lds_u32*)(uintptr_t)(a & ~3u);
+      wr[k][0] = rw[0];
+      wr[k][1] = rw[1];
+      wr[k][2] = rw[2];
+      wr[k][3] = rw[3];
+      wsh[k] = __float_as_uint(sp[k].x) << 4;
+#else
+      const lds_u32* rw = (const lds_u32*)(uintptr_t)((__float_as_uint(sp[k].x) << 2) + ta[k]);
       wr[k][0] = rw[0];
       wr[k][1] = rw[2];
       wr[k][2] = rw[4];
       wr[k][3] = rw[6];
+#endif
     }
     // kTail: the window reaches the scalar tail of the row (x >= W - W % 4, rounded half up
     // instead of half to even) -- a wave-uniform case
@@ -2708,12 +2770,21 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void o
     nab_p = nab;
   };
   // keypoint j's 256 tests from the pending reads: descriptor dwords of lanes 4 j .. 4 j + 3
-  auto finish = [&](auto jc) {
+  auto finish = [&](auto jc) {  // the keypoint's index within its half
     constexpr int j = decltype(jc)::value;
     auto run = [&](auto tail_case) {
       constexpr bool kTail = decltype(tail_case)::value;
       // the 8 samples' sums level by level: consecutive v_dot2 are independent (a dependent one
       // needs wait states)
+#if OD_U16
+#pragma unroll
+      for (int k = 0; k < 8; k++) {  // (R0, R1), (R2, R3), (R4, R5), (R6, R7 | 0)
+        wr[k][0] = __builtin_amdgcn_alignbit(wr[k][1], wr[k][0], wsh[k]);
+        wr[k][1] = __builtin_amdgcn_alignbit(wr[k][2], wr[k][1], wsh[k]);
+        wr[k][2] = __builtin_amdgcn_alignbit(wr[k][3], wr[k][2], wsh[k]);
+        wr[k][3] = __builtin_amdgcn_alignbit(0u, wr[k][3], wsh[k]);
+      }
+#endif
       uint32_t smv[8];
 #pragma unroll
       for (int k = 0; k < 8; k++) smv[k] = dot2u(wr[k][3], K0, 0u);
@@ -2773,8 +2844,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void o
   };
   RsGeo gn = rs_geo(0);
   win_fill(gn);
-  static_for<KPW>([&](auto jc) {
-    constexpr int j = decltype(jc)::value;
+  // halves of KH keypoints: the keypoint loop unrolled within a half (its writelane lanes are
+  // constants), the halves rolled; each half stores its keypoints' descriptors
+  constexpr int KH = KPW < 8 ? KPW : 8;
+  const int64_t o = (int64_t)img * g->kp_cap + k0;
+#pragma unroll 1
+  for (int h = 0; h < KPW / KH; h++) {
+    if (KH * h >= nk) break;
+    static_for<KH>([&](auto jc) {
+    constexpr int jj = decltype(jc)::value;
+    const int j = KH * h + jj;
     const RsGeo G = gn;
     // the window has landed (buffer-to-LDS loads count in vmcnt; border windows were stored by
     // this wave's own ds_writes, which its LDS reads follow in order): the A operands
@@ -2787,7 +2866,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void o
     // keypoint j - 1's tests (their table reads were issued last iteration; this VALU covers the
     // A reads' latency, and the sample reads' registers are free again before the MFMA results
     // need theirs)
-    if constexpr (j > 0) finish(std::integral_constant<int, j - 1>{});
+    if constexpr (jj > 0) finish(std::integral_constant<int, jj - 1>{});
     // the row sums: 9 MFMAs (A bytes - 128 as int8: x ^ 0x80)
     v4i acc[3][3];
     {
@@ -2801,13 +2880,30 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void o
           acc[ti][tj] = __builtin_amdgcn_mfma_i32_16x16x64_i8(av, bm[tj], cinit, 0, 0, 0);
       }
     }
-    if (j + 1 < KPW) {
+    if (j + 1 < nk) {
       // the next keypoint's window: its loads overwrite the staging area this keypoint's A reads
-      // came from, so they wait for those (the MFMAs above consumed them)
+      // came from, so they wait for those (the MFMAs above consumed them); none is issued past
+      // the wave's last keypoint (no buffer-to-LDS load outlives the wave)
       gn = rs_geo(j + 1);
       __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
       win_fill(gn);
     }
+#if OD_U16
+    // the u16 table: lane (n, g) writes rows 12 g .. 12 g + 11 of column 16 tj + n as three
+    // 8-byte stores (rows past 43 land in the column's spare rows); columns past 39 are outside
+    // the table (tile column 2, n >= 8)
+    auto st64 = [&](int tj) {
+#pragma unroll
+      for (int q = 0; q < 3; q++) {
+        const uint32_t lo = __builtin_amdgcn_perm((uint32_t)acc[q][tj][1], (uint32_t)acc[q][tj][0], 0x05040100u);
+        const uint32_t hi = __builtin_amdgcn_perm((uint32_t)acc[q][tj][3], (uint32_t)acc[q][tj][2], 0x05040100u);
+        reinterpret_cast<uint2*>(tw_lane + 16 * tj * (kUs / 2))[q] = make_uint2(lo, hi);
+      }
+    };
+    st64(0);
+    st64(1);
+    if (mf_n < 8) st64(2);
+#else
     // the pair table: lane (n, g) writes W[12 g .. 12 g + 11] of column 16 tj + n. W[12 g + 11]'s
     // high half is R[12 g + 12], which the next lane group holds: that lane writes it (a u16
     // store after the b128 stores), so no lane waits for another's data; lane group 0's u16 lands
@@ -2848,15 +2944,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void o
       if (mf_g < 3) st(2, 2);
       st16(2);
     }
+#endif
     __asm__ volatile("" ::: "memory");
-    issue_reads(j, G);
+    issue_reads(angle_lane(j), G);
     __asm__ volatile("" ::: "memory");
-  });
-  finish(std::integral_constant<int, KPW - 1>{});
-  const int64_t o = (int64_t)img * g->kp_cap + k0;
-  if (lane < 4 * nk)
-    reinterpret_cast<uint64_t*>(desc + o * 32)[lane] = ((uint64_t)dhi << 32) | dlo;
-  const float my_angle = __shfl(angle, 8 * lane, 64);
+    });
+    finish(std::integral_constant<int, KH - 1>{});
+    if (lane < 4 * min(KH, nk - KH * h))
+      reinterpret_cast<uint64_t*>(desc + (o + KH * h) * 32)[lane] = ((uint64_t)dhi << 32) | dlo;
+  }
+  const float my_angle = __shfl(angle, angle_lane(lane), 64);
   if (lane < nk) {
     const LevelGeom& L = g->lv[my_level];
     KeyPoint kp;
@@ -3017,7 +3114,7 @@ void launch_extract(const ImageBatch& b, const OrbGeomDev& gd, int n_images, hip
                    gd.ws.node_scratch, gd.ws.oct_keys, gd.ws.oct_count, gd.ws.err);
   }
   if (n_images <= kOdSmallMaxImages) {
-    constexpr int kpw = kKpPerWave / 2;
+    constexpr int kpw = kKpPerWaveSmall;
     SLAMGPU_LAUNCH("orient_desc", st, orient_desc_kernel<kpw>,
                    dim3((g.kp_cap + 4 * kpw - 1) / (4 * kpw), n_images), dim3(256), 0, st, b,
                    gd.dev, gd.ws.oct_keys, gd.ws.oct_count, gd.out.kps, gd.out.desc, gd.out.nkps);
