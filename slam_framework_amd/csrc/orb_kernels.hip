@@ -2367,31 +2367,25 @@ __device__ __forceinline__ int reduce_scatter16(int (&v)[16], int lane) {
 // sums sum_j k_j I(y+i-3, x+j-3) <= 255 * 257 (u16).
 // Per keypoint the row sums of its window (rows y-21..y+21, the columns the rotated samples can
 // reach) come from the matrix cores: a banded int8 GEMM per 16 x 16 tile of the window
-// (v_mfma_i32_16x16x32_i8: A = the window's bytes - 128 as int8, B = the 7 taps, accumulator
+// (v_mfma_i32_16x16x64_i8: A = the window's bytes - 128 as int8, B = the 7 taps, accumulator
 // initialised to 128 * 257, so the i32 result IS the u16 row sum), 3 x 3 tiles per keypoint. The
 // A rows are mapped so that a lane's 12 accumulator elements are 12 consecutive window rows of one
-// column; it pairs them as dwords W[e] = R[e] | R[e + 1] << 16 (the overlapping-pair table, one
-// v_perm each, the row after its last from the next lane group by ds_bpermute) and stores them with
-// three ds_write_b128. A sample's 7 vertical taps are then the dwords e, e+2, e+4, e+6 of its
-// column: two ds_read2_b32 and four v_dot2_u32_u16, no realignment. It rounds with the column's
-// rule (half to even inside the SSE span x < W - W%4, half up in the scalar tail).
+// column; it packs them as u16 pairs (one v_perm per pair) and stores them with three
+// ds_write_b64 into the wave's transposed u16 table. A sample's 7 vertical taps are then 4
+// dwords of its column (two ds_read2_b32, a v_alignbit each for an odd first row) and four
+// v_dot2_u32_u16. It rounds with the column's rule (half to even inside the SSE span
+// x < W - W%4, half up in the scalar tail).
 // Border keypoints (the window leaves the image: reflect-101 rows and columns) gather the A bytes
-// one by one; the GEMM and the table are the same.
-// Round 3-5 variants (VALU row sums stored as transposed u16 with a v_alignbit per tap pair, an
-// MFMA row-sum variant without the pair table or the pipelined loads, dword row pairs, a shifted
-// copy of the table) are in git history and DESIGN.md sections 9-11.
-// The pair table per wave: kWCols columns (window column c = image column x - 18 - s + c, s the
-// window origin's misalignment) x kWs dwords (rows 0..43; 44 = 12 mod 32 banks, so the eight
-// lanes of a ds_write_b128 group write 32 distinct banks).
-constexpr int kWCols = 40, kWs = 44;
-// OD_U16: the plain u16 row-sum table instead (column stride kUs u16: 52 = 26 dwords, so the
-// 16 lanes of a ds_write_b64 group hit 16 distinct bank pairs), half the bytes stored per
-// keypoint, samples realigned by v_alignbit as before round 6
-#ifndef OD_U16
-#define OD_U16 1
-#endif
-constexpr int kUs = 52;
-constexpr int kWN = OD_U16 ? kWCols * kUs / 2 : kWCols * kWs;
+// into the same staging slots; the GEMM and the table are the same.
+// Variants measured in round 6 (profiles/r7*): an overlapping-pair table
+// (dwords R[e] | R[e+1] << 16, no v_alignbit but twice the bytes stored: 0.87 vs 0.82 ms), A
+// operands loaded straight from global memory (16 rows per quarter-wave), 8 keypoints per wave.
+// Round 3-5 variants are in git history and DESIGN.md sections 9-11.
+// The table per wave: kWCols columns (window column c = image column x - 18 - s + c, s the window
+// origin's misalignment) x kUs u16 (rows 0..47, 43 used; 52 u16 = 26 dwords per column, so the 16
+// lanes of a ds_write_b64 group hit 16 distinct bank pairs).
+constexpr int kWCols = 40, kUs = 52;
+constexpr int kWN = kWCols * kUs / 2;  // dwords
 // The window staging area per wave: 48 rows x 64 bytes from the dword-aligned origin, filled by
 // buffer-to-LDS loads in row order (four lanes per row: each load instruction's quarter-waves
 // fetch four rows as whole lines) and read back in the MFMA's A layout (16 rows per quarter-wave,
@@ -2683,31 +2677,19 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void o
   typedef __attribute__((address_space(3))) const uint32_t lds_u32;
   uint32_t* tw = &s_w[wid][4];
   // the lane's first table dword of tile column 0: column n, row 12 g
-#if OD_U16
   uint32_t* tw_lane = tw + mf_n * (kUs / 2) + 6 * mf_g;  // u16 row 12 g of column n
-#else
-  uint32_t* tw_lane = tw + mf_n * kWs + 12 * mf_g;
-#endif
   // Software pipeline over the wave's keypoints: iteration j issues keypoint j's MFMAs, stores
   // keypoint j's table, issues the next keypoint's window loads, finishes keypoint j - 1's tests
   // from the table reads it issued last iteration (their latency covered by this iteration's
   // MFMAs and stores), then issues keypoint j's sample reads. The table is single-buffered: a
   // wave's LDS operations execute in order, so j's stores cannot overtake j - 1's reads.
-#if OD_U16
   // byte address of u16 (c, r) = tw + 2 kUs c + 2 r, c = cx + 18 + s, r = cy + 18:
   // umul24(X, 2 kUs) + 2 Y + 2 kUs s - 2 kUs 0x400000 - 2 M
   const uint32_t rt_lds = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) const uint32_t*)tw -
                           2u * (uint32_t)kUs * 0x400000u - 2u * 0x4B400000u;
   constexpr uint32_t kColBytes = 2u * kUs;
-#else
-  const uint32_t rt_lds = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) const uint32_t*)tw -
-                          4u * (uint32_t)kWs * 0x400000u - 4u * 0x4B400000u;
-  constexpr uint32_t kColBytes = 4u * kWs;
-#endif
   uint32_t wr[8][4];         // the pending keypoint's sample reads
-#if OD_U16
   uint32_t wsh[8];           // ... and their realignment shifts (u16 table)
-#endif
   bool tail_p = false;       // ... whether its window reaches the row's scalar tail
   uint32_t xt_p = 0;         // ... and that tail's first column bits
   f32x2 ab_p = {0.f, 0.f}, nab_p = {0.f, 0.f};  // ... and its rotation (the tail case recomputes X)
@@ -2717,11 +2699,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void o
     const float cj = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(ca), alane));
     const float sj = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(sa), alane));
     const f32x2 ab = {sj, cj}, nab = {cj, -sj};
-    // A sample (cx, cy) reads column c = cx + 18 + s, dwords cy + 18 + {0, 2, 4, 6}: the pairs
-    // (R0, R1), (R2, R3), (R4, R5), (R6, R7) of its 7 taps for v_dot2 -- R7 meets K0's zero high
+    // A sample (cx, cy) reads column c = cx + 18 + s, u16 rows cy + 18 .. cy + 24: four aligned
+    // dwords from the one holding the first, realigned (v_alignbit by 16 for an odd first row)
+    // into the pairs (R0, R1), (R2, R3), (R4, R5), (R6, R7) for v_dot2 -- R7 meets K0's zero high
     // half. The byte address comes straight from the rounded coordinates' float bits
-    // X = M + 18 + cx, Y = M + 18 + cy (M = 0x4B400000, low 24 bits 0x400000):
-    // 4 (c kWs + cy + 18) = umul24(X, 4 kWs) + 4 Y + 4 kWs s - 4 kWs 0x400000 - 4 M, mod 2^32.
+    // X = M + 18 + cx, Y = M + 18 + cy (M = 0x4B400000, low 24 bits 0x400000): see rt_lds.
     const uint32_t rt_base = rt_lds + kColBytes * sft;
     // stage by stage over the 8 samples: a dependent packed-f32 / VALU pair needs a wait state,
     // a sample-at-a-time chain issued one s_nop per step
@@ -2738,12 +2720,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void o
     for (int k = 0; k < 8; k++) sp[k] = sp[k] + magic;
     uint32_t ta[8];
 #pragma unroll
-    for (int k = 0; k < 8; k++)  // X * 4 kWs + rt_base in one v_mad_u32_u24 (X's low 24 bits)
+    for (int k = 0; k < 8; k++)  // X * 2 kUs + rt_base in one v_mad_u32_u24 (X's low 24 bits)
       asm("v_mad_u32_u24 %0, %1, %2, %3"
           : "=v"(ta[k]) : "v"(__float_as_uint(sp[k].y)), "v"(kColBytes), "s"(rt_base));
 #pragma unroll
     for (int k = 0; k < 8; k++) {
-#if OD_U16
       // 4 aligned dwords from the dword holding row cy: u16 rows cy .. cy + 7 (+ one before
       // when cy is odd); the realignment shift (16 for odd cy) rides along in wsh
       const uint32_t a = (__float_as_uint(sp[k].x) << 1) + ta[k];
@@ -2753,13 +2734,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void o
       wr[k][2] = rw[2];
       wr[k][3] = rw[3];
       wsh[k] = __float_as_uint(sp[k].x) << 4;
-#else
-      const lds_u32* rw = (const lds_u32*)(uintptr_t)((__float_as_uint(sp[k].x) << 2) + ta[k]);
-      wr[k][0] = rw[0];
-      wr[k][1] = rw[2];
-      wr[k][2] = rw[4];
-      wr[k][3] = rw[6];
-#endif
     }
     // kTail: the window reaches the scalar tail of the row (x >= W - W % 4, rounded half up
     // instead of half to even) -- a wave-uniform case
@@ -2776,7 +2750,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void o
       constexpr bool kTail = decltype(tail_case)::value;
       // the 8 samples' sums level by level: consecutive v_dot2 are independent (a dependent one
       // needs wait states)
-#if OD_U16
 #pragma unroll
       for (int k = 0; k < 8; k++) {  // (R0, R1), (R2, R3), (R4, R5), (R6, R7 | 0)
         wr[k][0] = __builtin_amdgcn_alignbit(wr[k][1], wr[k][0], wsh[k]);
@@ -2784,7 +2757,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void o
         wr[k][2] = __builtin_amdgcn_alignbit(wr[k][3], wr[k][2], wsh[k]);
         wr[k][3] = __builtin_amdgcn_alignbit(0u, wr[k][3], wsh[k]);
       }
-#endif
       uint32_t smv[8];
 #pragma unroll
       for (int k = 0; k < 8; k++) smv[k] = dot2u(wr[k][3], K0, 0u);
@@ -2888,7 +2860,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void o
       __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
       win_fill(gn);
     }
-#if OD_U16
     // the u16 table: lane (n, g) writes rows 12 g .. 12 g + 11 of column 16 tj + n as three
     // 8-byte stores (rows past 43 land in the column's spare rows); columns past 39 are outside
     // the table (tile column 2, n >= 8)
@@ -2903,48 +2874,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void o
     st64(0);
     st64(1);
     if (mf_n < 8) st64(2);
-#else
-    // the pair table: lane (n, g) writes W[12 g .. 12 g + 11] of column 16 tj + n. W[12 g + 11]'s
-    // high half is R[12 g + 12], which the next lane group holds: that lane writes it (a u16
-    // store after the b128 stores), so no lane waits for another's data; lane group 0's u16 lands
-    // in the previous column's row 43 (never read) or, for column 0, the table's front pad.
-    // Stores are grouped by predicate (columns past 39 and rows past 43 are outside the table):
-    // one exec change per group instead of one per store.
-    uint32_t wv[3][12];
-#pragma unroll
-    for (int tj = 0; tj < 3; tj++) {
-#pragma unroll
-      for (int i = 0; i < 11; i++)
-        wv[tj][i] = __builtin_amdgcn_perm((uint32_t)acc[(i + 1) >> 2][tj][(i + 1) & 3],
-                                          (uint32_t)acc[i >> 2][tj][i & 3], 0x05040100u);
-      wv[tj][11] = (uint32_t)acc[2][tj][3];
-    }
-    auto st = [&](int tj, int q) {
-      reinterpret_cast<uint4*>(tw_lane + 16 * tj * kWs)[q] =
-          make_uint4(wv[tj][4 * q], wv[tj][4 * q + 1], wv[tj][4 * q + 2], wv[tj][4 * q + 3]);
-    };
-    auto st16 = [&](int tj) {
-      reinterpret_cast<uint16_t*>(tw_lane + 16 * tj * kWs - 1)[1] = (uint16_t)acc[0][tj][0];
-    };
-    // (a u16 store must follow the b128 store of the lane group below it, which writes the
-    // whole dword with a zero high half)
-    st(0, 0);
-    st(0, 1);
-    st(1, 0);
-    st(1, 1);
-    if (mf_g < 3) {
-      st(0, 2);
-      st(1, 2);
-    }
-    st16(0);
-    st16(1);
-    if (mf_n < 8) {
-      st(2, 0);
-      st(2, 1);
-      if (mf_g < 3) st(2, 2);
-      st16(2);
-    }
-#endif
     __asm__ volatile("" ::: "memory");
     issue_reads(angle_lane(j), G);
     __asm__ volatile("" ::: "memory");
