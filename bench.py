@@ -43,14 +43,13 @@ LEVEL_PX = None  # filled from the context geometry
 
 
 TRAFFIC_FILE = os.path.join(ROOT, "profiles", "traffic.json")
-VALU_FILE = os.path.join(ROOT, "profiles", "valu.json")
 
 
 # bench.py's timing names -> kernel symbols where they differ (the octree timing is the per-image
 # kernel; octree_kernel is its global-memory fallback; the batches' pyramid levels run
 # pyr_ring_kernel, the single-frame call pyr_down_kernel)
 KERNEL_SYMBOL = {"octree": ("octree_img",), "octree_global": ("octree",),
-                 "pyr_down": ("pyr_down", "pyr_ring")}
+                 "pyr_down": ("pyr_down", "pyr_ring", "pyr_cascade")}
 
 
 def _symbol_matches(sym, kernel):
@@ -61,28 +60,66 @@ def _symbol_matches(sym, kernel):
 # at 8 waves per SIMD, chains of v_dot4 / v_dot2 / v_alignbit / v_perm / v_lerp_u8 / v_bfe /
 # v_pk_* / v_cvt issue at 0.44-0.48 of the nominal one-wave64-instruction-per-2-cycles peak
 # (256 CUs x 4 SIMD x 2.4 GHz / 2), v_add / v_xor / v_bitop3 / f32 add, mul, fma at 0.70-0.83.
-# The sustained peak is the fastest class (0.83 of nominal), so `valu_sustained_frac` is a lower
-# bound of a kernel's issue utilisation whatever its instruction mix (round 4 priced against
-# the integer class alone, and kernels rich in adds read above 1).
-VALU_SUSTAINED_FRAC_OF_NOMINAL = 0.83
+# A kernel's VALU roof is the rate its own instruction mix sustains: the harmonic mean of the
+# class rates weighted by its ISA's class histogram (tools/isa_mix.py -> profiles/isa_mix.json);
+# `valu_mix_frac` is its measured issue rate over that roof.
+PIPES_FILE = os.path.join(ROOT, "profiles", "pipes.json")
+ISA_MIX_FILE = os.path.join(ROOT, "profiles", "isa_mix.json")
+
+
+def _load_json(path):
+    try:
+        with open(path) as f:
+            return json.load(f)
+    except (OSError, ValueError):
+        return None
+
+
+def _kernel_entries(d, kernel):
+    return [v for k, v in (d or {}).get("kernels", {}).items() if _symbol_matches(k, kernel)]
+
+
+def measured_pipes(kernel, batch):
+    """The batch instantiation's entry of profiles/pipes.json (tools/pmc_pipes.sh +
+    tools/pipes.py: per-dispatch instruction counts and pipe busy fractions from PMC passes of
+    this bench configuration); None when absent or measured on another batch size."""
+    d = _load_json(PIPES_FILE)
+    if not d or d.get("batch") != batch:
+        return None
+    ents = _kernel_entries(d, kernel)
+    # several instantiations may match (orient_desc_kernel<4> serves the single-frame call): the
+    # batch launches are the largest
+    return max(ents, key=lambda v: v.get("sq_insts_valu_per_dispatch") or 0) if ents else None
+
+
+def mix_roof(kernel):
+    """The VALU roof of the kernel's instruction mix, as a fraction of the nominal issue peak."""
+    ents = _kernel_entries(_load_json(ISA_MIX_FILE), kernel)
+    # the batch instantiation: the largest body
+    return max(ents, key=lambda v: v["valu_static_instr"])["mix_roof_frac_of_nominal"] \
+        if ents else None
 
 
 def measured_valu(kernel, batch):
-    """SQ_INSTS_VALU per dispatch of `kernel` (tools/pmc_valu.sh + tools/valu.py, committed as
-    profiles/valu.json) and the chip's VALU issue peak; (None, None) when absent or measured on
-    another batch size."""
-    try:
-        with open(VALU_FILE) as f:
-            d = json.load(f)
-    except (OSError, ValueError):
+    """SQ_INSTS_VALU per dispatch of `kernel` (profiles/pipes.json) and the chip's nominal VALU
+    issue peak; (None, None) when absent or measured on another batch size."""
+    e = measured_pipes(kernel, batch)
+    if not e or not e.get("sq_insts_valu_per_dispatch"):
         return None, None
-    if d.get("batch") != batch:
-        return None, None
-    # several instantiations may match (orient_desc_kernel<4> serves the single-frame call): the
-    # batch launches are the largest
-    vals = [v.get("sq_insts_valu_per_dispatch") or 0 for k, v in d.get("kernels", {}).items()
-            if _symbol_matches(k, kernel)]
-    return (max(vals), d.get("valu_issue_peak_per_s")) if vals else (None, None)
+    return e["sq_insts_valu_per_dispatch"], _load_json(PIPES_FILE).get("valu_issue_peak_per_s")
+
+
+def binding_pipe(kernel, batch, hbm_frac):
+    """The pipe nearest its roof: HBM (live) against the PMC pipe fractions of pipes.json."""
+    e = measured_pipes(kernel, batch)
+    # throughput roofs only: issue activity and the TA / TD busy counters measure occupancy
+    # (latency included), not a pipe's rate (tools/pipes.py)
+    fr = {k: v for k, v in (e or {}).get("pipe_frac", {}).items() if k in ("valu_mix", "lds", "mfma")}
+    if hbm_frac is not None:
+        fr["hbm"] = hbm_frac
+    if not fr:
+        return None, {}
+    return max(fr, key=fr.get), fr
 
 
 def measured_traffic(kernel, batch):
@@ -338,19 +375,40 @@ def main():
         if traffic is not None:
             roofline["traffic"] = round(traffic)
             roofline["traffic_source"] = tsrc
-        # the pipe that actually binds this integer kernel: VALU issue (PMC instruction count per
-        # dispatch over the live-measured dispatch time)
+        # the pipe that actually binds the kernel: VALU issue against its own mix's roof (PMC
+        # instruction count per dispatch over the live-measured dispatch time), the LDS / TA /
+        # TD / MFMA busy fractions of profiles/pipes.json, HBM above
         vi, vpeak = measured_valu(dominant, B)
-        if vi is not None:
+        mr = mix_roof(dominant)
+        hbm = {k: roofline[k] for k in ("achieved", "peak", "unit", "frac", "traffic")}
+        if traffic is not None:
+            hbm["traffic_frac"] = round(traffic / avg_launch_s / 1e9 / HBM_PEAK_GBS, 5)
+        roofline["hbm"] = hbm
+        if vi is not None and mr:
             rate = vi / avg_launch_s
-            roofline["valu_issue"] = {"wave_instr_per_launch": round(vi), "achieved": rate,
-                                      "peak": vpeak, "unit": "wave-instr/s",
-                                      "frac": round(rate / vpeak, 4),
-                                      "sustained_peak": vpeak * VALU_SUSTAINED_FRAC_OF_NOMINAL,
-                                      "sustained_frac": round(
-                                          rate / (vpeak * VALU_SUSTAINED_FRAC_OF_NOMINAL), 4),
-                                      "source": "profiles/valu.json; sustained peak "
-                                                "tools/valu_rates.hip"}
+            roofline["valu_mix"] = {"wave_instr_per_launch": round(vi), "achieved": rate,
+                                    "peak": vpeak * mr, "unit": "wave-instr/s",
+                                    "frac": round(rate / (vpeak * mr), 4),
+                                    "nominal_peak": vpeak, "mix_roof_frac_of_nominal": mr,
+                                    "source": "SQ_INSTS_VALU: profiles/pipes.json; mix roof: "
+                                              "profiles/isa_mix.json (tools/isa_mix.py)"}
+        bp, fr = binding_pipe(dominant, B, hbm.get("traffic_frac", hbm["frac"]))
+        if bp:
+            if "valu_mix" in roofline:
+                fr["valu_mix"] = roofline["valu_mix"]["frac"]  # live time, not the PMC pass
+                bp = max(fr, key=fr.get)
+            roofline["pipes"] = {k: round(v, 4) for k, v in fr.items()}
+            roofline["bound"] = {"valu_mix": "valu"}.get(bp, bp)
+            if bp == "valu_mix":
+                v = roofline["valu_mix"]
+                roofline.update(achieved=round(v["achieved"] / 1e9, 2), peak=round(v["peak"] / 1e9, 2),
+                                unit="G wave-instr/s", frac=v["frac"])
+            elif bp != "hbm":
+                roofline.update(achieved=round(fr[bp], 4), peak=1.0, unit="busy fraction",
+                                frac=round(fr[bp], 4))
+            roofline["bound_source"] = ("largest of the live VALU mix fraction, the HBM "
+                                        "fraction of the measured traffic and the PMC busy "
+                                        "fractions of profiles/pipes.json (tools/pipes.py)")
         cpu = None
         if not args.no_cpu_baseline:
             dk, dd = ctx.keypoints(0)   # the left view of the batch's frame 0
@@ -386,11 +444,23 @@ def main():
                 ent["traffic_bytes_per_launch"] = round(tr)
                 ent["traffic_frac"] = round(tr / avg_s / 1e9 / HBM_PEAK_GBS, 4)
             vi, vpeak = measured_valu(n, B)
+            mr = mix_roof(n)
             if vi is not None:
                 ent["valu_wave_instr_per_launch"] = round(vi)
                 ent["valu_issue_frac"] = round(vi / avg_s / vpeak, 4)
-                ent["valu_sustained_frac"] = round(
-                    vi / avg_s / (vpeak * VALU_SUSTAINED_FRAC_OF_NOMINAL), 4)
+                if mr:
+                    ent["valu_mix_roof_frac_of_nominal"] = mr
+                    ent["valu_mix_frac"] = round(vi / avg_s / (vpeak * mr), 4)
+            bp, fr = binding_pipe(n, B, ent.get("traffic_frac", ent.get("hbm_frac")))
+            if bp:
+                if "valu_mix_frac" in ent:
+                    fr["valu_mix"] = ent["valu_mix_frac"]
+                    bp = max(fr, key=fr.get)
+                ent["pipes"] = {k: round(v, 4) for k, v in fr.items()}
+                ent["binding_pipe"] = bp
+            pe = measured_pipes(n, B)
+            if pe and pe.get("lds_conflict_per_instr") is not None:
+                ent["lds_conflict_per_instr"] = pe["lds_conflict_per_instr"]
             kernels[n] = ent
         if "octree" in kernels:
             kernels["octree"]["fast_candidates_per_image"] = round(fast_cand)

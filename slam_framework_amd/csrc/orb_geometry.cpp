@@ -229,6 +229,53 @@ int compute_geometry(const OrbParams& p, int cols, int rows, OrbGeom* g,
     g->pyr_band_lds = (lds + 15) & ~15;
     if (2 * g->pyr_band_lds > 64 * 1024) g->pyr_bands = 0;  // per-level launches instead
   }
+  {  // pyr_cascade_kernel: lane tasks, LDS layout and the step count (simulated here)
+    g->casc_waves = 0;
+    int tasks = 0;
+    for (int l = 1; l <= p.nlevels; l++) {
+      g->casc_task_base[l] = tasks;
+      if (l < p.nlevels) tasks += (g->lv[l].w + 7) / 8;
+    }
+    const int waves = (tasks + 63) / 64;
+    int off = 0;
+    for (int l = 0; l + 1 < p.nlevels; l++) {  // rows read by level l + 1: 16-byte chunks + over-read
+      g->casc_ring_stride[l] = ((g->lv[l].w + 15) & ~15) + 16;
+      g->casc_ring_off[l] = off;
+      off += (l == 0 ? kCascR0 : kCascSlots) * g->casc_ring_stride[l];
+    }
+    g->casc_ry_off = off;
+    if (p.nlevels > 1)
+      off += 8 * (g->lv[p.nlevels - 1].ry_base + g->lv[p.nlevels - 1].h - g->lv[1].ry_base);
+    g->casc_p_off = off;
+    off += 2 * kMaxLevels * 4;
+    g->casc_lds = off;
+    // the schedule: level l's next source row ns[l] / next output row nd[l]; level l consumes at
+    // step t every row level l - 1 had emitted by step t - 1 (level 1: level-0 rows 0 .. t)
+    bool ok = p.nlevels > 1 && waves + 1 <= 16 && off <= 64 * 1024 &&
+              ((g->lv[0].w + 15) >> 4) <= 128;
+    int ns[kMaxLevels] = {0}, nd[kMaxLevels] = {0}, prev[kMaxLevels] = {0};
+    int t = 0;
+    for (; ok; t++) {
+      bool done = true;
+      for (int l = 1; l < p.nlevels; l++) {
+        const LevelGeom& L = g->lv[l];
+        const int avail = l == 1 ? std::min(t + 1, g->lv[0].h) : prev[l - 1];
+        const int before = nd[l];
+        for (; ns[l] < avail; ns[l]++)
+          while (nd[l] < L.h && (*ry)[L.ry_base + nd[l]].y1 == ns[l]) nd[l]++;
+        // two rows per step at most: a level's consumer reads the rows of the step before while
+        // it writes the next two (kCascSlots = 4)
+        if (nd[l] - before > 2) ok = false;
+        done = done && nd[l] == L.h;
+      }
+      for (int l = 1; l < p.nlevels; l++) prev[l] = nd[l];
+      if (done || t > 4 * g->lv[0].h) break;
+    }
+    if (ok && t <= 4 * g->lv[0].h) {
+      g->casc_waves = waves;
+      g->casc_steps = t + 1;
+    }
+  }
   gauss_kernel_int(g->gauss);
   {  // orient_desc packs taps into bytes and row sums into u16 (sum of taps <= 257)
     int sum = 0;

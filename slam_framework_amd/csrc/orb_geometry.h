@@ -21,6 +21,7 @@ constexpr int kMaxLevels = 12;
 #endif
 constexpr int kCellGroup = FAST_CELLS_PER_WAVE;
 constexpr int kPyrMaxBands = 32;
+constexpr int kCascR0 = 8, kCascDepth = 6, kCascSlots = 4;  // pyr_cascade_kernel (OrbGeom)
 constexpr int kEdgeThreshold = 19;
 constexpr int kMinBorder = kEdgeThreshold - 3;  // minBorderX/Y (:712)
 constexpr int kPatchSize = 31;
@@ -108,6 +109,18 @@ struct OrbGeom {
   int pyr_ring_slots;  // pyr_ring_kernel: 1 KiB LDS slots per wave (max over levels; 0: unusable)
   int pyr_band_lds;  // bytes of one of its two LDS row buffers (the largest band level)
   int16_t pyr_band[kPyrMaxBands][kMaxLevels][2];
+  // pyr_cascade_kernel (batches): one work-group per image streams level 0 top to bottom
+  // through every level at once; per barrier step level 1 consumes one level-0 row and level l
+  // the rows level l - 1 emitted in the step before. casc_waves compute waves (lane task k of
+  // level l: columns 8 (k - casc_task_base[l]) .. + 7) + one loader wave; casc_steps steps;
+  // LDS: level-0 rows (kCascR0 slots, loaded kCascDepth rows ahead by buffer-to-LDS loads), the
+  // rows of levels 1 .. nlevels - 2 (kCascSlots slots), the packed row table of levels >= 1
+  // (uint2 {y1 | (y0 == y1) << 16, b0 | b1 << 16} from lv[1].ry_base on), the per-level produced
+  // row counters (int [2][kMaxLevels]). casc_waves == 0: not usable for this geometry.
+  int casc_waves, casc_steps, casc_lds;
+  int casc_task_base[kMaxLevels + 1];
+  int casc_ring_off[kMaxLevels], casc_ring_stride[kMaxLevels];
+  int casc_ry_off, casc_p_off;
   // orient_desc per-lane constants (host-built from gauss / umax, read once per wave):
   // od_band[tj][lane]: the v_mfma_i32_16x16x64_i8 B operand of tile column tj -- byte b of lane
   // (n = lane & 15, g = lane >> 4) is gauss[16 g + b - 16 tj - n] inside the 7 taps, else 0;

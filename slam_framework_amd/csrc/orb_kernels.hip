@@ -321,6 +321,176 @@ __global__ __launch_bounds__(64 * kPyrBandWaves) void pyr_band_kernel(
   }
 }
 
+// Batches: the whole pyramid of one image in one work-group, streamed top to bottom (a cascade
+// of line buffers): every barrier step level 1 consumes the next level-0 row and each level
+// l >= 2 the rows level l - 1 emitted in the step before, so all levels advance together and a
+// level's rows go from LDS to the next level without a global round trip. One launch instead of
+// nlevels - 1 dependent ones; level 0 is read once and every level written once (the section
+// 8(d) bytes), and the small levels no longer pay a launch and a strip chain each.
+// Lanes: task k of level l owns output columns x0 = 8 (k - casc_task_base[l]) .. x0 + 7 as two
+// groups of 4 (the pyr_strip column math: an 8-byte window from the group's first source byte,
+// v_perm + v_dot2 per column); it keeps the previous / current source row's horizontal results
+// in registers (hp, hc) and emits output row y when its lower source row y1 arrives -- from
+// (hp, hc), or (hc, hc) where the row table clamps y0 == y1. Every lane of a level takes the
+// same steps; the level's first lane publishes the rows emitted so far (P[t & 1][l]).
+// The loader wave streams level-0 rows into kCascR0 LDS slots kCascDepth rows ahead (16-byte
+// buffer-to-LDS loads; only it issues vector-memory loads, so its vmcnt counts rows).
+__global__ __launch_bounds__(1024) void pyr_cascade_kernel(ImageBatch b, const OrbGeom* __restrict__ g,
+                                                           const ResizeX* __restrict__ rxt,
+                                                           const ResizeY* __restrict__ ryt) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t s_c[];
+  const int img = blockIdx.x, tid = threadIdx.x, wid = tid >> 6, lane = tid & 63;
+  const int nl = g->nlevels, nw = g->casc_waves, T = g->casc_steps;
+  const int H0 = g->lv[0].h;
+  const int ry0 = g->lv[1].ry_base, nry = g->lv[nl - 1].ry_base + g->lv[nl - 1].h - ry0;
+  uint2* s_ry = reinterpret_cast<uint2*>(s_c + g->casc_ry_off);
+  int* s_p = reinterpret_cast<int*>(s_c + g->casc_p_off);
+  for (int i = tid; i < nry; i += blockDim.x) {
+    const ResizeY e = ryt[ry0 + i];
+    s_ry[i] = make_uint2((uint32_t)e.y1 | (uint32_t)(e.y0 == e.y1) << 16,
+                         (uint32_t)(uint16_t)e.b0 | (uint32_t)(uint16_t)e.b1 << 16);
+  }
+  if (tid < 2 * kMaxLevels) s_p[tid] = 0;
+  const bool loader = wid == nw;
+  // ---- the loader: level-0 row r -> slot r % kCascR0, 16-byte chunks, ipr instructions per row
+  const int chunks0 = (g->lv[0].w + 15) >> 4, ipr = (chunks0 + 63) >> 6;
+  uint8_t* ring0 = s_c + g->casc_ring_off[0];
+  const int stride0 = g->casc_ring_stride[0];
+  const int pitch0 = __builtin_amdgcn_readfirstlane(b.in_pitch);
+  const __amdgpu_buffer_rsrc_t rsrc0 = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)uniform_ptr(batch_image(b, img)), 0, __builtin_amdgcn_readfirstlane(pitch0 * H0),
+      0x00020000);
+  auto issue = [&](int r) {
+    uint8_t* dst = ring0 + (r % kCascR0) * stride0;
+    for (int k = 0; k < ipr; k++)
+      if (64 * k + lane < chunks0)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(
+            rsrc0, (__attribute__((address_space(3))) void*)(dst + 1024 * k), 16,
+            (uint32_t)(r * pitch0 + 16 * (64 * k + lane)), 0, 0, 0);
+  };
+  // wait until row r has landed, rows up to min(r + kCascDepth - 1, H0 - 1) issued
+  auto wait_row = [&](int r) {
+    if (r + kCascDepth - 1 < H0) {
+      if (ipr == 1) __builtin_amdgcn_s_waitcnt(0x0F70 | (kCascDepth - 1));
+      else __builtin_amdgcn_s_waitcnt(0x0F70 | (2 * (kCascDepth - 1)));
+    } else {
+      __builtin_amdgcn_s_waitcnt(0x0F70);
+    }
+  };
+  if (loader) {
+    for (int r = 0; r < kCascDepth && r < H0; r++) issue(r);
+    wait_row(0);
+  }
+  // ---- a compute lane's level, columns and constants
+  const int task = wid * 64 + lane;
+  int lvl = 0;
+  if (!loader)
+    for (int l = 1; l < nl; l++)
+      if (task >= g->casc_task_base[l] && task < g->casc_task_base[l + 1]) lvl = l;
+  const LevelGeom& D = g->lv[lvl > 0 ? lvl : 1];
+  const int x0 = 8 * (task - g->casc_task_base[lvl > 0 ? lvl : 1]);
+  const int Hl = D.h, Wl = D.w;
+  uint32_t sel[8], A[8];
+  int qo[2], sh[2];
+#pragma unroll
+  for (int gi = 0; gi < 2; gi++) {
+    int s0 = 0;
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      const int dx = min(x0 + 4 * gi + k, Wl - 1);
+      const ResizeX e = rxt[D.rx_base + dx];
+      if (k == 0) s0 = e.sx;
+      const uint32_t bk = (uint32_t)min(e.sx - s0, 6);
+      sel[4 * gi + k] = bk | 0x0c00u | (bk + 1) << 16 | 0x0c000000u;
+      A[4 * gi + k] = dx < D.xmax ? ((uint32_t)(16 * e.a0) | (uint32_t)(16 * e.a1) << 16) : 32768u;
+    }
+    qo[gi] = 4 * (s0 >> 2);
+    sh[gi] = s0 & 3;
+  }
+  // source ring (level lvl - 1) and destination ring (level lvl; none for the last level)
+  const int sl = lvl > 0 ? lvl - 1 : 0;
+  const uint8_t* sring = s_c + g->casc_ring_off[sl];
+  const int sstride = g->casc_ring_stride[sl], smod = sl == 0 ? kCascR0 : kCascSlots;
+  const bool to_lds = lvl > 0 && lvl + 1 < nl;
+  uint8_t* dring = s_c + g->casc_ring_off[to_lds ? lvl : 0];
+  const int dstride = g->casc_ring_stride[to_lds ? lvl : 0];
+  uint8_t* dst = b.pyr + (int64_t)img * g->pyr_bytes + D.offset;
+  const int dpitch = D.pitch;
+  const uint2* rytab = s_ry + (D.ry_base - ry0);
+  const bool leader = lvl > 0 && task == g->casc_task_base[lvl];
+  const bool full = x0 + 8 <= Wl;
+  __syncthreads();  // row tables, counters and level-0 row 0 in LDS
+  int ns = 0, nd = 0;
+  uint2 cur = rytab[0];
+  uint32_t hp[8] = {0, 0, 0, 0, 0, 0, 0, 0}, hc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  for (int t = 0; t < T; t++) {
+    if (loader) {
+      if (t + kCascDepth < H0) issue(t + kCascDepth);
+    } else if (lvl > 0) {
+      const int avail = lvl == 1 ? min(t + 1, H0) : s_p[((t + 1) & 1) * kMaxLevels + lvl - 1];
+      while (ns < avail) {
+        const uint8_t* row = sring + (ns & (smod - 1)) * sstride;
+#pragma unroll
+        for (int gi = 0; gi < 2; gi++) {
+          const uint32_t* rw = reinterpret_cast<const uint32_t*>(row + qo[gi]);
+          const uint32_t d0 = rw[0], d1 = rw[1], d2 = rw[2];
+          const uint32_t W0 = __builtin_amdgcn_alignbyte(d1, d0, sh[gi]);
+          const uint32_t W1 = __builtin_amdgcn_alignbyte(d2, d1, sh[gi]);
+#pragma unroll
+          for (int k = 0; k < 4; k++) {
+            hp[4 * gi + k] = hc[4 * gi + k];
+            hc[4 * gi + k] =
+                dot2u(__builtin_amdgcn_perm(W1, W0, sel[4 * gi + k]), A[4 * gi + k], 0u) & 0xffff00u;
+          }
+        }
+        while (nd < Hl && (int)(cur.x & 0xffffu) == ns) {
+          const uint32_t b0 = (cur.y & 0xffffu) << 8, b1 = (cur.y >> 16) << 8;
+          if (cur.x >> 16) {  // y0 == y1 (the last rows): both source rows are this one
+#pragma unroll
+            for (int k = 0; k < 8; k++) hp[k] = hc[k];
+          }
+          uint32_t pk[2];
+#pragma unroll
+          for (int gi = 0; gi < 2; gi++) {
+            uint32_t tt[4];
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+              const uint32_t r0 = hp[4 * gi + k];
+              uint32_t m0, m1;
+              asm("v_mul_hi_u32_u24 %0, %1, %2" : "=v"(m0) : "v"(b0), "v"(r0));
+              asm("v_mul_hi_u32_u24 %0, %1, %2" : "=v"(m1) : "v"(b1), "v"(hc[4 * gi + k]));
+              tt[k] = m0 + m1 + 2u;
+            }
+            typedef unsigned short u16x2_t __attribute__((ext_vector_type(2)));
+            const u16x2_t two = {2, 2};
+            const uint32_t p01 = __builtin_bit_cast(uint32_t, __builtin_bit_cast(u16x2_t, tt[0] | tt[1] << 16) >> two);
+            const uint32_t p23 = __builtin_bit_cast(uint32_t, __builtin_bit_cast(u16x2_t, tt[2] | tt[3] << 16) >> two);
+            pk[gi] = __builtin_amdgcn_perm(p23, p01, 0x06040200u);
+          }
+          if (to_lds)
+            *reinterpret_cast<uint2*>(dring + ((uint32_t)nd % kCascSlots) * dstride + x0) =
+                make_uint2(pk[0], pk[1]);
+          uint8_t* drow = dst + (uint32_t)(nd * dpitch);
+          if (full) {
+            *reinterpret_cast<uint2*>(drow + x0) = make_uint2(pk[0], pk[1]);
+          } else {
+            for (int k = 0; x0 + k < Wl; k++) drow[x0 + k] = (uint8_t)(pk[k >> 2] >> (8 * (k & 3)));
+          }
+          nd++;
+          cur = rytab[min(nd, Hl - 1)];
+        }
+        ns++;
+      }
+      if (leader) s_p[(t & 1) * kMaxLevels + lvl] = nd;
+    }
+    if (loader) wait_row(t + 1);
+    // a work-group barrier that orders LDS only: __syncthreads() (or an LDS-scope fence, as the
+    // loader's buffer-to-LDS loads are LDS writes counted by vmcnt) would make every wave wait
+    // for its global stores of the step (vmcnt(0)) -- an HBM write latency per step
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+  }
+}
+
 // ---------------------------------------------------------------------------------------
 __device__ __forceinline__ int reflect101(int i, int n) {  // cv::BORDER_REFLECT_101, |overshoot| < n
   if (i < 0) i = -i;
@@ -2968,7 +3138,15 @@ void launch_extract(const ImageBatch& b, const OrbGeomDev& gd, int n_images, hip
   // SLAMGPU_PYR_RING: bit l selects the LDS-staged kernel for level l (A/B)
   const bool ring_ok = glds && g.pyr_ring_slots > 0 && g.pyr_ring_slots <= 8;
   // small launches: level 1 over the chip, then levels 2+ in one launch of row bands
-  const int l_end = (short_strips && g.pyr_bands > 0) ? 2 : g.nlevels;
+  // SLAMGPU_PYR_CASCADE=1: batches take the whole pyramid in one cascade launch where the
+  // geometry allows it. Not the default: it is 0.57 ms standalone against the per-level
+  // launches' 0.69, but its lanes idle in the steps their level emits nothing (186M VALU
+  // wave-instructions against 134M) and it holds every CU for its whole run, so level 0's FAST
+  // beside it stretches 0.68 -> 0.98 ms and the step gets slower, 2.45 -> 2.57 ms
+  // (profiles/r8c_pyr_cascade_ab.log). Read per launch, so that tests can exercise both paths.
+  const char* cenv = std::getenv("SLAMGPU_PYR_CASCADE");
+  const bool cascade = cenv && std::atoi(cenv) != 0 && glds && !short_strips && g.casc_waves > 0;
+  const int l_end = cascade ? 1 : (short_strips && g.pyr_bands > 0) ? 2 : g.nlevels;
   for (int l = 1; l < l_end; l++) {
     const bool ring = ring_ok && !short_strips && ((ring_mode >> l) & 1);
     const int strip = short_strips ? kPyrShortStrip : ring ? kPyrRingStrip : kPyrStrip;
@@ -2992,7 +3170,10 @@ void launch_extract(const ImageBatch& b, const OrbGeomDev& gd, int n_images, hip
                      b, gd.dev, l, gd.rx, gd.ry);
     }
   }
-  if (l_end < g.nlevels)
+  if (cascade)
+    SLAMGPU_LAUNCH("pyr_down", st, pyr_cascade_kernel, dim3(n_images), dim3(64 * (g.casc_waves + 1)),
+                   (size_t)g.casc_lds, st, b, gd.dev, gd.rx, gd.ry);
+  else if (l_end < g.nlevels)
     SLAMGPU_LAUNCH("pyr_down", st, pyr_band_kernel, dim3(g.pyr_bands, n_images),
                    dim3(64 * kPyrBandWaves), 2 * (size_t)g.pyr_band_lds, st, b, gd.dev, gd.rx,
                    gd.ry);

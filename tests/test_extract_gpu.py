@@ -124,8 +124,9 @@ def test_batch_extract_other_sizes(oracle, gpu_lib, cols, rows, nf):
                                               (0, (2000, 1.2, 10, 20, 7))])
 def test_batch_extract_pitch_and_parameters(oracle, gpu_lib, pitch_pad, params):
     """Batches off the LDS-staged paths (a caller pitch that is not a multiple of 16: the
-    register-staged pyramid, FAST and window loads) and with other scale factors / level counts
-    (the ring's row segments grow with the scale factor): 9 frames, four images vs the oracle."""
+    per-level register-staged pyramid, FAST and window loads) and with other scale factors /
+    level counts (the cascade pyramid's lane tasks, row rings and step schedule follow the
+    geometry): 9 frames, four images vs the oracle, every pyramid level included."""
     import torch
     nf, sf, nl, ini, mn = params
     cols, rows, B = S.KITTI_COLS, S.KITTI_ROWS, 9
@@ -143,7 +144,45 @@ def test_batch_extract_pitch_and_parameters(oracle, gpu_lib, pitch_pad, params):
     ctx.sync()
     for f, side in ((0, 0), (2, 1), (6, 0), (8, 1)):
         src = np.ascontiguousarray((L if side == 0 else R)[f, :, :cols])
-        kr, dr = oracle.extract(t, src)[:2]
+        kr, dr, pyr = oracle.extract(t, src, with_pyramid=True)
+        for l in range(1, nl):
+            np.testing.assert_array_equal(ctx.pyramid_level(2 * f + side, l), pyr.level(l),
+                                          err_msg=f"image {2 * f + side} level {l}")
+        kg, dg = ctx.keypoints(2 * f + side)
+        _compare_kps(kg, kr)
+        np.testing.assert_array_equal(dg, dr)
+
+
+@pytest.mark.parametrize("cols,rows,params", [(1241, 376, (2000, 1.2, 8, 20, 7)),
+                                              (752, 480, (1200, 1.2, 8, 20, 7)),
+                                              (1241, 376, (1500, 1.3, 6, 12, 5)),
+                                              (1241, 376, (2000, 1.2, 10, 20, 7))])
+def test_batch_extract_cascade_pyramid(oracle, gpu_lib, monkeypatch, cols, rows, params):
+    """The opt-in one-launch pyramid (pyr_cascade_kernel, SLAMGPU_PYR_CASCADE=1: one work-group
+    streams an image through every level; lane tasks, row rings and the step schedule from the
+    geometry): a 9-frame batch, every level of four images and their keypoints vs the oracle."""
+    import torch
+    monkeypatch.setenv("SLAMGPU_PYR_CASCADE", "1")
+    nf, sf, nl, ini, mn = params
+    B, pitch = 9, (cols + 63) // 64 * 64
+    t = oracle.tables(nfeatures=nf, scale_factor=sf, nlevels=nl, ini_th=ini, min_th=mn)
+    ctx = gpu_lib.Context(cols, rows, nf, sf, nl, ini, mn, max_frames=B)
+    L = np.zeros((B, rows, pitch), np.uint8)
+    R = np.zeros((B, rows, pitch), np.uint8)
+    for f in range(B):
+        L[f, :, :cols], R[f, :, :cols] = S.stereo_pair(5000 + f, cols, rows)
+    dev = torch.device("cuda", 0)
+    d_l, d_r = torch.from_numpy(L).to(dev), torch.from_numpy(R).to(dev)
+    torch.cuda.synchronize()
+    cam = (0.8 * cols, 0.8 * cols, cols / 2, rows / 2, 0.4 * cols)
+    ctx.frontend_device(d_l, d_r, rows * pitch, pitch, B, cam)
+    ctx.sync()
+    for f, side in ((0, 0), (3, 1), (7, 0), (8, 1)):
+        src = np.ascontiguousarray((L if side == 0 else R)[f, :, :cols])
+        kr, dr, pyr = oracle.extract(t, src, with_pyramid=True)
+        for l in range(1, nl):
+            np.testing.assert_array_equal(ctx.pyramid_level(2 * f + side, l), pyr.level(l),
+                                          err_msg=f"image {2 * f + side} level {l}")
         kg, dg = ctx.keypoints(2 * f + side)
         _compare_kps(kg, kr)
         np.testing.assert_array_equal(dg, dr)

@@ -7,8 +7,8 @@
 #   bench           python3 bench.py (default line) -> bench.json
 #   quick           python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-optimizer
 #   stats           rocprofv3 --kernel-trace --stats of the default bench + the timed-region split
-#   valu            one --pmc pass: SQ_INSTS_VALU/SALU/LDS, SQ_WAVES per dispatch
 #   traffic         FETCH_SIZE / WRITE_SIZE passes (tools/pmc_traffic.sh)
+#   pipes           two --pmc passes of pipe counters (tools/pmc_pipes.sh -> tools/pipes.py)
 #   pmc=GROUPFILE   one --pmc pass with the counters listed in GROUPFILE (tools/pmc_groups/)
 #   ab=LIB,LIB,...  tools/ab.py A/B of library builds (bench --steps 10), run twice
 #   py=SCRIPT[:ARGS] python3 SCRIPT ARGS (ARGS ':'-separated)
@@ -47,9 +47,9 @@ for s in "$@"; do
       f=$(ls $O/stats/*/run_kernel_trace.csv $O/stats/run_kernel_trace.csv 2>/dev/null | head -1)
       [ -n "$f" ] && python3 tools/stats_timed.py $f > $O/timed_kernel_stats.csv
       echo "stats ok" ;;
-    valu)
-      OUT=$O/valu timeout -k 10 400 bash tools/pmc_valu.sh > $O/valu.log 2>&1 || { echo "valu rc=$?"; exit 1; }
-      echo "valu ok" ;;
+    pipes)
+      OUT=$O/pipes timeout -k 10 560 bash tools/pmc_pipes.sh > $O/pipes.log 2>&1 || { echo "pipes rc=$?"; cat $O/pipes.log; exit 1; }
+      echo "pipes ok" ;;
     traffic)
       OUT=$O/traffic timeout -k 10 700 bash tools/pmc_traffic.sh > $O/traffic.log 2>&1 || { echo "traffic rc=$?"; exit 1; }
       echo "traffic ok" ;;
