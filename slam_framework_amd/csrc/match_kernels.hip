@@ -868,14 +868,24 @@ __device__ __forceinline__ uint64_t key64(K k) {
 
 // G lanes per query (the group of `lane`): 64 for the resolution pass's rescans, 16 for
 // search_cand (a window holds a handful of keypoints: four queries per wave keep the lanes busy)
+// float -> int of a cell coordinate with its argument held in range first: a float-to-int
+// conversion out of int's range (or of NaN) is undefined, so no coordinate reaches one
+__device__ __forceinline__ int cell_floor(float v) { return (int)floorf(fminf(fmaxf(v, -1e6f), 1e6f)); }
+__device__ __forceinline__ int cell_ceil(float v) { return (int)ceilf(fminf(fmaxf(v, -1e6f), 1e6f)); }
+
+// skip: the group has no query (or its context failed): it scans nothing -- no cell bound is
+// derived from its coordinates -- but still takes part in the group's shuffles and the merge
 template <typename K, int G = 64>
 __device__ int scan_query_k(const ScanCtx& c, const Camera& cam, const FrameView& F,
-                            const uint32_t* claimed, uint64_t* top, int lane) {
+                            const uint32_t* claimed, uint64_t* top, int lane, bool skip = false) {
   const int gl = lane & (G - 1), gb = lane & ~(G - 1);
-  const int nMinCellX = max(0, (int)floorf((c.x - cam.min_x - c.r) / cam.cell_w));
-  const int nMaxCellX = min(kGridCols - 1, (int)ceilf((c.x - cam.min_x + c.r) / cam.cell_w));
-  const int nMinCellY = max(0, (int)floorf((c.y - cam.min_y - c.r) / cam.cell_h));
-  const int nMaxCellY = min(kGridRows - 1, (int)ceilf((c.y - cam.min_y + c.r) / cam.cell_h));
+  int nMinCellX = 0, nMaxCellX = -1, nMinCellY = 0, nMaxCellY = -1;  // empty window
+  if (!skip) {
+    nMinCellX = max(0, cell_floor((c.x - cam.min_x - c.r) / cam.cell_w));
+    nMaxCellX = min(kGridCols - 1, cell_ceil((c.x - cam.min_x + c.r) / cam.cell_w));
+    nMinCellY = max(0, cell_floor((c.y - cam.min_y - c.r) / cam.cell_h));
+    nMaxCellY = min(kGridRows - 1, cell_ceil((c.y - cam.min_y + c.r) / cam.cell_h));
+  }
   constexpr K kNone = (K)~(K)0;
   K t[kTopK];
 #pragma unroll
@@ -976,9 +986,9 @@ __device__ int scan_query_k(const ScanCtx& c, const Camera& cam, const FrameView
 template <int G = 64>
 __device__ __forceinline__ int scan_query(const ScanCtx& c, const Camera& cam, const FrameView& F,
                                           const uint32_t* claimed, uint64_t* top, int lane,
-                                          int kp_cap) {
-  if (kp_cap <= 2048) return scan_query_k<uint32_t, G>(c, cam, F, claimed, top, lane);
-  return scan_query_k<uint64_t, G>(c, cam, F, claimed, top, lane);
+                                          int kp_cap, bool skip = false) {
+  if (kp_cap <= 2048) return scan_query_k<uint32_t, G>(c, cam, F, claimed, top, lane, skip);
+  return scan_query_k<uint64_t, G>(c, cam, F, claimed, top, lane, skip);
 }
 
 __device__ __forceinline__ int key_idx(uint64_t k) { return (int)(k & 0xfff); }
@@ -1077,12 +1087,9 @@ __global__ __launch_bounds__(256) void search_cand_kernel(
     ok = mps_ctx(queries[q], th, g, &c);
   }
   ok = ok && live;
-  if (!ok) {  // a window left of the grid: the group scans nothing but takes part in the merge
-    c.x = c.y = -1e30f;
-    c.r = 0.0f;
-  }
   uint64_t top[kTopK];
-  const int n = scan_query<kSearchG>(c, cam, F, nullptr, top, lane, g->kp_cap);
+  // a group without a query scans nothing but takes part in the merge
+  const int n = scan_query<kSearchG>(c, cam, F, nullptr, top, lane, g->kp_cap, !ok);
   if (live && gl < kTopK) {
     uint64_t v = top[0];
 #pragma unroll

@@ -85,6 +85,8 @@ int compute_geometry(const OrbParams& p, int cols, int rows, OrbGeom* g,
   OrbTables t;
   compute_tables(p, &t);
   std::memset(g, 0, sizeof(*g));
+  g->pyr_ring_strip = PYR_RING_STRIP;
+  g->cell_group = kCellGroup;
   g->nlevels = p.nlevels;
   g->cols = cols;
   g->rows = rows;

@@ -20,6 +20,8 @@ constexpr int kMaxLevels = 12;
 #define FAST_CELLS_PER_WAVE 8
 #endif
 constexpr int kCellGroup = FAST_CELLS_PER_WAVE;
+static_assert(kCellGroup > 0 && (kCellGroup & (kCellGroup - 1)) == 0,
+              "kCellGroup masks (i & ~(kCellGroup - 1)) need a power of two");
 constexpr int kPyrMaxBands = 32;
 constexpr int kCascR0 = 8, kCascDepth = 6, kCascSlots = 4;  // pyr_cascade_kernel (OrbGeom)
 constexpr int kEdgeThreshold = 19;
@@ -78,6 +80,10 @@ struct LevelGeom {
 };
 
 struct OrbGeom {
+  // the build constants this geometry was laid out with (orb_geometry.cpp's translation unit):
+  // the kernels' own must agree (extract_build_matches), or a -D flag passed to one source only
+  // would size LDS slots / key groups for another strip or group than the kernels use
+  int pyr_ring_strip, cell_group;
   int nlevels, cols, rows;
   int nfeatures, ini_th, min_th;
   int cells_per_image;

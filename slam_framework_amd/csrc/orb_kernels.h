@@ -72,5 +72,8 @@ void launch_extract(const ImageBatch& b, const OrbGeomDev& g, int n_images, hipS
 // each kernel's static LDS (octree_img_kernel, octree_lvl_kernel); compute_geometry sizes their
 // key capacities within these.
 hipError_t octree_lds_limits(int device, int* img_bytes, int* lvl_bytes);
+// The geometry was laid out with the kernels' own build constants (ring strip, FAST key group):
+// false when orb_geometry.cpp and orb_kernels.hip were built with different -D flags.
+bool extract_build_matches(const OrbGeom& g);
 
 }  // namespace slamgpu

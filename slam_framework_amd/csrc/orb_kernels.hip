@@ -1368,12 +1368,13 @@ __device__ __forceinline__ void octree_global(
   }
 }
 
-// The fallback after octree_img_kernel: a small grid scans the (image, level) results for the
-// levels octree_img left at -1 (every thread checks one entry per sweep, one ballot per wave)
-// and redoes only those, one at a time per work-group. A batch whose levels all fit costs one
-// load per thread -- not a work-group (and its 41 KB of LDS) per (level, image) queued behind
-// the other stream's kernels on the batch's critical path (0.1-0.5 ms in the round-4 traces).
-constexpr int kOctFbMaxGroups = 64;
+// The fallback after octree_img_kernel: a grid of G <= kOctFbMaxGroups work-groups redoes the
+// (image, level) entries octree_img left at -1; group b owns the entries e = b (mod G), reads
+// their results at once (one load per thread) and redoes its -1 entries one after another.
+// However many levels overflow -- all of them in a batch of busy textures -- they spread over
+// the whole grid (at most total / G per group), and no group reads an entry another group
+// writes. A batch whose levels all fit costs each group one load per thread.
+constexpr int kOctFbMaxGroups = 256;
 __global__ __launch_bounds__(kOctThreads) void octree_kernel(
     const OrbGeom* __restrict__ g, int n_images, const uint32_t* __restrict__ cell_keys,
     const int* __restrict__ cell_count, uint32_t* __restrict__ key_scratch,
@@ -1381,23 +1382,30 @@ __global__ __launch_bounds__(kOctThreads) void octree_kernel(
     int* __restrict__ oct_count, uint32_t* __restrict__ err) {
   __shared__ OctShared S;
   __shared__ int s_todo[kOctThreads];
-  __shared__ int s_ntodo;
-  const int tid = threadIdx.x, nlev = g->nlevels;
+  __shared__ int s_wcnt[kOctWaves];
+  const int tid = threadIdx.x, wid = tid >> 6, lane = tid & 63, nlev = g->nlevels;
   const int total = n_images * nlev;  // entry e = img * nlevels + level (oct_count's layout)
-  for (int e0 = blockIdx.x * kOctThreads; e0 < total; e0 += gridDim.x * kOctThreads) {
-    if (tid == 0) s_ntodo = 0;
+  const int G = gridDim.x;
+  for (int j0 = 0; (int)blockIdx.x + j0 * G < total; j0 += kOctThreads) {
+    const int e = (int)blockIdx.x + (j0 + tid) * G;
+    const bool redo = e < total && oct_count[e] == -1;
+    const uint64_t m = __ballot(redo);
+    if (lane == 0) s_wcnt[wid] = __popcll(m);
     __syncthreads();
-    const int e = e0 + tid;
-    if (e < total && oct_count[e] == -1) s_todo[atomicAdd(&s_ntodo, 1)] = e;
+    int off = 0, nt = 0;
+    for (int w = 0; w < kOctWaves; w++) {
+      if (w < wid) off += s_wcnt[w];
+      nt += s_wcnt[w];
+    }
+    if (redo) s_todo[off + lanes_below(m)] = e;
     __syncthreads();
-    const int nt = s_ntodo;
     for (int i = 0; i < nt; i++) {  // octree_global re-initialises everything it uses in S
       const int ei = s_todo[i];
       octree_global<kOctThreads>(S, ei % nlev, ei / nlev, g, cell_keys, cell_count, key_scratch,
                                  node_scratch, oct_keys, oct_count, err);
       __syncthreads();
     }
-    __syncthreads();  // every thread has read s_ntodo before the next sweep resets it
+    __syncthreads();  // s_wcnt / s_todo read by every thread before the next sweep writes them
   }
 }
 
@@ -3217,8 +3225,7 @@ void launch_extract(const ImageBatch& b, const OrbGeomDev& gd, int n_images, hip
                    (size_t)g.oct_lds_bytes, st, gd.dev, gd.ws.cell_keys, gd.ws.cell_count,
                    gd.ws.key_scratch, gd.ws.oct_keys, gd.ws.oct_count, gd.ws.err);
   if (!lvl) {
-    const int groups = std::min((g.nlevels * n_images + kOctThreads - 1) / kOctThreads,
-                                kOctFbMaxGroups);
+    const int groups = std::min(g.nlevels * n_images, kOctFbMaxGroups);
     SLAMGPU_LAUNCH("octree_global", st, octree_kernel, dim3(groups), dim3(kOctThreads), 0, st,
                    gd.dev, n_images, gd.ws.cell_keys, gd.ws.cell_count, gd.ws.key_scratch,
                    gd.ws.node_scratch, gd.ws.oct_keys, gd.ws.oct_count, gd.ws.err);
@@ -3234,6 +3241,10 @@ void launch_extract(const ImageBatch& b, const OrbGeomDev& gd, int n_images, hip
                    0, st, b, gd.dev, gd.ws.oct_keys, gd.ws.oct_count, gd.out.kps, gd.out.desc,
                    gd.out.nkps);
   }
+}
+
+bool extract_build_matches(const OrbGeom& g) {
+  return g.pyr_ring_strip == kPyrRingStrip && g.cell_group == kCellsPerWave;
 }
 
 hipError_t octree_lds_limits(int device, int* img_bytes, int* lvl_bytes) {

@@ -269,6 +269,12 @@ int slamgpu_create(int device, const slamgpu_orb_params* p, int cols, int rows, 
                        rows, p->nlevels, (double)p->scale_factor,
                        why[std::min(std::max(-gr, 0), 7)]);
   }
+  if (!extract_build_matches(c->geom)) {
+    delete c;
+    return create_fail(SLAMGPU_EINVAL,
+                       "slamgpu_create: orb_geometry.cpp and orb_kernels.hip were built with "
+                       "different PYR_RING_STRIP / FAST_CELLS_PER_WAVE");
+  }
   compute_tables(c->params, &c->tables);
   if (c->geom.kp_cap > 4096) {  // matcher keys carry a 12-bit keypoint index
     const int kpc = c->geom.kp_cap;
