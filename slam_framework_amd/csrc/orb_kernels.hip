@@ -3155,12 +3155,19 @@ void launch_extract(const ImageBatch& b, const OrbGeomDev& gd, int n_images, hip
   const char* cenv = std::getenv("SLAMGPU_PYR_CASCADE");
   const bool cascade = cenv && std::atoi(cenv) != 0 && glds && !short_strips && g.casc_waves > 0;
   const int l_end = cascade ? 1 : (short_strips && g.pyr_bands > 0) ? 2 : g.nlevels;
+  // SLAMGPU_PYR_SHORT_FROM=l: batches take short strips (more waves, shorter row chains) from
+  // level l on (A/B)
+  static const int short_from = [] {
+    const char* e = std::getenv("SLAMGPU_PYR_SHORT_FROM");
+    return e ? std::atoi(e) : kMaxLevels;
+  }();
   for (int l = 1; l < l_end; l++) {
-    const bool ring = ring_ok && !short_strips && ((ring_mode >> l) & 1);
-    const int strip = short_strips ? kPyrShortStrip : ring ? kPyrRingStrip : kPyrStrip;
+    const bool shortl = short_strips || l >= short_from;
+    const bool ring = ring_ok && !shortl && ((ring_mode >> l) & 1);
+    const int strip = shortl ? kPyrShortStrip : ring ? kPyrRingStrip : kPyrStrip;
     const int tiles = ((g.lv[l].w + 255) >> 8) * ((g.lv[l].h + 4 * strip - 1) / (4 * strip));
     const dim3 grid(tiles, n_images);
-    if (short_strips) {
+    if (shortl) {
       if (l > 1 || in_aligned)
         SLAMGPU_LAUNCH("pyr_down", st, (pyr_down_kernel<true, kPyrShortStrip>), grid, dim3(256), 0,
                        st, b, gd.dev, l, gd.rx, gd.ry);
