@@ -26,6 +26,28 @@ __global__ void copy4(const uint32_t* __restrict__ a, uint32_t* __restrict__ b, 
     b[i] = a[i];
 }
 
+// copy16 through LDS: each wave moves 1 KiB per step HBM -> LDS by one 16-byte-per-lane
+// buffer-to-LDS load (the orient_desc / fast_cells / pyr_ring load form), then LDS -> HBM
+__global__ void copylds(const uint8_t* __restrict__ a, uint8_t* __restrict__ b, size_t n) {
+  __shared__ __attribute__((aligned(16))) uint8_t s[4][1024];
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)a, 0, 0x7fffffff, 0x00020000);
+  for (size_t base = ((size_t)blockIdx.x * 4 + w) * 1024; base < n; base += (size_t)gridDim.x * 4096) {
+    const uint8_t* src = a + base;
+    const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)src, 0, 1024, 0x00020000);
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)s[w], 16,
+                                             16 * lane, 0, 0, 0);
+    __builtin_amdgcn_s_waitcnt(0x0F70);
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    reinterpret_cast<uint4*>(b + base)[lane] = reinterpret_cast<const uint4*>(s[w])[lane];
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+  }
+  (void)rs;
+}
+
 // blur7-like: each thread owns 4 columns of a 32-row strip, 3 dword loads per input row,
 // one dword store per output row; trivial arithmetic (sum of the 12 bytes' dwords).
 __global__ void strip3(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst, int w, int h,
@@ -76,6 +98,9 @@ int main() {
   });
   timeit("copy4 512MB", 2.0 * bytes, [&] {
     hipLaunchKernelGGL(copy4, dim3(4096), dim3(256), 0, 0, (const uint32_t*)a, (uint32_t*)b, bytes / 4);
+  });
+  timeit("copylds 512MB", 2.0 * bytes, [&] {
+    hipLaunchKernelGGL(copylds, dim3(4096), dim3(256), 0, 0, (const uint8_t*)a, (uint8_t*)b, bytes);
   });
   const int w = 1241, h = 376, pitch = 1280, nimg = 256;
   timeit("strip3 256 x 1241x376", 2.0 * nimg * w * h, [&] {

@@ -53,7 +53,7 @@ def main():
     known = 512 << 20  # membench: each copy reads and writes 512 MiB
     cal = {}
     for k, v in mb_f.items():
-        if k.startswith("copy16") or k.startswith("copy4"):
+        if k.startswith("copy16") or k.startswith("copy4") or k.startswith("copylds"):
             cal[k.split("(")[0]] = known / (v * 1024.0)
     f = per_kernel(os.path.join(base, "bench_fetch"), "FETCH_SIZE")
     w = per_kernel(os.path.join(base, "bench_write"), "WRITE_SIZE")
