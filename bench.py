@@ -414,6 +414,13 @@ def main():
             dk, dd = ctx.keypoints(0)   # the left view of the batch's frame 0
             cpu = cpu_baseline(Ls, Rs, args.cpu_frames,
                                device_check=(int(job.gframe[0]) % D, dk, dd))
+        # the drop-in legs run before the optimizer legs: after their cooperative launches the
+        # host-fed step's copies and kernels overlap less on this runtime (batched_h2d 56k ->
+        # 39k frames/s measured after them, profiles/r8m_h2d_leg_ab.log)
+        drop_in = None
+        if not args.no_latency:
+            drop_in = {"single_frame": bench_frame_latency(Ls, Rs, cam, local),
+                       "batched_h2d": bench_h2d(ctxs[0], host_l, host_r, poses, cam, dev, args)}
         opt = None
         if not args.no_optimizer:
             opt = {"pose_optimization": bench_pose(dev, not args.no_cpu_baseline),
@@ -421,10 +428,6 @@ def main():
         bow_leg = None
         if not args.no_bow:
             bow_leg = bench_bow(ctx, Bs, dev, not args.no_cpu_baseline)
-        drop_in = None
-        if not args.no_latency:
-            drop_in = {"single_frame": bench_frame_latency(Ls, Rs, cam, local),
-                       "batched_h2d": bench_h2d(ctxs[0], host_l, host_r, poses, cam, dev, args)}
         # every frontend kernel on its roofs: standalone launch times of the breakdown pass (one
         # batch, nothing else in flight), algorithmic bytes, PMC traffic and VALU counts
         kernels = {}
