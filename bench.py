@@ -414,9 +414,9 @@ def main():
             dk, dd = ctx.keypoints(0)   # the left view of the batch's frame 0
             cpu = cpu_baseline(Ls, Rs, args.cpu_frames,
                                device_check=(int(job.gframe[0]) % D, dk, dd))
-        # the drop-in legs run before the optimizer legs: after their cooperative launches the
-        # host-fed step's copies and kernels overlap less on this runtime (batched_h2d 56k ->
-        # 39k frames/s measured after them, profiles/r8m_h2d_leg_ab.log)
+        # the drop-in legs run before the optimizer legs: run after them, the host-fed step's
+        # copies and kernels overlap less (batched_h2d 56k -> 39k frames/s, the copy and compute
+        # times unchanged; profiles/r8m_h2d_leg_ab.log -- the cause is not isolated)
         drop_in = None
         if not args.no_latency:
             drop_in = {"single_frame": bench_frame_latency(Ls, Rs, cam, local),
