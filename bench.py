@@ -375,9 +375,10 @@ def main():
         if traffic is not None:
             roofline["traffic"] = round(traffic)
             roofline["traffic_source"] = tsrc
-        # the pipe that actually binds the kernel: VALU issue against its own mix's roof (PMC
-        # instruction count per dispatch over the live-measured dispatch time), the LDS / TA /
-        # TD / MFMA busy fractions of profiles/pipes.json, HBM above
+        # the dominant kernel against each pipe over the timed region (co-running with the other
+        # batch's kernels): HBM above, VALU issue against its own mix's roof (PMC instruction
+        # count per dispatch over the live launch time); the binding pipe is chosen below on the
+        # standalone basis of kernels_standalone
         vi, vpeak = measured_valu(dominant, B)
         mr = mix_roof(dominant)
         hbm = {k: roofline[k] for k in ("achieved", "peak", "unit", "frac", "traffic")}
@@ -390,25 +391,9 @@ def main():
                                     "peak": vpeak * mr, "unit": "wave-instr/s",
                                     "frac": round(rate / (vpeak * mr), 4),
                                     "nominal_peak": vpeak, "mix_roof_frac_of_nominal": mr,
+                                    "basis": "timed region (co-running launches)",
                                     "source": "SQ_INSTS_VALU: profiles/pipes.json; mix roof: "
                                               "profiles/isa_mix.json (tools/isa_mix.py)"}
-        bp, fr = binding_pipe(dominant, B, hbm.get("traffic_frac", hbm["frac"]))
-        if bp:
-            if "valu_mix" in roofline:
-                fr["valu_mix"] = roofline["valu_mix"]["frac"]  # live time, not the PMC pass
-                bp = max(fr, key=fr.get)
-            roofline["pipes"] = {k: round(v, 4) for k, v in fr.items()}
-            roofline["bound"] = {"valu_mix": "valu"}.get(bp, bp)
-            if bp == "valu_mix":
-                v = roofline["valu_mix"]
-                roofline.update(achieved=round(v["achieved"] / 1e9, 2), peak=round(v["peak"] / 1e9, 2),
-                                unit="G wave-instr/s", frac=v["frac"])
-            elif bp != "hbm":
-                roofline.update(achieved=round(fr[bp], 4), peak=1.0, unit="busy fraction",
-                                frac=round(fr[bp], 4))
-            roofline["bound_source"] = ("largest of the live VALU mix fraction, the HBM "
-                                        "fraction of the measured traffic and the PMC busy "
-                                        "fractions of profiles/pipes.json (tools/pipes.py)")
         cpu = None
         if not args.no_cpu_baseline:
             dk, dd = ctx.keypoints(0)   # the left view of the batch's frame 0
@@ -472,6 +457,27 @@ def main():
             # keypoint/descriptor/row-table reads, per launch (tools/stereo_lines.py restates it)
             lb = stereo_line_bytes(ctx, level_px)
             kernels["stereo_match"]["line_granular_bytes_per_launch"] = lb * Bs
+        # the binding pipe of the dominant kernel, every fraction on one (standalone) basis: the
+        # breakdown pass's launch time for HBM traffic and VALU, the PMC pass's serialised
+        # dispatch for the LDS / MFMA busy fractions
+        ke = kernels.get(dominant, {})
+        if ke.get("pipes"):
+            fr = ke["pipes"]
+            bp = max(fr, key=fr.get)
+            roofline["pipes"] = fr
+            roofline["bound"] = {"valu_mix": "valu"}.get(bp, bp)
+            if bp == "valu_mix":
+                ra = ke["valu_wave_instr_per_launch"] / (ke["avg_launch_us"] * 1e-6)
+                roofline.update(achieved=round(ra / 1e9, 2),
+                                peak=round(vpeak * ke["valu_mix_roof_frac_of_nominal"] / 1e9, 2),
+                                unit="G wave-instr/s", frac=fr[bp])
+            elif bp != "hbm":
+                roofline.update(achieved=fr[bp], peak=1.0, unit="busy fraction", frac=fr[bp])
+            roofline["bound_source"] = (
+                "largest pipe fraction of kernels_standalone[kernel].pipes (HBM traffic and VALU "
+                "over the breakdown pass's launch time, LDS / MFMA busy of the PMC pass's "
+                "serialised dispatch, profiles/pipes.json); the timed-region figures are in hbm / "
+                "valu_mix")
         line = {
             "metric": "stereo frames/sec ORB extract+match @1241x376, 2000 kp/frame",
             "value": round(value, 2), "unit": "stereo frames/s", "n_gpus": world,
