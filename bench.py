@@ -309,6 +309,18 @@ def main():
     print("[rank %d] kernel ms/step: " % rank + ", ".join(
         f"{n} {brk[n][0]:.3f} ({100 * brk[n][0] / tot:.0f}%)" for n in names), file=sys.stderr)
     dominant = max(names, key=lambda n: brk[n][0])
+    # the same pass with level 0's FAST after the pyramid instead of beside it (a side stream in
+    # the step): every kernel alone, the basis of the per-kernel pipe fractions (the PMC pass
+    # serialises dispatches too); the step itself keeps the fork
+    for c in ctxs:
+        c.set_extract_fork(False)
+    torch.cuda.synchronize()
+    ctx.timing_start("*", 4096)
+    step(group=0)
+    ctx.timing_stop()
+    alone = {n: ctx.timing_read(n) for n in names}
+    for c in ctxs:
+        c.set_extract_fork(True)
 
     # ---- timed region
     launches_per_step = max(1, brk[dominant][1])
@@ -415,6 +427,10 @@ def main():
             bow_leg = bench_bow(ctx, Bs, dev, not args.no_cpu_baseline)
         # every frontend kernel on its roofs: standalone launch times of the breakdown pass (one
         # batch, nothing else in flight), algorithmic bytes, PMC traffic and VALU counts
+        # every frontend kernel on its roofs, from the breakdown passes (one batch, nothing else
+        # in flight): `ms_per_step` as the step runs it (level 0's FAST beside the pyramid),
+        # `alone_ms_per_step` with each kernel alone -- the basis of the fractions, per step
+        # (bytes and instructions per launch x launches, over the alone time), like the PMC pass
         kernels = {}
         for n in names:
             ms, nl = brk[n]
@@ -423,22 +439,25 @@ def main():
             avg_s = ms / 1000.0 / nl
             ent = {"ms_per_step": round(ms, 4), "launches_per_step": nl,
                    "avg_launch_us": round(avg_s * 1e6, 2)}
+            ams = alone[n][0] if alone[n][0] > 0 else ms
+            ent["alone_ms_per_step"] = round(ams, 4)
+            step_s = ams / 1000.0
             kb = kernel_bytes(n, 2 * Bs, Bs, kp_img, level_px, nqueries // NS, fast_cand)
             if kb:
                 ent["algorithmic_bytes_per_launch"] = kb / nl
-                ent["hbm_frac"] = round(kb / nl / avg_s / 1e9 / HBM_PEAK_GBS, 4)
+                ent["hbm_frac"] = round(kb / step_s / 1e9 / HBM_PEAK_GBS, 4)
             tr, _ = measured_traffic(n, B)
             if tr is not None:
                 ent["traffic_bytes_per_launch"] = round(tr)
-                ent["traffic_frac"] = round(tr / avg_s / 1e9 / HBM_PEAK_GBS, 4)
+                ent["traffic_frac"] = round(tr * nl / step_s / 1e9 / HBM_PEAK_GBS, 4)
             vi, vpeak = measured_valu(n, B)
             mr = mix_roof(n)
             if vi is not None:
                 ent["valu_wave_instr_per_launch"] = round(vi)
-                ent["valu_issue_frac"] = round(vi / avg_s / vpeak, 4)
+                ent["valu_issue_frac"] = round(vi * nl / step_s / vpeak, 4)
                 if mr:
                     ent["valu_mix_roof_frac_of_nominal"] = mr
-                    ent["valu_mix_frac"] = round(vi / avg_s / (vpeak * mr), 4)
+                    ent["valu_mix_frac"] = round(vi * nl / step_s / (vpeak * mr), 4)
             bp, fr = binding_pipe(n, B, ent.get("traffic_frac", ent.get("hbm_frac")))
             if bp:
                 if "valu_mix_frac" in ent:
@@ -467,7 +486,8 @@ def main():
             roofline["pipes"] = fr
             roofline["bound"] = {"valu_mix": "valu"}.get(bp, bp)
             if bp == "valu_mix":
-                ra = ke["valu_wave_instr_per_launch"] / (ke["avg_launch_us"] * 1e-6)
+                ra = (ke["valu_wave_instr_per_launch"] * ke["launches_per_step"]
+                      / (ke["alone_ms_per_step"] * 1e-3))
                 roofline.update(achieved=round(ra / 1e9, 2),
                                 peak=round(vpeak * ke["valu_mix_roof_frac_of_nominal"] / 1e9, 2),
                                 unit="G wave-instr/s", frac=fr[bp])
@@ -475,7 +495,7 @@ def main():
                 roofline.update(achieved=fr[bp], peak=1.0, unit="busy fraction", frac=fr[bp])
             roofline["bound_source"] = (
                 "largest pipe fraction of kernels_standalone[kernel].pipes (HBM traffic and VALU "
-                "over the breakdown pass's launch time, LDS / MFMA busy of the PMC pass's "
+                "over the kernel's alone time per step, LDS / MFMA busy of the PMC pass's "
                 "serialised dispatch, profiles/pipes.json); the timed-region figures are in hbm / "
                 "valu_mix")
         line = {

@@ -266,6 +266,10 @@ int slamgpu_make_vo_queries_device(slamgpu_ctx* ctx, const slamgpu_f2f_pose* d_p
  * blur7, fast_cells, octree, orient_desc, stereo_rows, stereo_match, stereo_median, grid_build,
  * vo_queries, search_cand, search_resolve. */
 int slamgpu_timing_start(slamgpu_ctx* ctx, const char* kernel, int max_launches);
+/* Batches run level 0's FAST on a side stream beside the pyramid (the default, on = 1); on = 0
+ * runs it after the pyramid on the call's stream, so that a timing pass sees each kernel alone.
+ * (SLAMGPU_FORK=0 at context creation removes the side stream altogether.) */
+int slamgpu_set_extract_fork(slamgpu_ctx* ctx, int on);
 int slamgpu_timing_stop(slamgpu_ctx* ctx, void* stream);
 int slamgpu_timing_read(slamgpu_ctx* ctx, const char* kernel, double* total_ms, int* launches);
 

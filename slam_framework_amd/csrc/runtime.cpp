@@ -32,6 +32,7 @@ struct slamgpu_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
   ExtractStreams fx;  // side streams of the extraction (launch_extract)
+  bool fork_level0 = true;  // level 0's FAST on fx.side0 beside the pyramid (slamgpu_set_extract_fork)
   OrbParams params{};
   OrbTables tables{};
   OrbGeom geom{};
@@ -439,7 +440,9 @@ static int run_frontend(slamgpu_ctx* c, const ImageBatch& b, int n_frames, int n
   c->n_frames_last = n_frames;
   c->n_images_last = n_images;
   OrbGeomDev g = c->gd();
-  launch_extract(b, g, n_images, st, c->fx);
+  ExtractStreams fx = c->fx;
+  if (!c->fork_level0) fx.side0 = nullptr;  // level 0's FAST after the pyramid, on `st`
+  launch_extract(b, g, n_images, st, fx);
   if (stereo) {
     // UndistortKeyPoints + AssignFeaturesToGrid read only the left views' keypoints (frame.cpp:
     // 96, 110; stereo matching reads the distorted ones): on the side stream beside
@@ -881,6 +884,12 @@ int slamgpu_make_vo_queries_device(slamgpu_ctx* c, const slamgpu_f2f_pose* d_pos
                     reinterpret_cast<F2FQuery*>(d_queries), d_q_start, d_q_count, n_frames,
                     pick_stream(c, stream));
   HIPCHECK(c, hipGetLastError());
+  return 0;
+}
+
+int slamgpu_set_extract_fork(slamgpu_ctx* c, int on) {
+  if (!c) return SLAMGPU_EINVAL;
+  c->fork_level0 = on != 0;
   return 0;
 }
 

@@ -58,6 +58,7 @@ EXPORTS = [
     "slamgpu_search_by_projection_mps", "slamgpu_search_by_projection_frame_device",
     "slamgpu_search_by_projection_mps_device", "slamgpu_debug_level_keys",
     "slamgpu_make_vo_queries_device", "slamgpu_timing_start", "slamgpu_timing_stop",
+    "slamgpu_set_extract_fork",
     "slamgpu_trace_marker",
     "slamgpu_timing_read", "slamgpu_pose_optimization", "slamgpu_pose_optimization_device",
     "slamgpu_optimizer_last_error", "slamgpu_coop_slots_in_use", "slamgpu_local_bundle_adjustment",
@@ -169,6 +170,7 @@ def lib():
         L.slamgpu_debug_level_keys.argtypes = [vp, ip, ip, ip, vp, ip, C.POINTER(ip)]
         L.slamgpu_make_vo_queries_device.argtypes = [vp, vp, ip, vp, vp, vp, ip, vp]
         L.slamgpu_timing_start.argtypes = [vp, C.c_char_p, ip]
+        L.slamgpu_set_extract_fork.argtypes = [vp, ip]
         L.slamgpu_timing_stop.argtypes = [vp, vp]
         if hasattr(L, "slamgpu_trace_marker"):  # absent from older A/B builds (tools/abl)
             L.slamgpu_trace_marker.argtypes = [ip, vp]
@@ -381,6 +383,11 @@ class Context:
             self.h, _ptr(d_queries), total_queries, _ptr(d_q_start), _ptr(d_q_count), max_queries,
             _ptr(d_poses), _ptr(d_map_point), _ptr(d_blocked), mp_stride, _ptr(d_nmatches),
             n_frames, C.c_void_p(stream or 0)))
+
+    def set_extract_fork(self, on):
+        """Level 0's FAST beside the pyramid on a side stream (True, the default) or after it
+        (False: a timing pass then sees each kernel alone)."""
+        self.check(lib().slamgpu_set_extract_fork(self.h, 1 if on else 0))
 
     def timing_start(self, kernel="*", max_launches=8192):
         self.check(lib().slamgpu_timing_start(self.h, kernel.encode(), max_launches))
