@@ -2947,6 +2947,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void o
       uint64_t words[4];
       static_for<4>([&](auto rc) {
         constexpr int r = decltype(rc)::value;
+        if constexpr (!kTail) {
+          // rounded half to even: o = (s + 0x7fff + bit 16 of s) >> 16, saturated to 255; the
+          // test min(o_a, 255) < min(o_b, 255) is (a >> 16) < (b >> 16) && a < 255 << 16 on the
+          // biased sums -- compared on their high halves (SDWA) with no shift or clamp
+          const uint32_t a = smv[2 * r] + 0x7fffu + ((smv[2 * r] >> 16) & 1u);
+          const uint32_t b = smv[2 * r + 1] + 0x7fffu + ((smv[2 * r + 1] >> 16) & 1u);
+          words[r] = __ballot((a >> 16) < (b >> 16)) & __ballot(a < 0xff0000u);
+          return;
+        }
         uint32_t v[2];
 #pragma unroll
         for (int e = 0; e < 2; e++) {
