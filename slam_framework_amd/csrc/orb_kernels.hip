@@ -2,10 +2,14 @@
 //
 // Pipeline for a batch of n images (all levels of all images in flight together):
 //   pyr_down      level l from level l-1 (resize INTER_LINEAR 8U)        one launch per level
-//   fast_cells    per-cell FAST-9 score, threshold fallback, cell NMS    one wave per cell
-//   octree        DistributeOctTree, exact list / pointer-order semantics one workgroup per level
-//   orient_desc   IC_Angle + 7x7-blurred rBRIEF (the blur at the samples), output in
-//                 ORBextractor::Compute order                            8 keypoints per wave
+//                 (batches: pyr_ring_kernel; opt-in pyr_cascade_kernel, one launch for all)
+//   fast_cells    per-cell FAST-9 score, threshold fallback, cell NMS    8 cells per wave
+//                 (batches: level 0 on a side stream beside the pyramid)
+//   octree        DistributeOctTree, exact list / pointer-order semantics one work-group per
+//                 image, a wave per level (small launches: a work-group per level)
+//   orient_desc   IC_Angle + 7x7-blurred rBRIEF (the blur's row sums on the matrix cores, the
+//                 vertical taps at the samples), in ORBextractor::Compute order
+//                                                                        16 keypoints per wave
 // Reference: src/orb_features/orb_extractor.cpp (citations per kernel). Built with
 // -ffp-contract=off; fused multiply-adds are explicit where the reference's Release build fuses.
 #include <hip/hip_runtime.h>
@@ -2552,7 +2556,8 @@ __device__ __forceinline__ int reduce_scatter16(int (&v)[16], int lane) {
 // ds_write_b64 into the wave's transposed u16 table. A sample's 7 vertical taps are then 4
 // dwords of its column (two ds_read2_b32, a v_alignbit each for an odd first row) and four
 // v_dot2_u32_u16. It rounds with the column's rule (half to even inside the SSE span
-// x < W - W%4, half up in the scalar tail).
+// x < W - W%4, half up in the scalar tail); inside the span a test compares the two biased
+// sums' high halves directly.
 // Border keypoints (the window leaves the image: reflect-101 rows and columns) gather the A bytes
 // into the same staging slots; the GEMM and the table are the same.
 // Variants measured in round 6 (profiles/r7*): an overlapping-pair table
