@@ -228,6 +228,9 @@ def main():
                     help="skip the ComputeBoW / SearchByBoW measurement")
     ap.add_argument("--no-latency", action="store_true",
                     help="skip the single-frame drop-in latency and the PCIe-inclusive rate")
+    ap.add_argument("--no-alone", action="store_true",
+                    help="skip the second breakdown pass (level 0's FAST after the pyramid): the "
+                         "PMC passes use it so that every kernel's dispatches are the step's")
     ap.add_argument("--dist-backend", choices=("nccl", "gloo"),
                     default=os.environ.get("SLAMGPU_BENCH_BACKEND", "nccl"),
                     help="process-group backend for N > 1: nccl (RCCL, one GPU per rank; the "
@@ -312,15 +315,17 @@ def main():
     # the same pass with level 0's FAST after the pyramid instead of beside it (a side stream in
     # the step): every kernel alone, the basis of the per-kernel pipe fractions (the PMC pass
     # serialises dispatches too); the step itself keeps the fork
-    for c in ctxs:
-        c.set_extract_fork(False)
-    torch.cuda.synchronize()
-    ctx.timing_start("*", 4096)
-    step(group=0)
-    ctx.timing_stop()
-    alone = {n: ctx.timing_read(n) for n in names}
-    for c in ctxs:
-        c.set_extract_fork(True)
+    alone = brk
+    if not args.no_alone:
+        for c in ctxs:
+            c.set_extract_fork(False)
+        torch.cuda.synchronize()
+        ctx.timing_start("*", 4096)
+        step(group=0)
+        ctx.timing_stop()
+        alone = {n: ctx.timing_read(n) for n in names}
+        for c in ctxs:
+            c.set_extract_fork(True)
 
     # ---- timed region
     launches_per_step = max(1, brk[dominant][1])

@@ -5,7 +5,7 @@
 set -e
 export TMPDIR=/tmp
 OUT=${OUT:-gpurun_out/pipes}
-ARGS=${ARGS:-"--steps 2 --warmup 1 --no-cpu-baseline --no-optimizer --no-bow --no-latency"}
+ARGS=${ARGS:-"--steps 2 --warmup 1 --no-cpu-baseline --no-optimizer --no-bow --no-latency --no-alone"}
 mkdir -p $OUT
 P1="SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM SQ_WAVES SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_VALU_MFMA_BUSY_CYCLES TA_TA_BUSY_sum TD_TD_BUSY_sum GRBM_GUI_ACTIVE"
 P2="SQ_LDS_IDX_ACTIVE SQ_LDS_BANK_CONFLICT SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_WAIT_INST_LDS SQ_INSTS_SMEM SQ_BUSY_CYCLES TCP_TOTAL_CACHE_ACCESSES_sum TCP_TCC_READ_REQ_sum GRBM_GUI_ACTIVE"

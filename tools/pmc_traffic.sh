@@ -5,7 +5,7 @@
 set -e
 export TMPDIR=/tmp
 OUT=${OUT:-gpurun_out/traffic}
-ARGS=${ARGS:-"--steps 3 --warmup 1 --no-cpu-baseline --no-optimizer"}  # recorded by traffic.py via ARGS
+ARGS=${ARGS:-"--steps 3 --warmup 1 --no-cpu-baseline --no-optimizer --no-alone"}  # recorded by traffic.py via ARGS
 export ARGS
 mkdir -p $OUT
 for c in FETCH_SIZE WRITE_SIZE; do
