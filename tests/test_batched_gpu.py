@@ -212,3 +212,34 @@ def test_noise_frames_take_global_octree(oracle, gpu_lib):
     for img in (2, 4):  # the noise images produce many more level-0 candidates than fit in LDS
         assert len(ctx.debug_level_keys(img, 0, 0)) > 20000
     check_frames(gpu_lib, oracle, parts, poses, L, R, range(4))
+
+
+def test_level0_fast_fork_off_identical(gpu_lib):
+    """slamgpu_set_extract_fork(0) (level 0's FAST after the pyramid on the call's stream, as
+    bench.py's alone breakdown pass runs it) gives the same keypoints, descriptors and stereo as
+    the default side-stream fork, frame for frame, on a 9-frame (18-image) batch."""
+    import torch
+    B = 9
+    L = np.zeros((B, ROWS, PITCH), np.uint8)
+    R = np.zeros((B, ROWS, PITCH), np.uint8)
+    for f in range(B):
+        L[f, :, :COLS], R[f, :, :COLS] = S.stereo_pair(6000 + f)
+    dev = torch.device("cuda", 0)
+    d_l, d_r = torch.from_numpy(L).to(dev), torch.from_numpy(R).to(dev)
+    torch.cuda.synchronize()
+    ctx = gpu_lib.Context(COLS, ROWS, 2000, 1.2, 8, 20, 7, max_frames=B)
+    out = []
+    for fork in (True, False):
+        ctx.set_extract_fork(fork)
+        ctx.frontend_device(d_l, d_r, ROWS * PITCH, PITCH, B, CAM)
+        ctx.sync()
+        out.append([(ctx.keypoints(i), ctx.stereo(i // 2) if i % 2 == 0 else None)
+                    for i in range(2 * B)])
+    ctx.set_extract_fork(True)
+    for i, ((a, sa), (b, sb)) in enumerate(zip(*out)):
+        for f in a[0].dtype.names:
+            np.testing.assert_array_equal(a[0][f], b[0][f], err_msg=f"image {i} field {f}")
+        np.testing.assert_array_equal(a[1], b[1], err_msg=f"image {i} descriptors")
+        if sa is not None:
+            for x, y in zip(sa, sb):
+                np.testing.assert_array_equal(x, y, err_msg=f"frame {i // 2} stereo")
