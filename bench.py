@@ -363,8 +363,9 @@ def main():
         kp_img = float(nk.mean())
         nqueries = int(nq.sum())
         # FAST survivors per image (what the octree reads): images 0-3 of the batch, all levels
-        fast_cand = float(np.mean([sum(len(ctx.debug_level_keys(i, l, 0)) for l in range(8))
-                                   for i in range(min(4, 2 * Bs))]))
+        cand_lv = np.array([[len(ctx.debug_level_keys(i, l, 0)) for l in range(8)]
+                            for i in range(min(4, 2 * Bs))])
+        fast_cand = float(cand_lv.sum(1).mean())
         dom_bytes = kernel_bytes(dominant, 2 * Bs, Bs, kp_img, level_px, nqueries // NS, fast_cand)
         avg_launch_s = dom_ms / 1000.0 / max(1, dom_n)
         per_launch_bytes = dom_bytes / max(1, launches_per_step) if dom_bytes else None
@@ -476,6 +477,7 @@ def main():
             kernels[n] = ent
         if "octree" in kernels:
             kernels["octree"]["fast_candidates_per_image"] = round(fast_cand)
+            kernels["octree"]["fast_candidates_per_level_max"] = cand_lv.max(0).tolist()
         if "stereo_match" in kernels:
             # HBM moves lines: the windows' distinct 128-B lines (frame 0 of the batch) + the
             # keypoint/descriptor/row-table reads, per launch (tools/stereo_lines.py restates it)
