@@ -270,12 +270,13 @@ def main():
 
     cols, rows, B, D = S.KITTI_COLS, S.KITTI_ROWS, args.batch, args.distinct
     cam = S.KITTI_CAM
-    # ---- ONE synthetic sequence for the whole job (D distinct renders, frame g = render g % D),
-    # sharded contiguously with a one-frame halo, resident in HBM before timing
+    # ---- ONE synthetic sequence for the whole job (D distinct renders played back and forth,
+    # frame g = render_of(g, D)), sharded contiguously with a one-frame halo, resident in HBM
+    # before timing
     # (slam_framework_amd/sharded.py; the same object tests/test_sharded_gpu.py checks)
     Ls, Rs = S.layered_sequence(1000, D)
     from slam_framework_amd import dist as SD
-    from slam_framework_amd.sharded import ShardedFrontend
+    from slam_framework_amd.sharded import ShardedFrontend, render_of
     # per-frame results of the owned frames -> rank 0 (world > 1 only; SLAMGPU_BENCH_GATHER=1
     # runs the pack + gather path at world 1 too, as a local copy)
     gather = world > 1 or os.environ.get("SLAMGPU_BENCH_GATHER") == "1"
@@ -416,7 +417,7 @@ def main():
         if not args.no_cpu_baseline:
             dk, dd = ctx.keypoints(0)   # the left view of the batch's frame 0
             cpu = cpu_baseline(Ls, Rs, args.cpu_frames,
-                               device_check=(int(job.gframe[0]) % D, dk, dd))
+                               device_check=(render_of(int(job.gframe[0]), D), dk, dd))
         # the drop-in legs run before the optimizer legs: run after them, the host-fed step's
         # copies and kernels overlap less (batched_h2d 56k -> 39k frames/s, the copy and compute
         # times unchanged; profiles/r8m_h2d_leg_ab.log -- the cause is not isolated)
@@ -512,7 +513,8 @@ def main():
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u8",
             "data": "synthetic (seeded layered-surfaces scene: ~50% of keypoints with stereo "
                     "depth, ~1000 frame-to-frame queries/frame; camera turning + 0.3 m/frame "
-                    "forward; one sequence of 16 renders, sharded over the ranks)",
+                    "forward; one sequence of 16 renders played back and forth, sharded over the "
+                    "ranks)",
             "config": {"workload": "configs[1]: synthetic 1241x376 stereo stream, 2000 kp/frame, "
                                    "extract L+R + stereo match + frame-to-frame match",
                        "frames_per_gpu_per_step": NS * (Bs - 1), "batch": B, "streams": NS,
@@ -1218,6 +1220,7 @@ def cpu_baseline(Ls, Rs, n_frames, device_check=None):
     import oracle_lib as O
     import scenario
     from slam_framework_amd import synthetic as S
+    from slam_framework_amd.sharded import render_of
 
     O.build()
     native = None
@@ -1254,7 +1257,7 @@ def cpu_baseline(Ls, Rs, n_frames, device_check=None):
         def run(tid):
             prev = None
             for k in range(per_thread):
-                f = (tid * per_thread + k) % D
+                f = render_of(tid * per_thread + k, D)  # the bench's back-and-forth order
                 kl, dl, pl = O.extract(t, Ls[f], True)
                 kr, dr, pr = O.extract(t, Rs[f], True)
                 ur, depth, _ = O.stereo(t, kl, dl, kr, dr, pl, pr, cam[0], cam[4])
@@ -1287,7 +1290,7 @@ def cpu_baseline(Ls, Rs, n_frames, device_check=None):
     t1 = time.perf_counter()
     with cf.ThreadPoolExecutor(2) as ex:
         for k in range(n_seq):
-            f = k % D
+            f = render_of(k, D)
             fl, fr = ex.submit(O.extract, t, Ls[f], True), ex.submit(O.extract, t, Rs[f], True)
             (kl, dl, pl), (kr, dr, pr) = fl.result(), fr.result()
             ur, depth, _ = O.stereo(t, kl, dl, kr, dr, pl, pr, cam[0], cam[4])

@@ -31,12 +31,23 @@ from . import synthetic as S
 PITCH = 1280  # device row pitch of the resident input images (>= 1241, 256-B multiple)
 
 
+def render_of(g, D):
+    """Render of global frame g in a sequence of D renders played back and forth (0, 1, ..,
+    D - 1, D - 2, .., 1, 0, 1, ..): consecutive frames are always neighbouring renders, so every
+    frame-to-frame search sees the sequence's one-render motion (a cyclic order would pair render
+    D - 1 with render 0 once per D frames: a jump with few matches)."""
+    if D <= 1:
+        return 0
+    u = int(g) % (2 * (D - 1))
+    return u if u < D else 2 * (D - 1) - u
+
+
 def sequence_poses(gframe, D, cam):
-    """F2F pose records of the global frames `gframe` of a D-render cyclic layered sequence
-    (frame g is render g % D; its last frame is g - 1, render (g - 1) % D)."""
+    """F2F pose records of the global frames `gframe` of a D-render layered sequence (frame g is
+    render render_of(g, D); its last frame is g - 1)."""
     poses = np.zeros(len(gframe), G.F2F_POSE_DTYPE)
     for f, g in enumerate(gframe):
-        t, tl = int(g) % D, (int(g) - 1) % D
+        t, tl = render_of(g, D), render_of(int(g) - 1, D)
         Rf, tf = S.layered_pose(t)
         poses["Rcw"][f] = Rf.astype(np.float32).reshape(-1)
         poses["tcw"][f] = tf.astype(np.float32)
@@ -49,7 +60,7 @@ def sequence_poses(gframe, D, cam):
 
 
 class ShardedFrontend:
-    """Ls, Rs: the D distinct renders of the sequence (frame g = render g % D), uploaded once so
+    """Ls, Rs: the D distinct renders of the sequence (frame g = render_of(g, D)), uploaded once so
     the inputs are resident in HBM before any timed step. batch: stereo frames per rank per step
     (split into `streams` parts of >= 2 frames). gather: pack + gather every step's owned frames
     to rank 0 (FrameGather; host_gather stages the slots through host memory for a CPU (gloo)
@@ -77,8 +88,8 @@ class ShardedFrontend:
         self.host_l = np.zeros((batch, rows, PITCH), np.uint8)
         self.host_r = np.zeros((batch, rows, PITCH), np.uint8)
         for f in range(batch):
-            self.host_l[f, :, :cols] = Ls[self.gframe[f] % D]
-            self.host_r[f, :, :cols] = Rs[self.gframe[f] % D]
+            self.host_l[f, :, :cols] = Ls[render_of(self.gframe[f], D)]
+            self.host_r[f, :, :cols] = Rs[render_of(self.gframe[f], D)]
         self.d_l = torch.from_numpy(self.host_l).to(device)
         self.d_r = torch.from_numpy(self.host_r).to(device)
         self.stride = rows * PITCH
@@ -211,7 +222,7 @@ class ShardedFrontend:
 
     def check_gather(self):
         """Rank 0, after sync(): every gathered frame must equal, byte for byte, rank 0's own
-        result for the same render pair (frames are a cyclic sequence of D renders: the frontend
+        result for the same render pair (frames play D renders back and forth: the frontend
         output depends only on the render, the frame-to-frame search only on (t-1, t)). Up to 64
         frames spread over the other ranks' shards (at world 1: rank 0's own) are checked."""
         got = self.gathered()
@@ -219,13 +230,13 @@ class ShardedFrontend:
             return None
         own = {}
         for g, d in self.own_results(0).items():
-            own.setdefault((g % self.D, (g - 1) % self.D), d)
+            own.setdefault((render_of(g, self.D), render_of(g - 1, self.D)), d)
         F, world = self.F, self.world
         j0 = F if world > 1 else 0
         checked = 0
         for j in range(j0, world * F, max(1, (world * F - j0) // 64)):
             g = j + 1
-            b = own.get((g % self.D, (g - 1) % self.D))
+            b = own.get((render_of(g, self.D), render_of(g - 1, self.D)))
             if b is None:   # rank 0 owns fewer frames than the sequence has render pairs
                 continue
             a = got[j]

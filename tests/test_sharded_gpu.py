@@ -21,6 +21,7 @@ import pytest
 
 import sharded_gpu_job as J
 from slam_framework_amd import slamgpu as G
+from slam_framework_amd.sharded import render_of
 from slam_framework_amd import synthetic as S
 
 pytestmark = pytest.mark.gpu
@@ -54,8 +55,8 @@ def _check_vs_oracle(oracle, got, gframe, Bs, poses, D, Ls, Rs, parts=None):
 
     def orc(f):
         if f not in cache:
-            kl, dl, pl = oracle.extract(t, Ls[f % D], True)
-            kr, dr, pr = oracle.extract(t, Rs[f % D], True)
+            kl, dl, pl = oracle.extract(t, Ls[render_of(f, D)], True)
+            kr, dr, pr = oracle.extract(t, Rs[render_of(f, D)], True)
             ur, depth, _ = oracle.stereo(t, kl, dl, kr, dr, pl, pr, CAM[0], CAM[4])
             cache[f] = (kl, dl, kr, dr, ur, depth)
         return cache[f]
@@ -204,8 +205,9 @@ def test_bench_shape_gather_matches_oracle(oracle, gpu_lib):
     info = job.check_gather()
     assert info["identical"] and info["frames_checked_vs_rank0"] >= 15
     _, _, parts = job.groups[last]
-    # (frames g with g % 16 == 0 pair the sequence's last render with its first: few matches)
-    pick = [got[i] for i in (0, 1, 126, 200, 254)]
+    # frames at the start, at the turns of the back-and-forth sequence (frames 15, 16: renders
+    # 15 -> 14; frames 30, 31: renders 0 -> 1), in the middle and at the end
+    pick = [got[i] for i in (0, 1, 14, 15, 29, 30, 126, 200, 254)]
     _check_vs_oracle(oracle, pick, job.gframe, job.Bs, job.poses, job.D, Ls, Rs, parts)
 
 
