@@ -29,5 +29,9 @@ for spec in argv:
     k = d.get("kernel_ms_per_step", {})
     ks = " ".join(f"{n}={v:.3f}" for n, v in k.items() if v > 0.02)
     lat = (d.get("drop_in") or {}).get("single_frame", {}).get("median_ms")
+    ks_alone = {n: e.get("alone_ms_per_step") for n, e in d.get("kernels_standalone", {}).items()}
+    al = " ".join(f"{n}={v:.3f}" for n, v in ks_alone.items() if v and v > 0.02)
+    if al:
+        ks += f" | alone {al}"
     print(f"{spec:36s} {d['ms_per_step']:.3f} ms {d['value']:.0f} f/s | {ks}"
           + (f" | drop-in {lat:.3f} ms" if lat else ""), flush=True)
