@@ -1426,6 +1426,9 @@ __global__ __launch_bounds__(kOctThreads) void octree_kernel(
 // vPrev, whose nodes were all created in the same pass -- in push order, i.e. ascending list
 // position -- so nodes carry no sequence number. Levels whose keys do not fit set
 // oct_count = -1 and octree_kernel (global memory) redoes them.
+#ifndef OCT_PROF
+#define OCT_PROF 0
+#endif
 #ifndef OCT_LANE_KEYS
 #define OCT_LANE_KEYS 64
 #endif
@@ -1439,6 +1442,17 @@ struct OctNodeS {
 static_assert(sizeof(OctNodeS) == 12, "compact node");
 __device__ __forceinline__ int node_kbeg(const OctNodeS& d) { return (int)(d.kn & 0xffffu); }
 __device__ __forceinline__ int node_n(const OctNodeS& d) { return (int)(d.kn >> 16); }
+
+// lane l's node (l wave-uniform): three readlanes instead of an LDS round trip
+__device__ __forceinline__ OctNodeS readlane_node(const OctNodeS& nd, int l) {
+  uint32_t w[3];
+  __builtin_memcpy(w, &nd, sizeof(w));
+#pragma unroll
+  for (int i = 0; i < 3; i++) w[i] = (uint32_t)__builtin_amdgcn_readlane((int)w[i], l);
+  OctNodeS o;
+  __builtin_memcpy(&o, w, sizeof(w));
+  return o;
+}
 
 __device__ __forceinline__ int quadrant(uint32_t k, int xm, int ym) {
   return (key_x(k) >= xm ? 1 : 0) + (key_y(k) >= ym ? 2 : 0);
@@ -1515,9 +1529,7 @@ __device__ __forceinline__ void wave_count(const OctNodeS& nd, const uint32_t* k
 __device__ void wave_partition(const OctNodeS& nd, uint32_t* keys, uint32_t* gscratch, int lane,
                                int cnt[4]) {
   const int xm = node_xm(nd), ym = node_ym(nd), kb = node_kbeg(nd), n = node_n(nd);
-  wave_count(nd, keys, lane, cnt);
-  int run[4] = {0, cnt[0], cnt[0] + cnt[1], cnt[0] + cnt[1] + cnt[2]};
-  if (n <= 64 * kOctDivRegs) {  // through registers
+  if (n <= 64 * kOctDivRegs) {  // through registers: one read of the keys, counted, then placed
     const int R = (n + 63) >> 6;
     uint32_t kr[kOctDivRegs];
     int qr[kOctDivRegs];
@@ -1530,6 +1542,15 @@ __device__ void wave_partition(const OctNodeS& nd, uint32_t* keys, uint32_t* gsc
       }
     }
 #pragma unroll
+    for (int q = 0; q < 4; q++) cnt[q] = 0;
+#pragma unroll
+    for (int r = 0; r < kOctDivRegs; r++)
+      if (r < R) {
+#pragma unroll
+        for (int q = 0; q < 4; q++) cnt[q] += __popcll(__ballot(qr[r] == q));
+      }
+    int run[4] = {0, cnt[0], cnt[0] + cnt[1], cnt[0] + cnt[1] + cnt[2]};
+#pragma unroll
     for (int r = 0; r < kOctDivRegs; r++)
       if (r < R) {
 #pragma unroll
@@ -1540,6 +1561,8 @@ __device__ void wave_partition(const OctNodeS& nd, uint32_t* keys, uint32_t* gsc
         }
       }
   } else {  // through this level's global scratch (first passes of very dense levels only)
+    wave_count(nd, keys, lane, cnt);
+    int run[4] = {0, cnt[0], cnt[0] + cnt[1], cnt[0] + cnt[1] + cnt[2]};
     for (int i = lane; i < n; i += 64) gscratch[kb + i] = keys[kb + i];
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "agent");
     for (int s0 = 0; s0 < n; s0 += 64) {
@@ -1572,6 +1595,19 @@ __global__ __launch_bounds__(64 * kMaxLevels) void octree_img_kernel(
   const LevelGeom& L = g->lv[active ? level : 0];
   const int ncell = L.ncols * L.nrows;
   const int64_t cbase = (int64_t)img * g->cells_per_image + L.cell_base;
+#if OCT_PROF  // diagnostic build: per-phase shader cycles of images 0-1 (printf at the end)
+  uint64_t op_t = clock64(), op_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  int op_np = 0, op_V = 0;
+  uint32_t op_pass[8][6] = {};  // per pass: V, big nodes, sort, count, scan, place cycles
+  auto optick = [&](int i) {
+    const uint64_t t = clock64();
+    op_acc[i] += t - op_t;
+    if (i >= 2 && i <= 5 && op_np >= 1 && op_np <= 8) op_pass[op_np - 1][i] += (uint32_t)(t - op_t);
+    op_t = t;
+  };
+#else
+  auto optick = [](int) {};
+#endif
   // ---- 1. candidate counts -> this level's key range (levels that do not fit fall back)
   int K = 0;
   if (active) {
@@ -1581,6 +1617,7 @@ __global__ __launch_bounds__(64 * kMaxLevels) void octree_img_kernel(
   }
   __syncthreads();
   if (!active) return;
+  optick(0);
   int* const outc = oct_count + img * nlev + level;
   uint32_t* const outk = oct_keys + (int64_t)img * g->out_per_image + L.out_base;
   const int nIni = L.n_ini;
@@ -1619,9 +1656,12 @@ __global__ __launch_bounds__(64 * kMaxLevels) void octree_img_kernel(
   constexpr int kGatherChunks = 8, kGatherRegs = 48;
   int bcnt = 0;  // lane b < nIni: keys in bucket b
   if (ncell <= 64 * kGatherChunks && K <= 64 * kGatherRegs && ncell + 1 <= NC) {
-    // cell prefix in LDS (the level's sort scratch, free until the passes), then every key
-    // slot finds its cell by a binary search and all key loads are issued at once
-    int* const cpre = reinterpret_cast<int*>(sortk);
+    // key-group prefixes in LDS (the level's sort scratch, free until the passes): a group's
+    // keys are contiguous from its first slot, so a key slot needs only its group -- the
+    // largest g with gp[g] <= s (empty groups repeat the next prefix and are skipped) -- found by
+    // a branch-free binary search over the <= 64 groups whose probes for all the wave's slots
+    // are issued together, step by step, then every key load at once
+    int* const gp = reinterpret_cast<int*>(sortk);
     int ccnt[kGatherChunks];
 #pragma unroll
     for (int ch = 0; ch < kGatherChunks; ch++) {
@@ -1634,29 +1674,35 @@ __global__ __launch_bounds__(64 * kMaxLevels) void octree_img_kernel(
       if (64 * ch < ncell) {
         int ctot;
         const int cex = wave_excl_scan(ccnt[ch], lane, &ctot);
-        if (64 * ch + lane < ncell) cpre[64 * ch + lane] = carry + cex;
+        const int c = 64 * ch + lane;
+        if (c < ncell && (c & (kCellGroup - 1)) == 0) gp[c / kCellGroup] = carry + cex;
         carry += ctot;
       }
     }
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     __builtin_amdgcn_wave_barrier();
     const int R = (K + 63) >> 6;
+    const int ng = (ncell + kCellGroup - 1) / kCellGroup;  // <= 64
     uint32_t kr[kGatherRegs];
-    int br[kGatherRegs];
+    int br[kGatherRegs];  // the slot's group during the search, its bucket after
+#pragma unroll
+    for (int r = 0; r < kGatherRegs; r++) br[r] = 0;
+#pragma unroll
+    for (int step = 32; step >= 1; step >>= 1) {
+#pragma unroll
+      for (int r = 0; r < kGatherRegs; r++) {
+        if (r < R) {
+          const int cand = br[r] + step;
+          if (cand < ng && gp[cand] <= 64 * r + lane) br[r] = cand;
+        }
+      }
+    }
 #pragma unroll
     for (int r = 0; r < kGatherRegs; r++) {
-      br[r] = -1;
       const int s = 64 * r + lane;
-      if (r < R && s < K) {
-        int lo = 0, hi = ncell;  // largest c with cpre[c] <= s: the non-empty cell holding s
-        while (hi - lo > 1) {
-          const int mid = (lo + hi) >> 1;
-          if (cpre[mid] <= s) lo = mid;
-          else hi = mid;
-        }
-        const int gs = lo & ~(kCellGroup - 1);  // key group of cell lo: contiguous from gs
-        kr[r] = cell_keys[(cbase + gs) * g->cell_cap + (s - cpre[gs])];
-      }
+      if (r < R && s < K)
+        kr[r] = cell_keys[(cbase + kCellGroup * br[r]) * g->cell_cap + (s - gp[br[r]])];
+      br[r] = -1;
     }
 #pragma unroll
     for (int r = 0; r < kGatherRegs; r++) {
@@ -1679,7 +1725,7 @@ __global__ __launch_bounds__(64 * kMaxLevels) void octree_img_kernel(
       if (r < R)
         for (int bb = 0; bb < nIni; bb++) {
           const uint64_t mm = __ballot(br[r] == bb);
-          const int at = __shfl(brun, bb, 64);
+          const int at = __builtin_amdgcn_readlane(brun, bb);  // bb is wave-uniform
           if (br[r] == bb) keys[at + lanes_below(mm)] = kr[r];
           if (lane == bb) brun += __popcll(mm);
         }
@@ -1716,7 +1762,7 @@ __global__ __launch_bounds__(64 * kMaxLevels) void octree_img_kernel(
           for (int bb = 0; bb < nIni; bb++) {
             const uint64_t m = __ballot(b == bb);
             if (sweep == 1) {
-              const int at = __shfl(brun, bb, 64);
+              const int at = __builtin_amdgcn_readlane(brun, bb);  // bb is wave-uniform
               if (b == bb) keys[at + lanes_below(m)] = k;
               if (lane == bb) brun += __popcll(m);
             } else if (lane == bb) {
@@ -1746,6 +1792,7 @@ __global__ __launch_bounds__(64 * kMaxLevels) void octree_img_kernel(
     m = __popcll(hm);
   }
   // ---- 3. passes
+  optick(1);
   const int N = L.budget;
   int cur = 0, nexp = 0;
   bool outer = true;
@@ -1753,6 +1800,11 @@ __global__ __launch_bounds__(64 * kMaxLevels) void octree_img_kernel(
     const OctNodeS* Lc = lists + cur * NC;
     OctNodeS* Ln = lists + (cur ^ 1) * NC;
     const int V = outer ? m : nexp;
+#if OCT_PROF
+    op_np++;
+    op_V += V;
+    if (op_np <= 8) op_pass[op_np - 1][0] = V;
+#endif
     if (!outer) {  // vPrev: positions in push order -> descending (n, creation order)
       int P2 = 64;
       while (P2 < V) P2 <<= 1;
@@ -1783,6 +1835,7 @@ __global__ __launch_bounds__(64 * kMaxLevels) void octree_img_kernel(
       __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
       __builtin_amdgcn_wave_barrier();
     }
+    optick(2);
     auto nidx = [&](int j) { return outer ? j : 4095 - (int)(sortk[j] & 0xfffu); };
     // -- count children: t (non-empty), e (> 1 key); pu = survivor flag (outer) or t - 1
     for (int j0 = 0; j0 < V; j0 += 64) {
@@ -1802,10 +1855,13 @@ __global__ __launch_bounds__(64 * kMaxLevels) void octree_img_kernel(
         }
       }
       uint64_t bigm = __ballot(valid && n > kOctLaneKeys);
+#if OCT_PROF
+      if (op_np <= 8) op_pass[op_np - 1][1] += __popcll(bigm);
+#endif
       while (bigm) {
         const int bl = __builtin_ctzll(bigm);
         bigm &= bigm - 1;
-        const OctNodeS nb = Lc[nidx(j0 + bl)];
+        const OctNodeS nb = readlane_node(nd, bl);
         int cnt[4];
         wave_count(nb, keys, lane, cnt);
         if (lane == bl) {
@@ -1822,6 +1878,7 @@ __global__ __launch_bounds__(64 * kMaxLevels) void octree_img_kernel(
         pu[j] = (int16_t)(outer ? (n == 1) : t - 1);
       }
     }
+    optick(3);
     int nproc = V;
     if (!outer) {
       // processing stops once the list reaches N: first j with m + sum_{i<=j}(t_i - 1) >= N
@@ -1859,6 +1916,7 @@ __global__ __launch_bounds__(64 * kMaxLevels) void octree_img_kernel(
     }
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     __builtin_amdgcn_wave_barrier();
+    optick(4);
     // -- divide in place and place children: push order gpos -> list position T-1-gpos
     auto place = [&](int j, const OctNodeS& nd, uint32_t c4) {
       int gpos = pt[j], epos = pe[j];
@@ -1895,12 +1953,13 @@ __global__ __launch_bounds__(64 * kMaxLevels) void octree_img_kernel(
       while (bigm) {
         const int bl = __builtin_ctzll(bigm);
         bigm &= bigm - 1;
-        const OctNodeS nb = Lc[nidx(j0 + bl)];
+        const OctNodeS nb = readlane_node(nd, bl);
+        const int gpos0 = pt[j0 + bl], epos0 = pe[j0 + bl];  // read before the partition's stores
         int cnt[4];
         wave_partition(nb, keys, gscratch, lane, cnt);
         if (lane == 0) {
           // counts can exceed 255 here: place() takes 8-bit counts, so place big ones inline
-          int gpos = pt[j0 + bl], epos = pe[j0 + bl];
+          int gpos = gpos0, epos = epos0;
           const int xm = node_xm(nb), ym = node_ym(nb);
           const int16_t xs[3] = {nb.x0, (int16_t)xm, nb.x1};
           const int16_t ys[3] = {nb.y0, (int16_t)ym, nb.y1};
@@ -1930,6 +1989,7 @@ __global__ __launch_bounds__(64 * kMaxLevels) void octree_img_kernel(
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     __builtin_amdgcn_wave_barrier();
     for (int i = lane; i < E; i += 64) sortk[i] = (uint32_t)vnext[i];
+    optick(5);
     const int mprev = m;
     m = newm;
     nexp = E;
@@ -1956,6 +2016,20 @@ __global__ __launch_bounds__(64 * kMaxLevels) void octree_img_kernel(
     if (m > L.out_cap) atomicOr(err, kErrNodeOverflow);
     *outc = mout;
   }
+#if OCT_PROF
+  optick(6);
+  if (lane == 0 && img < 2)
+    printf("[octprof] img %d level %d K %d passes %d V %d | cyc: count %llu gather %llu sort %llu "
+           "count %llu scan %llu place %llu retain %llu\n", img, level, K, op_np, op_V,
+           (unsigned long long)op_acc[0], (unsigned long long)op_acc[1],
+           (unsigned long long)op_acc[2], (unsigned long long)op_acc[3],
+           (unsigned long long)op_acc[4], (unsigned long long)op_acc[5],
+           (unsigned long long)op_acc[6]);
+  if (lane == 0 && img == 0 && level == 0)
+    for (int i = 0; i < op_np && i < 8; i++)
+      printf("[octpass] pass %d V %u big %u sort %u count %u scan %u place %u\n", i,
+             op_pass[i][0], op_pass[i][1], op_pass[i][2], op_pass[i][3], op_pass[i][4], op_pass[i][5]);
+#endif
 }
 
 // ---------------------------------------------------------------------------------------
